@@ -1,0 +1,499 @@
+/*
+ * pluss_oracle.c — CPU ORACLE for the PLUSS GEMM reuse-interval path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (the HIP library under
+ * pluss_sampler_optimization_amd/) links, loads or calls this file.  Only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it, and
+ * only as the checker / the timed CPU baseline.
+ *
+ * It is a plain-C restatement of the reference's algorithm (no code copied):
+ *
+ *   orc_fulltrace  — the full-trace sampler `sampler()` of
+ *                    c_lib/test/sampler/gemm-t4-pluss-pro-model-ri-omp-seq.cpp:37-333
+ *                    (per-tid LAT per array, count[tid], share test :203,
+ *                    cold = |LAT| per tid :305-319).  Static schedule per
+ *                    ChunkDispatcher (runtime/pluss_utils.h:298-334, 386-425).
+ *   orc_faithful   — one `sampler_<REF>` of
+ *                    c_lib/test/sampler/gemm-t4-pluss-pro-model-rs-ri-opt-r10.cpp
+ *                    (sampler_C3 :135-696 is the template; B0 share test
+ *                    :2482-2486), including its cross-sample control flow:
+ *                    priority-queue order (IterationComp, pluss_utils.h:175-267),
+ *                    START (:187-274), lockstep interleaving (:275-654), meet
+ *                    (:541-556), early exit (:345, :356), cold accounting of
+ *                    LAT[0] only (:194-199, :669-674).  It steps access by
+ *                    access exactly like the reference.
+ *   orc_clean      — per-sample forward RI by stepping the sample's simulated
+ *                    thread access by access until the next touch of the same
+ *                    cache line by a reference of the same array (the per-tid
+ *                    counting of r10 without the cross-sample quirks).
+ *   orc_expand     — the sample-list bijection (spec in DESIGN.md §4).  Written
+ *                    independently of the device implementation so the two
+ *                    can be compared.
+ *
+ * Reference ids (access order inside one c1 iteration, pluss seq.cpp:102-288):
+ *   0=C0 C[c0][c1]  1=C1 C[c0][c1]  2=A0 A[c0][c2]  3=B0 B[c2][c1]
+ *   4=C2 C[c0][c1]  5=C3 C[c0][c1]
+ * Histogram keys are exact (raw) RI values; -1 = cold.  kind 0 = noshare,
+ * kind 1 = share (share_ratio THREAD_NUM-1 in the reference).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <pthread.h>
+
+typedef struct {
+    int64_t N, T, CS, DS, CLS;
+    int32_t thr_variant; /* 0: r10 THR=(4N+2)N (r10:2482); 1: v1 THR=(N+1)N+1 (seq.cpp:203) */
+    int32_t range_full;  /* expansion: 0 -> indices in [0,N-2] (rand()%(N-1), r10:159); 1 -> [0,N-1] */
+} orc_cfg;
+
+typedef struct {
+    int32_t ref, kind;
+    int64_t ri;
+    uint64_t count;
+} orc_entry;
+
+enum { R_C0 = 0, R_C1 = 1, R_A0 = 2, R_B0 = 3, R_C2 = 4, R_C3 = 5 };
+enum { ARR_C = 0, ARR_A = 1, ARR_B = 2 };
+static const int REF_ARRAY[6] = {ARR_C, ARR_C, ARR_A, ARR_B, ARR_C, ARR_C};
+
+/* ---------------------------------------------------------------- maps -- */
+/* u64 -> u64 open addressing with backward-shift deletion; key 0 reserved. */
+typedef struct { uint64_t *k, *v; size_t cap, n; } omap;
+
+static uint64_t h64(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33; return x;
+}
+static int om_init(omap *m, size_t cap) {
+    size_t c = 16; while (c < cap * 2) c <<= 1;
+    m->k = (uint64_t *)calloc(c, 8); m->v = (uint64_t *)calloc(c, 8);
+    m->cap = c; m->n = 0; return (m->k && m->v) ? 0 : -1;
+}
+static void om_free(omap *m) { free(m->k); free(m->v); m->k = m->v = 0; m->cap = m->n = 0; }
+static void om_clear(omap *m) {
+    if (m->n) { memset(m->k, 0, m->cap * 8); m->n = 0; }
+}
+static uint64_t *om_find(omap *m, uint64_t key) {
+    size_t msk = m->cap - 1, i = h64(key) & msk;
+    while (m->k[i]) { if (m->k[i] == key) return &m->v[i]; i = (i + 1) & msk; }
+    return 0;
+}
+static int om_grow(omap *m);
+static uint64_t *om_put(omap *m, uint64_t key) { /* returns slot (value 0 if new) */
+    if ((m->n + 1) * 2 > m->cap && om_grow(m)) return 0;
+    size_t msk = m->cap - 1, i = h64(key) & msk;
+    while (m->k[i]) { if (m->k[i] == key) return &m->v[i]; i = (i + 1) & msk; }
+    m->k[i] = key; m->v[i] = 0; m->n++; return &m->v[i];
+}
+static int om_grow(omap *m) {
+    omap nm; if (om_init(&nm, m->cap)) return -1;
+    for (size_t i = 0; i < m->cap; i++) if (m->k[i]) *om_put(&nm, m->k[i]) = m->v[i];
+    om_free(m); *m = nm; return 0;
+}
+static void om_del(omap *m, uint64_t key) {
+    size_t msk = m->cap - 1, i = h64(key) & msk;
+    while (m->k[i] && m->k[i] != key) i = (i + 1) & msk;
+    if (!m->k[i]) return;
+    m->k[i] = 0; m->n--;
+    size_t j = i;
+    for (;;) {
+        j = (j + 1) & msk;
+        if (!m->k[j]) break;
+        size_t h = h64(m->k[j]) & msk;
+        /* can slot j's entry move to hole i? */
+        if ((j > i && (h <= i || h > j)) || (j < i && (h <= i && h > j))) {
+            m->k[i] = m->k[j]; m->v[i] = m->v[j]; m->k[j] = 0; i = j;
+        }
+    }
+}
+
+/* histogram: key = ref<<60 | kind<<56 | (ri+2)  (+2 keeps every key != 0) */
+static uint64_t hkey(int ref, int kind, int64_t ri) {
+    return ((uint64_t)ref << 60) | ((uint64_t)kind << 56) | (uint64_t)(ri + 2);
+}
+static int hist_add(omap *h, int ref, int kind, int64_t ri, uint64_t c) {
+    uint64_t *s = om_put(h, hkey(ref, kind, ri)); if (!s) return -1; *s += c; return 0;
+}
+static int cmp_entry(const void *a, const void *b) {
+    const orc_entry *x = (const orc_entry *)a, *y = (const orc_entry *)b;
+    if (x->ref != y->ref) return x->ref < y->ref ? -1 : 1;
+    if (x->kind != y->kind) return x->kind < y->kind ? -1 : 1;
+    return x->ri < y->ri ? -1 : (x->ri > y->ri);
+}
+static int hist_export(omap *h, orc_entry *out, int64_t cap, int64_t *n_out) {
+    int64_t n = 0;
+    for (size_t i = 0; i < h->cap; i++) if (h->k[i]) {
+        if (n >= cap) return -2;
+        uint64_t k = h->k[i];
+        out[n].ref = (int32_t)(k >> 60); out[n].kind = (int32_t)((k >> 56) & 0xF);
+        out[n].ri = (int64_t)(k & ((1ULL << 56) - 1)) - 2; out[n].count = h->v[i]; n++;
+    }
+    qsort(out, (size_t)n, sizeof(orc_entry), cmp_entry);
+    *n_out = n; return 0;
+}
+
+/* ------------------------------------------------------ loop-nest model -- */
+static uint64_t line_of(const orc_cfg *c, int64_t i, int64_t j) {
+    /* GetAddress_*: (i*N + j)*DS/CLS   (seq.cpp:12-35) */
+    return (uint64_t)((i * c->N + j) * c->DS / c->CLS);
+}
+static uint64_t addr_of(const orc_cfg *c, int ref, int64_t c0, int64_t c1, int64_t c2) {
+    switch (ref) {
+    case R_A0: return line_of(c, c0, c2);
+    case R_B0: return line_of(c, c2, c1);
+    default:   return line_of(c, c0, c1);
+    }
+}
+static int is_share(const orc_cfg *c, int64_t reuse) {
+    /* distance_to(reuse,0) > distance_to(reuse,THR)   (pluss_utils.h:703-708) */
+    uint64_t thr = c->thr_variant ? (uint64_t)((c->N + 1) * c->N + 1)
+                                  : (uint64_t)((4 * c->N + 2) * c->N);
+    uint64_t r = (uint64_t)reuse;
+    uint64_t d0 = r, d1 = r > thr ? r - thr : thr - r;
+    return d0 > d1;
+}
+
+/* cursor over one simulated thread's static-schedule stream */
+typedef struct { int64_t c0, c1, c2, ub, lb_next; int ref; int done; } cursor;
+
+static void cur_next_chunk(const orc_cfg *c, cursor *u) {
+    /* getNextStaticChunk: [lb, min(lb+CS-1, last)], lb += CS*T (pluss_utils.h:410-425) */
+    int64_t lb = u->lb_next;
+    if (lb > c->N - 1) { u->done = 1; return; }
+    u->c0 = lb; u->ub = (lb + c->CS - 1 < c->N - 1) ? lb + c->CS - 1 : c->N - 1;
+    u->lb_next = lb + c->CS * c->T; u->c1 = 0; u->c2 = 0; u->ref = R_C0;
+}
+static void cur_step(const orc_cfg *c, cursor *u) {
+    switch (u->ref) {
+    case R_C0: u->ref = R_C1; return;
+    case R_C1: u->c2 = 0; u->ref = R_A0; return;
+    case R_A0: u->ref = R_B0; return;
+    case R_B0: u->ref = R_C2; return;
+    case R_C2: u->ref = R_C3; return;
+    default: break;
+    }
+    if (u->c2 + 1 < c->N) { u->c2++; u->ref = R_A0; return; }
+    if (u->c1 + 1 < c->N) { u->c1++; u->c2 = 0; u->ref = R_C0; return; }
+    u->c0++;
+    if (u->c0 <= u->ub) { u->c1 = 0; u->c2 = 0; u->ref = R_C0; return; }
+    cur_next_chunk(c, u);
+}
+
+static int cfg_ok(const orc_cfg *c) {
+    if (c->N < 1 || c->T < 1 || c->CS < 1 || c->DS < 1 || c->CLS < 1) return 0;
+    if (c->N >= (1 << 20)) return 0;
+    return 1;
+}
+
+/* ------------------------------------------------------------ full trace -- */
+int orc_fulltrace(const orc_cfg *c, orc_entry *out, int64_t cap, int64_t *n_out,
+                  int64_t *traversed) {
+    if (!cfg_ok(c)) return -1;
+    int64_t nlines = (c->N * c->N * c->DS) / c->CLS + 1;
+    /* LAT value = (count << 3) | (src ref + 1); 0 = absent */
+    uint64_t *lat[3];
+    for (int a = 0; a < 3; a++) { lat[a] = (uint64_t *)malloc((size_t)nlines * 8); if (!lat[a]) return -3; }
+    omap h; if (om_init(&h, 64)) return -3;
+    int64_t total = 0;
+    for (int64_t tid = 0; tid < c->T; tid++) {
+        for (int a = 0; a < 3; a++) memset(lat[a], 0, (size_t)nlines * 8);
+        cursor u; memset(&u, 0, sizeof u); u.lb_next = tid * c->CS;
+        cur_next_chunk(c, &u);
+        uint64_t count = 0;
+        while (!u.done) {
+            int arr = REF_ARRAY[u.ref];
+            uint64_t line = addr_of(c, u.ref, u.c0, u.c1, u.c2);
+            uint64_t prev = lat[arr][line];
+            if (prev) {
+                int src = (int)(prev & 7) - 1;
+                int64_t reuse = (int64_t)(count - (prev >> 3));
+                int kind = (u.ref == R_B0 && is_share(c, reuse)) ? 1 : 0;
+                if (hist_add(&h, src, kind, reuse, 1)) return -3;
+            }
+            lat[arr][line] = (count << 3) | (uint64_t)(u.ref + 1);
+            count++;
+            cur_step(c, &u);
+        }
+        /* cold: every line still in a LAT had no later touch (seq.cpp:305-319) */
+        for (int a = 0; a < 3; a++)
+            for (int64_t l = 0; l < nlines; l++)
+                if (lat[a][l]) { if (hist_add(&h, (int)(lat[a][l] & 7) - 1, 0, -1, 1)) return -3; }
+        total += (int64_t)count;
+    }
+    for (int a = 0; a < 3; a++) free(lat[a]);
+    int rc = hist_export(&h, out, cap, n_out);
+    om_free(&h);
+    if (traversed) *traversed = total;
+    return rc;
+}
+
+/* ------------------------------------------------- clean per-sample RI -- */
+static int unpack(const orc_cfg *c, uint64_t s, int *ref, int64_t *c0, int64_t *c1, int64_t *c2) {
+    *ref = (int)(s >> 60); *c0 = (int64_t)((s >> 40) & 0xFFFFF);
+    *c1 = (int64_t)((s >> 20) & 0xFFFFF); *c2 = (int64_t)(s & 0xFFFFF);
+    if (*ref > 5 || *c0 >= c->N || *c1 >= c->N || *c2 >= c->N) return -1;
+    return 0;
+}
+
+/* RI of one sample by stepping its thread's stream (-1 = cold). */
+static int64_t clean_one(const orc_cfg *c, int ref, int64_t c0, int64_t c1, int64_t c2) {
+    if (ref == R_C0 || ref == R_C1) c2 = 0;
+    cursor u; memset(&u, 0, sizeof u);
+    int64_t k = c0 / c->CS, tid = k % c->T;
+    int64_t lb = k * c->CS;
+    u.c0 = c0; u.c1 = c1; u.c2 = c2; u.ref = ref;
+    u.ub = (lb + c->CS - 1 < c->N - 1) ? lb + c->CS - 1 : c->N - 1;
+    u.lb_next = lb + c->CS * c->T;
+    (void)tid;
+    int arr = REF_ARRAY[ref];
+    uint64_t line = addr_of(c, ref, c0, c1, c2);
+    int64_t d = 0;
+    for (;;) {
+        cur_step(c, &u); d++;
+        if (u.done) return -1;
+        if (REF_ARRAY[u.ref] == arr && addr_of(c, u.ref, u.c0, u.c1, u.c2) == line) return d;
+    }
+}
+
+typedef struct { const orc_cfg *c; const uint64_t *s; int64_t *ri; int64_t lo, hi; int rc; } clean_job;
+static void *clean_worker(void *p) {
+    clean_job *j = (clean_job *)p;
+    for (int64_t i = j->lo; i < j->hi; i++) {
+        int ref; int64_t c0, c1, c2;
+        if (unpack(j->c, j->s[i], &ref, &c0, &c1, &c2)) { j->rc = -4; return 0; }
+        j->ri[i] = clean_one(j->c, ref, c0, c1, c2);
+    }
+    return 0;
+}
+int orc_clean(const orc_cfg *c, const uint64_t *samples, int64_t n, int64_t *ri_out, int nthreads) {
+    if (!cfg_ok(c)) return -1;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256]; clean_job jb[256];
+    int64_t per = (n + nthreads - 1) / nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        jb[t].c = c; jb[t].s = samples; jb[t].ri = ri_out; jb[t].rc = 0;
+        jb[t].lo = t * per < n ? t * per : n; jb[t].hi = (t + 1) * per < n ? (t + 1) * per : n;
+        if (nthreads == 1) clean_worker(&jb[t]); else pthread_create(&th[t], 0, clean_worker, &jb[t]);
+    }
+    int rc = 0;
+    for (int t = 0; t < nthreads; t++) { if (nthreads > 1) pthread_join(th[t], 0); if (jb[t].rc) rc = jb[t].rc; }
+    return rc;
+}
+
+/* ---------------------------------------------- faithful r10 sampler -- */
+typedef struct { int64_t c0, c1, c2; int64_t cid, pos, tid; } smp;
+
+static int g_dim3; /* comparator context: 3D or 2D ivs */
+static int cmp_smp(const void *a, const void *b) {
+    /* IterationComp (pluss_utils.h:175-267): top of the max-heap is the
+       smallest (cid, pos, ivs[1..], tid); priorities are all 1. */
+    const smp *x = (const smp *)a, *y = (const smp *)b;
+    if (x->cid != y->cid) return x->cid < y->cid ? -1 : 1;
+    if (x->pos != y->pos) return x->pos < y->pos ? -1 : 1;
+    if (x->c1 != y->c1) return x->c1 < y->c1 ? -1 : 1;
+    if (g_dim3 && x->c2 != y->c2) return x->c2 < y->c2 ? -1 : 1;
+    if (x->tid != y->tid) return x->tid < y->tid ? -1 : 1;
+    return 0;
+}
+static uint64_t ivkey(int64_t c0, int64_t c1, int64_t c2) {
+    return ((uint64_t)c0 << 40) | ((uint64_t)c1 << 20) | (uint64_t)c2 | (1ULL << 62);
+}
+
+/* per simulated thread progress (Progress, pluss_utils.h:620-662) */
+typedef struct { int64_t c0, c1, c2, lb, ub; int ref; int active; } prog;
+
+static void prog_advance(const orc_cfg *c, prog *p) {
+    /* transitions of the generated state machine (r10:384,446-447,456,465,527,618-648) */
+    switch (p->ref) {
+    case R_C0: p->ref = R_C1; return;
+    case R_C1: p->c2 = 0; p->ref = R_A0; return;
+    case R_A0: p->ref = R_B0; return;
+    case R_B0: p->ref = R_C2; return;
+    case R_C2: p->ref = R_C3; return;
+    default: break;
+    }
+    if (p->c2 + 1 < c->N) { p->c2++; p->ref = R_A0; return; }
+    if (p->c1 + 1 < c->N) { p->c1++; p->ref = R_C0; return; }
+    p->c0++;
+    if (p->c0 <= p->ub) { p->c1 = 0; p->c2 = 0; p->ref = R_C0; return; }
+    p->active = 0; /* moved to idle_threads (r10:642-648) */
+}
+
+int orc_faithful(const orc_cfg *c, int REF, const uint64_t *samples, int64_t n,
+                 orc_entry *out, int64_t cap, int64_t *n_out, int64_t *traversed) {
+    if (!cfg_ok(c) || REF < 0 || REF > 5 || c->T > 4096) return -1;
+    const int dim3 = !(REF == R_C0 || REF == R_C1);
+    const int arr = REF_ARRAY[REF];
+    const int64_t T = c->T, CS = c->CS, last = c->N - 1;
+    smp *q = (smp *)malloc((size_t)(n > 0 ? n : 1) * sizeof(smp));
+    if (!q) return -3;
+    omap names; if (om_init(&names, (size_t)n + 16)) return -3;
+    for (int64_t i = 0; i < n; i++) {
+        int ref; int64_t c0, c1, c2;
+        if (unpack(c, samples[i], &ref, &c0, &c1, &c2) || ref != REF) { free(q); om_free(&names); return -4; }
+        if (!dim3) c2 = 0;
+        q[i].c0 = c0; q[i].c1 = c1; q[i].c2 = c2;
+        q[i].cid = c0 / (CS * T); q[i].tid = c0 / CS - q[i].cid * T; q[i].pos = c0 % CS;
+        uint64_t *s = om_put(&names, ivkey(c0, c1, c2));
+        if (*s) { free(q); om_free(&names); return -5; } /* duplicate sample */
+        *s = 1;
+    }
+    g_dim3 = dim3;
+    qsort(q, (size_t)n, sizeof(smp), cmp_smp);
+    int64_t head = 0; /* priority queue == sorted array popped from the front */
+
+    omap hist; if (om_init(&hist, 64)) return -3;
+    omap *lat = (omap *)calloc((size_t)T, sizeof(omap));
+    for (int64_t t = 0; t < T; t++) if (om_init(&lat[t], 16)) return -3;
+    int lat_touched = 0;           /* outer LAT map non-empty (r10:194) */
+    int64_t *count = (int64_t *)calloc((size_t)T, 8);
+    prog *pr = (prog *)calloc((size_t)T, sizeof(prog));
+    int64_t *ptsp = (int64_t *)calloc((size_t)T, 8); /* per_thread_start_point */
+    int64_t met = 0;               /* samples_meet.size() */
+    omap metset; if (om_init(&metset, 64)) return -3;
+    int64_t traversing = 0;
+    uint64_t cold = 0;
+    int cold_key = 0;
+
+    while (head < n) {
+        /* ---------------- START_SAMPLE (r10:187-274) ---------------- */
+        smp st = q[head++];
+        traversing++;
+        if (lat_touched) { cold += lat[0].n; cold_key = 1; for (int64_t t = 0; t < T; t++) om_clear(&lat[t]); lat_touched = 0; }
+        int srs = 0; /* start_reuse_search */
+        int64_t start_cid = st.cid, start_tid = st.tid;
+        for (int64_t t = 0; t < T; t++) { ptsp[t] = t * CS + start_cid * CS * T; pr[t].active = 0; }
+        for (int64_t t = 0; t < T; t++) {
+            if (ptsp[t] <= last) { /* hasNextStaticChunk */
+                int64_t lb = ptsp[t] + st.pos;
+                int64_t ub = (ptsp[t] + CS - 1 < last) ? ptsp[t] + CS - 1 : last;
+                ptsp[t] += CS * T;
+                if (lb > ub) continue; /* no iteration for this tid at the sample point */
+                pr[t].c0 = lb; pr[t].c1 = st.c1; pr[t].c2 = dim3 ? st.c2 : 0;
+                pr[t].lb = lb; pr[t].ub = ub; pr[t].ref = REF; pr[t].active = 1;
+            }
+        }
+        int any = 0; for (int64_t t = 0; t < T; t++) any |= pr[t].active;
+        if (!any) goto END_SAMPLE;
+        int first_pass = 1;
+        for (;;) {
+            if (!first_pass) {
+                /* assign next static chunks to idle threads (r10:276-302) */
+                int has_any = 0; for (int64_t t = 0; t < T; t++) has_any |= (ptsp[t] <= last);
+                if (has_any) {
+                    for (int64_t t = 0; t < T; t++) {
+                        if (pr[t].active) continue;
+                        if (!(ptsp[t] <= last)) continue;
+                        int64_t lb = ptsp[t], ub = (lb + CS - 1 < last) ? lb + CS - 1 : last;
+                        ptsp[t] += CS * T;
+                        pr[t].c0 = lb; pr[t].c1 = 0; pr[t].c2 = 0; pr[t].lb = lb; pr[t].ub = ub;
+                        pr[t].ref = R_C0; pr[t].active = 1;
+                    }
+                }
+            }
+            first_pass = 0;
+            /* INTERLEAVING_LOOP: one access per worker thread, sorted tids (r10:303-650) */
+            for (int64_t t = 0; t < T; t++) {
+                prog *p = &pr[t];
+                if (!p->active) continue;
+                if (p->c0 > p->ub) continue; /* !isInBound */
+                int ref = p->ref;
+                if (ref == REF && !srs) srs = (start_tid == t);
+                if (srs) {
+                    int same = (REF_ARRAY[ref] == arr);
+                    int is_sample = 0;
+                    uint64_t line = 0;
+                    if (same) line = addr_of(c, ref, p->c0, p->c1, p->c2);
+                    if (ref == REF) {
+                        int64_t a2 = dim3 ? p->c2 : 0;
+                        if (p->c0 == st.c0 && p->c1 == st.c1 && a2 == st.c2) {
+                            is_sample = 1;
+                        } else {
+                            int top_eq = head < n && q[head].c0 == p->c0 && q[head].c1 == p->c1 && q[head].c2 == a2;
+                            if (top_eq || om_find(&names, ivkey(p->c0, p->c1, a2))) {
+                                traversing++;
+                                if (top_eq) head++;
+                                is_sample = 1;
+                                uint64_t *ms = om_put(&metset, ivkey(p->c0, p->c1, a2));
+                                if (!*ms) { *ms = 1; met++; }
+                            }
+                        }
+                    }
+                    if (same) {
+                        lat_touched = 1;
+                        uint64_t *e = om_find(&lat[t], line + 1);
+                        if (e) {
+                            int64_t reuse = count[t] - (int64_t)(*e);
+                            int kind = (REF == R_B0 && is_share(c, reuse)) ? 1 : 0;
+                            if (hist_add(&hist, REF, kind, reuse, 1)) return -3;
+                            traversing--;
+                            if (head >= n && traversing == 0) goto END_SAMPLE;       /* r10:345 (Q3) */
+                            if (traversing == 0) {
+                                om_del(&lat[t], line + 1);
+                                if (met >= n - head) goto END_SAMPLE;                /* r10:356 (Q1) */
+                                /* skip already-met samples at the top (r10:358-366) */
+                                while (head < n && om_find(&metset, ivkey(q[head].c0, q[head].c1, q[head].c2))) head++;
+                                if (head < n) goto NEXT_START;
+                                goto END_SAMPLE;
+                            }
+                            om_del(&lat[t], line + 1);
+                        }
+                        if (is_sample) { uint64_t *s = om_put(&lat[t], line + 1); *s = (uint64_t)count[t]; }
+                    }
+                    count[t]++;
+                }
+                prog_advance(c, p);
+            }
+            int all_idle = 1, has_chunk = 0;
+            for (int64_t t = 0; t < T; t++) { all_idle &= !pr[t].active; has_chunk |= (ptsp[t] <= last); }
+            if (all_idle && !has_chunk) break;
+        }
+        goto END_SAMPLE;
+    NEXT_START:;
+    }
+END_SAMPLE:
+    if (lat_touched) { cold += lat[0].n; cold_key = 1; }
+    if (cold_key || cold) { if (hist_add(&hist, REF, 0, -1, cold)) return -3; }
+    int rc = hist_export(&hist, out, cap, n_out);
+    int64_t tot = 0; for (int64_t t = 0; t < T; t++) tot += count[t];
+    if (traversed) *traversed = tot;
+    for (int64_t t = 0; t < T; t++) om_free(&lat[t]);
+    free(lat); free(count); free(pr); free(ptsp); free(q);
+    om_free(&names); om_free(&hist); om_free(&metset);
+    return rc;
+}
+
+/* --------------------------------------------------- sample bijection -- */
+static uint64_t mix64(uint64_t z) { /* splitmix64 finaliser */
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+int orc_expand(const orc_cfg *c, uint64_t seed, int ref, uint64_t first, uint64_t n, uint64_t *out) {
+    if (!cfg_ok(c) || ref < 0 || ref > 5) return -1;
+    int dim3 = !(ref == R_C0 || ref == R_C1);
+    uint64_t m = (uint64_t)(c->range_full ? c->N : c->N - 1);
+    if (m == 0) return -1;
+    uint64_t D = dim3 ? m * m * m : m * m;
+    if (first + n > D) return -2;
+    int h = 1; while ((1ULL << (2 * h)) < D) h++;
+    uint64_t M = (1ULL << h) - 1;
+    uint64_t key[4];
+    for (int r = 0; r < 4; r++)
+        key[r] = mix64(seed ^ ((uint64_t)(ref + 1) * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)(r + 1) * 0xD1B54A32D192ED03ULL));
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t y = first + i;
+        do {
+            uint64_t L = y >> h, R = y & M;
+            for (int r = 0; r < 4; r++) { uint64_t t = R; R = L ^ (mix64(key[r] ^ R) & M); L = t; }
+            y = (L << h) | R;
+        } while (y >= D);
+        uint64_t c0, c1, c2 = 0;
+        if (dim3) { c2 = y % m; y /= m; }
+        c1 = y % m; c0 = y / m;
+        out[i] = ((uint64_t)ref << 60) | (c0 << 40) | (c1 << 20) | c2;
+    }
+    return 0;
+}
