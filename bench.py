@@ -1,0 +1,208 @@
+#!/usr/bin/env python
+"""bench.py — throughput of the PLUSS sampled reuse-interval hot path on MI355X.
+
+Workload (BASELINE.json configs[1]): GEMM N=1024,
+8 simulated threads, chunk 4, DS=8, CLS=64, clean mode, 2^24 sampled
+accesses per GPU (default per-reference split, keyed Feistel sample lists).
+One step = reset the histogram, run the sampling kernel over the resident
+sample list, merge the per-workgroup tables and export the canonical table;
+with N>1 GPUs the step also all-gathers the per-GPU tables over RCCL (the
+only exchange of the path).  Samples are sharded across ranks with no other
+communication, so per-GPU work is fixed (weak scaling).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import pluss_sampler_optimization_amd as P  # noqa: E402
+
+METRIC = "sampled accesses/sec (node) at 1/2/4/8 MI355X; HBM roofline %; MRC abs err"
+SEED = 0x5EED0001
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+BYTES_PER_SAMPLE = 8   # one packed u64 sample descriptor read once
+TABLE_CAP = 4096
+
+CONFIGS = {
+    "config2": dict(n=1024, threads=8, per_gpu=1 << 24,
+                    workload="GEMM N=1024, 8 simulated threads, chunk 4, 2^24 sampled accesses per GPU (clean)"),
+    "config4": dict(n=2048, threads=64, per_gpu=1 << 24,
+                    workload="GEMM N=2048, 64 simulated threads, chunk 4, 2^24 sampled accesses per GPU (clean)"),
+}
+
+
+def shard(counts, rank, world):
+    """Contiguous slice of each reference's sample-index range for this rank."""
+    out = []
+    for c in counts:
+        lo, hi = c * rank // world, c * (rank + 1) // world
+        out.append((lo, hi - lo))
+    return out
+
+
+def cpu_baseline(cfg, host_samples, target_s):
+    """The reference's per-sample replay (stepping oracle, one host thread per
+    core) on a bounded, evenly strided sub-sample of the same list."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    orc.build()
+    threads = max(1, min(16, os.cpu_count() or 1))
+    oc = orc.cfg(cfg.n, cfg.threads, cfg.chunk, cfg.ds, cfg.cls)
+    rng = np.random.default_rng(1)
+    pilot = host_samples[rng.choice(len(host_samples), 512, replace=False)]
+    t = time.perf_counter()
+    orc.clean_ri(oc, pilot, nthreads=threads)
+    per = (time.perf_counter() - t) / len(pilot)
+    n = int(min(len(host_samples), max(2048, target_s / max(per, 1e-9))))
+    stride = max(1, len(host_samples) // n)
+    sub = host_samples[::stride][:n]
+    t = time.perf_counter()
+    orc.clean_ri(oc, sub, nthreads=threads)
+    dt = time.perf_counter() - t
+    return {"value": len(sub) / dt, "unit": "sampled accesses/s", "cores": threads, "kind": "port",
+            "sample": f"every {stride}th sample of the rank-0 list ({len(sub)} samples, all six references), "
+                      f"stepping replay of each sample's simulated thread (oracle/pluss_oracle.c orc_clean), "
+                      f"{dt:.1f} s wall on {threads} host threads"}
+
+
+def pmc_traffic():
+    """Per-launch HBM bytes of the hot kernel from the committed rocprofv3 --pmc summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_sampled_hist.json")
+    if os.path.exists(path):
+        try:
+            return json.load(open(path)).get("hbm_bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (rank 0, N=1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    spec = CONFIGS[args.config]
+    cfg = P.SamplerConfig(n=spec["n"], threads=spec["threads"], chunk=4, ds=8, cls=64, mode="clean", device=local)
+    total = spec["per_gpu"] * world
+    counts = P.default_counts(cfg.n, total)
+    parts = shard(counts, rank, world)
+    n_local = sum(c for _, c in parts)
+
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    samples = torch.empty(n_local, dtype=torch.int64, device=dev)
+    keys = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
+    cnts = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
+    gk = torch.empty(world * TABLE_CAP, dtype=torch.int64, device=dev)
+    gc = torch.empty(world * TABLE_CAP, dtype=torch.int64, device=dev)
+    ctx = P.Context(cfg)
+    off = 0
+    for ref, (lo, cnt) in enumerate(parts):
+        ctx.expand(SEED, ref, lo, cnt, samples.data_ptr() + 8 * off, sp)
+        off += cnt
+    torch.cuda.synchronize()
+
+    pairs = []
+
+    def step(timed):
+        ctx.reset(sp)
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        ctx.sampled_hist(samples.data_ptr(), n_local, sp)
+        if timed:
+            e1.record(stream)
+            pairs.append((e0, e1))
+        ctx.export(keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
+        if world > 1:
+            dist.all_gather_into_tensor(gk, keys)
+            dist.all_gather_into_tensor(gc, cnts)
+
+    for _ in range(args.warmup):
+        step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in pairs])) if pairs else float("nan")
+    # correctness of the merged histogram: every sample of every rank is counted once
+    if world > 1:
+        h = P.hist_from_tables(gk.cpu().numpy().view(np.uint64), gc.cpu().numpy().view(np.uint64))
+    else:
+        h = P.hist_from_tables(keys.cpu().numpy().view(np.uint64), cnts.cpu().numpy().view(np.uint64))
+    assert h.total() == total, (h.total(), total)
+
+    achieved = BYTES_PER_SAMPLE * n_local / (kern_ms * 1e-3) / 1e9
+    result = {
+        "metric": METRIC,
+        "value": total * args.steps / elapsed,
+        "unit": "sampled accesses/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic: keyed cycle-walking Feistel sample lists (seed 0x5EED0001), indices in [0,N-2]",
+        "config": {"workload": spec["workload"], "N": cfg.n, "threads": cfg.threads, "chunk": 4, "ds": 8,
+                   "cls": 64, "mode": "clean", "samples_per_gpu": n_local, "global_samples": total,
+                   "parallelism": f"sample-shard x{world}" + (" + RCCL all_gather of histogram tables" if world > 1
+                                                             else "")},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic()},
+        "kernel": {"name": "k_sampled_hist<true>", "avg_ms": kern_ms, "bytes_per_launch": BYTES_PER_SAMPLE * n_local},
+        "histogram_bins": len(h.bins),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        host = samples.cpu().numpy().view(np.uint64)
+        result["cpu_baseline"] = cpu_baseline(cfg, host, args.cpu_seconds)
+    else:
+        result["cpu_baseline"] = None
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

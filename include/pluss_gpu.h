@@ -1,0 +1,127 @@
+/*
+ * pluss_gpu.h — C ABI of the MI355X-native PLUSS GEMM reuse-interval sampler.
+ *
+ * Drop-in boundary for the reference's sampler entry points (reference paths
+ * relative to sauceeeeage/PLUSS_Sampler_Optimization):
+ *
+ *   pluss_gemm_sampled_hist   replaces  void sampler_<REF>(std::unordered_map<long,double>&)
+ *                                        c_lib/test/sampler/gemm-t4-pluss-pro-model-rs-ri-opt-r10.cpp:135,698,1261,1667,2221,2638
+ *                                        (the raw no_share/share histograms it builds before
+ *                                        no_share_distribute, r10:690) — mode FAITHFUL;
+ *                                        and the per-sample RI engine with every sample
+ *                                        counted — mode CLEAN.
+ *   pluss_gemm_fulltrace_hist replaces  fn sampler(pool) / rayon_sampler(...)
+ *                                        src/gemm_sampler_rayon.rs:71,186 ;
+ *                                        fn sampler() src/gemm_sampler.rs:56 ;
+ *                                        void sampler() c_lib/test/sampler/gemm-t4-pluss-pro-model-ri-omp-seq.cpp:37
+ *                                        (the per-tid _NoSharePRI/_SharePRI contents,
+ *                                        runtime/pluss_utils.h:924-937, raw keys).
+ *   pluss_gemm_sampled_ri     per-sample parity dump (no reference counterpart; the RI
+ *                                        and sink the reference derives at r10:333/558).
+ *   pluss_expand_samples      replaces  the rand()%(N-1) sample generation + dedup,
+ *                                        r10:156-185 (deterministic, distinct by construction).
+ *   pluss_default_counts      the per-reference sample counts of r10:156,719,1282,1688,2242,2659
+ *                                        generalised to a total sample budget.
+ *
+ * Everything the reference hard-codes at compile time (THREAD_NUM, CHUNK_SIZE,
+ * DS, CLS: c_lib/test/Makefile:14-15; N=128 literals; the two share thresholds
+ * seq.cpp:203 vs r10:2482) is a field of pluss_cfg.  Outputs are caller-owned;
+ * the library keeps no global state between calls except per-handle buffers.
+ * No function throws across the ABI; all return 0 or a negative PLUSS_ERR_*.
+ */
+#ifndef PLUSS_GPU_H
+#define PLUSS_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* reference ids = access order inside one c1 iteration (seq.cpp:102-288) */
+enum { PLUSS_C0 = 0, PLUSS_C1 = 1, PLUSS_A0 = 2, PLUSS_B0 = 3, PLUSS_C2 = 4, PLUSS_C3 = 5, PLUSS_NREFS = 6 };
+enum { PLUSS_NOSHARE = 0, PLUSS_SHARE = 1 };
+enum { PLUSS_MODE_CLEAN = 0, PLUSS_MODE_FAITHFUL = 1 };
+enum { PLUSS_THR_R10 = 0, PLUSS_THR_V1 = 1 };
+
+#define PLUSS_OK 0
+#define PLUSS_ERR_CONFIG (-1)   /* invalid or unsupported pluss_cfg */
+#define PLUSS_ERR_HIP (-2)      /* HIP runtime error (see pluss_last_error) */
+#define PLUSS_ERR_ALLOC (-3)    /* device/host allocation failed */
+#define PLUSS_ERR_CAPACITY (-4) /* output or histogram table too small */
+#define PLUSS_ERR_INPUT (-5)    /* malformed sample (ref > 5 or index >= N, wrong ref) */
+
+typedef struct pluss_cfg {
+  int64_t n;           /* loop bound N of the GEMM nest (reference: literal 128) */
+  int64_t threads;     /* simulated OpenMP threads (THREAD_NUM) */
+  int64_t chunk;       /* static chunk size (CHUNK_SIZE) */
+  int64_t ds;          /* element size in bytes (DS) */
+  int64_t cls;         /* cache-line size in bytes (CLS); must be a multiple of ds */
+  int32_t mode;        /* PLUSS_MODE_CLEAN | PLUSS_MODE_FAITHFUL */
+  int32_t thr_variant; /* PLUSS_THR_R10: (4N+2)N (r10:2482) | PLUSS_THR_V1: (N+1)N+1 (seq.cpp:203) */
+  int32_t range_full;  /* sample indices: 0 -> [0,N-2] like rand()%(N-1) (r10:159); 1 -> [0,N-1] */
+  int32_t device;      /* HIP device ordinal */
+} pluss_cfg;
+
+/* one histogram bin: (reference, noshare/share, raw reuse interval) -> count.
+   ri == -1 is the cold bin (the reference's key -1, seq.cpp:305-319, r10:196,671). */
+typedef struct pluss_hist_entry {
+  int32_t ref;
+  int32_t kind;
+  int64_t ri;
+  uint64_t count;
+} pluss_hist_entry;
+
+typedef struct pluss_hist {
+  pluss_hist_entry *entries; /* caller-owned array */
+  uint64_t capacity;         /* entries available */
+  uint64_t n_entries;        /* out: bins written, sorted by (ref, kind, ri) */
+  uint64_t traversed[6];     /* out: faithful mode: per-ref accesses replayed (r10:694); full trace: total */
+} pluss_hist;
+
+typedef struct pluss_ctx pluss_ctx;
+
+/* --- diagnostics ------------------------------------------------------- */
+const char *pluss_last_error(void);
+int pluss_device_count(int *n);
+int pluss_version(void);
+
+/* --- one-shot entry points (host buffers in, host histogram out) --------- */
+int pluss_gemm_sampled_hist(const pluss_cfg *cfg, const uint64_t *samples, uint64_t n, pluss_hist *out);
+int pluss_gemm_fulltrace_hist(const pluss_cfg *cfg, pluss_hist *out);
+int pluss_gemm_sampled_ri(const pluss_cfg *cfg, const uint64_t *samples, uint64_t n, int64_t *ri_out,
+                          uint64_t *sink_key_out);
+int pluss_expand_samples(const pluss_cfg *cfg, uint64_t seed, int32_t ref, uint64_t first, uint64_t n,
+                         uint64_t *out);
+int pluss_default_counts(int64_t n, uint64_t total, uint64_t counts[6]);
+
+/* --- handle API: device-resident inputs, explicit streams ----------------
+   `stream` is a hipStream_t (NULL = the handle's own stream).  Device
+   pointers are plain addresses of device memory on cfg->device.           */
+int pluss_ctx_create(const pluss_cfg *cfg, pluss_ctx **out);
+int pluss_ctx_destroy(pluss_ctx *ctx);
+void *pluss_ctx_stream(pluss_ctx *ctx);
+int pluss_dev_expand(pluss_ctx *ctx, uint64_t seed, int32_t ref, uint64_t first, uint64_t n, uint64_t *d_out,
+                     void *stream);
+int pluss_dev_hist_reset(pluss_ctx *ctx, void *stream);
+/* clean mode: accumulate every sample of a mixed-reference list */
+int pluss_dev_sampled_hist(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t n, void *stream);
+/* faithful mode: one sampler_<REF> over a list holding only reference `ref` */
+int pluss_dev_faithful_hist(pluss_ctx *ctx, int32_t ref, const uint64_t *d_samples, uint64_t n, void *stream);
+/* full trace: every access of the nest (sampling rate 1.0) */
+int pluss_dev_fulltrace_hist(pluss_ctx *ctx, void *stream);
+int pluss_dev_sampled_ri(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t n, int64_t *d_ri, uint64_t *d_sink,
+                         void *stream);
+/* canonical table: `cap` (key,count) pairs sorted by key, unused = (~0,0);
+   key = ref<<60 | kind<<56 | (ri+2).  Equal histograms give equal tables,
+   so per-GPU tables can be exchanged by one collective and merged. */
+int pluss_dev_hist_export(pluss_ctx *ctx, uint64_t *d_keys, uint64_t *d_counts, uint64_t cap, void *stream);
+/* synchronise and copy the handle's histogram into a host pluss_hist */
+int pluss_hist_fetch(pluss_ctx *ctx, pluss_hist *out);
+/* merge canonical (key,count) tables on the host into a pluss_hist */
+int pluss_hist_from_tables(const uint64_t *keys, const uint64_t *counts, uint64_t n_pairs, pluss_hist *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PLUSS_GPU_H */

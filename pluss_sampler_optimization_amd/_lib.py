@@ -1,0 +1,97 @@
+"""ctypes binding of libpluss_gpu.so (include/pluss_gpu.h).
+
+The library is loaded from this package's lib/ directory (built in-tree by
+build.py).  There is deliberately no fallback: if the library is missing or a
+call fails, an exception is raised.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libpluss_gpu.so")
+
+PLUSS_OK = 0
+ERRORS = {-1: "PLUSS_ERR_CONFIG", -2: "PLUSS_ERR_HIP", -3: "PLUSS_ERR_ALLOC", -4: "PLUSS_ERR_CAPACITY",
+          -5: "PLUSS_ERR_INPUT"}
+
+# every symbol declared in include/pluss_gpu.h
+EXPORTS = [
+    "pluss_last_error", "pluss_device_count", "pluss_version",
+    "pluss_gemm_sampled_hist", "pluss_gemm_fulltrace_hist", "pluss_gemm_sampled_ri", "pluss_expand_samples",
+    "pluss_default_counts",
+    "pluss_ctx_create", "pluss_ctx_destroy", "pluss_ctx_stream", "pluss_dev_expand", "pluss_dev_hist_reset",
+    "pluss_dev_sampled_hist", "pluss_dev_faithful_hist", "pluss_dev_fulltrace_hist", "pluss_dev_sampled_ri",
+    "pluss_dev_hist_export", "pluss_hist_fetch", "pluss_hist_from_tables",
+]
+
+
+class PlussCfg(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("threads", ctypes.c_int64), ("chunk", ctypes.c_int64),
+                ("ds", ctypes.c_int64), ("cls", ctypes.c_int64), ("mode", ctypes.c_int32),
+                ("thr_variant", ctypes.c_int32), ("range_full", ctypes.c_int32), ("device", ctypes.c_int32)]
+
+
+class PlussHistEntry(ctypes.Structure):
+    _fields_ = [("ref", ctypes.c_int32), ("kind", ctypes.c_int32), ("ri", ctypes.c_int64),
+                ("count", ctypes.c_uint64)]
+
+
+class PlussHist(ctypes.Structure):
+    _fields_ = [("entries", ctypes.POINTER(PlussHistEntry)), ("capacity", ctypes.c_uint64),
+                ("n_entries", ctypes.c_uint64), ("traversed", ctypes.c_uint64 * 6)]
+
+
+class PlussError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libpluss_gpu.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PlussError(f"{LIB_PATH} is missing: build it with `python -m pluss_sampler_optimization_amd.build` "
+                         "(hipcc, gfx950); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    u64, i64, i32, vp = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
+    cfgp, histp = P(PlussCfg), P(PlussHist)
+    sig = {
+        "pluss_last_error": (ctypes.c_char_p, []),
+        "pluss_device_count": (ctypes.c_int, [P(ctypes.c_int)]),
+        "pluss_version": (ctypes.c_int, []),
+        "pluss_gemm_sampled_hist": (ctypes.c_int, [cfgp, vp, u64, histp]),
+        "pluss_gemm_fulltrace_hist": (ctypes.c_int, [cfgp, histp]),
+        "pluss_gemm_sampled_ri": (ctypes.c_int, [cfgp, vp, u64, vp, vp]),
+        "pluss_expand_samples": (ctypes.c_int, [cfgp, u64, i32, u64, u64, vp]),
+        "pluss_default_counts": (ctypes.c_int, [i64, u64, P(u64)]),
+        "pluss_ctx_create": (ctypes.c_int, [cfgp, P(vp)]),
+        "pluss_ctx_destroy": (ctypes.c_int, [vp]),
+        "pluss_ctx_stream": (vp, [vp]),
+        "pluss_dev_expand": (ctypes.c_int, [vp, u64, i32, u64, u64, vp, vp]),
+        "pluss_dev_hist_reset": (ctypes.c_int, [vp, vp]),
+        "pluss_dev_sampled_hist": (ctypes.c_int, [vp, vp, u64, vp]),
+        "pluss_dev_faithful_hist": (ctypes.c_int, [vp, i32, vp, u64, vp]),
+        "pluss_dev_fulltrace_hist": (ctypes.c_int, [vp, vp]),
+        "pluss_dev_sampled_ri": (ctypes.c_int, [vp, vp, u64, vp, vp, vp]),
+        "pluss_dev_hist_export": (ctypes.c_int, [vp, vp, vp, u64, vp]),
+        "pluss_hist_fetch": (ctypes.c_int, [vp, histp]),
+        "pluss_hist_from_tables": (ctypes.c_int, [vp, vp, u64, histp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc, what=""):
+    if rc != PLUSS_OK:
+        msg = lib().pluss_last_error().decode(errors="replace")
+        raise PlussError(f"{what}: {ERRORS.get(rc, rc)}: {msg}")
+    return rc

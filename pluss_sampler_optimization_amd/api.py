@@ -1,0 +1,232 @@
+"""Python front end of the MI355X PLUSS sampler (thin layer over the C ABI).
+
+Mirrors the reference's sampler entry points:
+
+  sampled_hist(cfg, samples)  ~ r10 sampler_<REF>(histogram) raw histograms
+                                (c_lib/test/sampler/gemm-t4-pluss-pro-model-rs-ri-opt-r10.cpp:135..3190)
+  fulltrace_hist(cfg)         ~ seq sampler() / rayon sampler(pool)
+                                (…-ri-omp-seq.cpp:37, src/gemm_sampler_rayon.rs:71)
+  expand_samples(...)         ~ the rand()%(N-1) sample generation (r10:156-185)
+
+Every computation runs in libpluss_gpu.so on a HIP device.
+"""
+import ctypes
+from collections import defaultdict
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import PlussCfg, PlussHist, PlussHistEntry, check, lib
+
+REFS = ["C0", "C1", "A0", "B0", "C2", "C3"]
+REF_ID = {r: i for i, r in enumerate(REFS)}
+REF_ARRAY = {"C0": "C", "C1": "C", "A0": "A", "B0": "B", "C2": "C", "C3": "C"}
+DIM = {"C0": 2, "C1": 2, "A0": 3, "B0": 3, "C2": 3, "C3": 3}
+NOSHARE, SHARE = 0, 1
+KEY_EMPTY = (1 << 64) - 1
+
+
+@dataclass
+class SamplerConfig:
+    """Everything the reference fixes at compile time (Makefile:14-15, N=128 literals)."""
+    n: int = 128           # GEMM loop bound N
+    threads: int = 4       # THREAD_NUM
+    chunk: int = 4         # CHUNK_SIZE
+    ds: int = 8            # DS
+    cls: int = 64          # CLS
+    mode: str = "clean"    # "clean" (every sample) | "faithful" (r10 queue semantics)
+    thr_variant: str = "r10"  # "r10": (4N+2)N (r10:2482) | "v1": (N+1)N+1 (seq.cpp:203)
+    range_full: bool = False  # sample indices in [0,N-1] instead of rand()%(N-1)'s [0,N-2]
+    device: int = 0
+
+    def to_c(self):
+        return PlussCfg(self.n, self.threads, self.chunk, self.ds, self.cls,
+                        {"clean": 0, "faithful": 1}[self.mode], {"r10": 0, "v1": 1}[self.thr_variant],
+                        1 if self.range_full else 0, self.device)
+
+
+class Histogram:
+    """Exact raw reuse-interval bins: {(ref, kind, ri): count}; ri = -1 is cold."""
+
+    def __init__(self, bins=None, traversed=None):
+        self.bins = dict(bins or {})
+        self.traversed = list(traversed or [0] * 6)
+
+    @classmethod
+    def _from_c(cls, h):
+        bins = {}
+        for i in range(h.n_entries):
+            e = h.entries[i]
+            bins[(REFS[e.ref], int(e.kind), int(e.ri))] = int(e.count)
+        return cls(bins, [int(x) for x in h.traversed])
+
+    def _select(self, kind, ref):
+        out = defaultdict(int)
+        for (r, k, ri), c in self.bins.items():
+            if k == kind and (ref is None or r == ref):
+                out[ri] += c
+        return dict(out)
+
+    def noshare(self, ref=None):
+        """{ri: count} of the noshare histogram (cold at key -1), like no_share_histogram (r10:146)."""
+        return self._select(NOSHARE, ref)
+
+    def share(self, ref=None):
+        """{ri: count} of the share histogram (share_ratio THREAD_NUM-1, r10:2483)."""
+        return self._select(SHARE, ref)
+
+    def cold(self, ref=None):
+        return self.noshare(ref).get(-1, 0)
+
+    def total(self):
+        return sum(self.bins.values())
+
+    def __eq__(self, other):
+        a = {k: v for k, v in self.bins.items() if v}
+        b = {k: v for k, v in other.bins.items() if v}
+        return a == b
+
+    def __repr__(self):
+        return f"Histogram({len(self.bins)} bins, total={self.total()})"
+
+
+def _hist_buf(cap=1 << 14):
+    entries = (PlussHistEntry * cap)()
+    h = PlussHist()
+    h.entries = entries
+    h.capacity = cap
+    return h, entries
+
+
+def _u64(a):
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    return a, a.ctypes.data_as(ctypes.c_void_p)
+
+
+def pack(ref, c0, c1, c2=0):
+    """Packed sample ref(4)|c0(20)|c1(20)|c2(20)."""
+    rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
+    return (rid << 60) | (int(c0) << 40) | (int(c1) << 20) | int(c2)
+
+
+def pack_array(ref, idx):
+    rid = np.uint64(REF_ID[ref] if isinstance(ref, str) else int(ref))
+    idx = np.asarray(idx, dtype=np.uint64)
+    c2 = idx[:, 2] if idx.shape[1] > 2 else np.zeros(len(idx), np.uint64)
+    return (rid << np.uint64(60)) | (idx[:, 0] << np.uint64(40)) | (idx[:, 1] << np.uint64(20)) | c2
+
+
+def unpack_array(s):
+    s = np.asarray(s, dtype=np.uint64)
+    m = np.uint64(0xFFFFF)
+    return ((s >> np.uint64(60)).astype(np.int64), ((s >> np.uint64(40)) & m).astype(np.int64),
+            ((s >> np.uint64(20)) & m).astype(np.int64), (s & m).astype(np.int64))
+
+
+def sampled_hist(cfg, samples):
+    """Histogram of a host sample list (clean: all samples; faithful: per-ref r10 semantics)."""
+    s, p = _u64(samples)
+    h, keep = _hist_buf()
+    c = cfg.to_c()
+    check(lib().pluss_gemm_sampled_hist(ctypes.byref(c), p, len(s), ctypes.byref(h)), "pluss_gemm_sampled_hist")
+    return Histogram._from_c(h)
+
+
+def fulltrace_hist(cfg):
+    h, keep = _hist_buf()
+    c = cfg.to_c()
+    check(lib().pluss_gemm_fulltrace_hist(ctypes.byref(c), ctypes.byref(h)), "pluss_gemm_fulltrace_hist")
+    return Histogram._from_c(h)
+
+
+def sampled_ri(cfg, samples):
+    """Per-sample (ri, sink_key) on the device; ri = -1 cold, sink = 2^64-1 for cold."""
+    s, p = _u64(samples)
+    ri = np.empty(len(s), dtype=np.int64)
+    sink = np.empty(len(s), dtype=np.uint64)
+    c = cfg.to_c()
+    check(lib().pluss_gemm_sampled_ri(ctypes.byref(c), p, len(s), ri.ctypes.data_as(ctypes.c_void_p),
+                                      sink.ctypes.data_as(ctypes.c_void_p)), "pluss_gemm_sampled_ri")
+    return ri, sink
+
+
+def expand_samples(cfg, seed, ref, first, n):
+    out = np.empty(n, dtype=np.uint64)
+    c = cfg.to_c()
+    rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
+    check(lib().pluss_expand_samples(ctypes.byref(c), seed, rid, first, n, out.ctypes.data_as(ctypes.c_void_p)),
+          "pluss_expand_samples")
+    return out
+
+
+def default_counts(n, total):
+    counts = (ctypes.c_uint64 * 6)()
+    check(lib().pluss_default_counts(n, total, counts), "pluss_default_counts")
+    return [int(x) for x in counts]
+
+
+def hist_from_tables(keys, counts):
+    k, kp = _u64(keys)
+    c, cp = _u64(counts)
+    h, keep = _hist_buf()
+    check(lib().pluss_hist_from_tables(kp, cp, len(k), ctypes.byref(h)), "pluss_hist_from_tables")
+    return Histogram._from_c(h)
+
+
+class Context:
+    """Handle API: device-resident samples, explicit HIP streams (raw pointers)."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self._c = cfg.to_c()
+        self._h = ctypes.c_void_p()
+        check(lib().pluss_ctx_create(ctypes.byref(self._c), ctypes.byref(self._h)), "pluss_ctx_create")
+
+    @property
+    def stream(self):
+        return lib().pluss_ctx_stream(self._h)
+
+    def close(self):
+        if self._h:
+            lib().pluss_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self, stream=None):
+        check(lib().pluss_dev_hist_reset(self._h, stream), "pluss_dev_hist_reset")
+
+    def expand(self, seed, ref, first, n, d_out, stream=None):
+        rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
+        check(lib().pluss_dev_expand(self._h, seed, rid, first, n, d_out, stream), "pluss_dev_expand")
+
+    def sampled_hist(self, d_samples, n, stream=None):
+        check(lib().pluss_dev_sampled_hist(self._h, d_samples, n, stream), "pluss_dev_sampled_hist")
+
+    def faithful_hist(self, ref, d_samples, n, stream=None):
+        rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
+        check(lib().pluss_dev_faithful_hist(self._h, rid, d_samples, n, stream), "pluss_dev_faithful_hist")
+
+    def fulltrace(self, stream=None):
+        check(lib().pluss_dev_fulltrace_hist(self._h, stream), "pluss_dev_fulltrace_hist")
+
+    def sampled_ri(self, d_samples, n, d_ri, d_sink, stream=None):
+        check(lib().pluss_dev_sampled_ri(self._h, d_samples, n, d_ri, d_sink, stream), "pluss_dev_sampled_ri")
+
+    def export(self, d_keys, d_counts, cap, stream=None):
+        check(lib().pluss_dev_hist_export(self._h, d_keys, d_counts, cap, stream), "pluss_dev_hist_export")
+
+    def fetch(self):
+        h, keep = _hist_buf()
+        check(lib().pluss_hist_fetch(self._h, ctypes.byref(h)), "pluss_hist_fetch")
+        return Histogram._from_c(h)

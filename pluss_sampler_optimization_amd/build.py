@@ -1,0 +1,69 @@
+"""Build libpluss_gpu.so (gfx950) in-tree with hipcc.
+
+The shared library is the product: the C ABI of include/pluss_gpu.h over the
+HIP kernels in csrc/.  It is built next to this file (lib/) so it travels
+with the repository snapshot to the GPU box.
+"""
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+OBJDIR = os.path.join(LIBDIR, "obj")
+LIB = os.path.join(LIBDIR, "libpluss_gpu.so")
+ARCH = os.environ.get("PLUSS_OFFLOAD_ARCH", "gfx950")
+SOURCES = ["pluss_kernels.hip", "pluss_faithful.hip", "pluss_capi.hip"]
+HEADERS = ["pluss_model.h", "pluss_internal.h", "pluss_device.h"]
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: the PLUSS GPU library needs ROCm's hipcc")
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(verbose=False, force=False):
+    os.makedirs(OBJDIR, exist_ok=True)
+    hipcc = _hipcc()
+    inc = os.path.join(HERE, "..", "include")
+    common_deps = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(inc, "pluss_gpu.h"), __file__]
+    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", inc, "-I", CSRC,
+             "-Wall", "-Wno-unused-result"]
+    jobs = []
+    objs = []
+    for src in SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(OBJDIR, src.replace(".hip", ".o"))
+        objs.append(o)
+        if force or _stale(o, [s] + common_deps):
+            jobs.append([hipcc, *flags, "-c", s, "-o", o])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        return r
+
+    with ThreadPoolExecutor(max_workers=len(jobs) or 1) as ex:
+        list(ex.map(run, jobs))
+    if force or jobs or _stale(LIB, objs):
+        run([hipcc, "-shared", f"--offload-arch={ARCH}", "-o", LIB, *objs])
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True, force="--force" in sys.argv))

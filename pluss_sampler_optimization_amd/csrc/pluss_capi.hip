@@ -1,0 +1,367 @@
+// pluss_capi.hip — the extern "C" boundary (include/pluss_gpu.h).
+//
+// Host-side plumbing only: configuration checks, handle lifetime, device
+// buffers, launches on the caller's stream and copies of the final histogram.
+// All per-sample work runs in the kernels of pluss_kernels.hip /
+// pluss_faithful.hip; there is no CPU fallback — without a usable HIP device
+// every entry point returns PLUSS_ERR_HIP.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "pluss_internal.h"
+
+namespace pluss {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+int validate_cfg(const pluss_cfg* c, Model* m) {
+  if (!c) {
+    set_error("null pluss_cfg");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (c->n < 1 || c->n >= (1 << 20)) {
+    set_error("cfg.n must be in [1, 2^20) (20-bit sample fields)");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (c->threads < 1 || c->threads > 65536 || c->chunk < 1 || c->chunk > 65536 ||
+      c->threads * c->chunk > (1ll << 30)) {
+    set_error("cfg.threads and cfg.chunk must be in [1, 65536] with threads*chunk < 2^30");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (c->ds < 1 || c->cls < c->ds || c->cls % c->ds != 0 || c->cls / c->ds > 4096) {
+    set_error("cfg.cls must be a positive multiple of cfg.ds (<= 4096 elements per line)");
+    return PLUSS_ERR_CONFIG;
+  }
+  if ((c->mode != PLUSS_MODE_CLEAN && c->mode != PLUSS_MODE_FAITHFUL) ||
+      (c->thr_variant != PLUSS_THR_R10 && c->thr_variant != PLUSS_THR_V1) || (c->range_full != 0 && c->range_full != 1)) {
+    set_error("cfg.mode / cfg.thr_variant / cfg.range_full out of range");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (m) {
+    const uint64_t N = (uint64_t)c->n;
+    m->N = (uint32_t)N;
+    m->T = (uint32_t)c->threads;
+    m->CS = (uint32_t)c->chunk;
+    m->W = (uint32_t)(c->cls / c->ds);
+    m->S = (uint32_t)(4 * N + 2);
+    m->R = N * (4 * N + 2);
+    m->fast = (N % m->W == 0) ? 1u : 0u;
+    m->thr = c->thr_variant == PLUSS_THR_V1 ? (N + 1) * N + 1 : (4 * N + 2) * N;
+    m->A = (N % ((uint64_t)c->chunk * c->threads) == 0) ? (N / c->threads) * m->R : 0;
+    m->dCS = make_fastdiv(m->CS);
+    m->dT = make_fastdiv(m->T);
+    m->dW = make_fastdiv(m->W);
+    m->dN = make_fastdiv(m->N);
+  }
+  return PLUSS_OK;
+}
+
+static int check_flags(pluss_ctx* ctx) {
+  unsigned int f[4] = {0, 0, 0, 0};
+  PLUSS_HIP_CHECK(hipMemcpy(f, ctx->g.flags, sizeof f, hipMemcpyDeviceToHost));
+  if (f[1]) {
+    set_error("malformed sample: ref > 5, an index >= N, or a reference other than the one requested");
+    return PLUSS_ERR_INPUT;
+  }
+  if (f[0]) {
+    set_error("histogram table overflow (more distinct (ref,kind,RI) keys than the table holds)");
+    return PLUSS_ERR_CAPACITY;
+  }
+  return PLUSS_OK;
+}
+
+static hipStream_t pick(pluss_ctx* ctx, void* stream) {
+  ctx->last = stream ? (hipStream_t)stream : ctx->stream;
+  return ctx->last;
+}
+
+static void decode_entry(uint64_t key, uint64_t cnt, pluss_hist_entry* e) {
+  e->ref = (int32_t)key_ref(key);
+  e->kind = (int32_t)key_kind(key);
+  e->ri = key_ri(key);
+  e->count = cnt;
+}
+
+}  // namespace pluss
+
+using namespace pluss;
+
+extern "C" {
+
+const char* pluss_last_error(void) { return g_err.c_str(); }
+
+int pluss_version(void) { return 1; }
+
+int pluss_device_count(int* n) {
+  if (!n) return PLUSS_ERR_CONFIG;
+  PLUSS_HIP_CHECK(hipGetDeviceCount(n));
+  return PLUSS_OK;
+}
+
+int pluss_default_counts(int64_t n, uint64_t total, uint64_t counts[6]) {
+  // r10 uses 164 samples for the 2-D references and 2098 for the 3-D ones at
+  // N=128 (r10:156,1688).  Generalised: 2-D refs get
+  // ceil(1% of (N-1)^2); the rest is split evenly over the four 3-D refs with
+  // the remainder going to B0.
+  if (n < 2 || !counts) {
+    set_error("pluss_default_counts: n must be >= 2");
+    return PLUSS_ERR_CONFIG;
+  }
+  const uint64_t m = (uint64_t)(n - 1);
+  const uint64_t c2d = (m * m + 99) / 100;
+  if (2 * c2d > total) {
+    set_error("pluss_default_counts: total too small for the 2-D references");
+    return PLUSS_ERR_CONFIG;
+  }
+  const uint64_t rest = total - 2 * c2d, c3d = rest / 4;
+  if (c3d + (rest - 4 * c3d) > m * m * m) {
+    set_error("pluss_default_counts: more 3-D samples than distinct iteration points");
+    return PLUSS_ERR_CONFIG;
+  }
+  counts[PLUSS_C0] = counts[PLUSS_C1] = c2d;
+  counts[PLUSS_A0] = counts[PLUSS_C2] = counts[PLUSS_C3] = c3d;
+  counts[PLUSS_B0] = c3d + (rest - 4 * c3d);
+  return PLUSS_OK;
+}
+
+int pluss_ctx_create(const pluss_cfg* cfg, pluss_ctx** out) {
+  if (!out) return PLUSS_ERR_CONFIG;
+  *out = nullptr;
+  Model m;
+  if (int rc = validate_cfg(cfg, &m)) return rc;
+  int ndev = 0;
+  PLUSS_HIP_CHECK(hipGetDeviceCount(&ndev));
+  if (cfg->device < 0 || cfg->device >= ndev) {
+    set_error("cfg.device out of range (" + std::to_string(ndev) + " HIP devices)");
+    return PLUSS_ERR_CONFIG;
+  }
+  PLUSS_HIP_CHECK(hipSetDevice(cfg->device));
+  pluss_ctx* c = new pluss_ctx();
+  std::memset((void*)c, 0, sizeof(pluss_ctx));
+  c->fb = FaithfulBufs();
+  c->cfg = *cfg;
+  c->m = m;
+  c->device = cfg->device;
+  auto fail = [&](const char* what) {
+    set_error(std::string("pluss_ctx_create: ") + what);
+    pluss_ctx_destroy(c);
+    return PLUSS_ERR_ALLOC;
+  };
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+  if (hipMalloc((void**)&c->g.keys, GCAP * 8) != hipSuccess) return fail("table");
+  if (hipMalloc((void**)&c->g.counts, GCAP * 8) != hipSuccess) return fail("table");
+  if (hipMalloc((void**)&c->g.flags, 16) != hipSuccess) return fail("flags");
+  if (hipMalloc((void**)&c->slabs.keys, (size_t)MAX_BLOCKS * TCAP * 8) != hipSuccess) return fail("slabs");
+  if (hipMalloc((void**)&c->slabs.counts, (size_t)MAX_BLOCKS * TCAP * 4) != hipSuccess) return fail("slabs");
+  if (hipMalloc((void**)&c->slabs.n, (size_t)MAX_BLOCKS * 4) != hipSuccess) return fail("slabs");
+  if (hipMalloc((void**)&c->d_trav, 8 * 8) != hipSuccess) return fail("trav");
+  if (hipMalloc((void**)&c->d_exp_keys, GCAP * 8) != hipSuccess) return fail("export");
+  if (hipMalloc((void**)&c->d_exp_counts, GCAP * 8) != hipSuccess) return fail("export");
+  if (hipMalloc((void**)&c->d_exp_n, 16) != hipSuccess) return fail("export");
+  if (int rc = launch_table_reset(c, c->stream)) {
+    pluss_ctx_destroy(c);
+    return rc;
+  }
+  if (hipStreamSynchronize(c->stream) != hipSuccess) return fail("init sync");
+  *out = c;
+  return PLUSS_OK;
+}
+
+int pluss_ctx_destroy(pluss_ctx* c) {
+  if (!c) return PLUSS_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  void* bufs[] = {c->g.keys,   c->g.counts,   c->g.flags,       c->slabs.keys,  c->slabs.counts, c->slabs.n,
+                  c->d_trav,   c->d_exp_keys, c->d_exp_counts,  c->d_exp_n,     c->fb.keys,      c->fb.sinks,
+                  c->fb.keys_s, c->fb.sinks_s, c->fb.pmax,       c->fb.flags,    c->fb.nstart,    c->fb.tmp,
+                  c->fb.scal};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return PLUSS_OK;
+}
+
+void* pluss_ctx_stream(pluss_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int pluss_dev_hist_reset(pluss_ctx* ctx, void* stream) {
+  if (!ctx) return PLUSS_ERR_CONFIG;
+  return launch_table_reset(ctx, pick(ctx, stream));
+}
+
+int pluss_dev_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, void* stream) {
+  if (!ctx || (!d_samples && n)) return PLUSS_ERR_CONFIG;
+  return launch_sampled_hist(ctx, d_samples, n, pick(ctx, stream));
+}
+
+int pluss_dev_faithful_hist(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, void* stream) {
+  if (!ctx || (!d_samples && n) || ref < 0 || ref > 5) return PLUSS_ERR_CONFIG;
+  return launch_faithful(ctx, ref, d_samples, n, pick(ctx, stream));
+}
+
+int pluss_dev_fulltrace_hist(pluss_ctx* ctx, void* stream) {
+  if (!ctx) return PLUSS_ERR_CONFIG;
+  if (int rc = launch_fulltrace(ctx, pick(ctx, stream))) return rc;
+  const unsigned long long total = (unsigned long long)ctx->m.N * ctx->m.N * ctx->m.S;
+  PLUSS_HIP_CHECK(hipMemcpyAsync(ctx->d_trav, &total, 8, hipMemcpyHostToDevice, pick(ctx, stream)));
+  PLUSS_HIP_CHECK(hipStreamSynchronize(pick(ctx, stream)));  // `total` is a stack value
+  return PLUSS_OK;
+}
+
+int pluss_dev_sampled_ri(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, int64_t* d_ri, uint64_t* d_sink,
+                         void* stream) {
+  if (!ctx || (n && (!d_samples || !d_ri))) return PLUSS_ERR_CONFIG;
+  return launch_ri_dump(ctx, d_samples, n, d_ri, d_sink, pick(ctx, stream));
+}
+
+int pluss_dev_expand(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t first, uint64_t n, uint64_t* d_out,
+                     void* stream) {
+  if (!ctx || ref < 0 || ref > 5 || (n && !d_out)) return PLUSS_ERR_CONFIG;
+  return launch_expand(ctx, seed, ref, first, n, d_out, pick(ctx, stream));
+}
+
+int pluss_dev_hist_export(pluss_ctx* ctx, uint64_t* d_keys, uint64_t* d_counts, uint64_t cap, void* stream) {
+  if (!ctx || !d_keys || !d_counts) return PLUSS_ERR_CONFIG;
+  return launch_export(ctx, (unsigned long long*)d_keys, (unsigned long long*)d_counts, cap, pick(ctx, stream));
+}
+
+int pluss_hist_fetch(pluss_ctx* ctx, pluss_hist* out) {
+  if (!ctx || !out) return PLUSS_ERR_CONFIG;
+  hipStream_t s = ctx->last ? ctx->last : ctx->stream;
+  if (int rc = launch_export(ctx, ctx->d_exp_keys, ctx->d_exp_counts, GCAP, s)) return rc;
+  PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+  if (int rc = check_flags(ctx)) return rc;
+  unsigned int n = 0;
+  PLUSS_HIP_CHECK(hipMemcpy(&n, ctx->d_exp_n, 4, hipMemcpyDeviceToHost));
+  std::vector<unsigned long long> k(n), c(n), tr(8);
+  if (n) {
+    PLUSS_HIP_CHECK(hipMemcpy(k.data(), ctx->d_exp_keys, n * 8ull, hipMemcpyDeviceToHost));
+    PLUSS_HIP_CHECK(hipMemcpy(c.data(), ctx->d_exp_counts, n * 8ull, hipMemcpyDeviceToHost));
+  }
+  PLUSS_HIP_CHECK(hipMemcpy(tr.data(), ctx->d_trav, 64, hipMemcpyDeviceToHost));
+  for (int r = 0; r < 6; ++r) out->traversed[r] = tr[r];
+  out->n_entries = n;
+  if (n > out->capacity) {
+    set_error("pluss_hist_fetch: output capacity " + std::to_string(out->capacity) + " < " + std::to_string(n) +
+              " bins");
+    return PLUSS_ERR_CAPACITY;
+  }
+  for (unsigned int i = 0; i < n; ++i) decode_entry(k[i], c[i], &out->entries[i]);
+  return PLUSS_OK;
+}
+
+int pluss_hist_from_tables(const uint64_t* keys, const uint64_t* counts, uint64_t n_pairs, pluss_hist* out) {
+  if (!out || (n_pairs && (!keys || !counts))) return PLUSS_ERR_CONFIG;
+  std::map<uint64_t, uint64_t> acc;
+  for (uint64_t i = 0; i < n_pairs; ++i)
+    if (keys[i] != KEY_EMPTY) acc[keys[i]] += counts[i];
+  out->n_entries = acc.size();
+  if (acc.size() > out->capacity) {
+    set_error("pluss_hist_from_tables: output capacity too small");
+    return PLUSS_ERR_CAPACITY;
+  }
+  uint64_t i = 0;
+  for (auto& kv : acc) decode_entry(kv.first, kv.second, &out->entries[i++]);
+  return PLUSS_OK;
+}
+
+// ---------------------------------------------------------- one-shot API --
+struct Scoped {
+  pluss_ctx* ctx = nullptr;
+  std::vector<void*> bufs;
+  ~Scoped() {
+    for (void* p : bufs) (void)hipFree(p);
+    if (ctx) pluss_ctx_destroy(ctx);
+  }
+};
+
+static int upload(Scoped& sc, const uint64_t* h, uint64_t n, uint64_t** d) {
+  *d = nullptr;
+  if (!n) return PLUSS_OK;
+  PLUSS_HIP_CHECK(hipMalloc((void**)d, n * 8));
+  sc.bufs.push_back(*d);
+  PLUSS_HIP_CHECK(hipMemcpy(*d, h, n * 8, hipMemcpyHostToDevice));
+  return PLUSS_OK;
+}
+
+int pluss_gemm_sampled_hist(const pluss_cfg* cfg, const uint64_t* samples, uint64_t n, pluss_hist* out) {
+  if (!out || (n && !samples)) return PLUSS_ERR_CONFIG;
+  Scoped sc;
+  if (int rc = pluss_ctx_create(cfg, &sc.ctx)) return rc;
+  if (cfg->mode == PLUSS_MODE_CLEAN) {
+    uint64_t* d = nullptr;
+    if (int rc = upload(sc, samples, n, &d)) return rc;
+    if (int rc = launch_sampled_hist(sc.ctx, d, n, sc.ctx->stream)) return rc;
+  } else {
+    // faithful: one sampler_<REF> per reference present in the list
+    std::vector<uint64_t> per[6];
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint32_t r = (uint32_t)(samples[i] >> 60);
+      if (r > 5) {
+        set_error("malformed sample: ref > 5");
+        return PLUSS_ERR_INPUT;
+      }
+      per[r].push_back(samples[i]);
+    }
+    for (int r = 0; r < 6; ++r) {
+      if (per[r].empty()) continue;
+      uint64_t* d = nullptr;
+      if (int rc = upload(sc, per[r].data(), per[r].size(), &d)) return rc;
+      if (int rc = launch_faithful(sc.ctx, r, d, per[r].size(), sc.ctx->stream)) return rc;
+    }
+  }
+  return pluss_hist_fetch(sc.ctx, out);
+}
+
+int pluss_gemm_fulltrace_hist(const pluss_cfg* cfg, pluss_hist* out) {
+  if (!out) return PLUSS_ERR_CONFIG;
+  Scoped sc;
+  if (int rc = pluss_ctx_create(cfg, &sc.ctx)) return rc;
+  if (int rc = pluss_dev_fulltrace_hist(sc.ctx, nullptr)) return rc;
+  return pluss_hist_fetch(sc.ctx, out);
+}
+
+int pluss_gemm_sampled_ri(const pluss_cfg* cfg, const uint64_t* samples, uint64_t n, int64_t* ri_out,
+                          uint64_t* sink_key_out) {
+  if (n && (!samples || !ri_out)) return PLUSS_ERR_CONFIG;
+  Scoped sc;
+  if (int rc = pluss_ctx_create(cfg, &sc.ctx)) return rc;
+  if (!n) return PLUSS_OK;
+  uint64_t *d = nullptr, *dri = nullptr, *dsk = nullptr;
+  if (int rc = upload(sc, samples, n, &d)) return rc;
+  PLUSS_HIP_CHECK(hipMalloc((void**)&dri, n * 8));
+  sc.bufs.push_back(dri);
+  if (sink_key_out) {
+    PLUSS_HIP_CHECK(hipMalloc((void**)&dsk, n * 8));
+    sc.bufs.push_back(dsk);
+  }
+  if (int rc = launch_ri_dump(sc.ctx, d, n, (int64_t*)dri, dsk, sc.ctx->stream)) return rc;
+  PLUSS_HIP_CHECK(hipStreamSynchronize(sc.ctx->stream));
+  if (int rc = check_flags(sc.ctx)) return rc;
+  PLUSS_HIP_CHECK(hipMemcpy(ri_out, dri, n * 8, hipMemcpyDeviceToHost));
+  if (sink_key_out) PLUSS_HIP_CHECK(hipMemcpy(sink_key_out, dsk, n * 8, hipMemcpyDeviceToHost));
+  return PLUSS_OK;
+}
+
+int pluss_expand_samples(const pluss_cfg* cfg, uint64_t seed, int32_t ref, uint64_t first, uint64_t n,
+                         uint64_t* out) {
+  if ((n && !out) || ref < 0 || ref > 5) return PLUSS_ERR_CONFIG;
+  Scoped sc;
+  if (int rc = pluss_ctx_create(cfg, &sc.ctx)) return rc;
+  if (!n) return PLUSS_OK;
+  uint64_t* d = nullptr;
+  PLUSS_HIP_CHECK(hipMalloc((void**)&d, n * 8));
+  sc.bufs.push_back(d);
+  if (int rc = launch_expand(sc.ctx, seed, ref, first, n, d, sc.ctx->stream)) return rc;
+  PLUSS_HIP_CHECK(hipStreamSynchronize(sc.ctx->stream));
+  PLUSS_HIP_CHECK(hipMemcpy(out, d, n * 8, hipMemcpyDeviceToHost));
+  return PLUSS_OK;
+}
+
+}  // extern "C"

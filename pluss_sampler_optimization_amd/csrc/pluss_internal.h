@@ -1,0 +1,87 @@
+// pluss_internal.h — handle layout and kernel launchers shared by the
+// translation units of libpluss_gpu.so.  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "../../include/pluss_gpu.h"
+#include "pluss_model.h"
+
+namespace pluss {
+
+constexpr int BLOCK = 256;             // 4 waves of 64
+constexpr int TCAP = 256;              // LDS histogram slots per workgroup (power of two)
+constexpr uint32_t GCAP = 4096;        // global histogram slots (power of two)
+constexpr int MAX_BLOCKS = 2048;       // 256 CUs x 8 workgroups
+constexpr int UNROLL = 4;              // 16-byte sample pairs in flight per lane
+
+// Global open-addressing histogram (one per handle).
+struct GTable {
+  unsigned long long* keys;    // GCAP, KEY_EMPTY = free
+  unsigned long long* counts;  // GCAP
+  unsigned int* flags;         // [0] overflow, [1] bad input
+};
+
+// Per-workgroup compacted LDS tables written by the hot kernel.
+struct Slabs {
+  unsigned long long* keys;  // MAX_BLOCKS * TCAP
+  unsigned int* counts;      // MAX_BLOCKS * TCAP
+  unsigned int* n;           // MAX_BLOCKS
+};
+
+struct FaithfulBufs {
+  uint64_t cap = 0;
+  unsigned long long *keys = nullptr, *sinks = nullptr, *keys_s = nullptr, *sinks_s = nullptr, *pmax = nullptr;
+  unsigned int *flags = nullptr, *nstart = nullptr;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  unsigned long long* scal = nullptr;  // [0] cut, [1] cold, [2] traversed
+};
+
+}  // namespace pluss
+
+struct pluss_ctx {
+  pluss_cfg cfg;
+  pluss::Model m;
+  int device;
+  hipStream_t stream;
+  pluss::GTable g;
+  pluss::Slabs slabs;
+  unsigned long long* d_trav;  // [6] per-ref traversed (faithful) / [0] total (full trace)
+  unsigned long long *d_exp_keys, *d_exp_counts;  // GCAP each, canonical export
+  unsigned int* d_exp_n;
+  pluss::FaithfulBufs fb;
+  hipStream_t last;   // stream of the most recent launch (fetch orders after it)
+  int slabs_pending;  // workgroup tables written by the last sampling launch, not yet merged
+};
+
+namespace pluss {
+
+// error plumbing
+void set_error(const std::string& msg);
+#define PLUSS_HIP_CHECK(expr)                                                                            \
+  do {                                                                                                   \
+    hipError_t e_ = (expr);                                                                              \
+    if (e_ != hipSuccess) {                                                                              \
+      ::pluss::set_error(std::string(#expr) + ": " + hipGetErrorString(e_));                             \
+      return PLUSS_ERR_HIP;                                                                              \
+    }                                                                                                    \
+  } while (0)
+
+int validate_cfg(const pluss_cfg* cfg, Model* m);
+
+// launchers (return PLUSS_OK or PLUSS_ERR_*)
+int launch_table_reset(pluss_ctx* ctx, hipStream_t s);
+int flush_slabs(pluss_ctx* ctx, hipStream_t s);
+int launch_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hipStream_t s);
+int launch_fulltrace(pluss_ctx* ctx, hipStream_t s);
+int launch_ri_dump(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, int64_t* d_ri, uint64_t* d_sink,
+                   hipStream_t s);
+int launch_expand(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t first, uint64_t n, uint64_t* d_out,
+                  hipStream_t s);
+int launch_export(pluss_ctx* ctx, unsigned long long* d_keys, unsigned long long* d_counts, uint64_t cap,
+                  hipStream_t s);
+int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s);
+
+}  // namespace pluss

@@ -1,0 +1,241 @@
+// pluss_model.h — integer model of the PLUSS GEMM sampler, evaluated per
+// sampled access on the device (and on the host by the C-ABI for validation).
+//
+// The reference replays the simulated static OpenMP schedule access by access
+// and finds a sample's reuse with a per-thread last-access table
+// (r10 sampler_<REF>, c_lib/test/sampler/gemm-t4-pluss-pro-model-rs-ri-opt-r10.cpp:275-654;
+// full trace seq.cpp:37-333).  Here the same forward search is done by
+// JUMPING: for the sampled cache line we enumerate the <= CLS/DS array
+// elements that map to it and compute, per element, the first touch by the
+// same simulated thread after the sample, from the loop-nest structure.  The
+// minimum over those candidates is the thread-local reuse interval.
+//
+// Loop nest (gemm.ppcg_omp.c:72-98; generated order seq.cpp:102-288):
+//   for c0 in [0,N) (static, chunk CS, T threads):
+//     for c1 in [0,N):  C0 C[c0][c1]; C1 C[c0][c1];
+//       for c2 in [0,N): A0 A[c0][c2]; B0 B[c2][c1]; C2 C[c0][c1]; C3 C[c0][c1]
+// Thread t owns rows c0 with (c0/CS)%T == t; its local row index is
+// q = (c0/(CS*T))*CS + c0%CS (ChunkDispatcher, pluss_utils.h:410-439).
+// Thread-local access position: P = q*R + c1*S + off, S = 4N+2, R = N*S,
+// off(C0)=0, off(C1)=1, off(A0)=2+4c2, off(B0)=3+4c2, off(C2)=4+4c2, off(C3)=5+4c2.
+// Line of element (i,j): (i*N+j)*DS/CLS (GetAddress_*, seq.cpp:12-35).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define PM_HD __host__ __device__ __forceinline__
+#else
+#define PM_HD inline
+#endif
+
+namespace pluss {
+
+enum : uint32_t { C0 = 0, C1 = 1, A0 = 2, B0 = 3, C2 = 4, C3 = 5 };
+enum : uint32_t { ARR_C = 0, ARR_A = 1, ARR_B = 2 };
+PM_HD uint32_t ref_array(uint32_t ref) { return ref == A0 ? ARR_A : (ref == B0 ? ARR_B : ARR_C); }
+
+// Division by a run-time invariant (round-up multiplier).  Valid for n < 2^31.
+struct FastDiv {
+  uint32_t d, m, s;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.s = l;
+  f.m = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+  return f;
+}
+PM_HD uint32_t umulhi32(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umulhi(a, b);
+#else
+  return (uint32_t)(((uint64_t)a * b) >> 32);
+#endif
+}
+PM_HD uint32_t fdiv(uint32_t n, const FastDiv& f) { return (umulhi32(n, f.m) + n) >> f.s; }
+PM_HD uint32_t fmod_(uint32_t n, const FastDiv& f) { return n - fdiv(n, f) * f.d; }
+
+// Everything a kernel needs, precomputed on the host.  Passed by value.
+struct Model {
+  uint32_t N, T, CS, W;  // W = CLS/DS elements per line
+  uint32_t S;            // 4N+2 accesses per c1 iteration
+  uint32_t fast;         // N % W == 0 and R < 2^31: closed 32-bit rules apply
+  uint64_t R;            // N*S accesses per row
+  uint64_t thr;          // share threshold (B0 only)
+  uint64_t A;            // accesses per simulated thread when N % (CS*T) == 0
+  FastDiv dCS, dT, dW, dN;
+};
+
+// Histogram key: ref(4) | kind(4) | (ri + 2)(56).  ri = -1 encodes cold.
+constexpr uint64_t KEY_EMPTY = ~0ull;
+PM_HD uint64_t make_key(uint32_t ref, uint32_t kind, int64_t ri) {
+  return ((uint64_t)ref << 60) | ((uint64_t)kind << 56) | (uint64_t)(ri + 2);
+}
+PM_HD uint32_t key_ref(uint64_t k) { return (uint32_t)(k >> 60); }
+PM_HD uint32_t key_kind(uint64_t k) { return (uint32_t)((k >> 56) & 0xF); }
+PM_HD int64_t key_ri(uint64_t k) { return (int64_t)(k & ((1ull << 56) - 1)) - 2; }
+
+// Packed sample: ref(4) | c0(20) | c1(20) | c2(20)   
+struct Sample {
+  uint32_t ref, c0, c1, c2;
+};
+PM_HD Sample unpack(uint64_t x) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  Sample s;
+  s.c2 = lo & 0xFFFFFu;
+  s.c1 = (lo >> 20) | ((hi & 0xFFu) << 12);
+  s.c0 = (hi >> 8) & 0xFFFFFu;
+  s.ref = hi >> 28;
+  return s;
+}
+PM_HD uint64_t pack(uint32_t ref, uint32_t c0, uint32_t c1, uint32_t c2) {
+  return ((uint64_t)ref << 60) | ((uint64_t)c0 << 40) | ((uint64_t)c1 << 20) | (uint64_t)c2;
+}
+
+PM_HD uint32_t ref_off(uint32_t ref, uint32_t c2) { return ref < 2 ? ref : ref + 4u * c2; }
+
+// Does thread owning row c0 own another row after it?
+PM_HD bool next_row_exists(const Model& m, uint32_t c0, uint32_t p) {
+  uint32_t nxt = (p + 1 != m.CS) ? c0 + 1 : c0 + 1 + (m.T - 1) * m.CS;
+  return nxt < m.N;
+}
+
+constexpr int64_t RI_COLD = -1;
+
+// Closed rules for N % W == 0 (every BASELINE configuration).  32-bit.
+// These are the generic rules below specialised: a line never spans two rows.
+PM_HD int64_t ri_fast(const Model& m, uint32_t ref, uint32_t c0, uint32_t c1, uint32_t c2) {
+  const uint32_t Wm1 = m.W - 1;
+  switch (ref) {
+    case C0: return 1;                                   // -> C1 same element
+    case C1: return 3;                                   // -> C2(c2=0)
+    case C2: return 1;                                   // -> C3 same c2
+    case C3:
+      if (c2 + 1 < m.N) return 3;                        // -> C2(c2+1)
+      return fmod_(c1, m.dW) != Wm1 ? 1 : RI_COLD;       // -> C0(c1+1) same line
+    case A0:
+      if (fmod_(c2, m.dW) != Wm1) return 4;              // -> A0(c2+1) same line
+      return (c1 + 1 < m.N) ? (int64_t)(m.S - 4u * Wm1) : RI_COLD;  // -> first c2 of the line, next c1
+    default: {                                           // B0
+      if (fmod_(c1, m.dW) != Wm1) return m.S;            // -> B0(c1+1) same c2
+      uint32_t p = fmod_(c0, m.dCS);
+      return next_row_exists(m, c0, p) ? (int64_t)(m.R - (uint64_t)Wm1 * m.S) : RI_COLD;  // next owned row
+    }
+  }
+}
+
+// Generic rules (any N, W, T, CS).  64-bit positions.
+PM_HD int64_t ri_generic(const Model& m, uint32_t ref, uint32_t c0, uint32_t c1, uint32_t c2) {
+  const uint64_t INF = ~0ull;
+  const uint32_t k = fdiv(c0, m.dCS), p = c0 - k * m.CS;
+  const uint32_t t = fmod_(k, m.dT), q = fdiv(k, m.dT) * m.CS + p;
+  const uint32_t off = ref_off(ref, c2);
+  const uint64_t rowbase = (uint64_t)q * m.R;
+  const uint64_t P = rowbase + (uint64_t)c1 * m.S + off;
+  const uint32_t arr = ref_array(ref);
+  uint32_t i, j;
+  if (arr == ARR_A) { i = c0; j = c2; } else if (arr == ARR_B) { i = c2; j = c1; } else { i = c0; j = c1; }
+  const uint64_t e = (uint64_t)i * m.N + j;
+  const uint64_t elo = (e / m.W) * m.W;
+  uint64_t ehi = elo + m.W - 1;
+  const uint64_t emax = (uint64_t)m.N * m.N - 1;
+  if (ehi > emax) ehi = emax;
+  const bool more_rows = next_row_exists(m, c0, p);
+  uint64_t best = INF;
+  for (uint64_t e2 = elo; e2 <= ehi; ++e2) {
+    const uint32_t i2 = (uint32_t)(e2 / m.N), j2 = (uint32_t)(e2 - (uint64_t)i2 * m.N);
+    uint64_t cand = INF;
+    if (arr == ARR_B) {                      // B[c2'][c1'] is touched in every owned row
+      const uint64_t o = 3ull + 4ull * i2;
+      const uint64_t same = rowbase + (uint64_t)j2 * m.S + o;
+      if (same > P) cand = same;
+      else if (more_rows) cand = rowbase + m.R + (uint64_t)j2 * m.S + o;
+    } else {
+      const uint32_t k2 = fdiv(i2, m.dCS);
+      if (fmod_(k2, m.dT) != t) continue;    // row i2 belongs to another simulated thread
+      const uint32_t q2 = fdiv(k2, m.dT) * m.CS + (i2 - k2 * m.CS);
+      const uint64_t base2 = (uint64_t)q2 * m.R;
+      if (arr == ARR_A) {                    // A[c0'][c2'] touched once per c1 of row c0'
+        const uint64_t o = 2ull + 4ull * j2;
+        if (q2 > q) cand = base2 + o;
+        else if (q2 == q) {
+          if (o > off) cand = P - off + o;
+          else if (c1 + 1 < m.N) cand = P - off + m.S + o;
+        }
+      } else {                               // C[c0'][c1'] touched in column c1' of row c0'
+        if (q2 > q || (q2 == q && j2 > c1)) cand = base2 + (uint64_t)j2 * m.S;
+        else if (q2 == q && j2 == c1) {      // same element: next C offset in this column
+          uint32_t no = 0xFFFFFFFFu;
+          if (off == 0) no = 1;
+          else if (off < 4) no = 4;
+          else if (((off - 4) & 3) == 0) no = off + 1;       // C2 -> C3
+          else if ((off - 4) / 4 + 1 < m.N) no = off + 3;    // C3 -> C2(c2+1)
+          if (no != 0xFFFFFFFFu) cand = P - off + no;
+        }
+      }
+    }
+    if (cand < best) best = cand;
+  }
+  return best == INF ? RI_COLD : (int64_t)(best - P);
+}
+
+PM_HD uint32_t share_kind(const Model& m, uint32_t ref, int64_t ri) {
+  // distance_to(reuse,0) > distance_to(reuse,THR)  <=>  2*ri > THR  (r10:2482, seq.cpp:203)
+  return (ref == B0 && ri > 0 && 2ull * (uint64_t)ri > m.thr) ? 1u : 0u;
+}
+
+template <bool FAST>
+PM_HD int64_t ri_of(const Model& m, uint32_t ref, uint32_t c0, uint32_t c1, uint32_t c2) {
+  return FAST ? ri_fast(m, ref, c0, c1, c2) : ri_generic(m, ref, c0, c1, c2);
+}
+
+// Thread-local position P and simulated thread id of a sampled access.
+PM_HD void position(const Model& m, uint32_t ref, uint32_t c0, uint32_t c1, uint32_t c2, uint64_t* P,
+                    uint32_t* tid) {
+  const uint32_t k = fdiv(c0, m.dCS), p = c0 - k * m.CS;
+  const uint32_t t = fmod_(k, m.dT), q = fdiv(k, m.dT) * m.CS + p;
+  *P = (uint64_t)q * m.R + (uint64_t)c1 * m.S + ref_off(ref, c2);
+  *tid = t;
+}
+
+// ---- sample-list bijection (cycle-walking 4-round Feistel) ----
+PM_HD uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+struct Perm {
+  uint64_t key[4];
+  uint64_t D, mask, span;  // domain size, half mask, radix
+  uint32_t h, dim3;
+};
+inline Perm make_perm(uint64_t seed, uint32_t ref, uint64_t span, bool dim3) {
+  Perm p;
+  p.dim3 = dim3;
+  p.span = span;
+  p.D = dim3 ? span * span * span : span * span;
+  uint32_t h = 1;
+  while ((1ull << (2 * h)) < p.D) ++h;
+  p.h = h;
+  p.mask = (1ull << h) - 1;
+  for (int r = 0; r < 4; ++r)
+    p.key[r] = mix64(seed ^ ((uint64_t)(ref + 1) * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)(r + 1) * 0xD1B54A32D192ED03ull));
+  return p;
+}
+PM_HD uint64_t perm_apply(const Perm& p, uint64_t y) {
+  do {
+    uint64_t L = y >> p.h, R = y & p.mask;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      uint64_t t = R;
+      R = L ^ (mix64(p.key[r] ^ R) & p.mask);
+      L = t;
+    }
+    y = (L << p.h) | R;
+  } while (y >= p.D);
+  return y;
+}
+
+}  // namespace pluss

@@ -1,0 +1,111 @@
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); runs the product library's kernels")
+    config.addinivalue_line("markers", "slow: longer CPU-side checks")
+
+
+@pytest.fixture(scope="session")
+def orc():
+    import oracle
+    oracle.build()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def model_host():
+    """Host build of the product's integer model (tests/helpers/model_host.cpp)."""
+    src = os.path.join(ROOT, "tests", "helpers", "model_host.cpp")
+    out_dir = os.path.join(ROOT, "tests", "helpers", "_build")
+    os.makedirs(out_dir, exist_ok=True)
+    so = os.path.join(out_dir, "model_host.so")
+    deps = [src, os.path.join(ROOT, "pluss_sampler_optimization_amd", "csrc", "pluss_model.h")]
+    if not os.path.exists(so) or any(os.path.getmtime(d) > os.path.getmtime(so) for d in deps):
+        subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", so, src], check=True)
+    L = ctypes.CDLL(so)
+    P = ctypes.POINTER
+    L.mh_ri.argtypes = [ctypes.c_int64] * 5 + [ctypes.c_int, ctypes.c_int, P(ctypes.c_uint64), ctypes.c_int64,
+                                               P(ctypes.c_int64), P(ctypes.c_int32), P(ctypes.c_uint64)]
+    L.mh_fdiv.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    L.mh_fdiv.restype = ctypes.c_uint32
+    L.mh_expand.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64,
+                            ctypes.c_uint64, P(ctypes.c_uint64)]
+
+    class MH:
+        lib = L
+
+        @staticmethod
+        def ri(N, T, CS, DS, CLS, samples, fast, thr_variant=0):
+            s = np.ascontiguousarray(samples, np.uint64)
+            n = len(s)
+            ri = np.empty(n, np.int64)
+            kind = np.empty(n, np.int32)
+            sink = np.empty(n, np.uint64)
+            rc = L.mh_ri(N, T, CS, DS, CLS, thr_variant, fast, s.ctypes.data_as(P(ctypes.c_uint64)), n,
+                         ri.ctypes.data_as(P(ctypes.c_int64)), kind.ctypes.data_as(P(ctypes.c_int32)),
+                         sink.ctypes.data_as(P(ctypes.c_uint64)))
+            assert rc == 0
+            return ri, kind, sink
+
+        @staticmethod
+        def expand(N, range_full, seed, ref, first, n):
+            out = np.empty(n, np.uint64)
+            assert L.mh_expand(N, range_full, seed, ref, first, n, out.ctypes.data_as(P(ctypes.c_uint64))) == 0
+            return out
+
+    return MH
+
+
+def golden_configs():
+    import json
+    import glob
+    out = []
+    for js in sorted(glob.glob(os.path.join(GOLDEN, "r10_*.json"))):
+        with open(js) as f:
+            d = json.load(f)
+        z = np.load(js[:-5] + ".npz")
+        out.append((os.path.basename(js)[:-5], d, {k: z[k] for k in z.files}))
+    return out
+
+
+def expected_raw(d, ref):
+    exp = d["raw"][ref]
+    e = {(ref, 0, int(k)): v for k, v in exp["noshare"].items()}
+    e.update({(ref, 1, int(k)): v for k, v in exp["share"].items()})
+    return e, exp["traversed"]
+
+
+def closed_form_ri(N, T, CS, W, refs, c0, c1, c2):
+    """SURVEY.md Appendix A.3 closed forms (N % W == 0), vectorised; -1 = cold.
+
+    An independent third statement of the reuse rules (besides the stepping
+    oracle and the product's pluss_model.h)."""
+    refs = np.asarray(refs); c0 = np.asarray(c0, np.int64); c1 = np.asarray(c1, np.int64); c2 = np.asarray(c2, np.int64)
+    S = 4 * N + 2
+    ri = np.full(len(refs), -9, np.int64)
+    p = c0 % CS
+    nxt = np.where(p != CS - 1, c0 + 1, c0 + 1 + (T - 1) * CS)
+    more_rows = nxt < N
+    ri[refs == 0] = 1
+    ri[refs == 1] = 3
+    ri[refs == 4] = 1
+    m = refs == 5
+    ri[m] = np.where(c2[m] < N - 1, 3, np.where(c1[m] % W != W - 1, 1, -1))
+    m = refs == 2
+    ri[m] = np.where(c2[m] % W != W - 1, 4, np.where(c1[m] + 1 < N, S - 4 * (W - 1), -1))
+    m = refs == 3
+    ri[m] = np.where(c1[m] % W != W - 1, S, np.where(more_rows[m], N * S - (W - 1) * S, -1))
+    assert (ri != -9).all()
+    return ri

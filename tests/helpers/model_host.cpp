@@ -1,0 +1,51 @@
+// Host build of the product's integer model (pluss_model.h) for CPU tests:
+// lets the closed/generic reuse rules be checked against the stepping oracle
+// without a GPU.  Test-only; the product library evaluates the model on the
+// device exclusively.
+#include <stdint.h>
+#include "../../pluss_sampler_optimization_amd/csrc/pluss_model.h"
+
+using namespace pluss;
+
+static Model mk(int64_t N, int64_t T, int64_t CS, int64_t DS, int64_t CLS, int thr_variant) {
+  Model m;
+  m.N = (uint32_t)N; m.T = (uint32_t)T; m.CS = (uint32_t)CS; m.W = (uint32_t)(CLS / DS);
+  m.S = (uint32_t)(4 * N + 2); m.R = (uint64_t)N * (4 * N + 2);
+  m.fast = (N % m.W == 0);
+  m.thr = thr_variant ? (uint64_t)((N + 1) * N + 1) : (uint64_t)((4 * N + 2) * N);
+  m.A = (N % (CS * T) == 0) ? (uint64_t)(N / T) * m.R : 0;
+  m.dCS = make_fastdiv(m.CS); m.dT = make_fastdiv(m.T); m.dW = make_fastdiv(m.W); m.dN = make_fastdiv(m.N);
+  return m;
+}
+
+extern "C" int mh_ri(int64_t N, int64_t T, int64_t CS, int64_t DS, int64_t CLS, int thr_variant, int use_fast,
+                     const uint64_t* smp, int64_t n, int64_t* ri, int32_t* kind, uint64_t* sink) {
+  Model m = mk(N, T, CS, DS, CLS, thr_variant);
+  if (use_fast && !m.fast) return -1;
+  for (int64_t i = 0; i < n; i++) {
+    Sample s = unpack(smp[i]);
+    int64_t r = use_fast ? ri_fast(m, s.ref, s.c0, s.c1, s.c2) : ri_generic(m, s.ref, s.c0, s.c1, s.c2);
+    ri[i] = r;
+    kind[i] = (int32_t)share_kind(m, s.ref, r);
+    uint64_t P; uint32_t t;
+    position(m, s.ref, s.c0, s.c1, s.c2, &P, &t);
+    sink[i] = r < 0 ? ~0ull : (P + (uint64_t)r) * m.T + t;
+  }
+  return 0;
+}
+
+extern "C" uint32_t mh_fdiv(uint32_t n, uint32_t d) { FastDiv f = make_fastdiv(d); return fdiv(n, f); }
+
+extern "C" int mh_expand(int64_t N, int range_full, uint64_t seed, int ref, uint64_t first, uint64_t n, uint64_t* out) {
+  bool dim3 = !(ref == 0 || ref == 1);
+  uint64_t span = range_full ? (uint64_t)N : (uint64_t)N - 1;
+  Perm p = make_perm(seed, (uint32_t)ref, span, dim3);
+  if (first + n > p.D) return -2;
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t y = perm_apply(p, first + i), c2 = 0;
+    if (dim3) { c2 = y % span; y /= span; }
+    uint64_t c1 = y % span, c0 = y / span;
+    out[i] = pack((uint32_t)ref, (uint32_t)c0, (uint32_t)c1, (uint32_t)c2);
+  }
+  return 0;
+}

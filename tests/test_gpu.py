@@ -1,0 +1,205 @@
+"""GPU parity tests: the HIP kernels (through the C ABI) against the CPU oracle
+and the reference's own r10 dumps.  Integer results must be bit-exact.
+
+Run on an MI355X:  python -m pytest tests -m gpu -x -q
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import closed_form_ri, expected_raw, golden_configs
+
+pytestmark = pytest.mark.gpu
+
+P = pytest.importorskip("pluss_sampler_optimization_amd")
+GOLD = golden_configs()
+
+IRREGULAR = [(16, 2, 4, 8, 64), (24, 3, 2, 8, 64), (12, 5, 1, 8, 64), (10, 1, 3, 8, 64), (5, 2, 1, 8, 64),
+             (20, 2, 3, 4, 64), (18, 3, 2, 8, 32), (7, 2, 2, 8, 8), (100, 3, 5, 8, 64), (9, 4, 2, 16, 64),
+             (1, 1, 1, 8, 64), (2, 3, 1, 8, 64)]
+
+
+def cfg(N, T, CS=4, DS=8, CLS=64, **kw):
+    return P.SamplerConfig(n=N, threads=T, chunk=CS, ds=DS, cls=CLS, **kw)
+
+
+def oracle_clean_hist(orc, c, samples, thr_variant=0):
+    """Histogram of every sample's stepping-replay RI (clean mode), as {(ref,kind,ri): count}."""
+    ri = orc.clean_ri(c, samples, nthreads=8)
+    refs = (samples >> np.uint64(60)).astype(np.int64)
+    N = c.N
+    thr = (N + 1) * N + 1 if thr_variant else (4 * N + 2) * N
+    kind = ((refs == 3) & (ri > 0) & (2 * ri > thr)).astype(np.int64)
+    out = {}
+    for r, k, x in zip(refs, kind, ri):
+        key = (P.REFS[r], int(k), int(x))
+        out[key] = out.get(key, 0) + 1
+    return out
+
+
+def all_samples(orc, smp):
+    return np.concatenate([orc.pack_array(ref, smp[ref]) for ref in orc.REFS])
+
+
+@pytest.mark.parametrize("name,d,smp", GOLD, ids=[g[0] for g in GOLD])
+def test_faithful_gpu_equals_reference_r10_dumps(orc, name, d, smp):
+    """FAITHFUL mode reproduces r10's raw per-reference histograms and traversed counts."""
+    h = P.sampled_hist(cfg(d["N"], d["T"], mode="faithful"), all_samples(orc, smp))
+    for ref in orc.REFS:
+        exp, etrav = expected_raw(d, ref)
+        got = {k: v for k, v in h.bins.items() if k[0] == ref}
+        assert got == exp, (name, ref)
+        assert h.traversed[P.REF_ID[ref]] == etrav, (name, ref)
+
+
+@pytest.mark.parametrize("name,d,smp", GOLD, ids=[g[0] for g in GOLD])
+def test_clean_gpu_equals_oracle_on_reference_samples(orc, name, d, smp):
+    s = all_samples(orc, smp)
+    h = P.sampled_hist(cfg(d["N"], d["T"]), s)
+    assert h.bins == oracle_clean_hist(orc, orc.cfg(d["N"], d["T"]), s)
+
+
+@pytest.mark.parametrize("shape", IRREGULAR, ids=[str(s) for s in IRREGULAR])
+def test_ri_dump_generic_path_equals_oracle(orc, model_host, shape):
+    N, T, CS, DS, CLS = shape
+    from test_host_model import edge_samples
+    s = edge_samples(orc, N, 256, seed=N + 7 * T)
+    ri, sink = P.sampled_ri(cfg(N, T, CS, DS, CLS), s)
+    np.testing.assert_array_equal(ri, orc.clean_ri(orc.cfg(N, T, CS, DS, CLS), s))
+    _, _, hsink = model_host.ri(N, T, CS, DS, CLS, s, 0)
+    np.testing.assert_array_equal(sink, hsink)
+    h = P.sampled_hist(cfg(N, T, CS, DS, CLS), s)
+    assert h.bins == oracle_clean_hist(orc, orc.cfg(N, T, CS, DS, CLS), s)
+
+
+@pytest.mark.parametrize("N,T,CS,DS,CLS,thr", [(128, 4, 4, 8, 64, 1), (64, 8, 4, 8, 64, 0), (100, 3, 5, 8, 64, 1),
+                                              (20, 2, 3, 4, 64, 1), (33, 4, 2, 8, 64, 0), (256, 4, 4, 8, 64, 1)])
+def test_fulltrace_gpu_equals_oracle(orc, N, T, CS, DS, CLS, thr):
+    """Full trace (sampling rate 1.0) == seq.cpp sampler() restated (per-source-ref raw bins)."""
+    h = P.fulltrace_hist(cfg(N, T, CS, DS, CLS, thr_variant="v1" if thr else "r10"))
+    want, trav = orc.fulltrace(N, T, CS, DS, CLS, thr_variant=thr)
+    assert h.bins == want
+    assert h.traversed[0] == trav
+
+
+def test_fulltrace_kat_n128(orc):
+    """SURVEY.md §4 KAT against the reference seq binary."""
+    h = P.fulltrace_hist(cfg(128, 4, thr_variant="v1"))
+    assert h.noshare() == {-1: 12288, 1: 2127872, 3: 2097152, 4: 1835008, 486: 260096, 514: 1835008}
+    assert h.share() == {62194: 253952}
+    assert h.traversed[0] == 8421376
+
+
+@pytest.mark.parametrize("N,rf", [(20, 0), (128, 0), (1024, 0), (31, 1)])
+def test_expand_gpu_equals_oracle(orc, N, rf):
+    c = cfg(N, 4, range_full=bool(rf))
+    span = N if rf else N - 1
+    for ref in range(6):
+        n = min(20000, span ** (2 if ref < 2 else 3) - 5)
+        a = P.expand_samples(c, 0x5EED0001, ref, 5, n)
+        np.testing.assert_array_equal(a, orc.expand(orc.cfg(N, 4, range_full=rf), 0x5EED0001, ref, 5, n))
+        assert len(np.unique(a)) == n
+
+
+def test_faithful_gpu_equals_oracle_expanded_lists(orc):
+    """Faithful mode on longer bijection lists (more Q1 drops and cold samples)."""
+    for N, T, per in [(64, 4, 6000), (128, 8, 9000), (256, 4, 3000)]:
+        c = cfg(N, T, mode="faithful")
+        s = np.concatenate([P.expand_samples(c, 0x5EED0000 + N, r, 0, per if r >= 2 else min(per, (N - 1) ** 2))
+                            for r in range(6)])
+        h = P.sampled_hist(c, s)
+        oc = orc.cfg(N, T)
+        for ref in orc.REFS:
+            part = s[(s >> np.uint64(60)) == np.uint64(P.REF_ID[ref])]
+            want, trav = orc.faithful(oc, ref, part)
+            got = {k: v for k, v in h.bins.items() if k[0] == ref}
+            assert got == want, (N, T, ref)
+            assert h.traversed[P.REF_ID[ref]] == trav, (N, T, ref)
+
+
+def test_config2_full_size_clean_histogram():
+    """BASELINE config 2 at full size (N=1024, T=8, 2^24 samples): the device
+    histogram equals the closed-form histogram of the same list (an independent
+    restatement) and accounts for every sample."""
+    N, T = 1024, 8
+    c = cfg(N, T)
+    counts = P.default_counts(N, 1 << 24)
+    s = np.concatenate([P.expand_samples(c, 0x5EED0001, r, 0, counts[r]) for r in range(6)])
+    h = P.sampled_hist(c, s)
+    assert h.total() == 1 << 24
+    refs, c0, c1, c2 = P.unpack_array(s)
+    ri = closed_form_ri(N, T, 4, 8, refs, c0, c1, c2)
+    kind = (refs == 3) & (ri > 0) & (2 * ri > (4 * N + 2) * N)
+    keys = (refs * 4 + kind.astype(np.int64)) * (1 << 40) + (ri + 2)
+    u, cnt = np.unique(keys, return_counts=True)
+    want = {(P.REFS[int(k >> 42)], int((k >> 40) & 3), int(k & ((1 << 40) - 1)) - 2): int(n) for k, n in zip(u, cnt)}
+    assert h.bins == want
+
+
+def test_invalid_samples_raise():
+    c = cfg(32, 4)
+    bad = np.array([P.pack("C3", 1, 2, 3), P.pack("A0", 40, 0, 0)], np.uint64)
+    with pytest.raises(P.PlussError):
+        P.sampled_hist(c, bad)
+    with pytest.raises(P.PlussError):
+        P.sampled_hist(c, np.array([7 << 60], np.uint64))
+
+
+def test_empty_and_odd_lengths(orc):
+    c = cfg(32, 4)
+    assert P.sampled_hist(c, np.zeros(0, np.uint64)).bins == {}
+    s = P.expand_samples(c, 1, "B0", 0, 777)
+    for n in (1, 2, 3, 777):
+        assert P.sampled_hist(c, s[:n]).bins == oracle_clean_hist(orc, orc.cfg(32, 4), s[:n])
+
+
+def test_device_handle_path_and_canonical_export(orc):
+    """Handle API with device-resident samples (torch memory), unaligned views,
+    and the canonical table used for the cross-GPU merge."""
+    torch = pytest.importorskip("torch")
+    N, T = 256, 4
+    c = cfg(N, T)
+    counts = P.default_counts(N, 200000)
+    total = sum(counts)
+    buf = torch.empty(total + 1, dtype=torch.int64, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    with P.Context(c) as ctx:
+        off = 1  # 8-byte aligned, not 16-byte aligned
+        for r in range(6):
+            ctx.expand(0x5EED0001, r, 0, counts[r], buf.data_ptr() + 8 * off, stream)
+            off += counts[r]
+        ctx.reset(stream)
+        ctx.sampled_hist(buf.data_ptr() + 8, total, stream)
+        keys = torch.empty(4096, dtype=torch.int64, device="cuda")
+        cnts = torch.empty(4096, dtype=torch.int64, device="cuda")
+        ctx.export(keys.data_ptr(), cnts.data_ptr(), 4096, stream)
+        torch.cuda.synchronize()
+        h = ctx.fetch()
+    host = buf[1:].cpu().numpy().view(np.uint64)
+    assert h == P.sampled_hist(c, host)
+    k = keys.cpu().numpy().view(np.uint64)
+    n = cnts.cpu().numpy().view(np.uint64)
+    used = k[k != np.uint64(2 ** 64 - 1)]
+    assert (used[1:] > used[:-1]).all()
+    assert P.hist_from_tables(k, n) == h
+    assert h.total() == total
+
+
+def test_long_windows_config4_t64(orc):
+    """BASELINE config 4 shape (N=2048, T=64): long B reuse windows, share split and
+    cold B samples in a thread's last row, checked against the closed forms."""
+    N, T = 2048, 64
+    c = cfg(N, T)
+    s = P.expand_samples(c, 0x5EED0001, "B0", 0, 400000)
+    # add cold candidates: c1 % 8 == 7 in each thread's last row
+    last_rows = np.array([N - 1 - k for k in range(0, N, 4)][:32])
+    extra = np.array([P.pack("B0", r, 8 * j + 7, j) for j, r in enumerate(last_rows)], np.uint64)
+    s = np.unique(np.concatenate([s, extra]))
+    h = P.sampled_hist(c, s)
+    refs, c0, c1, c2 = P.unpack_array(s)
+    ri = closed_form_ri(N, T, 4, 8, refs, c0, c1, c2)
+    assert h.cold("B0") == int((ri == -1).sum()) > 0
+    assert set(h.share("B0")) == {(N - 7) * (4 * N + 2)}
+    assert h.share("B0")[(N - 7) * (4 * N + 2)] == int((ri == (N - 7) * (4 * N + 2)).sum())
+    assert h.noshare("B0")[4 * N + 2] == int((ri == 4 * N + 2).sum())

@@ -1,0 +1,170 @@
+"""CPU checks of the product's integer model and host logic (no GPU).
+
+The device kernels evaluate pluss_model.h; here the same header is compiled
+for the host (tests/helpers/model_host.cpp) and compared with the stepping
+oracle, so the reuse rules are exercised on irregular shapes before any GPU
+run.  Also: the faithful-mode sort/scan formulation on the reference dumps,
+the C-ABI exports, and the sample-count rule.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, closed_form_ri, expected_raw, golden_configs
+
+SHAPES = [(16, 2, 4, 8, 64), (24, 3, 2, 8, 64), (12, 5, 1, 8, 64), (10, 1, 3, 8, 64), (5, 2, 1, 8, 64),
+          (3, 1, 1, 8, 64), (32, 4, 4, 8, 64), (20, 2, 3, 4, 64), (18, 3, 2, 8, 32), (7, 2, 2, 8, 8),
+          (64, 4, 4, 8, 64), (100, 3, 5, 8, 64), (9, 4, 2, 16, 64), (1, 1, 1, 8, 64), (2, 3, 1, 8, 64)]
+
+
+def edge_samples(orc, N, cnt, seed=0):
+    rng = np.random.default_rng(seed)
+    out = []
+    for r in range(6):
+        c0 = rng.integers(0, N, cnt); c1 = rng.integers(0, N, cnt)
+        c2 = rng.integers(0, N, cnt) if r >= 2 else np.zeros(cnt, np.int64)
+        c1[: cnt // 8] = N - 1
+        if r >= 2:
+            c2[cnt // 8: cnt // 4] = N - 1
+        c0[cnt // 4: cnt // 3] = N - 1
+        out.append(orc.pack_array(r, np.stack([c0, c1, c2], 1)))
+    return np.concatenate(out)
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+def test_model_rules_match_stepping_oracle(orc, model_host, shape):
+    N, T, CS, DS, CLS = shape
+    s = edge_samples(orc, N, 64, seed=N * 31 + T)
+    want = orc.clean_ri(orc.cfg(N, T, CS, DS, CLS), s)
+    gen, _, _ = model_host.ri(N, T, CS, DS, CLS, s, 0)
+    np.testing.assert_array_equal(gen, want)
+    if N % (CLS // DS) == 0:
+        fast, _, _ = model_host.ri(N, T, CS, DS, CLS, s, 1)
+        np.testing.assert_array_equal(fast, want)
+
+
+def test_fast_rules_equal_closed_forms_large(orc, model_host):
+    N, T, CS = 1024, 8, 4
+    s = edge_samples(orc, N, 5000, seed=7)
+    refs = (s >> np.uint64(60)).astype(np.int64)
+    c0 = ((s >> np.uint64(40)) & np.uint64(0xFFFFF)).astype(np.int64)
+    c1 = ((s >> np.uint64(20)) & np.uint64(0xFFFFF)).astype(np.int64)
+    c2 = (s & np.uint64(0xFFFFF)).astype(np.int64)
+    fast, kind, _ = model_host.ri(N, T, CS, 8, 64, s, 1)
+    np.testing.assert_array_equal(fast, closed_form_ri(N, T, CS, 8, refs, c0, c1, c2))
+    share = (refs == 3) & (fast > 0) & (2 * fast > (4 * N + 2) * N)
+    np.testing.assert_array_equal(kind.astype(bool), share)
+
+
+def test_fastdiv_exact(model_host):
+    rng = np.random.default_rng(3)
+    ds = list(range(1, 70)) + [127, 128, 129, 1000, 4095, 65535, 65536, 1 << 20, (1 << 30) + 7]
+    ns = np.concatenate([np.arange(0, 5000), rng.integers(0, (1 << 31) - 1, 3000), [(1 << 31) - 1]])
+    for d in ds:
+        for n in ns[:: max(1, len(ns) // 800)]:
+            assert model_host.lib.mh_fdiv(int(n), d) == int(n) // d, (n, d)
+
+
+@pytest.mark.parametrize("N,rf", [(20, 0), (21, 1), (128, 0), (1024, 0)])
+def test_product_bijection_equals_oracle_spec(orc, model_host, N, rf):
+    """The device's sample bijection (pluss_model.h, host build) and the oracle's
+    independent implementation produce identical lists."""
+    c = orc.cfg(N, 4, range_full=rf)
+    span = N if rf else N - 1
+    for ref in range(6):
+        n = min(3000, span ** (2 if ref < 2 else 3) - 11)
+        a = model_host.expand(N, rf, 0x5EED0001, ref, 11, n)
+        b = orc.expand(c, 0x5EED0001, ref, 11, n)
+        np.testing.assert_array_equal(a, b)
+        assert len(np.unique(a)) == n
+
+
+def _faithful_scan_model(N, T, CS, ref, s, ri):
+    """The sort/scan form used by pluss_faithful.hip, in numpy."""
+    refi = (s >> np.uint64(60)).astype(np.int64)
+    c0 = ((s >> np.uint64(40)) & np.uint64(0xFFFFF)).astype(np.int64)
+    c1 = ((s >> np.uint64(20)) & np.uint64(0xFFFFF)).astype(np.int64)
+    c2 = (s & np.uint64(0xFFFFF)).astype(np.int64)
+    S_, R = 4 * N + 2, N * (4 * N + 2)
+    k = c0 // CS; t = k % T; q = (k // T) * CS + c0 % CS
+    P = q * R + c1 * S_ + np.where(refi < 2, refi, refi + 4 * c2)
+    INF = np.uint64(2 ** 64 - 1)
+    key = (P * T + t).astype(np.uint64)
+    sink = np.where(ri < 0, INF, ((P + np.maximum(ri, 0)) * T + t).astype(np.uint64))
+    o = np.argsort(key, kind="stable")
+    key, sink, rio, to = key[o], sink[o], ri[o], t[o]
+    n = len(key)
+    pmax = np.maximum.accumulate(sink)
+    start = np.ones(n, bool)
+    start[1:] = key[1:] > pmax[:-1]
+    nst = np.cumsum(start)
+    j = np.arange(n)
+    cand = start & (j > 0) & ((j - (nst - 1)) >= n - j)
+    cut = int(j[cand].min()) if cand.any() else n
+    thr = (4 * N + 2) * N
+    hist = {}
+    for x in range(cut):
+        r = int(rio[x])
+        if r >= 0:
+            kk = 1 if (ref == "B0" and 2 * r > thr) else 0
+            hist[(ref, kk, r)] = hist.get((ref, kk, r), 0) + 1
+    cold = int(((rio[:cut] < 0) & (to[:cut] == 0)).sum())
+    if cut == n and pmax[n - 1] != INF and int(pmax[n - 1]) % T == 0:
+        cold += 1
+    hist[(ref, 0, -1)] = cold
+    A = (N // T) * R
+    trav = 0
+    for x in range(cut):
+        if start[x]:
+            trav -= int(key[x])
+        if x == cut - 1 or start[x + 1]:
+            trav += A * T if pmax[x] == INF else int(pmax[x])
+    return hist, trav
+
+
+GOLD = golden_configs()
+
+
+@pytest.mark.parametrize("name,d,smp", GOLD, ids=[g[0] for g in GOLD])
+def test_faithful_scan_formulation_matches_reference(orc, model_host, name, d, smp):
+    N, T = d["N"], d["T"]
+    for ref in orc.REFS:
+        s = orc.pack_array(ref, smp[ref])
+        ri, _, _ = model_host.ri(N, T, 4, 8, 64, s, 1)
+        h, trav = _faithful_scan_model(N, T, 4, ref, s, ri)
+        exp, etrav = expected_raw(d, ref)
+        assert h == exp, (name, ref)
+        assert trav == etrav, (name, ref)
+
+
+def test_capi_library_exports_every_header_symbol():
+    """libpluss_gpu.so loads without a GPU and exports what include/pluss_gpu.h declares."""
+    from pluss_sampler_optimization_amd import _lib
+    hdr = open(os.path.join(ROOT, "include", "pluss_gpu.h")).read()
+    declared = set(re.findall(r"\b(pluss_[a-z_]+)\s*\(", hdr))
+    assert declared == set(_lib.EXPORTS)
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared:
+        assert hasattr(L, name), name
+    _lib.lib()  # argtypes binding succeeds
+
+
+def test_default_counts_match_survey_configs():
+    """SURVEY.md §8d / BASELINE.md §3 sample budgets (host-only function)."""
+    from pluss_sampler_optimization_amd import default_counts
+    assert default_counts(1024, 1 << 24) == [10466, 10466, 4189071, 4189071, 4189071, 4189071]
+    assert default_counts(4096, 1 << 28) == [167691, 167691, 67025018, 67025020, 67025018, 67025018]
+    assert default_counts(2048, 1 << 24) == [41903, 41903, 4173352, 4173354, 4173352, 4173352]
+    c = default_counts(1024, 1 << 24)
+    assert sum(c) == 1 << 24
+
+
+def test_config_errors_are_reported_without_gpu():
+    from pluss_sampler_optimization_amd import PlussError, SamplerConfig, default_counts
+    with pytest.raises(PlussError):
+        default_counts(1, 100)
+    with pytest.raises(KeyError):
+        SamplerConfig(mode="bogus").to_c()
