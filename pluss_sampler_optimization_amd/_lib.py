@@ -53,6 +53,16 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    # PyTorch-ROCm wheels bundle their own libamdhip64 (same SONAME as ROCm's).
+    # If our library were loaded first, a later `import torch` would map a
+    # second HIP runtime into the process and torch would find no GPU.  Loading
+    # torch first makes both share one runtime (the dynamic linker resolves our
+    # NEEDED libamdhip64.so.7 to the copy torch already mapped).
+    if os.environ.get("PLUSS_NO_TORCH_PRELOAD") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     if not os.path.exists(LIB_PATH):
         raise PlussError(f"{LIB_PATH} is missing: build it with `python -m pluss_sampler_optimization_amd.build` "
                          "(hipcc, gfx950); there is no CPU fallback")

@@ -60,17 +60,53 @@ def convert(dump_dir, N, T, seed):
                 raw[cur][kind][int(k)] = int(round(float(v)))
             else:
                 cur = None
+    printed = parse_printed(os.path.join(dump_dir, f"out_{N}_{T}_{seed}.txt"))
     stem = os.path.join(HERE, f"r10_N{N}_T{T}_s{seed}")
     np.savez_compressed(stem + ".npz", **{r: np.array(samples[r], dtype=np.uint16).reshape(-1, 3) for r in REFS})
     with open(stem + ".json", "w") as f:
         json.dump({"N": N, "T": T, "CS": 4, "DS": 8, "CLS": 64, "seed": seed,
                    "source": "reference r10 sampler dump (see make_r10_fixtures.py)",
-                   "raw": raw}, f, indent=1, sort_keys=True)
+                   "raw": raw, "printed": printed}, f, indent=1, sort_keys=True)
     return stem
+
+
+def parse_printed(path):
+    """The reference's own printout after the raw dump (r10 main, r10:3280-3293):
+    per-reference CRI-distributed histograms (_pluss_histogram_print: "ri,count,fraction",
+    6 significant digits), the merged log2 reuse histogram, the MRC ("c, miss ratio")
+    and "max iteration traversed"."""
+    out = {"per_ref": {}, "reuse": [], "mrc": [], "max_traversed": None}
+    cur = None
+    lines = open(path).read().splitlines()
+    i = 0
+    while i < len(lines):
+        line = lines[i].strip()
+        if line in REFS:
+            cur = out["per_ref"].setdefault(line, [])
+        elif line == "Start to dump reuse time":
+            cur = out["reuse"]
+        elif line == "miss ratio":
+            cur = out["mrc"]
+        elif line == "max iteration traversed":
+            out["max_traversed"] = int(lines[i + 1])
+            cur = None
+            i += 1
+        elif line.startswith("RAW_"):
+            cur = None
+        elif cur is not None and re.match(r"^-?\d+,", line):
+            cur.append([float(x) for x in line.split(",")])
+        i += 1
+    return out
 
 
 def main():
     dump_dir = sys.argv[1] if len(sys.argv) > 1 else "/tmp/oracle"
+    # the unmodified full-trace seq binary's `acc` printout at N=128, T=4
+    # (seq.cpp:336-350): noshare (floor-log2), share, CRI reuse histogram, MRC
+    seq = os.path.join(dump_dir, "seq_acc.txt")
+    if os.path.exists(seq):
+        with open(seq) as f, open(os.path.join(HERE, "seq_N128_T4_acc.txt"), "w") as g:
+            g.write(f.read())
     for path in sorted(glob.glob(os.path.join(dump_dir, "out_*_*_*.txt"))):
         N, T, seed = (int(x) for x in os.path.basename(path)[4:-4].split("_"))
         print(convert(dump_dir, N, T, seed))
