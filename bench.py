@@ -114,7 +114,10 @@ def main():
     n_local = sum(c for _, c in parts)
 
     dev = torch.device("cuda", local)
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated stream: the HIP events below and the library's launches must
+    # share it (the null stream would make the library use its own stream)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
     samples = torch.empty(n_local, dtype=torch.int64, device=dev)
     keys = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
@@ -189,7 +192,7 @@ def main():
                                                              else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic()},
-        "kernel": {"name": "k_sampled_hist<true>", "avg_ms": kern_ms, "bytes_per_launch": BYTES_PER_SAMPLE * n_local},
+        "kernel": {"name": "pluss::k_sampled_hist<2> (FAST_P2)", "avg_ms": kern_ms, "bytes_per_launch": BYTES_PER_SAMPLE * n_local},
         "histogram_bins": len(h.bins),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -43,22 +43,8 @@ int validate_cfg(const pluss_cfg* c, Model* m) {
     set_error("cfg.mode / cfg.thr_variant / cfg.range_full out of range");
     return PLUSS_ERR_CONFIG;
   }
-  if (m) {
-    const uint64_t N = (uint64_t)c->n;
-    m->N = (uint32_t)N;
-    m->T = (uint32_t)c->threads;
-    m->CS = (uint32_t)c->chunk;
-    m->W = (uint32_t)(c->cls / c->ds);
-    m->S = (uint32_t)(4 * N + 2);
-    m->R = N * (4 * N + 2);
-    m->fast = (N % m->W == 0) ? 1u : 0u;
-    m->thr = c->thr_variant == PLUSS_THR_V1 ? (N + 1) * N + 1 : (4 * N + 2) * N;
-    m->A = (N % ((uint64_t)c->chunk * c->threads) == 0) ? (N / c->threads) * m->R : 0;
-    m->dCS = make_fastdiv(m->CS);
-    m->dT = make_fastdiv(m->T);
-    m->dW = make_fastdiv(m->W);
-    m->dN = make_fastdiv(m->N);
-  }
+  if (m) *m = make_model((uint64_t)c->n, (uint64_t)c->threads, (uint64_t)c->chunk, (uint64_t)c->ds,
+                         (uint64_t)c->cls, c->thr_variant == PLUSS_THR_V1);
   return PLUSS_OK;
 }
 
@@ -154,13 +140,16 @@ int pluss_ctx_create(const pluss_cfg* cfg, pluss_ctx** out) {
     return PLUSS_ERR_ALLOC;
   };
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
-  if (hipMalloc((void**)&c->g.keys, GCAP * 8) != hipSuccess) return fail("table");
-  if (hipMalloc((void**)&c->g.counts, GCAP * 8) != hipSuccess) return fail("table");
-  if (hipMalloc((void**)&c->g.flags, 16) != hipSuccess) return fail("flags");
-  if (hipMalloc((void**)&c->slabs.keys, (size_t)MAX_BLOCKS * TCAP * 8) != hipSuccess) return fail("slabs");
-  if (hipMalloc((void**)&c->slabs.counts, (size_t)MAX_BLOCKS * TCAP * 4) != hipSuccess) return fail("slabs");
-  if (hipMalloc((void**)&c->slabs.n, (size_t)MAX_BLOCKS * 4) != hipSuccess) return fail("slabs");
-  if (hipMalloc((void**)&c->d_trav, 8 * 8) != hipSuccess) return fail("trav");
+  if (hipMalloc(&c->d_table, TABLE_BYTES) != hipSuccess) return fail("table");
+  {
+    unsigned long long* base = (unsigned long long*)c->d_table;
+    c->g.keys = base;
+    c->g.rkeys = base + GCAP;
+    c->g.counts = base + GCAP + NREP * RCAP;
+    c->g.rcounts = base + 2 * GCAP + NREP * RCAP;
+    c->g.flags = (unsigned int*)(base + 2 * (GCAP + NREP * RCAP));
+    c->g.trav = base + 2 * (GCAP + NREP * RCAP) + 2;
+  }
   if (hipMalloc((void**)&c->d_exp_keys, GCAP * 8) != hipSuccess) return fail("export");
   if (hipMalloc((void**)&c->d_exp_counts, GCAP * 8) != hipSuccess) return fail("export");
   if (hipMalloc((void**)&c->d_exp_n, 16) != hipSuccess) return fail("export");
@@ -177,9 +166,8 @@ int pluss_ctx_destroy(pluss_ctx* c) {
   if (!c) return PLUSS_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->g.keys,   c->g.counts,   c->g.flags,       c->slabs.keys,  c->slabs.counts, c->slabs.n,
-                  c->d_trav,   c->d_exp_keys, c->d_exp_counts,  c->d_exp_n,     c->fb.keys,      c->fb.sinks,
-                  c->fb.keys_s, c->fb.sinks_s, c->fb.pmax,       c->fb.flags,    c->fb.nstart,    c->fb.tmp,
+  void* bufs[] = {c->d_table,  c->d_exp_keys, c->d_exp_counts, c->d_exp_n, c->fb.keys,  c->fb.sinks,
+                  c->fb.keys_s, c->fb.sinks_s, c->fb.pmax,      c->fb.flags, c->fb.nstart, c->fb.tmp,
                   c->fb.scal};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -209,7 +197,7 @@ int pluss_dev_fulltrace_hist(pluss_ctx* ctx, void* stream) {
   if (!ctx) return PLUSS_ERR_CONFIG;
   if (int rc = launch_fulltrace(ctx, pick(ctx, stream))) return rc;
   const unsigned long long total = (unsigned long long)ctx->m.N * ctx->m.N * ctx->m.S;
-  PLUSS_HIP_CHECK(hipMemcpyAsync(ctx->d_trav, &total, 8, hipMemcpyHostToDevice, pick(ctx, stream)));
+  PLUSS_HIP_CHECK(hipMemcpyAsync(ctx->g.trav, &total, 8, hipMemcpyHostToDevice, pick(ctx, stream)));
   PLUSS_HIP_CHECK(hipStreamSynchronize(pick(ctx, stream)));  // `total` is a stack value
   return PLUSS_OK;
 }
@@ -244,7 +232,7 @@ int pluss_hist_fetch(pluss_ctx* ctx, pluss_hist* out) {
     PLUSS_HIP_CHECK(hipMemcpy(k.data(), ctx->d_exp_keys, n * 8ull, hipMemcpyDeviceToHost));
     PLUSS_HIP_CHECK(hipMemcpy(c.data(), ctx->d_exp_counts, n * 8ull, hipMemcpyDeviceToHost));
   }
-  PLUSS_HIP_CHECK(hipMemcpy(tr.data(), ctx->d_trav, 64, hipMemcpyDeviceToHost));
+  PLUSS_HIP_CHECK(hipMemcpy(tr.data(), ctx->g.trav, 64, hipMemcpyDeviceToHost));
   for (int r = 0; r < 6; ++r) out->traversed[r] = tr[r];
   out->n_entries = n;
   if (n > out->capacity) {
@@ -260,7 +248,7 @@ int pluss_hist_from_tables(const uint64_t* keys, const uint64_t* counts, uint64_
   if (!out || (n_pairs && (!keys || !counts))) return PLUSS_ERR_CONFIG;
   std::map<uint64_t, uint64_t> acc;
   for (uint64_t i = 0; i < n_pairs; ++i)
-    if (keys[i] != KEY_EMPTY) acc[keys[i]] += counts[i];
+    if (keys[i] != KEY_EMPTY && keys[i] != KEY_NONE) acc[keys[i]] += counts[i];
   out->n_entries = acc.size();
   if (acc.size() > out->capacity) {
     set_error("pluss_hist_from_tables: output capacity too small");

@@ -1,6 +1,17 @@
 // pluss_device.h — device helpers shared by the kernel translation units:
-// the LDS-privatised exact-key histogram table, the wave-aggregated insert and
-// the handle's global table.
+// the exact-key histogram path (wave ballot -> per-wave scalar cache -> LDS
+// table -> one of NREP global replica tables) and the handle's global table.
+//
+// Exact keys are required for bit-exact parity (SURVEY.md §7 hard part 2), but
+// a GEMM sampler produces only a handful of distinct (ref, kind, RI) keys, and a
+// wave's 64 samples usually share one or two of them.  So:
+//   1. wave_count(): lanes with equal keys are counted by one ballot+popcount;
+//   2. the (key, count) pair goes to a 4-entry cache held in SGPRs by the wave
+//      (pure scalar compares and adds, no LDS latency on the hot path);
+//   3. cache evictions and the end-of-block flush go to an LDS open-addressing
+//      table, and each workgroup finally adds its few table entries into one of
+//      NREP global replicas (blockIdx % NREP) so the end-of-kernel atomics are
+//      spread over NREP addresses per key.  k_export folds the replicas.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -20,96 +31,146 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// Global table insert (any lane).  Keys never change once published, so a
-// stale read can only show KEY_EMPTY, which the CAS then corrects.
-__device__ inline void g_add(GTable g, uint64_t key, uint64_t cnt) {
-  uint32_t s = slot_hash(key, GCAP);
-  for (uint32_t p = 0; p < GCAP; ++p) {
-    unsigned long long k = __hip_atomic_load(&g.keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (k == key) {
-      atomicAdd(&g.counts[s], (unsigned long long)cnt);
-      return;
-    }
-    if (k == KEY_EMPTY) {
-      unsigned long long prev = atomicCAS(&g.keys[s], KEY_EMPTY, (unsigned long long)key);
-      if (prev == KEY_EMPTY || prev == key) {
-        atomicAdd(&g.counts[s], (unsigned long long)cnt);
-        return;
+// Insert into a global open-addressing table of `cap` slots (any lane).
+// Keys never change once published, so a stale read can only show KEY_NONE,
+// which the CAS then corrects.  Returns false when the table is full.
+__device__ __noinline__ bool g_add_cap(unsigned long long* keys, unsigned long long* counts, uint32_t cap,
+                                       uint64_t key, uint64_t cnt) {
+  uint32_t s = slot_hash(key, cap);
+#pragma unroll 1
+  for (uint32_t p = 0; p < cap; ++p) {
+    unsigned long long k = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k == KEY_NONE) {
+      unsigned long long prev = atomicCAS(&keys[s], KEY_NONE, (unsigned long long)key);
+      if (prev == KEY_NONE || prev == key) {
+        atomicAdd(&counts[s], (unsigned long long)cnt);
+        return true;
       }
+    } else if (k == key) {
+      atomicAdd(&counts[s], (unsigned long long)cnt);
+      return true;
     }
-    s = (s + 1) & (GCAP - 1);
+    s = (s + 1) & (cap - 1);
   }
-  atomicOr(&g.flags[0], 1u);
+  return false;
+}
+
+__device__ __forceinline__ void g_add(GTable g, uint64_t key, uint64_t cnt) {
+  if (!g_add_cap(g.keys, g.counts, GCAP, key, cnt)) atomicOr(&g.flags[0], 1u);
+}
+
+__device__ __forceinline__ void g_add_rep(GTable g, uint32_t rep, uint64_t key, uint64_t cnt) {
+  if (!g_add_cap(g.rkeys + (size_t)rep * RCAP, g.rcounts + (size_t)rep * RCAP, RCAP, key, cnt)) g_add(g, key, cnt);
 }
 
 // LDS table insert (one lane).  Returns false when the table is full.
 template <typename CT, int CAP>
-__device__ __forceinline__ bool lds_add(unsigned long long* tk, CT* tc, uint64_t key, CT cnt) {
+__device__ __noinline__ bool lds_add(unsigned long long* tk, CT* tc, uint64_t key, CT cnt) {
   uint32_t s = slot_hash(key, CAP);
+#pragma unroll 1
   for (int p = 0; p < CAP; ++p) {
     unsigned long long k = __hip_atomic_load(&tk[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (k == key) {
-      atomicAdd(&tc[s], cnt);
-      return true;
-    }
-    if (k == KEY_EMPTY) {
-      unsigned long long prev = atomicCAS(&tk[s], KEY_EMPTY, (unsigned long long)key);
-      if (prev == KEY_EMPTY || prev == key) {
+    if (k == KEY_NONE) {
+      unsigned long long prev = atomicCAS(&tk[s], KEY_NONE, (unsigned long long)key);
+      if (prev == KEY_NONE || prev == key) {
         atomicAdd(&tc[s], cnt);
         return true;
       }
+    } else if (k == key) {
+      atomicAdd(&tc[s], cnt);
+      return true;
     }
     s = (s + 1) & (CAP - 1);
   }
   return false;
 }
 
-// Wave-aggregated insert: the lanes holding the same key are counted with one
-// ballot + popcount and inserted once by a leader lane.  All lanes of the wave
-// must call it (converged); `valid` masks lanes without a sample.
-__device__ __forceinline__ void wave_insert(unsigned long long* tk, unsigned int* tc, GTable g, uint64_t key,
-                                            bool valid) {
-  uint64_t pend = __ballot(valid);
+// Workgroup histogram: LDS table + per-wave scalar cache.
+struct BlockTable {
+  unsigned long long* tk;
+  unsigned int* tc;
+};
+
+struct WaveCache {
+  uint64_t k0, k1, k2, k3;
+  uint32_t c0, c1, c2, c3;
+  uint32_t victim;
+};
+
+__device__ __forceinline__ void wc_init(WaveCache& w) {
+  w.k0 = w.k1 = w.k2 = w.k3 = KEY_NONE;
+  w.c0 = w.c1 = w.c2 = w.c3 = 0;
+  w.victim = 0;
+}
+
+__device__ __forceinline__ void bt_spill(BlockTable bt, GTable g, uint64_t key, uint32_t cnt) {
+  if (key == KEY_NONE || cnt == 0) return;
+  if (__lane_id() == 0) {
+    if (!lds_add<unsigned int, TCAP>(bt.tk, bt.tc, key, cnt)) g_add(g, key, cnt);
+  }
+}
+
+__device__ __forceinline__ uint32_t rfl32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) { return ((uint64_t)rfl32((uint32_t)(v >> 32)) << 32) | rfl32((uint32_t)v); }
+
+// Count one uniform key `lk` `cnt` times in the wave's cache.  Every value is
+// re-asserted wave-uniform (readfirstlane) so the cache lives in SGPRs and the
+// compare chain is scalar.
+__device__ __forceinline__ void wc_add(WaveCache& w, BlockTable bt, GTable g, uint64_t lk, uint32_t cnt) {
+  if (w.k0 == lk) {
+    w.c0 = rfl32(w.c0 + cnt);
+  } else if (w.k1 == lk) {
+    w.c1 = rfl32(w.c1 + cnt);
+  } else if (w.k2 == lk) {
+    w.c2 = rfl32(w.c2 + cnt);
+  } else if (w.k3 == lk) {
+    w.c3 = rfl32(w.c3 + cnt);
+  } else {
+    switch (w.victim) {  // evict round-robin into the LDS table
+      case 0: bt_spill(bt, g, w.k0, w.c0); w.k0 = lk; w.c0 = cnt; break;
+      case 1: bt_spill(bt, g, w.k1, w.c1); w.k1 = lk; w.c1 = cnt; break;
+      case 2: bt_spill(bt, g, w.k2, w.c2); w.k2 = lk; w.c2 = cnt; break;
+      default: bt_spill(bt, g, w.k3, w.c3); w.k3 = lk; w.c3 = cnt; break;
+    }
+    w.victim = rfl32((w.victim + 1) & 3);
+  }
+  w.k0 = rfl64(w.k0); w.k1 = rfl64(w.k1); w.k2 = rfl64(w.k2); w.k3 = rfl64(w.k3);
+  w.c0 = rfl32(w.c0); w.c1 = rfl32(w.c1); w.c2 = rfl32(w.c2); w.c3 = rfl32(w.c3);
+}
+
+// Wave-aggregated count of per-lane keys.  All lanes of the wave must call it
+// (converged); `valid` masks lanes without a sample.
+__device__ __forceinline__ void wave_count(WaveCache& w, BlockTable bt, GTable g, uint64_t key, bool valid) {
+  uint64_t pend = rfl64(__ballot(valid));
   while (pend) {
     const int leader = __builtin_ctzll(pend);
     const uint64_t lk = readlane64(key, leader);
-    const uint64_t hit = __ballot(valid && key == lk) & pend;
-    if ((int)__lane_id() == leader) {
-      const unsigned int c = (unsigned int)__popcll(hit);
-      if (!lds_add<unsigned int, TCAP>(tk, tc, lk, c)) g_add(g, lk, c);
-    }
-    pend &= ~hit;
+    const uint64_t hit = rfl64(__ballot(key == lk) & pend);
+    wc_add(w, bt, g, lk, (uint32_t)__popcll(hit));
+    pend = rfl64(pend & ~hit);
   }
 }
 
-template <bool FAST>
-__device__ __forceinline__ uint64_t sample_key(const Model& m, uint64_t x, bool* bad) {
-  const Sample s = unpack(x);
-  const bool b = s.ref > 5 || s.c0 >= m.N || s.c1 >= m.N || s.c2 >= m.N;
-  *bad = b;
-  if (b) return KEY_EMPTY;
-  const int64_t ri = ri_of<FAST>(m, s.ref, s.c0, s.c1, s.c2);
-  return make_key(s.ref, share_kind(m, s.ref, ri), ri);
-}
-
-__device__ __forceinline__ void table_init(unsigned long long* tk, unsigned int* tc) {
-  for (int i = threadIdx.x; i < TCAP; i += BLOCK) {
-    tk[i] = KEY_EMPTY;
-    tc[i] = 0;
+__device__ __forceinline__ void bt_init(BlockTable bt) {
+  for (int i = threadIdx.x; i < TCAP; i += blockDim.x) {
+    bt.tk[i] = KEY_NONE;
+    bt.tc[i] = 0;
   }
 }
 
-__device__ __forceinline__ void table_flush(unsigned long long* tk, unsigned int* tc, unsigned int* nf, Slabs slabs) {
-  for (int i = threadIdx.x; i < TCAP; i += BLOCK) {
-    const unsigned long long k = tk[i];
-    if (k != KEY_EMPTY) {
-      const unsigned int pos = atomicAdd(nf, 1u);
-      slabs.keys[(size_t)blockIdx.x * TCAP + pos] = k;
-      slabs.counts[(size_t)blockIdx.x * TCAP + pos] = tc[i];
-    }
-  }
+// End of kernel: waves spill their caches, then the workgroup adds its table
+// into replica blockIdx % NREP.
+__device__ __forceinline__ void bt_finish(WaveCache& w, BlockTable bt, GTable g) {
+  bt_spill(bt, g, w.k0, w.c0);
+  bt_spill(bt, g, w.k1, w.c1);
+  bt_spill(bt, g, w.k2, w.c2);
+  bt_spill(bt, g, w.k3, w.c3);
   __syncthreads();
-  if (threadIdx.x == 0) slabs.n[blockIdx.x] = *nf;
+  const uint32_t rep = blockIdx.x & (NREP - 1);
+  for (int i = threadIdx.x; i < TCAP; i += blockDim.x) {
+    const unsigned long long k = bt.tk[i];
+    if (k != KEY_NONE) g_add_rep(g, rep, k, bt.tc[i]);
+  }
 }
 
 }  // namespace pluss

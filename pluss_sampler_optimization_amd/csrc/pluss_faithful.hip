@@ -85,7 +85,10 @@ __global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, con
   __shared__ unsigned long long tk[TCAP];
   __shared__ unsigned int tc[TCAP];
   __shared__ unsigned long long red[2];
-  table_init(tk, tc);
+  const BlockTable bt{tk, tc};
+  bt_init(bt);
+  WaveCache wc;
+  wc_init(wc);
   if (threadIdx.x == 0) red[0] = red[1] = 0;
   __syncthreads();
   const uint64_t cut = scal[0];
@@ -95,7 +98,7 @@ __global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, con
   for (uint64_t base = (uint64_t)blockIdx.x * BLOCK; base < cut; base += step) {
     const uint64_t j = base + threadIdx.x;
     const bool v = j < cut;
-    uint64_t key = KEY_EMPTY;
+    uint64_t key = KEY_NONE;
     bool rec = false;
     if (v) {
       const unsigned long long k = keys[j], s = sinks[j];
@@ -109,13 +112,12 @@ __global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, con
       if (flags[j]) trav -= k;
       if (j + 1 == cut || flags[j + 1]) trav += (pmax[j] == KEY_EMPTY) ? endkey : pmax[j];
     }
-    wave_insert(tk, tc, g, key, rec);
+    wave_count(wc, bt, g, key, rec);
   }
   atomicAdd(&red[0], cold);
   atomicAdd(&red[1], trav);
+  bt_finish(wc, bt, g);
   __syncthreads();
-  for (int i = threadIdx.x; i < TCAP; i += BLOCK)
-    if (tk[i] != KEY_EMPTY) g_add(g, tk[i], tc[i]);
   if (threadIdx.x == 0) {
     atomicAdd(&scal[1], red[0]);
     atomicAdd(&scal[2], red[1]);
@@ -123,12 +125,12 @@ __global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, con
 }
 
 __global__ void k_faith_finish(Model m, uint32_t ref, uint64_t n, const unsigned long long* pmax,
-                               const unsigned long long* scal, GTable g, unsigned long long* trav) {
+                               const unsigned long long* scal, GTable g) {
   unsigned long long cold = scal[1];
   const uint64_t cut = scal[0];
   if (n > 0 && cut == n && pmax[n - 1] != KEY_EMPTY && (pmax[n - 1] % m.T) == 0) cold += 1;  // Q3
   g_add(g, make_key(ref, 0, -1), cold);  // the reference always materialises key -1 (r10:671)
-  trav[ref] += scal[2];
+  g.trav[ref] += scal[2];
 }
 
 template <typename T>
@@ -148,7 +150,6 @@ int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint
     set_error("faithful mode needs N % (chunk*threads) == 0 (lockstep interleaving order)");
     return PLUSS_ERR_CONFIG;
   }
-  if (int rc = flush_slabs(ctx, s)) return rc;
   FaithfulBufs& b = ctx->fb;
   if (!b.scal) {
     if (int rc = grow(&b.scal, 4)) return rc;
@@ -211,7 +212,7 @@ int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint
   else
     hipLaunchKernelGGL(k_faith_hist<false>, dim3(grid), dim3(BLOCK), 0, s, m, (uint32_t)ref, b.keys_s, b.sinks_s,
                        b.pmax, b.flags, n, b.scal, ctx->g);
-  hipLaunchKernelGGL(k_faith_finish, dim3(1), dim3(1), 0, s, m, (uint32_t)ref, n, b.pmax, b.scal, ctx->g, ctx->d_trav);
+  hipLaunchKernelGGL(k_faith_finish, dim3(1), dim3(1), 0, s, m, (uint32_t)ref, n, b.pmax, b.scal, ctx->g);
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }

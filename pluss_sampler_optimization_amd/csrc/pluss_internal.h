@@ -12,23 +12,25 @@ namespace pluss {
 
 constexpr int BLOCK = 256;             // 4 waves of 64
 constexpr int TCAP = 256;              // LDS histogram slots per workgroup (power of two)
-constexpr uint32_t GCAP = 4096;        // global histogram slots (power of two)
-constexpr int MAX_BLOCKS = 2048;       // 256 CUs x 8 workgroups
-constexpr int UNROLL = 4;              // 16-byte sample pairs in flight per lane
+constexpr uint32_t GCAP = 4096;        // main global histogram slots (power of two)
+constexpr uint32_t NREP = 8;           // global replica tables (one per XCD-sized group of workgroups)
+constexpr uint32_t RCAP = 512;         // slots per replica (power of two)
+constexpr int MAX_BLOCKS = 1024;       // 256 CUs x 4 workgroups
+constexpr int UNROLL = 4;              // 16-byte sample pairs per lane per step
+constexpr unsigned long long KEY_NONE = 0;  // free table slot (histogram keys are never 0)
 
-// Global open-addressing histogram (one per handle).
+// Global open-addressing histogram (one per handle), one contiguous
+// allocation so a single memset resets it:
+//   keys[GCAP] rkeys[NREP*RCAP] counts[GCAP] rcounts[NREP*RCAP] flags[4] trav[8]
 struct GTable {
-  unsigned long long* keys;    // GCAP, KEY_EMPTY = free
-  unsigned long long* counts;  // GCAP
-  unsigned int* flags;         // [0] overflow, [1] bad input
+  unsigned long long* keys;     // GCAP
+  unsigned long long* rkeys;    // NREP * RCAP
+  unsigned long long* counts;   // GCAP
+  unsigned long long* rcounts;  // NREP * RCAP
+  unsigned int* flags;          // [0] overflow, [1] bad input
+  unsigned long long* trav;     // [6] per-ref traversed (faithful) / [0] total (full trace)
 };
-
-// Per-workgroup compacted LDS tables written by the hot kernel.
-struct Slabs {
-  unsigned long long* keys;  // MAX_BLOCKS * TCAP
-  unsigned int* counts;      // MAX_BLOCKS * TCAP
-  unsigned int* n;           // MAX_BLOCKS
-};
+constexpr size_t TABLE_BYTES = (size_t)(GCAP + NREP * RCAP) * 16 + 16 + 64;
 
 struct FaithfulBufs {
   uint64_t cap = 0;
@@ -47,13 +49,11 @@ struct pluss_ctx {
   int device;
   hipStream_t stream;
   pluss::GTable g;
-  pluss::Slabs slabs;
-  unsigned long long* d_trav;  // [6] per-ref traversed (faithful) / [0] total (full trace)
+  void* d_table;  // backing store of g (TABLE_BYTES)
   unsigned long long *d_exp_keys, *d_exp_counts;  // GCAP each, canonical export
   unsigned int* d_exp_n;
   pluss::FaithfulBufs fb;
   hipStream_t last;   // stream of the most recent launch (fetch orders after it)
-  int slabs_pending;  // workgroup tables written by the last sampling launch, not yet merged
 };
 
 namespace pluss {
@@ -73,7 +73,6 @@ int validate_cfg(const pluss_cfg* cfg, Model* m);
 
 // launchers (return PLUSS_OK or PLUSS_ERR_*)
 int launch_table_reset(pluss_ctx* ctx, hipStream_t s);
-int flush_slabs(pluss_ctx* ctx, hipStream_t s);
 int launch_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hipStream_t s);
 int launch_fulltrace(pluss_ctx* ctx, hipStream_t s);
 int launch_ri_dump(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, int64_t* d_ri, uint64_t* d_sink,

@@ -3,16 +3,13 @@
 //   k_sampled_hist  (HOT)  one lane per sampled access: decode the packed
 //                   sample, jump to its next same-line touch on the simulated
 //                   static schedule (pluss_model.h), and count the exact
-//                   (ref, noshare/share, RI) key in an LDS-privatised
-//                   open-addressing table.  Lanes with equal keys are merged
-//                   by a wave ballot first, so one LDS atomic is issued per
-//                   distinct key per wave.  Replaces the replay loop of
-//                   r10 sampler_<REF> (r10:275-654) + pluss_parallel_histogram_update
-//                   (pluss_utils.h:726-729).
+//                   (ref, noshare/share, RI) key (pluss_device.h: wave ballot
+//                   -> scalar cache -> LDS table -> replica table).  Replaces
+//                   the replay loop of r10 sampler_<REF> (r10:275-654) and
+//                   pluss_parallel_histogram_update (pluss_utils.h:726-729).
 //   k_fulltrace     every access of the nest, indices generated in-kernel (no
 //                   HBM input); replaces seq.cpp:37-333 / rayon.rs:186-378.
-//   k_slab_reduce   merges the per-workgroup tables into the handle's global table.
-//   k_export        canonical (sorted) table for host fetch / cross-GPU merge.
+//   k_export        folds the replicas into a canonical sorted table.
 //   k_ri_dump       per-sample (RI, sink key) parity dump.
 //   k_expand        the sample-list bijection (pluss_model.h).
 #include <hip/hip_runtime.h>
@@ -21,156 +18,183 @@
 
 namespace pluss {
 
+// Kernel variants: GENERIC (any shape: line-element enumeration), FAST
+// (N % W == 0: case index + key table), FAST_P2 (also W, CS powers of two).
+enum : int { GENERIC = 0, FAST = 1, FAST_P2 = 2 };
+
+template <int MODE>
+__device__ __forceinline__ uint64_t key_of(const Model& m, const unsigned long long* ktab, uint32_t ref, uint32_t c0,
+                                           uint32_t c1, uint32_t c2) {
+  if (MODE == GENERIC) {
+    const int64_t ri = ri_generic(m, ref, c0, c1, c2);
+    return make_key(ref, share_kind(m, ref, ri), ri);
+  }
+  return ktab[ref * 3 + case_fast<MODE == FAST_P2>(m, ref, c0, c1, c2)];
+}
+
+template <int MODE>
+__device__ __forceinline__ uint64_t sample_key(const Model& m, const unsigned long long* ktab, uint64_t x, bool* bad) {
+  const Sample s = unpack(x);
+  const bool b = s.ref > 5 || s.c0 >= m.N || s.c1 >= m.N || s.c2 >= m.N;
+  *bad = b;
+  if (MODE == GENERIC && b) return KEY_NONE;  // the generic rules loop over line elements: skip bad input
+  // fast paths: evaluate branch-free on clamped fields, the caller masks bad lanes
+  return key_of<MODE>(m, ktab, s.ref > 5 ? 5u : s.ref, s.c0, s.c1, s.c2);
+}
+
+__device__ __forceinline__ void ktab_init(const Model& m, unsigned long long* ktab) {
+  if (threadIdx.x < 18) ktab[threadIdx.x] = m.keytab[threadIdx.x];
+}
+
 // ------------------------------------------------------------------ HOT --
-template <bool FAST>
+// Grid-stride over 16-byte sample pairs, UNROLL pairs per lane per step, the
+// next step's loads issued before the current step's keys are counted.
+template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t* __restrict__ smp, uint64_t n,
-                                                        const uint64_t* __restrict__ head, Slabs slabs, GTable g) {
+                                                        const uint64_t* __restrict__ head, GTable g) {
   __shared__ unsigned long long tk[TCAP];
   __shared__ unsigned int tc[TCAP];
-  __shared__ unsigned int nf;
-  table_init(tk, tc);
-  if (threadIdx.x == 0) nf = 0;
+  __shared__ unsigned long long ktab[18];
+  const BlockTable bt{tk, tc};
+  bt_init(bt);
+  ktab_init(m, ktab);
+  WaveCache wc;
+  wc_init(wc);
   __syncthreads();
 
   const uint64_t npairs = n >> 1;
   const ulonglong2* __restrict__ v = reinterpret_cast<const ulonglong2*>(smp);
   const uint64_t step = (uint64_t)gridDim.x * BLOCK * UNROLL;
   bool anybad = false;
-  for (uint64_t base = (uint64_t)blockIdx.x * BLOCK * UNROLL; base < npairs; base += step) {
-    ulonglong2 x[UNROLL];
-    bool ok[UNROLL];
+  uint64_t base = (uint64_t)blockIdx.x * BLOCK * UNROLL;
+  const uint64_t last = npairs ? npairs - 1 : 0;  // loads are clamped, lanes past the end are masked
+  ulonglong2 x[UNROLL];
+  if (npairs) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const uint64_t i = base + (uint64_t)u * BLOCK + threadIdx.x;
-      ok[u] = i < npairs;
-      x[u] = ok[u] ? v[i] : ulonglong2{0, 0};
+      x[u] = v[i < last ? i : last];
+    }
+  }
+  for (; base < npairs; base += step) {
+    ulonglong2 y[UNROLL];
+    const uint64_t nb = base + step;
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {  // prefetch the next step
+      const uint64_t i = nb + (uint64_t)u * BLOCK + threadIdx.x;
+      y[u] = v[i < last ? i : last];
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
+      const bool ok = base + (uint64_t)u * BLOCK + threadIdx.x < npairs;
       bool b0, b1;
-      const uint64_t k0 = sample_key<FAST>(m, x[u].x, &b0);
-      const uint64_t k1 = sample_key<FAST>(m, x[u].y, &b1);
-      anybad |= ok[u] && (b0 || b1);
-      wave_insert(tk, tc, g, k0, ok[u] && !b0);
-      wave_insert(tk, tc, g, k1, ok[u] && !b1);
+      const uint64_t k0 = sample_key<MODE>(m, ktab, x[u].x, &b0);
+      const uint64_t k1 = sample_key<MODE>(m, ktab, x[u].y, &b1);
+      anybad |= ok && (b0 || b1);
+      wave_count(wc, bt, g, k0, ok && !b0);
+      wave_count(wc, bt, g, k1, ok && !b1);
     }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) x[u] = y[u];
   }
   if (((n & 1) || head) && blockIdx.x == 0 && threadIdx.x < 64) {
     // odd tail (lane 0) and, for an 8-byte-aligned list, its first sample (lane 1)
     bool b = false;
     const bool mine = (threadIdx.x == 0 && (n & 1)) || (threadIdx.x == 1 && head);
-    const uint64_t k = mine ? sample_key<FAST>(m, threadIdx.x == 0 ? smp[n - 1] : *head, &b) : KEY_EMPTY;
+    const uint64_t k = mine ? sample_key<MODE>(m, ktab, threadIdx.x == 0 ? smp[n - 1] : *head, &b) : KEY_NONE;
     anybad |= mine && b;
-    wave_insert(tk, tc, g, k, mine && !b);
+    wave_count(wc, bt, g, k, mine && !b);
   }
   if (anybad) atomicOr(&g.flags[1], 1u);
-  __syncthreads();
-  table_flush(tk, tc, &nf, slabs);
+  bt_finish(wc, bt, g);
 }
 
 // ----------------------------------------------------------- full trace --
-template <bool FAST>
-__global__ __launch_bounds__(BLOCK) void k_fulltrace(Model m, Slabs slabs, GTable g) {
+// One wave per (c0, c1) pair: C0, C1, then the c2 loop 64 iterations at a time.
+template <int MODE>
+__global__ __launch_bounds__(BLOCK) void k_fulltrace(Model m, GTable g) {
   __shared__ unsigned long long tk[TCAP];
   __shared__ unsigned int tc[TCAP];
-  __shared__ unsigned int nf;
-  table_init(tk, tc);
-  if (threadIdx.x == 0) nf = 0;
+  __shared__ unsigned long long ktab[18];
+  const BlockTable bt{tk, tc};
+  bt_init(bt);
+  ktab_init(m, ktab);
+  WaveCache wc;
+  wc_init(wc);
   __syncthreads();
   const uint32_t lane = __lane_id();
   const uint64_t nwaves = (uint64_t)gridDim.x * (BLOCK / 64);
   const uint64_t npairs = (uint64_t)m.N * m.N;
   for (uint64_t pr = (uint64_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64; pr < npairs; pr += nwaves) {
     const uint32_t c0 = (uint32_t)(pr / m.N), c1 = (uint32_t)(pr - (uint64_t)c0 * m.N);
-    {  // C0, C1 of this (c0, c1)
+    {
       const bool v = lane < 2;
-      uint64_t key = KEY_EMPTY;
-      if (v) {
-        const int64_t ri = ri_of<FAST>(m, lane, c0, c1, 0);
-        key = make_key(lane, 0, ri);
-      }
-      wave_insert(tk, tc, g, key, v);
+      uint64_t key = KEY_NONE;
+      if (v) key = key_of<MODE>(m, ktab, lane, c0, c1, 0);
+      wave_count(wc, bt, g, key, v);
     }
     for (uint32_t c2b = 0; c2b < m.N; c2b += 64) {
       const uint32_t c2 = c2b + lane;
       const bool v = c2 < m.N;
 #pragma unroll
       for (uint32_t ref = A0; ref <= C3; ++ref) {
-        uint64_t key = KEY_EMPTY;
-        if (v) {
-          const int64_t ri = ri_of<FAST>(m, ref, c0, c1, c2);
-          key = make_key(ref, share_kind(m, ref, ri), ri);
-        }
-        wave_insert(tk, tc, g, key, v);
+        uint64_t key = KEY_NONE;
+        if (v) key = key_of<MODE>(m, ktab, ref, c0, c1, c2);
+        wave_count(wc, bt, g, key, v);
       }
     }
   }
-  __syncthreads();
-  table_flush(tk, tc, &nf, slabs);
-}
-
-// --------------------------------------------------------- slab reduce --
-constexpr int RCAP = 1024;
-__global__ __launch_bounds__(BLOCK) void k_slab_reduce(Slabs slabs, int nslabs, GTable g) {
-  __shared__ unsigned long long tk[RCAP];
-  __shared__ unsigned long long tc[RCAP];
-  for (int i = threadIdx.x; i < RCAP; i += BLOCK) {
-    tk[i] = KEY_EMPTY;
-    tc[i] = 0;
-  }
-  __syncthreads();
-  for (int b = blockIdx.x; b < nslabs; b += gridDim.x) {
-    const unsigned int cnt = slabs.n[b];
-    for (unsigned int i = threadIdx.x; i < cnt; i += BLOCK) {
-      const uint64_t k = slabs.keys[(size_t)b * TCAP + i];
-      const unsigned long long c = slabs.counts[(size_t)b * TCAP + i];
-      if (!lds_add<unsigned long long, RCAP>(tk, tc, k, c)) g_add(g, k, c);
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < RCAP; i += BLOCK)
-    if (tk[i] != KEY_EMPTY) g_add(g, tk[i], tc[i]);
+  bt_finish(wc, bt, g);
 }
 
 // --------------------------------------------------------------- export --
+// Fold main table + replicas, sort by key, write `cap` (key,count) pairs;
+// unused pairs are (~0, 0) so tables compare and merge canonically.
 constexpr int EXP_THREADS = 1024;
 __global__ __launch_bounds__(EXP_THREADS) void k_export(GTable g, unsigned long long* ok, unsigned long long* oc,
                                                        uint64_t cap, unsigned int* nout) {
   __shared__ unsigned long long sk[GCAP];
   __shared__ unsigned long long sc[GCAP];
+  __shared__ unsigned long long ck[GCAP];
   __shared__ unsigned int cnt;
-  if (threadIdx.x == 0) cnt = 0;
+  __shared__ unsigned int full;
+  for (uint32_t i = threadIdx.x; i < GCAP; i += EXP_THREADS) {
+    sk[i] = KEY_NONE;
+    sc[i] = 0;
+  }
+  if (threadIdx.x == 0) cnt = full = 0;
+  __syncthreads();
+  const uint32_t total_slots = GCAP + NREP * RCAP;
+  for (uint32_t i = threadIdx.x; i < total_slots; i += EXP_THREADS) {
+    const unsigned long long k = i < GCAP ? g.keys[i] : g.rkeys[i - GCAP];
+    if (k != KEY_NONE) {
+      const unsigned long long c = i < GCAP ? g.counts[i] : g.rcounts[i - GCAP];
+      if (!lds_add<unsigned long long, GCAP>(sk, sc, k, c)) atomicOr(&full, 1u);
+    }
+  }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < GCAP; i += EXP_THREADS) {
-    const unsigned long long k = g.keys[i];
-    if (k != KEY_EMPTY) {
+    if (sk[i] != KEY_NONE) {
       const unsigned int p = atomicAdd(&cnt, 1u);
-      sk[p] = k;
-      sc[p] = g.counts[i];
+      ck[p] = sk[i];
     }
   }
   __syncthreads();
   const uint32_t n = cnt;
   uint32_t P = 1;
   while (P < n) P <<= 1;
-  for (uint32_t i = n + threadIdx.x; i < P; i += EXP_THREADS) {
-    sk[i] = KEY_EMPTY;
-    sc[i] = 0;
-  }
+  for (uint32_t i = n + threadIdx.x; i < P; i += EXP_THREADS) ck[i] = KEY_EMPTY;
   __syncthreads();
-  for (uint32_t k = 2; k <= P; k <<= 1) {
+  for (uint32_t k = 2; k <= P; k <<= 1) {  // bitonic sort of the distinct keys
     for (uint32_t j = k >> 1; j > 0; j >>= 1) {
       for (uint32_t i = threadIdx.x; i < P; i += EXP_THREADS) {
         const uint32_t ixj = i ^ j;
         if (ixj > i) {
           const bool up = (i & k) == 0;
-          const unsigned long long a = sk[i], b = sk[ixj];
+          const unsigned long long a = ck[i], b = ck[ixj];
           if ((a > b) == up) {
-            sk[i] = b;
-            sk[ixj] = a;
-            const unsigned long long t = sc[i];
-            sc[i] = sc[ixj];
-            sc[ixj] = t;
+            ck[i] = b;
+            ck[ixj] = a;
           }
         }
       }
@@ -178,12 +202,20 @@ __global__ __launch_bounds__(EXP_THREADS) void k_export(GTable g, unsigned long 
     }
   }
   for (uint64_t i = threadIdx.x; i < cap; i += EXP_THREADS) {
-    ok[i] = i < n ? sk[i] : KEY_EMPTY;
-    oc[i] = i < n ? sc[i] : 0ull;
+    if (i < n) {  // counts follow their keys: look each sorted key up in the LDS table
+      const unsigned long long key = ck[i];
+      uint32_t s = slot_hash(key, GCAP);
+      while (sk[s] != key) s = (s + 1) & (GCAP - 1);
+      ok[i] = key;
+      oc[i] = sc[s];
+    } else {
+      ok[i] = KEY_EMPTY;
+      oc[i] = 0ull;
+    }
   }
   if (threadIdx.x == 0) {
     *nout = n;
-    if (n > cap) atomicOr(&g.flags[0], 2u);
+    if (n > cap || full) atomicOr(&g.flags[0], 2u);
   }
 }
 
@@ -227,32 +259,15 @@ __global__ __launch_bounds__(BLOCK) void k_expand(Perm p, uint32_t ref, uint64_t
 }
 
 // ------------------------------------------------------------ launchers --
-static int grid_for(uint64_t work, uint64_t per_block) {
+static int grid_for(uint64_t work, uint64_t per_block, int max_blocks = MAX_BLOCKS) {
   uint64_t b = (work + per_block - 1) / per_block;
   if (b < 1) b = 1;
-  if (b > (uint64_t)MAX_BLOCKS) b = MAX_BLOCKS;
+  if (b > (uint64_t)max_blocks) b = max_blocks;
   return (int)b;
 }
 
 int launch_table_reset(pluss_ctx* ctx, hipStream_t s) {
-  ctx->slabs_pending = 0;  // pending partial tables belong to the histogram being discarded
-  PLUSS_HIP_CHECK(hipMemsetAsync(ctx->g.keys, 0xFF, GCAP * sizeof(unsigned long long), s));
-  PLUSS_HIP_CHECK(hipMemsetAsync(ctx->g.counts, 0, GCAP * sizeof(unsigned long long), s));
-  PLUSS_HIP_CHECK(hipMemsetAsync(ctx->g.flags, 0, 4 * sizeof(unsigned int), s));
-  PLUSS_HIP_CHECK(hipMemsetAsync(ctx->d_trav, 0, 8 * sizeof(unsigned long long), s));
-  return PLUSS_OK;
-}
-
-// The per-workgroup tables of the last sampling launch are merged lazily, just
-// before the slabs are reused or the table is read, so the sampling kernel can
-// be timed on its own.
-int flush_slabs(pluss_ctx* ctx, hipStream_t s) {
-  const int nblocks = ctx->slabs_pending;
-  if (!nblocks) return PLUSS_OK;
-  ctx->slabs_pending = 0;
-  const int rg = nblocks < 64 ? nblocks : 64;
-  hipLaunchKernelGGL(k_slab_reduce, dim3(rg), dim3(BLOCK), 0, s, ctx->slabs, nblocks, ctx->g);
-  PLUSS_HIP_CHECK(hipGetLastError());
+  PLUSS_HIP_CHECK(hipMemsetAsync(ctx->d_table, 0, TABLE_BYTES, s));
   return PLUSS_OK;
 }
 
@@ -262,7 +277,6 @@ int launch_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, h
     set_error("pluss_dev_sampled_hist: sample buffer must be 8-byte aligned");
     return PLUSS_ERR_INPUT;
   }
-  if (int rc = flush_slabs(ctx, s)) return rc;
   const uint64_t* head = nullptr;
   if (((uintptr_t)d_samples & 15u) != 0) {  // peel one sample so the pairs are 16-byte aligned
     head = d_samples;
@@ -270,27 +284,26 @@ int launch_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, h
     --n;
   }
   const int nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL);
-  if (ctx->m.fast)
-    hipLaunchKernelGGL(k_sampled_hist<true>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->slabs,
-                       ctx->g);
+  if (ctx->m.fast && ctx->m.p2)
+    hipLaunchKernelGGL(k_sampled_hist<FAST_P2>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
+  else if (ctx->m.fast)
+    hipLaunchKernelGGL(k_sampled_hist<FAST>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
   else
-    hipLaunchKernelGGL(k_sampled_hist<false>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->slabs,
-                       ctx->g);
+    hipLaunchKernelGGL(k_sampled_hist<GENERIC>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
   PLUSS_HIP_CHECK(hipGetLastError());
-  ctx->slabs_pending = nb;
   return PLUSS_OK;
 }
 
 int launch_fulltrace(pluss_ctx* ctx, hipStream_t s) {
-  if (int rc = flush_slabs(ctx, s)) return rc;
   const uint64_t npairs = (uint64_t)ctx->m.N * ctx->m.N;
   const int nb = grid_for(npairs, BLOCK / 64 * 8);
-  if (ctx->m.fast)
-    hipLaunchKernelGGL(k_fulltrace<true>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ctx->slabs, ctx->g);
+  if (ctx->m.fast && ctx->m.p2)
+    hipLaunchKernelGGL(k_fulltrace<FAST_P2>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ctx->g);
+  else if (ctx->m.fast)
+    hipLaunchKernelGGL(k_fulltrace<FAST>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ctx->g);
   else
-    hipLaunchKernelGGL(k_fulltrace<false>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ctx->slabs, ctx->g);
+    hipLaunchKernelGGL(k_fulltrace<GENERIC>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ctx->g);
   PLUSS_HIP_CHECK(hipGetLastError());
-  ctx->slabs_pending = nb;
   return PLUSS_OK;
 }
 
@@ -320,7 +333,7 @@ int launch_expand(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t first, ui
     set_error("pluss_expand_samples: first+n exceeds the index domain of this reference");
     return PLUSS_ERR_CONFIG;
   }
-  const int nb = grid_for(n, BLOCK * 4);
+  const int nb = grid_for(n, BLOCK * 4, 4096);
   hipLaunchKernelGGL(k_expand, dim3(nb), dim3(BLOCK), 0, s, p, (uint32_t)ref, first, n, d_out);
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
@@ -328,7 +341,6 @@ int launch_expand(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t first, ui
 
 int launch_export(pluss_ctx* ctx, unsigned long long* d_keys, unsigned long long* d_counts, uint64_t cap,
                   hipStream_t s) {
-  if (int rc = flush_slabs(ctx, s)) return rc;
   hipLaunchKernelGGL(k_export, dim3(1), dim3(EXP_THREADS), 0, s, ctx->g, d_keys, d_counts, cap, ctx->d_exp_n);
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;

@@ -61,11 +61,14 @@ PM_HD uint32_t fmod_(uint32_t n, const FastDiv& f) { return n - fdiv(n, f) * f.d
 struct Model {
   uint32_t N, T, CS, W;  // W = CLS/DS elements per line
   uint32_t S;            // 4N+2 accesses per c1 iteration
-  uint32_t fast;         // N % W == 0 and R < 2^31: closed 32-bit rules apply
+  uint32_t fast;         // N % W == 0: the closed rules (ri_fast / case_fast) apply
+  uint32_t p2;           // W and CS are powers of two (mask/shift instead of FastDiv)
+  uint32_t wmask, csmask, csshift;
   uint64_t R;            // N*S accesses per row
   uint64_t thr;          // share threshold (B0 only)
   uint64_t A;            // accesses per simulated thread when N % (CS*T) == 0
   FastDiv dCS, dT, dW, dN;
+  uint64_t keytab[18];   // fast path: histogram key of (ref, case), case 0/1/2 (see case_fast)
 };
 
 // Histogram key: ref(4) | kind(4) | (ri + 2)(56).  ri = -1 encodes cold.
@@ -186,9 +189,65 @@ PM_HD uint32_t share_kind(const Model& m, uint32_t ref, int64_t ri) {
   return (ref == B0 && ri > 0 && 2ull * (uint64_t)ri > m.thr) ? 1u : 0u;
 }
 
+// The fast rules have three outcomes per reference: case 0 (the next touch
+// inside the same c1/c2 sweep), case 1 (the next sweep or row) and case 2
+// (cold).  case_fast() computes only the case; the key of every (ref, case)
+// is precomputed on the host (Model::keytab, from ri_fast) so the hot kernel
+// turns a sample into its histogram key with selects and one table read.
+template <bool P2>
+PM_HD uint32_t case_fast(const Model& m, uint32_t ref, uint32_t c0, uint32_t c1, uint32_t c2) {
+  const uint32_t Wm1 = m.W - 1;
+  const uint32_t r1 = P2 ? (c1 & m.wmask) : fmod_(c1, m.dW);
+  const uint32_t r2 = P2 ? (c2 & m.wmask) : fmod_(c2, m.dW);
+  const uint32_t p = P2 ? (c0 & m.csmask) : fmod_(c0, m.dCS);
+  const bool c1last = r1 == Wm1, c2last = r2 == Wm1;
+  const uint32_t nxt = (p + 1 != m.CS) ? c0 + 1 : c0 + 1 + (m.T - 1) * m.CS;
+  // (first, second) condition per reference: case = first ? 0 : (second ? 1 : 2)
+  bool a = true, b = true;
+  a = (ref == C3) ? (c2 + 1 < m.N) : a;
+  b = (ref == C3) ? !c1last : b;
+  a = (ref == A0) ? !c2last : a;
+  b = (ref == A0) ? (c1 + 1 < m.N) : b;
+  a = (ref == B0) ? !c1last : a;
+  b = (ref == B0) ? (nxt < m.N) : b;
+  return a ? 0u : (b ? 1u : 2u);
+}
+
 template <bool FAST>
 PM_HD int64_t ri_of(const Model& m, uint32_t ref, uint32_t c0, uint32_t c1, uint32_t c2) {
   return FAST ? ri_fast(m, ref, c0, c1, c2) : ri_generic(m, ref, c0, c1, c2);
+}
+
+// Host-side construction of the Model (validated inputs; see validate_cfg).
+inline Model make_model(uint64_t N, uint64_t T, uint64_t CS, uint64_t DS, uint64_t CLS, bool thr_v1) {
+  Model m;
+  m.N = (uint32_t)N;
+  m.T = (uint32_t)T;
+  m.CS = (uint32_t)CS;
+  m.W = (uint32_t)(CLS / DS);
+  m.S = (uint32_t)(4 * N + 2);
+  m.R = N * (4 * N + 2);
+  m.fast = (N % m.W == 0) ? 1u : 0u;
+  const bool wp2 = (m.W & (m.W - 1)) == 0, cp2 = (m.CS & (m.CS - 1)) == 0;
+  m.p2 = (wp2 && cp2) ? 1u : 0u;
+  m.wmask = m.W - 1;
+  m.csmask = m.CS - 1;
+  m.csshift = 0;
+  while ((1u << m.csshift) < m.CS) ++m.csshift;
+  m.thr = thr_v1 ? (N + 1) * N + 1 : (4 * N + 2) * N;
+  m.A = (N % (CS * T) == 0) ? (N / T) * m.R : 0;
+  m.dCS = make_fastdiv(m.CS);
+  m.dT = make_fastdiv(m.T);
+  m.dW = make_fastdiv(m.W);
+  m.dN = make_fastdiv(m.N);
+  // (ref, case) -> key, from the same closed rules as ri_fast
+  const int64_t Wm1 = m.W - 1;
+  const int64_t ri[6][3] = {
+      {1, 1, 1}, {3, 3, 3}, {4, (int64_t)m.S - 4 * Wm1, RI_COLD},
+      {(int64_t)m.S, (int64_t)(m.R - (uint64_t)Wm1 * m.S), RI_COLD}, {1, 1, 1}, {3, 1, RI_COLD}};
+  for (uint32_t r = 0; r < 6; ++r)
+    for (uint32_t c = 0; c < 3; ++c) m.keytab[r * 3 + c] = make_key(r, share_kind(m, r, ri[r][c]), ri[r][c]);
+  return m;
 }
 
 // Thread-local position P and simulated thread id of a sampled access.

@@ -8,14 +8,7 @@
 using namespace pluss;
 
 static Model mk(int64_t N, int64_t T, int64_t CS, int64_t DS, int64_t CLS, int thr_variant) {
-  Model m;
-  m.N = (uint32_t)N; m.T = (uint32_t)T; m.CS = (uint32_t)CS; m.W = (uint32_t)(CLS / DS);
-  m.S = (uint32_t)(4 * N + 2); m.R = (uint64_t)N * (4 * N + 2);
-  m.fast = (N % m.W == 0);
-  m.thr = thr_variant ? (uint64_t)((N + 1) * N + 1) : (uint64_t)((4 * N + 2) * N);
-  m.A = (N % (CS * T) == 0) ? (uint64_t)(N / T) * m.R : 0;
-  m.dCS = make_fastdiv(m.CS); m.dT = make_fastdiv(m.T); m.dW = make_fastdiv(m.W); m.dN = make_fastdiv(m.N);
-  return m;
+  return make_model(N, T, CS, DS, CLS, thr_variant != 0);
 }
 
 extern "C" int mh_ri(int64_t N, int64_t T, int64_t CS, int64_t DS, int64_t CLS, int thr_variant, int use_fast,
@@ -25,6 +18,11 @@ extern "C" int mh_ri(int64_t N, int64_t T, int64_t CS, int64_t DS, int64_t CLS, 
   for (int64_t i = 0; i < n; i++) {
     Sample s = unpack(smp[i]);
     int64_t r = use_fast ? ri_fast(m, s.ref, s.c0, s.c1, s.c2) : ri_generic(m, s.ref, s.c0, s.c1, s.c2);
+    if (use_fast) {  // the hot kernel's (case, key table) path must agree with ri_fast
+      const uint64_t k = m.p2 ? m.keytab[s.ref * 3 + case_fast<true>(m, s.ref, s.c0, s.c1, s.c2)]
+                              : m.keytab[s.ref * 3 + case_fast<false>(m, s.ref, s.c0, s.c1, s.c2)];
+      if (k != make_key(s.ref, share_kind(m, s.ref, r), r)) return -2;
+    }
     ri[i] = r;
     kind[i] = (int32_t)share_kind(m, s.ref, r);
     uint64_t P; uint32_t t;
