@@ -15,6 +15,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 OBJDIR = os.path.join(LIBDIR, "obj")
 LIB = os.path.join(LIBDIR, "libpluss_gpu.so")
+HOST_LIB = os.path.join(LIBDIR, "libpluss_host.so")
+HOST_SOURCES = ["host/pluss_host.cpp"]
 ARCH = os.environ.get("PLUSS_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["pluss_kernels.hip", "pluss_faithful.hip", "pluss_capi.hip"]
 HEADERS = ["pluss_model.h", "pluss_internal.h", "pluss_device.h"]
@@ -62,6 +64,11 @@ def build(verbose=False, force=False):
         list(ex.map(run, jobs))
     if force or jobs or _stale(LIB, objs):
         run([hipcc, "-shared", f"--offload-arch={ARCH}", "-o", LIB, *objs])
+    # host half of the pipeline (CRI / AET / formats): plain C++, no HIP
+    hsrc = [os.path.join(CSRC, h) for h in HOST_SOURCES]
+    if force or _stale(HOST_LIB, hsrc + [os.path.join(inc, "pluss_host.h"), os.path.join(inc, "pluss_gpu.h")]):
+        run([os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-I", inc, "-o",
+             HOST_LIB, *hsrc])
     return LIB
 
 

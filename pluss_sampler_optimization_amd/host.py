@@ -1,9 +1,131 @@
-"""Host-side views of raw reuse-interval histograms.
+"""Host half of the PLUSS pipeline: CRI distribution, AET miss-ratio curve and
+the reference's text formats, over raw reuse-interval histograms.
 
-The device histograms are exact-key (raw RI).  The reference bins some of its
-histograms on the host side of the hot path; these helpers derive those views
-from the exact bins so they can be compared with the reference's printouts.
+Bindings of libpluss_host.so (include/pluss_host.h, C++).  Mirrors the
+reference's host code after the sampler:
+  r10_sampler_output  ~ no_share_distribute + share_distribute (r10:42-131, 690-691)
+  v1_reuse_histogram  ~ pluss_cri_distribute(THREAD_NUM) (pluss_utils.h:987-1208)
+  log2_merge          ~ pluss_histogram_update into _RIHist (pluss_utils.h:722-725)
+  aet                 ~ pluss_AET (pluss_utils.h:758-804)
+  format_hist / format_mrc ~ _pluss_histogram_print / pluss_print_mrc
 """
+import ctypes
+import os
+
+from ._lib import PlussError, PlussHistEntry
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+HOST_LIB_PATH = os.path.join(HERE, "lib", "libpluss_host.so")
+REFS = ["C0", "C1", "A0", "B0", "C2", "C3"]
+
+
+class PlussKV(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_int64), ("value", ctypes.c_double)]
+
+
+_hl = None
+
+
+def host_lib():
+    global _hl
+    if _hl is None:
+        if not os.path.exists(HOST_LIB_PATH):
+            raise PlussError(f"{HOST_LIB_PATH} is missing: run `python -m pluss_sampler_optimization_amd.build`")
+        L = ctypes.CDLL(HOST_LIB_PATH)
+        P = ctypes.POINTER
+        u64p = P(ctypes.c_uint64)
+        L.pluss_cri_r10.argtypes = [ctypes.c_int64, P(PlussHistEntry), ctypes.c_uint64, P(PlussKV), ctypes.c_uint64, u64p]
+        L.pluss_cri_v1.argtypes = [ctypes.c_int64, P(PlussHistEntry), ctypes.c_uint64, P(PlussKV), ctypes.c_uint64, u64p]
+        L.pluss_log2_merge.argtypes = [P(PlussKV), ctypes.c_uint64, P(PlussKV), ctypes.c_uint64, u64p]
+        L.pluss_aet.argtypes = [P(PlussKV), ctypes.c_uint64, P(PlussKV), ctypes.c_uint64, u64p]
+        L.pluss_format_hist.argtypes = [ctypes.c_char_p, P(PlussKV), ctypes.c_uint64, ctypes.c_char_p,
+                                        ctypes.c_uint64, u64p]
+        L.pluss_format_mrc.argtypes = [P(PlussKV), ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64, u64p]
+        for f in (L.pluss_cri_r10, L.pluss_cri_v1, L.pluss_log2_merge, L.pluss_aet, L.pluss_format_hist,
+                  L.pluss_format_mrc):
+            f.restype = ctypes.c_int
+        _hl = L
+    return _hl
+
+
+def _entries(bins):
+    """{(ref, kind, ri): count} or {(kind, ri): count} -> PlussHistEntry array."""
+    items = list(bins.items())
+    arr = (PlussHistEntry * max(1, len(items)))()
+    for i, (k, c) in enumerate(items):
+        ref, kind, ri = k if len(k) == 3 else ("C0",) + tuple(k)
+        arr[i].ref = REFS.index(ref) if isinstance(ref, str) else int(ref)
+        arr[i].kind = int(kind)
+        arr[i].ri = int(ri)
+        arr[i].count = int(c)
+    return arr, len(items)
+
+
+def _kv(d):
+    items = sorted(d.items())
+    arr = (PlussKV * max(1, len(items)))()
+    for i, (k, v) in enumerate(items):
+        arr[i].key = int(k)
+        arr[i].value = float(v)
+    return arr, len(items)
+
+
+def _call_kv(fn, *args, cap=1 << 20):
+    out = (PlussKV * cap)()
+    n = ctypes.c_uint64()
+    rc = fn(*args, out, cap, ctypes.byref(n))
+    if rc == -4:
+        return _call_kv(fn, *args, cap=int(n.value) + 1)
+    if rc:
+        raise PlussError(f"{fn.__name__}: rc={rc}")
+    return {out[i].key: out[i].value for i in range(n.value)}
+
+
+def r10_sampler_output(threads, bins):
+    """Raw histogram of ONE reference -> that sampler_<REF>'s output histogram."""
+    arr, n = _entries(bins)
+    return _call_kv(host_lib().pluss_cri_r10, threads, arr, n)
+
+
+def v1_reuse_histogram(threads, bins):
+    """Full-trace raw histogram -> _RIHist after pluss_cri_distribute (floor-log2 keys)."""
+    arr, n = _entries(bins)
+    return _call_kv(host_lib().pluss_cri_v1, threads, arr, n)
+
+
+def log2_merge(*hists):
+    merged = {}
+    for h in hists:
+        for k, v in h.items():
+            merged[k] = merged.get(k, 0.0) + v
+    arr, n = _kv(merged)
+    # merging in key order, then binning, matches pluss_histogram_update's sums up to rounding order
+    return _call_kv(host_lib().pluss_log2_merge, arr, n)
+
+
+def aet(hist):
+    arr, n = _kv(hist)
+    return _call_kv(host_lib().pluss_aet, arr, n)
+
+
+def _text(fn, *args):
+    n = ctypes.c_uint64()
+    fn(*args, None, 0, ctypes.byref(n))
+    buf = ctypes.create_string_buffer(n.value + 1)
+    rc = fn(*args, buf, n.value + 1, ctypes.byref(n))
+    if rc:
+        raise PlussError(f"{fn.__name__}: rc={rc}")
+    return buf.value.decode()
+
+
+def format_hist(title, hist):
+    arr, n = _kv(hist)
+    return _text(host_lib().pluss_format_hist, title.encode(), arr, n)
+
+
+def format_mrc(mrc):
+    arr, n = _kv(mrc)
+    return _text(host_lib().pluss_format_mrc, arr, n)
 
 
 def floor_pow2(x):
@@ -32,3 +154,17 @@ def log2_ceil_bins(hist):
         k = ceil_pow2(ri) if ri > 0 else ri
         out[k] = out.get(k, 0) + c
     return out
+
+
+def mrc_from_r10(threads, hist):
+    """The r10 main() pipeline (r10:3259-3277): per-reference CRI output, merged
+    with floor-log2 binning into _RIHist, then AET.  `hist` is a
+    pluss_sampler_optimization_amd.Histogram (raw bins of all six references).
+    Returns (per_ref_outputs, reuse_histogram, mrc)."""
+    per_ref = {}
+    for ref in REFS:
+        bins = {k: v for k, v in hist.bins.items() if k[0] == ref}
+        if bins:
+            per_ref[ref] = r10_sampler_output(threads, bins)
+    reuse = log2_merge(*per_ref.values())
+    return per_ref, reuse, aet(reuse)

@@ -1,0 +1,85 @@
+"""Host pipeline (CRI distribute -> log2 merge -> AET -> MRC, text formats)
+against the reference's own printouts.  CPU only.
+
+Inputs are the raw histograms the reference itself produced (r10 dumps) or the
+oracle's full-trace histogram (pinned to the seq binary), so these tests pin
+the host half independently of the GPU.  The reference prints 6 significant
+digits; every printed row must match exactly at that precision.
+"""
+import os
+
+import pytest
+
+from conftest import GOLDEN, golden_configs
+
+H = pytest.importorskip("pluss_sampler_optimization_amd.host")
+GOLD = golden_configs()
+ORDER = ["C3", "C2", "A0", "C0", "B0", "C1"]  # r10 main print order (r10:3280-3285)
+
+
+def _rows(text):
+    return [[float(x) for x in line.split(",")] for line in text.splitlines()[1:]]
+
+
+def _raw_bins(d, ref):
+    raw = d["raw"][ref]
+    b = {(ref, 0, int(k)): v for k, v in raw["noshare"].items()}
+    b.update({(ref, 1, int(k)): v for k, v in raw["share"].items()})
+    return b
+
+
+@pytest.mark.parametrize("name,d,smp", GOLD, ids=[g[0] for g in GOLD])
+def test_r10_pipeline_matches_reference_printout(name, d, smp):
+    per = {ref: H.r10_sampler_output(d["T"], _raw_bins(d, ref)) for ref in ORDER}
+    for ref in ORDER:
+        assert _rows(H.format_hist(ref, per[ref])) == d["printed"]["per_ref"][ref], (name, ref)
+    reuse = H.log2_merge(*[per[r] for r in ORDER])
+    assert _rows(H.format_hist("Start to dump reuse time", reuse)) == d["printed"]["reuse"]
+    mrc = H.aet(reuse)
+    assert _rows(H.format_mrc(mrc)) == d["printed"]["mrc"]
+    assert d["printed"]["max_traversed"] == max(d["raw"][r]["traversed"] for r in ORDER)
+
+
+def _section(lines, title, titles):
+    i = lines.index(title)
+    out = []
+    for line in lines[i + 1:]:
+        if line in titles or not line.strip():
+            break
+        out.append(line)
+    return out
+
+
+def test_v1_fulltrace_pipeline_matches_seq_acc_output(orc):
+    """seq.cpp `acc` (N=128, T=4): noshare/share dumps, CRI reuse histogram and MRC, byte for byte."""
+    txt = open(os.path.join(GOLDEN, "seq_N128_T4_acc.txt")).read().split("\n")
+    titles = ["Start to dump noshare private reuse time", "Start to dump share private reuse time",
+              "Start to dump reuse time", "miss ratio", "max iteration traversed"]
+    h, trav = orc.fulltrace(128, 4, thr_variant=1)
+    noshare, share = {}, {}
+    for (r, k, ri), c in h.items():
+        tgt = share if k else noshare
+        tgt[ri] = tgt.get(ri, 0) + c
+    assert H.format_hist(titles[0], H.log2_floor_bins(noshare)).splitlines()[1:] == _section(txt, titles[0], titles)
+    assert H.format_hist(titles[1], share).splitlines()[1:] == _section(txt, titles[1], titles)
+    reuse = H.v1_reuse_histogram(4, h)
+    assert H.format_hist(titles[2], reuse).splitlines()[1:] == _section(txt, titles[2], titles)
+    assert H.format_mrc(H.aet(reuse)).splitlines()[1:] == _section(txt, titles[3], titles)
+    assert str(trav) == _section(txt, titles[4], titles)[0]
+
+
+def test_aet_edge_cases():
+    assert H.aet({}) == {0: 1.0}  # pluss_AET: P[0] = 1 and c = 0 is always emitted
+    m = H.aet({-1: 10.0})
+    assert m == {0: 1.0}
+    m = H.aet({1: 5.0, 2: 5.0})
+    assert m[0] == 1.0 and all(0.0 <= v <= 1.0 for v in m.values())
+
+
+def test_racetrack_and_nbd_quirks():
+    """Q5: r10 share path maps RI r to T*2^floor(log2 r) before the racetrack with exponent T-2."""
+    out = H.r10_sampler_output(4, {("B0", 1, 62194): 1})
+    assert abs(sum(out.values()) - 1.0) < 1e-12
+    assert max(out) <= 4 * 32768
+    # threads == 1: no distribution at all
+    assert H.r10_sampler_output(1, {("C3", 0, 3): 7, ("C3", 0, -1): 2}) == {3: 7.0, -1: 2.0}
