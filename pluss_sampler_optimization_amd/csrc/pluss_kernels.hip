@@ -14,6 +14,8 @@
 //   k_expand        the sample-list bijection (pluss_model.h).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "pluss_device.h"
 
 namespace pluss {
@@ -49,7 +51,10 @@ __device__ __forceinline__ void ktab_init(const Model& m, unsigned long long* kt
 // ------------------------------------------------------------------ HOT --
 // Grid-stride over 16-byte sample pairs, UNROLL pairs per lane per step, the
 // next step's loads issued before the current step's keys are counted.
-template <int MODE>
+// ABL (diagnostics only, PLUSS_ABLATE env var): 0 = the product kernel;
+// 1 = keys computed but not counted; 2 = samples loaded only.  Used to split
+// the kernel's time between HBM streaming, key computation and counting.
+template <int MODE, int ABL = 0>
 __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t* __restrict__ smp, uint64_t n,
                                                         const uint64_t* __restrict__ head, GTable g) {
   __shared__ unsigned long long tk[TCAP];
@@ -66,6 +71,7 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
   const ulonglong2* __restrict__ v = reinterpret_cast<const ulonglong2*>(smp);
   const uint64_t step = (uint64_t)gridDim.x * BLOCK * UNROLL;
   bool anybad = false;
+  uint64_t sink = 0;
   uint64_t base = (uint64_t)blockIdx.x * BLOCK * UNROLL;
   const uint64_t last = npairs ? npairs - 1 : 0;  // loads are clamped, lanes past the end are masked
   ulonglong2 x[UNROLL];
@@ -87,10 +93,18 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const bool ok = base + (uint64_t)u * BLOCK + threadIdx.x < npairs;
+      if (ABL == 2) {
+        sink ^= ok ? (x[u].x ^ x[u].y) : 0;
+        continue;
+      }
       bool b0, b1;
       const uint64_t k0 = sample_key<MODE>(m, ktab, x[u].x, &b0);
       const uint64_t k1 = sample_key<MODE>(m, ktab, x[u].y, &b1);
       anybad |= ok && (b0 || b1);
+      if (ABL == 1) {
+        sink += ok ? (k0 ^ k1) : 0;
+        continue;
+      }
       wave_count(wc, bt, g, k0, ok && !b0);
       wave_count(wc, bt, g, k1, ok && !b1);
     }
@@ -106,6 +120,10 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
     wave_count(wc, bt, g, k, mine && !b);
   }
   if (anybad) atomicOr(&g.flags[1], 1u);
+  if (ABL) {
+    if (sink == 0x5EED5EED5EED5EEDull) atomicOr(&g.flags[2], 1u);  // keeps the ablated work alive
+    return;
+  }
   bt_finish(wc, bt, g);
 }
 
@@ -284,7 +302,13 @@ int launch_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, h
     --n;
   }
   const int nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL);
-  if (ctx->m.fast && ctx->m.p2)
+  const char* abl = getenv("PLUSS_ABLATE");  // diagnostics only (tools/ablate.py)
+  if (abl && ctx->m.fast && ctx->m.p2 && (abl[0] == '1' || abl[0] == '2')) {
+    if (abl[0] == '1')
+      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 1>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
+    else
+      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 2>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
+  } else if (ctx->m.fast && ctx->m.p2)
     hipLaunchKernelGGL(k_sampled_hist<FAST_P2>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
   else if (ctx->m.fast)
     hipLaunchKernelGGL(k_sampled_hist<FAST>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);

@@ -1,0 +1,57 @@
+"""Split the hot kernel's time (diagnostics): PLUSS_ABLATE=2 loads only,
+=1 loads + key computation, 0 = product kernel.  Also a torch copy for a
+bandwidth reference.  Prints one JSON line per variant."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import pluss_sampler_optimization_amd as P  # noqa: E402
+
+
+def timeit(fn, stream, reps=50):
+    for _ in range(5):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    N, T = int(os.environ.get("ABL_N", 1024)), int(os.environ.get("ABL_T", 8))
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(s)
+    cfg = P.SamplerConfig(n=N, threads=T)
+    for total in (1 << 24, 1 << 26):
+        counts = P.default_counts(N, total)
+        buf = torch.empty(total, dtype=torch.int64, device=dev)
+        ctx = P.Context(cfg)
+        off = 0
+        for r, c in enumerate(counts):
+            ctx.expand(0x5EED0001, r, 0, c, buf.data_ptr() + 8 * off, s.cuda_stream)
+            off += c
+        torch.cuda.synchronize()
+        for mode in ("2", "1", "0"):
+            os.environ["PLUSS_ABLATE"] = mode
+            ms = timeit(lambda: ctx.sampled_hist(buf.data_ptr(), total, s.cuda_stream), s)
+            print(json.dumps({"samples": total, "ablate": mode, "ms": ms, "GBps": 8 * total / ms / 1e6}), flush=True)
+        os.environ["PLUSS_ABLATE"] = "0"
+        dst = torch.empty_like(buf)
+        ms = timeit(lambda: dst.copy_(buf), s)
+        print(json.dumps({"samples": total, "torch_copy_ms": ms, "GBps_rd+wr": 16 * total / ms / 1e6}), flush=True)
+        ctx.reset(s.cuda_stream)
+        ctx.sampled_hist(buf.data_ptr(), total, s.cuda_stream)
+        h = ctx.fetch()
+        assert h.total() == total
+        ctx.close()
+
+
+if __name__ == "__main__":
+    main()
