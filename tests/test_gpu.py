@@ -203,3 +203,46 @@ def test_long_windows_config4_t64(orc):
     assert set(h.share("B0")) == {(N - 7) * (4 * N + 2)}
     assert h.share("B0")[(N - 7) * (4 * N + 2)] == int((ri == (N - 7) * (4 * N + 2)).sum())
     assert h.noshare("B0")[4 * N + 2] == int((ri == 4 * N + 2).sum())
+
+
+def _dist_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import torch.distributed as dist
+    import pluss_sampler_optimization_amd as P2
+    from pluss_sampler_optimization_amd import dist as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = P2.SamplerConfig(n=512, threads=4)
+    counts = P2.default_counts(512, 1 << 20)
+    h = D.sharded_clean_hist(cfg, 0x5EED0001, counts)
+    q.put((rank, h.bins))
+    dist.destroy_process_group()
+
+
+def test_sharded_two_ranks_on_one_gpu_equals_single_rank():
+    """The sharded path (2 processes, each expanding and histogramming its slice
+    on cuda:0, tables exchanged over gloo) equals one process over the whole list."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cfg = cfg_ = P.SamplerConfig(n=512, threads=4)
+    counts = P.default_counts(512, 1 << 20)
+    whole = np.concatenate([P.expand_samples(cfg_, 0x5EED0001, r, 0, c) for r, c in enumerate(counts)])
+    want = P.sampled_hist(cfg, whole).bins
+    for _, bins in res:
+        assert bins == want
