@@ -17,6 +17,7 @@ OBJDIR = os.path.join(LIBDIR, "obj")
 LIB = os.path.join(LIBDIR, "libpluss_gpu.so")
 HOST_LIB = os.path.join(LIBDIR, "libpluss_host.so")
 HOST_SOURCES = ["host/pluss_host.cpp"]
+CLI = os.path.join(LIBDIR, "pluss_cli")
 ARCH = os.environ.get("PLUSS_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["pluss_kernels.hip", "pluss_faithful.hip", "pluss_capi.hip"]
 HEADERS = ["pluss_model.h", "pluss_internal.h", "pluss_device.h"]
@@ -69,6 +70,11 @@ def build(verbose=False, force=False):
     if force or _stale(HOST_LIB, hsrc + [os.path.join(inc, "pluss_host.h"), os.path.join(inc, "pluss_gpu.h")]):
         run([os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-I", inc, "-o",
              HOST_LIB, *hsrc])
+    # the reference's drivers (acc / speed / sample / replay) over both libraries
+    csrc_cli = os.path.join(CSRC, "host", "pluss_cli.cpp")
+    if force or _stale(CLI, [csrc_cli, LIB, HOST_LIB]):
+        run([os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", "-I", inc, "-o", CLI, csrc_cli,
+             "-L", LIBDIR, "-lpluss_gpu", "-lpluss_host", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath,/opt/rocm/lib"])
     return LIB
 
 

@@ -1,0 +1,246 @@
+// pluss_cli — the reference's drivers on top of the two C ABIs.
+//
+//   pluss_cli acc    [opts]   full trace + CRI + AET + prints   (seq main `acc`, …-ri-omp-seq.cpp:336-350)
+//   pluss_cli speed  [opts]   10 timed full-trace runs           (seq main `speed`, :351-360)
+//   pluss_cli sample [opts]   six r10 samplers + merge + AET     (r10 main, r10:3191-3293)
+//   pluss_cli replay FILE     like `sample`, on a given list of "SAMPLE <REF> c0 c1 [c2]" lines
+//
+// opts: --n N --threads T --chunk CS --ds DS --cls CLS --seed S --total K --device D
+// Output formats are the reference's (_pluss_histogram_print, pluss_print_mrc).
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../../include/pluss_gpu.h"
+#include "../../../include/pluss_host.h"
+
+namespace {
+
+const char* REFNAME[6] = {"C0", "C1", "A0", "B0", "C2", "C3"};
+const int PRINT_ORDER[6] = {PLUSS_C3, PLUSS_C2, PLUSS_A0, PLUSS_C0, PLUSS_B0, PLUSS_C1};  // r10:3280-3285
+
+void die(const char* what, int rc) {
+  std::cerr << what << " failed (" << rc << "): " << pluss_last_error() << "\n";
+  std::exit(1);
+}
+
+std::string text_hist(const char* title, const std::vector<pluss_kv>& h) {
+  uint64_t len = 0;
+  pluss_format_hist(title, h.data(), h.size(), nullptr, 0, &len);
+  std::string s(len + 1, '\0');
+  pluss_format_hist(title, h.data(), h.size(), &s[0], len + 1, &len);
+  s.resize(len);
+  return s;
+}
+
+std::string text_mrc(const std::vector<pluss_kv>& m) {
+  uint64_t len = 0;
+  pluss_format_mrc(m.data(), m.size(), nullptr, 0, &len);
+  std::string s(len + 1, '\0');
+  pluss_format_mrc(m.data(), m.size(), &s[0], len + 1, &len);
+  s.resize(len);
+  return s;
+}
+
+template <typename F, typename... A>
+std::vector<pluss_kv> call_kv(F fn, A... args) {
+  std::vector<pluss_kv> out(1 << 16);
+  uint64_t n = 0;
+  int rc = fn(args..., out.data(), out.size(), &n);
+  if (rc == PLUSS_ERR_CAPACITY) {
+    out.resize(n);
+    rc = fn(args..., out.data(), out.size(), &n);
+  }
+  if (rc) die("host pipeline", rc);
+  out.resize(n);
+  return out;
+}
+
+std::vector<pluss_hist_entry> fetch(pluss_hist& h, std::vector<pluss_hist_entry>& buf) {
+  return std::vector<pluss_hist_entry>(buf.begin(), buf.begin() + h.n_entries);
+}
+
+struct Opts {
+  pluss_cfg cfg{128, 4, 4, 8, 64, PLUSS_MODE_CLEAN, PLUSS_THR_R10, 0, 0};
+  uint64_t seed = 0x5EED0001;
+  uint64_t total = 0;  // 0: the reference's counts (164 / 2098 at any N)
+};
+
+Opts parse(int argc, char** argv, int first) {
+  Opts o;
+  for (int i = first; i + 1 < argc; i += 2) {
+    std::string k = argv[i];
+    long long v = std::strtoll(argv[i + 1], nullptr, 0);
+    if (k == "--n") o.cfg.n = v;
+    else if (k == "--threads") o.cfg.threads = v;
+    else if (k == "--chunk") o.cfg.chunk = v;
+    else if (k == "--ds") o.cfg.ds = v;
+    else if (k == "--cls") o.cfg.cls = v;
+    else if (k == "--seed") o.seed = (uint64_t)v;
+    else if (k == "--total") o.total = (uint64_t)v;
+    else if (k == "--device") o.cfg.device = (int32_t)v;
+  }
+  return o;
+}
+
+double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// full trace: seq sampler() + pluss_cri_distribute(THREAD_NUM) [+ AET]
+std::vector<pluss_hist_entry> fulltrace(pluss_cfg cfg, uint64_t* traversed) {
+  cfg.thr_variant = PLUSS_THR_V1;  // seq.cpp:203
+  std::vector<pluss_hist_entry> buf(1 << 14);
+  pluss_hist h{buf.data(), buf.size(), 0, {0}};
+  if (int rc = pluss_gemm_fulltrace_hist(&cfg, &h)) die("pluss_gemm_fulltrace_hist", rc);
+  *traversed = h.traversed[0];
+  return fetch(h, buf);
+}
+
+int run_acc(const Opts& o) {
+  const double t0 = now();
+  uint64_t trav = 0;
+  auto raw = fulltrace(o.cfg, &trav);
+  auto rih = call_kv(pluss_cri_v1, (int64_t)o.cfg.threads, raw.data(), (uint64_t)raw.size());
+  auto mrc = call_kv(pluss_aet, rih.data(), (uint64_t)rih.size());
+  const double t1 = now();
+  std::map<long, double> ns, sh;
+  for (auto& e : raw) {
+    if (e.kind) sh[(long)e.ri] += (double)e.count;
+    else {
+      long k = (long)e.ri;
+      if (k > 0) {  // pluss_cri_noshare_histogram_update bins floor-log2 (pluss_utils.h:924-927)
+        long x = k;
+        x |= x >> 1; x |= x >> 2; x |= x >> 4; x |= x >> 8; x |= x >> 16; x |= x >> 32;
+        k = x ^ (x >> 1);
+      }
+      ns[k] += (double)e.count;
+    }
+  }
+  std::vector<pluss_kv> vns, vsh;
+  for (auto& kv : ns) vns.push_back({kv.first, kv.second});
+  for (auto& kv : sh) vsh.push_back({kv.first, kv.second});
+  std::cout << "MI355X: " << (t1 - t0) << "\n";
+  std::cout << text_hist("Start to dump noshare private reuse time", vns);
+  std::cout << text_hist("Start to dump share private reuse time", vsh);
+  std::cout << text_hist("Start to dump reuse time", rih);
+  std::cout << text_mrc(mrc);
+  std::cout << "max iteration traversed\n" << trav << "\n\n";
+  return 0;
+}
+
+int run_speed(const Opts& o) {
+  std::cout << "MI355X:\n";
+  for (int i = 0; i < 10; ++i) {
+    const double t0 = now();
+    uint64_t trav = 0;
+    auto raw = fulltrace(o.cfg, &trav);
+    auto rih = call_kv(pluss_cri_v1, (int64_t)o.cfg.threads, raw.data(), (uint64_t)raw.size());
+    (void)rih;
+    std::cout << (now() - t0) << "\n";
+  }
+  std::cout << "\n";
+  return 0;
+}
+
+int run_samplers(const Opts& o, const std::vector<uint64_t>* given) {
+  pluss_cfg cfg = o.cfg;
+  cfg.mode = PLUSS_MODE_FAITHFUL;
+  std::vector<uint64_t> samples;
+  if (given) {
+    samples = *given;
+  } else {
+    uint64_t counts[6];
+    if (o.total) {
+      if (int rc = pluss_default_counts(cfg.n, o.total, counts)) die("pluss_default_counts", rc);
+    } else {
+      for (int r = 0; r < 6; ++r) counts[r] = (r == PLUSS_C0 || r == PLUSS_C1) ? 164 : 2098;  // r10:156,1688
+    }
+    for (int r = 0; r < 6; ++r) {
+      std::vector<uint64_t> s(counts[r]);
+      if (int rc = pluss_expand_samples(&cfg, o.seed, r, 0, counts[r], s.data())) die("pluss_expand_samples", rc);
+      samples.insert(samples.end(), s.begin(), s.end());
+    }
+  }
+  const double t0 = now();
+  std::vector<pluss_hist_entry> buf(1 << 16);
+  pluss_hist h{buf.data(), buf.size(), 0, {0}};
+  if (int rc = pluss_gemm_sampled_hist(&cfg, samples.data(), samples.size(), &h)) die("pluss_gemm_sampled_hist", rc);
+  auto raw = fetch(h, buf);
+  std::vector<std::vector<pluss_kv>> per(6);
+  std::vector<pluss_kv> all;
+  for (int r = 0; r < 6; ++r) {
+    std::vector<pluss_hist_entry> mine;
+    for (auto& e : raw)
+      if (e.ref == r) mine.push_back(e);
+    if (mine.empty()) continue;
+    per[r] = call_kv(pluss_cri_r10, (int64_t)cfg.threads, mine.data(), (uint64_t)mine.size());
+    all.insert(all.end(), per[r].begin(), per[r].end());
+  }
+  auto rih = call_kv(pluss_log2_merge, all.data(), (uint64_t)all.size());
+  auto mrc = call_kv(pluss_aet, rih.data(), (uint64_t)rih.size());
+  std::cout << (now() - t0) << "\n";
+  for (int r : PRINT_ORDER) std::cout << text_hist(REFNAME[r], per[r]);
+  std::cout << text_hist("Start to dump reuse time", rih);
+  std::cout << text_mrc(mrc);
+  uint64_t mx = 0;
+  for (int r = 0; r < 6; ++r) mx = h.traversed[r] > mx ? h.traversed[r] : mx;
+  std::cout << "max iteration traversed\n" << mx << "\n";
+  return 0;
+}
+
+std::vector<uint64_t> read_samples(const char* path) {
+  std::ifstream f(path);
+  if (!f) {
+    std::cerr << "cannot open " << path << "\n";
+    std::exit(1);
+  }
+  std::vector<uint64_t> out;
+  std::string tag, ref;
+  while (f >> tag) {
+    if (tag != "SAMPLE") {
+      std::string rest;
+      std::getline(f, rest);
+      continue;
+    }
+    std::string line;
+    std::getline(f, line);
+    std::istringstream is(line);
+    is >> ref;
+    uint64_t c[3] = {0, 0, 0};
+    for (int i = 0; i < 3 && (is >> c[i]); ++i) {
+    }
+    int r = -1;
+    for (int k = 0; k < 6; ++k)
+      if (ref == REFNAME[k]) r = k;
+    if (r < 0) continue;
+    out.push_back(((uint64_t)r << 60) | (c[0] << 40) | (c[1] << 20) | c[2]);
+  }
+  return out;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::cerr << "usage: pluss_cli acc|speed|sample [--n N --threads T ...] | replay FILE [opts]\n";
+    return 2;
+  }
+  const std::string mode = argv[1];
+  if (mode == "acc") return run_acc(parse(argc, argv, 2));
+  if (mode == "speed") return run_speed(parse(argc, argv, 2));
+  if (mode == "sample") return run_samplers(parse(argc, argv, 2), nullptr);
+  if (mode == "replay" && argc >= 3) {
+    auto s = read_samples(argv[2]);
+    return run_samplers(parse(argc, argv, 3), &s);
+  }
+  std::cerr << "unknown mode " << mode << "\n";
+  return 2;
+}

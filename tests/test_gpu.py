@@ -246,3 +246,47 @@ def test_sharded_two_ranks_on_one_gpu_equals_single_rank():
     want = P.sampled_hist(cfg, whole).bins
     for _, bins in res:
         assert bins == want
+
+
+CLI = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "pluss_sampler_optimization_amd",
+                   "lib", "pluss_cli")
+
+
+def test_cli_acc_matches_reference_seq_printout():
+    """`pluss_cli acc` (full trace on the GPU + host CRI/AET) prints what the
+    reference seq binary printed in `acc` mode, line for line after the timer."""
+    import subprocess
+    from conftest import GOLDEN
+    out = subprocess.run([CLI, "acc", "--n", "128", "--threads", "4"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    want = open(os.path.join(GOLDEN, "seq_N128_T4_acc.txt")).read().splitlines()[1:]
+    assert out.stdout.splitlines()[1:] == want
+
+
+@pytest.mark.parametrize("name,d,smp", GOLD[:3], ids=[g[0] for g in GOLD[:3]])
+def test_cli_replay_matches_reference_r10_printout(tmp_path, orc, name, d, smp):
+    """`pluss_cli replay` on the reference's own sample list reproduces its printed
+    per-reference CRI histograms, reuse histogram, MRC and max traversed."""
+    import subprocess
+    f = tmp_path / "samples.txt"
+    with open(f, "w") as fh:
+        for ref in orc.REFS:
+            for row in smp[ref]:
+                fh.write(f"SAMPLE {ref} {row[0]} {row[1]} {row[2]}\n")
+    out = subprocess.run([CLI, "replay", str(f), "--n", str(d["N"]), "--threads", str(d["T"])],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.splitlines()[1:]
+    sections, cur = {}, None
+    for line in lines:
+        if line in ("C3", "C2", "A0", "C0", "B0", "C1", "Start to dump reuse time", "miss ratio",
+                    "max iteration traversed"):
+            cur = sections.setdefault(line, [])
+        elif cur is not None:
+            cur.append(line)
+    rows = lambda ls: [[float(x) for x in l.split(",")] for l in ls]  # noqa: E731
+    for ref in ("C3", "C2", "A0", "C0", "B0", "C1"):
+        assert rows(sections[ref]) == d["printed"]["per_ref"][ref], ref
+    assert rows(sections["Start to dump reuse time"]) == d["printed"]["reuse"]
+    assert rows(sections["miss ratio"]) == d["printed"]["mrc"]
+    assert int(sections["max iteration traversed"][0]) == d["printed"]["max_traversed"]
