@@ -54,7 +54,7 @@ __device__ __forceinline__ void ktab_init(const Model& m, unsigned long long* kt
 // ABL (diagnostics only, PLUSS_ABLATE env var): 0 = the product kernel;
 // 1 = keys computed but not counted; 2 = samples loaded only.  Used to split
 // the kernel's time between HBM streaming, key computation and counting.
-template <int MODE, int ABL = 0>
+template <int MODE, int ABL = 0, int UNR = UNROLL>
 __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t* __restrict__ smp, uint64_t n,
                                                         const uint64_t* __restrict__ head, GTable g) {
   __shared__ unsigned long long tk[TCAP];
@@ -69,29 +69,29 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
 
   const uint64_t npairs = n >> 1;
   const ulonglong2* __restrict__ v = reinterpret_cast<const ulonglong2*>(smp);
-  const uint64_t step = (uint64_t)gridDim.x * BLOCK * UNROLL;
+  const uint64_t step = (uint64_t)gridDim.x * BLOCK * UNR;
   bool anybad = false;
   uint64_t sink = 0;
-  uint64_t base = (uint64_t)blockIdx.x * BLOCK * UNROLL;
+  uint64_t base = (uint64_t)blockIdx.x * BLOCK * UNR;
   const uint64_t last = npairs ? npairs - 1 : 0;  // loads are clamped, lanes past the end are masked
-  ulonglong2 x[UNROLL];
+  ulonglong2 x[UNR];
   if (npairs) {
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
+    for (int u = 0; u < UNR; ++u) {
       const uint64_t i = base + (uint64_t)u * BLOCK + threadIdx.x;
       x[u] = v[i < last ? i : last];
     }
   }
   for (; base < npairs; base += step) {
-    ulonglong2 y[UNROLL];
+    ulonglong2 y[UNR];
     const uint64_t nb = base + step;
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {  // prefetch the next step
+    for (int u = 0; u < UNR; ++u) {  // prefetch the next step
       const uint64_t i = nb + (uint64_t)u * BLOCK + threadIdx.x;
       y[u] = v[i < last ? i : last];
     }
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
+    for (int u = 0; u < UNR; ++u) {
       const bool ok = base + (uint64_t)u * BLOCK + threadIdx.x < npairs;
       if (ABL == 2) {
         sink ^= ok ? (x[u].x ^ x[u].y) : 0;
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
       wave_count(wc, bt, g, k1, ok && !b1);
     }
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) x[u] = y[u];
+    for (int u = 0; u < UNR; ++u) x[u] = y[u];
   }
   if (((n & 1) || head) && blockIdx.x == 0 && threadIdx.x < 64) {
     // odd tail (lane 0) and, for an 8-byte-aligned list, its first sample (lane 1)
@@ -301,13 +301,22 @@ int launch_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, h
     ++d_samples;
     --n;
   }
-  const int nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL);
-  const char* abl = getenv("PLUSS_ABLATE");  // diagnostics only (tools/ablate.py)
+  int nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL);
+  // diagnostics only (tools/ablate.py): PLUSS_ABLATE=1|2, PLUSS_UNROLL=2|8, PLUSS_GRID=<blocks>
+  const char* abl = getenv("PLUSS_ABLATE");
+  const char* unr = getenv("PLUSS_UNROLL");
+  const char* grd = getenv("PLUSS_GRID");
+  if (grd && atoi(grd) > 0) nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL, atoi(grd));
   if (abl && ctx->m.fast && ctx->m.p2 && (abl[0] == '1' || abl[0] == '2')) {
     if (abl[0] == '1')
       hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 1>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
     else
       hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 2>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
+  } else if (unr && ctx->m.fast && ctx->m.p2 && (unr[0] == '2' || unr[0] == '8')) {
+    if (unr[0] == '2')
+      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 0, 2>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
+    else
+      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 0, 8>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
   } else if (ctx->m.fast && ctx->m.p2)
     hipLaunchKernelGGL(k_sampled_hist<FAST_P2>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
   else if (ctx->m.fast)

@@ -38,11 +38,18 @@ def main():
             ctx.expand(0x5EED0001, r, 0, c, buf.data_ptr() + 8 * off, s.cuda_stream)
             off += c
         torch.cuda.synchronize()
-        for mode in ("2", "1", "0"):
-            os.environ["PLUSS_ABLATE"] = mode
+        variants = [dict(PLUSS_ABLATE=m) for m in ("2", "1", "0")]
+        variants += [dict(PLUSS_UNROLL=u) for u in ("2", "8")]
+        variants += [dict(PLUSS_GRID=g) for g in ("512", "1792", "2048", "4096")]
+        variants += [dict(PLUSS_ABLATE="2", PLUSS_GRID=g) for g in ("2048", "4096")]
+        for v in variants:
+            for k in ("PLUSS_ABLATE", "PLUSS_UNROLL", "PLUSS_GRID"):
+                os.environ.pop(k, None)
+            os.environ.update(v)
             ms = timeit(lambda: ctx.sampled_hist(buf.data_ptr(), total, s.cuda_stream), s)
-            print(json.dumps({"samples": total, "ablate": mode, "ms": ms, "GBps": 8 * total / ms / 1e6}), flush=True)
-        os.environ["PLUSS_ABLATE"] = "0"
+            print(json.dumps({"samples": total, **v, "ms": ms, "GBps": 8 * total / ms / 1e6}), flush=True)
+        for k in ("PLUSS_ABLATE", "PLUSS_UNROLL", "PLUSS_GRID"):
+            os.environ.pop(k, None)
         dst = torch.empty_like(buf)
         ms = timeit(lambda: dst.copy_(buf), s)
         print(json.dumps({"samples": total, "torch_copy_ms": ms, "GBps_rd+wr": 16 * total / ms / 1e6}), flush=True)
