@@ -49,22 +49,107 @@ __device__ __forceinline__ void ktab_init(const Model& m, unsigned long long* kt
 }
 
 // ------------------------------------------------------------------ HOT --
-// Grid-stride over 16-byte sample pairs, UNROLL pairs per lane per step, the
-// next step's loads issued before the current step's keys are counted.
-// ABL (diagnostics only, PLUSS_ABLATE env var): 0 = the product kernel;
-// 1 = keys computed but not counted; 2 = samples loaded only.  Used to split
-// the kernel's time between HBM streaming, key computation and counting.
+// Grid-stride over 16-byte sample pairs, UNR pairs per lane per step, the
+// next step's loads issued before the current step's samples are counted.
+//
+// FAST / FAST_P2 (N % W == 0): a sample's key is one of 18 (ref, case) keys
+// (Model::keytab), so counting is one conflict-free `ds_add_u32` into the
+// lane's own LDS counter for that bin (bank = lane); the block reduces its
+// counters once at the end.  GENERIC: arbitrary exact keys, counted through
+// the wave-aggregated cache path (pluss_device.h).
+constexpr int NBINS = 20;  // 18 (ref, case) bins + 1 malformed-sample bin + 1 masked-lane bin
+constexpr int BIN_BAD = 18, BIN_OFF = 19;
+
+// Per-sample bin for any mix of references (selects only).
+template <bool P2>
+__device__ __forceinline__ uint32_t sample_bin_any(const Model& m, uint64_t x, bool ok) {
+  const Sample s = unpack(x);
+  const bool bad = s.ref > 5 || s.c0 >= m.N || s.c1 >= m.N || s.c2 >= m.N;
+  const uint32_t ref = s.ref > 5 ? 5u : s.ref;
+  const uint32_t bin = ref * 3 + case_fast<P2>(m, ref, s.c0, s.c1, s.c2);
+  return ok ? (bad ? (uint32_t)BIN_BAD : bin) : (uint32_t)BIN_OFF;
+}
+
+// Per-sample bin when every active lane holds the same reference `ref`
+// (wave-uniform, so the rule is chosen by a scalar branch and only the
+// compares that reference needs are evaluated).
+template <bool P2>
+__device__ __forceinline__ uint32_t sample_bin_ref(const Model& m, uint32_t ref, uint64_t x, bool ok) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t c2 = lo & 0xFFFFFu;
+  const uint32_t c1 = __builtin_amdgcn_alignbit(hi, lo, 20) & 0xFFFFFu;
+  const uint32_t c0 = (hi >> 8) & 0xFFFFFu;
+  const uint32_t mx = c0 > c1 ? (c0 > c2 ? c0 : c2) : (c1 > c2 ? c1 : c2);
+  const bool bad = mx >= m.N;
+  const uint32_t Wm1 = m.W - 1;
+  uint32_t cs = 0;
+  if (ref == C3) {
+    const bool c1last = (P2 ? (c1 & m.wmask) : fmod_(c1, m.dW)) == Wm1;
+    cs = (c2 + 1 < m.N) ? 0u : (c1last ? 2u : 1u);
+  } else if (ref == A0) {
+    const bool c2last = (P2 ? (c2 & m.wmask) : fmod_(c2, m.dW)) == Wm1;
+    cs = !c2last ? 0u : (c1 + 1 < m.N ? 1u : 2u);
+  } else if (ref == B0) {
+    const bool c1last = (P2 ? (c1 & m.wmask) : fmod_(c1, m.dW)) == Wm1;
+    const uint32_t p = P2 ? (c0 & m.csmask) : fmod_(c0, m.dCS);
+    const uint32_t nxt = c0 + 1 + (p + 1 == m.CS ? (m.T - 1) * m.CS : 0u);
+    cs = !c1last ? 0u : (nxt < m.N ? 1u : 2u);
+  }
+  const uint32_t bin = ref * 3 + cs;
+  return ok ? (bad ? (uint32_t)BIN_BAD : bin) : (uint32_t)BIN_OFF;
+}
+
+template <bool P2>
+__device__ __forceinline__ uint32_t sample_bin(const Model& m, uint64_t x, bool ok) {
+  const uint32_t r = (uint32_t)(x >> 60);
+  const uint32_t r0 = __builtin_amdgcn_readfirstlane(r);
+  if (r0 <= 5 && __ballot(ok && r != r0) == 0) {
+    switch (r0) {  // scalar branch on the wave's reference
+      case C3: return sample_bin_ref<P2>(m, C3, x, ok);
+      case A0: return sample_bin_ref<P2>(m, A0, x, ok);
+      case B0: return sample_bin_ref<P2>(m, B0, x, ok);
+      default: return sample_bin_ref<P2>(m, r0, x, ok);  // C0, C1, C2: case 0
+    }
+  }
+  return sample_bin_any<P2>(m, x, ok);
+}
+
+// Block-wide reduction of the per-lane bin counters; bins with a count go to
+// replica blockIdx % NREP under their precomputed key.
+__device__ __forceinline__ void bins_finish(const Model& m, unsigned int (*pc)[NBINS][64], GTable g) {
+  __shared__ unsigned long long tot[NBINS];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int b = wave; b < NBINS; b += BLOCK / 64) {
+    unsigned long long v = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / 64; ++w) v += pc[w][b][lane];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) tot[b] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 18 && tot[threadIdx.x])
+    g_add_rep(g, blockIdx.x & (NREP - 1), m.keytab[threadIdx.x], tot[threadIdx.x]);
+  if (threadIdx.x == BIN_BAD && tot[BIN_BAD]) atomicOr(&g.flags[1], 1u);
+}
+
 template <int MODE, int ABL = 0, int UNR = UNROLL>
 __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t* __restrict__ smp, uint64_t n,
                                                         const uint64_t* __restrict__ head, GTable g) {
-  __shared__ unsigned long long tk[TCAP];
-  __shared__ unsigned int tc[TCAP];
-  __shared__ unsigned long long ktab[18];
+  constexpr bool BINS = MODE != GENERIC;
+  __shared__ unsigned long long tk[BINS ? 1 : TCAP];
+  __shared__ unsigned int tc[BINS ? 1 : TCAP];
+  __shared__ unsigned int pc[BINS ? BLOCK / 64 : 1][NBINS][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const BlockTable bt{tk, tc};
-  bt_init(bt);
-  ktab_init(m, ktab);
   WaveCache wc;
-  wc_init(wc);
+  if (BINS) {
+    for (int i = threadIdx.x; i < (BLOCK / 64) * NBINS * 64; i += BLOCK) (&pc[0][0][0])[i] = 0;
+  } else {
+    bt_init(bt);
+    wc_init(wc);
+  }
   __syncthreads();
 
   const uint64_t npairs = n >> 1;
@@ -97,34 +182,52 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
         sink ^= ok ? (x[u].x ^ x[u].y) : 0;
         continue;
       }
-      bool b0, b1;
-      const uint64_t k0 = sample_key<MODE>(m, ktab, x[u].x, &b0);
-      const uint64_t k1 = sample_key<MODE>(m, ktab, x[u].y, &b1);
-      anybad |= ok && (b0 || b1);
-      if (ABL == 1) {
-        sink += ok ? (k0 ^ k1) : 0;
-        continue;
+      if (BINS) {
+        const uint32_t b0 = sample_bin<MODE == FAST_P2>(m, x[u].x, ok);
+        const uint32_t b1 = sample_bin<MODE == FAST_P2>(m, x[u].y, ok);
+        if (ABL == 1) {
+          sink += b0 ^ (b1 << 5);
+          continue;
+        }
+        atomicAdd(&pc[wave][b0][lane], 1u);
+        atomicAdd(&pc[wave][b1][lane], 1u);
+      } else {
+        bool b0, b1;
+        const uint64_t k0 = sample_key<MODE>(m, nullptr, x[u].x, &b0);
+        const uint64_t k1 = sample_key<MODE>(m, nullptr, x[u].y, &b1);
+        anybad |= ok && (b0 || b1);
+        if (ABL == 1) {
+          sink += ok ? (k0 ^ k1) : 0;
+          continue;
+        }
+        wave_count(wc, bt, g, k0, ok && !b0);
+        wave_count(wc, bt, g, k1, ok && !b1);
       }
-      wave_count(wc, bt, g, k0, ok && !b0);
-      wave_count(wc, bt, g, k1, ok && !b1);
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) x[u] = y[u];
   }
   if (((n & 1) || head) && blockIdx.x == 0 && threadIdx.x < 64) {
     // odd tail (lane 0) and, for an 8-byte-aligned list, its first sample (lane 1)
-    bool b = false;
     const bool mine = (threadIdx.x == 0 && (n & 1)) || (threadIdx.x == 1 && head);
-    const uint64_t k = mine ? sample_key<MODE>(m, ktab, threadIdx.x == 0 ? smp[n - 1] : *head, &b) : KEY_NONE;
-    anybad |= mine && b;
-    wave_count(wc, bt, g, k, mine && !b);
+    const uint64_t xs = mine ? (threadIdx.x == 0 ? smp[n - 1] : *head) : 0;
+    if (BINS) {
+      const uint32_t bin = sample_bin_any<MODE == FAST_P2>(m, xs, mine);
+      if (ABL == 0) atomicAdd(&pc[0][bin][lane], 1u);
+    } else {
+      bool b = false;
+      const uint64_t k = mine ? sample_key<MODE>(m, nullptr, xs, &b) : KEY_NONE;
+      anybad |= mine && b;
+      if (ABL == 0) wave_count(wc, bt, g, k, mine && !b);
+    }
   }
   if (anybad) atomicOr(&g.flags[1], 1u);
   if (ABL) {
     if (sink == 0x5EED5EED5EED5EEDull) atomicOr(&g.flags[2], 1u);  // keeps the ablated work alive
     return;
   }
-  bt_finish(wc, bt, g);
+  if (BINS) bins_finish(m, pc, g);
+  else bt_finish(wc, bt, g);
 }
 
 // ----------------------------------------------------------- full trace --
