@@ -136,7 +136,7 @@ __device__ __forceinline__ void bins_finish(const Model& m, unsigned int (*pc)[N
 
 template <int MODE, int ABL = 0, int UNR = UNROLL>
 __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t* __restrict__ smp, uint64_t n,
-                                                        const uint64_t* __restrict__ head, GTable g) {
+                                                        const uint64_t* __restrict__ head, int has_head, GTable g) {
   constexpr bool BINS = MODE != GENERIC;
   __shared__ unsigned long long tk[BINS ? 1 : TCAP];
   __shared__ unsigned int tc[BINS ? 1 : TCAP];
@@ -207,10 +207,12 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
 #pragma unroll
     for (int u = 0; u < UNR; ++u) x[u] = y[u];
   }
-  if (((n & 1) || head) && blockIdx.x == 0 && threadIdx.x < 64) {
-    // odd tail (lane 0) and, for an 8-byte-aligned list, its first sample (lane 1)
-    const bool mine = (threadIdx.x == 0 && (n & 1)) || (threadIdx.x == 1 && head);
-    const uint64_t xs = mine ? (threadIdx.x == 0 ? smp[n - 1] : *head) : 0;
+  if (((n & 1) || has_head) && blockIdx.x == 0 && threadIdx.x < 64) {
+    // odd tail (lane 0) and, for an 8-byte-aligned list, its first sample (lane 1).
+    // `head` always points at valid memory, so a speculated load cannot fault.
+    const bool mine = (threadIdx.x == 0 && (n & 1)) || (threadIdx.x == 1 && has_head);
+    const uint64_t* src = (threadIdx.x == 0 && n) ? smp + (n - 1) : head;
+    const uint64_t xs = mine ? *src : 0;
     if (BINS) {
       const uint32_t bin = sample_bin_any<MODE == FAST_P2>(m, xs, mine);
       if (ABL == 0) atomicAdd(&pc[0][bin][lane], 1u);
@@ -398,9 +400,10 @@ int launch_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, h
     set_error("pluss_dev_sampled_hist: sample buffer must be 8-byte aligned");
     return PLUSS_ERR_INPUT;
   }
-  const uint64_t* head = nullptr;
+  const uint64_t* head = d_samples;  // always dereferenceable; used only when has_head
+  int has_head = 0;
   if (((uintptr_t)d_samples & 15u) != 0) {  // peel one sample so the pairs are 16-byte aligned
-    head = d_samples;
+    has_head = 1;
     ++d_samples;
     --n;
   }
@@ -412,20 +415,20 @@ int launch_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, h
   if (grd && atoi(grd) > 0) nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL, atoi(grd));
   if (abl && ctx->m.fast && ctx->m.p2 && (abl[0] == '1' || abl[0] == '2')) {
     if (abl[0] == '1')
-      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 1>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
+      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 1>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, has_head, ctx->g);
     else
-      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 2>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
+      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 2>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, has_head, ctx->g);
   } else if (unr && ctx->m.fast && ctx->m.p2 && (unr[0] == '2' || unr[0] == '8')) {
     if (unr[0] == '2')
-      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 0, 2>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
+      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 0, 2>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, has_head, ctx->g);
     else
-      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 0, 8>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
+      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 0, 8>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, has_head, ctx->g);
   } else if (ctx->m.fast && ctx->m.p2)
-    hipLaunchKernelGGL(k_sampled_hist<FAST_P2>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
+    hipLaunchKernelGGL(k_sampled_hist<FAST_P2>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, has_head, ctx->g);
   else if (ctx->m.fast)
-    hipLaunchKernelGGL(k_sampled_hist<FAST>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
+    hipLaunchKernelGGL(k_sampled_hist<FAST>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, has_head, ctx->g);
   else
-    hipLaunchKernelGGL(k_sampled_hist<GENERIC>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, ctx->g);
+    hipLaunchKernelGGL(k_sampled_hist<GENERIC>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, has_head, ctx->g);
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }

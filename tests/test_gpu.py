@@ -140,10 +140,16 @@ def test_config2_full_size_clean_histogram():
 def test_invalid_samples_raise():
     c = cfg(32, 4)
     bad = np.array([P.pack("C3", 1, 2, 3), P.pack("A0", 40, 0, 0)], np.uint64)
-    with pytest.raises(P.PlussError):
+    with pytest.raises(P.PlussError, match="PLUSS_ERR_INPUT"):
         P.sampled_hist(c, bad)
-    with pytest.raises(P.PlussError):
+    with pytest.raises(P.PlussError, match="PLUSS_ERR_INPUT"):
         P.sampled_hist(c, np.array([7 << 60], np.uint64))
+    with pytest.raises(P.PlussError, match="PLUSS_ERR_INPUT"):
+        P.sampled_hist(c, np.array([P.pack("C3", 1, 2, 3), P.pack("B0", 3, 2, 1), 7 << 60], np.uint64))
+    with pytest.raises(P.PlussError, match="PLUSS_ERR_INPUT"):
+        P.sampled_hist(cfg(32, 4, mode="faithful"), bad)
+    # the device is still healthy afterwards
+    assert P.sampled_hist(c, bad[:1]).total() == 1
 
 
 def test_empty_and_odd_lengths(orc):
