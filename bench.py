@@ -4,8 +4,9 @@
 Workload (BASELINE.json configs[1]): GEMM N=1024,
 8 simulated threads, chunk 4, DS=8, CLS=64, clean mode, 2^24 sampled
 accesses per GPU (default per-reference split, keyed Feistel sample lists).
-One step = reset the histogram, run the sampling kernel over the resident
-sample list, merge the per-workgroup tables and export the canonical table;
+One step = run the sampling kernel over the resident sample list, then fold
+the per-workgroup tables into the canonical exported table and clear the
+histogram for the next step (one launch);
 with N>1 GPUs the step also all-gathers the per-GPU tables over RCCL (the
 only exchange of the path).  Samples are sharded across ranks with no other
 communication, so per-GPU work is fixed (weak scaling).
@@ -134,7 +135,6 @@ def main():
     pairs = []
 
     def step(timed):
-        ctx.reset(sp)
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -142,11 +142,13 @@ def main():
         if timed:
             e1.record(stream)
             pairs.append((e0, e1))
-        ctx.export(keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
+        # canonical table out + histogram cleared for the next pass, in one launch
+        ctx.export_reset(keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
         if world > 1:
             dist.all_gather_into_tensor(gk, keys)
             dist.all_gather_into_tensor(gc, cnts)
 
+    ctx.reset(sp)
     for _ in range(args.warmup):
         step(False)
     if world > 1:

@@ -116,6 +116,10 @@ int pluss_dev_sampled_ri(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t n, 
    key = ref<<60 | kind<<56 | (ri+2).  Equal histograms give equal tables,
    so per-GPU tables can be exchanged by one collective and merged. */
 int pluss_dev_hist_export(pluss_ctx *ctx, uint64_t *d_keys, uint64_t *d_counts, uint64_t cap, void *stream);
+/* the same, and leave the handle's histogram empty for the next pass (bins and
+   traversed counters; error flags are kept until pluss_dev_hist_reset) —
+   one launch instead of export + reset between passes */
+int pluss_dev_hist_export_reset(pluss_ctx *ctx, uint64_t *d_keys, uint64_t *d_counts, uint64_t cap, void *stream);
 /* synchronise and copy the handle's histogram into a host pluss_hist */
 int pluss_hist_fetch(pluss_ctx *ctx, pluss_hist *out);
 /* merge canonical (key,count) tables on the host into a pluss_hist */

@@ -226,6 +226,10 @@ class Context:
     def export(self, d_keys, d_counts, cap, stream=None):
         check(lib().pluss_dev_hist_export(self._h, d_keys, d_counts, cap, stream), "pluss_dev_hist_export")
 
+    def export_reset(self, d_keys, d_counts, cap, stream=None):
+        """export(), then leave the histogram empty for the next pass (one launch)."""
+        check(lib().pluss_dev_hist_export_reset(self._h, d_keys, d_counts, cap, stream), "pluss_dev_hist_export_reset")
+
     def fetch(self):
         h, keep = _hist_buf()
         check(lib().pluss_hist_fetch(self._h, ctypes.byref(h)), "pluss_hist_fetch")

@@ -219,6 +219,11 @@ int pluss_dev_hist_export(pluss_ctx* ctx, uint64_t* d_keys, uint64_t* d_counts, 
   return launch_export(ctx, (unsigned long long*)d_keys, (unsigned long long*)d_counts, cap, pick(ctx, stream));
 }
 
+int pluss_dev_hist_export_reset(pluss_ctx* ctx, uint64_t* d_keys, uint64_t* d_counts, uint64_t cap, void* stream) {
+  if (!ctx || !d_keys || !d_counts) return PLUSS_ERR_CONFIG;
+  return launch_export(ctx, (unsigned long long*)d_keys, (unsigned long long*)d_counts, cap, pick(ctx, stream), true);
+}
+
 int pluss_hist_fetch(pluss_ctx* ctx, pluss_hist* out) {
   if (!ctx || !out) return PLUSS_ERR_CONFIG;
   hipStream_t s = ctx->last ? ctx->last : ctx->stream;

@@ -16,7 +16,7 @@ constexpr uint32_t GCAP = 4096;        // main global histogram slots (power of 
 constexpr uint32_t NREP = 8;           // global replica tables (one per XCD-sized group of workgroups)
 constexpr uint32_t RCAP = 512;         // slots per replica (power of two)
 constexpr int MAX_BLOCKS = 1024;       // 256 CUs x 4 workgroups
-constexpr int UNROLL = 4;              // 16-byte sample pairs per lane per step
+constexpr int UNROLL = 2;              // 16-byte sample pairs per lane per step (tools/ablate.py)
 constexpr unsigned long long KEY_NONE = 0;  // free table slot (histogram keys are never 0)
 
 // Global open-addressing histogram (one per handle), one contiguous
@@ -80,7 +80,7 @@ int launch_ri_dump(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, int64_
 int launch_expand(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t first, uint64_t n, uint64_t* d_out,
                   hipStream_t s);
 int launch_export(pluss_ctx* ctx, unsigned long long* d_keys, unsigned long long* d_counts, uint64_t cap,
-                  hipStream_t s);
+                  hipStream_t s, bool consume = false);
 int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s);
 
 }  // namespace pluss

@@ -134,7 +134,7 @@ __device__ __forceinline__ void bins_finish(const Model& m, unsigned int (*pc)[N
   if (threadIdx.x == BIN_BAD && tot[BIN_BAD]) atomicOr(&g.flags[1], 1u);
 }
 
-template <int MODE, int ABL = 0, int UNR = UNROLL>
+template <int MODE, int ABL = 0, int UNR = UNROLL, bool NT = false>
 __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t* __restrict__ smp, uint64_t n,
                                                         const uint64_t* __restrict__ head, int has_head, GTable g) {
   constexpr bool BINS = MODE != GENERIC;
@@ -159,12 +159,20 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
   uint64_t sink = 0;
   uint64_t base = (uint64_t)blockIdx.x * BLOCK * UNR;
   const uint64_t last = npairs ? npairs - 1 : 0;  // loads are clamped, lanes past the end are masked
+  auto ld = [&](uint64_t i) -> ulonglong2 {
+    if (NT) {  // streamed once: non-temporal hint
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(v + i));
+      return ulonglong2{((unsigned long long)q.y << 32) | q.x, ((unsigned long long)q.w << 32) | q.z};
+    }
+    return v[i];
+  };
   ulonglong2 x[UNR];
   if (npairs) {
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const uint64_t i = base + (uint64_t)u * BLOCK + threadIdx.x;
-      x[u] = v[i < last ? i : last];
+      x[u] = ld(i < last ? i : last);
     }
   }
   for (; base < npairs; base += step) {
@@ -173,7 +181,7 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {  // prefetch the next step
       const uint64_t i = nb + (uint64_t)u * BLOCK + threadIdx.x;
-      y[u] = v[i < last ? i : last];
+      y[u] = ld(i < last ? i : last);
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
@@ -275,7 +283,7 @@ __global__ __launch_bounds__(BLOCK) void k_fulltrace(Model m, GTable g) {
 // unused pairs are (~0, 0) so tables compare and merge canonically.
 constexpr int EXP_THREADS = 1024;
 __global__ __launch_bounds__(EXP_THREADS) void k_export(GTable g, unsigned long long* ok, unsigned long long* oc,
-                                                       uint64_t cap, unsigned int* nout) {
+                                                       uint64_t cap, unsigned int* nout, int consume) {
   __shared__ unsigned long long sk[GCAP];
   __shared__ unsigned long long sc[GCAP];
   __shared__ unsigned long long ck[GCAP];
@@ -287,13 +295,27 @@ __global__ __launch_bounds__(EXP_THREADS) void k_export(GTable g, unsigned long 
   }
   if (threadIdx.x == 0) cnt = full = 0;
   __syncthreads();
-  const uint32_t total_slots = GCAP + NREP * RCAP;
-  for (uint32_t i = threadIdx.x; i < total_slots; i += EXP_THREADS) {
-    const unsigned long long k = i < GCAP ? g.keys[i] : g.rkeys[i - GCAP];
-    if (k != KEY_NONE) {
-      const unsigned long long c = i < GCAP ? g.counts[i] : g.rcounts[i - GCAP];
-      if (!lds_add<unsigned long long, GCAP>(sk, sc, k, c)) atomicOr(&full, 1u);
+  // keys[] and rkeys[] are contiguous (GCAP + NREP*RCAP slots), as are counts[]/rcounts[]:
+  // issue all of a thread's key loads before using any (latency, not bandwidth, bound)
+  constexpr uint32_t SLOTS = GCAP + NREP * RCAP, PER = SLOTS / EXP_THREADS;
+  static_assert(SLOTS % EXP_THREADS == 0, "slot count must divide evenly");
+  unsigned long long kk[PER];
+#pragma unroll
+  for (uint32_t j = 0; j < PER; ++j) kk[j] = g.keys[j * EXP_THREADS + threadIdx.x];
+#pragma unroll
+  for (uint32_t j = 0; j < PER; ++j) {
+    if (kk[j] != KEY_NONE) {
+      const unsigned long long c = g.counts[j * EXP_THREADS + threadIdx.x];
+      if (!lds_add<unsigned long long, GCAP>(sk, sc, kk[j], c)) atomicOr(&full, 1u);
     }
+  }
+  if (consume) {  // export-and-reset: this thread has read its slots, clear them for the next histogram
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+      g.keys[j * EXP_THREADS + threadIdx.x] = KEY_NONE;
+      g.counts[j * EXP_THREADS + threadIdx.x] = 0;
+    }
+    if (threadIdx.x < 8) g.trav[threadIdx.x] = 0;
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < GCAP; i += EXP_THREADS) {
@@ -408,27 +430,33 @@ int launch_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, h
     --n;
   }
   int nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL);
-  // diagnostics only (tools/ablate.py): PLUSS_ABLATE=1|2, PLUSS_UNROLL=2|8, PLUSS_GRID=<blocks>
+  // diagnostics only (tools/ablate.py): PLUSS_ABLATE=1|2, PLUSS_UNROLL=1|4|8, PLUSS_NT=1, PLUSS_GRID=<blocks>
   const char* abl = getenv("PLUSS_ABLATE");
   const char* unr = getenv("PLUSS_UNROLL");
+  const char* ntv = getenv("PLUSS_NT");
   const char* grd = getenv("PLUSS_GRID");
   if (grd && atoi(grd) > 0) nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL, atoi(grd));
-  if (abl && ctx->m.fast && ctx->m.p2 && (abl[0] == '1' || abl[0] == '2')) {
-    if (abl[0] == '1')
-      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 1>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, has_head, ctx->g);
-    else
-      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 2>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, has_head, ctx->g);
-  } else if (unr && ctx->m.fast && ctx->m.p2 && (unr[0] == '2' || unr[0] == '8')) {
-    if (unr[0] == '2')
-      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 0, 2>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, has_head, ctx->g);
-    else
-      hipLaunchKernelGGL((k_sampled_hist<FAST_P2, 0, 8>), dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, has_head, ctx->g);
-  } else if (ctx->m.fast && ctx->m.p2)
-    hipLaunchKernelGGL(k_sampled_hist<FAST_P2>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, has_head, ctx->g);
-  else if (ctx->m.fast)
-    hipLaunchKernelGGL(k_sampled_hist<FAST>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, has_head, ctx->g);
-  else
-    hipLaunchKernelGGL(k_sampled_hist<GENERIC>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, d_samples, n, head, has_head, ctx->g);
+  const int a = abl ? atoi(abl) : 0, u = unr ? atoi(unr) : UNROLL;
+  const bool nt = ntv && ntv[0] == '1';
+  const Model& m = ctx->m;
+  const GTable& g = ctx->g;
+#define PLUSS_LAUNCH_HOT(...) \
+  hipLaunchKernelGGL((k_sampled_hist<__VA_ARGS__>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n, head, has_head, g)
+  if (m.fast && m.p2 && (a || u != UNROLL || nt)) {
+    if (a == 1) PLUSS_LAUNCH_HOT(FAST_P2, 1, UNROLL, false);
+    else if (a == 2) PLUSS_LAUNCH_HOT(FAST_P2, 2, UNROLL, false);
+    else if (u == 1) PLUSS_LAUNCH_HOT(FAST_P2, 0, 1, false);
+    else if (u == 4) PLUSS_LAUNCH_HOT(FAST_P2, 0, 4, false);
+    else if (u == 8) PLUSS_LAUNCH_HOT(FAST_P2, 0, 8, false);
+    else PLUSS_LAUNCH_HOT(FAST_P2, 0, UNROLL, true);
+  } else if (m.fast && m.p2) {
+    PLUSS_LAUNCH_HOT(FAST_P2);
+  } else if (m.fast) {
+    PLUSS_LAUNCH_HOT(FAST);
+  } else {
+    PLUSS_LAUNCH_HOT(GENERIC);
+  }
+#undef PLUSS_LAUNCH_HOT
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }
@@ -479,8 +507,9 @@ int launch_expand(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t first, ui
 }
 
 int launch_export(pluss_ctx* ctx, unsigned long long* d_keys, unsigned long long* d_counts, uint64_t cap,
-                  hipStream_t s) {
-  hipLaunchKernelGGL(k_export, dim3(1), dim3(EXP_THREADS), 0, s, ctx->g, d_keys, d_counts, cap, ctx->d_exp_n);
+                  hipStream_t s, bool consume) {
+  hipLaunchKernelGGL(k_export, dim3(1), dim3(EXP_THREADS), 0, s, ctx->g, d_keys, d_counts, cap, ctx->d_exp_n,
+                     consume ? 1 : 0);
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }

@@ -182,6 +182,15 @@ def test_device_handle_path_and_canonical_export(orc):
         ctx.export(keys.data_ptr(), cnts.data_ptr(), 4096, stream)
         torch.cuda.synchronize()
         h = ctx.fetch()
+        # export-and-reset: two passes give identical tables and leave the table empty
+        k1 = torch.empty(4096, dtype=torch.int64, device="cuda")
+        n1 = torch.empty(4096, dtype=torch.int64, device="cuda")
+        for _ in range(2):
+            ctx.sampled_hist(buf.data_ptr() + 8, total, stream)
+            ctx.export_reset(k1.data_ptr(), n1.data_ptr(), 4096, stream)
+            torch.cuda.synchronize()
+            assert torch.equal(k1, keys) and torch.equal(n1, cnts)
+        assert ctx.fetch().bins == {}
     host = buf[1:].cpu().numpy().view(np.uint64)
     assert h == P.sampled_hist(c, host)
     k = keys.cpu().numpy().view(np.uint64)

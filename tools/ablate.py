@@ -39,8 +39,9 @@ def main():
             off += c
         torch.cuda.synchronize()
         variants = [dict(PLUSS_ABLATE=m) for m in ("2", "1", "0")]
-        variants += [dict(PLUSS_UNROLL=u) for u in ("2", "8")]
-        variants += [dict(PLUSS_GRID=g) for g in ("512", "1792", "2048", "4096")]
+        variants += [dict(PLUSS_UNROLL=u) for u in ("1", "4", "8")]
+        variants += [dict(PLUSS_NT="1")]
+        variants += [dict(PLUSS_GRID=g) for g in ("512", "1792", "2048", "4096", "8192")]
         variants += [dict(PLUSS_ABLATE="2", PLUSS_GRID=g) for g in ("2048", "4096")]
         for v in variants:
             for k in ("PLUSS_ABLATE", "PLUSS_UNROLL", "PLUSS_GRID"):
