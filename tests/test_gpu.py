@@ -185,6 +185,7 @@ def test_device_handle_path_and_canonical_export(orc):
         # export-and-reset: two passes give identical tables and leave the table empty
         k1 = torch.empty(4096, dtype=torch.int64, device="cuda")
         n1 = torch.empty(4096, dtype=torch.int64, device="cuda")
+        ctx.reset(stream)  # fetch() does not clear; start the passes from an empty table
         for _ in range(2):
             ctx.sampled_hist(buf.data_ptr() + 8, total, stream)
             ctx.export_reset(k1.data_ptr(), n1.data_ptr(), 4096, stream)
