@@ -76,6 +76,85 @@ def cpu_baseline(cfg, host_samples, target_s):
                       f"{dt:.1f} s wall on {threads} host threads"}
 
 
+def closed_form_hist(cfg, host):
+    """Independent restatement of the per-sample rules (numpy) for the MRC check."""
+    s = host.astype(np.uint64)
+    m = np.uint64(0xFFFFF)
+    refs = (s >> np.uint64(60)).astype(np.int64)
+    c0 = ((s >> np.uint64(40)) & m).astype(np.int64)
+    c1 = ((s >> np.uint64(20)) & m).astype(np.int64)
+    c2 = (s & m).astype(np.int64)
+    N, T, CS, W = cfg.n, cfg.threads, cfg.chunk, cfg.cls // cfg.ds
+    S = 4 * N + 2
+    p = c0 % CS
+    nxt = np.where(p != CS - 1, c0 + 1, c0 + 1 + (T - 1) * CS)
+    ri = np.select([refs == 0, refs == 1, refs == 4,
+                    (refs == 5) & (c2 < N - 1), (refs == 5) & (c1 % W != W - 1), refs == 5,
+                    (refs == 2) & (c2 % W != W - 1), (refs == 2) & (c1 + 1 < N), refs == 2,
+                    (refs == 3) & (c1 % W != W - 1), (refs == 3) & (nxt < N), refs == 3],
+                   [1, 3, 1, 3, 1, -1, 4, S - 4 * (W - 1), -1, S, N * S - (W - 1) * S, -1])
+    kind = ((refs == 3) & (ri > 0) & (2 * ri > (4 * N + 2) * N)).astype(np.int64)
+    keys = (refs * 4 + kind) * (1 << 40) + (ri + 2)
+    u, cnt = np.unique(keys, return_counts=True)
+    return P.Histogram({(P.REFS[int(k >> 42)], int((k >> 40) & 3), int(k & ((1 << 40) - 1)) - 2): int(n)
+                        for k, n in zip(u, cnt)})
+
+
+def mrc_check(cfg, h, samples):
+    """MRC abs err: r10 host pipeline (CRI -> log2 merge -> AET) on the device
+    histogram vs on an independent closed-form histogram of the same samples."""
+    from pluss_sampler_optimization_amd import host as H
+    ref = closed_form_hist(cfg, samples.cpu().numpy().view(np.uint64))
+    if h.total() != ref.total():  # multi-GPU: h is the merged job; compare this rank's shard only
+        return None
+    _, _, m_gpu = H.mrc_from_r10(cfg.threads, h)
+    _, _, m_ref = H.mrc_from_r10(cfg.threads, ref)
+    keys = set(m_gpu) | set(m_ref)
+    return max(abs(m_gpu.get(k, 0.0) - m_ref.get(k, 0.0)) for k in keys)
+
+
+def fulltrace_bench(device):
+    """BASELINE config 5: full trace (sampling rate 1.0) GEMM N=512, T=4."""
+    cfg = P.SamplerConfig(n=512, threads=4, thr_variant="v1", device=device)
+    with P.Context(cfg) as ctx:
+        ctx.fulltrace()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            ctx.reset()
+            ctx.fulltrace()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / reps
+        h = ctx.fetch()
+    acc = 512 * 512 * (4 * 512 + 2)
+    assert h.total() == acc
+    return {"workload": "GEMM N=512, T=4, full trace (every access evaluated)", "accesses": acc,
+            "ms": dt * 1e3, "accesses_per_s": acc / dt}
+
+
+def faithful_bench(cfg, samples, stream):
+    """FAITHFUL mode (r10 queue semantics: sort + scans) over the same 2^24 list, one sampler per reference."""
+    fcfg = P.SamplerConfig(n=cfg.n, threads=cfg.threads, chunk=cfg.chunk, mode="faithful", device=cfg.device)
+    counts = P.default_counts(cfg.n, len(samples))
+    with P.Context(fcfg) as ctx:
+        def run():
+            ctx.reset(stream.cuda_stream)
+            off = 0
+            for r, c in enumerate(counts):
+                ctx.faithful_hist(r, samples.data_ptr() + 8 * off, c, stream.cuda_stream)
+                off += c
+        run()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        run()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        h = ctx.fetch()
+    return {"samples": len(samples), "ms": dt * 1e3, "samples_per_s": len(samples) / dt,
+            "recorded": h.total() - sum(h.cold(r) for r in P.REFS), "max_traversed": max(h.traversed)}
+
+
 def pmc_traffic():
     """Per-launch HBM bytes of the hot kernel from the committed rocprofv3 --pmc summary, if any."""
     path = os.path.join(ROOT, "profiles", "pmc_sampled_hist.json")
@@ -95,6 +174,7 @@ def main():
     ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the full-trace / faithful side measurements")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -197,6 +277,11 @@ def main():
         "kernel": {"name": "pluss::k_sampled_hist<2> (FAST_P2)", "avg_ms": kern_ms, "bytes_per_launch": BYTES_PER_SAMPLE * n_local},
         "histogram_bins": len(h.bins),
     }
+    if rank == 0:
+        result["mrc_abs_err"] = mrc_check(cfg, h, samples)
+    if rank == 0 and world == 1 and not args.no_extras:
+        result["fulltrace"] = fulltrace_bench(local)
+        result["faithful"] = faithful_bench(cfg, samples, stream)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         host = samples.cpu().numpy().view(np.uint64)
         result["cpu_baseline"] = cpu_baseline(cfg, host, args.cpu_seconds)

@@ -73,14 +73,9 @@ __device__ __forceinline__ uint32_t sample_bin_any(const Model& m, uint64_t x, b
 // Per-sample bin when every active lane holds the same reference `ref`
 // (wave-uniform, so the rule is chosen by a scalar branch and only the
 // compares that reference needs are evaluated).
+// (ref, case) bin of an access whose reference is wave-uniform.
 template <bool P2>
-__device__ __forceinline__ uint32_t sample_bin_ref(const Model& m, uint32_t ref, uint64_t x, bool ok) {
-  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-  const uint32_t c2 = lo & 0xFFFFFu;
-  const uint32_t c1 = __builtin_amdgcn_alignbit(hi, lo, 20) & 0xFFFFFu;
-  const uint32_t c0 = (hi >> 8) & 0xFFFFFu;
-  const uint32_t mx = c0 > c1 ? (c0 > c2 ? c0 : c2) : (c1 > c2 ? c1 : c2);
-  const bool bad = mx >= m.N;
+__device__ __forceinline__ uint32_t bin_uniform(const Model& m, uint32_t ref, uint32_t c0, uint32_t c1, uint32_t c2) {
   const uint32_t Wm1 = m.W - 1;
   uint32_t cs = 0;
   if (ref == C3) {
@@ -95,7 +90,18 @@ __device__ __forceinline__ uint32_t sample_bin_ref(const Model& m, uint32_t ref,
     const uint32_t nxt = c0 + 1 + (p + 1 == m.CS ? (m.T - 1) * m.CS : 0u);
     cs = !c1last ? 0u : (nxt < m.N ? 1u : 2u);
   }
-  const uint32_t bin = ref * 3 + cs;
+  return ref * 3 + cs;
+}
+
+template <bool P2>
+__device__ __forceinline__ uint32_t sample_bin_ref(const Model& m, uint32_t ref, uint64_t x, bool ok) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t c2 = lo & 0xFFFFFu;
+  const uint32_t c1 = __builtin_amdgcn_alignbit(hi, lo, 20) & 0xFFFFFu;
+  const uint32_t c0 = (hi >> 8) & 0xFFFFFu;
+  const uint32_t mx = c0 > c1 ? (c0 > c2 ? c0 : c2) : (c1 > c2 ? c1 : c2);
+  const bool bad = mx >= m.N;
+  const uint32_t bin = bin_uniform<P2>(m, ref, c0, c1, c2);
   return ok ? (bad ? (uint32_t)BIN_BAD : bin) : (uint32_t)BIN_OFF;
 }
 
@@ -241,41 +247,60 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
 }
 
 // ----------------------------------------------------------- full trace --
-// One wave per (c0, c1) pair: C0, C1, then the c2 loop 64 iterations at a time.
+// One wave per (c0, c1) pair: C0, C1, then the c2 loop 64 iterations at a time;
+// the reference is uniform in each inner step.  FAST modes count into the
+// lane-private LDS bins (one ds_add per access), GENERIC through the key cache.
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_fulltrace(Model m, GTable g) {
-  __shared__ unsigned long long tk[TCAP];
-  __shared__ unsigned int tc[TCAP];
-  __shared__ unsigned long long ktab[18];
+  constexpr bool BINS = MODE != GENERIC;
+  __shared__ unsigned long long tk[BINS ? 1 : TCAP];
+  __shared__ unsigned int tc[BINS ? 1 : TCAP];
+  __shared__ unsigned int pc[BINS ? BLOCK / 64 : 1][NBINS][64];
   const BlockTable bt{tk, tc};
-  bt_init(bt);
-  ktab_init(m, ktab);
   WaveCache wc;
-  wc_init(wc);
+  const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
+  if (BINS) {
+    for (int i = threadIdx.x; i < (BLOCK / 64) * NBINS * 64; i += BLOCK) (&pc[0][0][0])[i] = 0;
+  } else {
+    bt_init(bt);
+    wc_init(wc);
+  }
   __syncthreads();
-  const uint32_t lane = __lane_id();
   const uint64_t nwaves = (uint64_t)gridDim.x * (BLOCK / 64);
   const uint64_t npairs = (uint64_t)m.N * m.N;
-  for (uint64_t pr = (uint64_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64; pr < npairs; pr += nwaves) {
+  for (uint64_t pr = (uint64_t)blockIdx.x * (BLOCK / 64) + wave; pr < npairs; pr += nwaves) {
     const uint32_t c0 = (uint32_t)(pr / m.N), c1 = (uint32_t)(pr - (uint64_t)c0 * m.N);
-    {
-      const bool v = lane < 2;
-      uint64_t key = KEY_NONE;
-      if (v) key = key_of<MODE>(m, ktab, lane, c0, c1, 0);
-      wave_count(wc, bt, g, key, v);
-    }
-    for (uint32_t c2b = 0; c2b < m.N; c2b += 64) {
-      const uint32_t c2 = c2b + lane;
-      const bool v = c2 < m.N;
+    if (BINS) {
+      if (lane < 2) atomicAdd(&pc[wave][lane * 3][lane], 1u);  // C0, C1: case 0
+      for (uint32_t c2b = 0; c2b < m.N; c2b += 64) {
+        const uint32_t c2 = c2b + lane;
+        if (c2 < m.N) {
 #pragma unroll
-      for (uint32_t ref = A0; ref <= C3; ++ref) {
+          for (uint32_t ref = A0; ref <= C3; ++ref)
+            atomicAdd(&pc[wave][bin_uniform<MODE == FAST_P2>(m, ref, c0, c1, c2)][lane], 1u);
+        }
+      }
+    } else {
+      {
+        const bool v = lane < 2;
         uint64_t key = KEY_NONE;
-        if (v) key = key_of<MODE>(m, ktab, ref, c0, c1, c2);
+        if (v) key = key_of<MODE>(m, nullptr, lane, c0, c1, 0);
         wave_count(wc, bt, g, key, v);
+      }
+      for (uint32_t c2b = 0; c2b < m.N; c2b += 64) {
+        const uint32_t c2 = c2b + lane;
+        const bool v = c2 < m.N;
+#pragma unroll
+        for (uint32_t ref = A0; ref <= C3; ++ref) {
+          uint64_t key = KEY_NONE;
+          if (v) key = key_of<MODE>(m, nullptr, ref, c0, c1, c2);
+          wave_count(wc, bt, g, key, v);
+        }
       }
     }
   }
-  bt_finish(wc, bt, g);
+  if (BINS) bins_finish(m, pc, g);
+  else bt_finish(wc, bt, g);
 }
 
 // --------------------------------------------------------------- export --
