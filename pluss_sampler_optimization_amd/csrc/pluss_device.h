@@ -56,6 +56,7 @@ __device__ __noinline__ bool g_add_cap(unsigned long long* keys, unsigned long l
 }
 
 __device__ __forceinline__ void g_add(GTable g, uint64_t key, uint64_t cnt) {
+  atomicOr(&g.flags[3], 1u);  // main table in use: k_export must scan it
   if (!g_add_cap(g.keys, g.counts, GCAP, key, cnt)) atomicOr(&g.flags[0], 1u);
 }
 

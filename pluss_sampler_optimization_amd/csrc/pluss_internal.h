@@ -14,7 +14,7 @@ constexpr int BLOCK = 256;             // 4 waves of 64
 constexpr int TCAP = 256;              // LDS histogram slots per workgroup (power of two)
 constexpr uint32_t GCAP = 4096;        // main global histogram slots (power of two)
 constexpr uint32_t NREP = 8;           // global replica tables (one per XCD-sized group of workgroups)
-constexpr uint32_t RCAP = 512;         // slots per replica (power of two)
+constexpr uint32_t RCAP = 256;         // slots per replica (power of two)
 constexpr int MAX_BLOCKS = 1024;       // 256 CUs x 4 workgroups
 constexpr int UNROLL = 2;              // 16-byte sample pairs per lane per step (tools/ablate.py)
 constexpr unsigned long long KEY_NONE = 0;  // free table slot (histogram keys are never 0)
@@ -27,7 +27,7 @@ struct GTable {
   unsigned long long* rkeys;    // NREP * RCAP
   unsigned long long* counts;   // GCAP
   unsigned long long* rcounts;  // NREP * RCAP
-  unsigned int* flags;          // [0] overflow, [1] bad input
+  unsigned int* flags;          // [0] overflow, [1] bad input, [2] diagnostics, [3] main table used
   unsigned long long* trav;     // [6] per-ref traversed (faithful) / [0] total (full trace)
 };
 constexpr size_t TABLE_BYTES = (size_t)(GCAP + NREP * RCAP) * 16 + 16 + 64;

@@ -320,28 +320,48 @@ __global__ __launch_bounds__(EXP_THREADS) void k_export(GTable g, unsigned long 
   }
   if (threadIdx.x == 0) cnt = full = 0;
   __syncthreads();
-  // keys[] and rkeys[] are contiguous (GCAP + NREP*RCAP slots), as are counts[]/rcounts[]:
-  // issue all of a thread's key loads before using any (latency, not bandwidth, bound)
-  constexpr uint32_t SLOTS = GCAP + NREP * RCAP, PER = SLOTS / EXP_THREADS;
-  static_assert(SLOTS % EXP_THREADS == 0, "slot count must divide evenly");
-  unsigned long long kk[PER];
+  // Replicas always; the main table only if a spill reached it (flags[3]).
+  // All of a thread's key and count loads are issued before any is used.
+  constexpr uint32_t RSLOTS = NREP * RCAP, RPER = RSLOTS / EXP_THREADS, MPER = GCAP / EXP_THREADS;
+  static_assert(RSLOTS % EXP_THREADS == 0 && GCAP % EXP_THREADS == 0, "slot counts must divide evenly");
+  const bool main_used = __hip_atomic_load(&g.flags[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  {
+    unsigned long long kk[RPER], cc[RPER];
 #pragma unroll
-  for (uint32_t j = 0; j < PER; ++j) kk[j] = g.keys[j * EXP_THREADS + threadIdx.x];
+    for (uint32_t j = 0; j < RPER; ++j) {
+      kk[j] = g.rkeys[j * EXP_THREADS + threadIdx.x];
+      cc[j] = g.rcounts[j * EXP_THREADS + threadIdx.x];
+    }
 #pragma unroll
-  for (uint32_t j = 0; j < PER; ++j) {
-    if (kk[j] != KEY_NONE) {
-      const unsigned long long c = g.counts[j * EXP_THREADS + threadIdx.x];
-      if (!lds_add<unsigned long long, GCAP>(sk, sc, kk[j], c)) atomicOr(&full, 1u);
+    for (uint32_t j = 0; j < RPER; ++j)
+      if (kk[j] != KEY_NONE && !lds_add<unsigned long long, GCAP>(sk, sc, kk[j], cc[j])) atomicOr(&full, 1u);
+    if (consume) {  // export-and-reset: clear what this thread has read
+#pragma unroll
+      for (uint32_t j = 0; j < RPER; ++j) {
+        g.rkeys[j * EXP_THREADS + threadIdx.x] = KEY_NONE;
+        g.rcounts[j * EXP_THREADS + threadIdx.x] = 0;
+      }
     }
   }
-  if (consume) {  // export-and-reset: this thread has read its slots, clear them for the next histogram
+  if (main_used) {
+    unsigned long long kk[MPER], cc[MPER];
 #pragma unroll
-    for (uint32_t j = 0; j < PER; ++j) {
-      g.keys[j * EXP_THREADS + threadIdx.x] = KEY_NONE;
-      g.counts[j * EXP_THREADS + threadIdx.x] = 0;
+    for (uint32_t j = 0; j < MPER; ++j) {
+      kk[j] = g.keys[j * EXP_THREADS + threadIdx.x];
+      cc[j] = g.counts[j * EXP_THREADS + threadIdx.x];
     }
-    if (threadIdx.x < 8) g.trav[threadIdx.x] = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < MPER; ++j)
+      if (kk[j] != KEY_NONE && !lds_add<unsigned long long, GCAP>(sk, sc, kk[j], cc[j])) atomicOr(&full, 1u);
+    if (consume) {
+#pragma unroll
+      for (uint32_t j = 0; j < MPER; ++j) {
+        g.keys[j * EXP_THREADS + threadIdx.x] = KEY_NONE;
+        g.counts[j * EXP_THREADS + threadIdx.x] = 0;
+      }
+    }
   }
+  if (consume && threadIdx.x < 8) g.trav[threadIdx.x] = 0;
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < GCAP; i += EXP_THREADS) {
     if (sk[i] != KEY_NONE) {
@@ -386,6 +406,7 @@ __global__ __launch_bounds__(EXP_THREADS) void k_export(GTable g, unsigned long 
   if (threadIdx.x == 0) {
     *nout = n;
     if (n > cap || full) atomicOr(&g.flags[0], 2u);
+    if (consume) g.flags[3] = 0;  // every thread read it before the first __syncthreads
   }
 }
 
