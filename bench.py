@@ -166,6 +166,12 @@ def pmc_traffic():
     return None
 
 
+def gather_cpu(t):
+    out = torch.empty(dist.get_world_size() * t.numel(), dtype=t.dtype)
+    dist.all_gather_into_tensor(out, t.cpu())
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -175,6 +181,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the full-trace / faithful side measurements")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend (nccl = RCCL over xGMI; gloo only to rehearse N>1 on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -183,9 +191,13 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    local = local % max(1, torch.cuda.device_count())  # rehearsal: several ranks may share one GPU
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     spec = CONFIGS[args.config]
     cfg = P.SamplerConfig(n=spec["n"], threads=spec["threads"], chunk=4, ds=8, cls=64, mode="clean", device=local)
@@ -225,8 +237,12 @@ def main():
         # canonical table out + histogram cleared for the next pass, in one launch
         ctx.export_reset(keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
         if world > 1:
-            dist.all_gather_into_tensor(gk, keys)
-            dist.all_gather_into_tensor(gc, cnts)
+            if args.backend == "nccl":
+                dist.all_gather_into_tensor(gk, keys)
+                dist.all_gather_into_tensor(gc, cnts)
+            else:
+                gk.copy_(gather_cpu(keys))
+                gc.copy_(gather_cpu(cnts))
 
     ctx.reset(sp)
     for _ in range(args.warmup):
@@ -242,7 +258,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
