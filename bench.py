@@ -175,8 +175,8 @@ def gather_cpu(t):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -224,18 +224,10 @@ def main():
         off += cnt
     torch.cuda.synchronize()
 
-    pairs = []
-
-    def step(timed):
-        if timed:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-        ctx.sampled_hist(samples.data_ptr(), n_local, sp)
-        if timed:
-            e1.record(stream)
-            pairs.append((e0, e1))
-        # canonical table out + histogram cleared for the next pass, in one launch
-        ctx.export_reset(keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
+    def step():
+        # one launch: count every sample, the last workgroup writes the canonical
+        # (key, count) table and empties the histogram for the next pass
+        ctx.sampled_hist_export(samples.data_ptr(), n_local, keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
         if world > 1:
             if args.backend == "nccl":
                 dist.all_gather_into_tensor(gk, keys)
@@ -246,13 +238,18 @@ def main():
 
     ctx.reset(sp)
     for _ in range(args.warmup):
-        step(False)
+        step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # HIP events on the library's stream bracket the timed region: with one
+    # launch per step (N=1) their span / K is the kernel's average duration
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    e0.record(stream)
     for _ in range(args.steps):
-        step(True)
+        step()
+    e1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -262,7 +259,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in pairs])) if pairs else float("nan")
+    kern_ms = e0.elapsed_time(e1) / args.steps
     # correctness of the merged histogram: every sample of every rank is counted once
     if world > 1:
         h = P.hist_from_tables(gk.cpu().numpy().view(np.uint64), gc.cpu().numpy().view(np.uint64))
@@ -290,7 +287,9 @@ def main():
                                                              else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic()},
-        "kernel": {"name": "pluss::k_sampled_hist<2> (FAST_P2)", "avg_ms": kern_ms, "bytes_per_launch": BYTES_PER_SAMPLE * n_local},
+        "kernel": {"name": "pluss::k_sampled_hist<2,0,2,false,true> (FAST_P2, fused export)",
+                   "avg_ms": kern_ms, "timing": "HIP events on the launch stream around the K timed steps / K"
+                   + (" (includes the all_gather)" if world > 1 else ""), "bytes_per_launch": BYTES_PER_SAMPLE * n_local},
         "histogram_bins": len(h.bins),
     }
     if rank == 0:

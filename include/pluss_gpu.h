@@ -120,6 +120,11 @@ int pluss_dev_hist_export(pluss_ctx *ctx, uint64_t *d_keys, uint64_t *d_counts, 
    traversed counters; error flags are kept until pluss_dev_hist_reset) —
    one launch instead of export + reset between passes */
 int pluss_dev_hist_export_reset(pluss_ctx *ctx, uint64_t *d_keys, uint64_t *d_counts, uint64_t cap, void *stream);
+/* one pass: pluss_dev_sampled_hist, then pluss_dev_hist_export_reset — a
+   single launch when N % (CLS/DS) == 0 and the handle holds only clean-mode
+   counts (the last workgroup to finish writes the table) */
+int pluss_dev_sampled_hist_export(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t n, uint64_t *d_keys,
+                                  uint64_t *d_counts, uint64_t cap, void *stream);
 /* synchronise and copy the handle's histogram into a host pluss_hist */
 int pluss_hist_fetch(pluss_ctx *ctx, pluss_hist *out);
 /* merge canonical (key,count) tables on the host into a pluss_hist */

@@ -21,7 +21,7 @@ EXPORTS = [
     "pluss_default_counts",
     "pluss_ctx_create", "pluss_ctx_destroy", "pluss_ctx_stream", "pluss_dev_expand", "pluss_dev_hist_reset",
     "pluss_dev_sampled_hist", "pluss_dev_faithful_hist", "pluss_dev_fulltrace_hist", "pluss_dev_sampled_ri",
-    "pluss_dev_hist_export", "pluss_dev_hist_export_reset", "pluss_hist_fetch", "pluss_hist_from_tables",
+    "pluss_dev_hist_export", "pluss_dev_hist_export_reset", "pluss_dev_sampled_hist_export", "pluss_hist_fetch", "pluss_hist_from_tables",
 ]
 
 
@@ -90,6 +90,7 @@ def lib():
         "pluss_dev_sampled_ri": (ctypes.c_int, [vp, vp, u64, vp, vp, vp]),
         "pluss_dev_hist_export": (ctypes.c_int, [vp, vp, vp, u64, vp]),
         "pluss_dev_hist_export_reset": (ctypes.c_int, [vp, vp, vp, u64, vp]),
+        "pluss_dev_sampled_hist_export": (ctypes.c_int, [vp, vp, u64, vp, vp, u64, vp]),
         "pluss_hist_fetch": (ctypes.c_int, [vp, histp]),
         "pluss_hist_from_tables": (ctypes.c_int, [vp, vp, u64, histp]),
     }

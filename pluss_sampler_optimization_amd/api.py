@@ -230,6 +230,11 @@ class Context:
         """export(), then leave the histogram empty for the next pass (one launch)."""
         check(lib().pluss_dev_hist_export_reset(self._h, d_keys, d_counts, cap, stream), "pluss_dev_hist_export_reset")
 
+    def sampled_hist_export(self, d_samples, n, d_keys, d_counts, cap, stream=None):
+        """sampled_hist() then export_reset() -- one launch for N % (CLS/DS) == 0 shapes."""
+        check(lib().pluss_dev_sampled_hist_export(self._h, d_samples, n, d_keys, d_counts, cap, stream),
+              "pluss_dev_sampled_hist_export")
+
     def fetch(self):
         h, keep = _hist_buf()
         check(lib().pluss_hist_fetch(self._h, ctypes.byref(h)), "pluss_hist_fetch")

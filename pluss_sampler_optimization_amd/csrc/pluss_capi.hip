@@ -147,8 +147,9 @@ int pluss_ctx_create(const pluss_cfg* cfg, pluss_ctx** out) {
     c->g.rkeys = base + GCAP;
     c->g.counts = base + GCAP + NREP * RCAP;
     c->g.rcounts = base + 2 * GCAP + NREP * RCAP;
-    c->g.flags = (unsigned int*)(base + 2 * (GCAP + NREP * RCAP));
-    c->g.trav = base + 2 * (GCAP + NREP * RCAP) + 2;
+    c->g.bins = base + 2 * (GCAP + NREP * RCAP);
+    c->g.flags = (unsigned int*)(c->g.bins + NREP * BSTRIDE);
+    c->g.trav = c->g.bins + NREP * BSTRIDE + 4;
   }
   if (hipMalloc((void**)&c->d_exp_keys, GCAP * 8) != hipSuccess) return fail("export");
   if (hipMalloc((void**)&c->d_exp_counts, GCAP * 8) != hipSuccess) return fail("export");
@@ -222,6 +223,13 @@ int pluss_dev_hist_export(pluss_ctx* ctx, uint64_t* d_keys, uint64_t* d_counts, 
 int pluss_dev_hist_export_reset(pluss_ctx* ctx, uint64_t* d_keys, uint64_t* d_counts, uint64_t cap, void* stream) {
   if (!ctx || !d_keys || !d_counts) return PLUSS_ERR_CONFIG;
   return launch_export(ctx, (unsigned long long*)d_keys, (unsigned long long*)d_counts, cap, pick(ctx, stream), true);
+}
+
+int pluss_dev_sampled_hist_export(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, uint64_t* d_keys,
+                                  uint64_t* d_counts, uint64_t cap, void* stream) {
+  if (!ctx || (!d_samples && n) || !d_keys || !d_counts) return PLUSS_ERR_CONFIG;
+  return launch_sampled_hist_export(ctx, d_samples, n, (unsigned long long*)d_keys, (unsigned long long*)d_counts,
+                                    cap, pick(ctx, stream));
 }
 
 int pluss_hist_fetch(pluss_ctx* ctx, pluss_hist* out) {

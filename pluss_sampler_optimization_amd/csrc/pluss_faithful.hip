@@ -155,6 +155,7 @@ int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint
     if (int rc = grow(&b.scal, 4)) return rc;
   }
   if (n == 0) return PLUSS_OK;
+  ctx->tables_dirty = true;
   if (n > 0xFFFFFFFFull) {
     set_error("faithful mode: at most 2^32-1 samples per reference");
     return PLUSS_ERR_CONFIG;

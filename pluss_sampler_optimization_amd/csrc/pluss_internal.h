@@ -19,18 +19,26 @@ constexpr int MAX_BLOCKS = 1024;       // 256 CUs x 4 workgroups
 constexpr int UNROLL = 2;              // 16-byte sample pairs per lane per step (tools/ablate.py)
 constexpr unsigned long long KEY_NONE = 0;  // free table slot (histogram keys are never 0)
 
-// Global open-addressing histogram (one per handle), one contiguous
-// allocation so a single memset resets it:
-//   keys[GCAP] rkeys[NREP*RCAP] counts[GCAP] rcounts[NREP*RCAP] flags[4] trav[8]
+constexpr uint32_t BSTRIDE = 32;       // direct (ref, case) counters per replica (18 used; 256 B apart)
+
+// Global histogram state (one per handle), one contiguous allocation so a
+// single memset resets it:
+//   keys[GCAP] rkeys[NREP*RCAP] counts[GCAP] rcounts[NREP*RCAP] bins[NREP*BSTRIDE] flags[8] trav[8]
+// FAST-mode kernels count into `bins` (18 fixed (ref, case) keys, Model::keytab);
+// arbitrary exact keys (GENERIC shapes, faithful mode) go to the open-addressing
+// replicas, spilling to the main table.
 struct GTable {
   unsigned long long* keys;     // GCAP
   unsigned long long* rkeys;    // NREP * RCAP
   unsigned long long* counts;   // GCAP
   unsigned long long* rcounts;  // NREP * RCAP
-  unsigned int* flags;          // [0] overflow, [1] bad input, [2] diagnostics, [3] main table used
+  unsigned long long* bins;     // NREP * BSTRIDE
+  unsigned int* flags;          // [0] overflow, [1] bad input, [2] diagnostics, [3] main table used,
+                                // [4] finished workgroups of a fused count+export launch
   unsigned long long* trav;     // [6] per-ref traversed (faithful) / [0] total (full trace)
 };
-constexpr size_t TABLE_BYTES = (size_t)(GCAP + NREP * RCAP) * 16 + 16 + 64;
+constexpr size_t TABLE_WORDS = 2 * (size_t)(GCAP + NREP * RCAP) + NREP * BSTRIDE + 4 + 8;
+constexpr size_t TABLE_BYTES = TABLE_WORDS * 8;
 
 struct FaithfulBufs {
   uint64_t cap = 0;
@@ -54,6 +62,7 @@ struct pluss_ctx {
   unsigned int* d_exp_n;
   pluss::FaithfulBufs fb;
   hipStream_t last;   // stream of the most recent launch (fetch orders after it)
+  bool tables_dirty;  // hash tables may hold counts (GENERIC / faithful launches since the last reset)
 };
 
 namespace pluss {
@@ -81,6 +90,10 @@ int launch_expand(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t first, ui
                   hipStream_t s);
 int launch_export(pluss_ctx* ctx, unsigned long long* d_keys, unsigned long long* d_counts, uint64_t cap,
                   hipStream_t s, bool consume = false);
+// count a sample list and export-and-reset in one launch when only the direct
+// bins can hold counts (FAST shapes); otherwise the two launches
+int launch_sampled_hist_export(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, unsigned long long* d_keys,
+                               unsigned long long* d_counts, uint64_t cap, hipStream_t s);
 int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s);
 
 }  // namespace pluss

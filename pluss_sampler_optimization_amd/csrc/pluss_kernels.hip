@@ -120,9 +120,10 @@ __device__ __forceinline__ uint32_t sample_bin(const Model& m, uint64_t x, bool 
   return sample_bin_any<P2>(m, x, ok);
 }
 
-// Block-wide reduction of the per-lane bin counters; bins with a count go to
-// replica blockIdx % NREP under their precomputed key.
-__device__ __forceinline__ void bins_finish(const Model& m, unsigned int (*pc)[NBINS][64], GTable g) {
+// Block-wide reduction of the per-lane bin counters; each bin with a count is
+// added to its direct counter in replica blockIdx % NREP (workgroups are
+// dealt round-robin over the 8 XCDs, so a replica is hit from one XCD).
+__device__ __forceinline__ void bins_finish(unsigned int (*pc)[NBINS][64], GTable g) {
   __shared__ unsigned long long tot[NBINS];
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -136,13 +137,88 @@ __device__ __forceinline__ void bins_finish(const Model& m, unsigned int (*pc)[N
   }
   __syncthreads();
   if (threadIdx.x < 18 && tot[threadIdx.x])
-    g_add_rep(g, blockIdx.x & (NREP - 1), m.keytab[threadIdx.x], tot[threadIdx.x]);
+    atomicAdd(&g.bins[(blockIdx.x & (NREP - 1)) * BSTRIDE + threadIdx.x], tot[threadIdx.x]);
   if (threadIdx.x == BIN_BAD && tot[BIN_BAD]) atomicOr(&g.flags[1], 1u);
 }
 
-template <int MODE, int ABL = 0, int UNR = UNROLL, bool NT = false>
+// Tail of a fused count+export launch, run by the last workgroup to finish:
+// fold the direct bins of all replicas (equal keys merged), write the
+// canonical table -- distinct keys ascending, then (~0, 0) up to `cap` --
+// and leave the histogram empty (bins, traversed, the finish counter).
+// Only used when the hash tables hold nothing (pluss_ctx::tables_dirty).
+__device__ void bins_export_tail(const Model& m, GTable g, unsigned long long* ok, unsigned long long* oc,
+                                 uint64_t cap, unsigned int* nout) {
+  __shared__ unsigned long long ek[18], ec[18];
+  __shared__ unsigned int en;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) en = 0;
+  if (t < 18) {
+    unsigned long long c = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < NREP; ++r) {
+      c += __hip_atomic_load(&g.bins[r * BSTRIDE + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      g.bins[r * BSTRIDE + t] = 0;
+    }
+    ek[t] = m.keytab[t];
+    ec[t] = c;
+  }
+  if (t < 8) g.trav[t] = 0;
+  __syncthreads();
+  unsigned long long key = 0, tot = 0;
+  uint32_t rank = 0;
+  bool first = false;
+  if (t < 18 && ec[t]) {
+    key = ek[t];
+    first = true;
+    for (uint32_t j = 0; j < 18; ++j) {
+      if (!ec[j]) continue;
+      if (ek[j] == key) {
+        tot += ec[j];
+        first &= j >= t;
+      }
+    }
+    if (first) {
+      // rank = distinct nonzero keys below `key` (count each key at its first index)
+      for (uint32_t j = 0; j < 18; ++j) {
+        if (!ec[j] || ek[j] >= key) continue;
+        bool jfirst = true;
+        for (uint32_t i = 0; i < j; ++i) jfirst &= !(ec[i] && ek[i] == ek[j]);
+        rank += jfirst;
+      }
+      atomicAdd(&en, 1u);
+    }
+  }
+  __syncthreads();
+  const uint32_t n = en;
+  if (first && rank < cap) {
+    ok[rank] = key;
+    oc[rank] = tot;
+  }
+  for (uint64_t i = n + t; i < cap; i += BLOCK) {
+    ok[i] = KEY_EMPTY;
+    oc[i] = 0ull;
+  }
+  if (t == 0) {
+    *nout = n;
+    if (n > cap) atomicOr(&g.flags[0], 2u);
+    g.flags[4] = 0;
+  }
+}
+
+// Export arguments of a fused launch (FUSE: the last workgroup to finish
+// writes the canonical table and empties the histogram).
+struct ExportArgs {
+  unsigned long long* keys;
+  unsigned long long* counts;
+  uint64_t cap;
+  unsigned int* nout;
+};
+
+template <int MODE, int ABL = 0, int UNR = UNROLL, bool NT = false, bool FUSE = false>
 __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t* __restrict__ smp, uint64_t n,
-                                                        const uint64_t* __restrict__ head, int has_head, GTable g) {
+                                                        const uint64_t* __restrict__ head, int has_head, GTable g,
+                                                        ExportArgs ex) {
+  static_assert(!FUSE || MODE != GENERIC, "fused export needs the direct bins");
   constexpr bool BINS = MODE != GENERIC;
   __shared__ unsigned long long tk[BINS ? 1 : TCAP];
   __shared__ unsigned int tc[BINS ? 1 : TCAP];
@@ -242,8 +318,19 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
     if (sink == 0x5EED5EED5EED5EEDull) atomicOr(&g.flags[2], 1u);  // keeps the ablated work alive
     return;
   }
-  if (BINS) bins_finish(m, pc, g);
+  if (BINS) bins_finish(pc, g);
   else bt_finish(wc, bt, g);
+  if (FUSE) {
+    __shared__ unsigned int amlast;
+    __threadfence();  // this workgroup's bin atomics are ordered before its finish count
+    __syncthreads();
+    if (threadIdx.x == 0) amlast = atomicAdd(&g.flags[4], 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (amlast) {
+      __threadfence();
+      bins_export_tail(m, g, ex.keys, ex.counts, ex.cap, ex.nout);
+    }
+  }
 }
 
 // ----------------------------------------------------------- full trace --
@@ -299,7 +386,7 @@ __global__ __launch_bounds__(BLOCK) void k_fulltrace(Model m, GTable g) {
       }
     }
   }
-  if (BINS) bins_finish(m, pc, g);
+  if (BINS) bins_finish(pc, g);
   else bt_finish(wc, bt, g);
 }
 
@@ -307,8 +394,9 @@ __global__ __launch_bounds__(BLOCK) void k_fulltrace(Model m, GTable g) {
 // Fold main table + replicas, sort by key, write `cap` (key,count) pairs;
 // unused pairs are (~0, 0) so tables compare and merge canonically.
 constexpr int EXP_THREADS = 1024;
-__global__ __launch_bounds__(EXP_THREADS) void k_export(GTable g, unsigned long long* ok, unsigned long long* oc,
-                                                       uint64_t cap, unsigned int* nout, int consume) {
+__global__ __launch_bounds__(EXP_THREADS) void k_export(Model m, GTable g, unsigned long long* ok,
+                                                       unsigned long long* oc, uint64_t cap, unsigned int* nout,
+                                                       int consume) {
   __shared__ unsigned long long sk[GCAP];
   __shared__ unsigned long long sc[GCAP];
   __shared__ unsigned long long ck[GCAP];
@@ -360,6 +448,12 @@ __global__ __launch_bounds__(EXP_THREADS) void k_export(GTable g, unsigned long 
         g.counts[j * EXP_THREADS + threadIdx.x] = 0;
       }
     }
+  }
+  if (threadIdx.x < NREP * BSTRIDE) {  // direct (ref, case) bins of the FAST kernels
+    const uint32_t b = threadIdx.x % BSTRIDE;
+    const unsigned long long c = b < 18 ? g.bins[threadIdx.x] : 0ull;
+    if (c && !lds_add<unsigned long long, GCAP>(sk, sc, m.keytab[b], c)) atomicOr(&full, 1u);
+    if (consume && c) g.bins[threadIdx.x] = 0;
   }
   if (consume && threadIdx.x < 8) g.trav[threadIdx.x] = 0;
   __syncthreads();
@@ -459,23 +553,38 @@ static int grid_for(uint64_t work, uint64_t per_block, int max_blocks = MAX_BLOC
 
 int launch_table_reset(pluss_ctx* ctx, hipStream_t s) {
   PLUSS_HIP_CHECK(hipMemsetAsync(ctx->d_table, 0, TABLE_BYTES, s));
+  ctx->tables_dirty = false;
   return PLUSS_OK;
 }
 
-int launch_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hipStream_t s) {
-  if (n == 0) return PLUSS_OK;
+// `fuse` != null: FAST shapes only, the launch also exports and resets (the
+// caller checked pluss_ctx::tables_dirty); n may then be 0.
+static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hipStream_t s, const ExportArgs* fuse,
+                      const char* api) {
+  if (n == 0 && !fuse) return PLUSS_OK;
   if (((uintptr_t)d_samples & 7u) != 0) {
-    set_error("pluss_dev_sampled_hist: sample buffer must be 8-byte aligned");
+    set_error(std::string(api) + ": sample buffer must be 8-byte aligned");
     return PLUSS_ERR_INPUT;
   }
   const uint64_t* head = d_samples;  // always dereferenceable; used only when has_head
   int has_head = 0;
-  if (((uintptr_t)d_samples & 15u) != 0) {  // peel one sample so the pairs are 16-byte aligned
+  if (n && ((uintptr_t)d_samples & 15u) != 0) {  // peel one sample so the pairs are 16-byte aligned
     has_head = 1;
     ++d_samples;
     --n;
   }
   int nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL);
+  const Model& m = ctx->m;
+  const GTable& g = ctx->g;
+#define PLUSS_LAUNCH_HOT(EX, ...)                                                                                  \
+  hipLaunchKernelGGL((k_sampled_hist<__VA_ARGS__>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n, head, has_head, g, \
+                     EX)
+  if (fuse) {
+    if (m.p2) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, UNROLL, false, true);
+    else PLUSS_LAUNCH_HOT(*fuse, FAST, 0, UNROLL, false, true);
+    PLUSS_HIP_CHECK(hipGetLastError());
+    return PLUSS_OK;
+  }
   // diagnostics only (tools/ablate.py): PLUSS_ABLATE=1|2, PLUSS_UNROLL=1|4|8, PLUSS_NT=1, PLUSS_GRID=<blocks>
   const char* abl = getenv("PLUSS_ABLATE");
   const char* unr = getenv("PLUSS_UNROLL");
@@ -484,30 +593,43 @@ int launch_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, h
   if (grd && atoi(grd) > 0) nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL, atoi(grd));
   const int a = abl ? atoi(abl) : 0, u = unr ? atoi(unr) : UNROLL;
   const bool nt = ntv && ntv[0] == '1';
-  const Model& m = ctx->m;
-  const GTable& g = ctx->g;
-#define PLUSS_LAUNCH_HOT(...) \
-  hipLaunchKernelGGL((k_sampled_hist<__VA_ARGS__>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n, head, has_head, g)
+  const ExportArgs ex{nullptr, nullptr, 0, nullptr};
+  if (!m.fast) ctx->tables_dirty = true;
   if (m.fast && m.p2 && (a || u != UNROLL || nt)) {
-    if (a == 1) PLUSS_LAUNCH_HOT(FAST_P2, 1, UNROLL, false);
-    else if (a == 2) PLUSS_LAUNCH_HOT(FAST_P2, 2, UNROLL, false);
-    else if (u == 1) PLUSS_LAUNCH_HOT(FAST_P2, 0, 1, false);
-    else if (u == 4) PLUSS_LAUNCH_HOT(FAST_P2, 0, 4, false);
-    else if (u == 8) PLUSS_LAUNCH_HOT(FAST_P2, 0, 8, false);
-    else PLUSS_LAUNCH_HOT(FAST_P2, 0, UNROLL, true);
+    if (a == 1) PLUSS_LAUNCH_HOT(ex, FAST_P2, 1, UNROLL, false);
+    else if (a == 2) PLUSS_LAUNCH_HOT(ex, FAST_P2, 2, UNROLL, false);
+    else if (u == 1) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, 1, false);
+    else if (u == 4) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, 4, false);
+    else if (u == 8) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, 8, false);
+    else PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, true);
   } else if (m.fast && m.p2) {
-    PLUSS_LAUNCH_HOT(FAST_P2);
+    PLUSS_LAUNCH_HOT(ex, FAST_P2);
   } else if (m.fast) {
-    PLUSS_LAUNCH_HOT(FAST);
+    PLUSS_LAUNCH_HOT(ex, FAST);
   } else {
-    PLUSS_LAUNCH_HOT(GENERIC);
+    PLUSS_LAUNCH_HOT(ex, GENERIC);
   }
 #undef PLUSS_LAUNCH_HOT
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }
 
+int launch_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hipStream_t s) {
+  return hot_launch(ctx, d_samples, n, s, nullptr, "pluss_dev_sampled_hist");
+}
+
+int launch_sampled_hist_export(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, unsigned long long* d_keys,
+                               unsigned long long* d_counts, uint64_t cap, hipStream_t s) {
+  if (ctx->m.fast && !ctx->tables_dirty) {
+    const ExportArgs ex{d_keys, d_counts, cap, ctx->d_exp_n};
+    return hot_launch(ctx, d_samples, n, s, &ex, "pluss_dev_sampled_hist_export");
+  }
+  if (int rc = hot_launch(ctx, d_samples, n, s, nullptr, "pluss_dev_sampled_hist_export")) return rc;
+  return launch_export(ctx, d_keys, d_counts, cap, s, true);
+}
+
 int launch_fulltrace(pluss_ctx* ctx, hipStream_t s) {
+  if (!ctx->m.fast) ctx->tables_dirty = true;
   const uint64_t npairs = (uint64_t)ctx->m.N * ctx->m.N;
   const int nb = grid_for(npairs, BLOCK / 64 * 8);
   if (ctx->m.fast && ctx->m.p2)
@@ -554,9 +676,10 @@ int launch_expand(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t first, ui
 
 int launch_export(pluss_ctx* ctx, unsigned long long* d_keys, unsigned long long* d_counts, uint64_t cap,
                   hipStream_t s, bool consume) {
-  hipLaunchKernelGGL(k_export, dim3(1), dim3(EXP_THREADS), 0, s, ctx->g, d_keys, d_counts, cap, ctx->d_exp_n,
-                     consume ? 1 : 0);
+  hipLaunchKernelGGL(k_export, dim3(1), dim3(EXP_THREADS), 0, s, ctx->m, ctx->g, d_keys, d_counts, cap,
+                     ctx->d_exp_n, consume ? 1 : 0);
   PLUSS_HIP_CHECK(hipGetLastError());
+  if (consume) ctx->tables_dirty = false;
   return PLUSS_OK;
 }
 

@@ -202,6 +202,76 @@ def test_device_handle_path_and_canonical_export(orc):
     assert h.total() == total
 
 
+@pytest.mark.parametrize("N,T,CS", [(256, 4, 4), (96, 3, 3), (100, 3, 5)], ids=["fast_p2", "fast", "generic"])
+def test_fused_count_and_export(orc, N, T, CS):
+    """pluss_dev_sampled_hist_export (one launch on FAST shapes: the last
+    workgroup writes the table) == sampled_hist + export_reset == the oracle;
+    repeated passes, empty lists, unaligned lists, a too-small table, and a
+    handle already holding faithful-mode counts (two-launch fallback)."""
+    torch = pytest.importorskip("torch")
+    c = cfg(N, T, CS)
+    counts = P.default_counts(N, 60000)
+    total = sum(counts)
+    host = np.concatenate([P.expand_samples(c, 0x5EED0002, r, 0, counts[r]) for r in range(6)])
+    buf = torch.from_numpy(np.concatenate([host[:1], host]).view(np.int64)).cuda()
+    stream = torch.cuda.current_stream().cuda_stream
+    want = oracle_clean_hist(orc, orc.cfg(N, T, CS), host)
+
+    def tables():
+        return (torch.full((4096,), 7, dtype=torch.int64, device="cuda"),
+                torch.full((4096,), 7, dtype=torch.int64, device="cuda"))
+
+    def as_hist(k, n):
+        return P.hist_from_tables(k.cpu().numpy().view(np.uint64), n.cpu().numpy().view(np.uint64))
+
+    with P.Context(c) as ctx, P.Context(c) as ref_ctx:
+        rk, rn = tables()
+        ref_ctx.sampled_hist(buf.data_ptr() + 8, total, stream)
+        ref_ctx.export_reset(rk.data_ptr(), rn.data_ptr(), 4096, stream)
+        for off in (1, 0):  # 16-byte aligned list, then 8-byte aligned (peeled head)
+            for _ in range(2):
+                k, n = tables()
+                cnt = total if off else total + 1
+                ctx.sampled_hist_export(buf.data_ptr() + 8 * off, cnt, k.data_ptr(), n.data_ptr(), 4096, stream)
+                torch.cuda.synchronize()
+                if off:
+                    assert torch.equal(k, rk) and torch.equal(n, rn)
+                    assert as_hist(k, n).bins == want
+                else:
+                    assert as_hist(k, n).total() == total + 1
+        assert ctx.fetch().bins == {}
+        k, n = tables()
+        ctx.sampled_hist_export(buf.data_ptr(), 0, k.data_ptr(), n.data_ptr(), 4096, stream)
+        torch.cuda.synchronize()
+        assert (k.cpu().numpy().view(np.uint64) == np.uint64(2 ** 64 - 1)).all() and (n.cpu() == 0).all()
+        # a table smaller than the histogram: flagged, the next fetch reports it
+        k, n = tables()
+        ctx.sampled_hist_export(buf.data_ptr() + 8, total, k.data_ptr(), n.data_ptr(), 2, stream)
+        with pytest.raises(P.PlussError):
+            ctx.fetch()
+        assert (k[2:].cpu() == 7).all()  # nothing written past `cap`
+        ctx.reset(stream)
+        if N % (CS * T):
+            return  # faithful mode needs N % (chunk*threads) == 0
+        # faithful counts already in the handle: the two-launch path folds them in
+        fa = P.expand_samples(c, 0x5EED0003, "B0", 0, 5000)
+        fbuf = torch.from_numpy(fa.view(np.int64)).cuda()
+        for x in (ctx, ref_ctx):
+            x.reset(stream)
+            x.faithful_hist("B0", fbuf.data_ptr(), len(fa), stream)
+        ref_ctx.sampled_hist(buf.data_ptr() + 8, total, stream)
+        ref_ctx.export_reset(rk.data_ptr(), rn.data_ptr(), 4096, stream)
+        k, n = tables()
+        ctx.sampled_hist_export(buf.data_ptr() + 8, total, k.data_ptr(), n.data_ptr(), 4096, stream)
+        torch.cuda.synchronize()
+        assert torch.equal(k, rk) and torch.equal(n, rn)
+        assert as_hist(k, n).total() == total + sum(P.sampled_hist(cfg(N, T, CS, mode="faithful"), fa).bins.values())
+        # and afterwards the one-launch path is used again
+        ctx.sampled_hist_export(buf.data_ptr() + 8, total, k.data_ptr(), n.data_ptr(), 4096, stream)
+        torch.cuda.synchronize()
+        assert as_hist(k, n).bins == want
+
+
 def test_long_windows_config4_t64(orc):
     """BASELINE config 4 shape (N=2048, T=64): long B reuse windows, share split and
     cold B samples in a thread's last row, checked against the closed forms."""

@@ -44,13 +44,25 @@ def main():
         variants += [dict(PLUSS_GRID=g) for g in ("512", "1792", "2048", "4096", "8192")]
         variants += [dict(PLUSS_ABLATE="2", PLUSS_GRID=g) for g in ("2048", "4096")]
         for v in variants:
-            for k in ("PLUSS_ABLATE", "PLUSS_UNROLL", "PLUSS_GRID"):
+            for k in ("PLUSS_ABLATE", "PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT"):
                 os.environ.pop(k, None)
             os.environ.update(v)
             ms = timeit(lambda: ctx.sampled_hist(buf.data_ptr(), total, s.cuda_stream), s)
             print(json.dumps({"samples": total, **v, "ms": ms, "GBps": 8 * total / ms / 1e6}), flush=True)
-        for k in ("PLUSS_ABLATE", "PLUSS_UNROLL", "PLUSS_GRID"):
+        for k in ("PLUSS_ABLATE", "PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT"):
             os.environ.pop(k, None)
+        keys = torch.empty(4096, dtype=torch.int64, device=dev)
+        cnts = torch.empty(4096, dtype=torch.int64, device=dev)
+        ms = timeit(lambda: ctx.sampled_hist_export(buf.data_ptr(), total, keys.data_ptr(), cnts.data_ptr(), 4096,
+                                                    s.cuda_stream), s)
+        print(json.dumps({"samples": total, "fused_count_export_ms": ms, "GBps": 8 * total / ms / 1e6}), flush=True)
+
+        def two():
+            ctx.sampled_hist(buf.data_ptr(), total, s.cuda_stream)
+            ctx.export_reset(keys.data_ptr(), cnts.data_ptr(), 4096, s.cuda_stream)
+        ms = timeit(two, s)
+        print(json.dumps({"samples": total, "count_then_export_reset_ms": ms, "GBps": 8 * total / ms / 1e6}),
+              flush=True)
         dst = torch.empty_like(buf)
         ms = timeit(lambda: dst.copy_(buf), s)
         print(json.dumps({"samples": total, "torch_copy_ms": ms, "GBps_rd+wr": 16 * total / ms / 1e6}), flush=True)
