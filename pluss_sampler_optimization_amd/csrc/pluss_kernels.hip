@@ -123,6 +123,7 @@ __device__ __forceinline__ uint32_t sample_bin(const Model& m, uint64_t x, bool 
 // Block-wide reduction of the per-lane bin counters; each bin with a count is
 // added to its direct counter in replica blockIdx % NREP (workgroups are
 // dealt round-robin over the 8 XCDs, so a replica is hit from one XCD).
+template <int PCS>
 __device__ __forceinline__ void bins_finish(unsigned int (*pc)[NBINS][64], GTable g) {
   __shared__ unsigned long long tot[NBINS];
   __syncthreads();
@@ -130,7 +131,7 @@ __device__ __forceinline__ void bins_finish(unsigned int (*pc)[NBINS][64], GTabl
   for (int b = wave; b < NBINS; b += BLOCK / 64) {
     unsigned long long v = 0;
 #pragma unroll
-    for (int w = 0; w < BLOCK / 64; ++w) v += pc[w][b][lane];
+    for (int w = 0; w < PCS; ++w) v += pc[w][b][lane];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     if (lane == 0) tot[b] = v;
@@ -157,7 +158,7 @@ __device__ void bins_export_tail(const Model& m, GTable g, unsigned long long* o
 #pragma unroll
     for (uint32_t r = 0; r < NREP; ++r) {
       c += __hip_atomic_load(&g.bins[r * BSTRIDE + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      g.bins[r * BSTRIDE + t] = 0;
+      __hip_atomic_store(&g.bins[r * BSTRIDE + t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     ek[t] = m.keytab[t];
     ec[t] = c;
@@ -201,7 +202,7 @@ __device__ void bins_export_tail(const Model& m, GTable g, unsigned long long* o
   if (t == 0) {
     *nout = n;
     if (n > cap) atomicOr(&g.flags[0], 2u);
-    g.flags[4] = 0;
+    __hip_atomic_store(&g.flags[4], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -214,7 +215,10 @@ struct ExportArgs {
   unsigned int* nout;
 };
 
-template <int MODE, int ABL = 0, int UNR = UNROLL, bool NT = false, bool FUSE = false>
+// PCS: sets of lane counters per workgroup (waves share a set: ds_add is
+// atomic and a wave's 64 lanes still hit 64 distinct banks), so LDS per
+// workgroup is PCS * 5 KiB.
+template <int MODE, int ABL = 0, int UNR = UNROLL, bool NT = false, bool FUSE = false, int PCS = 1>
 __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t* __restrict__ smp, uint64_t n,
                                                         const uint64_t* __restrict__ head, int has_head, GTable g,
                                                         ExportArgs ex) {
@@ -222,12 +226,12 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
   constexpr bool BINS = MODE != GENERIC;
   __shared__ unsigned long long tk[BINS ? 1 : TCAP];
   __shared__ unsigned int tc[BINS ? 1 : TCAP];
-  __shared__ unsigned int pc[BINS ? BLOCK / 64 : 1][NBINS][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ unsigned int pc[BINS ? PCS : 1][NBINS][64];
+  const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) % PCS;
   const BlockTable bt{tk, tc};
   WaveCache wc;
   if (BINS) {
-    for (int i = threadIdx.x; i < (BLOCK / 64) * NBINS * 64; i += BLOCK) (&pc[0][0][0])[i] = 0;
+    for (int i = threadIdx.x; i < PCS * NBINS * 64; i += BLOCK) (&pc[0][0][0])[i] = 0;
   } else {
     bt_init(bt);
     wc_init(wc);
@@ -318,18 +322,22 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
     if (sink == 0x5EED5EED5EED5EEDull) atomicOr(&g.flags[2], 1u);  // keeps the ablated work alive
     return;
   }
-  if (BINS) bins_finish(pc, g);
+  if (BINS) bins_finish<PCS>(pc, g);
   else bt_finish(wc, bt, g);
   if (FUSE) {
+    // Arrival count without fences: every bin update above is an agent-scope
+    // atomic RMW issued by wave 0 (threads 0..18), performed at the coherent
+    // point; once the wave's vmcnt drains they are visible to every XCD, and
+    // the last arriver reads them back with agent-scope atomic loads.  (A
+    // __threadfence here costs an L2 writeback + invalidate per workgroup,
+    // measured 4x the kernel's run time.)
     __shared__ unsigned int amlast;
-    __threadfence();  // this workgroup's bin atomics are ordered before its finish count
-    __syncthreads();
-    if (threadIdx.x == 0) amlast = atomicAdd(&g.flags[4], 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (amlast) {
-      __threadfence();
-      bins_export_tail(m, g, ex.keys, ex.counts, ex.cap, ex.nout);
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_s_waitcnt(0);
+      amlast = __hip_atomic_fetch_add(&g.flags[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     }
+    __syncthreads();
+    if (amlast) bins_export_tail(m, g, ex.keys, ex.counts, ex.cap, ex.nout);
   }
 }
 
@@ -342,12 +350,12 @@ __global__ __launch_bounds__(BLOCK) void k_fulltrace(Model m, GTable g) {
   constexpr bool BINS = MODE != GENERIC;
   __shared__ unsigned long long tk[BINS ? 1 : TCAP];
   __shared__ unsigned int tc[BINS ? 1 : TCAP];
-  __shared__ unsigned int pc[BINS ? BLOCK / 64 : 1][NBINS][64];
+  __shared__ unsigned int pc[BINS ? 1 : 1][NBINS][64];  // one counter set shared by the waves
   const BlockTable bt{tk, tc};
   WaveCache wc;
-  const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
+  const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6, cw = 0;
   if (BINS) {
-    for (int i = threadIdx.x; i < (BLOCK / 64) * NBINS * 64; i += BLOCK) (&pc[0][0][0])[i] = 0;
+    for (int i = threadIdx.x; i < NBINS * 64; i += BLOCK) (&pc[0][0][0])[i] = 0;
   } else {
     bt_init(bt);
     wc_init(wc);
@@ -358,13 +366,13 @@ __global__ __launch_bounds__(BLOCK) void k_fulltrace(Model m, GTable g) {
   for (uint64_t pr = (uint64_t)blockIdx.x * (BLOCK / 64) + wave; pr < npairs; pr += nwaves) {
     const uint32_t c0 = (uint32_t)(pr / m.N), c1 = (uint32_t)(pr - (uint64_t)c0 * m.N);
     if (BINS) {
-      if (lane < 2) atomicAdd(&pc[wave][lane * 3][lane], 1u);  // C0, C1: case 0
+      if (lane < 2) atomicAdd(&pc[cw][lane * 3][lane], 1u);  // C0, C1: case 0
       for (uint32_t c2b = 0; c2b < m.N; c2b += 64) {
         const uint32_t c2 = c2b + lane;
         if (c2 < m.N) {
 #pragma unroll
           for (uint32_t ref = A0; ref <= C3; ++ref)
-            atomicAdd(&pc[wave][bin_uniform<MODE == FAST_P2>(m, ref, c0, c1, c2)][lane], 1u);
+            atomicAdd(&pc[cw][bin_uniform<MODE == FAST_P2>(m, ref, c0, c1, c2)][lane], 1u);
         }
       }
     } else {
@@ -386,7 +394,7 @@ __global__ __launch_bounds__(BLOCK) void k_fulltrace(Model m, GTable g) {
       }
     }
   }
-  if (BINS) bins_finish(pc, g);
+  if (BINS) bins_finish<1>(pc, g);
   else bt_finish(wc, bt, g);
 }
 
@@ -585,18 +593,22 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
     PLUSS_HIP_CHECK(hipGetLastError());
     return PLUSS_OK;
   }
-  // diagnostics only (tools/ablate.py): PLUSS_ABLATE=1|2, PLUSS_UNROLL=1|4|8, PLUSS_NT=1, PLUSS_GRID=<blocks>
+  // diagnostics only (tools/ablate.py): PLUSS_ABLATE=1|2, PLUSS_UNROLL=1|4|8, PLUSS_NT=1, PLUSS_GRID=<blocks>,
+  // PLUSS_PCS=4 (a counter set per wave)
   const char* abl = getenv("PLUSS_ABLATE");
   const char* unr = getenv("PLUSS_UNROLL");
   const char* ntv = getenv("PLUSS_NT");
   const char* grd = getenv("PLUSS_GRID");
+  const char* pcs = getenv("PLUSS_PCS");
   if (grd && atoi(grd) > 0) nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL, atoi(grd));
   const int a = abl ? atoi(abl) : 0, u = unr ? atoi(unr) : UNROLL;
   const bool nt = ntv && ntv[0] == '1';
+  const bool pc4 = pcs && pcs[0] == '4';
   const ExportArgs ex{nullptr, nullptr, 0, nullptr};
   if (!m.fast) ctx->tables_dirty = true;
-  if (m.fast && m.p2 && (a || u != UNROLL || nt)) {
-    if (a == 1) PLUSS_LAUNCH_HOT(ex, FAST_P2, 1, UNROLL, false);
+  if (m.fast && m.p2 && (a || u != UNROLL || nt || pc4)) {
+    if (pc4) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, false, false, 4);
+    else if (a == 1) PLUSS_LAUNCH_HOT(ex, FAST_P2, 1, UNROLL, false);
     else if (a == 2) PLUSS_LAUNCH_HOT(ex, FAST_P2, 2, UNROLL, false);
     else if (u == 1) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, 1, false);
     else if (u == 4) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, 4, false);

@@ -40,16 +40,16 @@ def main():
         torch.cuda.synchronize()
         variants = [dict(PLUSS_ABLATE=m) for m in ("2", "1", "0")]
         variants += [dict(PLUSS_UNROLL=u) for u in ("1", "4", "8")]
-        variants += [dict(PLUSS_NT="1")]
-        variants += [dict(PLUSS_GRID=g) for g in ("512", "1792", "2048", "4096", "8192")]
+        variants += [dict(PLUSS_NT="1"), dict(PLUSS_PCS="4")]
+        variants += [dict(PLUSS_GRID=g) for g in ("512", "1792", "2048", "3072", "4096", "8192")]
         variants += [dict(PLUSS_ABLATE="2", PLUSS_GRID=g) for g in ("2048", "4096")]
         for v in variants:
-            for k in ("PLUSS_ABLATE", "PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT"):
+            for k in ("PLUSS_ABLATE", "PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT", "PLUSS_PCS"):
                 os.environ.pop(k, None)
             os.environ.update(v)
             ms = timeit(lambda: ctx.sampled_hist(buf.data_ptr(), total, s.cuda_stream), s)
             print(json.dumps({"samples": total, **v, "ms": ms, "GBps": 8 * total / ms / 1e6}), flush=True)
-        for k in ("PLUSS_ABLATE", "PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT"):
+        for k in ("PLUSS_ABLATE", "PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT", "PLUSS_PCS"):
             os.environ.pop(k, None)
         keys = torch.empty(4096, dtype=torch.int64, device=dev)
         cnts = torch.empty(4096, dtype=torch.int64, device=dev)
