@@ -148,8 +148,8 @@ int pluss_ctx_create(const pluss_cfg* cfg, pluss_ctx** out) {
     c->g.counts = base + GCAP + NREP * RCAP;
     c->g.rcounts = base + 2 * GCAP + NREP * RCAP;
     c->g.bins = base + 2 * (GCAP + NREP * RCAP);
-    c->g.flags = (unsigned int*)(c->g.bins + NREP * BSTRIDE);
-    c->g.trav = c->g.bins + NREP * BSTRIDE + 4;
+    c->g.flags = (unsigned int*)(c->g.bins + NBROW * BSTRIDE);
+    c->g.trav = c->g.bins + NBROW * BSTRIDE + 4;
   }
   if (hipMalloc((void**)&c->d_exp_keys, GCAP * 8) != hipSuccess) return fail("export");
   if (hipMalloc((void**)&c->d_exp_counts, GCAP * 8) != hipSuccess) return fail("export");

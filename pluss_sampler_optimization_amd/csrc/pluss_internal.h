@@ -19,11 +19,13 @@ constexpr int MAX_BLOCKS = 1024;       // 256 CUs x 4 workgroups
 constexpr int UNROLL = 2;              // 16-byte sample pairs per lane per step (tools/ablate.py)
 constexpr unsigned long long KEY_NONE = 0;  // free table slot (histogram keys are never 0)
 
-constexpr uint32_t BSTRIDE = 32;       // direct (ref, case) counters per replica (18 used; 256 B apart)
+constexpr uint32_t NBROW = 64;         // rows of direct (ref, case) counters (workgroup -> row blockIdx % 64)
+constexpr uint32_t BSTRIDE = 32;       // u64 per row: 18 counters, [BARRIVE] arrival count; rows 256 B apart
+constexpr uint32_t BARRIVE = 31;
 
 // Global histogram state (one per handle), one contiguous allocation so a
 // single memset resets it:
-//   keys[GCAP] rkeys[NREP*RCAP] counts[GCAP] rcounts[NREP*RCAP] bins[NREP*BSTRIDE] flags[8] trav[8]
+//   keys[GCAP] rkeys[NREP*RCAP] counts[GCAP] rcounts[NREP*RCAP] bins[NBROW*BSTRIDE] flags[8] trav[8]
 // FAST-mode kernels count into `bins` (18 fixed (ref, case) keys, Model::keytab);
 // arbitrary exact keys (GENERIC shapes, faithful mode) go to the open-addressing
 // replicas, spilling to the main table.
@@ -32,12 +34,12 @@ struct GTable {
   unsigned long long* rkeys;    // NREP * RCAP
   unsigned long long* counts;   // GCAP
   unsigned long long* rcounts;  // NREP * RCAP
-  unsigned long long* bins;     // NREP * BSTRIDE
+  unsigned long long* bins;     // NBROW * BSTRIDE
   unsigned int* flags;          // [0] overflow, [1] bad input, [2] diagnostics, [3] main table used,
-                                // [4] finished workgroups of a fused count+export launch
+                                // [4] finished bin rows of a fused count+export launch
   unsigned long long* trav;     // [6] per-ref traversed (faithful) / [0] total (full trace)
 };
-constexpr size_t TABLE_WORDS = 2 * (size_t)(GCAP + NREP * RCAP) + NREP * BSTRIDE + 4 + 8;
+constexpr size_t TABLE_WORDS = 2 * (size_t)(GCAP + NREP * RCAP) + NBROW * BSTRIDE + 4 + 8;
 constexpr size_t TABLE_BYTES = TABLE_WORDS * 8;
 
 struct FaithfulBufs {

@@ -121,8 +121,9 @@ __device__ __forceinline__ uint32_t sample_bin(const Model& m, uint64_t x, bool 
 }
 
 // Block-wide reduction of the per-lane bin counters; each bin with a count is
-// added to its direct counter in replica blockIdx % NREP (workgroups are
-// dealt round-robin over the 8 XCDs, so a replica is hit from one XCD).
+// added to its direct counter in row blockIdx % 64 (workgroups are dealt
+// round-robin over the 8 XCDs, so a row is hit from one XCD, by 1/64 of the
+// grid: 16 adds per address at 1024 workgroups).
 template <int PCS>
 __device__ __forceinline__ void bins_finish(unsigned int (*pc)[NBINS][64], GTable g) {
   __shared__ unsigned long long tot[NBINS];
@@ -138,7 +139,7 @@ __device__ __forceinline__ void bins_finish(unsigned int (*pc)[NBINS][64], GTabl
   }
   __syncthreads();
   if (threadIdx.x < 18 && tot[threadIdx.x])
-    atomicAdd(&g.bins[(blockIdx.x & (NREP - 1)) * BSTRIDE + threadIdx.x], tot[threadIdx.x]);
+    atomicAdd(&g.bins[(blockIdx.x & (NBROW - 1)) * BSTRIDE + threadIdx.x], tot[threadIdx.x]);
   if (threadIdx.x == BIN_BAD && tot[BIN_BAD]) atomicOr(&g.flags[1], 1u);
 }
 
@@ -154,16 +155,19 @@ __device__ void bins_export_tail(const Model& m, GTable g, unsigned long long* o
   const uint32_t t = threadIdx.x;
   if (t == 0) en = 0;
   if (t < 18) {
-    unsigned long long c = 0;
-#pragma unroll
-    for (uint32_t r = 0; r < NREP; ++r) {
-      c += __hip_atomic_load(&g.bins[r * BSTRIDE + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&g.bins[r * BSTRIDE + t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     ek[t] = m.keytab[t];
-    ec[t] = c;
+    ec[t] = 0;
   }
   if (t < 8) g.trav[t] = 0;
+  __syncthreads();
+  for (uint32_t i = t; i < NBROW * 18; i += BLOCK) {
+    unsigned long long* p = &g.bins[(i / 18) * BSTRIDE + i % 18];
+    const unsigned long long c = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c) {
+      atomicAdd(&ec[i % 18], c);
+      __hip_atomic_store(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   __syncthreads();
   unsigned long long key = 0, tot = 0;
   uint32_t rank = 0;
@@ -333,8 +337,20 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
     // measured 4x the kernel's run time.)
     __shared__ unsigned int amlast;
     if (threadIdx.x == 0) {
+      // two-level arrival (one counter per bin row, then one per grid) so
+      // the simultaneous finishes of ~1000 workgroups do not serialise on
+      // a single address
+      const uint32_t row = blockIdx.x & (NBROW - 1);
+      const uint32_t rows = gridDim.x < NBROW ? gridDim.x : NBROW;
+      const uint32_t in_row = (gridDim.x - row + NBROW - 1) / NBROW;
+      unsigned long long* rc = &g.bins[row * BSTRIDE + BARRIVE];
       __builtin_amdgcn_s_waitcnt(0);
-      amlast = __hip_atomic_fetch_add(&g.flags[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+      bool last = false;
+      if (__hip_atomic_fetch_add(rc, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_row - 1) {
+        __hip_atomic_store(rc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = __hip_atomic_fetch_add(&g.flags[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == rows - 1;
+      }
+      amlast = last;
     }
     __syncthreads();
     if (amlast) bins_export_tail(m, g, ex.keys, ex.counts, ex.cap, ex.nout);
@@ -457,11 +473,11 @@ __global__ __launch_bounds__(EXP_THREADS) void k_export(Model m, GTable g, unsig
       }
     }
   }
-  if (threadIdx.x < NREP * BSTRIDE) {  // direct (ref, case) bins of the FAST kernels
-    const uint32_t b = threadIdx.x % BSTRIDE;
-    const unsigned long long c = b < 18 ? g.bins[threadIdx.x] : 0ull;
+  for (uint32_t i = threadIdx.x; i < NBROW * BSTRIDE; i += EXP_THREADS) {  // direct (ref, case) bins
+    const uint32_t b = i % BSTRIDE;
+    const unsigned long long c = b < 18 ? g.bins[i] : 0ull;
     if (c && !lds_add<unsigned long long, GCAP>(sk, sc, m.keytab[b], c)) atomicOr(&full, 1u);
-    if (consume && c) g.bins[threadIdx.x] = 0;
+    if (consume && c) g.bins[i] = 0;
   }
   if (consume && threadIdx.x < 8) g.trav[threadIdx.x] = 0;
   __syncthreads();
