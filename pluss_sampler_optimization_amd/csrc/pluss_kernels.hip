@@ -120,6 +120,37 @@ __device__ __forceinline__ uint32_t sample_bin(const Model& m, uint64_t x, bool 
   return sample_bin_any<P2>(m, x, ok);
 }
 
+// Bins of the K samples a lane holds in one step.  The reference check and
+// the scalar branch are paid once for all K (a wave almost always holds one
+// reference: lists are per-reference blocks); a mixed step falls back to the
+// all-reference select chain.
+template <bool P2, int K>
+__device__ __forceinline__ void sample_bins(const Model& m, const uint64_t (&xs)[K], const bool (&ok)[K],
+                                            uint32_t (&bin)[K]) {
+  const uint32_t r0 = __builtin_amdgcn_readfirstlane((uint32_t)(xs[0] >> 60));
+  bool mixed = false;
+#pragma unroll
+  for (int k = 0; k < K; ++k) mixed |= ok[k] && (uint32_t)(xs[k] >> 60) != r0;
+  if (r0 <= 5 && __ballot(mixed) == 0) {
+    switch (r0) {  // scalar branch on the wave's reference
+#define PLUSS_BIN_CASE(R)                                                              \
+  case R:                                                                              \
+    _Pragma("unroll") for (int k = 0; k < K; ++k) bin[k] = sample_bin_ref<P2>(m, R, xs[k], ok[k]); \
+    return;
+      PLUSS_BIN_CASE(C3)
+      PLUSS_BIN_CASE(A0)
+      PLUSS_BIN_CASE(B0)
+#undef PLUSS_BIN_CASE
+      default:  // C0, C1, C2: case 0
+#pragma unroll
+        for (int k = 0; k < K; ++k) bin[k] = sample_bin_ref<P2>(m, r0, xs[k], ok[k]);
+        return;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) bin[k] = sample_bin_any<P2>(m, xs[k], ok[k]);
+}
+
 // Block-wide reduction of the per-lane bin counters; each bin with a count is
 // added to its direct counter in row blockIdx % 64 (workgroups are dealt
 // round-robin over the 8 XCDs, so a row is hit from one XCD, by 1/64 of the
@@ -160,12 +191,21 @@ __device__ void bins_export_tail(const Model& m, GTable g, unsigned long long* o
   }
   if (t < 8) g.trav[t] = 0;
   __syncthreads();
-  for (uint32_t i = t; i < NBROW * 18; i += BLOCK) {
-    unsigned long long* p = &g.bins[(i / 18) * BSTRIDE + i % 18];
-    const unsigned long long c = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (c) {
-      atomicAdd(&ec[i % 18], c);
-      __hip_atomic_store(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  constexpr uint32_t PER = (NBROW * 18 + BLOCK - 1) / BLOCK;
+  unsigned long long c[PER];
+#pragma unroll
+  for (uint32_t j = 0; j < PER; ++j) {  // every load in flight before the first is used
+    const uint32_t i = t + j * BLOCK;
+    c[j] = i < NBROW * 18
+               ? __hip_atomic_load(&g.bins[(i / 18) * BSTRIDE + i % 18], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+               : 0ull;
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < PER; ++j) {
+    const uint32_t i = t + j * BLOCK;
+    if (c[j]) {
+      atomicAdd(&ec[i % 18], c[j]);
+      __hip_atomic_store(&g.bins[(i / 18) * BSTRIDE + i % 18], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   __syncthreads();
@@ -272,6 +312,26 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
     for (int u = 0; u < UNR; ++u) {  // prefetch the next step
       const uint64_t i = nb + (uint64_t)u * BLOCK + threadIdx.x;
       y[u] = ld(i < last ? i : last);
+    }
+    if (BINS && ABL != 2) {  // all 2*UNR samples of the step binned under one reference check
+      uint64_t xs[2 * UNR];
+      bool oks[2 * UNR];
+      uint32_t bin[2 * UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        xs[2 * u] = x[u].x;
+        xs[2 * u + 1] = x[u].y;
+        oks[2 * u] = oks[2 * u + 1] = base + (uint64_t)u * BLOCK + threadIdx.x < npairs;
+      }
+      sample_bins<MODE == FAST_P2>(m, xs, oks, bin);
+#pragma unroll
+      for (int k = 0; k < 2 * UNR; ++k) {
+        if (ABL == 1) sink += bin[k] << (k & 7);
+        else atomicAdd(&pc[wave][bin[k]][lane], 1u);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) x[u] = y[u];
+      continue;
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
