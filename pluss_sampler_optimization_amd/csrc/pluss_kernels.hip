@@ -239,7 +239,25 @@ __device__ void bins_export_tail(const Model& m, GTable g, unsigned long long* o
     ok[rank] = key;
     oc[rank] = tot;
   }
-  for (uint64_t i = n + t; i < cap; i += BLOCK) {
+  uint64_t i0 = n < cap ? n : cap;
+  if (((((uintptr_t)ok) | ((uintptr_t)oc)) & 15u) == 0) {  // 16-byte stores for the empty pairs
+    if ((i0 & 1) && i0 < cap) {
+      if (t == 0) {
+        ok[i0] = KEY_EMPTY;
+        oc[i0] = 0ull;
+      }
+      ++i0;
+    }
+    const uint64_t np = (cap - i0) / 2;
+    ulonglong2* k2 = reinterpret_cast<ulonglong2*>(ok + i0);
+    ulonglong2* c2 = reinterpret_cast<ulonglong2*>(oc + i0);
+    for (uint64_t p = t; p < np; p += BLOCK) {
+      k2[p] = ulonglong2{KEY_EMPTY, KEY_EMPTY};
+      c2[p] = ulonglong2{0ull, 0ull};
+    }
+    i0 += 2 * np;
+  }
+  for (uint64_t i = i0 + t; i < cap; i += BLOCK) {
     ok[i] = KEY_EMPTY;
     oc[i] = 0ull;
   }
@@ -663,14 +681,8 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
 #define PLUSS_LAUNCH_HOT(EX, ...)                                                                                  \
   hipLaunchKernelGGL((k_sampled_hist<__VA_ARGS__>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n, head, has_head, g, \
                      EX)
-  if (fuse) {
-    if (m.p2) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, UNROLL, false, true);
-    else PLUSS_LAUNCH_HOT(*fuse, FAST, 0, UNROLL, false, true);
-    PLUSS_HIP_CHECK(hipGetLastError());
-    return PLUSS_OK;
-  }
-  // diagnostics only (tools/ablate.py): PLUSS_ABLATE=1|2, PLUSS_UNROLL=1|4|8, PLUSS_NT=1, PLUSS_GRID=<blocks>,
-  // PLUSS_PCS=4 (a counter set per wave)
+  // diagnostics only (tools/ablate.py): PLUSS_ABLATE=1|2, PLUSS_UNROLL=1|4|8, PLUSS_NT=0|1, PLUSS_GRID=<blocks>,
+  // PLUSS_PCS=4 (a counter set per wave); the fused launch honours UNROLL=1|2, NT and GRID
   const char* abl = getenv("PLUSS_ABLATE");
   const char* unr = getenv("PLUSS_UNROLL");
   const char* ntv = getenv("PLUSS_NT");
@@ -678,22 +690,31 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
   const char* pcs = getenv("PLUSS_PCS");
   if (grd && atoi(grd) > 0) nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL, atoi(grd));
   const int a = abl ? atoi(abl) : 0, u = unr ? atoi(unr) : UNROLL;
-  const bool nt = ntv && ntv[0] == '1';
+  const bool nt = ntv ? ntv[0] == '1' : HOT_NT;
   const bool pc4 = pcs && pcs[0] == '4';
+  if (fuse) {
+    if (m.p2 && u == 1 && nt) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, 1, true, true);
+    else if (m.p2 && u == 1) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, 1, false, true);
+    else if (m.p2 && nt) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, UNROLL, true, true);
+    else if (m.p2) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, UNROLL, false, true);
+    else PLUSS_LAUNCH_HOT(*fuse, FAST, 0, UNROLL, HOT_NT, true);
+    PLUSS_HIP_CHECK(hipGetLastError());
+    return PLUSS_OK;
+  }
   const ExportArgs ex{nullptr, nullptr, 0, nullptr};
   if (!m.fast) ctx->tables_dirty = true;
-  if (m.fast && m.p2 && (a || u != UNROLL || nt || pc4)) {
+  if (m.fast && m.p2 && (a || u != UNROLL || nt != HOT_NT || pc4)) {
     if (pc4) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, false, false, 4);
     else if (a == 1) PLUSS_LAUNCH_HOT(ex, FAST_P2, 1, UNROLL, false);
     else if (a == 2) PLUSS_LAUNCH_HOT(ex, FAST_P2, 2, UNROLL, false);
     else if (u == 1) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, 1, false);
     else if (u == 4) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, 4, false);
     else if (u == 8) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, 8, false);
-    else PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, true);
+    else PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, !HOT_NT);
   } else if (m.fast && m.p2) {
-    PLUSS_LAUNCH_HOT(ex, FAST_P2);
+    PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, HOT_NT);
   } else if (m.fast) {
-    PLUSS_LAUNCH_HOT(ex, FAST);
+    PLUSS_LAUNCH_HOT(ex, FAST, 0, UNROLL, HOT_NT);
   } else {
     PLUSS_LAUNCH_HOT(ex, GENERIC);
   }

@@ -240,6 +240,10 @@ def test_fused_count_and_export(orc, N, T, CS):
                 else:
                     assert as_hist(k, n).total() == total + 1
         assert ctx.fetch().bins == {}
+        k, n = tables()  # an output table that is only 8-byte aligned
+        ctx.sampled_hist_export(buf.data_ptr() + 8, total, k.data_ptr() + 8, n.data_ptr() + 8, 4095, stream)
+        torch.cuda.synchronize()
+        assert torch.equal(k[1:], rk[:4095]) and torch.equal(n[1:], rn[:4095]) and int(k[0]) == 7
         k, n = tables()
         ctx.sampled_hist_export(buf.data_ptr(), 0, k.data_ptr(), n.data_ptr(), 4096, stream)
         torch.cuda.synchronize()

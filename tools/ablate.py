@@ -53,9 +53,19 @@ def main():
             os.environ.pop(k, None)
         keys = torch.empty(4096, dtype=torch.int64, device=dev)
         cnts = torch.empty(4096, dtype=torch.int64, device=dev)
-        ms = timeit(lambda: ctx.sampled_hist_export(buf.data_ptr(), total, keys.data_ptr(), cnts.data_ptr(), 4096,
-                                                    s.cuda_stream), s)
-        print(json.dumps({"samples": total, "fused_count_export_ms": ms, "GBps": 8 * total / ms / 1e6}), flush=True)
+        fused = [{}, dict(PLUSS_NT="1"), dict(PLUSS_UNROLL="1"), dict(PLUSS_UNROLL="1", PLUSS_NT="1")]
+        fused += [dict(PLUSS_GRID=g, **kv) for g in ("384", "512", "768") for kv in ({}, dict(PLUSS_NT="1"))]
+        fused += [dict(PLUSS_GRID=g, PLUSS_UNROLL="1", PLUSS_NT="1") for g in ("512", "1536", "2048")]
+        for v in fused:
+            for k in ("PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT"):
+                os.environ.pop(k, None)
+            os.environ.update(v)
+            ms = timeit(lambda: ctx.sampled_hist_export(buf.data_ptr(), total, keys.data_ptr(), cnts.data_ptr(), 4096,
+                                                        s.cuda_stream), s)
+            print(json.dumps({"samples": total, "fused": v, "fused_count_export_ms": ms, "GBps": 8 * total / ms / 1e6}),
+                  flush=True)
+        for k in ("PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT"):
+            os.environ.pop(k, None)
 
         def two():
             ctx.sampled_hist(buf.data_ptr(), total, s.cuda_stream)
