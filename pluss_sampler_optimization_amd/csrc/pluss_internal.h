@@ -17,7 +17,7 @@ constexpr uint32_t NREP = 8;           // global replica tables (one per XCD-siz
 constexpr uint32_t RCAP = 256;         // slots per replica (power of two)
 constexpr int MAX_BLOCKS = 1024;       // 256 CUs x 4 workgroups
 constexpr int UNROLL = 2;              // 16-byte sample pairs per lane per step (tools/ablate.py)
-constexpr bool HOT_NT = false;         // non-temporal sample loads (tools/ablate.py)
+constexpr bool HOT_NT = true;          // non-temporal sample loads: streamed once (tools/ablate.py, r01k)
 constexpr unsigned long long KEY_NONE = 0;  // free table slot (histogram keys are never 0)
 
 constexpr uint32_t NBROW = 64;         // rows of direct (ref, case) counters (workgroup -> row blockIdx % 64)

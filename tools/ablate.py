@@ -1,4 +1,4 @@
-"""Split the hot kernel's time (diagnostics): PLUSS_ABLATE=2 loads only,
+"""Split the hot kernel's time (diagnostics; defaults: UNROLL=2, NT=1, grid 1024): PLUSS_ABLATE=2 loads only,
 =1 loads + key computation, 0 = product kernel.  Also a torch copy for a
 bandwidth reference.  Prints one JSON line per variant."""
 import json
@@ -40,7 +40,7 @@ def main():
         torch.cuda.synchronize()
         variants = [dict(PLUSS_ABLATE=m) for m in ("2", "1", "0")]
         variants += [dict(PLUSS_UNROLL=u) for u in ("1", "4", "8")]
-        variants += [dict(PLUSS_NT="1"), dict(PLUSS_PCS="4")]
+        variants += [dict(PLUSS_NT="0"), dict(PLUSS_PCS="4")]
         variants += [dict(PLUSS_GRID=g) for g in ("512", "1792", "2048", "3072", "4096", "8192")]
         variants += [dict(PLUSS_ABLATE="2", PLUSS_GRID=g) for g in ("2048", "4096")]
         for v in variants:
@@ -53,9 +53,7 @@ def main():
             os.environ.pop(k, None)
         keys = torch.empty(4096, dtype=torch.int64, device=dev)
         cnts = torch.empty(4096, dtype=torch.int64, device=dev)
-        fused = [{}, dict(PLUSS_NT="1"), dict(PLUSS_UNROLL="1"), dict(PLUSS_UNROLL="1", PLUSS_NT="1")]
-        fused += [dict(PLUSS_GRID=g, **kv) for g in ("384", "512", "768") for kv in ({}, dict(PLUSS_NT="1"))]
-        fused += [dict(PLUSS_GRID=g, PLUSS_UNROLL="1", PLUSS_NT="1") for g in ("512", "1536", "2048")]
+        fused = [{}, dict(PLUSS_NT="0"), dict(PLUSS_UNROLL="1"), dict(PLUSS_GRID="768")]
         for v in fused:
             for k in ("PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT"):
                 os.environ.pop(k, None)
