@@ -125,6 +125,44 @@ int pluss_dev_hist_export_reset(pluss_ctx *ctx, uint64_t *d_keys, uint64_t *d_co
    counts (the last workgroup to finish writes the table) */
 int pluss_dev_sampled_hist_export(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t n, uint64_t *d_keys,
                                   uint64_t *d_counts, uint64_t cap, void *stream);
+/* --- faithful mode over key-range shards (multi-GPU) ----------------------
+   One r10 sampler_<REF> (r10:135-696 and its five twins) split over ranks by
+   contiguous ranges of its sort key a*T+tid (pluss_utils.h:175-267 order).
+   Every rank passes the WHOLE per-reference sample list; each keeps the
+   samples whose key lies in its [key_lo, key_hi) and sorts only those.  The
+   library holds no communicator: between phases the caller exchanges the
+   small pluss_faith_shard summaries of all ranks (one all-gather each):
+
+     1 keys    -> n, first_key, max_sink
+                  j_off   = sum of n over earlier ranks, n_total = sum of all n,
+                  pmax_in = max of max_sink over earlier ranks with n > 0 (0 if none)
+     2 starts  -> n_starts;  s_off = sum of n_starts over earlier ranks
+     3 cut     -> cut;       cut = min over ranks
+     4 hist    (next_first_key = first_key of the next rank with n > 0, ~0 if
+                none; is_last = no later rank has n > 0) accumulates this
+                shard's part into the handle's histogram; then export and merge
+                the tables like clean mode.  The merged histogram and the sum of
+                `traversed` equal one pluss_dev_faithful_hist over the list.
+   Needs N % (chunk*threads) == 0 like pluss_dev_faithful_hist.             */
+typedef struct pluss_faith_shard {
+  uint64_t n;         /* phase 1: samples whose key is in [key_lo, key_hi) */
+  uint64_t first_key; /* phase 1: smallest key (~0 if n == 0) */
+  uint64_t max_sink;  /* phase 1: largest sink key (~0 if one is cold, 0 if n == 0) */
+  uint64_t n_starts;  /* phase 2: replay starts in this shard */
+  uint64_t cut;       /* phase 3: first Q1 cut candidate (global index), n_total if none */
+} pluss_faith_shard;
+
+/* keys of this shape lie in [0, *key_end) (= accesses per thread * threads) */
+int pluss_faithful_key_space(const pluss_cfg *cfg, uint64_t *key_end);
+int pluss_dev_faithful_shard_keys(pluss_ctx *ctx, int32_t ref, const uint64_t *d_samples, uint64_t n,
+                                  uint64_t key_lo, uint64_t key_hi, pluss_faith_shard *out, void *stream);
+int pluss_dev_faithful_shard_starts(pluss_ctx *ctx, uint64_t j_off, uint64_t pmax_in, pluss_faith_shard *out,
+                                    void *stream);
+int pluss_dev_faithful_shard_cut(pluss_ctx *ctx, uint64_t s_off, uint64_t n_total, pluss_faith_shard *out,
+                                 void *stream);
+int pluss_dev_faithful_shard_hist(pluss_ctx *ctx, uint64_t cut, uint64_t next_first_key, int32_t is_last,
+                                  void *stream);
+
 /* synchronise and copy the handle's histogram into a host pluss_hist */
 int pluss_hist_fetch(pluss_ctx *ctx, pluss_hist *out);
 /* merge canonical (key,count) tables on the host into a pluss_hist */

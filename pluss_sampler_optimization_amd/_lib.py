@@ -21,7 +21,9 @@ EXPORTS = [
     "pluss_default_counts",
     "pluss_ctx_create", "pluss_ctx_destroy", "pluss_ctx_stream", "pluss_dev_expand", "pluss_dev_hist_reset",
     "pluss_dev_sampled_hist", "pluss_dev_faithful_hist", "pluss_dev_fulltrace_hist", "pluss_dev_sampled_ri",
-    "pluss_dev_hist_export", "pluss_dev_hist_export_reset", "pluss_dev_sampled_hist_export", "pluss_hist_fetch", "pluss_hist_from_tables",
+    "pluss_dev_hist_export", "pluss_dev_hist_export_reset", "pluss_dev_sampled_hist_export", "pluss_hist_fetch",
+    "pluss_hist_from_tables", "pluss_faithful_key_space", "pluss_dev_faithful_shard_keys",
+    "pluss_dev_faithful_shard_starts", "pluss_dev_faithful_shard_cut", "pluss_dev_faithful_shard_hist",
 ]
 
 
@@ -39,6 +41,11 @@ class PlussHistEntry(ctypes.Structure):
 class PlussHist(ctypes.Structure):
     _fields_ = [("entries", ctypes.POINTER(PlussHistEntry)), ("capacity", ctypes.c_uint64),
                 ("n_entries", ctypes.c_uint64), ("traversed", ctypes.c_uint64 * 6)]
+
+
+class PlussFaithShard(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("first_key", ctypes.c_uint64), ("max_sink", ctypes.c_uint64),
+                ("n_starts", ctypes.c_uint64), ("cut", ctypes.c_uint64)]
 
 
 class PlussError(RuntimeError):
@@ -93,6 +100,11 @@ def lib():
         "pluss_dev_sampled_hist_export": (ctypes.c_int, [vp, vp, u64, vp, vp, u64, vp]),
         "pluss_hist_fetch": (ctypes.c_int, [vp, histp]),
         "pluss_hist_from_tables": (ctypes.c_int, [vp, vp, u64, histp]),
+        "pluss_faithful_key_space": (ctypes.c_int, [cfgp, P(u64)]),
+        "pluss_dev_faithful_shard_keys": (ctypes.c_int, [vp, i32, vp, u64, u64, u64, P(PlussFaithShard), vp]),
+        "pluss_dev_faithful_shard_starts": (ctypes.c_int, [vp, u64, u64, P(PlussFaithShard), vp]),
+        "pluss_dev_faithful_shard_cut": (ctypes.c_int, [vp, u64, u64, P(PlussFaithShard), vp]),
+        "pluss_dev_faithful_shard_hist": (ctypes.c_int, [vp, u64, u64, i32, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -16,7 +16,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import PlussCfg, PlussHist, PlussHistEntry, check, lib
+from ._lib import PlussCfg, PlussFaithShard, PlussHist, PlussHistEntry, check, lib
 
 REFS = ["C0", "C1", "A0", "B0", "C2", "C3"]
 REF_ID = {r: i for i, r in enumerate(REFS)}
@@ -165,6 +165,13 @@ def default_counts(n, total):
     return [int(x) for x in counts]
 
 
+def faithful_key_space(cfg):
+    """Faithful-mode sort keys a*T+tid of this shape lie in [0, key_space)."""
+    out = ctypes.c_uint64()
+    check(lib().pluss_faithful_key_space(ctypes.byref(cfg.to_c()), ctypes.byref(out)), "pluss_faithful_key_space")
+    return int(out.value)
+
+
 def hist_from_tables(keys, counts):
     k, kp = _u64(keys)
     c, cp = _u64(counts)
@@ -234,6 +241,35 @@ class Context:
         """sampled_hist() then export_reset() -- one launch for N % (CLS/DS) == 0 shapes."""
         check(lib().pluss_dev_sampled_hist_export(self._h, d_samples, n, d_keys, d_counts, cap, stream),
               "pluss_dev_sampled_hist_export")
+
+    # faithful mode over key-range shards: the four phases of
+    # pluss_dev_faithful_shard_* (the caller exchanges the summaries; see dist.py)
+    def faithful_shard_keys(self, ref, d_samples, n, key_lo, key_hi, stream=None):
+        """Phase 1 -> (n, first_key, max_sink) of the samples with key in [key_lo, key_hi)."""
+        rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
+        o = PlussFaithShard()
+        check(lib().pluss_dev_faithful_shard_keys(self._h, rid, d_samples, n, key_lo, key_hi, ctypes.byref(o), stream),
+              "pluss_dev_faithful_shard_keys")
+        return int(o.n), int(o.first_key), int(o.max_sink)
+
+    def faithful_shard_starts(self, j_off, pmax_in, stream=None):
+        """Phase 2 -> number of replay starts in this shard."""
+        o = PlussFaithShard()
+        check(lib().pluss_dev_faithful_shard_starts(self._h, j_off, pmax_in, ctypes.byref(o), stream),
+              "pluss_dev_faithful_shard_starts")
+        return int(o.n_starts)
+
+    def faithful_shard_cut(self, s_off, n_total, stream=None):
+        """Phase 3 -> this shard's first Q1 cut candidate (global index; n_total if none)."""
+        o = PlussFaithShard()
+        check(lib().pluss_dev_faithful_shard_cut(self._h, s_off, n_total, ctypes.byref(o), stream),
+              "pluss_dev_faithful_shard_cut")
+        return int(o.cut)
+
+    def faithful_shard_hist(self, cut, next_first_key, is_last, stream=None):
+        """Phase 4: accumulate this shard's part of the sampler's histogram."""
+        check(lib().pluss_dev_faithful_shard_hist(self._h, cut, next_first_key, 1 if is_last else 0, stream),
+              "pluss_dev_faithful_shard_hist")
 
     def fetch(self):
         h, keep = _hist_buf()

@@ -232,6 +232,42 @@ int pluss_dev_sampled_hist_export(pluss_ctx* ctx, const uint64_t* d_samples, uin
                                     cap, pick(ctx, stream));
 }
 
+int pluss_faithful_key_space(const pluss_cfg* cfg, uint64_t* key_end) {
+  Model m;
+  if (!key_end) return PLUSS_ERR_CONFIG;
+  if (int rc = validate_cfg(cfg, &m)) return rc;
+  if (m.A == 0) {
+    set_error("faithful mode needs N % (chunk*threads) == 0 (lockstep interleaving order)");
+    return PLUSS_ERR_CONFIG;
+  }
+  *key_end = m.A * m.T;
+  return PLUSS_OK;
+}
+
+int pluss_dev_faithful_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, uint64_t key_lo,
+                                  uint64_t key_hi, pluss_faith_shard* out, void* stream) {
+  if (!ctx || !out || (!d_samples && n) || ref < 0 || ref > 5 || key_lo > key_hi) return PLUSS_ERR_CONFIG;
+  return faith_shard_keys(ctx, ref, d_samples, n, key_lo, key_hi, out, pick(ctx, stream));
+}
+
+int pluss_dev_faithful_shard_starts(pluss_ctx* ctx, uint64_t j_off, uint64_t pmax_in, pluss_faith_shard* out,
+                                    void* stream) {
+  if (!ctx || !out) return PLUSS_ERR_CONFIG;
+  return faith_shard_starts(ctx, j_off, pmax_in, out, pick(ctx, stream));
+}
+
+int pluss_dev_faithful_shard_cut(pluss_ctx* ctx, uint64_t s_off, uint64_t n_total, pluss_faith_shard* out,
+                                 void* stream) {
+  if (!ctx || !out) return PLUSS_ERR_CONFIG;
+  return faith_shard_cut(ctx, s_off, n_total, out, pick(ctx, stream));
+}
+
+int pluss_dev_faithful_shard_hist(pluss_ctx* ctx, uint64_t cut, uint64_t next_first_key, int32_t is_last,
+                                  void* stream) {
+  if (!ctx) return PLUSS_ERR_CONFIG;
+  return faith_shard_hist(ctx, cut, next_first_key, is_last, pick(ctx, stream));
+}
+
 int pluss_hist_fetch(pluss_ctx* ctx, pluss_hist* out) {
   if (!ctx || !out) return PLUSS_ERR_CONFIG;
   hipStream_t s = ctx->last ? ctx->last : ctx->stream;

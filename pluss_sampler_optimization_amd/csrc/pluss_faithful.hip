@@ -30,57 +30,114 @@
 
 namespace pluss {
 
+// Key and sink of every sample.  cnt == nullptr: sample i -> slot i (one
+// GPU).  Otherwise only samples with key in [lo, hi) are kept, compacted
+// through a wave-aggregated counter (their order is irrelevant: they are
+// sorted next).
 template <bool FAST>
 __global__ __launch_bounds__(BLOCK) void k_faith_keys(Model m, uint32_t ref, const uint64_t* __restrict__ smp,
-                                                      uint64_t n, unsigned long long* __restrict__ keys,
-                                                      unsigned long long* __restrict__ sinks, GTable g) {
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
-    const Sample s = unpack(smp[i]);
-    if (s.ref != ref || s.c0 >= m.N || s.c1 >= m.N || s.c2 >= m.N) {
-      atomicOr(&g.flags[1], 1u);
-      keys[i] = KEY_EMPTY;
-      sinks[i] = KEY_EMPTY;
+                                                      uint64_t n, uint64_t lo, uint64_t hi,
+                                                      unsigned long long* __restrict__ keys,
+                                                      unsigned long long* __restrict__ sinks, unsigned long long* cnt,
+                                                      GTable g) {
+  const uint64_t step = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t base = (uint64_t)blockIdx.x * BLOCK; base < n; base += step) {
+    const uint64_t i = base + threadIdx.x;
+    unsigned long long key = KEY_EMPTY, sink = KEY_EMPTY;
+    bool keep = false;
+    if (i < n) {
+      const Sample s = unpack(smp[i]);
+      if (s.ref != ref || s.c0 >= m.N || s.c1 >= m.N || s.c2 >= m.N) {
+        atomicOr(&g.flags[1], 1u);
+        keep = cnt == nullptr;  // one GPU: the slot still has to be filled
+      } else {
+        const uint32_t c2 = (ref == C0 || ref == C1) ? 0u : s.c2;
+        const int64_t ri = ri_of<FAST>(m, ref, s.c0, s.c1, c2);
+        uint64_t P;
+        uint32_t t;
+        position(m, ref, s.c0, s.c1, c2, &P, &t);
+        key = P * m.T + t;
+        sink = ri < 0 ? KEY_EMPTY : (P + (uint64_t)ri) * m.T + t;
+        keep = cnt == nullptr || (key >= lo && key < hi);
+      }
+    }
+    if (cnt == nullptr) {
+      if (i < n) {
+        keys[i] = key;
+        sinks[i] = sink;
+      }
       continue;
     }
-    const uint32_t c2 = (ref == C0 || ref == C1) ? 0u : s.c2;
-    const int64_t ri = ri_of<FAST>(m, ref, s.c0, s.c1, c2);
-    uint64_t P;
-    uint32_t t;
-    position(m, ref, s.c0, s.c1, c2, &P, &t);
-    keys[i] = P * m.T + t;
-    sinks[i] = ri < 0 ? KEY_EMPTY : (P + (uint64_t)ri) * m.T + t;
+    const unsigned long long mask = __ballot(keep);
+    if (!mask) continue;
+    unsigned long long at = 0;
+    if (__lane_id() == (uint32_t)(__ffsll((long long)mask) - 1)) at = atomicAdd(cnt, (unsigned long long)__popcll(mask));
+    at = __shfl(at, __ffsll((long long)mask) - 1, 64);
+    if (keep) {
+      const uint64_t o = at + __popcll(mask & ((1ull << __lane_id()) - 1));
+      keys[o] = key;
+      sinks[o] = sink;
+    }
   }
 }
 
-__global__ void k_faith_init(unsigned long long* scal, uint64_t n) {
-  scal[0] = n;  // cut
-  scal[1] = 0;  // cold (tid 0)
-  scal[2] = 0;  // traversed (mod 2^64)
+// scal: [0] cut, [1] cold (tid 0), [2] traversed (mod 2^64), [3] shard size
+__global__ void k_faith_init(unsigned long long* scal, uint64_t cut) {
+  scal[0] = cut;
+  scal[1] = 0;
+  scal[2] = 0;
+}
+
+// Global prefix max at local i of a shard = max(pmax_in, local pmax_i);
+// pmax_in = largest sink of every earlier shard (0 if none).
+__device__ __forceinline__ unsigned long long gmax(const unsigned long long* pmax, uint64_t i,
+                                                   unsigned long long pmax_in) {
+  const unsigned long long v = pmax[i];
+  return v > pmax_in ? v : pmax_in;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_faith_flags(const unsigned long long* __restrict__ keys,
                                                        const unsigned long long* __restrict__ pmax, uint64_t n,
+                                                       uint64_t j_off, unsigned long long pmax_in,
                                                        unsigned int* __restrict__ flags) {
-  for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (uint64_t)gridDim.x * BLOCK)
-    flags[j] = (j == 0 || keys[j] > pmax[j - 1]) ? 1u : 0u;
-}
-
-__global__ __launch_bounds__(BLOCK) void k_faith_cut(const unsigned int* __restrict__ flags,
-                                                     const unsigned int* __restrict__ nstart, uint64_t n,
-                                                     unsigned long long* scal) {
-  for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (uint64_t)gridDim.x * BLOCK) {
-    if (j > 0 && flags[j]) {
-      const uint64_t met = j - ((uint64_t)nstart[j] - 1);  // samples met before this START
-      if (met >= n - j) atomicMin(&scal[0], (unsigned long long)j);
-    }
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
+    const unsigned long long before = i == 0 ? pmax_in : gmax(pmax, i - 1, pmax_in);
+    flags[i] = (j_off + i == 0 || keys[i] > before) ? 1u : 0u;
   }
 }
 
+// Q1: the first START j > 0 (global index) whose met-sample count
+// j - starts_before_j reaches the number of samples left, n_total - j.
+__global__ __launch_bounds__(BLOCK) void k_faith_cut(const unsigned int* __restrict__ flags,
+                                                     const unsigned int* __restrict__ nstart, uint64_t n,
+                                                     uint64_t j_off, uint64_t s_off, uint64_t n_total,
+                                                     unsigned long long* scal) {
+  unsigned long long best = KEY_EMPTY;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
+    const uint64_t j = j_off + i;
+    if (j > 0 && flags[i]) {
+      const uint64_t met = j - (s_off + (uint64_t)nstart[i] - 1);  // samples met before this START
+      if (met >= n_total - j && j < best) best = j;
+    }
+  }
+  // one atomic per wave instead of one per qualifying sample
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long x = __shfl_xor(best, o, 64);
+    best = x < best ? x : best;
+  }
+  if (__lane_id() == 0 && best != KEY_EMPTY) atomicMin(&scal[0], best);
+}
+
+// Record the shard's samples with global index < cut: RI bins, tid-0 cold
+// samples, and the traversed contributions of the replays that start or end
+// here (a replay ends at j when j + 1 == cut or j + 1 starts one; for the
+// shard's last sample that is `next_start`, decided by the caller).
 template <bool FAST>
 __global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, const unsigned long long* __restrict__ keys,
                                                       const unsigned long long* __restrict__ sinks,
                                                       const unsigned long long* __restrict__ pmax,
                                                       const unsigned int* __restrict__ flags, uint64_t n,
+                                                      uint64_t j_off, unsigned long long pmax_in, int next_start,
                                                       unsigned long long* scal, GTable g) {
   __shared__ unsigned long long tk[TCAP];
   __shared__ unsigned int tc[TCAP];
@@ -92,16 +149,17 @@ __global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, con
   if (threadIdx.x == 0) red[0] = red[1] = 0;
   __syncthreads();
   const uint64_t cut = scal[0];
+  const uint64_t lim = cut > j_off ? (cut - j_off < n ? cut - j_off : n) : 0;  // local samples recorded
   const uint64_t endkey = m.A * m.T;
   unsigned long long cold = 0, trav = 0;
   const uint64_t step = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t base = (uint64_t)blockIdx.x * BLOCK; base < cut; base += step) {
-    const uint64_t j = base + threadIdx.x;
-    const bool v = j < cut;
+  for (uint64_t base = (uint64_t)blockIdx.x * BLOCK; base < lim; base += step) {
+    const uint64_t i = base + threadIdx.x;
+    const bool v = i < lim;
     uint64_t key = KEY_NONE;
     bool rec = false;
     if (v) {
-      const unsigned long long k = keys[j], s = sinks[j];
+      const unsigned long long k = keys[i], s = sinks[i];
       if (s == KEY_EMPTY) {
         cold += (k % m.T == 0) ? 1u : 0u;
       } else {
@@ -109,8 +167,12 @@ __global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, con
         key = make_key(ref, share_kind(m, ref, ri), ri);
         rec = true;
       }
-      if (flags[j]) trav -= k;
-      if (j + 1 == cut || flags[j + 1]) trav += (pmax[j] == KEY_EMPTY) ? endkey : pmax[j];
+      if (flags[i]) trav -= k;
+      const bool ends = j_off + i + 1 == cut || (i + 1 < n ? flags[i + 1] != 0 : next_start != 0);
+      if (ends) {
+        const unsigned long long gm = gmax(pmax, i, pmax_in);
+        trav += (gm == KEY_EMPTY) ? endkey : gm;
+      }
     }
     wave_count(wc, bt, g, key, rec);
   }
@@ -124,12 +186,18 @@ __global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, con
   }
 }
 
-__global__ void k_faith_finish(Model m, uint32_t ref, uint64_t n, const unsigned long long* pmax,
+// Q3 (only on the shard holding the global last sample, with nothing
+// dropped): the owner of the final largest sink stays in LAT; +1 cold if it
+// is tid 0.  Every shard materialises key -1 (r10:671), possibly with 0.
+__global__ void k_faith_finish(Model m, uint32_t ref, uint64_t n, uint64_t n_total, int is_last,
+                               unsigned long long pmax_in, const unsigned long long* pmax,
                                const unsigned long long* scal, GTable g) {
   unsigned long long cold = scal[1];
-  const uint64_t cut = scal[0];
-  if (n > 0 && cut == n && pmax[n - 1] != KEY_EMPTY && (pmax[n - 1] % m.T) == 0) cold += 1;  // Q3
-  g_add(g, make_key(ref, 0, -1), cold);  // the reference always materialises key -1 (r10:671)
+  if (is_last && n > 0 && scal[0] == n_total) {
+    const unsigned long long gm = gmax(pmax, n - 1, pmax_in);
+    if (gm != KEY_EMPTY && gm % m.T == 0) cold += 1;
+  }
+  g_add(g, make_key(ref, 0, -1), cold);
   g.trav[ref] += scal[2];
 }
 
@@ -144,18 +212,31 @@ static int grow(T** p, uint64_t n) {
   return PLUSS_OK;
 }
 
-int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s) {
-  const Model& m = ctx->m;
+static int faith_check_shape(const pluss_ctx* ctx) {
   if ((uint64_t)ctx->cfg.n % ((uint64_t)ctx->cfg.chunk * (uint64_t)ctx->cfg.threads) != 0) {
     set_error("faithful mode needs N % (chunk*threads) == 0 (lockstep interleaving order)");
     return PLUSS_ERR_CONFIG;
   }
+  return PLUSS_OK;
+}
+
+static unsigned key_bits(const Model& m) {  // keys < A*T: sort only the significant bits
+  unsigned end_bit = 1;
+  while (end_bit < 64 && (m.A * m.T) >> end_bit) ++end_bit;
+  return end_bit;
+}
+
+static int grid_of(uint64_t n) {
+  const uint64_t b = (n + BLOCK * 4 - 1) / (BLOCK * 4);
+  return b < 1 ? 1 : (b > (uint64_t)MAX_BLOCKS ? MAX_BLOCKS : (int)b);
+}
+
+// buffers for n samples (keys, sinks, sorted copies, prefix max, flags, scan)
+static int faith_reserve(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
   FaithfulBufs& b = ctx->fb;
   if (!b.scal) {
     if (int rc = grow(&b.scal, 4)) return rc;
   }
-  if (n == 0) return PLUSS_OK;
-  ctx->tables_dirty = true;
   if (n > 0xFFFFFFFFull) {
     set_error("faithful mode: at most 2^32-1 samples per reference");
     return PLUSS_ERR_CONFIG;
@@ -168,14 +249,17 @@ int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint
       return rc;
     b.cap = n;
   }
-  // key range: keys < A*T, so sort only the significant bits
-  unsigned end_bit = 1;
-  while (end_bit < 64 && (m.A * m.T) >> end_bit) ++end_bit;
-  size_t need = 0, t1 = 0, t2 = 0, t3 = 0;
-  PLUSS_HIP_CHECK(rocprim::radix_sort_pairs(nullptr, t1, b.keys, b.keys_s, b.sinks, b.sinks_s, n, 0, end_bit, s));
+  return PLUSS_OK;
+}
+
+static int faith_tmp(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
+  FaithfulBufs& b = ctx->fb;
+  size_t t1 = 0, t2 = 0, t3 = 0;
+  PLUSS_HIP_CHECK(
+      rocprim::radix_sort_pairs(nullptr, t1, b.keys, b.keys_s, b.sinks, b.sinks_s, n, 0, key_bits(ctx->m), s));
   PLUSS_HIP_CHECK(rocprim::inclusive_scan(nullptr, t2, b.sinks_s, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
   PLUSS_HIP_CHECK(rocprim::inclusive_scan(nullptr, t3, b.flags, b.nstart, n, rocprim::plus<unsigned int>(), s));
-  need = t1 > t2 ? t1 : t2;
+  size_t need = t1 > t2 ? t1 : t2;
   need = need > t3 ? need : t3;
   if (need > b.tmp_bytes) {
     PLUSS_HIP_CHECK(hipStreamSynchronize(s));
@@ -187,35 +271,169 @@ int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint
     }
     b.tmp_bytes = need;
   }
-  const int nb = (int)((n + BLOCK * 4 - 1) / (BLOCK * 4) < (uint64_t)MAX_BLOCKS ? (n + BLOCK * 4 - 1) / (BLOCK * 4)
-                                                                               : MAX_BLOCKS);
-  const int grid = nb < 1 ? 1 : nb;
+  return PLUSS_OK;
+}
+
+static int faith_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, uint64_t lo, uint64_t hi,
+                      unsigned long long* cnt, hipStream_t s) {
+  const Model& m = ctx->m;
+  FaithfulBufs& b = ctx->fb;
   if (m.fast)
-    hipLaunchKernelGGL(k_faith_keys<true>, dim3(grid), dim3(BLOCK), 0, s, m, (uint32_t)ref, d_samples, n, b.keys,
-                       b.sinks, ctx->g);
+    hipLaunchKernelGGL(k_faith_keys<true>, dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, d_samples, n, lo, hi,
+                       b.keys, b.sinks, cnt, ctx->g);
   else
-    hipLaunchKernelGGL(k_faith_keys<false>, dim3(grid), dim3(BLOCK), 0, s, m, (uint32_t)ref, d_samples, n, b.keys,
-                       b.sinks, ctx->g);
-  PLUSS_HIP_CHECK(hipGetLastError());
-  size_t sz = b.tmp_bytes;
-  PLUSS_HIP_CHECK(rocprim::radix_sort_pairs(b.tmp, sz, b.keys, b.keys_s, b.sinks, b.sinks_s, n, 0, end_bit, s));
-  sz = b.tmp_bytes;
-  PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, b.sinks_s, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
-  hipLaunchKernelGGL(k_faith_flags, dim3(grid), dim3(BLOCK), 0, s, b.keys_s, b.pmax, n, b.flags);
-  PLUSS_HIP_CHECK(hipGetLastError());
-  sz = b.tmp_bytes;
-  PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, b.flags, b.nstart, n, rocprim::plus<unsigned int>(), s));
-  hipLaunchKernelGGL(k_faith_init, dim3(1), dim3(1), 0, s, b.scal, n);
-  hipLaunchKernelGGL(k_faith_cut, dim3(grid), dim3(BLOCK), 0, s, b.flags, b.nstart, n, b.scal);
-  if (m.fast)
-    hipLaunchKernelGGL(k_faith_hist<true>, dim3(grid), dim3(BLOCK), 0, s, m, (uint32_t)ref, b.keys_s, b.sinks_s, b.pmax,
-                       b.flags, n, b.scal, ctx->g);
-  else
-    hipLaunchKernelGGL(k_faith_hist<false>, dim3(grid), dim3(BLOCK), 0, s, m, (uint32_t)ref, b.keys_s, b.sinks_s,
-                       b.pmax, b.flags, n, b.scal, ctx->g);
-  hipLaunchKernelGGL(k_faith_finish, dim3(1), dim3(1), 0, s, m, (uint32_t)ref, n, b.pmax, b.scal, ctx->g);
+    hipLaunchKernelGGL(k_faith_keys<false>, dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, d_samples, n, lo,
+                       hi, b.keys, b.sinks, cnt, ctx->g);
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
+}
+
+// sort the shard's n (key, sink) pairs by key and take the prefix max of sinks
+static int faith_sort(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
+  FaithfulBufs& b = ctx->fb;
+  if (int rc = faith_tmp(ctx, n, s)) return rc;
+  size_t sz = b.tmp_bytes;
+  PLUSS_HIP_CHECK(
+      rocprim::radix_sort_pairs(b.tmp, sz, b.keys, b.keys_s, b.sinks, b.sinks_s, n, 0, key_bits(ctx->m), s));
+  sz = b.tmp_bytes;
+  PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, b.sinks_s, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
+  return PLUSS_OK;
+}
+
+static int faith_starts(pluss_ctx* ctx, uint64_t n, uint64_t j_off, unsigned long long pmax_in, hipStream_t s) {
+  FaithfulBufs& b = ctx->fb;
+  hipLaunchKernelGGL(k_faith_flags, dim3(grid_of(n)), dim3(BLOCK), 0, s, b.keys_s, b.pmax, n, j_off, pmax_in, b.flags);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  size_t sz = b.tmp_bytes;
+  PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, b.flags, b.nstart, n, rocprim::plus<unsigned int>(), s));
+  return PLUSS_OK;
+}
+
+static int faith_record(pluss_ctx* ctx, int32_t ref, uint64_t n, uint64_t j_off, unsigned long long pmax_in,
+                        int next_start, uint64_t n_total, int is_last, hipStream_t s) {
+  const Model& m = ctx->m;
+  FaithfulBufs& b = ctx->fb;
+  if (n) {
+    if (m.fast)
+      hipLaunchKernelGGL(k_faith_hist<true>, dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, b.keys_s, b.sinks_s,
+                         b.pmax, b.flags, n, j_off, pmax_in, next_start, b.scal, ctx->g);
+    else
+      hipLaunchKernelGGL(k_faith_hist<false>, dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, b.keys_s,
+                         b.sinks_s, b.pmax, b.flags, n, j_off, pmax_in, next_start, b.scal, ctx->g);
+  }
+  hipLaunchKernelGGL(k_faith_finish, dim3(1), dim3(1), 0, s, m, (uint32_t)ref, n, n_total, is_last, pmax_in, b.pmax,
+                     b.scal, ctx->g);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  ctx->tables_dirty = true;
+  return PLUSS_OK;
+}
+
+int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s) {
+  if (int rc = faith_check_shape(ctx)) return rc;
+  if (int rc = faith_reserve(ctx, n, s)) return rc;
+  if (n == 0) return PLUSS_OK;
+  FaithfulBufs& b = ctx->fb;
+  if (int rc = faith_keys(ctx, ref, d_samples, n, 0, 0, nullptr, s)) return rc;
+  if (int rc = faith_sort(ctx, n, s)) return rc;
+  if (int rc = faith_starts(ctx, n, 0, 0, s)) return rc;
+  hipLaunchKernelGGL(k_faith_init, dim3(1), dim3(1), 0, s, b.scal, n);
+  hipLaunchKernelGGL(k_faith_cut, dim3(grid_of(n)), dim3(BLOCK), 0, s, b.flags, b.nstart, n, (uint64_t)0, (uint64_t)0,
+                     n, b.scal);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  return faith_record(ctx, ref, n, 0, 0, 0, n, 1, s);
+}
+
+// ---- key-range shards (multi-GPU faithful mode; the caller exchanges the
+// ---- per-shard summaries between phases)
+int faith_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, uint64_t lo, uint64_t hi,
+                     pluss_faith_shard* out, hipStream_t s) {
+  if (int rc = faith_check_shape(ctx)) return rc;
+  if (int rc = faith_reserve(ctx, n, s)) return rc;
+  FaithShard& f = ctx->fsh;
+  FaithfulBufs& b = ctx->fb;
+  f = FaithShard{};
+  f.ref = ref;
+  PLUSS_HIP_CHECK(hipMemsetAsync(b.scal + 3, 0, 8, s));
+  if (n)
+    if (int rc = faith_keys(ctx, ref, d_samples, n, lo, hi, b.scal + 3, s)) return rc;
+  unsigned long long m = 0;
+  PLUSS_HIP_CHECK(hipMemcpyAsync(&m, b.scal + 3, 8, hipMemcpyDeviceToHost, s));
+  PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+  f.n = m;
+  out->n = m;
+  out->first_key = KEY_EMPTY;
+  out->max_sink = 0;
+  if (m) {
+    if (int rc = faith_sort(ctx, m, s)) return rc;
+    PLUSS_HIP_CHECK(hipMemcpyAsync(&out->first_key, b.keys_s, 8, hipMemcpyDeviceToHost, s));
+    PLUSS_HIP_CHECK(hipMemcpyAsync(&out->max_sink, b.pmax + (m - 1), 8, hipMemcpyDeviceToHost, s));
+    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  f.max_sink = out->max_sink;
+  f.phase = 1;
+  return PLUSS_OK;
+}
+
+int faith_shard_starts(pluss_ctx* ctx, uint64_t j_off, uint64_t pmax_in, pluss_faith_shard* out, hipStream_t s) {
+  FaithShard& f = ctx->fsh;
+  if (f.phase != 1) {
+    set_error("pluss_dev_faithful_shard_starts: call pluss_dev_faithful_shard_keys first");
+    return PLUSS_ERR_CONFIG;
+  }
+  f.j_off = j_off;
+  f.pmax_in = pmax_in;
+  out->n_starts = 0;
+  if (f.n) {
+    if (int rc = faith_starts(ctx, f.n, j_off, pmax_in, s)) return rc;
+    unsigned int c = 0;
+    PLUSS_HIP_CHECK(hipMemcpyAsync(&c, ctx->fb.nstart + (f.n - 1), 4, hipMemcpyDeviceToHost, s));
+    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+    out->n_starts = c;
+  }
+  f.phase = 2;
+  return PLUSS_OK;
+}
+
+int faith_shard_cut(pluss_ctx* ctx, uint64_t s_off, uint64_t n_total, pluss_faith_shard* out, hipStream_t s) {
+  FaithShard& f = ctx->fsh;
+  if (f.phase != 2) {
+    set_error("pluss_dev_faithful_shard_cut: call pluss_dev_faithful_shard_starts first");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (f.j_off + f.n > n_total) {
+    set_error("pluss_dev_faithful_shard_cut: n_total is smaller than this shard's end");
+    return PLUSS_ERR_CONFIG;
+  }
+  f.n_total = n_total;
+  out->cut = n_total;
+  if (f.n) {
+    FaithfulBufs& b = ctx->fb;
+    hipLaunchKernelGGL(k_faith_init, dim3(1), dim3(1), 0, s, b.scal, n_total);
+    hipLaunchKernelGGL(k_faith_cut, dim3(grid_of(f.n)), dim3(BLOCK), 0, s, b.flags, b.nstart, f.n, f.j_off, s_off,
+                       n_total, b.scal);
+    PLUSS_HIP_CHECK(hipGetLastError());
+    PLUSS_HIP_CHECK(hipMemcpyAsync(&out->cut, b.scal, 8, hipMemcpyDeviceToHost, s));
+    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  f.phase = 3;
+  return PLUSS_OK;
+}
+
+int faith_shard_hist(pluss_ctx* ctx, uint64_t cut, uint64_t next_first_key, int is_last, hipStream_t s) {
+  FaithShard& f = ctx->fsh;
+  if (f.phase != 3) {
+    set_error("pluss_dev_faithful_shard_hist: call pluss_dev_faithful_shard_cut first");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (cut > f.n_total) {
+    set_error("pluss_dev_faithful_shard_hist: cut > n_total");
+    return PLUSS_ERR_CONFIG;
+  }
+  const unsigned long long last = f.max_sink > f.pmax_in ? f.max_sink : f.pmax_in;  // global pmax at the shard end
+  const int next_start = next_first_key != KEY_EMPTY && next_first_key > last;
+  hipLaunchKernelGGL(k_faith_init, dim3(1), dim3(1), 0, s, ctx->fb.scal, cut);
+  f.phase = 0;
+  return faith_record(ctx, f.ref, f.n, f.j_off, f.pmax_in, next_start, f.n_total, is_last, s);
 }
 
 }  // namespace pluss

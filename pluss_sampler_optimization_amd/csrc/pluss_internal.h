@@ -52,6 +52,14 @@ struct FaithfulBufs {
   unsigned long long* scal = nullptr;  // [0] cut, [1] cold, [2] traversed
 };
 
+// state of a key-range shard between the phases of pluss_dev_faithful_shard_*
+struct FaithShard {
+  int phase = 0;  // last completed phase (1 keys, 2 starts, 3 cut)
+  int32_t ref = 0;
+  uint64_t n = 0, j_off = 0, n_total = 0;
+  unsigned long long pmax_in = 0, max_sink = 0;
+};
+
 }  // namespace pluss
 
 struct pluss_ctx {
@@ -64,6 +72,7 @@ struct pluss_ctx {
   unsigned long long *d_exp_keys, *d_exp_counts;  // GCAP each, canonical export
   unsigned int* d_exp_n;
   pluss::FaithfulBufs fb;
+  pluss::FaithShard fsh;
   hipStream_t last;   // stream of the most recent launch (fetch orders after it)
   bool tables_dirty;  // hash tables may hold counts (GENERIC / faithful launches since the last reset)
 };
@@ -98,5 +107,10 @@ int launch_export(pluss_ctx* ctx, unsigned long long* d_keys, unsigned long long
 int launch_sampled_hist_export(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, unsigned long long* d_keys,
                                unsigned long long* d_counts, uint64_t cap, hipStream_t s);
 int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s);
+int faith_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, uint64_t lo, uint64_t hi,
+                     pluss_faith_shard* out, hipStream_t s);
+int faith_shard_starts(pluss_ctx* ctx, uint64_t j_off, uint64_t pmax_in, pluss_faith_shard* out, hipStream_t s);
+int faith_shard_cut(pluss_ctx* ctx, uint64_t s_off, uint64_t n_total, pluss_faith_shard* out, hipStream_t s);
+int faith_shard_hist(pluss_ctx* ctx, uint64_t cut, uint64_t next_first_key, int is_last, hipStream_t s);
 
 }  // namespace pluss

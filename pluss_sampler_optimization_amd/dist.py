@@ -9,12 +9,20 @@ keys, fixed capacity) and the tables are all-gathered over RCCL and summed by
 key.  An all-gather of ~64 KB per rank replaces an all-reduce because the
 exact-key tables are sparse (a dense all-reduce over exact RI values would
 need one slot per possible RI).
+
+Faithful mode (one r10 sampler_<REF> with its cross-sample queue semantics)
+needs one global key order, so it is sharded by contiguous ranges of the sort
+key a*T+tid instead: every rank reads the whole per-reference
+list, keeps and sorts its key range, and four small all-gathers of per-shard
+summaries (count / first key / max sink, start count, cut candidate) carry
+the scan state across shards (include/pluss_gpu.h, pluss_dev_faithful_shard_*).
 """
 import numpy as np
 
-from .api import REFS, Context, hist_from_tables
+from .api import REFS, Context, Histogram, faithful_key_space, hist_from_tables
 
 TABLE_CAP = 4096
+KEY_EMPTY = (1 << 64) - 1
 
 
 def shard_ranges(counts, rank, world):
@@ -71,3 +79,71 @@ def sharded_clean_hist(cfg, seed, counts, group=None, stream=None):
     if dist.get_backend(group) == "gloo":  # e.g. several ranks sharing one GPU in tests
         keys, cnts = keys.cpu(), cnts.cpu()
     return allgather_tables(keys, cnts, group)
+
+
+def key_range(key_space, rank, world):
+    """Contiguous slice `rank` of `world` of the faithful key space [0, key_space)."""
+    return key_space * rank // world, key_space * (rank + 1) // world
+
+
+def torch_allgather(group=None, device=None):
+    """allgather(list of u64) -> one list per rank, over torch.distributed
+    (int64 tensors on `device`: a GPU with nccl/RCCL, the CPU with gloo)."""
+    import torch
+    import torch.distributed as dist
+
+    def allgather(vals):
+        t = torch.tensor(np.array(vals, dtype=np.uint64).view(np.int64), device=device)
+        out = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+        dist.all_gather(out, t, group=group)
+        return [[int(v) for v in o.cpu().numpy().view(np.uint64)] for o in out]
+    return allgather
+
+
+def faithful_shard_protocol(shard, ref, d_samples, n, key_lo, key_hi, rank, allgather, stream=None):
+    """The four phases of a key-range-sharded faithful sampler on `shard` (a
+    Context, or any object with the same faithful_shard_* methods), exchanging
+    the per-shard summaries with `allgather`.  Returns (n_total, cut)."""
+    m, first, mx = shard.faithful_shard_keys(ref, d_samples, n, key_lo, key_hi, stream)
+    g = allgather([m, first, mx])
+    j_off = sum(x[0] for x in g[:rank])
+    n_total = sum(x[0] for x in g)
+    pmax_in = max([x[2] for x in g[:rank] if x[0] > 0], default=0)
+    later = [x for x in g[rank + 1:] if x[0] > 0]
+    next_first = later[0][1] if later else KEY_EMPTY
+    ns = shard.faithful_shard_starts(j_off, pmax_in, stream)
+    s_off = sum(x[0] for x in allgather([ns])[:rank])
+    c = shard.faithful_shard_cut(s_off, n_total, stream)
+    cut = min(x[0] for x in allgather([c]))
+    shard.faithful_shard_hist(cut, next_first, not later, stream)
+    return n_total, cut
+
+
+def sharded_faithful_hist(cfg, samples_by_ref, group=None, stream=None):
+    """Faithful mode over key-range shards, one GPU per rank.
+
+    samples_by_ref: {ref: device int64 tensor holding that reference's whole
+    sample list} (identical on every rank).  Returns the merged Histogram,
+    with `traversed` summed over ranks (identical on all ranks)."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    nccl = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", cfg.device)
+    ag = torch_allgather(group, dev if nccl else "cpu")
+    lo, hi = key_range(faithful_key_space(cfg), rank, world)
+    sp = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    keys = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
+    cnts = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
+    with Context(cfg) as ctx:
+        ctx.reset(sp)
+        for ref, t in samples_by_ref.items():
+            faithful_shard_protocol(ctx, ref, t.data_ptr(), t.numel(), lo, hi, rank, ag, sp)
+        ctx.export(keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
+        torch.cuda.synchronize(dev)
+        trav = ctx.fetch().traversed
+    tsum = [sum(col) % (1 << 64) for col in zip(*ag(trav))]
+    if not nccl:
+        keys, cnts = keys.cpu(), cnts.cpu()
+    h = allgather_tables(keys, cnts, group)
+    return Histogram(h.bins, tsum)

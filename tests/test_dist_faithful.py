@@ -1,0 +1,213 @@
+"""Key-range-sharded faithful mode (multi-GPU path) on the CPU.
+
+The summary exchange of pluss_sampler_optimization_amd.dist.faithful_shard_protocol
+runs over gloo with world size 1-4.  Each rank's shard is an emulation of the
+four device phases (pluss_faithful.hip: k_faith_keys with the key-range
+filter, sort, prefix max, k_faith_flags, k_faith_cut, k_faith_hist,
+k_faith_finish) on host arrays; keys and sinks come from the oracle's
+per-sample RI.  Merged over ranks, the histogram and the summed `traversed`
+must equal the oracle's sequential restatement of one r10 sampler_<REF>
+(oracle/pluss_oracle.c orc_faithful), which is pinned to the reference's
+dumps.  The device phases themselves are checked against one-GPU faithful
+mode in tests/test_gpu.py.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT, expected_raw, golden_configs
+
+GOLD = golden_configs()
+
+KEY_EMPTY = (1 << 64) - 1
+OFF = {"C0": 0, "C1": 1, "A0": 2, "B0": 3, "C2": 4, "C3": 5}
+
+
+def keys_and_sinks(orc, c, N, T, CS, ref, samples):
+    """Sort key a*T+tid and sink key (a+RI)*T+tid of every sample."""
+    ri = orc.clean_ri(c, samples)
+    _, c0, c1, c2 = [x.astype(np.int64) for x in _unpack(samples)]
+    if ref in ("C0", "C1"):
+        c2 = np.zeros_like(c2)
+    S = 4 * N + 2
+    R = N * S
+    t = (c0 // CS) % T
+    q = (c0 // (CS * T)) * CS + c0 % CS
+    off = OFF[ref] + (4 * c2 if ref not in ("C0", "C1") else 0)
+    P = q * R + c1 * S + off
+    keys = (P * T + t).astype(np.uint64)
+    sinks = np.where(ri < 0, np.uint64(KEY_EMPTY), ((P + np.maximum(ri, 0)) * T + t).astype(np.uint64))
+    return keys, sinks, ri
+
+
+def _unpack(s):
+    s = np.asarray(s, np.uint64)
+    m = np.uint64(0xFFFFF)
+    return (s >> np.uint64(60), (s >> np.uint64(40)) & m, (s >> np.uint64(20)) & m, s & m)
+
+
+class HostShard:
+    """Host emulation of the four pluss_dev_faithful_shard_* phases."""
+
+    def __init__(self, N, T, keys, sinks, ref):
+        self.N, self.T, self.ref = N, T, ref
+        self.all_keys, self.all_sinks = keys, sinks
+        self.bins, self.trav = {}, 0
+
+    def faithful_shard_keys(self, ref, d, n, lo, hi, stream=None):
+        sel = (self.all_keys >= np.uint64(lo)) & (self.all_keys < np.uint64(hi))
+        order = np.argsort(self.all_keys[sel], kind="stable")
+        self.k = self.all_keys[sel][order]
+        self.s = self.all_sinks[sel][order]
+        self.pm = np.maximum.accumulate(self.s) if len(self.s) else self.s
+        m = len(self.k)
+        return m, int(self.k[0]) if m else KEY_EMPTY, int(self.pm[-1]) if m else 0
+
+    def _g(self, i):
+        return max(int(self.pm[i]), self.pmax_in)
+
+    def faithful_shard_starts(self, j_off, pmax_in, stream=None):
+        self.j_off, self.pmax_in = j_off, pmax_in
+        m = len(self.k)
+        self.f = np.array([(j_off + i == 0) or int(self.k[i]) > (pmax_in if i == 0 else self._g(i - 1))
+                           for i in range(m)], dtype=bool)
+        self.ns = np.cumsum(self.f)
+        return int(self.f.sum())
+
+    def faithful_shard_cut(self, s_off, n_total, stream=None):
+        self.n_total = n_total
+        for i in range(len(self.k)):
+            j = self.j_off + i
+            if j > 0 and self.f[i] and j - (s_off + int(self.ns[i]) - 1) >= n_total - j:
+                return j
+        return n_total
+
+    def faithful_shard_hist(self, cut, next_first, is_last, stream=None):
+        m, T, N = len(self.k), self.T, self.N
+        thr = (4 * N + 2) * N
+        last = max(int(self.pm[-1]), self.pmax_in) if m else self.pmax_in
+        next_start = next_first != KEY_EMPTY and next_first > last
+        lim = max(0, min(m, cut - self.j_off))
+        cold, trav = 0, 0
+        for i in range(lim):
+            k, s = int(self.k[i]), int(self.s[i])
+            if s == KEY_EMPTY:
+                cold += k % T == 0
+            else:
+                ri = (s - k) // T
+                kind = 1 if (self.ref == "B0" and ri > 0 and 2 * ri > thr) else 0
+                self.bins[(self.ref, kind, ri)] = self.bins.get((self.ref, kind, ri), 0) + 1
+            if self.f[i]:
+                trav -= k
+            ends = self.j_off + i + 1 == cut or (self.f[i + 1] if i + 1 < m else next_start)
+            if ends:
+                gm = self._g(i)
+                trav += (N // T) * N * (4 * N + 2) * T if gm == KEY_EMPTY else gm
+        if is_last and m and cut == self.n_total:
+            gm = self._g(m - 1)
+            if gm != KEY_EMPTY and gm % T == 0:
+                cold += 1
+        key = (self.ref, 0, -1)
+        self.bins[key] = self.bins.get(key, 0) + cold
+        self.trav = trav % (1 << 64)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, N, T, per, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    import oracle as orc
+    from pluss_sampler_optimization_amd import dist as D
+    from test_dist_faithful import HostShard, keys_and_sinks
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = orc.cfg(N, T)
+    ag = D.torch_allgather(None, "cpu")
+    key_space = (N // T) * N * (4 * N + 2) * T
+    lo, hi = D.key_range(key_space, rank, world)
+    out = {}
+    for r, ref in enumerate(orc.REFS):
+        cnt = min(per, (N - 1) ** (2 if r < 2 else 3))
+        s = orc.expand(c, 0x5EED0000 + N, r, 0, cnt)
+        keys, sinks, _ = keys_and_sinks(orc, c, N, T, 4, ref, s)
+        sh = HostShard(N, T, keys, sinks, ref)
+        D.faithful_shard_protocol(sh, r, None, len(s), lo, hi, rank, ag)
+        out[ref] = (sh.bins, sh.trav)
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N,T,per", [(1, 64, 4, 3000), (2, 64, 4, 3000), (3, 128, 8, 4000),
+                                           (4, 64, 2, 2500)])
+def test_key_range_shards_equal_sequential_sampler(orc, world, N, T, per):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, T, per, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    c = orc.cfg(N, T)
+    for r, ref in enumerate(orc.REFS):
+        cnt = min(per, (N - 1) ** (2 if r < 2 else 3))
+        s = orc.expand(c, 0x5EED0000 + N, r, 0, cnt)
+        want, wtrav = orc.faithful(c, ref, s)
+        got, trav = {}, 0
+        for _, out in res:
+            b, t = out[ref]
+            for k, v in b.items():
+                got[k] = got.get(k, 0) + v
+            trav = (trav + t) % (1 << 64)
+        assert got == want, (world, ref)
+        assert trav == wtrav, (world, ref)
+
+
+@pytest.mark.parametrize("name,d,smp", GOLD, ids=[g[0] for g in GOLD])
+def test_key_range_shards_on_reference_dumps(orc, name, d, smp):
+    """Single process, 3 emulated shards with an uneven split, on the reference's r10 dumps."""
+    from pluss_sampler_optimization_amd import dist as D
+    N, T = d["N"], d["T"]
+    c = orc.cfg(N, T)
+    key_space = (N // T) * N * (4 * N + 2) * T
+    bounds = [0, key_space // 7, key_space // 2, key_space]
+    for ref in orc.REFS:
+        s = orc.pack_array(ref, smp[ref])
+        keys, sinks, _ = keys_and_sinks(orc, c, N, T, 4, ref, s)
+        shards = [HostShard(N, T, keys, sinks, ref) for _ in range(3)]
+        # run the protocol in lockstep: a generator per shard, exchanging by hand
+        summaries = [sh.faithful_shard_keys(ref, None, len(s), bounds[i], bounds[i + 1]) for i, sh in enumerate(shards)]
+        g = [list(x) for x in summaries]
+        starts = []
+        for i, sh in enumerate(shards):
+            j_off = sum(x[0] for x in g[:i])
+            pmax_in = max([x[2] for x in g[:i] if x[0] > 0], default=0)
+            starts.append(sh.faithful_shard_starts(j_off, pmax_in))
+        n_total = sum(x[0] for x in g)
+        cuts = [sh.faithful_shard_cut(sum(starts[:i]), n_total) for i, sh in enumerate(shards)]
+        got, trav = {}, 0
+        for i, sh in enumerate(shards):
+            later = [x for x in g[i + 1:] if x[0] > 0]
+            sh.faithful_shard_hist(min(cuts), later[0][1] if later else KEY_EMPTY, not later)
+            for k, v in sh.bins.items():
+                got[k] = got.get(k, 0) + v
+            trav = (trav + sh.trav) % (1 << 64)
+        exp, etrav = expected_raw(d, ref)
+        assert got == exp, (name, ref)
+        assert trav == etrav, (name, ref)
+        assert D.KEY_EMPTY == KEY_EMPTY

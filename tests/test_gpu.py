@@ -338,6 +338,152 @@ def test_sharded_two_ranks_on_one_gpu_equals_single_rank():
         assert bins == want
 
 
+KEY_EMPTY = (1 << 64) - 1
+
+
+def _lockstep_shards(ctxs, bounds, ref, d_ptr, n, stream):
+    """Run the four pluss_dev_faithful_shard_* phases over several handles in
+    one process, exchanging the summaries by hand (what dist.py does with
+    all-gathers)."""
+    g = [ctx.faithful_shard_keys(ref, d_ptr, n, bounds[i], bounds[i + 1], stream) for i, ctx in enumerate(ctxs)]
+    starts = []
+    for i, ctx in enumerate(ctxs):
+        j_off = sum(x[0] for x in g[:i])
+        pmax_in = max([x[2] for x in g[:i] if x[0] > 0], default=0)
+        starts.append(ctx.faithful_shard_starts(j_off, pmax_in, stream))
+    n_total = sum(x[0] for x in g)
+    assert n_total == n
+    cut = min(ctx.faithful_shard_cut(sum(starts[:i]), n_total, stream) for i, ctx in enumerate(ctxs))
+    for i, ctx in enumerate(ctxs):
+        later = [x for x in g[i + 1:] if x[0] > 0]
+        ctx.faithful_shard_hist(cut, later[0][1] if later else KEY_EMPTY, not later, stream)
+    return g
+
+
+def _merged(ctxs):
+    bins, trav = {}, [0] * 6
+    for ctx in ctxs:
+        h = ctx.fetch()
+        for k, v in h.bins.items():
+            bins[k] = bins.get(k, 0) + v
+        trav = [(a + b) % (1 << 64) for a, b in zip(trav, h.traversed)]
+    return bins, trav
+
+
+@pytest.mark.parametrize("name,d,smp", GOLD[:4], ids=[g[0] for g in GOLD[:4]])
+def test_faithful_key_range_shards_equal_reference_dumps(orc, name, d, smp):
+    """Faithful mode split over 3 key-range shards (3 handles on one GPU, one of
+    them covering no key) reproduces the reference's r10 dumps."""
+    torch = pytest.importorskip("torch")
+    N, T = d["N"], d["T"]
+    c = cfg(N, T, mode="faithful")
+    ks = P.faithful_key_space(c)
+    bounds = [0, ks // 3, ks // 3, ks]  # shard 1 is empty
+    stream = torch.cuda.current_stream().cuda_stream
+    ctxs = [P.Context(c) for _ in range(3)]
+    try:
+        for x in ctxs:
+            x.reset(stream)
+        for ref in orc.REFS:
+            t = torch.from_numpy(orc.pack_array(ref, smp[ref]).view(np.int64)).cuda()
+            g = _lockstep_shards(ctxs, bounds, ref, t.data_ptr(), t.numel(), stream)
+            assert g[1][0] == 0
+        bins, trav = _merged(ctxs)
+    finally:
+        for x in ctxs:
+            x.close()
+    for ref in orc.REFS:
+        exp, etrav = expected_raw(d, ref)
+        assert {k: v for k, v in bins.items() if k[0] == ref} == exp, (name, ref)
+        assert trav[P.REF_ID[ref]] == etrav, (name, ref)
+
+
+@pytest.mark.parametrize("N,T,per,nshards", [(128, 8, 20000, 2), (256, 4, 60000, 5), (64, 2, 30000, 8)])
+def test_faithful_key_range_shards_equal_one_gpu(N, T, per, nshards):
+    """Longer lists (many replays, Q1 drops, cold samples): the sharded phases
+    equal one-handle faithful mode exactly, traversed included."""
+    torch = pytest.importorskip("torch")
+    c = cfg(N, T, mode="faithful")
+    ks = P.faithful_key_space(c)
+    bounds = [ks * i // nshards for i in range(nshards + 1)]
+    stream = torch.cuda.current_stream().cuda_stream
+    ctxs = [P.Context(c) for _ in range(nshards)]
+    one = P.Context(c)
+    try:
+        for x in ctxs + [one]:
+            x.reset(stream)
+        for r in range(6):
+            n = per if r >= 2 else min(per, (N - 1) ** 2)
+            s = P.expand_samples(c, 0x5EED0000 + N, r, 0, n)
+            t = torch.from_numpy(s.view(np.int64)).cuda()
+            _lockstep_shards(ctxs, bounds, r, t.data_ptr(), n, stream)
+            one.faithful_hist(r, t.data_ptr(), n, stream)
+        bins, trav = _merged(ctxs)
+        h = one.fetch()
+    finally:
+        for x in ctxs + [one]:
+            x.close()
+    assert bins == h.bins
+    assert trav == h.traversed
+
+
+def test_faithful_shard_phase_order_is_enforced():
+    c = cfg(64, 4, mode="faithful")
+    with P.Context(c) as ctx:
+        with pytest.raises(P.PlussError, match="PLUSS_ERR_CONFIG"):
+            ctx.faithful_shard_starts(0, 0)
+        with pytest.raises(P.PlussError, match="PLUSS_ERR_CONFIG"):
+            ctx.faithful_shard_hist(0, KEY_EMPTY, True)
+    with pytest.raises(P.PlussError, match="PLUSS_ERR_CONFIG"):
+        P.faithful_key_space(cfg(60, 4, mode="faithful"))
+
+
+def _faith_dist_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import torch.distributed as dist
+    import pluss_sampler_optimization_amd as P2
+    from pluss_sampler_optimization_amd import dist as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = P2.SamplerConfig(n=256, threads=8, mode="faithful")
+    counts = P2.default_counts(256, 1 << 18)
+    lists = {r: torch.from_numpy(P2.expand_samples(c, 0x5EED0001, r, 0, n).view("int64")).cuda()
+             for r, n in enumerate(counts)}
+    h = D.sharded_faithful_hist(c, lists)
+    q.put((rank, h.bins, h.traversed))
+    dist.destroy_process_group()
+
+
+def test_sharded_faithful_two_ranks_on_one_gpu():
+    """dist.sharded_faithful_hist end to end: 2 processes on cuda:0, summaries and
+    tables exchanged over gloo, equals one process over the same lists."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_faith_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    c = P.SamplerConfig(n=256, threads=8, mode="faithful")
+    counts = P.default_counts(256, 1 << 18)
+    whole = np.concatenate([P.expand_samples(c, 0x5EED0001, r, 0, n) for r, n in enumerate(counts)])
+    want = P.sampled_hist(c, whole)
+    for _, bins, trav in res:
+        assert bins == want.bins
+        assert trav == want.traversed
+
+
 CLI = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "pluss_sampler_optimization_amd",
                    "lib", "pluss_cli")
 
