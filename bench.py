@@ -4,12 +4,13 @@
 Workload (BASELINE.json configs[1]): GEMM N=1024,
 8 simulated threads, chunk 4, DS=8, CLS=64, clean mode, 2^24 sampled
 accesses per GPU (default per-reference split, keyed Feistel sample lists).
-One step = run the sampling kernel over the resident sample list, then fold
-the per-workgroup tables into the canonical exported table and clear the
-histogram for the next step (one launch);
-with N>1 GPUs the step also all-gathers the per-GPU tables over RCCL (the
-only exchange of the path).  Samples are sharded across ranks with no other
-communication, so per-GPU work is fixed (weak scaling).
+One step = one launch of the sampling kernel over the resident sample list
+that leaves this pass's complete histogram -- the dense vector of
+(ref, case) counts, pluss_dev_sampled_hist_dense -- in HBM and its own
+state zeroed for the next pass; with N>1 GPUs the step also all-reduces the
+per-GPU vectors over RCCL (the only exchange of the path).  Samples are
+sharded across ranks with no other communication, so per-GPU work is fixed
+(weak scaling).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -32,7 +33,6 @@ METRIC = "sampled accesses/sec (node) at 1/2/4/8 MI355X; HBM roofline %; MRC abs
 SEED = 0x5EED0001
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 BYTES_PER_SAMPLE = 8   # one packed u64 sample descriptor read once
-TABLE_CAP = 4096
 
 CONFIGS = {
     "config2": dict(n=1024, threads=8, per_gpu=1 << 24,
@@ -166,9 +166,9 @@ def pmc_traffic():
     return None
 
 
-def gather_cpu(t):
-    out = torch.empty(dist.get_world_size() * t.numel(), dtype=t.dtype)
-    dist.all_gather_into_tensor(out, t.cpu())
+def allreduce_cpu(t):
+    out = t.cpu()
+    dist.all_reduce(out)
     return out
 
 
@@ -213,10 +213,7 @@ def main():
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
     samples = torch.empty(n_local, dtype=torch.int64, device=dev)
-    keys = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
-    cnts = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
-    gk = torch.empty(world * TABLE_CAP, dtype=torch.int64, device=dev)
-    gc = torch.empty(world * TABLE_CAP, dtype=torch.int64, device=dev)
+    dense = torch.zeros(P.DENSE_BINS + 1, dtype=torch.int64, device=dev)
     ctx = P.Context(cfg)
     off = 0
     for ref, (lo, cnt) in enumerate(parts):
@@ -225,16 +222,14 @@ def main():
     torch.cuda.synchronize()
 
     def step():
-        # one launch: count every sample, the last workgroup writes the canonical
-        # (key, count) table and empties the histogram for the next pass
-        ctx.sampled_hist_export(samples.data_ptr(), n_local, keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
-        if world > 1:
+        # one launch: count every sample; the last adder of each bin writes this
+        # pass's total to `dense` and zeroes the kernel's state for the next pass
+        ctx.sampled_hist_dense(samples.data_ptr(), n_local, dense.data_ptr(), sp)
+        if world > 1:  # element-wise sum of the per-GPU vectors (counts < 2^63)
             if args.backend == "nccl":
-                dist.all_gather_into_tensor(gk, keys)
-                dist.all_gather_into_tensor(gc, cnts)
+                dist.all_reduce(dense)
             else:
-                gk.copy_(gather_cpu(keys))
-                gc.copy_(gather_cpu(cnts))
+                dense.copy_(allreduce_cpu(dense))
 
     ctx.reset(sp)
     for _ in range(args.warmup):
@@ -260,11 +255,10 @@ def main():
         elapsed = float(t.item())
 
     kern_ms = e0.elapsed_time(e1) / args.steps
-    # correctness of the merged histogram: every sample of every rank is counted once
-    if world > 1:
-        h = P.hist_from_tables(gk.cpu().numpy().view(np.uint64), gc.cpu().numpy().view(np.uint64))
-    else:
-        h = P.hist_from_tables(keys.cpu().numpy().view(np.uint64), cnts.cpu().numpy().view(np.uint64))
+    # correctness of the (merged) histogram: every sample of every rank is counted once
+    dv = dense.cpu().numpy()
+    assert dv[P.DENSE_BINS] == 0, "malformed samples"
+    h = P.hist_from_dense(cfg, dv)
     assert h.total() == total, (h.total(), total)
 
     achieved = BYTES_PER_SAMPLE * n_local / (kern_ms * 1e-3) / 1e9
@@ -283,11 +277,11 @@ def main():
         "data": "synthetic: keyed cycle-walking Feistel sample lists (seed 0x5EED0001), indices in [0,N-2]",
         "config": {"workload": spec["workload"], "N": cfg.n, "threads": cfg.threads, "chunk": 4, "ds": 8,
                    "cls": 64, "mode": "clean", "samples_per_gpu": n_local, "global_samples": total,
-                   "parallelism": f"sample-shard x{world}" + (" + RCCL all_gather of histogram tables" if world > 1
-                                                             else "")},
+                   "parallelism": f"sample-shard x{world}" + (" + RCCL all_reduce of the dense histogram"
+                                                             if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic()},
-        "kernel": {"name": "pluss::k_sampled_hist<2,0,2,true,true,1> (FAST_P2, non-temporal loads, fused export)",
+        "kernel": {"name": "pluss::k_sampled_hist<2,0,2,true,2,1> (FAST_P2, non-temporal loads, dense tail)",
                    "avg_ms": kern_ms, "timing": "HIP events on the launch stream around the K timed steps / K"
                    + (" (includes the all_gather)" if world > 1 else ""), "bytes_per_launch": BYTES_PER_SAMPLE * n_local},
         "histogram_bins": len(h.bins),

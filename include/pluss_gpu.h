@@ -125,6 +125,25 @@ int pluss_dev_hist_export_reset(pluss_ctx *ctx, uint64_t *d_keys, uint64_t *d_co
    counts (the last workgroup to finish writes the table) */
 int pluss_dev_sampled_hist_export(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t n, uint64_t *d_keys,
                                   uint64_t *d_counts, uint64_t cap, void *stream);
+/* --- dense per-pass histogram (N % (cls/ds) == 0: every BASELINE shape) ----
+   For these shapes a sample's (ref, kind, RI) key is one of PLUSS_DENSE_BINS
+   fixed keys -- three outcomes per reference, bin = ref*3 + case (SURVEY.md
+   A.3) -- so the histogram of a pass is a dense vector of counts.
+   pluss_dense_keys:  the key of each bin (ref<<60 | kind<<56 | (ri+2), as in
+                      the canonical table); PLUSS_ERR_CONFIG for other shapes.
+   pluss_dev_sampled_hist_dense:  ONE launch counts every sample of the list
+                      and OVERWRITES d_counts[0..PLUSS_DENSE_BINS] with this
+                      pass's counts: [0..17] per bin, [18] malformed samples
+                      (these also raise PLUSS_ERR_INPUT at the next fetch).
+                      The handle's accumulating histogram is not touched.
+                      Vectors of several GPUs merge by element-wise sum (one
+                      all-reduce).  Replaces one r10 pass over all six
+                      sampler_<REF> lists in clean mode (r10:135-3190). */
+#define PLUSS_DENSE_BINS 18
+int pluss_dense_keys(const pluss_cfg *cfg, uint64_t keys[PLUSS_DENSE_BINS]);
+int pluss_dev_sampled_hist_dense(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t n, uint64_t *d_counts,
+                                 void *stream);
+
 /* --- faithful mode over key-range shards (multi-GPU) ----------------------
    One r10 sampler_<REF> (r10:135-696 and its five twins) split over ranks by
    contiguous ranges of its sort key a*T+tid (pluss_utils.h:175-267 order).

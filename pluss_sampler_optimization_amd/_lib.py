@@ -11,6 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libpluss_gpu.so")
 
 PLUSS_OK = 0
+DENSE_BINS = 18  # PLUSS_DENSE_BINS; a dense count vector holds DENSE_BINS + 1 words (the last: malformed samples)
 ERRORS = {-1: "PLUSS_ERR_CONFIG", -2: "PLUSS_ERR_HIP", -3: "PLUSS_ERR_ALLOC", -4: "PLUSS_ERR_CAPACITY",
           -5: "PLUSS_ERR_INPUT"}
 
@@ -24,6 +25,7 @@ EXPORTS = [
     "pluss_dev_hist_export", "pluss_dev_hist_export_reset", "pluss_dev_sampled_hist_export", "pluss_hist_fetch",
     "pluss_hist_from_tables", "pluss_faithful_key_space", "pluss_dev_faithful_shard_keys",
     "pluss_dev_faithful_shard_starts", "pluss_dev_faithful_shard_cut", "pluss_dev_faithful_shard_hist",
+    "pluss_dense_keys", "pluss_dev_sampled_hist_dense",
 ]
 
 
@@ -105,6 +107,8 @@ def lib():
         "pluss_dev_faithful_shard_starts": (ctypes.c_int, [vp, u64, u64, P(PlussFaithShard), vp]),
         "pluss_dev_faithful_shard_cut": (ctypes.c_int, [vp, u64, u64, P(PlussFaithShard), vp]),
         "pluss_dev_faithful_shard_hist": (ctypes.c_int, [vp, u64, u64, i32, vp]),
+        "pluss_dense_keys": (ctypes.c_int, [cfgp, P(u64)]),
+        "pluss_dev_sampled_hist_dense": (ctypes.c_int, [vp, vp, u64, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -16,7 +16,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import PlussCfg, PlussFaithShard, PlussHist, PlussHistEntry, check, lib
+from ._lib import DENSE_BINS, PlussCfg, PlussFaithShard, PlussHist, PlussHistEntry, check, lib
 
 REFS = ["C0", "C1", "A0", "B0", "C2", "C3"]
 REF_ID = {r: i for i, r in enumerate(REFS)}
@@ -172,6 +172,19 @@ def faithful_key_space(cfg):
     return int(out.value)
 
 
+def dense_keys(cfg):
+    """Keys of the PLUSS_DENSE_BINS dense bins (bin = ref*3 + case) of a shape with N % (cls/ds) == 0."""
+    out = (ctypes.c_uint64 * DENSE_BINS)()
+    check(lib().pluss_dense_keys(ctypes.byref(cfg.to_c()), out), "pluss_dense_keys")
+    return [int(x) for x in out]
+
+
+def hist_from_dense(cfg, counts):
+    """Histogram of a dense count vector (DENSE_BINS counts, optionally followed by the malformed count)."""
+    c = np.asarray(counts).reshape(-1)[:DENSE_BINS].astype(np.int64).view(np.uint64)
+    return hist_from_tables(np.array(dense_keys(cfg), dtype=np.uint64), c)
+
+
 def hist_from_tables(keys, counts):
     k, kp = _u64(keys)
     c, cp = _u64(counts)
@@ -241,6 +254,11 @@ class Context:
         """sampled_hist() then export_reset() -- one launch for N % (CLS/DS) == 0 shapes."""
         check(lib().pluss_dev_sampled_hist_export(self._h, d_samples, n, d_keys, d_counts, cap, stream),
               "pluss_dev_sampled_hist_export")
+
+    def sampled_hist_dense(self, d_samples, n, d_counts, stream=None):
+        """One launch: this pass's dense counts (DENSE_BINS + 1 u64 at d_counts; see dense_keys)."""
+        check(lib().pluss_dev_sampled_hist_dense(self._h, d_samples, n, d_counts, stream),
+              "pluss_dev_sampled_hist_dense")
 
     # faithful mode over key-range shards: the four phases of
     # pluss_dev_faithful_shard_* (the caller exchanges the summaries; see dist.py)

@@ -150,6 +150,8 @@ int pluss_ctx_create(const pluss_cfg* cfg, pluss_ctx** out) {
     c->g.bins = base + 2 * (GCAP + NREP * RCAP);
     c->g.flags = (unsigned int*)(c->g.bins + NBROW * BSTRIDE);
     c->g.trav = c->g.bins + NBROW * BSTRIDE + 4;
+    c->g.dbins = base + DB_OFF;
+    c->g.dtot = base + DB_OFF + NBROW * BSTRIDE;
   }
   if (hipMalloc((void**)&c->d_exp_keys, GCAP * 8) != hipSuccess) return fail("export");
   if (hipMalloc((void**)&c->d_exp_counts, GCAP * 8) != hipSuccess) return fail("export");
@@ -230,6 +232,24 @@ int pluss_dev_sampled_hist_export(pluss_ctx* ctx, const uint64_t* d_samples, uin
   if (!ctx || (!d_samples && n) || !d_keys || !d_counts) return PLUSS_ERR_CONFIG;
   return launch_sampled_hist_export(ctx, d_samples, n, (unsigned long long*)d_keys, (unsigned long long*)d_counts,
                                     cap, pick(ctx, stream));
+}
+
+int pluss_dense_keys(const pluss_cfg* cfg, uint64_t keys[PLUSS_DENSE_BINS]) {
+  Model m;
+  if (!keys) return PLUSS_ERR_CONFIG;
+  if (int rc = validate_cfg(cfg, &m)) return rc;
+  if (!m.fast) {
+    set_error("pluss_dense_keys: needs N % (cls/ds) == 0");
+    return PLUSS_ERR_CONFIG;
+  }
+  for (int b = 0; b < PLUSS_DENSE_BINS; ++b) keys[b] = m.keytab[b];
+  return PLUSS_OK;
+}
+
+int pluss_dev_sampled_hist_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, uint64_t* d_counts,
+                                 void* stream) {
+  if (!ctx || (!d_samples && n) || !d_counts) return PLUSS_ERR_CONFIG;
+  return launch_sampled_hist_dense(ctx, d_samples, n, (unsigned long long*)d_counts, pick(ctx, stream));
 }
 
 int pluss_faithful_key_space(const pluss_cfg* cfg, uint64_t* key_end) {

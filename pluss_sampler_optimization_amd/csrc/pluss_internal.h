@@ -24,9 +24,18 @@ constexpr uint32_t NBROW = 64;         // rows of direct (ref, case) counters (w
 constexpr uint32_t BSTRIDE = 32;       // u64 per row: 18 counters, [BARRIVE] arrival count; rows 256 B apart
 constexpr uint32_t BARRIVE = 31;
 
+// Dense per-pass histogram (pluss_dev_sampled_hist_dense): DBINS u64 counters
+// per row (18 (ref, case) keys + the malformed-sample count), each word
+// (arrivals << DARR_SHIFT | count) so the last adder of a word knows its total
+// from the value its add returned.  dbins: NBROW rows, dtot: one row.
+constexpr uint32_t DBINS = 19;
+constexpr int DARR_SHIFT = 44;
+constexpr unsigned long long DCNT_MASK = (1ull << DARR_SHIFT) - 1;
+
 // Global histogram state (one per handle), one contiguous allocation so a
 // single memset resets it:
 //   keys[GCAP] rkeys[NREP*RCAP] counts[GCAP] rcounts[NREP*RCAP] bins[NBROW*BSTRIDE] flags[8] trav[8]
+//   (pad to 256 B) dbins[NBROW*BSTRIDE] dtot[BSTRIDE]
 // FAST-mode kernels count into `bins` (18 fixed (ref, case) keys, Model::keytab);
 // arbitrary exact keys (GENERIC shapes, faithful mode) go to the open-addressing
 // replicas, spilling to the main table.
@@ -39,8 +48,11 @@ struct GTable {
   unsigned int* flags;          // [0] overflow, [1] bad input, [2] diagnostics, [3] main table used,
                                 // [4] finished bin rows of a fused count+export launch
   unsigned long long* trav;     // [6] per-ref traversed (faithful) / [0] total (full trace)
+  unsigned long long* dbins;    // NBROW * BSTRIDE: dense pass, per-row words (zero between passes)
+  unsigned long long* dtot;     // BSTRIDE: dense pass, per-bin words over the rows (zero between passes)
 };
-constexpr size_t TABLE_WORDS = 2 * (size_t)(GCAP + NREP * RCAP) + NBROW * BSTRIDE + 4 + 8;
+constexpr size_t DB_OFF = (2 * (size_t)(GCAP + NREP * RCAP) + NBROW * BSTRIDE + 4 + 8 + BSTRIDE - 1) / BSTRIDE * BSTRIDE;
+constexpr size_t TABLE_WORDS = DB_OFF + (size_t)(NBROW + 1) * BSTRIDE;
 constexpr size_t TABLE_BYTES = TABLE_WORDS * 8;
 
 struct FaithfulBufs {
@@ -106,6 +118,9 @@ int launch_export(pluss_ctx* ctx, unsigned long long* d_keys, unsigned long long
 // bins can hold counts (FAST shapes); otherwise the two launches
 int launch_sampled_hist_export(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, unsigned long long* d_keys,
                                unsigned long long* d_counts, uint64_t cap, hipStream_t s);
+// count a sample list into a caller-owned dense vector of DBINS counts (FAST shapes), one launch
+int launch_sampled_hist_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, unsigned long long* d_counts,
+                              hipStream_t s);
 int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s);
 int faith_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, uint64_t lo, uint64_t hi,
                      pluss_faith_shard* out, hipStream_t s);

@@ -174,6 +174,52 @@ __device__ __forceinline__ void bins_finish(unsigned int (*pc)[NBINS][64], GTabl
   if (threadIdx.x == BIN_BAD && tot[BIN_BAD]) atomicOr(&g.flags[1], 1u);
 }
 
+// Dense tail (pluss_dev_sampled_hist_dense): the 18 (ref, case) totals and
+// the malformed-sample count of this launch go to out[0..18], and the state
+// is left zeroed -- with no arrival counter, fence or extra load.  Every
+// workgroup adds (1 << DARR_SHIFT | its count) to each of the DBINS words of
+// its row (one wave instruction, 19 lanes, returning).  The add that returns
+// arrivals == (workgroups in the row) - 1 is the row's last for that bin, so
+// old + own is the row total: that lane zeroes the word and adds
+// (1 << DARR_SHIFT | row total) to the bin's word in `dtot`; the add there
+// that returns arrivals == rows - 1 holds the launch total, which the lane
+// stores to out[b].  Critical path after the count: two returning atomics.
+template <int PCS>
+__device__ __forceinline__ void bins_finish_dense(unsigned int (*pc)[NBINS][64], GTable g, unsigned long long* out) {
+  __shared__ unsigned long long tot[NBINS];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int b = wave; b < NBINS; b += BLOCK / 64) {
+    unsigned long long v = 0;
+#pragma unroll
+    for (int w = 0; w < PCS; ++w) v += pc[w][b][lane];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) tot[b] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < DBINS) {
+    const uint32_t b = threadIdx.x;
+    const uint32_t row = blockIdx.x & (NBROW - 1);
+    const uint32_t rows = gridDim.x < NBROW ? gridDim.x : NBROW;
+    const uint32_t in_row = (gridDim.x - row + NBROW - 1) / NBROW;
+    const unsigned long long v = (1ull << DARR_SHIFT) | tot[b];
+    unsigned long long* w = &g.dbins[row * BSTRIDE + b];
+    const unsigned long long old = __hip_atomic_fetch_add(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((old >> DARR_SHIFT) == in_row - 1) {
+      __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long v2 = (1ull << DARR_SHIFT) | ((old + v) & DCNT_MASK);
+      unsigned long long* t = &g.dtot[b];
+      const unsigned long long old2 = __hip_atomic_fetch_add(t, v2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((old2 >> DARR_SHIFT) == rows - 1) {
+        __hip_atomic_store(t, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        out[b] = (old2 + v2) & DCNT_MASK;
+      }
+    }
+    if (b == BIN_BAD && tot[BIN_BAD]) atomicOr(&g.flags[1], 1u);
+  }
+}
+
 // Tail of a fused count+export launch, run by the last workgroup to finish:
 // fold the direct bins of all replicas (equal keys merged), write the
 // canonical table -- distinct keys ascending, then (~0, 0) up to `cap` --
@@ -268,23 +314,27 @@ __device__ void bins_export_tail(const Model& m, GTable g, unsigned long long* o
   }
 }
 
-// Export arguments of a fused launch (FUSE: the last workgroup to finish
-// writes the canonical table and empties the histogram).
+// What a launch does after counting: TAIL_NONE accumulates into the
+// handle's bins; TAIL_EXPORT (fused count + export) -- the last workgroup to
+// finish writes the canonical table and empties the histogram; TAIL_DENSE
+// writes this launch's dense counts to `dense` (bins_finish_dense).
+enum : int { TAIL_NONE = 0, TAIL_EXPORT = 1, TAIL_DENSE = 2 };
 struct ExportArgs {
   unsigned long long* keys;
   unsigned long long* counts;
   uint64_t cap;
   unsigned int* nout;
+  unsigned long long* dense;
 };
 
 // PCS: sets of lane counters per workgroup (waves share a set: ds_add is
 // atomic and a wave's 64 lanes still hit 64 distinct banks), so LDS per
 // workgroup is PCS * 5 KiB.
-template <int MODE, int ABL = 0, int UNR = UNROLL, bool NT = false, bool FUSE = false, int PCS = 1>
+template <int MODE, int ABL = 0, int UNR = UNROLL, bool NT = false, int TAIL = TAIL_NONE, int PCS = 1>
 __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t* __restrict__ smp, uint64_t n,
                                                         const uint64_t* __restrict__ head, int has_head, GTable g,
                                                         ExportArgs ex) {
-  static_assert(!FUSE || MODE != GENERIC, "fused export needs the direct bins");
+  static_assert(TAIL == TAIL_NONE || MODE != GENERIC, "fused export and dense output need the direct bins");
   constexpr bool BINS = MODE != GENERIC;
   __shared__ unsigned long long tk[BINS ? 1 : TCAP];
   __shared__ unsigned int tc[BINS ? 1 : TCAP];
@@ -404,9 +454,13 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
     if (sink == 0x5EED5EED5EED5EEDull) atomicOr(&g.flags[2], 1u);  // keeps the ablated work alive
     return;
   }
+  if (TAIL == TAIL_DENSE) {
+    bins_finish_dense<PCS>(pc, g, ex.dense);
+    return;
+  }
   if (BINS) bins_finish<PCS>(pc, g);
   else bt_finish(wc, bt, g);
-  if (FUSE) {
+  if (TAIL == TAIL_EXPORT) {
     // Arrival count without fences: every bin update above is an agent-scope
     // atomic RMW issued by wave 0 (threads 0..18), performed at the coherent
     // point; once the wave's vmcnt drains they are visible to every XCD, and
@@ -692,19 +746,27 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
   const int a = abl ? atoi(abl) : 0, u = unr ? atoi(unr) : UNROLL;
   const bool nt = ntv ? ntv[0] == '1' : HOT_NT;
   const bool pc4 = pcs && pcs[0] == '4';
-  if (fuse) {
-    if (m.p2 && u == 1 && nt) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, 1, true, true);
-    else if (m.p2 && u == 1) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, 1, false, true);
-    else if (m.p2 && nt) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, UNROLL, true, true);
-    else if (m.p2) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, UNROLL, false, true);
-    else PLUSS_LAUNCH_HOT(*fuse, FAST, 0, UNROLL, HOT_NT, true);
+  if (fuse && fuse->dense) {
+    if (m.p2 && u == 1) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, 1, true, TAIL_DENSE);
+    else if (m.p2 && !nt) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, UNROLL, false, TAIL_DENSE);
+    else if (m.p2) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, UNROLL, true, TAIL_DENSE);
+    else PLUSS_LAUNCH_HOT(*fuse, FAST, 0, UNROLL, HOT_NT, TAIL_DENSE);
     PLUSS_HIP_CHECK(hipGetLastError());
     return PLUSS_OK;
   }
-  const ExportArgs ex{nullptr, nullptr, 0, nullptr};
+  if (fuse) {
+    if (m.p2 && u == 1 && nt) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, 1, true, TAIL_EXPORT);
+    else if (m.p2 && u == 1) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, 1, false, TAIL_EXPORT);
+    else if (m.p2 && nt) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, UNROLL, true, TAIL_EXPORT);
+    else if (m.p2) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, UNROLL, false, TAIL_EXPORT);
+    else PLUSS_LAUNCH_HOT(*fuse, FAST, 0, UNROLL, HOT_NT, TAIL_EXPORT);
+    PLUSS_HIP_CHECK(hipGetLastError());
+    return PLUSS_OK;
+  }
+  const ExportArgs ex{nullptr, nullptr, 0, nullptr, nullptr};
   if (!m.fast) ctx->tables_dirty = true;
   if (m.fast && m.p2 && (a || u != UNROLL || nt != HOT_NT || pc4)) {
-    if (pc4) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, false, false, 4);
+    if (pc4) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, false, TAIL_NONE, 4);
     else if (a == 1) PLUSS_LAUNCH_HOT(ex, FAST_P2, 1, UNROLL, false);
     else if (a == 2) PLUSS_LAUNCH_HOT(ex, FAST_P2, 2, UNROLL, false);
     else if (u == 1) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, 1, false);
@@ -730,11 +792,25 @@ int launch_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, h
 int launch_sampled_hist_export(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, unsigned long long* d_keys,
                                unsigned long long* d_counts, uint64_t cap, hipStream_t s) {
   if (ctx->m.fast && !ctx->tables_dirty) {
-    const ExportArgs ex{d_keys, d_counts, cap, ctx->d_exp_n};
+    const ExportArgs ex{d_keys, d_counts, cap, ctx->d_exp_n, nullptr};
     return hot_launch(ctx, d_samples, n, s, &ex, "pluss_dev_sampled_hist_export");
   }
   if (int rc = hot_launch(ctx, d_samples, n, s, nullptr, "pluss_dev_sampled_hist_export")) return rc;
   return launch_export(ctx, d_keys, d_counts, cap, s, true);
+}
+
+int launch_sampled_hist_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, unsigned long long* d_counts,
+                              hipStream_t s) {
+  if (!ctx->m.fast) {
+    set_error("pluss_dev_sampled_hist_dense: needs N % (cls/ds) == 0 (a dense (ref, case) histogram)");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (((uintptr_t)d_counts & 7u) != 0) {
+    set_error("pluss_dev_sampled_hist_dense: counts buffer must be 8-byte aligned");
+    return PLUSS_ERR_INPUT;
+  }
+  const ExportArgs ex{nullptr, nullptr, 0, nullptr, d_counts};
+  return hot_launch(ctx, d_samples, n, s, &ex, "pluss_dev_sampled_hist_dense");
 }
 
 int launch_fulltrace(pluss_ctx* ctx, hipStream_t s) {

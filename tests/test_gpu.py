@@ -38,6 +38,16 @@ def oracle_clean_hist(orc, c, samples, thr_variant=0):
     return out
 
 
+def closed_form_hist(N, T, CS, samples):
+    """{(ref, kind, ri): count} of a list from the closed forms (N % 8 == 0 shapes)."""
+    refs, c0, c1, c2 = P.unpack_array(samples)
+    ri = closed_form_ri(N, T, CS, 8, refs, c0, c1, c2)
+    kind = ((refs == 3) & (ri > 0) & (2 * ri > (4 * N + 2) * N)).astype(np.int64)
+    keys = (refs * 4 + kind) * (1 << 40) + (ri + 2)
+    u, cnt = np.unique(keys, return_counts=True)
+    return {(P.REFS[int(k >> 42)], int((k >> 40) & 3), int(k & ((1 << 40) - 1)) - 2): int(n) for k, n in zip(u, cnt)}
+
+
 def all_samples(orc, smp):
     return np.concatenate([orc.pack_array(ref, smp[ref]) for ref in orc.REFS])
 
@@ -274,6 +284,96 @@ def test_fused_count_and_export(orc, N, T, CS):
         ctx.sampled_hist_export(buf.data_ptr() + 8, total, k.data_ptr(), n.data_ptr(), 4096, stream)
         torch.cuda.synchronize()
         assert as_hist(k, n).bins == want
+
+
+@pytest.mark.parametrize("N,T,CS", [(256, 4, 4), (96, 3, 3)], ids=["fast_p2", "fast"])
+def test_dense_pass(orc, N, T, CS):
+    """pluss_dev_sampled_hist_dense (one launch, dense (ref, case) counts) ==
+    the oracle, pass after pass (the in-kernel state is left zeroed), over
+    grids of 1..1024 workgroups (1..64 bin rows, uneven rows), unaligned and
+    odd-length lists, an empty list, malformed samples; and it leaves the
+    handle's accumulating histogram alone."""
+    torch = pytest.importorskip("torch")
+    c = cfg(N, T, CS)
+    counts = P.default_counts(N, 400000)  # 391 workgroups by default: 64 rows of 6-7
+    host = np.concatenate([P.expand_samples(c, 0x5EED0004, r, 0, counts[r]) for r in range(6)])
+    total = len(host)
+    buf = torch.from_numpy(np.concatenate([host[:1], host]).view(np.int64)).cuda()
+    stream = torch.cuda.current_stream().cuda_stream
+    want = closed_form_hist(N, T, CS, host)
+    sub = host[::97]  # the closed forms against the stepping oracle on a subsample
+    assert closed_form_hist(N, T, CS, sub) == oracle_clean_hist(orc, orc.cfg(N, T, CS), sub)
+
+    def out():
+        return torch.full((P.DENSE_BINS + 2,), 7, dtype=torch.int64, device="cuda")
+
+    def run(ctx, ptr, n):
+        d = out()
+        ctx.sampled_hist_dense(ptr, n, d.data_ptr(), stream)
+        torch.cuda.synchronize()
+        v = d.cpu().numpy()
+        assert v[P.DENSE_BINS + 1] == 7  # nothing written past the vector
+        return v
+
+    with P.Context(c) as ctx:
+        ctx.reset(stream)
+        ctx.sampled_hist(buf.data_ptr() + 8, 1000, stream)  # accumulating histogram: untouched by dense passes
+        first = None
+        try:
+            for grid in ("", "1", "3", "64", "65", "200", "1024"):
+                if grid:
+                    os.environ["PLUSS_GRID"] = grid
+                else:
+                    os.environ.pop("PLUSS_GRID", None)
+                for _ in range(2):
+                    v = run(ctx, buf.data_ptr() + 8, total)
+                    assert v[P.DENSE_BINS] == 0
+                    assert P.hist_from_dense(c, v).bins == want, grid
+                    first = v if first is None else first
+                    assert (v == first).all()
+        finally:
+            os.environ.pop("PLUSS_GRID", None)
+        v = run(ctx, buf.data_ptr(), total + 1)  # 8-byte aligned (peeled head), odd length
+        assert P.hist_from_dense(c, v).total() == total + 1
+        for n in (0, 1, 2, 3):
+            v = run(ctx, buf.data_ptr() + 8, n)
+            assert P.hist_from_dense(c, v).bins == oracle_clean_hist(orc, orc.cfg(N, T, CS), host[:n])
+        assert (run(ctx, buf.data_ptr() + 8, 0)[:P.DENSE_BINS + 1] == 0).all()
+        assert ctx.fetch().bins == oracle_clean_hist(orc, orc.cfg(N, T, CS), host[:1000])
+        bad = torch.from_numpy(np.array([P.pack("C3", 1, 2, 3), P.pack("A0", N, 0, 0), 7 << 60, 0], np.uint64)
+                               .view(np.int64)).cuda()
+        v = run(ctx, bad.data_ptr(), 4)
+        assert v[P.DENSE_BINS] == 2 and v[:P.DENSE_BINS].sum() == 2
+        with pytest.raises(P.PlussError, match="PLUSS_ERR_INPUT"):
+            ctx.fetch()
+        ctx.reset(stream)
+        assert (run(ctx, buf.data_ptr() + 8, total) == first).all()  # healthy after the error
+    with P.Context(cfg(100, 3, 5)) as g:
+        with pytest.raises(P.PlussError, match="PLUSS_ERR_CONFIG"):
+            g.sampled_hist_dense(buf.data_ptr(), 10, out().data_ptr(), stream)
+
+
+def test_dense_pass_config2_full_size():
+    """BASELINE config 2 (N=1024, T=8, 2^24 samples): the bench's step output
+    equals the closed-form histogram of the list."""
+    torch = pytest.importorskip("torch")
+    N, T = 1024, 8
+    c = cfg(N, T)
+    counts = P.default_counts(N, 1 << 24)
+    buf = torch.empty(1 << 24, dtype=torch.int64, device="cuda")
+    d = torch.zeros(P.DENSE_BINS + 1, dtype=torch.int64, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    with P.Context(c) as ctx:
+        off = 0
+        for r in range(6):
+            ctx.expand(0x5EED0001, r, 0, counts[r], buf.data_ptr() + 8 * off, stream)
+            off += counts[r]
+        for _ in range(3):
+            ctx.sampled_hist_dense(buf.data_ptr(), 1 << 24, d.data_ptr(), stream)
+        torch.cuda.synchronize()
+    v = d.cpu().numpy()
+    assert v[P.DENSE_BINS] == 0
+    assert P.hist_from_dense(c, v).bins == closed_form_hist(N, T, 4, buf.cpu().numpy().view(np.uint64))
 
 
 def test_long_windows_config4_t64(orc):

@@ -168,3 +168,23 @@ def test_config_errors_are_reported_without_gpu():
         default_counts(1, 100)
     with pytest.raises(KeyError):
         SamplerConfig(mode="bogus").to_c()
+
+
+def test_dense_keys_follow_closed_forms_without_gpu():
+    """pluss_dense_keys (host-only): bin ref*3+case holds the closed-form RI of
+    that case, B0's long reuse classed share by the r10 threshold."""
+    from pluss_sampler_optimization_amd import PlussError, REFS, SamplerConfig, dense_keys
+    for N, T in ((1024, 8), (128, 4), (2048, 64)):
+        S, W = 4 * N + 2, 8
+        want = {("C0", 0): 1, ("C1", 0): 3, ("C2", 0): 1, ("C3", 0): 3, ("C3", 1): 1, ("C3", 2): -1,
+                ("A0", 0): 4, ("A0", 1): S - 4 * (W - 1), ("A0", 2): -1,
+                ("B0", 0): S, ("B0", 1): N * S - (W - 1) * S, ("B0", 2): -1}
+        keys = dense_keys(SamplerConfig(n=N, threads=T))
+        assert len(keys) == 18
+        for b, k in enumerate(keys):
+            ref, case = REFS[b // 3], b % 3
+            ri = want.get((ref, case), want.get((ref, 0)))
+            kind = 1 if ref == "B0" and ri > 0 and 2 * ri > (4 * N + 2) * N else 0
+            assert k == (b // 3) << 60 | kind << 56 | (ri + 2), (N, ref, case)
+    with pytest.raises(PlussError, match="PLUSS_ERR_CONFIG"):
+        dense_keys(SamplerConfig(n=100, threads=3, chunk=5))  # N % (cls/ds) != 0

@@ -65,6 +65,19 @@ def main():
         for k in ("PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT"):
             os.environ.pop(k, None)
 
+        dense = torch.zeros(P.DENSE_BINS + 1, dtype=torch.int64, device=dev)
+        for v in [{}, dict(PLUSS_GRID="512"), dict(PLUSS_GRID="768"), dict(PLUSS_NT="0"), dict(PLUSS_UNROLL="1")]:
+            for k in ("PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT"):
+                os.environ.pop(k, None)
+            os.environ.update(v)
+            ms = timeit(lambda: ctx.sampled_hist_dense(buf.data_ptr(), total, dense.data_ptr(), s.cuda_stream), s)
+            print(json.dumps({"samples": total, "dense": v, "dense_ms": ms, "GBps": 8 * total / ms / 1e6}),
+                  flush=True)
+        for k in ("PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT"):
+            os.environ.pop(k, None)
+        torch.cuda.synchronize()
+        assert int(dense[:P.DENSE_BINS].sum()) == total and int(dense[P.DENSE_BINS]) == 0
+
         def two():
             ctx.sampled_hist(buf.data_ptr(), total, s.cuda_stream)
             ctx.export_reset(keys.data_ptr(), cnts.data_ptr(), 4096, s.cuda_stream)
