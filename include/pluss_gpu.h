@@ -184,9 +184,7 @@ int pluss_dev_faithful_shard_hist(pluss_ctx *ctx, uint64_t cut, uint64_t next_fi
 
 /* synchronise and copy the handle's histogram into a host pluss_hist */
 int pluss_hist_fetch(pluss_ctx *ctx, pluss_hist *out);
-/* merge (key,count) pairs on the host into a pluss_hist: canonical tables of
-   several GPUs, or pluss_dense_keys + a dense count vector; pairs with an
-   empty key or a zero count are skipped */
+/* merge canonical (key,count) tables on the host into a pluss_hist */
 int pluss_hist_from_tables(const uint64_t *keys, const uint64_t *counts, uint64_t n_pairs, pluss_hist *out);
 
 #ifdef __cplusplus

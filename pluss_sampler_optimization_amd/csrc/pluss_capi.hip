@@ -317,7 +317,7 @@ int pluss_hist_from_tables(const uint64_t* keys, const uint64_t* counts, uint64_
   if (!out || (n_pairs && (!keys || !counts))) return PLUSS_ERR_CONFIG;
   std::map<uint64_t, uint64_t> acc;
   for (uint64_t i = 0; i < n_pairs; ++i)
-    if (keys[i] != KEY_EMPTY && keys[i] != KEY_NONE && counts[i]) acc[keys[i]] += counts[i];
+    if (keys[i] != KEY_EMPTY && keys[i] != KEY_NONE) acc[keys[i]] += counts[i];
   out->n_entries = acc.size();
   if (acc.size() > out->capacity) {
     set_error("pluss_hist_from_tables: output capacity too small");
