@@ -180,9 +180,12 @@ def dense_keys(cfg):
 
 
 def hist_from_dense(cfg, counts):
-    """Histogram of a dense count vector (DENSE_BINS counts, optionally followed by the malformed count)."""
+    """Histogram of a dense count vector (DENSE_BINS counts, optionally followed by the malformed count).
+    Bins with a zero count are not histogram keys (unlike faithful mode's cold
+    bin, which r10 creates with += 0 at r10:196 and pluss_hist_from_tables keeps)."""
     c = np.asarray(counts).reshape(-1)[:DENSE_BINS].astype(np.int64).view(np.uint64)
-    return hist_from_tables(np.array(dense_keys(cfg), dtype=np.uint64), c)
+    k = np.array(dense_keys(cfg), dtype=np.uint64)
+    return hist_from_tables(k[c != 0], c[c != 0])
 
 
 def hist_from_tables(keys, counts):
