@@ -14,6 +14,7 @@
 //   k_expand        the sample-list bijection (pluss_model.h).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "pluss_device.h"
@@ -151,16 +152,13 @@ __device__ __forceinline__ void sample_bins(const Model& m, const uint64_t (&xs)
   for (int k = 0; k < K; ++k) bin[k] = sample_bin_any<P2>(m, xs[k], ok[k]);
 }
 
-// Block-wide reduction of the per-lane bin counters; each bin with a count is
-// added to its direct counter in row blockIdx % 64 (workgroups are dealt
-// round-robin over the 8 XCDs, so a row is hit from one XCD, by 1/64 of the
-// grid: 16 adds per address at 1024 workgroups).
+// Workgroup totals of the DBINS bins (18 (ref, case) bins + malformed) from
+// the per-lane LDS counters of k_sampled_hist.
 template <int PCS>
-__device__ __forceinline__ void bins_finish(unsigned int (*pc)[NBINS][64], GTable g) {
-  __shared__ unsigned long long tot[NBINS];
+__device__ __forceinline__ void reduce_lane_counters(unsigned int (*pc)[NBINS][64], unsigned long long* tot) {
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int b = wave; b < NBINS; b += BLOCK / 64) {
+  for (int b = wave; b < (int)DBINS; b += BLOCK / 64) {
     unsigned long long v = 0;
 #pragma unroll
     for (int w = 0; w < PCS; ++w) v += pc[w][b][lane];
@@ -169,6 +167,13 @@ __device__ __forceinline__ void bins_finish(unsigned int (*pc)[NBINS][64], GTabl
     if (lane == 0) tot[b] = v;
   }
   __syncthreads();
+}
+
+// Accumulating tail: each bin with a count is added to its direct counter in
+// row blockIdx % 64 (workgroups are dealt round-robin over the 8 XCDs, so a
+// row is hit from one XCD, by 1/64 of the grid: 16 adds per address at 1024
+// workgroups).  `tot` is in LDS, complete (after a barrier).
+__device__ __forceinline__ void tail_accumulate(const unsigned long long* tot, GTable g) {
   if (threadIdx.x < 18 && tot[threadIdx.x])
     atomicAdd(&g.bins[(blockIdx.x & (NBROW - 1)) * BSTRIDE + threadIdx.x], tot[threadIdx.x]);
   if (threadIdx.x == BIN_BAD && tot[BIN_BAD]) atomicOr(&g.flags[1], 1u);
@@ -184,20 +189,7 @@ __device__ __forceinline__ void bins_finish(unsigned int (*pc)[NBINS][64], GTabl
 // (1 << DARR_SHIFT | row total) to the bin's word in `dtot`; the add there
 // that returns arrivals == rows - 1 holds the launch total, which the lane
 // stores to out[b].  Critical path after the count: two returning atomics.
-template <int PCS>
-__device__ __forceinline__ void bins_finish_dense(unsigned int (*pc)[NBINS][64], GTable g, unsigned long long* out) {
-  __shared__ unsigned long long tot[NBINS];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int b = wave; b < NBINS; b += BLOCK / 64) {
-    unsigned long long v = 0;
-#pragma unroll
-    for (int w = 0; w < PCS; ++w) v += pc[w][b][lane];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) tot[b] = v;
-  }
-  __syncthreads();
+__device__ __forceinline__ void tail_dense(const unsigned long long* tot, GTable g, unsigned long long* out) {
   if (threadIdx.x < DBINS) {
     const uint32_t b = threadIdx.x;
     const uint32_t row = blockIdx.x & (NBROW - 1);
@@ -317,7 +309,7 @@ __device__ void bins_export_tail(const Model& m, GTable g, unsigned long long* o
 // What a launch does after counting: TAIL_NONE accumulates into the
 // handle's bins; TAIL_EXPORT (fused count + export) -- the last workgroup to
 // finish writes the canonical table and empties the histogram; TAIL_DENSE
-// writes this launch's dense counts to `dense` (bins_finish_dense).
+// writes this launch's dense counts to `dense` (tail_dense).
 enum : int { TAIL_NONE = 0, TAIL_EXPORT = 1, TAIL_DENSE = 2 };
 struct ExportArgs {
   unsigned long long* keys;
@@ -326,6 +318,35 @@ struct ExportArgs {
   unsigned int* nout;
   unsigned long long* dense;
 };
+
+// Fused export, after tail_accumulate: an arrival count without fences --
+// every bin update is an agent-scope atomic RMW issued by wave 0 (threads
+// 0..18), performed at the coherent point; once the wave's vmcnt drains they
+// are visible to every XCD, and the last arriver reads them back with
+// agent-scope atomic loads (bins_export_tail).  (A __threadfence here costs
+// an L2 writeback + invalidate per workgroup, measured 4x the kernel's run
+// time.)
+__device__ __forceinline__ void tail_export(const Model& m, GTable g, const ExportArgs& ex) {
+  __shared__ unsigned int amlast;
+  if (threadIdx.x == 0) {
+    // two-level arrival (one counter per bin row, then one per grid) so the
+    // simultaneous finishes of ~1000 workgroups do not serialise on a single
+    // address
+    const uint32_t row = blockIdx.x & (NBROW - 1);
+    const uint32_t rows = gridDim.x < NBROW ? gridDim.x : NBROW;
+    const uint32_t in_row = (gridDim.x - row + NBROW - 1) / NBROW;
+    unsigned long long* rc = &g.bins[row * BSTRIDE + BARRIVE];
+    __builtin_amdgcn_s_waitcnt(0);
+    bool last = false;
+    if (__hip_atomic_fetch_add(rc, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_row - 1) {
+      __hip_atomic_store(rc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = __hip_atomic_fetch_add(&g.flags[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == rows - 1;
+    }
+    amlast = last;
+  }
+  __syncthreads();
+  if (amlast) bins_export_tail(m, g, ex.keys, ex.counts, ex.cap, ex.nout);
+}
 
 // PCS: sets of lane counters per workgroup (waves share a set: ds_add is
 // atomic and a wave's 64 lanes still hit 64 distinct banks), so LDS per
@@ -454,39 +475,167 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
     if (sink == 0x5EED5EED5EED5EEDull) atomicOr(&g.flags[2], 1u);  // keeps the ablated work alive
     return;
   }
-  if (TAIL == TAIL_DENSE) {
-    bins_finish_dense<PCS>(pc, g, ex.dense);
-    return;
+  if (BINS) {
+    __shared__ unsigned long long tot[DBINS];
+    reduce_lane_counters<PCS>(pc, tot);
+    if (TAIL == TAIL_DENSE) tail_dense(tot, g, ex.dense);
+    else tail_accumulate(tot, g);
+  } else {
+    bt_finish(wc, bt, g);
   }
-  if (BINS) bins_finish<PCS>(pc, g);
-  else bt_finish(wc, bt, g);
-  if (TAIL == TAIL_EXPORT) {
-    // Arrival count without fences: every bin update above is an agent-scope
-    // atomic RMW issued by wave 0 (threads 0..18), performed at the coherent
-    // point; once the wave's vmcnt drains they are visible to every XCD, and
-    // the last arriver reads them back with agent-scope atomic loads.  (A
-    // __threadfence here costs an L2 writeback + invalidate per workgroup,
-    // measured 4x the kernel's run time.)
-    __shared__ unsigned int amlast;
-    if (threadIdx.x == 0) {
-      // two-level arrival (one counter per bin row, then one per grid) so
-      // the simultaneous finishes of ~1000 workgroups do not serialise on
-      // a single address
-      const uint32_t row = blockIdx.x & (NBROW - 1);
-      const uint32_t rows = gridDim.x < NBROW ? gridDim.x : NBROW;
-      const uint32_t in_row = (gridDim.x - row + NBROW - 1) / NBROW;
-      unsigned long long* rc = &g.bins[row * BSTRIDE + BARRIVE];
-      __builtin_amdgcn_s_waitcnt(0);
-      bool last = false;
-      if (__hip_atomic_fetch_add(rc, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_row - 1) {
-        __hip_atomic_store(rc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = __hip_atomic_fetch_add(&g.flags[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == rows - 1;
-      }
-      amlast = last;
+  if (TAIL == TAIL_EXPORT) tail_export(m, g, ex);
+}
+
+// --------------------------------------------------- HOT (FAST shapes) --
+// k_count: the same pass as k_sampled_hist's FAST path, counted by ballots.
+// A "slot" is one sample per lane (64 per wave).  The wave finds the
+// references present in the slot (almost always one: lists are per-reference
+// blocks), and for each one evaluates only that reference's case conditions
+// as lane predicates; their ballots, masked and popcounted, are added to
+// per-wave counters held in scalar registers.  So a sample costs its field
+// extraction and 0-3 compares (the rest is scalar work per 64 samples), and
+// there are no per-sample LDS atomics.  Samples are read as 16-byte pairs by
+// buffer loads with 32-bit offsets inside windows of up to 2^27 pairs; lanes
+// past the end read zeros (range check) and are masked.
+constexpr uint64_t CWIN = 1ull << 27;  // pairs per buffer window (2 GiB)
+
+// bins: C0 0, C1 3, A0 6/7/8, B0 9/10/11, C2 12, C3 15/16/17, malformed 18 (= ref*3 + case).
+// Counts live in one lane-indexed VGPR per wave: lane b holds bin b.
+//
+// Count the lanes `mr` of a slot whose reference is the wave-uniform `r`.
+template <bool P2, bool NP2>
+__device__ __forceinline__ void count_ref(const Model& m, uint32_t r, uint64_t mr, uint32_t lo, uint32_t hi,
+                                          uint32_t& acc) {
+  const uint32_t c2 = lo & 0xFFFFFu;
+  const uint32_t c0 = (hi >> 8) & 0xFFFFFu;
+  bool bad;
+  if (NP2) {
+    bad = ((lo & m.badlo) | (hi & m.badhi)) != 0u;
+  } else {
+    const uint32_t c1 = __builtin_amdgcn_alignbit(hi, lo, 20) & 0xFFFFFu;
+    bad = (c0 > c1 ? (c0 > c2 ? c0 : c2) : (c1 > c2 ? c1 : c2)) >= m.N;
+  }
+  const uint64_t mb = r > 5 ? mr : (__ballot(bad) & mr);
+  mr &= ~mb;
+  const uint32_t nr = (uint32_t)__popcll(mr);
+  const uint32_t Wm1 = m.W - 1;
+  uint64_t a = mr, b = 0;  // lanes of case 0 and case 1 (case 2: the rest); C0, C1, C2 are always case 0
+  if (r == C3) {  // case 0: c2+1 < N; case 1: c1 not the last element of its line
+    const uint32_t c1 = __builtin_amdgcn_alignbit(hi, lo, 20) & 0xFFFFFu;
+    const bool c1last = P2 ? (lo & (m.wmask << 20)) == (m.wmask << 20) : fmod_(c1, m.dW) == Wm1;
+    a = __ballot(c2 + 1 < m.N) & mr;
+    b = __ballot(!c1last) & mr & ~a;
+  } else if (r == A0) {  // case 0: c2 not the last element of its line; case 1: c1+1 < N
+    const uint32_t c1 = __builtin_amdgcn_alignbit(hi, lo, 20) & 0xFFFFFu;
+    const bool c2last = P2 ? (lo & m.wmask) == m.wmask : fmod_(c2, m.dW) == Wm1;
+    a = __ballot(!c2last) & mr;
+    b = __ballot(c1 + 1 < m.N) & mr & ~a;
+  } else if (r == B0) {  // case 0: c1 not the last element of its line; case 1: the thread owns a later row
+    const uint32_t c1 = __builtin_amdgcn_alignbit(hi, lo, 20) & 0xFFFFFu;
+    const bool c1last = P2 ? (lo & (m.wmask << 20)) == (m.wmask << 20) : fmod_(c1, m.dW) == Wm1;
+    const uint32_t p = P2 ? (c0 & m.csmask) : fmod_(c0, m.dCS);
+    const uint32_t nxt = c0 + 1 + (p + 1 == m.CS ? m.tcs : 0u);
+    a = __ballot(!c1last) & mr;
+    b = __ballot(nxt < m.N) & mr & ~a;
+  }
+  // lane-indexed add of a wave-uniform count: compare, select, add
+  const uint32_t lane = __lane_id();
+  auto bump = [&acc, lane](uint32_t bin, uint32_t v) { acc += lane == bin ? v : 0u; };
+  if (r <= 5 && nr) {
+    const uint32_t na = (uint32_t)__popcll(a);
+    bump(r * 3, na);
+    if (r == C3 || r == A0 || r == B0) {
+      const uint32_t nb = (uint32_t)__popcll(b);
+      bump(r * 3 + 1, nb);
+      bump(r * 3 + 2, nr - na - nb);
     }
-    __syncthreads();
-    if (amlast) bins_export_tail(m, g, ex.keys, ex.counts, ex.cap, ex.nout);
   }
+  if (mb) bump(BIN_BAD, (uint32_t)__popcll(mb));
+}
+
+// One slot: the wave's first live lane names the reference; lanes with
+// another reference (a slot that straddles two per-reference blocks, or a
+// mixed list) are counted one reference at a time.
+template <bool P2, bool NP2>
+__device__ __forceinline__ void count_slot(const Model& m, uint64_t x, bool ok, uint32_t& acc) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t ref = hi >> 28;
+  uint64_t live = __ballot(ok);
+  if (live == 0) return;
+  const uint32_t r0 = __builtin_amdgcn_readlane(ref, (int)__builtin_ctzll(live));
+  const uint64_t m0 = __ballot(ref == r0) & live;
+  count_ref<P2, NP2>(m, r0, m0, lo, hi, acc);
+  live &= ~m0;
+  while (live) {
+    const uint32_t r = __builtin_amdgcn_readlane(ref, (int)__builtin_ctzll(live));
+    const uint64_t mr = __ballot(ref == r) & live;
+    live &= ~mr;
+    count_ref<P2, NP2>(m, r, mr, lo, hi, acc);
+  }
+}
+
+// Add the wave's lane-indexed counts to the workgroup's LDS totals.
+__device__ __forceinline__ void flush_counts(uint32_t& acc, unsigned long long* tot) {
+  const uint32_t lane = __lane_id();
+  if (lane < DBINS && acc) atomicAdd(&tot[lane], (unsigned long long)acc);
+  acc = 0;
+}
+
+template <bool P2, bool NP2, bool NT, int TAIL, int UNR = UNROLL>
+__global__ __launch_bounds__(BLOCK) void k_count(Model m, const uint64_t* __restrict__ smp, uint64_t n,
+                                                 const uint64_t* __restrict__ head, int has_head, GTable g,
+                                                 ExportArgs ex) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  __shared__ unsigned long long tot[DBINS];
+  if (threadIdx.x < DBINS) tot[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t acc = 0;  // lane b: count of bin b
+  const uint64_t npairs = n >> 1;
+  const uint32_t step = gridDim.x * (uint32_t)(BLOCK * UNR);
+  constexpr int AUX = NT ? 2 : 0;  // nt: the list is streamed once per pass
+  for (uint64_t w0 = 0; w0 < npairs; w0 += CWIN) {
+    const uint32_t wn = (uint32_t)(npairs - w0 < CWIN ? npairs - w0 : CWIN);
+    const uint64_t* wp = smp + 2 * w0;
+    const uint32_t plo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)wp);
+    const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)wp >> 32));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((uintptr_t)phi << 32) | plo), 0, (int)__builtin_amdgcn_readfirstlane(wn * 16u), 0x00020000);
+    uint32_t base = blockIdx.x * (uint32_t)(BLOCK * UNR);
+    u32x4 x[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      x[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           rs, (int)((base + u * BLOCK + threadIdx.x) * 16u), 0, AUX));
+    for (; base < wn; base += step) {
+      u32x4 y[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)  // the next step's pairs (past the window: zeros)
+        y[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rs, (int)((base + step + u * BLOCK + threadIdx.x) * 16u), 0, AUX));
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const bool ok = base + u * BLOCK + threadIdx.x < wn;
+        count_slot<P2, NP2>(m, ((uint64_t)x[u].y << 32) | x[u].x, ok, acc);
+        count_slot<P2, NP2>(m, ((uint64_t)x[u].w << 32) | x[u].z, ok, acc);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) x[u] = y[u];
+    }
+    flush_counts(acc, tot);  // per window: keeps the 32-bit lane counters from overflowing
+  }
+  if (((n & 1) || has_head) && blockIdx.x == 0 && threadIdx.x < 64) {
+    // odd tail (lane 0) and, for an 8-byte-aligned list, its first sample (lane 1).
+    // `head` always points at valid memory, so a speculated load cannot fault.
+    const bool mine = (threadIdx.x == 0 && (n & 1)) || (threadIdx.x == 1 && has_head);
+    const uint64_t* src = (threadIdx.x == 0 && n) ? smp + (n - 1) : head;
+    const uint64_t xs = mine ? *src : 0;
+    count_slot<P2, NP2>(m, xs, mine, acc);
+    flush_counts(acc, tot);
+  }
+  __syncthreads();
+  if (TAIL == TAIL_DENSE) tail_dense(tot, g, ex.dense);
+  else tail_accumulate(tot, g);
+  if (TAIL == TAIL_EXPORT) tail_export(m, g, ex);
 }
 
 // ----------------------------------------------------------- full trace --
@@ -542,8 +691,13 @@ __global__ __launch_bounds__(BLOCK) void k_fulltrace(Model m, GTable g) {
       }
     }
   }
-  if (BINS) bins_finish<1>(pc, g);
-  else bt_finish(wc, bt, g);
+  if (BINS) {
+    __shared__ unsigned long long tot[DBINS];
+    reduce_lane_counters<1>(pc, tot);
+    tail_accumulate(tot, g);
+  } else {
+    bt_finish(wc, bt, g);
+  }
 }
 
 // --------------------------------------------------------------- export --
@@ -735,44 +889,70 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
 #define PLUSS_LAUNCH_HOT(EX, ...)                                                                                  \
   hipLaunchKernelGGL((k_sampled_hist<__VA_ARGS__>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n, head, has_head, g, \
                      EX)
-  // diagnostics only (tools/ablate.py): PLUSS_ABLATE=1|2, PLUSS_UNROLL=1|4|8, PLUSS_NT=0|1, PLUSS_GRID=<blocks>,
-  // PLUSS_PCS=4 (a counter set per wave); the fused launch honours UNROLL=1|2, NT and GRID
+  // diagnostics only (tools/ablate.py): PLUSS_ABLATE=1|2 (loads only / loads + bins, lane-counter kernel),
+  // PLUSS_LEGACY=1 (the lane-counter kernel k_sampled_hist for FAST shapes), PLUSS_UNROLL=1|4,
+  // PLUSS_NT=0|1, PLUSS_GRID=<max blocks>, PLUSS_PCS=4 (legacy: a counter set per wave)
   const char* abl = getenv("PLUSS_ABLATE");
   const char* unr = getenv("PLUSS_UNROLL");
   const char* ntv = getenv("PLUSS_NT");
   const char* grd = getenv("PLUSS_GRID");
   const char* pcs = getenv("PLUSS_PCS");
-  if (grd && atoi(grd) > 0) nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL, atoi(grd));
+  const char* leg = getenv("PLUSS_LEGACY");
+  if (grd && atoi(grd) > 0) nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL, std::min(atoi(grd), 16384));
   const int a = abl ? atoi(abl) : 0, u = unr ? atoi(unr) : UNROLL;
   const bool nt = ntv ? ntv[0] == '1' : HOT_NT;
   const bool pc4 = pcs && pcs[0] == '4';
-  if (fuse && fuse->dense) {
-    if (m.p2 && u == 1) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, 1, true, TAIL_DENSE);
-    else if (m.p2 && !nt) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, UNROLL, false, TAIL_DENSE);
-    else if (m.p2) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, UNROLL, true, TAIL_DENSE);
-    else PLUSS_LAUNCH_HOT(*fuse, FAST, 0, UNROLL, HOT_NT, TAIL_DENSE);
+  const bool legacy = (leg && leg[0] == '1') || a || pc4;
+  const ExportArgs none{nullptr, nullptr, 0, nullptr, nullptr};
+  const ExportArgs& ex = fuse ? *fuse : none;
+  const int tail = fuse ? (fuse->dense ? TAIL_DENSE : TAIL_EXPORT) : TAIL_NONE;
+  if (m.fast && !legacy) {
+#define PLUSS_LAUNCH_COUNT(P2, NP2, NT, UNR)                                                                      \
+  do {                                                                                                           \
+    if (tail == TAIL_DENSE)                                                                                      \
+      hipLaunchKernelGGL((k_count<P2, NP2, NT, TAIL_DENSE, UNR>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n,  \
+                         head, has_head, g, ex);                                                                 \
+    else if (tail == TAIL_EXPORT)                                                                                \
+      hipLaunchKernelGGL((k_count<P2, NP2, NT, TAIL_EXPORT, UNR>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n, \
+                         head, has_head, g, ex);                                                                 \
+    else                                                                                                         \
+      hipLaunchKernelGGL((k_count<P2, NP2, NT, TAIL_NONE, UNR>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n,   \
+                         head, has_head, g, ex);                                                                 \
+  } while (0)
+    if (m.p2 && m.np2 && (nt != HOT_NT || u != UNROLL)) {  // diagnostics
+      if (u == 1) PLUSS_LAUNCH_COUNT(true, true, HOT_NT, 1);
+      else if (u == 4) PLUSS_LAUNCH_COUNT(true, true, HOT_NT, 4);
+      else PLUSS_LAUNCH_COUNT(true, true, !HOT_NT, UNROLL);
+    } else if (m.p2 && m.np2) {
+      PLUSS_LAUNCH_COUNT(true, true, HOT_NT, UNROLL);
+    } else if (m.p2) {
+      PLUSS_LAUNCH_COUNT(true, false, HOT_NT, UNROLL);
+    } else if (m.np2) {
+      PLUSS_LAUNCH_COUNT(false, true, HOT_NT, UNROLL);
+    } else {
+      PLUSS_LAUNCH_COUNT(false, false, HOT_NT, UNROLL);
+    }
+#undef PLUSS_LAUNCH_COUNT
     PLUSS_HIP_CHECK(hipGetLastError());
     return PLUSS_OK;
   }
-  if (fuse) {
-    if (m.p2 && u == 1 && nt) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, 1, true, TAIL_EXPORT);
-    else if (m.p2 && u == 1) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, 1, false, TAIL_EXPORT);
-    else if (m.p2 && nt) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, UNROLL, true, TAIL_EXPORT);
-    else if (m.p2) PLUSS_LAUNCH_HOT(*fuse, FAST_P2, 0, UNROLL, false, TAIL_EXPORT);
-    else PLUSS_LAUNCH_HOT(*fuse, FAST, 0, UNROLL, HOT_NT, TAIL_EXPORT);
+  if (tail == TAIL_DENSE) {  // legacy lane-counter kernel (diagnostics)
+    if (m.p2) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, HOT_NT, TAIL_DENSE);
+    else PLUSS_LAUNCH_HOT(ex, FAST, 0, UNROLL, HOT_NT, TAIL_DENSE);
     PLUSS_HIP_CHECK(hipGetLastError());
     return PLUSS_OK;
   }
-  const ExportArgs ex{nullptr, nullptr, 0, nullptr, nullptr};
+  if (tail == TAIL_EXPORT) {
+    if (m.p2) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, HOT_NT, TAIL_EXPORT);
+    else PLUSS_LAUNCH_HOT(ex, FAST, 0, UNROLL, HOT_NT, TAIL_EXPORT);
+    PLUSS_HIP_CHECK(hipGetLastError());
+    return PLUSS_OK;
+  }
   if (!m.fast) ctx->tables_dirty = true;
-  if (m.fast && m.p2 && (a || u != UNROLL || nt != HOT_NT || pc4)) {
+  if (m.fast && m.p2 && (a || pc4)) {
     if (pc4) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, false, TAIL_NONE, 4);
     else if (a == 1) PLUSS_LAUNCH_HOT(ex, FAST_P2, 1, UNROLL, false);
-    else if (a == 2) PLUSS_LAUNCH_HOT(ex, FAST_P2, 2, UNROLL, false);
-    else if (u == 1) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, 1, false);
-    else if (u == 4) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, 4, false);
-    else if (u == 8) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, 8, false);
-    else PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, !HOT_NT);
+    else PLUSS_LAUNCH_HOT(ex, FAST_P2, 2, UNROLL, false);
   } else if (m.fast && m.p2) {
     PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, HOT_NT);
   } else if (m.fast) {

@@ -69,6 +69,9 @@ struct Model {
   uint64_t A;            // accesses per simulated thread when N % (CS*T) == 0
   FastDiv dCS, dT, dW, dN;
   uint64_t keytab[18];   // fast path: histogram key of (ref, case), case 0/1/2 (see case_fast)
+  uint32_t np2;          // N is a power of two: an index is out of range iff it has a bit in badlo/badhi
+  uint32_t badlo, badhi; // bits of a packed sample's low/high word that hold index bits >= log2(N)
+  uint32_t tcs;          // (T-1)*CS: distance from the last row of a chunk to the thread's next chunk
 };
 
 // Histogram key: ref(4) | kind(4) | (ri + 2)(56).  ri = -1 encodes cold.
@@ -240,6 +243,18 @@ inline Model make_model(uint64_t N, uint64_t T, uint64_t CS, uint64_t DS, uint64
   m.dT = make_fastdiv(m.T);
   m.dW = make_fastdiv(m.W);
   m.dN = make_fastdiv(m.N);
+  // packed-sample range check for N = 2^L: c2 = bits [0,20), c1 = [20,40), c0 = [40,60)
+  m.np2 = (N & (N - 1)) == 0 ? 1u : 0u;
+  m.badlo = m.badhi = 0;
+  if (m.np2) {
+    uint32_t L = 0;
+    while ((1ull << L) < N) ++L;
+    auto bits = [](uint32_t a, uint32_t b) -> uint64_t { return a < b ? (1ull << b) - (1ull << a) : 0ull; };
+    const uint64_t bad = bits(L, 20) | bits(20 + L, 40) | bits(40 + L, 60);
+    m.badlo = (uint32_t)bad;
+    m.badhi = (uint32_t)(bad >> 32);
+  }
+  m.tcs = (uint32_t)((T - 1) * CS);
   // (ref, case) -> key, from the same closed rules as ri_fast
   const int64_t Wm1 = m.W - 1;
   const int64_t ri[6][3] = {

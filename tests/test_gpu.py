@@ -286,7 +286,8 @@ def test_fused_count_and_export(orc, N, T, CS):
         assert as_hist(k, n).bins == want
 
 
-@pytest.mark.parametrize("N,T,CS", [(256, 4, 4), (96, 3, 3)], ids=["fast_p2", "fast"])
+@pytest.mark.parametrize("N,T,CS", [(256, 4, 4), (96, 3, 3), (96, 4, 4), (128, 3, 3)],
+                         ids=["p2_np2", "fast", "p2", "np2"])
 def test_dense_pass(orc, N, T, CS):
     """pluss_dev_sampled_hist_dense (one launch, dense (ref, case) counts) ==
     the oracle, pass after pass (the in-kernel state is left zeroed), over
@@ -320,11 +321,13 @@ def test_dense_pass(orc, N, T, CS):
         ctx.sampled_hist(buf.data_ptr() + 8, 1000, stream)  # accumulating histogram: untouched by dense passes
         first = None
         try:
-            for grid in ("", "1", "3", "64", "65", "200", "1024"):
-                if grid:
+            for grid in ("", "1", "3", "64", "65", "200", "1024", "legacy"):
+                os.environ.pop("PLUSS_GRID", None)
+                os.environ.pop("PLUSS_LEGACY", None)
+                if grid == "legacy":  # the lane-counter kernel (k_sampled_hist) agrees
+                    os.environ["PLUSS_LEGACY"] = "1"
+                elif grid:
                     os.environ["PLUSS_GRID"] = grid
-                else:
-                    os.environ.pop("PLUSS_GRID", None)
                 for _ in range(2):
                     v = run(ctx, buf.data_ptr() + 8, total)
                     assert v[P.DENSE_BINS] == 0
@@ -333,6 +336,7 @@ def test_dense_pass(orc, N, T, CS):
                     assert (v == first).all()
         finally:
             os.environ.pop("PLUSS_GRID", None)
+            os.environ.pop("PLUSS_LEGACY", None)
         v = run(ctx, buf.data_ptr(), total + 1)  # 8-byte aligned (peeled head), odd length
         assert P.hist_from_dense(c, v).total() == total + 1
         for n in (0, 1, 2, 3):
@@ -351,6 +355,43 @@ def test_dense_pass(orc, N, T, CS):
     with P.Context(cfg(100, 3, 5)) as g:
         with pytest.raises(P.PlussError, match="PLUSS_ERR_CONFIG"):
             g.sampled_hist_dense(buf.data_ptr(), 10, out().data_ptr(), stream)
+
+
+@pytest.mark.parametrize("N,T,CS", [(128, 4, 4), (96, 3, 3)], ids=["p2_np2", "fast"])
+def test_shuffled_mixed_reference_lists(orc, N, T, CS):
+    """Lists whose waves hold every reference at once (the per-reference loop of
+    k_count's slot counting) and malformed samples among them: accumulate,
+    fused export and dense passes all equal the oracle."""
+    torch = pytest.importorskip("torch")
+    c = cfg(N, T, CS)
+    counts = P.default_counts(N, 30000)
+    host = np.concatenate([P.expand_samples(c, 0x5EED0005, r, 0, counts[r]) for r in range(6)])
+    rng = np.random.default_rng(7)
+    host = host[rng.permutation(len(host))]
+    want = oracle_clean_hist(orc, orc.cfg(N, T, CS), host)
+    stream = torch.cuda.current_stream().cuda_stream
+    buf = torch.from_numpy(host.view(np.int64)).cuda()
+    d = torch.zeros(P.DENSE_BINS + 1, dtype=torch.int64, device="cuda")
+    with P.Context(c) as ctx:
+        ctx.sampled_hist(buf.data_ptr(), len(host), stream)
+        assert ctx.fetch().bins == want
+        ctx.sampled_hist_dense(buf.data_ptr(), len(host), d.data_ptr(), stream)
+        torch.cuda.synchronize()
+        assert P.hist_from_dense(c, d.cpu().numpy()).bins == want
+        # malformed samples scattered through the list: counted apart, flagged
+        bad = np.array([7 << 60, 6 << 60 | 1, P.pack("B0", N, 0, 0), P.pack("C3", 0, N + 3, 0), P.pack("A0", 0, 0, N)],
+                       np.uint64)
+        mixed = np.insert(host, rng.integers(0, len(host), len(bad)), bad)
+        mb = torch.from_numpy(mixed.view(np.int64)).cuda()
+        ctx.reset(stream)
+        ctx.sampled_hist_dense(mb.data_ptr(), len(mixed), d.data_ptr(), stream)
+        torch.cuda.synchronize()
+        v = d.cpu().numpy()
+        assert v[P.DENSE_BINS] == len(bad)
+        assert P.hist_from_dense(c, v).bins == want
+        ctx.sampled_hist(mb.data_ptr(), len(mixed), stream)
+        with pytest.raises(P.PlussError, match="PLUSS_ERR_INPUT"):
+            ctx.fetch()
 
 
 def test_dense_pass_config2_full_size():

@@ -1,5 +1,6 @@
 """Split the hot kernel's time (diagnostics; defaults: UNROLL=2, NT=1, grid 1024): PLUSS_ABLATE=2 loads only,
-=1 loads + key computation, 0 = product kernel.  Also a torch copy for a
+=1 loads + key computation (both on the lane-counter kernel, PLUSS_LEGACY=1), default = product kernel
+(k_count, ballot counting).  Also a torch copy for a
 bandwidth reference.  Prints one JSON line per variant."""
 import json
 import os
@@ -38,24 +39,22 @@ def main():
             ctx.expand(0x5EED0001, r, 0, c, buf.data_ptr() + 8 * off, s.cuda_stream)
             off += c
         torch.cuda.synchronize()
-        variants = [dict(PLUSS_ABLATE=m) for m in ("2", "1", "0")]
-        variants += [dict(PLUSS_UNROLL=u) for u in ("1", "4", "8")]
+        variants = [dict(PLUSS_ABLATE=m) for m in ("2", "1")] + [{}, dict(PLUSS_LEGACY="1")]
         variants += [dict(PLUSS_NT="0"), dict(PLUSS_PCS="4")]
-        variants += [dict(PLUSS_GRID=g) for g in ("512", "1792", "2048", "3072", "4096", "8192")]
         variants += [dict(PLUSS_ABLATE="2", PLUSS_GRID=g) for g in ("2048", "4096")]
         for v in variants:
-            for k in ("PLUSS_ABLATE", "PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT", "PLUSS_PCS"):
+            for k in ("PLUSS_ABLATE", "PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT", "PLUSS_PCS", "PLUSS_LEGACY"):
                 os.environ.pop(k, None)
             os.environ.update(v)
             ms = timeit(lambda: ctx.sampled_hist(buf.data_ptr(), total, s.cuda_stream), s)
             print(json.dumps({"samples": total, **v, "ms": ms, "GBps": 8 * total / ms / 1e6}), flush=True)
-        for k in ("PLUSS_ABLATE", "PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT", "PLUSS_PCS"):
+        for k in ("PLUSS_ABLATE", "PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT", "PLUSS_PCS", "PLUSS_LEGACY"):
             os.environ.pop(k, None)
         keys = torch.empty(4096, dtype=torch.int64, device=dev)
         cnts = torch.empty(4096, dtype=torch.int64, device=dev)
-        fused = [{}, dict(PLUSS_NT="0"), dict(PLUSS_UNROLL="1"), dict(PLUSS_GRID="768")]
+        fused = [{}, dict(PLUSS_LEGACY="1")]
         for v in fused:
-            for k in ("PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT"):
+            for k in ("PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT", "PLUSS_LEGACY"):
                 os.environ.pop(k, None)
             os.environ.update(v)
             ms = timeit(lambda: ctx.sampled_hist_export(buf.data_ptr(), total, keys.data_ptr(), cnts.data_ptr(), 4096,
@@ -66,14 +65,15 @@ def main():
             os.environ.pop(k, None)
 
         dense = torch.zeros(P.DENSE_BINS + 1, dtype=torch.int64, device=dev)
-        for v in [{}, dict(PLUSS_GRID="512"), dict(PLUSS_GRID="768"), dict(PLUSS_NT="0"), dict(PLUSS_UNROLL="1")]:
-            for k in ("PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT"):
+        for v in [{}, dict(PLUSS_LEGACY="1"), dict(PLUSS_GRID="512"), dict(PLUSS_GRID="768"),
+                  dict(PLUSS_GRID="2048"), dict(PLUSS_NT="0"), dict(PLUSS_UNROLL="1"), dict(PLUSS_UNROLL="4")]:
+            for k in ("PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT", "PLUSS_LEGACY"):
                 os.environ.pop(k, None)
             os.environ.update(v)
             ms = timeit(lambda: ctx.sampled_hist_dense(buf.data_ptr(), total, dense.data_ptr(), s.cuda_stream), s)
             print(json.dumps({"samples": total, "dense": v, "dense_ms": ms, "GBps": 8 * total / ms / 1e6}),
                   flush=True)
-        for k in ("PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT"):
+        for k in ("PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT", "PLUSS_LEGACY"):
             os.environ.pop(k, None)
         torch.cuda.synchronize()
         assert int(dense[:P.DENSE_BINS].sum()) == total and int(dense[P.DENSE_BINS]) == 0
