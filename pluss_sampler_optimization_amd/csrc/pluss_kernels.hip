@@ -574,6 +574,96 @@ __device__ __forceinline__ void count_slot(const Model& m, uint64_t x, bool ok, 
   }
 }
 
+// All 2*UNR slots of a step (lane-pair u holds slots 2u, 2u+1; okm[u] = its
+// live lanes).  When every live sample of the step has the reference of the
+// first live lane (almost always), that reference's conditions are evaluated
+// for all slots in one straight-line block -- independent ballots the
+// scheduler interleaves -- and the counts are summed in scalar registers
+// before one lane-indexed add per bin.  Otherwise slot by slot.
+template <bool P2, bool NP2, int UNR>
+__device__ __forceinline__ void count_step(const Model& m, const uint32_t (&lo)[2 * UNR], const uint32_t (&hi)[2 * UNR],
+                                           const uint64_t (&okm)[UNR], uint32_t& acc) {
+  constexpr int K = 2 * UNR;
+  uint64_t any = 0;
+#pragma unroll
+  for (int u = 0; u < UNR; ++u) any |= okm[u];
+  if (any == 0) return;
+  const int l0 = (int)__builtin_ctzll(any);
+  const uint32_t r0 = __builtin_amdgcn_readlane(hi[0] >> 28, l0);  // slot 0 is live wherever any slot is
+  uint64_t mixed = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) mixed |= __ballot((hi[k] >> 28) != r0) & okm[k / 2];
+  if (r0 > 5 || mixed) {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      count_slot<P2, NP2>(m, ((uint64_t)hi[k] << 32) | lo[k], (okm[k / 2] >> __lane_id()) & 1, acc);
+    return;
+  }
+  uint32_t nbad = 0, ng = 0, na = 0, nb = 0;
+  uint64_t good[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    bool bad;
+    if (NP2) {
+      bad = ((lo[k] & m.badlo) | (hi[k] & m.badhi)) != 0u;
+    } else {
+      const uint32_t c2 = lo[k] & 0xFFFFFu, c0 = (hi[k] >> 8) & 0xFFFFFu;
+      const uint32_t c1 = __builtin_amdgcn_alignbit(hi[k], lo[k], 20) & 0xFFFFFu;
+      bad = (c0 > c1 ? (c0 > c2 ? c0 : c2) : (c1 > c2 ? c1 : c2)) >= m.N;
+    }
+    const uint64_t mb = __ballot(bad) & okm[k / 2];
+    good[k] = okm[k / 2] & ~mb;
+    nbad += (uint32_t)__popcll(mb);
+    ng += (uint32_t)__popcll(good[k]);
+  }
+  const uint32_t Wm1 = m.W - 1;
+  switch (r0) {
+    case C3:
+#pragma unroll
+      for (int k = 0; k < K; ++k) {  // case 0: c2+1 < N; case 1: c1 not the last element of its line
+        const uint32_t c2 = lo[k] & 0xFFFFFu;
+        const uint32_t c1 = __builtin_amdgcn_alignbit(hi[k], lo[k], 20) & 0xFFFFFu;
+        const bool c1last = P2 ? (lo[k] & (m.wmask << 20)) == (m.wmask << 20) : fmod_(c1, m.dW) == Wm1;
+        const uint64_t a = __ballot(c2 + 1 < m.N) & good[k];
+        na += (uint32_t)__popcll(a);
+        nb += (uint32_t)__popcll(__ballot(!c1last) & good[k] & ~a);
+      }
+      break;
+    case A0:
+#pragma unroll
+      for (int k = 0; k < K; ++k) {  // case 0: c2 not the last element of its line; case 1: c1+1 < N
+        const uint32_t c2 = lo[k] & 0xFFFFFu;
+        const uint32_t c1 = __builtin_amdgcn_alignbit(hi[k], lo[k], 20) & 0xFFFFFu;
+        const bool c2last = P2 ? (lo[k] & m.wmask) == m.wmask : fmod_(c2, m.dW) == Wm1;
+        const uint64_t a = __ballot(!c2last) & good[k];
+        na += (uint32_t)__popcll(a);
+        nb += (uint32_t)__popcll(__ballot(c1 + 1 < m.N) & good[k] & ~a);
+      }
+      break;
+    case B0:
+#pragma unroll
+      for (int k = 0; k < K; ++k) {  // case 0: c1 not the last element of its line; case 1: a later owned row
+        const uint32_t c0 = (hi[k] >> 8) & 0xFFFFFu;
+        const uint32_t c1 = __builtin_amdgcn_alignbit(hi[k], lo[k], 20) & 0xFFFFFu;
+        const bool c1last = P2 ? (lo[k] & (m.wmask << 20)) == (m.wmask << 20) : fmod_(c1, m.dW) == Wm1;
+        const uint32_t p = P2 ? (c0 & m.csmask) : fmod_(c0, m.dCS);
+        const uint32_t nxt = c0 + 1 + (p + 1 == m.CS ? m.tcs : 0u);
+        const uint64_t a = __ballot(!c1last) & good[k];
+        na += (uint32_t)__popcll(a);
+        nb += (uint32_t)__popcll(__ballot(nxt < m.N) & good[k] & ~a);
+      }
+      break;
+    default:  // C0, C1, C2: always case 0
+      na = ng;
+      break;
+  }
+  const uint32_t lane = __lane_id(), b0 = r0 * 3;
+  acc += lane == b0 ? na : 0u;
+  acc += lane == b0 + 1 ? nb : 0u;
+  acc += lane == b0 + 2 ? ng - na - nb : 0u;
+  acc += lane == BIN_BAD ? nbad : 0u;
+}
+
 // Add the wave's lane-indexed counts to the workgroup's LDS totals.
 __device__ __forceinline__ void flush_counts(uint32_t& acc, unsigned long long* tot) {
   const uint32_t lane = __lane_id();
@@ -612,12 +702,17 @@ __global__ __launch_bounds__(BLOCK) void k_count(Model m, const uint64_t* __rest
       for (int u = 0; u < UNR; ++u)  // the next step's pairs (past the window: zeros)
         y[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                              rs, (int)((base + step + u * BLOCK + threadIdx.x) * 16u), 0, AUX));
+      uint32_t lo[2 * UNR], hi[2 * UNR];
+      uint64_t okm[UNR];
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        const bool ok = base + u * BLOCK + threadIdx.x < wn;
-        count_slot<P2, NP2>(m, ((uint64_t)x[u].y << 32) | x[u].x, ok, acc);
-        count_slot<P2, NP2>(m, ((uint64_t)x[u].w << 32) | x[u].z, ok, acc);
+        lo[2 * u] = x[u].x;
+        hi[2 * u] = x[u].y;
+        lo[2 * u + 1] = x[u].z;
+        hi[2 * u + 1] = x[u].w;
+        okm[u] = __ballot(base + u * BLOCK + threadIdx.x < wn);
       }
+      count_step<P2, NP2, UNR>(m, lo, hi, okm, acc);
 #pragma unroll
       for (int u = 0; u < UNR; ++u) x[u] = y[u];
     }
