@@ -281,7 +281,8 @@ def main():
                                                              if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic()},
-        "kernel": {"name": "pluss::k_sampled_hist<2,0,2,true,2,1> (FAST_P2, non-temporal loads, dense tail)",
+        "kernel": {"name": "pluss::k_count<true,true,true,TAIL_DENSE,2> (ballot counting, nt buffer loads, "
+                           "dense tail)",
                    "avg_ms": kern_ms, "timing": "HIP events on the launch stream around the K timed steps / K"
                    + (" (includes the all_gather)" if world > 1 else ""), "bytes_per_launch": BYTES_PER_SAMPLE * n_local},
         "histogram_bins": len(h.bins),

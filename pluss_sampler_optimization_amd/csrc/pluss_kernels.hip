@@ -671,7 +671,7 @@ __device__ __forceinline__ void flush_counts(uint32_t& acc, unsigned long long* 
   acc = 0;
 }
 
-template <bool P2, bool NP2, bool NT, int TAIL, int UNR = UNROLL>
+template <bool P2, bool NP2, bool NT, int TAIL, int UNR = UNROLL, bool LOADS_ONLY = false>
 __global__ __launch_bounds__(BLOCK) void k_count(Model m, const uint64_t* __restrict__ smp, uint64_t n,
                                                  const uint64_t* __restrict__ head, int has_head, GTable g,
                                                  ExportArgs ex) {
@@ -712,11 +712,16 @@ __global__ __launch_bounds__(BLOCK) void k_count(Model m, const uint64_t* __rest
         hi[2 * u + 1] = x[u].w;
         okm[u] = __ballot(base + u * BLOCK + threadIdx.x < wn);
       }
-      count_step<P2, NP2, UNR>(m, lo, hi, okm, acc);
+      if (LOADS_ONLY) {  // diagnostics (PLUSS_ABLATE=3): the same loads, nothing counted
+#pragma unroll
+        for (int k = 0; k < 2 * UNR; ++k) acc ^= lo[k] ^ hi[k];
+      } else {
+        count_step<P2, NP2, UNR>(m, lo, hi, okm, acc);
+      }
 #pragma unroll
       for (int u = 0; u < UNR; ++u) x[u] = y[u];
     }
-    flush_counts(acc, tot);  // per window: keeps the 32-bit lane counters from overflowing
+    if (!LOADS_ONLY) flush_counts(acc, tot);  // per window: keeps the 32-bit lane counters from overflowing
   }
   if (((n & 1) || has_head) && blockIdx.x == 0 && threadIdx.x < 64) {
     // odd tail (lane 0) and, for an 8-byte-aligned list, its first sample (lane 1).
@@ -726,6 +731,10 @@ __global__ __launch_bounds__(BLOCK) void k_count(Model m, const uint64_t* __rest
     const uint64_t xs = mine ? *src : 0;
     count_slot<P2, NP2>(m, xs, mine, acc);
     flush_counts(acc, tot);
+  }
+  if (LOADS_ONLY) {
+    if (acc == 0x5EED5EEDu) atomicOr(&g.flags[2], 1u);  // keeps the loads alive
+    return;
   }
   __syncthreads();
   if (TAIL == TAIL_DENSE) tail_dense(tot, g, ex.dense);
@@ -984,7 +993,8 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
 #define PLUSS_LAUNCH_HOT(EX, ...)                                                                                  \
   hipLaunchKernelGGL((k_sampled_hist<__VA_ARGS__>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n, head, has_head, g, \
                      EX)
-  // diagnostics only (tools/ablate.py): PLUSS_ABLATE=1|2 (loads only / loads + bins, lane-counter kernel),
+  // diagnostics only (tools/ablate.py): PLUSS_ABLATE=1|2 (loads + bins / loads only, lane-counter kernel),
+  // PLUSS_ABLATE=3 (loads only, k_count),
   // PLUSS_LEGACY=1 (the lane-counter kernel k_sampled_hist for FAST shapes), PLUSS_UNROLL=1|4,
   // PLUSS_NT=0|1, PLUSS_GRID=<max blocks>, PLUSS_PCS=4 (legacy: a counter set per wave)
   const char* abl = getenv("PLUSS_ABLATE");
@@ -997,8 +1007,14 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
   const int a = abl ? atoi(abl) : 0, u = unr ? atoi(unr) : UNROLL;
   const bool nt = ntv ? ntv[0] == '1' : HOT_NT;
   const bool pc4 = pcs && pcs[0] == '4';
-  const bool legacy = (leg && leg[0] == '1') || a || pc4;
   const ExportArgs none{nullptr, nullptr, 0, nullptr, nullptr};
+  const bool legacy = (leg && leg[0] == '1') || a == 1 || a == 2 || pc4;
+  if (a == 3 && m.fast && m.p2 && m.np2 && !fuse) {  // loads-only floor of k_count
+    hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_NONE, UNROLL, true>), dim3(nb), dim3(BLOCK), 0, s, m,
+                       d_samples, n, head, has_head, g, none);
+    PLUSS_HIP_CHECK(hipGetLastError());
+    return PLUSS_OK;
+  }
   const ExportArgs& ex = fuse ? *fuse : none;
   const int tail = fuse ? (fuse->dense ? TAIL_DENSE : TAIL_EXPORT) : TAIL_NONE;
   if (m.fast && !legacy) {

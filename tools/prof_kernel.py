@@ -20,12 +20,9 @@ off = 0
 for r, c in enumerate(counts):
     ctx.expand(0x5EED0001, r, 0, c, buf.data_ptr() + 8 * off, s.cuda_stream)
     off += c
-keys = torch.empty(4096, dtype=torch.int64, device=dev)
-cnts = torch.empty(4096, dtype=torch.int64, device=dev)
-ctx.reset(s.cuda_stream)
-for _ in range(int(os.environ.get("PROF_REPS", 5))):  # the bench step: one fused count+export launch
-    ctx.sampled_hist_export(buf.data_ptr(), total, keys.data_ptr(), cnts.data_ptr(), 4096, s.cuda_stream)
+dense = torch.zeros(P.DENSE_BINS + 1, dtype=torch.int64, device=dev)
+for _ in range(int(os.environ.get("PROF_REPS", 5))):  # the bench step: one dense-pass launch
+    ctx.sampled_hist_dense(buf.data_ptr(), total, dense.data_ptr(), s.cuda_stream)
 torch.cuda.synchronize()
-h = P.hist_from_tables(keys.cpu().numpy().view("uint64"), cnts.cpu().numpy().view("uint64"))
-assert h.total() == total
+assert P.hist_from_dense(cfg, dense.cpu().numpy()).total() == total
 print("ok")

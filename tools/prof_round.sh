@@ -19,7 +19,7 @@ import csv, sys, collections
 rows = list(csv.DictReader(open(sys.argv[1])))
 acc = collections.defaultdict(list)
 for r in rows:
-    if "k_sampled_hist" in r["Kernel_Name"]:
+    if "k_count" in r["Kernel_Name"]:
         acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, v in acc.items():
     print(f"  {k}: mean {sum(v)/len(v):.4g} over {len(v)} dispatches")
