@@ -10,6 +10,12 @@ key.  An all-gather of ~64 KB per rank replaces an all-reduce because the
 exact-key tables are sparse (a dense all-reduce over exact RI values would
 need one slot per possible RI).
 
+For N % (cls/ds) == 0 shapes (every BASELINE configuration) the histogram
+of a pass is a dense vector of PLUSS_DENSE_BINS (ref, case) counts
+(pluss_dev_sampled_hist_dense), identical in layout on every rank, so the
+merge is one element-wise all-reduce of DENSE_BINS + 1 int64 words
+(sharded_clean_dense) -- the bench's multi-GPU step.
+
 Faithful mode (one r10 sampler_<REF> with its cross-sample queue semantics)
 needs one global key order, so it is sharded by contiguous ranges of the sort
 key a*T+tid instead: every rank reads the whole per-reference
@@ -19,7 +25,8 @@ the scan state across shards (include/pluss_gpu.h, pluss_dev_faithful_shard_*).
 """
 import numpy as np
 
-from .api import REFS, Context, Histogram, faithful_key_space, hist_from_tables
+from ._lib import DENSE_BINS
+from .api import REFS, Context, Histogram, faithful_key_space, hist_from_dense, hist_from_tables
 
 TABLE_CAP = 4096
 KEY_EMPTY = (1 << 64) - 1
@@ -79,6 +86,41 @@ def sharded_clean_hist(cfg, seed, counts, group=None, stream=None):
     if dist.get_backend(group) == "gloo":  # e.g. several ranks sharing one GPU in tests
         keys, cnts = keys.cpu(), cnts.cpu()
     return allgather_tables(keys, cnts, group)
+
+
+def allreduce_dense(counts_t, group=None):
+    """Element-wise sum of per-rank dense count vectors (int64 tensors: on the
+    GPU with nccl/RCCL, on the CPU with gloo); in place, returns the tensor."""
+    import torch.distributed as dist
+    dist.all_reduce(counts_t, group=group)
+    return counts_t
+
+
+def sharded_clean_dense(cfg, seed, counts, group=None, stream=None):
+    """Every rank: expand its shard on its GPU, one dense pass, all-reduce.
+    Returns the merged Histogram (identical on all ranks)."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    parts = shard_ranges(counts, rank, world)
+    n = sum(c for _, c in parts)
+    dev = torch.device("cuda", cfg.device)
+    samples = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    dense = torch.zeros(DENSE_BINS + 1, dtype=torch.int64, device=dev)
+    sp = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    with Context(cfg) as ctx:
+        off = 0
+        for ref, (first, c) in zip(range(len(REFS)), parts):
+            ctx.expand(seed, ref, first, c, samples.data_ptr() + 8 * off, sp)
+            off += c
+        ctx.sampled_hist_dense(samples.data_ptr(), n, dense.data_ptr(), sp)
+        torch.cuda.synchronize(dev)
+    if dist.get_backend(group) == "gloo":  # e.g. several ranks sharing one GPU in tests
+        dense = dense.cpu()
+    v = allreduce_dense(dense, group).cpu().numpy()
+    if v[DENSE_BINS]:
+        raise ValueError(f"{int(v[DENSE_BINS])} malformed samples")
+    return hist_from_dense(cfg, v)
 
 
 def key_range(key_space, rank, world):

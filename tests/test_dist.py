@@ -100,3 +100,64 @@ def test_shard_ranges_partition():
                 assert first == seen[r]
                 seen[r] += n
         assert seen == counts
+
+
+def _dense_worker(rank, world, port, samples_per_ref, N, T, q):
+    """Per-rank dense vector (bin = ref*3 + case, located by pluss_dense_keys)
+    from the oracle's RIs of this rank's shard, merged by dist.allreduce_dense."""
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch
+    import torch.distributed as dist
+    import oracle as orc
+    import pluss_sampler_optimization_amd as P
+    from pluss_sampler_optimization_amd import dist as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = orc.cfg(N, T)
+    cfg = P.SamplerConfig(n=N, threads=T)
+    keys = P.dense_keys(cfg)
+    counts = [min(samples_per_ref, (N - 1) ** (2 if r < 2 else 3)) for r in range(6)]
+    parts = D.shard_ranges(counts, rank, world)
+    mine = np.concatenate([orc.expand(c, 0x5EED0001, r, first, n) for r, (first, n) in enumerate(parts) if n])
+    ri = orc.clean_ri(c, mine)
+    refs = (mine >> np.uint64(60)).astype(np.int64)
+    v = np.zeros(P.DENSE_BINS + 1, np.int64)
+    for r, x in zip(refs.tolist(), ri.tolist()):
+        k = 1 if (r == 3 and x > 0 and 2 * x > (4 * N + 2) * N) else 0
+        key = (r << 60) | (k << 56) | (x + 2)
+        v[next(b for b in range(3 * r, 3 * r + 3) if keys[b] == key)] += 1
+    merged = D.allreduce_dense(torch.from_numpy(v)).numpy()
+    q.put((rank, P.hist_from_dense(cfg, merged).bins, len(mine)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dense_allreduce_equals_whole_list(orc, world):
+    """The dense multi-GPU merge (bench step for N>1): per-rank (ref, case)
+    vectors summed by one all-reduce == the oracle histogram of the whole list."""
+    N, T, per = 64, 4, 600
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dense_worker, args=(r, world, port, per, N, T, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    c = orc.cfg(N, T)
+    counts = [min(per, (N - 1) ** (2 if r < 2 else 3)) for r in range(6)]
+    whole = np.concatenate([orc.expand(c, 0x5EED0001, r, 0, n) for r, n in enumerate(counts)])
+    ri = orc.clean_ri(c, whole)
+    refs = (whole >> np.uint64(60)).astype(np.int64)
+    want = {}
+    for r, x in zip(refs, ri):
+        k = 1 if (r == 3 and x > 0 and 2 * x > (4 * N + 2) * N) else 0
+        key = (orc.REFS[r], k, int(x))
+        want[key] = want.get(key, 0) + 1
+    assert sum(n for _, _, n in res) == len(whole)
+    for _, bins, _ in res:
+        assert bins == want

@@ -449,13 +449,15 @@ def _dist_worker(rank, world, port, q):
     cfg = P2.SamplerConfig(n=512, threads=4)
     counts = P2.default_counts(512, 1 << 20)
     h = D.sharded_clean_hist(cfg, 0x5EED0001, counts)
-    q.put((rank, h.bins))
+    hd = D.sharded_clean_dense(cfg, 0x5EED0001, counts)
+    q.put((rank, h.bins, hd.bins))
     dist.destroy_process_group()
 
 
 def test_sharded_two_ranks_on_one_gpu_equals_single_rank():
     """The sharded path (2 processes, each expanding and histogramming its slice
-    on cuda:0, tables exchanged over gloo) equals one process over the whole list."""
+    on cuda:0; canonical tables all-gathered, or dense vectors all-reduced,
+    over gloo) equals one process over the whole list."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -475,8 +477,9 @@ def test_sharded_two_ranks_on_one_gpu_equals_single_rank():
     counts = P.default_counts(512, 1 << 20)
     whole = np.concatenate([P.expand_samples(cfg_, 0x5EED0001, r, 0, c) for r, c in enumerate(counts)])
     want = P.sampled_hist(cfg, whole).bins
-    for _, bins in res:
+    for _, bins, dbins in res:
         assert bins == want
+        assert dbins == want
 
 
 KEY_EMPTY = (1 << 64) - 1
