@@ -29,6 +29,7 @@ constexpr uint32_t BARRIVE = 31;
 // (arrivals << DARR_SHIFT | count) so the last adder of a word knows its total
 // from the value its add returned.  dbins: NBROW rows, dtot: one row.
 constexpr uint32_t DBINS = 19;
+constexpr uint32_t DENSE_ROWS = 32;  // first-level rows of the dense tail (tools/ablate.py, PLUSS_DROWS)
 constexpr int DARR_SHIFT = 44;
 constexpr unsigned long long DCNT_MASK = (1ull << DARR_SHIFT) - 1;
 

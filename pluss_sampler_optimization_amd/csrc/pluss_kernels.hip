@@ -189,12 +189,14 @@ __device__ __forceinline__ void tail_accumulate(const unsigned long long* tot, G
 // (1 << DARR_SHIFT | row total) to the bin's word in `dtot`; the add there
 // that returns arrivals == rows - 1 holds the launch total, which the lane
 // stores to out[b].  Critical path after the count: two returning atomics.
-__device__ __forceinline__ void tail_dense(const unsigned long long* tot, GTable g, unsigned long long* out) {
+// `drows` (a power of two <= NBROW) rows: about sqrt(grid) balances the adds per word of the two levels.
+__device__ __forceinline__ void tail_dense(const unsigned long long* tot, GTable g, unsigned long long* out,
+                                           uint32_t drows) {
   if (threadIdx.x < DBINS) {
     const uint32_t b = threadIdx.x;
-    const uint32_t row = blockIdx.x & (NBROW - 1);
-    const uint32_t rows = gridDim.x < NBROW ? gridDim.x : NBROW;
-    const uint32_t in_row = (gridDim.x - row + NBROW - 1) / NBROW;
+    const uint32_t row = blockIdx.x & (drows - 1);
+    const uint32_t rows = gridDim.x < drows ? gridDim.x : drows;
+    const uint32_t in_row = (gridDim.x - row + drows - 1) / drows;
     const unsigned long long v = (1ull << DARR_SHIFT) | tot[b];
     unsigned long long* w = &g.dbins[row * BSTRIDE + b];
     const unsigned long long old = __hip_atomic_fetch_add(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -317,6 +319,7 @@ struct ExportArgs {
   uint64_t cap;
   unsigned int* nout;
   unsigned long long* dense;
+  uint32_t drows;  // dense tail: rows of the first level (power of two <= NBROW)
 };
 
 // Fused export, after tail_accumulate: an arrival count without fences --
@@ -478,7 +481,7 @@ __global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t*
   if (BINS) {
     __shared__ unsigned long long tot[DBINS];
     reduce_lane_counters<PCS>(pc, tot);
-    if (TAIL == TAIL_DENSE) tail_dense(tot, g, ex.dense);
+    if (TAIL == TAIL_DENSE) tail_dense(tot, g, ex.dense, ex.drows);
     else tail_accumulate(tot, g);
   } else {
     bt_finish(wc, bt, g);
@@ -671,17 +674,17 @@ __device__ __forceinline__ void flush_counts(uint32_t& acc, unsigned long long* 
   acc = 0;
 }
 
-template <bool P2, bool NP2, bool NT, int TAIL, int UNR = UNROLL, bool LOADS_ONLY = false>
-__global__ __launch_bounds__(BLOCK) void k_count(Model m, const uint64_t* __restrict__ smp, uint64_t n,
-                                                 const uint64_t* __restrict__ head, int has_head, GTable g,
-                                                 ExportArgs ex) {
+template <bool P2, bool NP2, bool NT, int TAIL, int UNR = UNROLL, bool LOADS_ONLY = false, int BS = BLOCK>
+__global__ __launch_bounds__(BS) void k_count(Model m, const uint64_t* __restrict__ smp, uint64_t n,
+                                              const uint64_t* __restrict__ head, int has_head, GTable g,
+                                              ExportArgs ex) {
+  static_assert(BS == BLOCK || TAIL != TAIL_EXPORT, "the export tail assumes BLOCK threads");
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   __shared__ unsigned long long tot[DBINS];
-  if (threadIdx.x < DBINS) tot[threadIdx.x] = 0;
-  __syncthreads();
+  if (threadIdx.x < DBINS) tot[threadIdx.x] = 0;  // the barrier before the first flush orders this
   uint32_t acc = 0;  // lane b: count of bin b
   const uint64_t npairs = n >> 1;
-  const uint32_t step = gridDim.x * (uint32_t)(BLOCK * UNR);
+  const uint32_t step = gridDim.x * (uint32_t)(BS * UNR);
   constexpr int AUX = NT ? 2 : 0;  // nt: the list is streamed once per pass
   for (uint64_t w0 = 0; w0 < npairs; w0 += CWIN) {
     const uint32_t wn = (uint32_t)(npairs - w0 < CWIN ? npairs - w0 : CWIN);
@@ -690,18 +693,18 @@ __global__ __launch_bounds__(BLOCK) void k_count(Model m, const uint64_t* __rest
     const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)wp >> 32));
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(((uintptr_t)phi << 32) | plo), 0, (int)__builtin_amdgcn_readfirstlane(wn * 16u), 0x00020000);
-    uint32_t base = blockIdx.x * (uint32_t)(BLOCK * UNR);
+    uint32_t base = blockIdx.x * (uint32_t)(BS * UNR);
     u32x4 x[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u)
       x[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                           rs, (int)((base + u * BLOCK + threadIdx.x) * 16u), 0, AUX));
+                                           rs, (int)((base + u * BS + threadIdx.x) * 16u), 0, AUX));
     for (; base < wn; base += step) {
       u32x4 y[UNR];
 #pragma unroll
       for (int u = 0; u < UNR; ++u)  // the next step's pairs (past the window: zeros)
         y[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             rs, (int)((base + step + u * BLOCK + threadIdx.x) * 16u), 0, AUX));
+                                             rs, (int)((base + step + u * BS + threadIdx.x) * 16u), 0, AUX));
       uint32_t lo[2 * UNR], hi[2 * UNR];
       uint64_t okm[UNR];
 #pragma unroll
@@ -710,7 +713,7 @@ __global__ __launch_bounds__(BLOCK) void k_count(Model m, const uint64_t* __rest
         hi[2 * u] = x[u].y;
         lo[2 * u + 1] = x[u].z;
         hi[2 * u + 1] = x[u].w;
-        okm[u] = __ballot(base + u * BLOCK + threadIdx.x < wn);
+        okm[u] = __ballot(base + u * BS + threadIdx.x < wn);
       }
       if (LOADS_ONLY) {  // diagnostics (PLUSS_ABLATE=3): the same loads, nothing counted
 #pragma unroll
@@ -721,7 +724,10 @@ __global__ __launch_bounds__(BLOCK) void k_count(Model m, const uint64_t* __rest
 #pragma unroll
       for (int u = 0; u < UNR; ++u) x[u] = y[u];
     }
-    if (!LOADS_ONLY) flush_counts(acc, tot);  // per window: keeps the 32-bit lane counters from overflowing
+    if (!LOADS_ONLY) {  // per window: keeps the 32-bit lane counters from overflowing
+      __syncthreads();
+      flush_counts(acc, tot);
+    }
   }
   if (((n & 1) || has_head) && blockIdx.x == 0 && threadIdx.x < 64) {
     // odd tail (lane 0) and, for an 8-byte-aligned list, its first sample (lane 1).
@@ -737,7 +743,7 @@ __global__ __launch_bounds__(BLOCK) void k_count(Model m, const uint64_t* __rest
     return;
   }
   __syncthreads();
-  if (TAIL == TAIL_DENSE) tail_dense(tot, g, ex.dense);
+  if (TAIL == TAIL_DENSE) tail_dense(tot, g, ex.dense, ex.drows);
   else tail_accumulate(tot, g);
   if (TAIL == TAIL_EXPORT) tail_export(m, g, ex);
 }
@@ -1007,7 +1013,7 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
   const int a = abl ? atoi(abl) : 0, u = unr ? atoi(unr) : UNROLL;
   const bool nt = ntv ? ntv[0] == '1' : HOT_NT;
   const bool pc4 = pcs && pcs[0] == '4';
-  const ExportArgs none{nullptr, nullptr, 0, nullptr, nullptr};
+  const ExportArgs none{nullptr, nullptr, 0, nullptr, nullptr, 0};
   const bool legacy = (leg && leg[0] == '1') || a == 1 || a == 2 || pc4;
   if (a == 3 && m.fast && m.p2 && m.np2 && !fuse) {  // loads-only floor of k_count
     hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_NONE, UNROLL, true>), dim3(nb), dim3(BLOCK), 0, s, m,
@@ -1030,7 +1036,13 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
       hipLaunchKernelGGL((k_count<P2, NP2, NT, TAIL_NONE, UNR>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n,   \
                          head, has_head, g, ex);                                                                 \
   } while (0)
-    if (m.p2 && m.np2 && (nt != HOT_NT || u != UNROLL)) {  // diagnostics
+    const char* bsv = getenv("PLUSS_BS");
+    if (m.p2 && m.np2 && tail == TAIL_DENSE && bsv && atoi(bsv) == 1024) {  // diagnostics: 1024-thread workgroups
+      int nb4 = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)1024 * UNROLL, MAX_BLOCKS / 4);
+      if (grd && atoi(grd) > 0) nb4 = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)1024 * UNROLL, std::min(atoi(grd), 4096));
+      hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_DENSE, UNROLL, false, 1024>), dim3(nb4), dim3(1024), 0, s, m,
+                         d_samples, n, head, has_head, g, ex);
+    } else if (m.p2 && m.np2 && (nt != HOT_NT || u != UNROLL)) {  // diagnostics
       if (u == 1) PLUSS_LAUNCH_COUNT(true, true, HOT_NT, 1);
       else if (u == 4) PLUSS_LAUNCH_COUNT(true, true, HOT_NT, 4);
       else PLUSS_LAUNCH_COUNT(true, true, !HOT_NT, UNROLL);
@@ -1083,7 +1095,7 @@ int launch_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, h
 int launch_sampled_hist_export(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, unsigned long long* d_keys,
                                unsigned long long* d_counts, uint64_t cap, hipStream_t s) {
   if (ctx->m.fast && !ctx->tables_dirty) {
-    const ExportArgs ex{d_keys, d_counts, cap, ctx->d_exp_n, nullptr};
+    const ExportArgs ex{d_keys, d_counts, cap, ctx->d_exp_n, nullptr, 0};
     return hot_launch(ctx, d_samples, n, s, &ex, "pluss_dev_sampled_hist_export");
   }
   if (int rc = hot_launch(ctx, d_samples, n, s, nullptr, "pluss_dev_sampled_hist_export")) return rc;
@@ -1100,7 +1112,13 @@ int launch_sampled_hist_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint64_
     set_error("pluss_dev_sampled_hist_dense: counts buffer must be 8-byte aligned");
     return PLUSS_ERR_INPUT;
   }
-  const ExportArgs ex{nullptr, nullptr, 0, nullptr, d_counts};
+  const char* dr = getenv("PLUSS_DROWS");  // diagnostics: first-level rows of the dense tail
+  uint32_t drows = DENSE_ROWS;
+  if (dr && atoi(dr) > 0) {
+    drows = 1;
+    while (drows * 2 <= (uint32_t)atoi(dr) && drows * 2 <= NBROW) drows *= 2;
+  }
+  const ExportArgs ex{nullptr, nullptr, 0, nullptr, d_counts, drows};
   return hot_launch(ctx, d_samples, n, s, &ex, "pluss_dev_sampled_hist_dense");
 }
 

@@ -321,11 +321,19 @@ def test_dense_pass(orc, N, T, CS):
         ctx.sampled_hist(buf.data_ptr() + 8, 1000, stream)  # accumulating histogram: untouched by dense passes
         first = None
         try:
-            for grid in ("", "1", "3", "64", "65", "200", "1024", "legacy"):
-                os.environ.pop("PLUSS_GRID", None)
-                os.environ.pop("PLUSS_LEGACY", None)
+            knobs = ("PLUSS_GRID", "PLUSS_LEGACY", "PLUSS_DROWS", "PLUSS_BS")
+            for grid in ("", "1", "3", "64", "65", "200", "1024", "legacy", "drows1", "drows8", "drows64", "bs1024",
+                         "bs1024_3"):
+                for k in knobs:
+                    os.environ.pop(k, None)
                 if grid == "legacy":  # the lane-counter kernel (k_sampled_hist) agrees
                     os.environ["PLUSS_LEGACY"] = "1"
+                elif grid.startswith("drows"):  # first-level rows of the dense tail
+                    os.environ["PLUSS_DROWS"] = grid[5:]
+                elif grid.startswith("bs1024"):  # 1024-thread workgroups (diagnostic variant)
+                    os.environ["PLUSS_BS"] = "1024"
+                    if grid == "bs1024_3":
+                        os.environ["PLUSS_GRID"] = "3"
                 elif grid:
                     os.environ["PLUSS_GRID"] = grid
                 for _ in range(2):
@@ -335,8 +343,8 @@ def test_dense_pass(orc, N, T, CS):
                     first = v if first is None else first
                     assert (v == first).all()
         finally:
-            os.environ.pop("PLUSS_GRID", None)
-            os.environ.pop("PLUSS_LEGACY", None)
+            for k in knobs:
+                os.environ.pop(k, None)
         v = run(ctx, buf.data_ptr(), total + 1)  # 8-byte aligned (peeled head), odd length
         assert P.hist_from_dense(c, v).total() == total + 1
         for n in (0, 1, 2, 3):

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Rehearse the N>1 bench path on a one-GPU box: 2 ranks share cuda:0, tables
-# exchanged over gloo (the round-end driver runs N=2..8 over RCCL on 8 GPUs).
+# Rehearse the N>1 bench path on a one-GPU box: 2 ranks share cuda:0, dense vectors
+# all-reduced over gloo (the round-end driver runs N=2..8 over RCCL on 8 GPUs).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${1:-rehearse}
