@@ -674,8 +674,7 @@ __device__ __forceinline__ void flush_counts(uint32_t& acc, unsigned long long* 
   acc = 0;
 }
 
-// ABL (diagnostics, tools/ablate.py): 0 product; 1 loads only (PLUSS_ABLATE=3); 2 count without the tail
-// (=4); 3 loads and the tail without the count (=5)
+// ABL (diagnostics, tools/ablate.py): 0 product; 1 loads only (PLUSS_ABLATE=3); 2 count without the tail (=4)
 template <bool P2, bool NP2, bool NT, int TAIL, int UNR = UNROLL, int ABL = 0, int BS = BLOCK>
 __global__ __launch_bounds__(BS) void k_count(Model m, const uint64_t* __restrict__ smp, uint64_t n,
                                               const uint64_t* __restrict__ head, int has_head, GTable g,
@@ -717,7 +716,7 @@ __global__ __launch_bounds__(BS) void k_count(Model m, const uint64_t* __restric
         hi[2 * u + 1] = x[u].w;
         okm[u] = __ballot(base + u * BS + threadIdx.x < wn);
       }
-      if (ABL == 1 || ABL == 3) {  // diagnostics: the same loads, nothing counted
+      if (ABL == 1) {  // diagnostics: the same loads, nothing counted
 #pragma unroll
         for (int k = 0; k < 2 * UNR; ++k) acc ^= lo[k] ^ hi[k];
       } else {
@@ -979,12 +978,6 @@ int launch_table_reset(pluss_ctx* ctx, hipStream_t s) {
   return PLUSS_OK;
 }
 
-// Scratch output of the loads+tail ablation (PLUSS_ABLATE=5): the handle's
-// export scratch keys (rewritten by every export before use).
-static ExportArgs ablate_dense(pluss_ctx* ctx) {
-  return ExportArgs{nullptr, nullptr, 0, nullptr, ctx->d_exp_keys, DENSE_ROWS};
-}
-
 // `fuse` != null: FAST shapes only, the launch also exports and resets (the
 // caller checked pluss_ctx::tables_dirty); n may then be 0.
 static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hipStream_t s, const ExportArgs* fuse,
@@ -1008,7 +1001,7 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
   hipLaunchKernelGGL((k_sampled_hist<__VA_ARGS__>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n, head, has_head, g, \
                      EX)
   // diagnostics only (tools/ablate.py): PLUSS_ABLATE=1|2 (loads + bins / loads only, lane-counter kernel),
-  // PLUSS_ABLATE=3|4|5 (k_count: loads only | count without the tail | loads + dense tail),
+  // PLUSS_ABLATE=3|4 (k_count: loads only | count without the tail),
   // PLUSS_LEGACY=1 (the lane-counter kernel k_sampled_hist for FAST shapes), PLUSS_UNROLL=1|4,
   // PLUSS_NT=0|1, PLUSS_GRID=<max blocks>, PLUSS_PCS=4 (legacy: a counter set per wave)
   const char* abl = getenv("PLUSS_ABLATE");
@@ -1023,16 +1016,13 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
   const bool pc4 = pcs && pcs[0] == '4';
   const ExportArgs none{nullptr, nullptr, 0, nullptr, nullptr, 0};
   const bool legacy = (leg && leg[0] == '1') || a == 1 || a == 2 || pc4;
-  if (a >= 3 && a <= 5 && m.fast && m.p2 && m.np2 && !fuse) {  // k_count ablations (no output)
+  if ((a == 3 || a == 4) && m.fast && m.p2 && m.np2 && !fuse) {  // k_count ablations (no output)
     if (a == 3)
       hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_NONE, UNROLL, 1>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples,
                          n, head, has_head, g, none);
-    else if (a == 4)
+    else
       hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_NONE, UNROLL, 2>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples,
                          n, head, has_head, g, none);
-    else
-      hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_DENSE, UNROLL, 3>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples,
-                         n, head, has_head, g, ablate_dense(ctx));
     PLUSS_HIP_CHECK(hipGetLastError());
     return PLUSS_OK;
   }

@@ -1,5 +1,5 @@
 """Split the hot kernel's time (diagnostics; defaults: UNROLL=2, NT=1, grid 1024): PLUSS_ABLATE=3 loads only
-(k_count's buffer loads), =4 count without the tail, =5 loads + dense tail without the count, =2 loads only and =1 loads + key computation (both on the lane-counter kernel,
+(k_count's buffer loads), =4 count without the tail, =2 loads only and =1 loads + key computation (both on the lane-counter kernel,
 PLUSS_LEGACY=1), default = product kernel (k_count, ballot counting).  Also a torch copy for a
 bandwidth reference.  Prints one JSON line per variant."""
 import json
@@ -39,7 +39,7 @@ def main():
             ctx.expand(0x5EED0001, r, 0, c, buf.data_ptr() + 8 * off, s.cuda_stream)
             off += c
         torch.cuda.synchronize()
-        variants = [dict(PLUSS_ABLATE=m) for m in ("3", "4", "5", "2", "1")] + [{}, dict(PLUSS_LEGACY="1")]
+        variants = [dict(PLUSS_ABLATE=m) for m in ("3", "4", "2", "1")] + [{}, dict(PLUSS_LEGACY="1")]
         variants += [dict(PLUSS_NT="0"), dict(PLUSS_PCS="4")]
         variants += [dict(PLUSS_ABLATE="2", PLUSS_GRID=g) for g in ("2048", "4096")]
         for v in variants:
