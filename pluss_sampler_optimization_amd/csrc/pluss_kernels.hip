@@ -811,6 +811,52 @@ __global__ __launch_bounds__(BLOCK) void k_fulltrace(Model m, GTable g) {
   }
 }
 
+// Full trace for N % W == 0 shapes, counted by ballots.  One wave per
+// (c0, c1) pair; lanes over c2, 64 at a time.  Of the six accesses of an
+// iteration only A0's and C3's outcome depends on c2 (the last element of a
+// line, the last c2), so each lane evaluates those two predicates for its
+// access and the wave popcounts their ballots; the outcomes of C0, C1, B0 and
+// C2 are wave-uniform for the pair.  Counts go to a lane-indexed 64-bit
+// register per wave (lane b: bin b), then the accumulate tail.
+template <bool P2>
+__global__ __launch_bounds__(BLOCK) void k_fulltrace_count(Model m, GTable g) {
+  __shared__ unsigned long long tot[DBINS];
+  if (threadIdx.x < DBINS) tot[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
+  unsigned long long acc = 0;
+  auto bump = [&acc, lane](uint32_t bin, uint32_t v) { acc += lane == bin ? (unsigned long long)v : 0ull; };
+  const uint32_t Wm1 = m.W - 1;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (BLOCK / 64);
+  const uint64_t npairs = (uint64_t)m.N * m.N;
+  for (uint64_t pr = (uint64_t)blockIdx.x * (BLOCK / 64) + wave; pr < npairs; pr += nwaves) {
+    const uint32_t c0 = (uint32_t)(pr / m.N), c1 = (uint32_t)(pr - (uint64_t)c0 * m.N);
+    uint32_t nlive = 0, nA0 = 0, nC3 = 0;  // accesses per reference; A0 case 0; C3 case 0
+    for (uint32_t c2b = 0; c2b < m.N; c2b += 64) {
+      const uint32_t c2 = c2b + lane;
+      const uint64_t live = __ballot(c2 < m.N);
+      const bool c2last = P2 ? (c2 & m.wmask) == m.wmask : fmod_(c2, m.dW) == Wm1;
+      nlive += (uint32_t)__popcll(live);
+      nA0 += (uint32_t)__popcll(__ballot(!c2last) & live);  // A0 -> A0(c2+1), same line
+      nC3 += (uint32_t)__popcll(__ballot(c2 + 1 < m.N) & live);  // C3 -> C2(c2+1)
+    }
+    const bool c1last = (P2 ? (c1 & m.wmask) : fmod_(c1, m.dW)) == Wm1;
+    const uint32_t p = P2 ? (c0 & m.csmask) : fmod_(c0, m.dCS);
+    const bool row_next = c0 + 1 + (p + 1 == m.CS ? m.tcs : 0u) < m.N;
+    bump(0, 1);                                           // C0 -> C1
+    bump(3, 1);                                           // C1 -> C2(0)
+    bump(6, nA0);                                         // A0, case 0
+    bump(c1 + 1 < m.N ? 7 : 8, nlive - nA0);              // A0 at a line's last c2: next c1, or cold
+    bump(!c1last ? 9 : (row_next ? 10 : 11), nlive);      // B0: next c1 / next owned row / cold
+    bump(12, nlive);                                      // C2 -> C3
+    bump(15, nC3);                                        // C3, case 0
+    bump(!c1last ? 16 : 17, nlive - nC3);                 // C3 at c2 = N-1: next c1, or cold
+  }
+  if (lane < DBINS && acc) atomicAdd(&tot[lane], acc);
+  __syncthreads();
+  tail_accumulate(tot, g);
+}
+
 // --------------------------------------------------------------- export --
 // Fold main table + replicas, sort by key, write `cap` (key,count) pairs;
 // unused pairs are (~0, 0) so tables compare and merge canonically.
@@ -1131,7 +1177,13 @@ int launch_fulltrace(pluss_ctx* ctx, hipStream_t s) {
   if (!ctx->m.fast) ctx->tables_dirty = true;
   const uint64_t npairs = (uint64_t)ctx->m.N * ctx->m.N;
   const int nb = grid_for(npairs, BLOCK / 64 * 8);
-  if (ctx->m.fast && ctx->m.p2)
+  const char* leg = getenv("PLUSS_LEGACY");  // diagnostics: the lane-counter full trace
+  const bool legacy = leg && leg[0] == '1';
+  if (ctx->m.fast && !legacy && ctx->m.p2)
+    hipLaunchKernelGGL(k_fulltrace_count<true>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ctx->g);
+  else if (ctx->m.fast && !legacy)
+    hipLaunchKernelGGL(k_fulltrace_count<false>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ctx->g);
+  else if (ctx->m.fast && ctx->m.p2)
     hipLaunchKernelGGL(k_fulltrace<FAST_P2>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ctx->g);
   else if (ctx->m.fast)
     hipLaunchKernelGGL(k_fulltrace<FAST>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ctx->g);

@@ -84,13 +84,21 @@ def test_ri_dump_generic_path_equals_oracle(orc, model_host, shape):
 
 
 @pytest.mark.parametrize("N,T,CS,DS,CLS,thr", [(128, 4, 4, 8, 64, 1), (64, 8, 4, 8, 64, 0), (100, 3, 5, 8, 64, 1),
-                                              (20, 2, 3, 4, 64, 1), (33, 4, 2, 8, 64, 0), (256, 4, 4, 8, 64, 1)])
+                                              (20, 2, 3, 4, 64, 1), (33, 4, 2, 8, 64, 0), (256, 4, 4, 8, 64, 1),
+                                              (96, 3, 3, 8, 64, 1), (72, 5, 2, 8, 64, 0), (40, 2, 4, 8, 32, 1)])
 def test_fulltrace_gpu_equals_oracle(orc, N, T, CS, DS, CLS, thr):
-    """Full trace (sampling rate 1.0) == seq.cpp sampler() restated (per-source-ref raw bins)."""
-    h = P.fulltrace_hist(cfg(N, T, CS, DS, CLS, thr_variant="v1" if thr else "r10"))
+    """Full trace (sampling rate 1.0) == seq.cpp sampler() restated (per-source-ref raw bins);
+    the ballot kernel (N % W == 0) also equals the lane-counter kernel."""
+    c = cfg(N, T, CS, DS, CLS, thr_variant="v1" if thr else "r10")
+    h = P.fulltrace_hist(c)
     want, trav = orc.fulltrace(N, T, CS, DS, CLS, thr_variant=thr)
     assert h.bins == want
     assert h.traversed[0] == trav
+    os.environ["PLUSS_LEGACY"] = "1"
+    try:
+        assert P.fulltrace_hist(c).bins == want
+    finally:
+        os.environ.pop("PLUSS_LEGACY", None)
 
 
 def test_fulltrace_kat_n128(orc):
