@@ -113,25 +113,28 @@ def mrc_check(cfg, h, samples):
     return max(abs(m_gpu.get(k, 0.0) - m_ref.get(k, 0.0)) for k in keys)
 
 
-def fulltrace_bench(device):
-    """BASELINE config 5: full trace (sampling rate 1.0) GEMM N=512, T=4."""
+def fulltrace_bench(device, stream):
+    """BASELINE config 5: full trace (sampling rate 1.0) GEMM N=512, T=4: back-to-back
+    launches accumulating into one histogram, timed by HIP events on their stream."""
     cfg = P.SamplerConfig(n=512, threads=4, thr_variant="v1", device=device)
+    reps = 20
     with P.Context(cfg) as ctx:
-        ctx.fulltrace()
+        ctx.fulltrace(stream.cuda_stream)
+        ctx.reset(stream.cuda_stream)
         torch.cuda.synchronize()
-        t = time.perf_counter()
-        reps = 3
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
         for _ in range(reps):
-            ctx.reset()
-            ctx.fulltrace()
+            ctx.fulltrace(stream.cuda_stream)
+        e1.record(stream)
         torch.cuda.synchronize()
-        dt = (time.perf_counter() - t) / reps
+        dt = e0.elapsed_time(e1) * 1e-3 / reps
         h = ctx.fetch()
     acc = 512 * 512 * (4 * 512 + 2)
-    assert h.total() == acc
+    assert h.total() == acc * reps and h.traversed[0] == acc * reps
     return {"workload": "GEMM N=512, T=4, full trace (every access evaluated)", "accesses": acc,
             "ms": dt * 1e3, "accesses_per_s": acc / dt,
-            "kernel": "pluss::k_fulltrace_count<true> (ballot counting; wall time of reset + launch)"}
+            "kernel": "pluss::k_fulltrace_count<true> (ballot counting; HIP events over 20 launches)"}
 
 
 def faithful_bench(cfg, samples, stream):
@@ -312,7 +315,7 @@ def main():
     if rank == 0:
         result["mrc_abs_err"] = mrc_check(cfg, h, samples)
     if rank == 0 and world == 1 and not args.no_extras:
-        result["fulltrace"] = fulltrace_bench(local)
+        result["fulltrace"] = fulltrace_bench(local, stream)
         result["faithful"] = faithful_bench(cfg, samples, stream)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         host = samples.cpu().numpy().view(np.uint64)

@@ -108,7 +108,8 @@ int pluss_dev_hist_reset(pluss_ctx *ctx, void *stream);
 int pluss_dev_sampled_hist(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t n, void *stream);
 /* faithful mode: one sampler_<REF> over a list holding only reference `ref` */
 int pluss_dev_faithful_hist(pluss_ctx *ctx, int32_t ref, const uint64_t *d_samples, uint64_t n, void *stream);
-/* full trace: every access of the nest (sampling rate 1.0) */
+/* full trace: every access of the nest (sampling rate 1.0); accumulates like
+   the other passes, and adds the N*N*(4N+2) accesses to traversed[0] */
 int pluss_dev_fulltrace_hist(pluss_ctx *ctx, void *stream);
 int pluss_dev_sampled_ri(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t n, int64_t *d_ri, uint64_t *d_sink,
                          void *stream);

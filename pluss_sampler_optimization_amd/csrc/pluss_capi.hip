@@ -198,11 +198,7 @@ int pluss_dev_faithful_hist(pluss_ctx* ctx, int32_t ref, const uint64_t* d_sampl
 
 int pluss_dev_fulltrace_hist(pluss_ctx* ctx, void* stream) {
   if (!ctx) return PLUSS_ERR_CONFIG;
-  if (int rc = launch_fulltrace(ctx, pick(ctx, stream))) return rc;
-  const unsigned long long total = (unsigned long long)ctx->m.N * ctx->m.N * ctx->m.S;
-  PLUSS_HIP_CHECK(hipMemcpyAsync(ctx->g.trav, &total, 8, hipMemcpyHostToDevice, pick(ctx, stream)));
-  PLUSS_HIP_CHECK(hipStreamSynchronize(pick(ctx, stream)));  // `total` is a stack value
-  return PLUSS_OK;
+  return launch_fulltrace(ctx, pick(ctx, stream));  // the kernel also adds N*N*(4N+2) to traversed[0]
 }
 
 int pluss_dev_sampled_ri(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, int64_t* d_ri, uint64_t* d_sink,

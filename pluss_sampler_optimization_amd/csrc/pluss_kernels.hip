@@ -771,6 +771,7 @@ __global__ __launch_bounds__(BLOCK) void k_fulltrace(Model m, GTable g) {
   __syncthreads();
   const uint64_t nwaves = (uint64_t)gridDim.x * (BLOCK / 64);
   const uint64_t npairs = (uint64_t)m.N * m.N;
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g.trav[0], npairs * m.S);  // accesses traversed
   for (uint64_t pr = (uint64_t)blockIdx.x * (BLOCK / 64) + wave; pr < npairs; pr += nwaves) {
     const uint32_t c0 = (uint32_t)(pr / m.N), c1 = (uint32_t)(pr - (uint64_t)c0 * m.N);
     if (BINS) {
@@ -853,6 +854,7 @@ __global__ __launch_bounds__(BLOCK) void k_fulltrace_count(Model m, GTable g) {
     bump(!c1last ? 16 : 17, nlive - nC3);                 // C3 at c2 = N-1: next c1, or cold
   }
   if (lane < DBINS && acc) atomicAdd(&tot[lane], acc);
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g.trav[0], npairs * m.S);  // accesses traversed
   __syncthreads();
   tail_accumulate(tot, g);
 }
