@@ -19,22 +19,59 @@
 //   traversed (r10:694) = sum over replays of (end key - start key), end key =
 //                 the replay's last sink, or A*T for a replay that runs to the end.
 //
+// Packed keys (N % W == 0 shapes): a sample's sink is key + RI*T with RI one of
+// its reference's three outcomes, so the sort carries (key << 2 | case) alone
+// -- a keys-only radix sort of 8-byte words instead of (key, sink) pairs --
+// and every later pass recomputes the sink from the case (PkView).
+//
 // Validated against the reference's own dumps (tests/golden/r10_*, 42/42).
 #include <hip/hip_runtime.h>
 
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "pluss_device.h"
 
 namespace pluss {
 
+// Reuse intervals of one reference's three outcomes (packed-key mode).
+struct PkView {
+  int64_t ri[3];
+  uint64_t T;
+};
+inline PkView make_pkview(const Model& m, uint32_t ref) {
+  PkView v;
+  for (int c = 0; c < 3; ++c) v.ri[c] = key_ri(m.keytab[ref * 3 + c]);
+  v.T = m.T;
+  return v;
+}
+__device__ __forceinline__ unsigned long long pk_sink(unsigned long long pk, const PkView& v) {
+  const uint32_t c = (uint32_t)(pk & 3u);
+  const int64_t ri = c == 0 ? v.ri[0] : (c == 1 ? v.ri[1] : v.ri[2]);
+  if (c == 3 || ri < 0 || pk == KEY_EMPTY) return KEY_EMPTY;
+  return (pk >> 2) + (unsigned long long)ri * v.T;
+}
+template <bool PK>
+__device__ __forceinline__ unsigned long long key_at(const unsigned long long* keys, uint64_t i) {
+  return PK ? (keys[i] == KEY_EMPTY ? KEY_EMPTY : keys[i] >> 2) : keys[i];
+}
+template <bool PK>
+__device__ __forceinline__ unsigned long long sink_at(const unsigned long long* keys, const unsigned long long* sinks,
+                                                      uint64_t i, const PkView& v) {
+  return PK ? pk_sink(keys[i], v) : sinks[i];
+}
+struct PkSinkOp {  // rocprim transform: packed key -> sink
+  PkView v;
+  __device__ unsigned long long operator()(unsigned long long pk) const { return pk_sink(pk, v); }
+};
+
 // Key and sink of every sample.  cnt == nullptr: sample i -> slot i (one
 // GPU).  Otherwise only samples with key in [lo, hi) are kept, compacted
 // through a wave-aggregated counter (their order is irrelevant: they are
 // sorted next).
-template <bool FAST>
+template <bool FAST, bool PK = false>
 __global__ __launch_bounds__(BLOCK) void k_faith_keys(Model m, uint32_t ref, const uint64_t* __restrict__ smp,
                                                       uint64_t n, uint64_t lo, uint64_t hi,
                                                       unsigned long long* __restrict__ keys,
@@ -52,19 +89,23 @@ __global__ __launch_bounds__(BLOCK) void k_faith_keys(Model m, uint32_t ref, con
         keep = cnt == nullptr;  // one GPU: the slot still has to be filled
       } else {
         const uint32_t c2 = (ref == C0 || ref == C1) ? 0u : s.c2;
-        const int64_t ri = ri_of<FAST>(m, ref, s.c0, s.c1, c2);
         uint64_t P;
         uint32_t t;
         position(m, ref, s.c0, s.c1, c2, &P, &t);
         key = P * m.T + t;
-        sink = ri < 0 ? KEY_EMPTY : (P + (uint64_t)ri) * m.T + t;
         keep = cnt == nullptr || (key >= lo && key < hi);
+        if (PK) {
+          key = (key << 2) | case_fast<false>(m, ref, s.c0, s.c1, c2);
+        } else {
+          const int64_t ri = ri_of<FAST>(m, ref, s.c0, s.c1, c2);
+          sink = ri < 0 ? KEY_EMPTY : (P + (uint64_t)ri) * m.T + t;
+        }
       }
     }
     if (cnt == nullptr) {
       if (i < n) {
         keys[i] = key;
-        sinks[i] = sink;
+        if (!PK) sinks[i] = sink;
       }
       continue;
     }
@@ -76,7 +117,7 @@ __global__ __launch_bounds__(BLOCK) void k_faith_keys(Model m, uint32_t ref, con
     if (keep) {
       const uint64_t o = at + __popcll(mask & ((1ull << __lane_id()) - 1));
       keys[o] = key;
-      sinks[o] = sink;
+      if (!PK) sinks[o] = sink;
     }
   }
 }
@@ -96,13 +137,14 @@ __device__ __forceinline__ unsigned long long gmax(const unsigned long long* pma
   return v > pmax_in ? v : pmax_in;
 }
 
+template <bool PK>
 __global__ __launch_bounds__(BLOCK) void k_faith_flags(const unsigned long long* __restrict__ keys,
                                                        const unsigned long long* __restrict__ pmax, uint64_t n,
                                                        uint64_t j_off, unsigned long long pmax_in,
                                                        unsigned int* __restrict__ flags) {
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
     const unsigned long long before = i == 0 ? pmax_in : gmax(pmax, i - 1, pmax_in);
-    flags[i] = (j_off + i == 0 || keys[i] > before) ? 1u : 0u;
+    flags[i] = (j_off + i == 0 || key_at<PK>(keys, i) > before) ? 1u : 0u;
   }
 }
 
@@ -132,13 +174,13 @@ __global__ __launch_bounds__(BLOCK) void k_faith_cut(const unsigned int* __restr
 // samples, and the traversed contributions of the replays that start or end
 // here (a replay ends at j when j + 1 == cut or j + 1 starts one; for the
 // shard's last sample that is `next_start`, decided by the caller).
-template <bool FAST>
+template <bool FAST, bool PK = false>
 __global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, const unsigned long long* __restrict__ keys,
                                                       const unsigned long long* __restrict__ sinks,
                                                       const unsigned long long* __restrict__ pmax,
                                                       const unsigned int* __restrict__ flags, uint64_t n,
                                                       uint64_t j_off, unsigned long long pmax_in, int next_start,
-                                                      unsigned long long* scal, GTable g) {
+                                                      unsigned long long* scal, GTable g, PkView pv) {
   __shared__ unsigned long long tk[TCAP];
   __shared__ unsigned int tc[TCAP];
   __shared__ unsigned long long red[2];
@@ -159,7 +201,7 @@ __global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, con
     uint64_t key = KEY_NONE;
     bool rec = false;
     if (v) {
-      const unsigned long long k = keys[i], s = sinks[i];
+      const unsigned long long k = key_at<PK>(keys, i), s = sink_at<PK>(keys, sinks, i, pv);
       if (s == KEY_EMPTY) {
         cold += (k % m.T == 0) ? 1u : 0u;
       } else {
@@ -255,9 +297,16 @@ static int faith_reserve(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
 static int faith_tmp(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
   FaithfulBufs& b = ctx->fb;
   size_t t1 = 0, t2 = 0, t3 = 0;
-  PLUSS_HIP_CHECK(
-      rocprim::radix_sort_pairs(nullptr, t1, b.keys, b.keys_s, b.sinks, b.sinks_s, n, 0, key_bits(ctx->m), s));
-  PLUSS_HIP_CHECK(rocprim::inclusive_scan(nullptr, t2, b.sinks_s, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
+  if (ctx->m.fast) {  // packed keys: keys-only sort, pmax over the recomputed sinks
+    PLUSS_HIP_CHECK(rocprim::radix_sort_keys(nullptr, t1, b.keys, b.keys_s, n, 0, key_bits(ctx->m) + 2, s));
+    auto it = rocprim::make_transform_iterator(b.keys_s, PkSinkOp{make_pkview(ctx->m, 0)});
+    PLUSS_HIP_CHECK(rocprim::inclusive_scan(nullptr, t2, it, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
+  } else {
+    PLUSS_HIP_CHECK(
+        rocprim::radix_sort_pairs(nullptr, t1, b.keys, b.keys_s, b.sinks, b.sinks_s, n, 0, key_bits(ctx->m), s));
+    PLUSS_HIP_CHECK(
+        rocprim::inclusive_scan(nullptr, t2, b.sinks_s, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
+  }
   PLUSS_HIP_CHECK(rocprim::inclusive_scan(nullptr, t3, b.flags, b.nstart, n, rocprim::plus<unsigned int>(), s));
   size_t need = t1 > t2 ? t1 : t2;
   need = need > t3 ? need : t3;
@@ -279,8 +328,8 @@ static int faith_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, ui
   const Model& m = ctx->m;
   FaithfulBufs& b = ctx->fb;
   if (m.fast)
-    hipLaunchKernelGGL(k_faith_keys<true>, dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, d_samples, n, lo, hi,
-                       b.keys, b.sinks, cnt, ctx->g);
+    hipLaunchKernelGGL((k_faith_keys<true, true>), dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, d_samples, n,
+                       lo, hi, b.keys, b.sinks, cnt, ctx->g);
   else
     hipLaunchKernelGGL(k_faith_keys<false>, dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, d_samples, n, lo,
                        hi, b.keys, b.sinks, cnt, ctx->g);
@@ -289,10 +338,17 @@ static int faith_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, ui
 }
 
 // sort the shard's n (key, sink) pairs by key and take the prefix max of sinks
-static int faith_sort(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
+static int faith_sort(pluss_ctx* ctx, int32_t ref, uint64_t n, hipStream_t s) {
   FaithfulBufs& b = ctx->fb;
   if (int rc = faith_tmp(ctx, n, s)) return rc;
   size_t sz = b.tmp_bytes;
+  if (ctx->m.fast) {
+    PLUSS_HIP_CHECK(rocprim::radix_sort_keys(b.tmp, sz, b.keys, b.keys_s, n, 0, key_bits(ctx->m) + 2, s));
+    sz = b.tmp_bytes;
+    auto it = rocprim::make_transform_iterator(b.keys_s, PkSinkOp{make_pkview(ctx->m, (uint32_t)ref)});
+    PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, it, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
+    return PLUSS_OK;
+  }
   PLUSS_HIP_CHECK(
       rocprim::radix_sort_pairs(b.tmp, sz, b.keys, b.keys_s, b.sinks, b.sinks_s, n, 0, key_bits(ctx->m), s));
   sz = b.tmp_bytes;
@@ -302,7 +358,12 @@ static int faith_sort(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
 
 static int faith_starts(pluss_ctx* ctx, uint64_t n, uint64_t j_off, unsigned long long pmax_in, hipStream_t s) {
   FaithfulBufs& b = ctx->fb;
-  hipLaunchKernelGGL(k_faith_flags, dim3(grid_of(n)), dim3(BLOCK), 0, s, b.keys_s, b.pmax, n, j_off, pmax_in, b.flags);
+  if (ctx->m.fast)
+    hipLaunchKernelGGL(k_faith_flags<true>, dim3(grid_of(n)), dim3(BLOCK), 0, s, b.keys_s, b.pmax, n, j_off, pmax_in,
+                       b.flags);
+  else
+    hipLaunchKernelGGL(k_faith_flags<false>, dim3(grid_of(n)), dim3(BLOCK), 0, s, b.keys_s, b.pmax, n, j_off, pmax_in,
+                       b.flags);
   PLUSS_HIP_CHECK(hipGetLastError());
   size_t sz = b.tmp_bytes;
   PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, b.flags, b.nstart, n, rocprim::plus<unsigned int>(), s));
@@ -314,12 +375,13 @@ static int faith_record(pluss_ctx* ctx, int32_t ref, uint64_t n, uint64_t j_off,
   const Model& m = ctx->m;
   FaithfulBufs& b = ctx->fb;
   if (n) {
+    const PkView pv = make_pkview(m, (uint32_t)ref);
     if (m.fast)
-      hipLaunchKernelGGL(k_faith_hist<true>, dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, b.keys_s, b.sinks_s,
-                         b.pmax, b.flags, n, j_off, pmax_in, next_start, b.scal, ctx->g);
+      hipLaunchKernelGGL((k_faith_hist<true, true>), dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, b.keys_s,
+                         b.sinks_s, b.pmax, b.flags, n, j_off, pmax_in, next_start, b.scal, ctx->g, pv);
     else
       hipLaunchKernelGGL(k_faith_hist<false>, dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, b.keys_s,
-                         b.sinks_s, b.pmax, b.flags, n, j_off, pmax_in, next_start, b.scal, ctx->g);
+                         b.sinks_s, b.pmax, b.flags, n, j_off, pmax_in, next_start, b.scal, ctx->g, pv);
   }
   hipLaunchKernelGGL(k_faith_finish, dim3(1), dim3(1), 0, s, m, (uint32_t)ref, n, n_total, is_last, pmax_in, b.pmax,
                      b.scal, ctx->g);
@@ -334,7 +396,7 @@ int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint
   if (n == 0) return PLUSS_OK;
   FaithfulBufs& b = ctx->fb;
   if (int rc = faith_keys(ctx, ref, d_samples, n, 0, 0, nullptr, s)) return rc;
-  if (int rc = faith_sort(ctx, n, s)) return rc;
+  if (int rc = faith_sort(ctx, ref, n, s)) return rc;
   if (int rc = faith_starts(ctx, n, 0, 0, s)) return rc;
   hipLaunchKernelGGL(k_faith_init, dim3(1), dim3(1), 0, s, b.scal, n);
   hipLaunchKernelGGL(k_faith_cut, dim3(grid_of(n)), dim3(BLOCK), 0, s, b.flags, b.nstart, n, (uint64_t)0, (uint64_t)0,
@@ -364,10 +426,11 @@ int faith_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uin
   out->first_key = KEY_EMPTY;
   out->max_sink = 0;
   if (m) {
-    if (int rc = faith_sort(ctx, m, s)) return rc;
+    if (int rc = faith_sort(ctx, ref, m, s)) return rc;
     PLUSS_HIP_CHECK(hipMemcpyAsync(&out->first_key, b.keys_s, 8, hipMemcpyDeviceToHost, s));
     PLUSS_HIP_CHECK(hipMemcpyAsync(&out->max_sink, b.pmax + (m - 1), 8, hipMemcpyDeviceToHost, s));
     PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+    if (ctx->m.fast && out->first_key != KEY_EMPTY) out->first_key >>= 2;  // packed (key << 2 | case)
   }
   f.max_sink = out->max_sink;
   f.phase = 1;

@@ -830,9 +830,12 @@ __global__ __launch_bounds__(BLOCK) void k_fulltrace_count(Model m, GTable g) {
   const uint32_t Wm1 = m.W - 1;
   const uint64_t nwaves = (uint64_t)gridDim.x * (BLOCK / 64);
   const uint64_t npairs = (uint64_t)m.N * m.N;
+  const bool small = npairs < (1ull << 31);  // pair index fits the 32-bit fast division by N
   for (uint64_t pr = (uint64_t)blockIdx.x * (BLOCK / 64) + wave; pr < npairs; pr += nwaves) {
-    const uint32_t c0 = (uint32_t)(pr / m.N), c1 = (uint32_t)(pr - (uint64_t)c0 * m.N);
+    const uint32_t c0 = small ? fdiv((uint32_t)pr, m.dN) : (uint32_t)(pr / m.N);
+    const uint32_t c1 = (uint32_t)(pr - (uint64_t)c0 * m.N);
     uint32_t nlive = 0, nA0 = 0, nC3 = 0;  // accesses per reference; A0 case 0; C3 case 0
+#pragma unroll 4
     for (uint32_t c2b = 0; c2b < m.N; c2b += 64) {
       const uint32_t c2 = c2b + lane;
       const uint64_t live = __ballot(c2 < m.N);
