@@ -824,7 +824,8 @@ __global__ __launch_bounds__(BLOCK) void k_fulltrace_count(Model m, GTable g) {
   __shared__ unsigned long long tot[DBINS];
   if (threadIdx.x < DBINS) tot[threadIdx.x] = 0;
   __syncthreads();
-  const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
+  const uint32_t lane = __lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: pair indices in SGPRs
   unsigned long long acc = 0;
   auto bump = [&acc, lane](uint32_t bin, uint32_t v) { acc += lane == bin ? (unsigned long long)v : 0ull; };
   const uint32_t Wm1 = m.W - 1;
@@ -835,7 +836,6 @@ __global__ __launch_bounds__(BLOCK) void k_fulltrace_count(Model m, GTable g) {
     const uint32_t c0 = small ? fdiv((uint32_t)pr, m.dN) : (uint32_t)(pr / m.N);
     const uint32_t c1 = (uint32_t)(pr - (uint64_t)c0 * m.N);
     uint32_t nlive = 0, nA0 = 0, nC3 = 0;  // accesses per reference; A0 case 0; C3 case 0
-#pragma unroll 4
     for (uint32_t c2b = 0; c2b < m.N; c2b += 64) {
       const uint32_t c2 = c2b + lane;
       const uint64_t live = __ballot(c2 < m.N);
@@ -1184,10 +1184,12 @@ int launch_fulltrace(pluss_ctx* ctx, hipStream_t s) {
   const int nb = grid_for(npairs, BLOCK / 64 * 8);
   const char* leg = getenv("PLUSS_LEGACY");  // diagnostics: the lane-counter full trace
   const bool legacy = leg && leg[0] == '1';
+  // the ballot kernel's waves are short dependency chains: 8 waves per SIMD (2048 workgroups) hide them
+  const int nbc = grid_for(npairs, BLOCK / 64 * 8, 2048);
   if (ctx->m.fast && !legacy && ctx->m.p2)
-    hipLaunchKernelGGL(k_fulltrace_count<true>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ctx->g);
+    hipLaunchKernelGGL(k_fulltrace_count<true>, dim3(nbc), dim3(BLOCK), 0, s, ctx->m, ctx->g);
   else if (ctx->m.fast && !legacy)
-    hipLaunchKernelGGL(k_fulltrace_count<false>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ctx->g);
+    hipLaunchKernelGGL(k_fulltrace_count<false>, dim3(nbc), dim3(BLOCK), 0, s, ctx->m, ctx->g);
   else if (ctx->m.fast && ctx->m.p2)
     hipLaunchKernelGGL(k_fulltrace<FAST_P2>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ctx->g);
   else if (ctx->m.fast)
