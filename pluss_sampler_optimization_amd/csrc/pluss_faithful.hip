@@ -20,14 +20,19 @@
 //                 the replay's last sink, or A*T for a replay that runs to the end.
 //
 // Packed keys (N % W == 0 shapes): a sample's sink is key + RI*T with RI one of
-// its reference's three outcomes, so the sort carries (key << 2 | case) alone
-// -- a keys-only radix sort of 8-byte words instead of (key, sink) pairs --
-// and every later pass recomputes the sink from the case (PkView).
+// its reference's three outcomes, so the sort carries only a packed word
+// (rank << 2 | case), where rank = ((q*N + c1)*N + c2)*T + tid is the
+// sample's position among its reference's N^3 possible keys in key order
+// (q = thread-local row).  That is a keys-only radix sort over
+// bitlen(N^3) + 2 bits -- 32-bit words up to N = 1024 -- instead of 64-bit
+// (key, sink) pairs, and every later pass recomputes key and sink from the
+// word (PkView).
 //
 // Validated against the reference's own dumps (tests/golden/r10_*, 42/42).
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <type_traits>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
@@ -36,51 +41,96 @@
 
 namespace pluss {
 
-// Reuse intervals of one reference's three outcomes (packed-key mode).
+// Faithful-mode key storage: FM_PAIRS = 64-bit (key, sink) pairs (any
+// shape); FM_PK64 / FM_PK32 = packed (rank << 2 | case) words of 64 / 32 bits.
+enum : int { FM_PAIRS = 0, FM_PK64 = 1, FM_PK32 = 2 };
+template <int FM>
+using fkey_t = typename std::conditional<FM == FM_PK32, uint32_t, unsigned long long>::type;
+
+// Decoding of packed words for one reference.
 struct PkView {
-  int64_t ri[3];
-  uint64_t T;
+  int64_t ri[3];             // RI of case 0/1/2 (-1: cold)
+  uint64_t T, N, R, S;
+  uint32_t ref, p2, tsh, nsh;  // p2: N and T powers of two (shifts)
 };
 inline PkView make_pkview(const Model& m, uint32_t ref) {
   PkView v;
   for (int c = 0; c < 3; ++c) v.ri[c] = key_ri(m.keytab[ref * 3 + c]);
   v.T = m.T;
+  v.N = m.N;
+  v.R = m.R;
+  v.S = m.S;
+  v.ref = ref;
+  v.tsh = v.nsh = 0;
+  while ((1ull << v.tsh) < v.T) ++v.tsh;
+  while ((1ull << v.nsh) < v.N) ++v.nsh;
+  v.p2 = ((1ull << v.tsh) == v.T && (1ull << v.nsh) == v.N) ? 1u : 0u;
   return v;
 }
-__device__ __forceinline__ unsigned long long pk_sink(unsigned long long pk, const PkView& v) {
+// the key a*T + tid of a packed word (KEY_EMPTY for the malformed marker ~0)
+template <typename KT>
+__host__ __device__ __forceinline__ unsigned long long pk_key(KT pk, const PkView& v) {
+  if (pk == (KT) ~(KT)0) return KEY_EMPTY;
+  uint64_t r = (uint64_t)(pk >> 2), t, c2, c1, q;
+  if (v.p2) {
+    t = r & (v.T - 1);
+    r >>= v.tsh;
+    c2 = r & (v.N - 1);
+    r >>= v.nsh;
+    c1 = r & (v.N - 1);
+    q = r >> v.nsh;
+  } else {
+    t = r % v.T;
+    r /= v.T;
+    c2 = r % v.N;
+    r /= v.N;
+    c1 = r % v.N;
+    q = r / v.N;
+  }
+  const uint64_t off = v.ref < 2 ? v.ref : v.ref + 4 * c2;
+  return (q * v.R + c1 * v.S + off) * v.T + t;
+}
+template <typename KT>
+__device__ __forceinline__ unsigned long long pk_sink(KT pk, const PkView& v) {
   const uint32_t c = (uint32_t)(pk & 3u);
+  if (pk == (KT) ~(KT)0 || c == 3) return KEY_EMPTY;
   const int64_t ri = c == 0 ? v.ri[0] : (c == 1 ? v.ri[1] : v.ri[2]);
-  if (c == 3 || ri < 0 || pk == KEY_EMPTY) return KEY_EMPTY;
-  return (pk >> 2) + (unsigned long long)ri * v.T;
+  return ri < 0 ? KEY_EMPTY : pk_key(pk, v) + (unsigned long long)ri * v.T;
 }
-template <bool PK>
-__device__ __forceinline__ unsigned long long key_at(const unsigned long long* keys, uint64_t i) {
-  return PK ? (keys[i] == KEY_EMPTY ? KEY_EMPTY : keys[i] >> 2) : keys[i];
+// key / sink of sorted element i
+template <int FM>
+__device__ __forceinline__ unsigned long long key_at(const void* keys, uint64_t i, const PkView& v) {
+  if (FM == FM_PAIRS) return static_cast<const unsigned long long*>(keys)[i];
+  return pk_key(static_cast<const fkey_t<FM>*>(keys)[i], v);
 }
-template <bool PK>
-__device__ __forceinline__ unsigned long long sink_at(const unsigned long long* keys, const unsigned long long* sinks,
-                                                      uint64_t i, const PkView& v) {
-  return PK ? pk_sink(keys[i], v) : sinks[i];
+template <int FM>
+__device__ __forceinline__ unsigned long long sink_at(const void* keys, const unsigned long long* sinks, uint64_t i,
+                                                      const PkView& v) {
+  if (FM == FM_PAIRS) return sinks[i];
+  return pk_sink(static_cast<const fkey_t<FM>*>(keys)[i], v);
 }
-struct PkSinkOp {  // rocprim transform: packed key -> sink
+template <typename KT>
+struct PkSinkOp {  // rocprim transform: packed word -> sink
   PkView v;
-  __device__ unsigned long long operator()(unsigned long long pk) const { return pk_sink(pk, v); }
+  __device__ unsigned long long operator()(KT pk) const { return pk_sink(pk, v); }
 };
 
 // Key and sink of every sample.  cnt == nullptr: sample i -> slot i (one
 // GPU).  Otherwise only samples with key in [lo, hi) are kept, compacted
 // through a wave-aggregated counter (their order is irrelevant: they are
 // sorted next).
-template <bool FAST, bool PK = false>
+template <bool FAST, int FM = FM_PAIRS>
 __global__ __launch_bounds__(BLOCK) void k_faith_keys(Model m, uint32_t ref, const uint64_t* __restrict__ smp,
-                                                      uint64_t n, uint64_t lo, uint64_t hi,
-                                                      unsigned long long* __restrict__ keys,
+                                                      uint64_t n, uint64_t lo, uint64_t hi, void* __restrict__ keys_out,
                                                       unsigned long long* __restrict__ sinks, unsigned long long* cnt,
                                                       GTable g) {
+  typedef fkey_t<FM> KT;
+  KT* keys = static_cast<KT*>(keys_out);
   const uint64_t step = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t base = (uint64_t)blockIdx.x * BLOCK; base < n; base += step) {
     const uint64_t i = base + threadIdx.x;
     unsigned long long key = KEY_EMPTY, sink = KEY_EMPTY;
+    KT word = (KT) ~(KT)0;
     bool keep = false;
     if (i < n) {
       const Sample s = unpack(smp[i]);
@@ -94,18 +144,22 @@ __global__ __launch_bounds__(BLOCK) void k_faith_keys(Model m, uint32_t ref, con
         position(m, ref, s.c0, s.c1, c2, &P, &t);
         key = P * m.T + t;
         keep = cnt == nullptr || (key >= lo && key < hi);
-        if (PK) {
-          key = (key << 2) | case_fast<false>(m, ref, s.c0, s.c1, c2);
+        if (FM != FM_PAIRS) {
+          const uint32_t k = fdiv(s.c0, m.dCS), p = s.c0 - k * m.CS;
+          const uint64_t q = (uint64_t)fdiv(k, m.dT) * m.CS + p;
+          const uint64_t rank = ((q * m.N + s.c1) * m.N + c2) * m.T + t;
+          word = (KT)((rank << 2) | case_fast<false>(m, ref, s.c0, s.c1, c2));
         } else {
           const int64_t ri = ri_of<FAST>(m, ref, s.c0, s.c1, c2);
           sink = ri < 0 ? KEY_EMPTY : (P + (uint64_t)ri) * m.T + t;
+          word = (KT)key;
         }
       }
     }
     if (cnt == nullptr) {
       if (i < n) {
-        keys[i] = key;
-        if (!PK) sinks[i] = sink;
+        keys[i] = word;
+        if (FM == FM_PAIRS) sinks[i] = sink;
       }
       continue;
     }
@@ -116,8 +170,8 @@ __global__ __launch_bounds__(BLOCK) void k_faith_keys(Model m, uint32_t ref, con
     at = __shfl(at, __ffsll((long long)mask) - 1, 64);
     if (keep) {
       const uint64_t o = at + __popcll(mask & ((1ull << __lane_id()) - 1));
-      keys[o] = key;
-      if (!PK) sinks[o] = sink;
+      keys[o] = word;
+      if (FM == FM_PAIRS) sinks[o] = sink;
     }
   }
 }
@@ -137,14 +191,14 @@ __device__ __forceinline__ unsigned long long gmax(const unsigned long long* pma
   return v > pmax_in ? v : pmax_in;
 }
 
-template <bool PK>
-__global__ __launch_bounds__(BLOCK) void k_faith_flags(const unsigned long long* __restrict__ keys,
+template <int FM>
+__global__ __launch_bounds__(BLOCK) void k_faith_flags(const void* __restrict__ keys,
                                                        const unsigned long long* __restrict__ pmax, uint64_t n,
                                                        uint64_t j_off, unsigned long long pmax_in,
-                                                       unsigned int* __restrict__ flags) {
+                                                       unsigned int* __restrict__ flags, PkView pv) {
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
     const unsigned long long before = i == 0 ? pmax_in : gmax(pmax, i - 1, pmax_in);
-    flags[i] = (j_off + i == 0 || key_at<PK>(keys, i) > before) ? 1u : 0u;
+    flags[i] = (j_off + i == 0 || key_at<FM>(keys, i, pv) > before) ? 1u : 0u;
   }
 }
 
@@ -174,8 +228,8 @@ __global__ __launch_bounds__(BLOCK) void k_faith_cut(const unsigned int* __restr
 // samples, and the traversed contributions of the replays that start or end
 // here (a replay ends at j when j + 1 == cut or j + 1 starts one; for the
 // shard's last sample that is `next_start`, decided by the caller).
-template <bool FAST, bool PK = false>
-__global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, const unsigned long long* __restrict__ keys,
+template <bool FAST, int FM = FM_PAIRS>
+__global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, const void* __restrict__ keys,
                                                       const unsigned long long* __restrict__ sinks,
                                                       const unsigned long long* __restrict__ pmax,
                                                       const unsigned int* __restrict__ flags, uint64_t n,
@@ -201,7 +255,7 @@ __global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, con
     uint64_t key = KEY_NONE;
     bool rec = false;
     if (v) {
-      const unsigned long long k = key_at<PK>(keys, i), s = sink_at<PK>(keys, sinks, i, pv);
+      const unsigned long long k = key_at<FM>(keys, i, pv), s = sink_at<FM>(keys, sinks, i, pv);
       if (s == KEY_EMPTY) {
         cold += (k % m.T == 0) ? 1u : 0u;
       } else {
@@ -268,6 +322,18 @@ static unsigned key_bits(const Model& m) {  // keys < A*T: sort only the signifi
   return end_bit;
 }
 
+static unsigned pk_bits(const Model& m) {  // packed words < N^3 << 2
+  const uint64_t top = (uint64_t)m.N * m.N * m.N - 1;
+  unsigned b = 1;
+  while (b < 62 && (top >> b)) ++b;
+  return b + 2;
+}
+
+static int faith_fm(const Model& m) {
+  if (!m.fast) return FM_PAIRS;
+  return pk_bits(m) <= 32 ? FM_PK32 : FM_PK64;
+}
+
 static int grid_of(uint64_t n) {
   const uint64_t b = (n + BLOCK * 4 - 1) / (BLOCK * 4);
   return b < 1 ? 1 : (b > (uint64_t)MAX_BLOCKS ? MAX_BLOCKS : (int)b);
@@ -297,9 +363,15 @@ static int faith_reserve(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
 static int faith_tmp(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
   FaithfulBufs& b = ctx->fb;
   size_t t1 = 0, t2 = 0, t3 = 0;
-  if (ctx->m.fast) {  // packed keys: keys-only sort, pmax over the recomputed sinks
-    PLUSS_HIP_CHECK(rocprim::radix_sort_keys(nullptr, t1, b.keys, b.keys_s, n, 0, key_bits(ctx->m) + 2, s));
-    auto it = rocprim::make_transform_iterator(b.keys_s, PkSinkOp{make_pkview(ctx->m, 0)});
+  const int fm = faith_fm(ctx->m);
+  if (fm == FM_PK32) {  // packed words: keys-only sort, pmax over the recomputed sinks
+    uint32_t *k = (uint32_t*)b.keys, *ks = (uint32_t*)b.keys_s;
+    PLUSS_HIP_CHECK(rocprim::radix_sort_keys(nullptr, t1, k, ks, n, 0, pk_bits(ctx->m), s));
+    auto it = rocprim::make_transform_iterator(ks, PkSinkOp<uint32_t>{make_pkview(ctx->m, 0)});
+    PLUSS_HIP_CHECK(rocprim::inclusive_scan(nullptr, t2, it, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
+  } else if (fm == FM_PK64) {
+    PLUSS_HIP_CHECK(rocprim::radix_sort_keys(nullptr, t1, b.keys, b.keys_s, n, 0, pk_bits(ctx->m), s));
+    auto it = rocprim::make_transform_iterator(b.keys_s, PkSinkOp<unsigned long long>{make_pkview(ctx->m, 0)});
     PLUSS_HIP_CHECK(rocprim::inclusive_scan(nullptr, t2, it, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
   } else {
     PLUSS_HIP_CHECK(
@@ -327,12 +399,16 @@ static int faith_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, ui
                       unsigned long long* cnt, hipStream_t s) {
   const Model& m = ctx->m;
   FaithfulBufs& b = ctx->fb;
-  if (m.fast)
-    hipLaunchKernelGGL((k_faith_keys<true, true>), dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, d_samples, n,
-                       lo, hi, b.keys, b.sinks, cnt, ctx->g);
+  const int fm = faith_fm(m);
+  if (fm == FM_PK32)
+    hipLaunchKernelGGL((k_faith_keys<true, FM_PK32>), dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, d_samples,
+                       n, lo, hi, (void*)b.keys, b.sinks, cnt, ctx->g);
+  else if (fm == FM_PK64)
+    hipLaunchKernelGGL((k_faith_keys<true, FM_PK64>), dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, d_samples,
+                       n, lo, hi, (void*)b.keys, b.sinks, cnt, ctx->g);
   else
     hipLaunchKernelGGL(k_faith_keys<false>, dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, d_samples, n, lo,
-                       hi, b.keys, b.sinks, cnt, ctx->g);
+                       hi, (void*)b.keys, b.sinks, cnt, ctx->g);
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }
@@ -342,10 +418,20 @@ static int faith_sort(pluss_ctx* ctx, int32_t ref, uint64_t n, hipStream_t s) {
   FaithfulBufs& b = ctx->fb;
   if (int rc = faith_tmp(ctx, n, s)) return rc;
   size_t sz = b.tmp_bytes;
-  if (ctx->m.fast) {
-    PLUSS_HIP_CHECK(rocprim::radix_sort_keys(b.tmp, sz, b.keys, b.keys_s, n, 0, key_bits(ctx->m) + 2, s));
+  const int fm = faith_fm(ctx->m);
+  if (fm == FM_PK32) {
+    uint32_t *k = (uint32_t*)b.keys, *ks = (uint32_t*)b.keys_s;
+    PLUSS_HIP_CHECK(rocprim::radix_sort_keys(b.tmp, sz, k, ks, n, 0, pk_bits(ctx->m), s));
     sz = b.tmp_bytes;
-    auto it = rocprim::make_transform_iterator(b.keys_s, PkSinkOp{make_pkview(ctx->m, (uint32_t)ref)});
+    auto it = rocprim::make_transform_iterator(ks, PkSinkOp<uint32_t>{make_pkview(ctx->m, (uint32_t)ref)});
+    PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, it, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
+    return PLUSS_OK;
+  }
+  if (fm == FM_PK64) {
+    PLUSS_HIP_CHECK(rocprim::radix_sort_keys(b.tmp, sz, b.keys, b.keys_s, n, 0, pk_bits(ctx->m), s));
+    sz = b.tmp_bytes;
+    auto it = rocprim::make_transform_iterator(b.keys_s,
+                                               PkSinkOp<unsigned long long>{make_pkview(ctx->m, (uint32_t)ref)});
     PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, it, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
     return PLUSS_OK;
   }
@@ -356,14 +442,20 @@ static int faith_sort(pluss_ctx* ctx, int32_t ref, uint64_t n, hipStream_t s) {
   return PLUSS_OK;
 }
 
-static int faith_starts(pluss_ctx* ctx, uint64_t n, uint64_t j_off, unsigned long long pmax_in, hipStream_t s) {
+static int faith_starts(pluss_ctx* ctx, int32_t ref, uint64_t n, uint64_t j_off, unsigned long long pmax_in,
+                        hipStream_t s) {
   FaithfulBufs& b = ctx->fb;
-  if (ctx->m.fast)
-    hipLaunchKernelGGL(k_faith_flags<true>, dim3(grid_of(n)), dim3(BLOCK), 0, s, b.keys_s, b.pmax, n, j_off, pmax_in,
-                       b.flags);
+  const PkView pv = make_pkview(ctx->m, (uint32_t)ref);
+  const int fm = faith_fm(ctx->m);
+  if (fm == FM_PK32)
+    hipLaunchKernelGGL(k_faith_flags<FM_PK32>, dim3(grid_of(n)), dim3(BLOCK), 0, s, (const void*)b.keys_s, b.pmax, n,
+                       j_off, pmax_in, b.flags, pv);
+  else if (fm == FM_PK64)
+    hipLaunchKernelGGL(k_faith_flags<FM_PK64>, dim3(grid_of(n)), dim3(BLOCK), 0, s, (const void*)b.keys_s, b.pmax, n,
+                       j_off, pmax_in, b.flags, pv);
   else
-    hipLaunchKernelGGL(k_faith_flags<false>, dim3(grid_of(n)), dim3(BLOCK), 0, s, b.keys_s, b.pmax, n, j_off, pmax_in,
-                       b.flags);
+    hipLaunchKernelGGL(k_faith_flags<FM_PAIRS>, dim3(grid_of(n)), dim3(BLOCK), 0, s, (const void*)b.keys_s, b.pmax, n,
+                       j_off, pmax_in, b.flags, pv);
   PLUSS_HIP_CHECK(hipGetLastError());
   size_t sz = b.tmp_bytes;
   PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, b.flags, b.nstart, n, rocprim::plus<unsigned int>(), s));
@@ -376,12 +468,19 @@ static int faith_record(pluss_ctx* ctx, int32_t ref, uint64_t n, uint64_t j_off,
   FaithfulBufs& b = ctx->fb;
   if (n) {
     const PkView pv = make_pkview(m, (uint32_t)ref);
-    if (m.fast)
-      hipLaunchKernelGGL((k_faith_hist<true, true>), dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, b.keys_s,
-                         b.sinks_s, b.pmax, b.flags, n, j_off, pmax_in, next_start, b.scal, ctx->g, pv);
+    const int fm = faith_fm(m);
+    if (fm == FM_PK32)
+      hipLaunchKernelGGL((k_faith_hist<true, FM_PK32>), dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref,
+                         (const void*)b.keys_s, b.sinks_s, b.pmax, b.flags, n, j_off, pmax_in, next_start, b.scal,
+                         ctx->g, pv);
+    else if (fm == FM_PK64)
+      hipLaunchKernelGGL((k_faith_hist<true, FM_PK64>), dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref,
+                         (const void*)b.keys_s, b.sinks_s, b.pmax, b.flags, n, j_off, pmax_in, next_start, b.scal,
+                         ctx->g, pv);
     else
-      hipLaunchKernelGGL(k_faith_hist<false>, dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, b.keys_s,
-                         b.sinks_s, b.pmax, b.flags, n, j_off, pmax_in, next_start, b.scal, ctx->g, pv);
+      hipLaunchKernelGGL(k_faith_hist<false>, dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref,
+                         (const void*)b.keys_s, b.sinks_s, b.pmax, b.flags, n, j_off, pmax_in, next_start, b.scal,
+                         ctx->g, pv);
   }
   hipLaunchKernelGGL(k_faith_finish, dim3(1), dim3(1), 0, s, m, (uint32_t)ref, n, n_total, is_last, pmax_in, b.pmax,
                      b.scal, ctx->g);
@@ -397,7 +496,7 @@ int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint
   FaithfulBufs& b = ctx->fb;
   if (int rc = faith_keys(ctx, ref, d_samples, n, 0, 0, nullptr, s)) return rc;
   if (int rc = faith_sort(ctx, ref, n, s)) return rc;
-  if (int rc = faith_starts(ctx, n, 0, 0, s)) return rc;
+  if (int rc = faith_starts(ctx, ref, n, 0, 0, s)) return rc;
   hipLaunchKernelGGL(k_faith_init, dim3(1), dim3(1), 0, s, b.scal, n);
   hipLaunchKernelGGL(k_faith_cut, dim3(grid_of(n)), dim3(BLOCK), 0, s, b.flags, b.nstart, n, (uint64_t)0, (uint64_t)0,
                      n, b.scal);
@@ -427,10 +526,15 @@ int faith_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uin
   out->max_sink = 0;
   if (m) {
     if (int rc = faith_sort(ctx, ref, m, s)) return rc;
-    PLUSS_HIP_CHECK(hipMemcpyAsync(&out->first_key, b.keys_s, 8, hipMemcpyDeviceToHost, s));
+    const int fm = faith_fm(ctx->m);
+    unsigned long long w64 = 0;
+    uint32_t w32 = 0;
+    if (fm == FM_PK32) PLUSS_HIP_CHECK(hipMemcpyAsync(&w32, b.keys_s, 4, hipMemcpyDeviceToHost, s));
+    else PLUSS_HIP_CHECK(hipMemcpyAsync(&w64, b.keys_s, 8, hipMemcpyDeviceToHost, s));
     PLUSS_HIP_CHECK(hipMemcpyAsync(&out->max_sink, b.pmax + (m - 1), 8, hipMemcpyDeviceToHost, s));
     PLUSS_HIP_CHECK(hipStreamSynchronize(s));
-    if (ctx->m.fast && out->first_key != KEY_EMPTY) out->first_key >>= 2;  // packed (key << 2 | case)
+    const PkView pv = make_pkview(ctx->m, (uint32_t)ref);  // the smallest key of the shard
+    out->first_key = fm == FM_PK32 ? pk_key(w32, pv) : (fm == FM_PK64 ? pk_key(w64, pv) : w64);
   }
   f.max_sink = out->max_sink;
   f.phase = 1;
@@ -447,7 +551,7 @@ int faith_shard_starts(pluss_ctx* ctx, uint64_t j_off, uint64_t pmax_in, pluss_f
   f.pmax_in = pmax_in;
   out->n_starts = 0;
   if (f.n) {
-    if (int rc = faith_starts(ctx, f.n, j_off, pmax_in, s)) return rc;
+    if (int rc = faith_starts(ctx, f.ref, f.n, j_off, pmax_in, s)) return rc;
     unsigned int c = 0;
     PLUSS_HIP_CHECK(hipMemcpyAsync(&c, ctx->fb.nstart + (f.n - 1), 4, hipMemcpyDeviceToHost, s));
     PLUSS_HIP_CHECK(hipStreamSynchronize(s));
