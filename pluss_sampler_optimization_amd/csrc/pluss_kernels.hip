@@ -675,7 +675,8 @@ __device__ __forceinline__ void flush_counts(uint32_t& acc, unsigned long long* 
 }
 
 // ABL (diagnostics, tools/ablate.py): 0 product; 1 loads only (PLUSS_ABLATE=3); 2 count without the tail (=4)
-template <bool P2, bool NP2, bool NT, int TAIL, int UNR = UNROLL, int ABL = 0, int BS = BLOCK>
+// XAUX >= 0 (diagnostics, PLUSS_AUX): that cache-policy immediate for the sample loads instead of NT's
+template <bool P2, bool NP2, bool NT, int TAIL, int UNR = UNROLL, int ABL = 0, int BS = BLOCK, int XAUX = -1>
 __global__ __launch_bounds__(BS) void k_count(Model m, const uint64_t* __restrict__ smp, uint64_t n,
                                               const uint64_t* __restrict__ head, int has_head, GTable g,
                                               ExportArgs ex) {
@@ -686,7 +687,7 @@ __global__ __launch_bounds__(BS) void k_count(Model m, const uint64_t* __restric
   uint32_t acc = 0;  // lane b: count of bin b
   const uint64_t npairs = n >> 1;
   const uint32_t step = gridDim.x * (uint32_t)(BS * UNR);
-  constexpr int AUX = NT ? 2 : 0;  // nt: the list is streamed once per pass
+  constexpr int AUX = XAUX >= 0 ? XAUX : (NT ? 2 : 0);  // nt: the list is streamed once per pass
   for (uint64_t w0 = 0; w0 < npairs; w0 += CWIN) {
     const uint32_t wn = (uint32_t)(npairs - w0 < CWIN ? npairs - w0 : CWIN);
     const uint64_t* wp = smp + 2 * w0;
@@ -1092,6 +1093,30 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
       hipLaunchKernelGGL((k_count<P2, NP2, NT, TAIL_NONE, UNR>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n,   \
                          head, has_head, g, ex);                                                                 \
   } while (0)
+    const char* auxv = getenv("PLUSS_AUX");
+    if (m.p2 && m.np2 && tail == TAIL_DENSE && auxv) {  // diagnostics: cache-policy bits of the sample loads
+#define PLUSS_AUX_CASE(V)                                                                                          \
+  case V:                                                                                                          \
+    hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_DENSE, UNROLL, 0, BLOCK, V>), dim3(nb), dim3(BLOCK), 0, s, \
+                       m, d_samples, n, head, has_head, g, ex);                                                    \
+    break;
+      switch (atoi(auxv)) {
+        PLUSS_AUX_CASE(0)
+        PLUSS_AUX_CASE(1)
+        PLUSS_AUX_CASE(2)
+        PLUSS_AUX_CASE(3)
+        PLUSS_AUX_CASE(16)
+        PLUSS_AUX_CASE(17)
+        PLUSS_AUX_CASE(18)
+        PLUSS_AUX_CASE(19)
+        default:
+          set_error("PLUSS_AUX: one of 0 1 2 3 16 17 18 19");
+          return PLUSS_ERR_CONFIG;
+      }
+#undef PLUSS_AUX_CASE
+      PLUSS_HIP_CHECK(hipGetLastError());
+      return PLUSS_OK;
+    }
     const char* bsv = getenv("PLUSS_BS");
     if (m.p2 && m.np2 && tail == TAIL_DENSE && bsv && atoi(bsv) == 1024) {  // diagnostics: 1024-thread workgroups
       int nb4 = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)1024 * UNROLL, MAX_BLOCKS / 4);
