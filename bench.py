@@ -162,15 +162,15 @@ def faithful_bench(cfg, samples, stream):
             "recorded": h.total() - sum(h.cold(r) for r in P.REFS), "max_traversed": max(h.traversed)}
 
 
-def pmc_traffic():
-    """Per-launch HBM bytes of the hot kernel from the committed rocprofv3 --pmc summary, if any."""
+def pmc_traffic(samples_per_launch):
+    """Per-launch HBM bytes of the hot kernel from the committed rocprofv3 --pmc
+    summary, if it was taken at this launch size (tools/prof_round.sh)."""
     path = os.path.join(ROOT, "profiles", "pmc_sampled_hist.json")
-    if os.path.exists(path):
-        try:
-            return json.load(open(path)).get("hbm_bytes_per_launch")
-        except Exception:
-            return None
-    return None
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    return d.get("hbm_bytes_per_launch") if d.get("samples_per_launch") == samples_per_launch else None
 
 
 def allreduce_cpu(t):
@@ -307,7 +307,7 @@ def main():
                    "parallelism": f"sample-shard x{world}" + (" + RCCL all_reduce of the dense histogram"
                                                              if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic()},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(n_local)},
         "kernel": {"name": "pluss::k_count<true,true,true,TAIL_DENSE,2> (ballot counting, nt buffer loads, "
                            "dense tail)",
                    "avg_ms": kern_ms, "timing": "HIP events on the launch stream around the K timed steps / K"
