@@ -170,7 +170,7 @@ int pluss_ctx_destroy(pluss_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->d_table,  c->d_exp_keys, c->d_exp_counts, c->d_exp_n, c->fb.keys,  c->fb.sinks,
-                  c->fb.keys_s, c->fb.sinks_s, c->fb.pmax,      c->fb.flags, c->fb.nstart, c->fb.tmp,
+                  c->fb.keys_s, c->fb.sinks_s, c->fb.pmax,      c->fb.nstart, c->fb.tmp,
                   c->fb.scal};
   for (void* p : bufs)
     if (p) (void)hipFree(p);

@@ -11,6 +11,7 @@
 // whole sequential queue algorithm becomes:
 //
 //   sort samples by key; pmax = inclusive prefix-max of sink keys;
+//   (start flags are recomputed wherever they are needed, never stored)
 //   start_j  <=>  j == 0 || key_j > pmax_{j-1}               (new START_SAMPLE)
 //   Q1 (r10:356): first start j > 0 with (j - starts_before_j) >= S - j  -> drop [j, S)
 //   Q2 (r10:669-674): cold samples count only when tid == 0
@@ -35,6 +36,7 @@
 #include <type_traits>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
 
 #include "pluss_device.h"
@@ -191,27 +193,38 @@ __device__ __forceinline__ unsigned long long gmax(const unsigned long long* pma
   return v > pmax_in ? v : pmax_in;
 }
 
+// What the start flag of sorted element i needs: START_i <=> it is the
+// global first sample, or its key exceeds every earlier sink (the prefix max
+// just before it).  Flags are never stored: the starts scan, the Q1 cut and
+// the record pass each evaluate them where they need them.
+struct FlagArgs {
+  const void* keys;
+  const unsigned long long* pmax;
+  uint64_t j_off;
+  unsigned long long pmax_in;
+  PkView pv;
+};
 template <int FM>
-__global__ __launch_bounds__(BLOCK) void k_faith_flags(const void* __restrict__ keys,
-                                                       const unsigned long long* __restrict__ pmax, uint64_t n,
-                                                       uint64_t j_off, unsigned long long pmax_in,
-                                                       unsigned int* __restrict__ flags, PkView pv) {
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
-    const unsigned long long before = i == 0 ? pmax_in : gmax(pmax, i - 1, pmax_in);
-    flags[i] = (j_off + i == 0 || key_at<FM>(keys, i, pv) > before) ? 1u : 0u;
-  }
+__device__ __forceinline__ bool flag_at(const FlagArgs& a, uint64_t i) {
+  const unsigned long long before = i == 0 ? a.pmax_in : gmax(a.pmax, i - 1, a.pmax_in);
+  return a.j_off + i == 0 || key_at<FM>(a.keys, i, a.pv) > before;
 }
+template <int FM>
+struct FlagOp {  // rocprim transform: element index -> start flag
+  FlagArgs a;
+  __device__ unsigned int operator()(uint64_t i) const { return flag_at<FM>(a, i) ? 1u : 0u; }
+};
 
 // Q1: the first START j > 0 (global index) whose met-sample count
 // j - starts_before_j reaches the number of samples left, n_total - j.
-__global__ __launch_bounds__(BLOCK) void k_faith_cut(const unsigned int* __restrict__ flags,
-                                                     const unsigned int* __restrict__ nstart, uint64_t n,
-                                                     uint64_t j_off, uint64_t s_off, uint64_t n_total,
-                                                     unsigned long long* scal) {
+template <int FM>
+__global__ __launch_bounds__(BLOCK) void k_faith_cut(FlagArgs fa, const unsigned int* __restrict__ nstart, uint64_t n,
+                                                     uint64_t s_off, uint64_t n_total, unsigned long long* scal) {
+  const uint64_t j_off = fa.j_off;
   unsigned long long best = KEY_EMPTY;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
     const uint64_t j = j_off + i;
-    if (j > 0 && flags[i]) {
+    if (j > 0 && flag_at<FM>(fa, i)) {
       const uint64_t met = j - (s_off + (uint64_t)nstart[i] - 1);  // samples met before this START
       if (met >= n_total - j && j < best) best = j;
     }
@@ -228,58 +241,80 @@ __global__ __launch_bounds__(BLOCK) void k_faith_cut(const unsigned int* __restr
 // samples, and the traversed contributions of the replays that start or end
 // here (a replay ends at j when j + 1 == cut or j + 1 starts one; for the
 // shard's last sample that is `next_start`, decided by the caller).
+//
+// Packed words (FM_PK*): a recorded sample's key is its reference's
+// (ref, case) key, so the cases are counted by ballots and added to the
+// direct bin row blockIdx % 64 (folded by k_export like clean-mode counts);
+// (key, sink) pairs take the exact-key path.
 template <bool FAST, int FM = FM_PAIRS>
-__global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, const void* __restrict__ keys,
-                                                      const unsigned long long* __restrict__ sinks,
-                                                      const unsigned long long* __restrict__ pmax,
-                                                      const unsigned int* __restrict__ flags, uint64_t n,
-                                                      uint64_t j_off, unsigned long long pmax_in, int next_start,
-                                                      unsigned long long* scal, GTable g, PkView pv) {
-  __shared__ unsigned long long tk[TCAP];
-  __shared__ unsigned int tc[TCAP];
-  __shared__ unsigned long long red[2];
+__global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, FlagArgs fa,
+                                                      const unsigned long long* __restrict__ sinks, uint64_t n,
+                                                      int next_start, unsigned long long* scal, GTable g) {
+  constexpr bool PKD = FM != FM_PAIRS;
+  __shared__ unsigned long long tk[PKD ? 1 : TCAP];
+  __shared__ unsigned int tc[PKD ? 1 : TCAP];
+  __shared__ unsigned long long red[5];  // cold, traversed, case 0/1/2 counts
   const BlockTable bt{tk, tc};
-  bt_init(bt);
+  if (!PKD) bt_init(bt);
   WaveCache wc;
   wc_init(wc);
-  if (threadIdx.x == 0) red[0] = red[1] = 0;
+  if (threadIdx.x < 5) red[threadIdx.x] = 0;
   __syncthreads();
+  const uint64_t j_off = fa.j_off;
   const uint64_t cut = scal[0];
   const uint64_t lim = cut > j_off ? (cut - j_off < n ? cut - j_off : n) : 0;  // local samples recorded
   const uint64_t endkey = m.A * m.T;
   unsigned long long cold = 0, trav = 0;
+  uint32_t nc0 = 0, nc1 = 0, nc2 = 0;  // wave totals of recorded samples per case (packed words)
   const uint64_t step = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t base = (uint64_t)blockIdx.x * BLOCK; base < lim; base += step) {
     const uint64_t i = base + threadIdx.x;
     const bool v = i < lim;
     uint64_t key = KEY_NONE;
     bool rec = false;
+    uint32_t c = 3;
     if (v) {
-      const unsigned long long k = key_at<FM>(keys, i, pv), s = sink_at<FM>(keys, sinks, i, pv);
+      const unsigned long long k = key_at<FM>(fa.keys, i, fa.pv), s = sink_at<FM>(fa.keys, sinks, i, fa.pv);
       if (s == KEY_EMPTY) {
         cold += (k % m.T == 0) ? 1u : 0u;
+      } else if (PKD) {
+        c = (uint32_t)(static_cast<const fkey_t<FM>*>(fa.keys)[i] & 3u);
+        rec = true;
       } else {
         const int64_t ri = (int64_t)((s - k) / m.T);
         key = make_key(ref, share_kind(m, ref, ri), ri);
         rec = true;
       }
-      if (flags[i]) trav -= k;
-      const bool ends = j_off + i + 1 == cut || (i + 1 < n ? flags[i + 1] != 0 : next_start != 0);
+      if (flag_at<FM>(fa, i)) trav -= k;
+      const bool ends = j_off + i + 1 == cut || (i + 1 < n ? flag_at<FM>(fa, i + 1) : next_start != 0);
       if (ends) {
-        const unsigned long long gm = gmax(pmax, i, pmax_in);
+        const unsigned long long gm = gmax(fa.pmax, i, fa.pmax_in);
         trav += (gm == KEY_EMPTY) ? endkey : gm;
       }
     }
-    wave_count(wc, bt, g, key, rec);
+    if (PKD) {
+      nc0 += (uint32_t)__popcll(__ballot(rec && c == 0));
+      nc1 += (uint32_t)__popcll(__ballot(rec && c == 1));
+      nc2 += (uint32_t)__popcll(__ballot(rec && c == 2));
+    } else {
+      wave_count(wc, bt, g, key, rec);
+    }
   }
   atomicAdd(&red[0], cold);
   atomicAdd(&red[1], trav);
-  bt_finish(wc, bt, g);
+  if (PKD && __lane_id() == 0) {
+    if (nc0) atomicAdd(&red[2], (unsigned long long)nc0);
+    if (nc1) atomicAdd(&red[3], (unsigned long long)nc1);
+    if (nc2) atomicAdd(&red[4], (unsigned long long)nc2);
+  }
+  if (!PKD) bt_finish(wc, bt, g);
   __syncthreads();
   if (threadIdx.x == 0) {
     atomicAdd(&scal[1], red[0]);
     atomicAdd(&scal[2], red[1]);
   }
+  if (PKD && threadIdx.x < 3 && red[2 + threadIdx.x])
+    atomicAdd(&g.bins[(blockIdx.x & (NBROW - 1)) * BSTRIDE + ref * 3 + threadIdx.x], red[2 + threadIdx.x]);
 }
 
 // Q3 (only on the shard holding the global last sample, with nothing
@@ -339,7 +374,7 @@ static int grid_of(uint64_t n) {
   return b < 1 ? 1 : (b > (uint64_t)MAX_BLOCKS ? MAX_BLOCKS : (int)b);
 }
 
-// buffers for n samples (keys, sinks, sorted copies, prefix max, flags, scan)
+// buffers for n samples (sort words or keys + sinks, sorted copies, prefix max, scan of the start flags)
 static int faith_reserve(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
   FaithfulBufs& b = ctx->fb;
   if (!b.scal) {
@@ -353,7 +388,7 @@ static int faith_reserve(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
     PLUSS_HIP_CHECK(hipStreamSynchronize(s));
     int rc = 0;
     if ((rc = grow(&b.keys, n)) || (rc = grow(&b.sinks, n)) || (rc = grow(&b.keys_s, n)) ||
-        (rc = grow(&b.sinks_s, n)) || (rc = grow(&b.pmax, n)) || (rc = grow(&b.flags, n)) || (rc = grow(&b.nstart, n)))
+        (rc = grow(&b.sinks_s, n)) || (rc = grow(&b.pmax, n)) || (rc = grow(&b.nstart, n)))
       return rc;
     b.cap = n;
   }
@@ -379,7 +414,11 @@ static int faith_tmp(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
     PLUSS_HIP_CHECK(
         rocprim::inclusive_scan(nullptr, t2, b.sinks_s, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
   }
-  PLUSS_HIP_CHECK(rocprim::inclusive_scan(nullptr, t3, b.flags, b.nstart, n, rocprim::plus<unsigned int>(), s));
+  {
+    const FlagArgs fa{b.keys_s, b.pmax, 0, 0, make_pkview(ctx->m, 0)};
+    auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint64_t>(0), FlagOp<FM_PAIRS>{fa});
+    PLUSS_HIP_CHECK(rocprim::inclusive_scan(nullptr, t3, it, b.nstart, n, rocprim::plus<unsigned int>(), s));
+  }
   size_t need = t1 > t2 ? t1 : t2;
   need = need > t3 ? need : t3;
   if (need > b.tmp_bytes) {
@@ -445,20 +484,39 @@ static int faith_sort(pluss_ctx* ctx, int32_t ref, uint64_t n, hipStream_t s) {
 static int faith_starts(pluss_ctx* ctx, int32_t ref, uint64_t n, uint64_t j_off, unsigned long long pmax_in,
                         hipStream_t s) {
   FaithfulBufs& b = ctx->fb;
-  const PkView pv = make_pkview(ctx->m, (uint32_t)ref);
+  const FlagArgs fa{b.keys_s, b.pmax, j_off, pmax_in, make_pkview(ctx->m, (uint32_t)ref)};
+  size_t sz = b.tmp_bytes;
+  rocprim::counting_iterator<uint64_t> idx(0);
+  const int fm = faith_fm(ctx->m);
+  // nstart = inclusive scan of the start flags, evaluated inside the scan
+  if (fm == FM_PK32)
+    PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, rocprim::make_transform_iterator(idx, FlagOp<FM_PK32>{fa}),
+                                            b.nstart, n, rocprim::plus<unsigned int>(), s));
+  else if (fm == FM_PK64)
+    PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, rocprim::make_transform_iterator(idx, FlagOp<FM_PK64>{fa}),
+                                            b.nstart, n, rocprim::plus<unsigned int>(), s));
+  else
+    PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, rocprim::make_transform_iterator(idx, FlagOp<FM_PAIRS>{fa}),
+                                            b.nstart, n, rocprim::plus<unsigned int>(), s));
+  return PLUSS_OK;
+}
+
+// Q1 cut of this shard's elements into scal[0] (already holding the default)
+static int faith_cut(pluss_ctx* ctx, int32_t ref, uint64_t n, uint64_t j_off, unsigned long long pmax_in,
+                     uint64_t s_off, uint64_t n_total, hipStream_t s) {
+  FaithfulBufs& b = ctx->fb;
+  const FlagArgs fa{b.keys_s, b.pmax, j_off, pmax_in, make_pkview(ctx->m, (uint32_t)ref)};
   const int fm = faith_fm(ctx->m);
   if (fm == FM_PK32)
-    hipLaunchKernelGGL(k_faith_flags<FM_PK32>, dim3(grid_of(n)), dim3(BLOCK), 0, s, (const void*)b.keys_s, b.pmax, n,
-                       j_off, pmax_in, b.flags, pv);
+    hipLaunchKernelGGL(k_faith_cut<FM_PK32>, dim3(grid_of(n)), dim3(BLOCK), 0, s, fa, b.nstart, n, s_off, n_total,
+                       b.scal);
   else if (fm == FM_PK64)
-    hipLaunchKernelGGL(k_faith_flags<FM_PK64>, dim3(grid_of(n)), dim3(BLOCK), 0, s, (const void*)b.keys_s, b.pmax, n,
-                       j_off, pmax_in, b.flags, pv);
+    hipLaunchKernelGGL(k_faith_cut<FM_PK64>, dim3(grid_of(n)), dim3(BLOCK), 0, s, fa, b.nstart, n, s_off, n_total,
+                       b.scal);
   else
-    hipLaunchKernelGGL(k_faith_flags<FM_PAIRS>, dim3(grid_of(n)), dim3(BLOCK), 0, s, (const void*)b.keys_s, b.pmax, n,
-                       j_off, pmax_in, b.flags, pv);
+    hipLaunchKernelGGL(k_faith_cut<FM_PAIRS>, dim3(grid_of(n)), dim3(BLOCK), 0, s, fa, b.nstart, n, s_off, n_total,
+                       b.scal);
   PLUSS_HIP_CHECK(hipGetLastError());
-  size_t sz = b.tmp_bytes;
-  PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, b.flags, b.nstart, n, rocprim::plus<unsigned int>(), s));
   return PLUSS_OK;
 }
 
@@ -467,20 +525,17 @@ static int faith_record(pluss_ctx* ctx, int32_t ref, uint64_t n, uint64_t j_off,
   const Model& m = ctx->m;
   FaithfulBufs& b = ctx->fb;
   if (n) {
-    const PkView pv = make_pkview(m, (uint32_t)ref);
+    const FlagArgs fa{b.keys_s, b.pmax, j_off, pmax_in, make_pkview(m, (uint32_t)ref)};
     const int fm = faith_fm(m);
     if (fm == FM_PK32)
-      hipLaunchKernelGGL((k_faith_hist<true, FM_PK32>), dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref,
-                         (const void*)b.keys_s, b.sinks_s, b.pmax, b.flags, n, j_off, pmax_in, next_start, b.scal,
-                         ctx->g, pv);
+      hipLaunchKernelGGL((k_faith_hist<true, FM_PK32>), dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, fa,
+                         b.sinks_s, n, next_start, b.scal, ctx->g);
     else if (fm == FM_PK64)
-      hipLaunchKernelGGL((k_faith_hist<true, FM_PK64>), dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref,
-                         (const void*)b.keys_s, b.sinks_s, b.pmax, b.flags, n, j_off, pmax_in, next_start, b.scal,
-                         ctx->g, pv);
+      hipLaunchKernelGGL((k_faith_hist<true, FM_PK64>), dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, fa,
+                         b.sinks_s, n, next_start, b.scal, ctx->g);
     else
-      hipLaunchKernelGGL(k_faith_hist<false>, dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref,
-                         (const void*)b.keys_s, b.sinks_s, b.pmax, b.flags, n, j_off, pmax_in, next_start, b.scal,
-                         ctx->g, pv);
+      hipLaunchKernelGGL(k_faith_hist<false>, dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, fa, b.sinks_s, n,
+                         next_start, b.scal, ctx->g);
   }
   hipLaunchKernelGGL(k_faith_finish, dim3(1), dim3(1), 0, s, m, (uint32_t)ref, n, n_total, is_last, pmax_in, b.pmax,
                      b.scal, ctx->g);
@@ -498,9 +553,7 @@ int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint
   if (int rc = faith_sort(ctx, ref, n, s)) return rc;
   if (int rc = faith_starts(ctx, ref, n, 0, 0, s)) return rc;
   hipLaunchKernelGGL(k_faith_init, dim3(1), dim3(1), 0, s, b.scal, n);
-  hipLaunchKernelGGL(k_faith_cut, dim3(grid_of(n)), dim3(BLOCK), 0, s, b.flags, b.nstart, n, (uint64_t)0, (uint64_t)0,
-                     n, b.scal);
-  PLUSS_HIP_CHECK(hipGetLastError());
+  if (int rc = faith_cut(ctx, ref, n, 0, 0, 0, n, s)) return rc;
   return faith_record(ctx, ref, n, 0, 0, 0, n, 1, s);
 }
 
@@ -576,9 +629,7 @@ int faith_shard_cut(pluss_ctx* ctx, uint64_t s_off, uint64_t n_total, pluss_fait
   if (f.n) {
     FaithfulBufs& b = ctx->fb;
     hipLaunchKernelGGL(k_faith_init, dim3(1), dim3(1), 0, s, b.scal, n_total);
-    hipLaunchKernelGGL(k_faith_cut, dim3(grid_of(f.n)), dim3(BLOCK), 0, s, b.flags, b.nstart, f.n, f.j_off, s_off,
-                       n_total, b.scal);
-    PLUSS_HIP_CHECK(hipGetLastError());
+    if (int rc = faith_cut(ctx, f.ref, f.n, f.j_off, f.pmax_in, s_off, n_total, s)) return rc;
     PLUSS_HIP_CHECK(hipMemcpyAsync(&out->cut, b.scal, 8, hipMemcpyDeviceToHost, s));
     PLUSS_HIP_CHECK(hipStreamSynchronize(s));
   }

@@ -59,7 +59,7 @@ constexpr size_t TABLE_BYTES = TABLE_WORDS * 8;
 struct FaithfulBufs {
   uint64_t cap = 0;
   unsigned long long *keys = nullptr, *sinks = nullptr, *keys_s = nullptr, *sinks_s = nullptr, *pmax = nullptr;
-  unsigned int *flags = nullptr, *nstart = nullptr;
+  unsigned int* nstart = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   unsigned long long* scal = nullptr;  // [0] cut, [1] cold, [2] traversed
