@@ -267,30 +267,42 @@ __global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, Fla
   unsigned long long cold = 0, trav = 0;
   uint32_t nc0 = 0, nc1 = 0, nc2 = 0;  // wave totals of recorded samples per case (packed words)
   const uint64_t step = (uint64_t)gridDim.x * BLOCK;
+  const uint32_t lane = __lane_id();
   for (uint64_t base = (uint64_t)blockIdx.x * BLOCK; base < lim; base += step) {
     const uint64_t i = base + threadIdx.x;
     const bool v = i < lim;
     uint64_t key = KEY_NONE;
     bool rec = false;
     uint32_t c = 3;
+    // each lane decodes its own key once; the next element's key (for "does
+    // a replay end here?") comes from the neighbouring lane
+    const unsigned long long k = i < n ? key_at<FM>(fa.keys, i, fa.pv) : KEY_EMPTY;
+    unsigned long long k_next = __shfl_down(k, 1, 64);
+    if (lane == 63 && i + 1 < n) k_next = key_at<FM>(fa.keys, i + 1, fa.pv);
     if (v) {
-      const unsigned long long k = key_at<FM>(fa.keys, i, fa.pv), s = sink_at<FM>(fa.keys, sinks, i, fa.pv);
+      unsigned long long s;
+      if (PKD) {
+        const fkey_t<FM> word = static_cast<const fkey_t<FM>*>(fa.keys)[i];
+        c = (uint32_t)(word & 3u);
+        const int64_t ri = c == 0 ? fa.pv.ri[0] : (c == 1 ? fa.pv.ri[1] : fa.pv.ri[2]);
+        s = (c == 3 || ri < 0 || k == KEY_EMPTY) ? KEY_EMPTY : k + (unsigned long long)ri * m.T;
+      } else {
+        s = sinks[i];
+      }
       if (s == KEY_EMPTY) {
         cold += (k % m.T == 0) ? 1u : 0u;
       } else if (PKD) {
-        c = (uint32_t)(static_cast<const fkey_t<FM>*>(fa.keys)[i] & 3u);
         rec = true;
       } else {
         const int64_t ri = (int64_t)((s - k) / m.T);
         key = make_key(ref, share_kind(m, ref, ri), ri);
         rec = true;
       }
-      if (flag_at<FM>(fa, i)) trav -= k;
-      const bool ends = j_off + i + 1 == cut || (i + 1 < n ? flag_at<FM>(fa, i + 1) : next_start != 0);
-      if (ends) {
-        const unsigned long long gm = gmax(fa.pmax, i, fa.pmax_in);
-        trav += (gm == KEY_EMPTY) ? endkey : gm;
-      }
+      const unsigned long long before = i == 0 ? fa.pmax_in : gmax(fa.pmax, i - 1, fa.pmax_in);
+      if (j_off + i == 0 || k > before) trav -= k;  // this element starts a replay
+      const unsigned long long gm = gmax(fa.pmax, i, fa.pmax_in);
+      const bool ends = j_off + i + 1 == cut || (i + 1 < n ? k_next > gm : next_start != 0);
+      if (ends) trav += (gm == KEY_EMPTY) ? endkey : gm;
     }
     if (PKD) {
       nc0 += (uint32_t)__popcll(__ballot(rec && c == 0));
