@@ -667,6 +667,107 @@ __device__ __forceinline__ void count_step(const Model& m, const uint32_t (&lo)[
   acc += lane == BIN_BAD ? nbad : 0u;
 }
 
+// Per-lane counters of the vector fast path (count_step_lanes): for each
+// reference the lanes count only the outcomes that need a per-sample test; the
+// sample totals per reference are wave-uniform (every lane holds 2*UNR
+// samples of the step) and live in scalar registers.
+struct LaneCounts {
+  uint32_t a_last, a_c1;    // A0: c2 last in its line; and c1+1 < N as well
+  uint32_t c_lt, c_last;    // C3: c2+1 < N; c2 = N-1 with c1 last in its line
+  uint32_t b_last, b_next;  // B0: c1 last in its line; and a later owned row as well
+  uint32_t tot[6];          // samples per reference (wave-uniform)
+};
+__device__ __forceinline__ void lc_init(LaneCounts& c) {
+  c.a_last = c.a_c1 = c.c_lt = c.c_last = c.b_last = c.b_next = 0;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) c.tot[r] = 0;
+}
+
+// 1 if x < y (both < 2^31), as an integer: no compare, no lane mask
+__device__ __forceinline__ uint32_t lt01(uint32_t x, uint32_t y) { return (x - y) >> 31; }
+
+// A full step whose samples all have the wave's reference r0 and are in
+// range, for N, W and CS powers of two (every BASELINE shape).  Each test is
+// integer arithmetic on the lane's own samples (VALU only); the scalar unit
+// does one check and one branch per step.  Returns false (nothing counted)
+// when the step needs count_step instead.
+template <int UNR>
+__device__ __forceinline__ bool count_step_lanes(const Model& m, const uint32_t (&lo)[2 * UNR],
+                                                 const uint32_t (&hi)[2 * UNR], LaneCounts& c) {
+  constexpr int K = 2 * UNR;
+  const uint32_t r0 = __builtin_amdgcn_readfirstlane(hi[0] >> 28);
+  if (r0 > 5) return false;
+  uint32_t odd = 0;  // another reference, or an index >= N, somewhere in the lane's samples
+#pragma unroll
+  for (int k = 0; k < K; ++k) odd |= ((hi[k] ^ (r0 << 28)) & (0xF0000000u | m.badhi)) | (lo[k] & m.badlo);
+  if (__ballot(odd != 0u) != 0) return false;
+  const uint32_t wsh = m.wsh, wm = m.wmask;
+  switch (r0) {
+    case A0:
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint32_t last = ((lo[k] & wm) + 1u) >> wsh;                                   // c2 % W == W-1
+        const uint32_t c1n = lt01(__builtin_amdgcn_alignbit(hi[k], lo[k], 20) & 0xFFFFFu, m.N - 1);  // c1+1 < N
+        c.a_last += last;
+        c.a_c1 += last & c1n;
+      }
+      c.tot[2] += K;
+      break;
+    case B0:
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint32_t last = (((lo[k] >> 20) & wm) + 1u) >> wsh;  // c1 % W == W-1
+        const uint32_t c0 = (hi[k] >> 8) & 0xFFFFFu;
+        const uint32_t pl = ((c0 & m.csmask) + 1u) >> m.csshift;   // c0 % CS == CS-1
+        c.b_last += last;
+        c.b_next += last & lt01(c0 + 1u + pl * m.tcs, m.N);        // the thread owns a later row
+      }
+      c.tot[3] += K;
+      break;
+    case C3:
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint32_t lt = lt01(lo[k] & 0xFFFFFu, m.N - 1);       // c2+1 < N
+        const uint32_t last = (((lo[k] >> 20) & wm) + 1u) >> wsh;  // c1 % W == W-1
+        c.c_lt += lt;
+        c.c_last += (lt ^ 1u) & last;
+      }
+      c.tot[5] += K;
+      break;
+    case C0:  // C0, C1, C2: always case 0
+      c.tot[0] += K;
+      break;
+    case C1:
+      c.tot[1] += K;
+      break;
+    default:
+      c.tot[4] += K;
+      break;
+  }
+  return true;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Fold the lane counters into the lane-indexed counts (lane b: bin b).
+__device__ __forceinline__ void lc_flush(LaneCounts& c, uint32_t& acc) {
+  const uint32_t al = wave_sum(c.a_last), ac = wave_sum(c.a_c1), cl = wave_sum(c.c_lt), cc = wave_sum(c.c_last);
+  const uint32_t bl = wave_sum(c.b_last), bn = wave_sum(c.b_next);
+  uint32_t t[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) t[r] = c.tot[r] * 64u;  // per-lane sample counts are the same in every lane
+  const uint32_t bins[18] = {t[0], 0, 0, t[1], 0, 0, t[2] - al, ac, al - ac, t[3] - bl, bn, bl - bn,
+                             t[4], 0, 0, cl, t[5] - cl - cc, cc};
+  const uint32_t lane = __lane_id();
+#pragma unroll
+  for (uint32_t b = 0; b < 18; ++b) acc += lane == b ? bins[b] : 0u;
+  lc_init(c);
+}
+
 // Add the wave's lane-indexed counts to the workgroup's LDS totals.
 __device__ __forceinline__ void flush_counts(uint32_t& acc, unsigned long long* tot) {
   const uint32_t lane = __lane_id();
@@ -676,7 +777,9 @@ __device__ __forceinline__ void flush_counts(uint32_t& acc, unsigned long long* 
 
 // ABL (diagnostics, tools/ablate.py): 0 product; 1 loads only (PLUSS_ABLATE=3); 2 count without the tail (=4)
 // XAUX >= 0 (diagnostics, PLUSS_AUX): that cache-policy immediate for the sample loads instead of NT's
-template <bool P2, bool NP2, bool NT, int TAIL, int UNR = UNROLL, int ABL = 0, int BS = BLOCK, int XAUX = -1>
+// LANES: full uniform steps counted by count_step_lanes (P2 && NP2 shapes); false = ballots only (PLUSS_LANES=0)
+template <bool P2, bool NP2, bool NT, int TAIL, int UNR = UNROLL, int ABL = 0, int BS = BLOCK, int XAUX = -1,
+          bool LANES = true>
 __global__ __launch_bounds__(BS) void k_count(Model m, const uint64_t* __restrict__ smp, uint64_t n,
                                               const uint64_t* __restrict__ head, int has_head, GTable g,
                                               ExportArgs ex) {
@@ -685,6 +788,8 @@ __global__ __launch_bounds__(BS) void k_count(Model m, const uint64_t* __restric
   __shared__ unsigned long long tot[DBINS];
   if (threadIdx.x < DBINS) tot[threadIdx.x] = 0;  // the barrier before the first flush orders this
   uint32_t acc = 0;  // lane b: count of bin b
+  LaneCounts lc;     // the vector fast path's counters (count_step_lanes)
+  lc_init(lc);
   const uint64_t npairs = n >> 1;
   const uint32_t step = gridDim.x * (uint32_t)(BS * UNR);
   constexpr int AUX = XAUX >= 0 ? XAUX : (NT ? 2 : 0);  // nt: the list is streamed once per pass
@@ -720,13 +825,14 @@ __global__ __launch_bounds__(BS) void k_count(Model m, const uint64_t* __restric
       if (ABL == 1) {  // diagnostics: the same loads, nothing counted
 #pragma unroll
         for (int k = 0; k < 2 * UNR; ++k) acc ^= lo[k] ^ hi[k];
-      } else {
+      } else if (!(P2 && NP2 && LANES && base + (uint32_t)(UNR * BS) <= wn && count_step_lanes<UNR>(m, lo, hi, lc))) {
         count_step<P2, NP2, UNR>(m, lo, hi, okm, acc);
       }
 #pragma unroll
       for (int u = 0; u < UNR; ++u) x[u] = y[u];
     }
     if (ABL != 1) {  // per window: keeps the 32-bit lane counters from overflowing
+      if (P2 && NP2 && LANES) lc_flush(lc, acc);
       __syncthreads();
       flush_counts(acc, tot);
     }
@@ -1093,6 +1199,13 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
       hipLaunchKernelGGL((k_count<P2, NP2, NT, TAIL_NONE, UNR>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n,   \
                          head, has_head, g, ex);                                                                 \
   } while (0)
+    const char* lanesv = getenv("PLUSS_LANES");
+    if (m.p2 && m.np2 && tail == TAIL_DENSE && lanesv && lanesv[0] == '0') {  // diagnostics: ballot counting only
+      hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_DENSE, UNROLL, 0, BLOCK, -1, false>), dim3(nb), dim3(BLOCK),
+                         0, s, m, d_samples, n, head, has_head, g, ex);
+      PLUSS_HIP_CHECK(hipGetLastError());
+      return PLUSS_OK;
+    }
     const char* auxv = getenv("PLUSS_AUX");
     if (m.p2 && m.np2 && tail == TAIL_DENSE && auxv) {  // diagnostics: cache-policy bits of the sample loads
 #define PLUSS_AUX_CASE(V)                                                                                          \

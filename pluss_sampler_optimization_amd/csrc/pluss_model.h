@@ -63,7 +63,7 @@ struct Model {
   uint32_t S;            // 4N+2 accesses per c1 iteration
   uint32_t fast;         // N % W == 0: the closed rules (ri_fast / case_fast) apply
   uint32_t p2;           // W and CS are powers of two (mask/shift instead of FastDiv)
-  uint32_t wmask, csmask, csshift;
+  uint32_t wmask, csmask, csshift, wsh;  // wsh = log2(W) when W is a power of two
   uint64_t R;            // N*S accesses per row
   uint64_t thr;          // share threshold (B0 only)
   uint64_t A;            // accesses per simulated thread when N % (CS*T) == 0
@@ -237,6 +237,8 @@ inline Model make_model(uint64_t N, uint64_t T, uint64_t CS, uint64_t DS, uint64
   m.csmask = m.CS - 1;
   m.csshift = 0;
   while ((1u << m.csshift) < m.CS) ++m.csshift;
+  m.wsh = 0;
+  while ((1u << m.wsh) < m.W) ++m.wsh;
   m.thr = thr_v1 ? (N + 1) * N + 1 : (4 * N + 2) * N;
   m.A = (N % (CS * T) == 0) ? (N / T) * m.R : 0;
   m.dCS = make_fastdiv(m.CS);

@@ -329,15 +329,17 @@ def test_dense_pass(orc, N, T, CS):
         ctx.sampled_hist(buf.data_ptr() + 8, 1000, stream)  # accumulating histogram: untouched by dense passes
         first = None
         try:
-            knobs = ("PLUSS_GRID", "PLUSS_LEGACY", "PLUSS_DROWS", "PLUSS_BS")
+            knobs = ("PLUSS_GRID", "PLUSS_LEGACY", "PLUSS_DROWS", "PLUSS_BS", "PLUSS_LANES")
             for grid in ("", "1", "3", "64", "65", "200", "1024", "legacy", "drows1", "drows8", "drows64", "bs1024",
-                         "bs1024_3"):
+                         "bs1024_3", "ballots"):
                 for k in knobs:
                     os.environ.pop(k, None)
                 if grid == "legacy":  # the lane-counter kernel (k_sampled_hist) agrees
                     os.environ["PLUSS_LEGACY"] = "1"
                 elif grid.startswith("drows"):  # first-level rows of the dense tail
                     os.environ["PLUSS_DROWS"] = grid[5:]
+                elif grid == "ballots":  # k_count without its vector fast path
+                    os.environ["PLUSS_LANES"] = "0"
                 elif grid.startswith("bs1024"):  # 1024-thread workgroups (diagnostic variant)
                     os.environ["PLUSS_BS"] = "1024"
                     if grid == "bs1024_3":
