@@ -675,12 +675,13 @@ struct LaneCounts {
   uint32_t a_last, a_c1;    // A0: c2 last in its line; and c1+1 < N as well
   uint32_t c_lt, c_last;    // C3: c2+1 < N; c2 = N-1 with c1 last in its line
   uint32_t b_last, b_next;  // B0: c1 last in its line; and a later owned row as well
-  uint32_t tot[6];          // samples per reference (wave-uniform)
+  // samples per reference per lane (wave-uniform); named, not an array, so no
+  // switch is turned into an indexed (scratch) update
+  uint32_t t_c0, t_c1, t_a0, t_b0, t_c2, t_c3;
 };
 __device__ __forceinline__ void lc_init(LaneCounts& c) {
   c.a_last = c.a_c1 = c.c_lt = c.c_last = c.b_last = c.b_next = 0;
-#pragma unroll
-  for (int r = 0; r < 6; ++r) c.tot[r] = 0;
+  c.t_c0 = c.t_c1 = c.t_a0 = c.t_b0 = c.t_c2 = c.t_c3 = 0;
 }
 
 // 1 if x < y (both < 2^31), as an integer: no compare, no lane mask
@@ -711,7 +712,6 @@ __device__ __forceinline__ bool count_step_lanes(const Model& m, const uint32_t 
         c.a_last += last;
         c.a_c1 += last & c1n;
       }
-      c.tot[2] += K;
       break;
     case B0:
 #pragma unroll
@@ -722,7 +722,6 @@ __device__ __forceinline__ bool count_step_lanes(const Model& m, const uint32_t 
         c.b_last += last;
         c.b_next += last & lt01(c0 + 1u + pl * m.tcs, m.N);        // the thread owns a later row
       }
-      c.tot[3] += K;
       break;
     case C3:
 #pragma unroll
@@ -732,18 +731,17 @@ __device__ __forceinline__ bool count_step_lanes(const Model& m, const uint32_t 
         c.c_lt += lt;
         c.c_last += (lt ^ 1u) & last;
       }
-      c.tot[5] += K;
       break;
-    case C0:  // C0, C1, C2: always case 0
-      c.tot[0] += K;
-      break;
-    case C1:
-      c.tot[1] += K;
-      break;
-    default:
-      c.tot[4] += K;
+    default:  // C0, C1, C2: always case 0
       break;
   }
+  // per-reference sample totals: branch-free scalar selects (wave-uniform)
+  c.t_c0 += r0 == C0 ? (uint32_t)K : 0u;
+  c.t_c1 += r0 == C1 ? (uint32_t)K : 0u;
+  c.t_a0 += r0 == A0 ? (uint32_t)K : 0u;
+  c.t_b0 += r0 == B0 ? (uint32_t)K : 0u;
+  c.t_c2 += r0 == C2 ? (uint32_t)K : 0u;
+  c.t_c3 += r0 == C3 ? (uint32_t)K : 0u;
   return true;
 }
 
@@ -757,11 +755,11 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 __device__ __forceinline__ void lc_flush(LaneCounts& c, uint32_t& acc) {
   const uint32_t al = wave_sum(c.a_last), ac = wave_sum(c.a_c1), cl = wave_sum(c.c_lt), cc = wave_sum(c.c_last);
   const uint32_t bl = wave_sum(c.b_last), bn = wave_sum(c.b_next);
-  uint32_t t[6];
-#pragma unroll
-  for (int r = 0; r < 6; ++r) t[r] = c.tot[r] * 64u;  // per-lane sample counts are the same in every lane
-  const uint32_t bins[18] = {t[0], 0, 0, t[1], 0, 0, t[2] - al, ac, al - ac, t[3] - bl, bn, bl - bn,
-                             t[4], 0, 0, cl, t[5] - cl - cc, cc};
+  // per-lane sample counts are the same in every lane
+  const uint32_t t0 = c.t_c0 * 64u, t1 = c.t_c1 * 64u, ta = c.t_a0 * 64u, tb = c.t_b0 * 64u, t4 = c.t_c2 * 64u,
+                 t5 = c.t_c3 * 64u;
+  const uint32_t bins[18] = {t0, 0, 0, t1, 0, 0, ta - al, ac, al - ac, tb - bl, bn, bl - bn,
+                             t4, 0, 0, cl, t5 - cl - cc, cc};
   const uint32_t lane = __lane_id();
 #pragma unroll
   for (uint32_t b = 0; b < 18; ++b) acc += lane == b ? bins[b] : 0u;
