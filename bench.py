@@ -187,6 +187,10 @@ def main():
     ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", type=int, default=20,
+                    help="steps per captured HIP graph for the timed region (0: eager launches)")
+    ap.add_argument("--allreduce", action="store_true",
+                    help="rehearsal: run the merge all-reduce even at world size 1 (under torch.distributed.run)")
     ap.add_argument("--no-extras", action="store_true", help="skip the full-trace / faithful side measurements")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend (nccl = RCCL over xGMI; gloo only to rehearse N>1 on one GPU)")
@@ -200,7 +204,7 @@ def main():
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
     local = local % max(1, torch.cuda.device_count())  # rehearsal: several ranks may share one GPU
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 or args.allreduce:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -232,34 +236,55 @@ def main():
         off += cnt
     torch.cuda.synchronize()
 
-    def step():
-        # one launch: count every sample; the last adder of each bin writes this
-        # pass's total to its output vector and zeroes the kernel's state for
-        # the next pass
-        i = nsteps[0] % 2
-        nsteps[0] += 1
-        if pending[i] is not None:  # the all-reduce that last read dense[i] (stream-ordered wait)
-            pending[i].wait()
-            pending[i] = None
-        ctx.sampled_hist_dense(samples.data_ptr(), n_local, dense[i].data_ptr(), sp)
-        if world > 1:  # element-wise sum of the per-GPU vectors (counts < 2^63)
-            if args.backend == "nccl":
-                # asynchronous: RCCL's stream waits for this launch, and the
-                # next step's launch overlaps the collective
-                pending[i] = dist.all_reduce(dense[i], async_op=True)
-            else:
-                dense[i].copy_(allreduce_cpu(dense[i]))
-
-    def drain():
-        for j in range(2):
+    def enqueue(k):
+        """Enqueue k steps.  Step s (global count) writes dense[s % 2]: one
+        launch counts every sample; the last adder of each bin writes this
+        pass's total to the vector and zeroes the kernel's state for the next
+        pass.  N>1: the vector is then summed over the ranks."""
+        for _ in range(k):
+            i = nsteps[0] % 2
+            nsteps[0] += 1
+            if pending[i] is not None:  # the all-reduce that last read dense[i] (stream-ordered wait)
+                pending[i].wait()
+                pending[i] = None
+            ctx.sampled_hist_dense(samples.data_ptr(), n_local, dense[i].data_ptr(), sp)
+            if world > 1 or args.allreduce:  # element-wise sum of the per-GPU vectors (counts < 2^63)
+                if args.backend == "nccl":
+                    # asynchronous: RCCL's stream waits for this launch, and the
+                    # next step's launch overlaps the collective
+                    pending[i] = dist.all_reduce(dense[i], async_op=True)
+                else:
+                    dense[i].copy_(allreduce_cpu(dense[i]))
+        for j in range(2):  # join: every all-reduce of these steps is complete (stream-ordered)
             if pending[j] is not None:
                 pending[j].wait()
                 pending[j] = None
+        return (nsteps[0] - 1) % 2  # the vector of the last step
 
     ctx.reset(sp)
-    for _ in range(args.warmup):
-        step()
-    drain()
+    enqueue(args.warmup)
+    # The timed steps are replayed from HIP graphs of G steps (kernel launches
+    # and, N>1, the all-reduces with their double-buffer dependencies): one
+    # graph launch per G steps instead of a Python launch + a c10d call per
+    # step, whose host cost alone (~25 us per all-reduce) exceeds a 21 us step.
+    # Each graph is replayed once, untimed, before timing (its upload).
+    graphs = []  # (graph, steps, vector of its last step)
+    launch_mode = "eager"
+    if args.graph and args.backend == "nccl":
+        G = min(args.steps, args.graph)
+        try:
+            for size in ([G] if args.steps % G == 0 else [G, args.steps % G]):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=stream, capture_error_mode="thread_local"):
+                    last = enqueue(size)
+                g.replay()
+                graphs.append((g, size, last))
+            launch_mode = f"hipGraph replay, {G} steps per graph"
+        except Exception as e:  # capture refused: time the same steps eagerly, and say so
+            print(f"bench: graph capture failed ({e!r}); timing eager launches", file=sys.stderr)
+            torch.cuda.synchronize()
+            graphs = []
+            launch_mode = "eager (graph capture failed)"
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -268,9 +293,15 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
-    for _ in range(args.steps):
-        step()
-    drain()  # every step's all-reduce is inside the timed region
+    if graphs:
+        g, size, last = graphs[0]
+        for _ in range(args.steps // size):
+            g.replay()
+        if len(graphs) > 1:
+            g, size, last = graphs[1]
+            g.replay()
+    else:
+        last = enqueue(args.steps)  # every step's all-reduce is inside the timed region
     e1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -283,7 +314,7 @@ def main():
 
     kern_ms = e0.elapsed_time(e1) / args.steps
     # correctness of the (merged) histogram: every sample of every rank is counted once
-    dv = dense[(nsteps[0] - 1) % 2].cpu().numpy()  # the last step's (merged) histogram
+    dv = dense[last].cpu().numpy()  # the last step's (merged) histogram
     assert dv[P.DENSE_BINS] == 0, "malformed samples"
     h = P.hist_from_dense(cfg, dv)
     assert h.total() == total, (h.total(), total)
@@ -313,6 +344,7 @@ def main():
                    "avg_ms": kern_ms, "timing": "HIP events on the launch stream around the K timed steps / K"
                    + (" (includes the overlapped all-reduces)" if world > 1 else ""),
                    "bytes_per_launch": BYTES_PER_SAMPLE * n_local},
+        "launch": launch_mode,
         "histogram_bins": len(h.bins),
     }
     if rank == 0:
@@ -332,7 +364,7 @@ def main():
     ctx.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

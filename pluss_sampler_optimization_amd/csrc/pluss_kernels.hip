@@ -776,8 +776,9 @@ __device__ __forceinline__ void flush_counts(uint32_t& acc, unsigned long long* 
 // ABL (diagnostics, tools/ablate.py): 0 product; 1 loads only (PLUSS_ABLATE=3); 2 count without the tail (=4)
 // XAUX >= 0 (diagnostics, PLUSS_AUX): that cache-policy immediate for the sample loads instead of NT's
 // LANES: full uniform steps counted by count_step_lanes (P2 && NP2 shapes); false = ballots only (PLUSS_LANES=0)
+// PREF: steps of sample loads in flight ahead of the step being counted (PLUSS_PREF=2: two)
 template <bool P2, bool NP2, bool NT, int TAIL, int UNR = UNROLL, int ABL = 0, int BS = BLOCK, int XAUX = -1,
-          bool LANES = true>
+          bool LANES = true, int PREF = 1>
 __global__ __launch_bounds__(BS) void k_count(Model m, const uint64_t* __restrict__ smp, uint64_t n,
                                               const uint64_t* __restrict__ head, int has_head, GTable g,
                                               ExportArgs ex) {
@@ -799,25 +800,27 @@ __global__ __launch_bounds__(BS) void k_count(Model m, const uint64_t* __restric
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(((uintptr_t)phi << 32) | plo), 0, (int)__builtin_amdgcn_readfirstlane(wn * 16u), 0x00020000);
     uint32_t base = blockIdx.x * (uint32_t)(BS * UNR);
-    u32x4 x[UNR];
+    u32x4 x[PREF][UNR];  // x[0]: this step's pairs; x[j]: step j ahead
 #pragma unroll
-    for (int u = 0; u < UNR; ++u)
-      x[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                           rs, (int)((base + u * BS + threadIdx.x) * 16u), 0, AUX));
+    for (int j = 0; j < PREF; ++j)
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+        x[j][u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                rs, (int)((base + j * step + u * BS + threadIdx.x) * 16u), 0, AUX));
     for (; base < wn; base += step) {
       u32x4 y[UNR];
 #pragma unroll
-      for (int u = 0; u < UNR; ++u)  // the next step's pairs (past the window: zeros)
+      for (int u = 0; u < UNR; ++u)  // the pairs PREF steps ahead (past the window: zeros)
         y[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             rs, (int)((base + step + u * BS + threadIdx.x) * 16u), 0, AUX));
+                                             rs, (int)((base + PREF * step + u * BS + threadIdx.x) * 16u), 0, AUX));
       uint32_t lo[2 * UNR], hi[2 * UNR];
       uint64_t okm[UNR];
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        lo[2 * u] = x[u].x;
-        hi[2 * u] = x[u].y;
-        lo[2 * u + 1] = x[u].z;
-        hi[2 * u + 1] = x[u].w;
+        lo[2 * u] = x[0][u].x;
+        hi[2 * u] = x[0][u].y;
+        lo[2 * u + 1] = x[0][u].z;
+        hi[2 * u + 1] = x[0][u].w;
         okm[u] = __ballot(base + u * BS + threadIdx.x < wn);
       }
       if (ABL == 1) {  // diagnostics: the same loads, nothing counted
@@ -827,7 +830,11 @@ __global__ __launch_bounds__(BS) void k_count(Model m, const uint64_t* __restric
         count_step<P2, NP2, UNR>(m, lo, hi, okm, acc);
       }
 #pragma unroll
-      for (int u = 0; u < UNR; ++u) x[u] = y[u];
+      for (int j = 0; j + 1 < PREF; ++j)
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) x[j][u] = x[j + 1][u];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) x[PREF - 1][u] = y[u];
     }
     if (ABL != 1) {  // per window: keeps the 32-bit lane counters from overflowing
       if (P2 && NP2 && LANES) lc_flush(lc, acc);
@@ -1201,6 +1208,19 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
     if (m.p2 && m.np2 && tail == TAIL_DENSE && lanesv && lanesv[0] == '0') {  // diagnostics: ballot counting only
       hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_DENSE, UNROLL, 0, BLOCK, -1, false>), dim3(nb), dim3(BLOCK),
                          0, s, m, d_samples, n, head, has_head, g, ex);
+      PLUSS_HIP_CHECK(hipGetLastError());
+      return PLUSS_OK;
+    }
+    const char* prefv = getenv("PLUSS_PREF");
+    if (m.p2 && m.np2 && tail == TAIL_DENSE && prefv && prefv[0] == '2') {  // diagnostics: two steps in flight
+      hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_DENSE, UNROLL, 0, BLOCK, -1, true, 2>), dim3(nb),
+                         dim3(BLOCK), 0, s, m, d_samples, n, head, has_head, g, ex);
+      PLUSS_HIP_CHECK(hipGetLastError());
+      return PLUSS_OK;
+    }
+    if (m.p2 && m.np2 && tail == TAIL_DENSE && prefv && prefv[0] == '3') {  // diagnostics: UNROLL 1, two steps in flight
+      hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_DENSE, 1, 0, BLOCK, -1, true, 2>), dim3(nb),
+                         dim3(BLOCK), 0, s, m, d_samples, n, head, has_head, g, ex);
       PLUSS_HIP_CHECK(hipGetLastError());
       return PLUSS_OK;
     }

@@ -65,19 +65,21 @@ def main():
             os.environ.pop(k, None)
 
         dense = torch.zeros(P.DENSE_BINS + 1, dtype=torch.int64, device=dev)
-        for v in [{}, dict(PLUSS_LANES="0"), dict(PLUSS_LEGACY="1"), dict(PLUSS_GRID="768"), dict(PLUSS_DROWS="8"), dict(PLUSS_DROWS="16"),
+        for v in [{}, dict(PLUSS_LANES="0"), dict(PLUSS_LEGACY="1"), dict(PLUSS_GRID="768"), dict(PLUSS_GRID="512"), dict(PLUSS_GRID="2048"),
+                  dict(PLUSS_PREF="2"), dict(PLUSS_PREF="2", PLUSS_GRID="512"), dict(PLUSS_PREF="3"),
+                  dict(PLUSS_UNROLL="1"), dict(PLUSS_DROWS="8"), dict(PLUSS_DROWS="16"),
                   dict(PLUSS_DROWS="64"), dict(PLUSS_BS="1024"), dict(PLUSS_BS="1024", PLUSS_GRID="512"),
                   dict(PLUSS_NT="0"), dict(PLUSS_UNROLL="4")] + [dict(PLUSS_AUX=a) for a in
                                                                   ("0", "1", "2", "3", "16", "17", "18", "19")]:
             for k in ("PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT", "PLUSS_LEGACY", "PLUSS_DROWS", "PLUSS_BS", "PLUSS_AUX",
-                      "PLUSS_LANES"):
+                      "PLUSS_LANES", "PLUSS_PREF"):
                 os.environ.pop(k, None)
             os.environ.update(v)
             ms = timeit(lambda: ctx.sampled_hist_dense(buf.data_ptr(), total, dense.data_ptr(), s.cuda_stream), s)
             print(json.dumps({"samples": total, "dense": v, "dense_ms": ms, "GBps": 8 * total / ms / 1e6}),
                   flush=True)
         for k in ("PLUSS_UNROLL", "PLUSS_GRID", "PLUSS_NT", "PLUSS_LEGACY", "PLUSS_DROWS", "PLUSS_BS", "PLUSS_AUX",
-                      "PLUSS_LANES"):
+                      "PLUSS_LANES", "PLUSS_PREF"):
             os.environ.pop(k, None)
         torch.cuda.synchronize()
         assert int(dense[:P.DENSE_BINS].sum()) == total and int(dense[P.DENSE_BINS]) == 0
