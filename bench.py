@@ -141,25 +141,39 @@ def fulltrace_bench(device, stream):
 
 
 def faithful_bench(cfg, samples, stream):
-    """FAITHFUL mode (r10 queue semantics: sort + scans) over the same 2^24 list, one sampler per reference."""
+    """FAITHFUL mode (r10 queue semantics: sort + scans) over the same 2^24 list: the six
+    sampler_<REF> at once (pluss_dev_faithful_hist_refs, one stream per reference, as r10
+    runs one thread per reference), and one after another for comparison."""
     fcfg = P.SamplerConfig(n=cfg.n, threads=cfg.threads, chunk=cfg.chunk, mode="faithful", device=cfg.device)
     counts = P.default_counts(cfg.n, len(samples))
+    out = {"samples": len(samples)}
     with P.Context(fcfg) as ctx:
-        def run():
+        def concurrent():
+            ctx.reset(stream.cuda_stream)
+            ctx.faithful_hist_refs(samples.data_ptr(), counts, stream.cuda_stream)
+
+        def serial():
             ctx.reset(stream.cuda_stream)
             off = 0
             for r, c in enumerate(counts):
                 ctx.faithful_hist(r, samples.data_ptr() + 8 * off, c, stream.cuda_stream)
                 off += c
-        run()
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        run()
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t
-        h = ctx.fetch()
-    return {"samples": len(samples), "ms": dt * 1e3, "samples_per_s": len(samples) / dt,
-            "recorded": h.total() - sum(h.cold(r) for r in P.REFS), "max_traversed": max(h.traversed)}
+        hs = {}
+        for name, run in (("concurrent", concurrent), ("serial", serial)):
+            run()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(3):
+                run()
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t) / 3
+            hs[name] = ctx.fetch()
+            out[name + "_ms"] = dt * 1e3
+    h = hs["concurrent"]
+    assert h.bins == hs["serial"].bins and list(h.traversed) == list(hs["serial"].traversed)
+    out.update({"ms": out["concurrent_ms"], "samples_per_s": len(samples) / (out["concurrent_ms"] * 1e-3),
+                "recorded": h.total() - sum(h.cold(r) for r in P.REFS), "max_traversed": max(h.traversed)})
+    return out
 
 
 def pmc_traffic(samples_per_launch):

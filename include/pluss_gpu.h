@@ -108,6 +108,12 @@ int pluss_dev_hist_reset(pluss_ctx *ctx, void *stream);
 int pluss_dev_sampled_hist(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t n, void *stream);
 /* faithful mode: one sampler_<REF> over a list holding only reference `ref` */
 int pluss_dev_faithful_hist(pluss_ctx *ctx, int32_t ref, const uint64_t *d_samples, uint64_t n, void *stream);
+/* faithful mode, all six sampler_<REF> of one list at once (r10's main runs
+   one thread per reference, r10:3203-3257): d_samples holds counts[0]
+   samples of reference 0, then counts[1] of reference 1, ...; equal to six
+   pluss_dev_faithful_hist calls.  The references run on streams of their
+   own, joined back into `stream`. */
+int pluss_dev_faithful_hist_refs(pluss_ctx *ctx, const uint64_t *d_samples, const uint64_t counts[6], void *stream);
 /* full trace: every access of the nest (sampling rate 1.0); accumulates like
    the other passes, and adds the N*N*(4N+2) accesses to traversed[0] */
 int pluss_dev_fulltrace_hist(pluss_ctx *ctx, void *stream);

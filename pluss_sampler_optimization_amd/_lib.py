@@ -21,7 +21,7 @@ EXPORTS = [
     "pluss_gemm_sampled_hist", "pluss_gemm_fulltrace_hist", "pluss_gemm_sampled_ri", "pluss_expand_samples",
     "pluss_default_counts",
     "pluss_ctx_create", "pluss_ctx_destroy", "pluss_ctx_stream", "pluss_dev_expand", "pluss_dev_hist_reset",
-    "pluss_dev_sampled_hist", "pluss_dev_faithful_hist", "pluss_dev_fulltrace_hist", "pluss_dev_sampled_ri",
+    "pluss_dev_sampled_hist", "pluss_dev_faithful_hist", "pluss_dev_faithful_hist_refs", "pluss_dev_fulltrace_hist", "pluss_dev_sampled_ri",
     "pluss_dev_hist_export", "pluss_dev_hist_export_reset", "pluss_dev_sampled_hist_export", "pluss_hist_fetch",
     "pluss_hist_from_tables", "pluss_faithful_key_space", "pluss_dev_faithful_shard_keys",
     "pluss_dev_faithful_shard_starts", "pluss_dev_faithful_shard_cut", "pluss_dev_faithful_shard_hist",
@@ -95,6 +95,7 @@ def lib():
         "pluss_dev_hist_reset": (ctypes.c_int, [vp, vp]),
         "pluss_dev_sampled_hist": (ctypes.c_int, [vp, vp, u64, vp]),
         "pluss_dev_faithful_hist": (ctypes.c_int, [vp, i32, vp, u64, vp]),
+        "pluss_dev_faithful_hist_refs": (ctypes.c_int, [vp, vp, ctypes.POINTER(ctypes.c_uint64), vp]),
         "pluss_dev_fulltrace_hist": (ctypes.c_int, [vp, vp]),
         "pluss_dev_sampled_ri": (ctypes.c_int, [vp, vp, u64, vp, vp, vp]),
         "pluss_dev_hist_export": (ctypes.c_int, [vp, vp, vp, u64, vp]),

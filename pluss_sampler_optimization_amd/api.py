@@ -240,6 +240,13 @@ class Context:
         rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
         check(lib().pluss_dev_faithful_hist(self._h, rid, d_samples, n, stream), "pluss_dev_faithful_hist")
 
+    def faithful_hist_refs(self, d_samples, counts, stream=None):
+        """All six sampler_<REF> at once (r10's main: one thread per reference):
+        d_samples holds counts[0] samples of reference 0, then counts[1] of
+        reference 1, ...  Same result as six faithful_hist calls."""
+        c = (ctypes.c_uint64 * 6)(*[int(x) for x in counts])
+        check(lib().pluss_dev_faithful_hist_refs(self._h, d_samples, c, stream), "pluss_dev_faithful_hist_refs")
+
     def fulltrace(self, stream=None):
         check(lib().pluss_dev_fulltrace_hist(self._h, stream), "pluss_dev_fulltrace_hist")
 

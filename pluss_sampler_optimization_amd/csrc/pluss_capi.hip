@@ -131,6 +131,7 @@ int pluss_ctx_create(const pluss_cfg* cfg, pluss_ctx** out) {
   pluss_ctx* c = new pluss_ctx();
   std::memset((void*)c, 0, sizeof(pluss_ctx));
   c->fb = FaithfulBufs();
+  for (auto& f : c->fbr) f = FaithfulBufs();
   c->cfg = *cfg;
   c->m = m;
   c->device = cfg->device;
@@ -171,9 +172,18 @@ int pluss_ctx_destroy(pluss_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->d_table,  c->d_exp_keys, c->d_exp_counts, c->d_exp_n, c->fb.keys,  c->fb.sinks,
                   c->fb.keys_s, c->fb.sinks_s, c->fb.pmax,      c->fb.nstart, c->fb.tmp,
-                  c->fb.scal};
+                  c->fb.scal, c->fb.st};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
+  for (const auto& f : c->fbr) {
+    void* fr[] = {f.keys, f.sinks, f.keys_s, f.sinks_s, f.pmax, f.nstart, f.tmp, f.scal, f.st};
+    for (void* p : fr)
+      if (p) (void)hipFree(p);
+  }
+  for (int r = 0; r < 6; ++r)
+    if (c->fst[r]) (void)hipStreamDestroy(c->fst[r]);
+  for (int e = 0; e < 7; ++e)
+    if (c->fev[e]) (void)hipEventDestroy(c->fev[e]);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return PLUSS_OK;
@@ -194,6 +204,11 @@ int pluss_dev_sampled_hist(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n
 int pluss_dev_faithful_hist(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, void* stream) {
   if (!ctx || (!d_samples && n) || ref < 0 || ref > 5) return PLUSS_ERR_CONFIG;
   return launch_faithful(ctx, ref, d_samples, n, pick(ctx, stream));
+}
+
+int pluss_dev_faithful_hist_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t counts[6], void* stream) {
+  if (!ctx || !counts) return PLUSS_ERR_CONFIG;
+  return launch_faithful_refs(ctx, d_samples, counts, pick(ctx, stream));
 }
 
 int pluss_dev_fulltrace_hist(pluss_ctx* ctx, void* stream) {

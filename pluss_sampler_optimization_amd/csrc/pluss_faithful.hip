@@ -32,6 +32,7 @@
 // Validated against the reference's own dumps (tests/golden/r10_*, 42/42).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <type_traits>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -237,6 +238,457 @@ __global__ __launch_bounds__(BLOCK) void k_faith_cut(FlagArgs fa, const unsigned
   if (__lane_id() == 0 && best != KEY_EMPTY) atomicMin(&scal[0], best);
 }
 
+// ---- one-GPU scan: prefix max of sinks, start flags, start counts and the Q1
+// cut in one pass over the sorted words (the shard path runs them as the
+// separate rocPRIM scans and k_faith_cut above, because its start offset and
+// cut need an exchange between the passes).  Tiles of SC_TILE elements take
+// their index from a counter in arrival order and chain through decoupled
+// look-back: each tile publishes its aggregate as soon as it has it and its
+// inclusive prefix once the look-back resolves; a status word is
+// flag (2 bits: 0 none, 1 aggregate, 2 inclusive) << 62 | value.
+constexpr int SC_ITEMS = 8;
+constexpr uint32_t SC_TILE = BLOCK * SC_ITEMS;
+constexpr unsigned long long ST_AGG = 1ull << 62, ST_INC = 2ull << 62, ST_VAL = (1ull << 62) - 1;
+
+__host__ __device__ inline uint64_t sc_tiles(uint64_t n) { return (n + SC_TILE - 1) / SC_TILE; }
+// sinks < 2^62 (keys < A*T); KEY_EMPTY (no reuse) travels as ST_VAL
+__device__ __forceinline__ unsigned long long st_cap(unsigned long long v) { return v > ST_VAL ? ST_VAL : v; }
+__device__ __forceinline__ unsigned long long st_uncap(unsigned long long v) { return v == ST_VAL ? KEY_EMPTY : v; }
+__device__ __forceinline__ unsigned long long st_ld(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_st(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool MAX>
+__device__ __forceinline__ unsigned long long sc_op(unsigned long long a, unsigned long long b) {
+  return MAX ? (a > b ? a : b) : a + b;
+}
+template <bool MAX>
+__device__ __forceinline__ unsigned long long sc_wave_red(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = sc_op<MAX>(v, __shfl_xor(v, o, 64));
+  return v;
+}
+template <bool MAX>
+__device__ __forceinline__ unsigned long long sc_wave_scan(unsigned long long v, uint32_t lane) {  // inclusive
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(v, o, 64);
+    if (lane >= (uint32_t)o) v = sc_op<MAX>(v, y);
+  }
+  return v;
+}
+// Exclusive prefix of tile t > 0 from the status words of tiles t-1, t-2, ...
+// (one whole wave, 64 predecessors per round).  Every predecessor took its
+// index earlier and publishes its aggregate without waiting on later tiles,
+// so the spin ends.
+template <bool MAX>
+__device__ unsigned long long sc_lookback(const unsigned long long* st, uint32_t t, uint32_t lane) {
+  unsigned long long acc = 0;
+  int64_t hi = (int64_t)t - 1;
+  while (true) {
+    const int64_t j = hi - (int64_t)lane;
+    unsigned long long w = j >= 0 ? st_ld(&st[j]) : ST_INC;  // before tile 0: the identity, inclusive
+    while (__ballot((w >> 62) == 0) != 0) {
+      __builtin_amdgcn_s_sleep(1);  // back off: the spinning waves share L2 with the publishers
+      if ((w >> 62) == 0) w = st_ld(&st[j]);
+    }
+    const unsigned long long inc = __ballot((w >> 62) == 2);
+    const uint32_t stop = inc ? (uint32_t)(__ffsll((long long)inc) - 1) : 64u;
+    acc = sc_op<MAX>(acc, sc_wave_red<MAX>(lane <= stop ? (w & ST_VAL) : 0ull));
+    if (inc) return acc;
+    hi -= 64;
+  }
+}
+// block-wide exclusive scan of one value per thread; returns (exclusive, aggregate)
+template <bool MAX>
+__device__ __forceinline__ void sc_block_scan(unsigned long long v, unsigned long long* sw, uint32_t lane, uint32_t wid,
+                                              unsigned long long& excl, unsigned long long& agg) {
+  const unsigned long long inc = sc_wave_scan<MAX>(v, lane);
+  if (lane == 63) sw[wid] = inc;
+  __syncthreads();
+  unsigned long long pre = 0, all = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < BLOCK / 64; ++w) {
+    const unsigned long long x = sw[w];
+    if (w < wid) pre = sc_op<MAX>(pre, x);
+    all = sc_op<MAX>(all, x);
+  }
+  const unsigned long long up = __shfl_up(inc, 1, 64);
+  excl = sc_op<MAX>(pre, lane ? up : 0ull);
+  agg = all;
+}
+// publish the tile's aggregate, resolve its exclusive prefix, publish the inclusive one (wave 0)
+template <bool MAX>
+__device__ __forceinline__ unsigned long long sc_chain(unsigned long long* st, uint32_t t, unsigned long long agg,
+                                                       uint32_t lane, unsigned long long* s_in) {
+  if (threadIdx.x < 64) {
+    unsigned long long in = 0;
+    if (t == 0) {
+      if (lane == 0) st_st(&st[0], ST_INC | st_cap(agg));
+    } else {
+      if (lane == 0) st_st(&st[t], ST_AGG | st_cap(agg));
+      in = sc_lookback<MAX>(st, t, lane);
+      if (lane == 0) st_st(&st[t], ST_INC | st_cap(sc_op<MAX>(in, agg)));
+    }
+    if (lane == 0) *s_in = in;
+  }
+  __syncthreads();
+  return *s_in;
+}
+
+// scal: [0] cut (= n beforehand), [4] tile counter; st: 2 * sc_tiles(n) zeroed words.
+// Wave w of a tile owns 64 * SC_ITEMS consecutive elements, visited as
+// SC_ITEMS rounds of 64 (lane l: element l of the round), so every load and
+// store is coalesced; the scans run across the lanes of each round with a
+// carry between rounds.
+template <int FM>
+__global__ __launch_bounds__(BLOCK) void k_faith_scan(FlagArgs fa, const unsigned long long* __restrict__ sinks,
+                                                      unsigned long long* __restrict__ pmax, uint64_t n,
+                                                      unsigned long long* st, unsigned long long* scal) {
+  __shared__ unsigned long long s_tile, s_w[BLOCK / 64], s_inm, s_inc;
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_tile = atomicAdd(&scal[4], 1ull);
+  __syncthreads();
+  const uint32_t t = (uint32_t)s_tile;
+  const uint64_t ntiles = sc_tiles(n);
+  unsigned long long* stm = st;
+  unsigned long long* stc = st + ntiles;
+  const uint64_t wbase = (uint64_t)t * SC_TILE + (uint64_t)wid * (64 * SC_ITEMS);
+  unsigned long long key[SC_ITEMS], snk[SC_ITEMS];
+  unsigned long long tm = 0;
+#pragma unroll
+  for (int k = 0; k < SC_ITEMS; ++k) {
+    const uint64_t i = wbase + (uint64_t)k * 64 + lane;
+    key[k] = KEY_EMPTY;
+    snk[k] = 0;  // the identity of max
+    if (i < n) {
+      if (FM == FM_PAIRS) {
+        key[k] = static_cast<const unsigned long long*>(fa.keys)[i];
+        snk[k] = sinks[i];
+      } else {
+        const fkey_t<FM> w = static_cast<const fkey_t<FM>*>(fa.keys)[i];
+        key[k] = pk_key(w, fa.pv);
+        snk[k] = pk_sink(w, fa.pv);
+      }
+    }
+    tm = snk[k] > tm ? snk[k] : tm;
+  }
+  // prefix max of sinks: wave aggregates -> tile aggregate -> look-back
+  const unsigned long long wagg = sc_wave_red<true>(st_cap(tm));
+  if (lane == 0) s_w[wid] = wagg;
+  __syncthreads();
+  unsigned long long pre = 0, agg = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < BLOCK / 64; ++w) {
+    const unsigned long long x = s_w[w];
+    if (w < wid) pre = x > pre ? x : pre;
+    agg = x > agg ? x : agg;
+  }
+  const unsigned long long m_in = sc_chain<true>(stm, t, agg, lane, &s_inm);
+  unsigned long long carry = st_uncap(m_in > pre ? m_in : pre);  // prefix max before the wave's first element
+  // per round: the prefix max (stored), the start flags (ballots), their count
+  unsigned long long fmask[SC_ITEMS];
+  uint32_t wcnt = 0;
+#pragma unroll
+  for (int k = 0; k < SC_ITEMS; ++k) {
+    const uint64_t i = wbase + (uint64_t)k * 64 + lane;
+    const bool valid = i < n;
+    unsigned long long inc = sc_wave_scan<true>(valid ? snk[k] : 0ull, lane);
+    inc = inc > carry ? inc : carry;
+    const unsigned long long up = __shfl_up(inc, 1, 64);
+    const unsigned long long before = lane ? up : carry;
+    fmask[k] = __ballot(valid && (i == 0 || key[k] > before));
+    wcnt += (uint32_t)__popcll(fmask[k]);
+    if (valid) pmax[i] = inc;
+    carry = __shfl(inc, 63, 64);
+  }
+  // start counts: wave totals -> tile total -> look-back
+  __syncthreads();  // s_w is reused
+  if (lane == 0) s_w[wid] = wcnt;
+  __syncthreads();
+  unsigned long long cpre = 0, cagg = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < BLOCK / 64; ++w) {
+    const unsigned long long x = s_w[w];
+    if (w < wid) cpre += x;
+    cagg += x;
+  }
+  const unsigned long long c_in = sc_chain<false>(stc, t, cagg, lane, &s_inc);
+  // Q1: the first start j > 0 whose met-sample count j - starts_before_j reaches n - j
+  uint64_t cb = c_in + cpre;  // starts before the round's first element
+  unsigned long long best = KEY_EMPTY;
+  const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int k = 0; k < SC_ITEMS; ++k) {
+    const unsigned long long F = fmask[k];
+    if (best == KEY_EMPTY && F) {
+      const uint64_t j = wbase + (uint64_t)k * 64 + lane;
+      const uint64_t before_j = cb + (uint64_t)__popcll(F & below);
+      const unsigned long long q = __ballot(((F >> lane) & 1ull) && j > 0 && j - before_j >= n - j);
+      if (q) best = wbase + (uint64_t)k * 64 + (uint64_t)(__ffsll((long long)q) - 1);
+    }
+    cb += (uint64_t)__popcll(F);
+  }
+  if (lane == 0 && best != KEY_EMPTY) atomicMin(&scal[0], best);
+}
+
+// scal [0] = cut default, [1] cold, [2] traversed, [4] tile counter; st zeroed
+__global__ void k_faith_scan_init(unsigned long long* scal, uint64_t cut, unsigned long long* st, uint64_t nw) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) {
+    scal[0] = cut;
+    scal[1] = 0;
+    scal[2] = 0;
+    scal[4] = 0;
+  }
+  for (uint64_t j = i; j < nw; j += (uint64_t)gridDim.x * blockDim.x) st[j] = 0;
+}
+
+// ---- one-GPU packed-word pass: scan, Q1 cut and record fused.  Chunks of
+// FCHUNK elements (1024 threads x FI) chain their prefix max and start count
+// through decoupled look-back (256 predecessors per round, so the chain
+// over a 2^22-element reference resolves in a couple of rounds), find their
+// own first qualifying start (the chunk's Q1 candidate) and record their
+// elements below it into per-chunk partial sums.  The condition of Q1,
+// j - starts_before_j >= n - j, is monotone in j, so the global cut is the
+// smallest candidate; k_faith_fused_finish adds the partials of the chunks
+// that start below it (the cut's own chunk recorded exactly the elements
+// before it; chunks before it have no candidate and recorded everything).
+// The prefix max is never stored.
+constexpr int FB = 1024, FI = 8;
+constexpr uint32_t FCHUNK = FB * FI;
+constexpr int FPART = 5;  // per chunk: cold (tid 0), traversed, case 0/1/2 counts
+__host__ __device__ inline uint64_t fu_tiles(uint64_t n) { return (n + FCHUNK - 1) / FCHUNK; }
+
+// exclusive prefix of tile t > 0, 4 predecessors per lane (256 per round)
+template <bool MAX>
+__device__ unsigned long long sc_lookback4(const unsigned long long* st, uint32_t t, uint32_t lane) {
+  unsigned long long acc = 0;
+  int64_t hi = (int64_t)t - 1;
+  while (true) {
+    unsigned long long w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t j = hi - (int64_t)(q * 64 + lane);
+      w[q] = j >= 0 ? st_ld(&st[j]) : ST_INC;
+    }
+    while (__ballot((w[0] >> 62) == 0 || (w[1] >> 62) == 0 || (w[2] >> 62) == 0 || (w[3] >> 62) == 0) != 0) {
+      __builtin_amdgcn_s_sleep(1);  // back off: the spinning waves share L2 with the publishers
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t j = hi - (int64_t)(q * 64 + lane);
+        if ((w[q] >> 62) == 0) w[q] = st_ld(&st[j]);
+      }
+    }
+    bool done = false;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (done) break;
+      const unsigned long long inc = __ballot((w[q] >> 62) == 2);
+      const uint32_t stop = inc ? (uint32_t)(__ffsll((long long)inc) - 1) : 64u;
+      acc = sc_op<MAX>(acc, sc_wave_red<MAX>(lane <= stop ? (w[q] & ST_VAL) : 0ull));
+      done = inc != 0;
+    }
+    if (done) return acc;
+    hi -= 256;
+  }
+}
+template <bool MAX>
+__device__ __forceinline__ unsigned long long fu_chain(unsigned long long* st, uint32_t t, unsigned long long agg,
+                                                       uint32_t lane, unsigned long long* s_in) {
+  if (threadIdx.x < 64) {
+    unsigned long long in = 0;
+    if (t == 0) {
+      if (lane == 0) st_st(&st[0], ST_INC | st_cap(agg));
+    } else {
+      if (lane == 0) st_st(&st[t], ST_AGG | st_cap(agg));
+      in = sc_lookback4<MAX>(st, t, lane);
+      if (lane == 0) st_st(&st[t], ST_INC | st_cap(sc_op<MAX>(in, agg)));
+    }
+    if (lane == 0) *s_in = in;
+  }
+  __syncthreads();
+  return *s_in;
+}
+
+// scal: [0] cut (= n beforehand), [4] tile counter; st: 2 * fu_tiles(n) zeroed words;
+// part: FPART words per chunk (written, not accumulated)
+template <int FM>
+__global__ __launch_bounds__(FB) void k_faith_fused(const void* __restrict__ words, PkView pv, uint64_t n,
+                                                    unsigned long long endkey, unsigned long long* st,
+                                                    unsigned long long* __restrict__ part,
+                                                    unsigned long long* scal) {
+  typedef fkey_t<FM> KT;
+  constexpr int NW = FB / 64;
+  __shared__ unsigned long long s_tile, s_w[NW], s_inm, s_inc, s_red[NW][FPART];
+  const KT* wd = static_cast<const KT*>(words);
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_tile = atomicAdd(&scal[4], 1ull);
+  __syncthreads();
+  const uint32_t t = (uint32_t)s_tile;
+  const uint64_t ntiles = fu_tiles(n);
+  const uint64_t wbase = (uint64_t)t * FCHUNK + (uint64_t)wid * (64 * FI);
+  KT w[FI];
+  unsigned long long tm = 0;
+#pragma unroll
+  for (int k = 0; k < FI; ++k) {
+    const uint64_t i = wbase + (uint64_t)k * 64 + lane;
+    w[k] = i < n ? wd[i] : (KT)0;
+    const unsigned long long sk = i < n ? pk_sink(w[k], pv) : 0ull;
+    tm = sk > tm ? sk : tm;
+  }
+  // prefix max of sinks
+  {
+    const unsigned long long wagg = sc_wave_red<true>(st_cap(tm));
+    if (lane == 0) s_w[wid] = wagg;
+  }
+  __syncthreads();
+  unsigned long long pre = 0, agg = 0;
+#pragma unroll
+  for (int x = 0; x < NW; ++x) {
+    const unsigned long long v = s_w[x];
+    if (x < (int)wid) pre = v > pre ? v : pre;
+    agg = v > agg ? v : agg;
+  }
+  const unsigned long long m_in = fu_chain<true>(st, t, agg, lane, &s_inm);
+  unsigned long long carry = st_uncap(m_in > pre ? m_in : pre);  // prefix max before the wave's first element
+  unsigned long long pm[FI], fmask[FI], key[FI];
+  uint32_t wcnt = 0;
+#pragma unroll
+  for (int k = 0; k < FI; ++k) {
+    const uint64_t i = wbase + (uint64_t)k * 64 + lane;
+    const bool valid = i < n;
+    unsigned long long inc = sc_wave_scan<true>(valid ? pk_sink(w[k], pv) : 0ull, lane);
+    inc = inc > carry ? inc : carry;
+    const unsigned long long up = __shfl_up(inc, 1, 64);
+    const unsigned long long before = lane ? up : carry;
+    key[k] = valid ? pk_key(w[k], pv) : KEY_EMPTY;
+    fmask[k] = __ballot(valid && (i == 0 || key[k] > before));
+    wcnt += (uint32_t)__popcll(fmask[k]);
+    pm[k] = inc;
+    carry = __shfl(inc, 63, 64);
+  }
+  // start counts
+  __syncthreads();  // s_w is reused
+  if (lane == 0) s_w[wid] = wcnt;
+  __syncthreads();
+  unsigned long long cpre = 0, cagg = 0;
+#pragma unroll
+  for (int x = 0; x < NW; ++x) {
+    const unsigned long long v = s_w[x];
+    if (x < (int)wid) cpre += v;
+    cagg += v;
+  }
+  const unsigned long long c_in = fu_chain<false>(st + ntiles, t, cagg, lane, &s_inc);
+  // the chunk's Q1 candidate: its first start j > 0 with j - starts_before_j >= n - j
+  unsigned long long best = KEY_EMPTY;
+  {
+    uint64_t cb = c_in + cpre;
+    const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int k = 0; k < FI; ++k) {
+      const unsigned long long F = fmask[k];
+      if (best == KEY_EMPTY && F) {
+        const uint64_t j = wbase + (uint64_t)k * 64 + lane;
+        const uint64_t before_j = cb + (uint64_t)__popcll(F & below);
+        const unsigned long long q = __ballot(((F >> lane) & 1ull) && j > 0 && j - before_j >= n - j);
+        if (q) best = wbase + (uint64_t)k * 64 + (uint64_t)(__ffsll((long long)q) - 1);
+      }
+      cb += (uint64_t)__popcll(F);
+    }
+  }
+  __syncthreads();  // s_w is reused
+  if (lane == 0) s_w[wid] = best;
+  __syncthreads();
+  unsigned long long cut = n;
+#pragma unroll
+  for (int x = 0; x < NW; ++x) cut = s_w[x] < cut ? s_w[x] : cut;
+  if (threadIdx.x == 0 && cut < n) atomicMin(&scal[0], cut);
+  // record the chunk's elements below its own cut
+  unsigned long long cold = 0, trav = 0;
+  uint32_t nc0 = 0, nc1 = 0, nc2 = 0;
+#pragma unroll
+  for (int k = 0; k < FI; ++k) {
+    const uint64_t i = wbase + (uint64_t)k * 64 + lane;
+    // the next element's key: the next lane, the next round's lane 0, or (the wave's last element) memory
+    unsigned long long kn = __shfl_down(key[k], 1, 64);
+    if (k + 1 < FI) {
+      const unsigned long long k0 = __shfl(key[k + 1], 0, 64);
+      if (lane == 63) kn = k0;
+    } else if (lane == 63) {
+      kn = i + 1 < n ? pk_key(wd[i + 1], pv) : KEY_EMPTY;
+    }
+    uint32_t c = 3;
+    bool rec = false;
+    if (i < cut) {
+      const unsigned long long kk = key[k];
+      c = (uint32_t)(w[k] & 3u);
+      if (pk_sink(w[k], pv) == KEY_EMPTY) cold += ((pv.p2 ? (kk & (pv.T - 1)) : kk % pv.T) == 0) ? 1u : 0u;
+      else rec = true;
+      if ((fmask[k] >> lane) & 1ull) trav -= kk;  // this element starts a replay
+      const unsigned long long gm = pm[k];
+      if (i + 1 == cut || (i + 1 < n ? kn > gm : true)) trav += (gm == KEY_EMPTY) ? endkey : gm;  // ends one
+    }
+    nc0 += (uint32_t)__popcll(__ballot(rec && c == 0));
+    nc1 += (uint32_t)__popcll(__ballot(rec && c == 1));
+    nc2 += (uint32_t)__popcll(__ballot(rec && c == 2));
+  }
+  cold = sc_wave_red<false>(cold);
+  trav = sc_wave_red<false>(trav);
+  if (lane == 0) {
+    s_red[wid][0] = cold;
+    s_red[wid][1] = trav;
+    s_red[wid][2] = nc0;
+    s_red[wid][3] = nc1;
+    s_red[wid][4] = nc2;
+  }
+  __syncthreads();
+  if (threadIdx.x < FPART) {
+    unsigned long long v = 0;
+#pragma unroll
+    for (int x = 0; x < NW; ++x) v += s_red[x][threadIdx.x];
+    part[(uint64_t)t * FPART + threadIdx.x] = v;
+  }
+}
+
+// Sum the partials of the chunks that start below the cut, then what
+// k_faith_finish does (Q3, the -1 key, traversed) and the case counts.
+__global__ __launch_bounds__(BLOCK) void k_faith_fused_finish(uint32_t ref, uint64_t n, PkView pv,
+                                                             const unsigned long long* st,
+                                                             const unsigned long long* part,
+                                                             const unsigned long long* scal, GTable g) {
+  __shared__ unsigned long long red[BLOCK / 64][FPART];
+  const uint64_t cut = scal[0];
+  const uint64_t ntiles = fu_tiles(n);
+  unsigned long long v[FPART] = {0, 0, 0, 0, 0};
+  for (uint64_t t = threadIdx.x; t < ntiles && t * FCHUNK < cut; t += BLOCK)
+#pragma unroll
+    for (int f = 0; f < FPART; ++f) v[f] += part[t * FPART + f];
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int f = 0; f < FPART; ++f) {
+    v[f] = sc_wave_red<false>(v[f]);
+    if (lane == 0) red[wid][f] = v[f];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tot[FPART] = {0, 0, 0, 0, 0};
+    for (int x = 0; x < BLOCK / 64; ++x)
+      for (int f = 0; f < FPART; ++f) tot[f] += red[x][f];
+    unsigned long long cold = tot[0];
+    if (n > 0 && cut == n) {  // Q3: nothing dropped; the owner of the largest sink stays in LAT
+      const unsigned long long gm = st_uncap(st[ntiles - 1] & ST_VAL);
+      if (gm != KEY_EMPTY && (pv.p2 ? (gm & (pv.T - 1)) : gm % pv.T) == 0) cold += 1;
+    }
+    g_add(g, make_key(ref, 0, -1), cold);
+    g.trav[ref] += tot[1];
+    for (int c = 0; c < 3; ++c)
+      if (tot[2 + c]) atomicAdd(&g.bins[ref * 3 + c], tot[2 + c]);
+  }
+}
+
 // Record the shard's samples with global index < cut: RI bins, tid-0 cold
 // samples, and the traversed contributions of the replays that start or end
 // here (a replay ends at j when j + 1 == cut or j + 1 starts one; for the
@@ -290,7 +742,7 @@ __global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, Fla
         s = sinks[i];
       }
       if (s == KEY_EMPTY) {
-        cold += (k % m.T == 0) ? 1u : 0u;
+        cold += ((fa.pv.p2 ? (k & (fa.pv.T - 1)) : k % fa.pv.T) == 0) ? 1u : 0u;  // tid 0
       } else if (PKD) {
         rec = true;
       } else {
@@ -312,8 +764,12 @@ __global__ __launch_bounds__(BLOCK) void k_faith_hist(Model m, uint32_t ref, Fla
       wave_count(wc, bt, g, key, rec);
     }
   }
-  atomicAdd(&red[0], cold);
-  atomicAdd(&red[1], trav);
+  cold = sc_wave_red<false>(cold);
+  trav = sc_wave_red<false>(trav);
+  if (lane == 0) {
+    atomicAdd(&red[0], cold);
+    atomicAdd(&red[1], trav);
+  }
   if (PKD && __lane_id() == 0) {
     if (nc0) atomicAdd(&red[2], (unsigned long long)nc0);
     if (nc1) atomicAdd(&red[3], (unsigned long long)nc1);
@@ -387,10 +843,9 @@ static int grid_of(uint64_t n) {
 }
 
 // buffers for n samples (sort words or keys + sinks, sorted copies, prefix max, scan of the start flags)
-static int faith_reserve(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
-  FaithfulBufs& b = ctx->fb;
+static int faith_reserve(pluss_ctx* ctx, FaithfulBufs& b, uint64_t n, hipStream_t s) {
   if (!b.scal) {
-    if (int rc = grow(&b.scal, 4)) return rc;
+    if (int rc = grow(&b.scal, 8)) return rc;
   }
   if (n > 0xFFFFFFFFull) {
     set_error("faithful mode: at most 2^32-1 samples per reference");
@@ -400,15 +855,15 @@ static int faith_reserve(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
     PLUSS_HIP_CHECK(hipStreamSynchronize(s));
     int rc = 0;
     if ((rc = grow(&b.keys, n)) || (rc = grow(&b.sinks, n)) || (rc = grow(&b.keys_s, n)) ||
-        (rc = grow(&b.sinks_s, n)) || (rc = grow(&b.pmax, n)) || (rc = grow(&b.nstart, n)))
+        (rc = grow(&b.sinks_s, n)) || (rc = grow(&b.pmax, n + FPART)) || (rc = grow(&b.nstart, n)) ||
+        (rc = grow(&b.st, 2 * sc_tiles(n))))
       return rc;
     b.cap = n;
   }
   return PLUSS_OK;
 }
 
-static int faith_tmp(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
-  FaithfulBufs& b = ctx->fb;
+static int faith_tmp(pluss_ctx* ctx, FaithfulBufs& b, uint64_t n, hipStream_t s) {
   size_t t1 = 0, t2 = 0, t3 = 0;
   const int fm = faith_fm(ctx->m);
   if (fm == FM_PK32) {  // packed words: keys-only sort, pmax over the recomputed sinks
@@ -446,10 +901,9 @@ static int faith_tmp(pluss_ctx* ctx, uint64_t n, hipStream_t s) {
   return PLUSS_OK;
 }
 
-static int faith_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, uint64_t lo, uint64_t hi,
+static int faith_keys(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, const uint64_t* d_samples, uint64_t n, uint64_t lo, uint64_t hi,
                       unsigned long long* cnt, hipStream_t s) {
   const Model& m = ctx->m;
-  FaithfulBufs& b = ctx->fb;
   const int fm = faith_fm(m);
   if (fm == FM_PK32)
     hipLaunchKernelGGL((k_faith_keys<true, FM_PK32>), dim3(grid_of(n)), dim3(BLOCK), 0, s, m, (uint32_t)ref, d_samples,
@@ -465,14 +919,14 @@ static int faith_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, ui
 }
 
 // sort the shard's n (key, sink) pairs by key and take the prefix max of sinks
-static int faith_sort(pluss_ctx* ctx, int32_t ref, uint64_t n, hipStream_t s) {
-  FaithfulBufs& b = ctx->fb;
-  if (int rc = faith_tmp(ctx, n, s)) return rc;
+static int faith_sort(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, uint64_t n, hipStream_t s, bool with_pmax = true) {
+  if (int rc = faith_tmp(ctx, b, n, s)) return rc;
   size_t sz = b.tmp_bytes;
   const int fm = faith_fm(ctx->m);
   if (fm == FM_PK32) {
     uint32_t *k = (uint32_t*)b.keys, *ks = (uint32_t*)b.keys_s;
     PLUSS_HIP_CHECK(rocprim::radix_sort_keys(b.tmp, sz, k, ks, n, 0, pk_bits(ctx->m), s));
+    if (!with_pmax) return PLUSS_OK;
     sz = b.tmp_bytes;
     auto it = rocprim::make_transform_iterator(ks, PkSinkOp<uint32_t>{make_pkview(ctx->m, (uint32_t)ref)});
     PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, it, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
@@ -480,6 +934,7 @@ static int faith_sort(pluss_ctx* ctx, int32_t ref, uint64_t n, hipStream_t s) {
   }
   if (fm == FM_PK64) {
     PLUSS_HIP_CHECK(rocprim::radix_sort_keys(b.tmp, sz, b.keys, b.keys_s, n, 0, pk_bits(ctx->m), s));
+    if (!with_pmax) return PLUSS_OK;
     sz = b.tmp_bytes;
     auto it = rocprim::make_transform_iterator(b.keys_s,
                                                PkSinkOp<unsigned long long>{make_pkview(ctx->m, (uint32_t)ref)});
@@ -488,14 +943,14 @@ static int faith_sort(pluss_ctx* ctx, int32_t ref, uint64_t n, hipStream_t s) {
   }
   PLUSS_HIP_CHECK(
       rocprim::radix_sort_pairs(b.tmp, sz, b.keys, b.keys_s, b.sinks, b.sinks_s, n, 0, key_bits(ctx->m), s));
+  if (!with_pmax) return PLUSS_OK;
   sz = b.tmp_bytes;
   PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, b.sinks_s, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
   return PLUSS_OK;
 }
 
-static int faith_starts(pluss_ctx* ctx, int32_t ref, uint64_t n, uint64_t j_off, unsigned long long pmax_in,
+static int faith_starts(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, uint64_t n, uint64_t j_off, unsigned long long pmax_in,
                         hipStream_t s) {
-  FaithfulBufs& b = ctx->fb;
   const FlagArgs fa{b.keys_s, b.pmax, j_off, pmax_in, make_pkview(ctx->m, (uint32_t)ref)};
   size_t sz = b.tmp_bytes;
   rocprim::counting_iterator<uint64_t> idx(0);
@@ -514,9 +969,8 @@ static int faith_starts(pluss_ctx* ctx, int32_t ref, uint64_t n, uint64_t j_off,
 }
 
 // Q1 cut of this shard's elements into scal[0] (already holding the default)
-static int faith_cut(pluss_ctx* ctx, int32_t ref, uint64_t n, uint64_t j_off, unsigned long long pmax_in,
+static int faith_cut(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, uint64_t n, uint64_t j_off, unsigned long long pmax_in,
                      uint64_t s_off, uint64_t n_total, hipStream_t s) {
-  FaithfulBufs& b = ctx->fb;
   const FlagArgs fa{b.keys_s, b.pmax, j_off, pmax_in, make_pkview(ctx->m, (uint32_t)ref)};
   const int fm = faith_fm(ctx->m);
   if (fm == FM_PK32)
@@ -532,10 +986,9 @@ static int faith_cut(pluss_ctx* ctx, int32_t ref, uint64_t n, uint64_t j_off, un
   return PLUSS_OK;
 }
 
-static int faith_record(pluss_ctx* ctx, int32_t ref, uint64_t n, uint64_t j_off, unsigned long long pmax_in,
+static int faith_record(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, uint64_t n, uint64_t j_off, unsigned long long pmax_in,
                         int next_start, uint64_t n_total, int is_last, hipStream_t s) {
   const Model& m = ctx->m;
-  FaithfulBufs& b = ctx->fb;
   if (n) {
     const FlagArgs fa{b.keys_s, b.pmax, j_off, pmax_in, make_pkview(m, (uint32_t)ref)};
     const int fm = faith_fm(m);
@@ -556,32 +1009,103 @@ static int faith_record(pluss_ctx* ctx, int32_t ref, uint64_t n, uint64_t j_off,
   return PLUSS_OK;
 }
 
+// the pipeline of one sampler_<REF> over its buffer set, on stream s
+static int faith_pipeline(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, const uint64_t* d_samples, uint64_t n,
+                          hipStream_t s) {
+  if (n == 0) return PLUSS_OK;
+  if (int rc = faith_keys(ctx, b, ref, d_samples, n, 0, 0, nullptr, s)) return rc;
+  if (int rc = faith_sort(ctx, b, ref, n, s, false)) return rc;
+  const int fm = faith_fm(ctx->m);
+  if (fm != FM_PAIRS) {
+    const uint64_t nt = fu_tiles(n);
+    hipLaunchKernelGGL(k_faith_scan_init, dim3((unsigned)std::min<uint64_t>((2 * nt + BLOCK - 1) / BLOCK + 1, 64)),
+                       dim3(BLOCK), 0, s, b.scal, n, b.st, 2 * nt);
+    const PkView pv = make_pkview(ctx->m, (uint32_t)ref);
+    const unsigned long long endkey = ctx->m.A * ctx->m.T;
+    unsigned long long* part = b.pmax;  // the prefix max is not stored: its buffer holds the partials
+    if (fm == FM_PK32)
+      hipLaunchKernelGGL(k_faith_fused<FM_PK32>, dim3((unsigned)nt), dim3(FB), 0, s, (const void*)b.keys_s, pv, n,
+                         endkey, b.st, part, b.scal);
+    else
+      hipLaunchKernelGGL(k_faith_fused<FM_PK64>, dim3((unsigned)nt), dim3(FB), 0, s, (const void*)b.keys_s, pv, n,
+                         endkey, b.st, part, b.scal);
+    hipLaunchKernelGGL(k_faith_fused_finish, dim3(1), dim3(BLOCK), 0, s, (uint32_t)ref, n, pv, b.st, part, b.scal,
+                       ctx->g);
+    PLUSS_HIP_CHECK(hipGetLastError());
+    ctx->tables_dirty = true;
+    return PLUSS_OK;
+  }
+  const uint64_t nw = 2 * sc_tiles(n);
+  hipLaunchKernelGGL(k_faith_scan_init, dim3((unsigned)std::min<uint64_t>((nw + BLOCK - 1) / BLOCK + 1, 64)),
+                     dim3(BLOCK), 0, s, b.scal, n, b.st, nw);
+  const FlagArgs fa{b.keys_s, b.pmax, 0, 0, make_pkview(ctx->m, (uint32_t)ref)};
+  const dim3 grid((unsigned)sc_tiles(n));
+  if (fm == FM_PK32)
+    hipLaunchKernelGGL(k_faith_scan<FM_PK32>, grid, dim3(BLOCK), 0, s, fa, b.sinks_s, b.pmax, n, b.st, b.scal);
+  else if (fm == FM_PK64)
+    hipLaunchKernelGGL(k_faith_scan<FM_PK64>, grid, dim3(BLOCK), 0, s, fa, b.sinks_s, b.pmax, n, b.st, b.scal);
+  else
+    hipLaunchKernelGGL(k_faith_scan<FM_PAIRS>, grid, dim3(BLOCK), 0, s, fa, b.sinks_s, b.pmax, n, b.st, b.scal);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  return faith_record(ctx, b, ref, n, 0, 0, 0, n, 1, s);
+}
+
 int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s) {
   if (int rc = faith_check_shape(ctx)) return rc;
-  if (int rc = faith_reserve(ctx, n, s)) return rc;
-  if (n == 0) return PLUSS_OK;
   FaithfulBufs& b = ctx->fb;
-  if (int rc = faith_keys(ctx, ref, d_samples, n, 0, 0, nullptr, s)) return rc;
-  if (int rc = faith_sort(ctx, ref, n, s)) return rc;
-  if (int rc = faith_starts(ctx, ref, n, 0, 0, s)) return rc;
-  hipLaunchKernelGGL(k_faith_init, dim3(1), dim3(1), 0, s, b.scal, n);
-  if (int rc = faith_cut(ctx, ref, n, 0, 0, 0, n, s)) return rc;
-  return faith_record(ctx, ref, n, 0, 0, 0, n, 1, s);
+  if (int rc = faith_reserve(ctx, b, n, s)) return rc;
+  return faith_pipeline(ctx, b, ref, d_samples, n, s);
+}
+
+// All six sampler_<REF> of one list at once, like r10's main, which runs
+// each on its own thread (r10:3203-3257): reference r's pipeline runs on its
+// own stream with its own buffers, forked from s and joined back into it.
+// The pipelines are chains of latency-bound steps (sort passes, look-back
+// scans) that leave most of the GPU idle one at a time.
+int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t* counts, hipStream_t s) {
+  if (int rc = faith_check_shape(ctx)) return rc;
+  uint64_t off[6], total = 0;
+  for (int r = 0; r < 6; ++r) {
+    off[r] = total;
+    total += counts[r];
+  }
+  if (total && !d_samples) {
+    set_error("pluss_dev_faithful_hist_refs: null sample list");
+    return PLUSS_ERR_CONFIG;
+  }
+  for (int r = 0; r < 6; ++r) {  // every allocation before the fork
+    if (!counts[r]) continue;
+    if (int rc = faith_reserve(ctx, ctx->fbr[r], counts[r], s)) return rc;
+    if (int rc = faith_tmp(ctx, ctx->fbr[r], counts[r], s)) return rc;
+  }
+  if (!ctx->fst[0]) {
+    for (int r = 0; r < 6; ++r) PLUSS_HIP_CHECK(hipStreamCreateWithFlags(&ctx->fst[r], hipStreamNonBlocking));
+    for (int e = 0; e < 7; ++e) PLUSS_HIP_CHECK(hipEventCreateWithFlags(&ctx->fev[e], hipEventDisableTiming));
+  }
+  PLUSS_HIP_CHECK(hipEventRecord(ctx->fev[6], s));
+  for (int r = 0; r < 6; ++r) {
+    if (!counts[r]) continue;
+    PLUSS_HIP_CHECK(hipStreamWaitEvent(ctx->fst[r], ctx->fev[6], 0));
+    if (int rc = faith_pipeline(ctx, ctx->fbr[r], r, d_samples + off[r], counts[r], ctx->fst[r])) return rc;
+    PLUSS_HIP_CHECK(hipEventRecord(ctx->fev[r], ctx->fst[r]));
+    PLUSS_HIP_CHECK(hipStreamWaitEvent(s, ctx->fev[r], 0));
+  }
+  return PLUSS_OK;
 }
 
 // ---- key-range shards (multi-GPU faithful mode; the caller exchanges the
 // ---- per-shard summaries between phases)
 int faith_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, uint64_t lo, uint64_t hi,
                      pluss_faith_shard* out, hipStream_t s) {
-  if (int rc = faith_check_shape(ctx)) return rc;
-  if (int rc = faith_reserve(ctx, n, s)) return rc;
-  FaithShard& f = ctx->fsh;
   FaithfulBufs& b = ctx->fb;
+  if (int rc = faith_check_shape(ctx)) return rc;
+  if (int rc = faith_reserve(ctx, b, n, s)) return rc;
+  FaithShard& f = ctx->fsh;
   f = FaithShard{};
   f.ref = ref;
   PLUSS_HIP_CHECK(hipMemsetAsync(b.scal + 3, 0, 8, s));
   if (n)
-    if (int rc = faith_keys(ctx, ref, d_samples, n, lo, hi, b.scal + 3, s)) return rc;
+    if (int rc = faith_keys(ctx, b, ref, d_samples, n, lo, hi, b.scal + 3, s)) return rc;
   unsigned long long m = 0;
   PLUSS_HIP_CHECK(hipMemcpyAsync(&m, b.scal + 3, 8, hipMemcpyDeviceToHost, s));
   PLUSS_HIP_CHECK(hipStreamSynchronize(s));
@@ -590,7 +1114,7 @@ int faith_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uin
   out->first_key = KEY_EMPTY;
   out->max_sink = 0;
   if (m) {
-    if (int rc = faith_sort(ctx, ref, m, s)) return rc;
+    if (int rc = faith_sort(ctx, b, ref, m, s)) return rc;
     const int fm = faith_fm(ctx->m);
     unsigned long long w64 = 0;
     uint32_t w32 = 0;
@@ -607,6 +1131,7 @@ int faith_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uin
 }
 
 int faith_shard_starts(pluss_ctx* ctx, uint64_t j_off, uint64_t pmax_in, pluss_faith_shard* out, hipStream_t s) {
+  FaithfulBufs& b = ctx->fb;
   FaithShard& f = ctx->fsh;
   if (f.phase != 1) {
     set_error("pluss_dev_faithful_shard_starts: call pluss_dev_faithful_shard_keys first");
@@ -616,9 +1141,9 @@ int faith_shard_starts(pluss_ctx* ctx, uint64_t j_off, uint64_t pmax_in, pluss_f
   f.pmax_in = pmax_in;
   out->n_starts = 0;
   if (f.n) {
-    if (int rc = faith_starts(ctx, f.ref, f.n, j_off, pmax_in, s)) return rc;
+    if (int rc = faith_starts(ctx, b, f.ref, f.n, j_off, pmax_in, s)) return rc;
     unsigned int c = 0;
-    PLUSS_HIP_CHECK(hipMemcpyAsync(&c, ctx->fb.nstart + (f.n - 1), 4, hipMemcpyDeviceToHost, s));
+    PLUSS_HIP_CHECK(hipMemcpyAsync(&c, b.nstart + (f.n - 1), 4, hipMemcpyDeviceToHost, s));
     PLUSS_HIP_CHECK(hipStreamSynchronize(s));
     out->n_starts = c;
   }
@@ -627,6 +1152,7 @@ int faith_shard_starts(pluss_ctx* ctx, uint64_t j_off, uint64_t pmax_in, pluss_f
 }
 
 int faith_shard_cut(pluss_ctx* ctx, uint64_t s_off, uint64_t n_total, pluss_faith_shard* out, hipStream_t s) {
+  FaithfulBufs& b = ctx->fb;
   FaithShard& f = ctx->fsh;
   if (f.phase != 2) {
     set_error("pluss_dev_faithful_shard_cut: call pluss_dev_faithful_shard_starts first");
@@ -639,9 +1165,8 @@ int faith_shard_cut(pluss_ctx* ctx, uint64_t s_off, uint64_t n_total, pluss_fait
   f.n_total = n_total;
   out->cut = n_total;
   if (f.n) {
-    FaithfulBufs& b = ctx->fb;
     hipLaunchKernelGGL(k_faith_init, dim3(1), dim3(1), 0, s, b.scal, n_total);
-    if (int rc = faith_cut(ctx, f.ref, f.n, f.j_off, f.pmax_in, s_off, n_total, s)) return rc;
+    if (int rc = faith_cut(ctx, b, f.ref, f.n, f.j_off, f.pmax_in, s_off, n_total, s)) return rc;
     PLUSS_HIP_CHECK(hipMemcpyAsync(&out->cut, b.scal, 8, hipMemcpyDeviceToHost, s));
     PLUSS_HIP_CHECK(hipStreamSynchronize(s));
   }
@@ -650,6 +1175,7 @@ int faith_shard_cut(pluss_ctx* ctx, uint64_t s_off, uint64_t n_total, pluss_fait
 }
 
 int faith_shard_hist(pluss_ctx* ctx, uint64_t cut, uint64_t next_first_key, int is_last, hipStream_t s) {
+  FaithfulBufs& b = ctx->fb;
   FaithShard& f = ctx->fsh;
   if (f.phase != 3) {
     set_error("pluss_dev_faithful_shard_hist: call pluss_dev_faithful_shard_cut first");
@@ -661,9 +1187,9 @@ int faith_shard_hist(pluss_ctx* ctx, uint64_t cut, uint64_t next_first_key, int 
   }
   const unsigned long long last = f.max_sink > f.pmax_in ? f.max_sink : f.pmax_in;  // global pmax at the shard end
   const int next_start = next_first_key != KEY_EMPTY && next_first_key > last;
-  hipLaunchKernelGGL(k_faith_init, dim3(1), dim3(1), 0, s, ctx->fb.scal, cut);
+  hipLaunchKernelGGL(k_faith_init, dim3(1), dim3(1), 0, s, b.scal, cut);
   f.phase = 0;
-  return faith_record(ctx, f.ref, f.n, f.j_off, f.pmax_in, next_start, f.n_total, is_last, s);
+  return faith_record(ctx, b, f.ref, f.n, f.j_off, f.pmax_in, next_start, f.n_total, is_last, s);
 }
 
 }  // namespace pluss

@@ -62,7 +62,8 @@ struct FaithfulBufs {
   unsigned int* nstart = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
-  unsigned long long* scal = nullptr;  // [0] cut, [1] cold, [2] traversed
+  unsigned long long* scal = nullptr;  // [0] cut, [1] cold, [2] traversed, [3] shard size, [4] scan tile counter
+  unsigned long long* st = nullptr;    // look-back status words of the one-GPU scan (2 per tile)
 };
 
 // state of a key-range shard between the phases of pluss_dev_faithful_shard_*
@@ -86,6 +87,9 @@ struct pluss_ctx {
   unsigned int* d_exp_n;
   pluss::FaithfulBufs fb;
   pluss::FaithShard fsh;
+  pluss::FaithfulBufs fbr[6];  // per-reference buffers of pluss_dev_faithful_hist_refs
+  hipStream_t fst[6];          // ... and its streams (created on first use)
+  hipEvent_t fev[7];           // fork / join events
   hipStream_t last;   // stream of the most recent launch (fetch orders after it)
   bool tables_dirty;  // hash tables may hold counts (GENERIC / faithful launches since the last reset)
 };
@@ -123,6 +127,7 @@ int launch_sampled_hist_export(pluss_ctx* ctx, const uint64_t* d_samples, uint64
 int launch_sampled_hist_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, unsigned long long* d_counts,
                               hipStream_t s);
 int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s);
+int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t* counts, hipStream_t s);
 int faith_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, uint64_t lo, uint64_t hi,
                      pluss_faith_shard* out, hipStream_t s);
 int faith_shard_starts(pluss_ctx* ctx, uint64_t j_off, uint64_t pmax_in, pluss_faith_shard* out, hipStream_t s);

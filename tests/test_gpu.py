@@ -688,3 +688,59 @@ def test_cli_replay_matches_reference_r10_printout(tmp_path, orc, name, d, smp):
     assert rows(sections["Start to dump reuse time"]) == d["printed"]["reuse"]
     assert rows(sections["miss ratio"]) == d["printed"]["mrc"]
     assert int(sections["max iteration traversed"][0]) == d["printed"]["max_traversed"]
+
+
+def _faithful_refs_vs_calls(c, s, counts, stream):
+    """(concurrent six-reference call, six single-reference calls) on the same handle."""
+    torch = pytest.importorskip("torch")
+    t = torch.from_numpy(np.ascontiguousarray(s).view(np.int64)).cuda()
+    with P.Context(c) as ctx:
+        ctx.reset(stream)
+        ctx.faithful_hist_refs(t.data_ptr(), counts, stream)
+        h_refs = ctx.fetch()
+        ctx.reset(stream)
+        off = 0
+        for r, n in enumerate(counts):
+            if n:
+                ctx.faithful_hist(r, t.data_ptr() + 8 * off, n, stream)
+            off += n
+        h_one = ctx.fetch()
+        ctx.reset(stream)
+        ctx.faithful_hist_refs(t.data_ptr(), counts, stream)  # again: buffers and streams are reused
+        h_again = ctx.fetch()
+    return h_refs, h_one, h_again
+
+
+@pytest.mark.parametrize("name,d,smp", GOLD, ids=[g[0] for g in GOLD])
+def test_faithful_refs_concurrent_equals_reference_dumps(orc, name, d, smp):
+    """pluss_dev_faithful_hist_refs (the six samplers on their own streams) reproduces r10's dumps."""
+    torch = pytest.importorskip("torch")
+    s = all_samples(orc, smp)
+    counts = [len(smp[ref]) for ref in orc.REFS]
+    assert [P.REF_ID[r] for r in orc.REFS] == list(range(6))
+    h, h_one, h_again = _faithful_refs_vs_calls(cfg(d["N"], d["T"], mode="faithful"), s, counts,
+                                                torch.cuda.current_stream().cuda_stream)
+    for ref in orc.REFS:
+        exp, etrav = expected_raw(d, ref)
+        assert {k: v for k, v in h.bins.items() if k[0] == ref} == exp, (name, ref)
+        assert h.traversed[P.REF_ID[ref]] == etrav, (name, ref)
+    assert h.bins == h_one.bins == h_again.bins
+    assert list(h.traversed) == list(h_one.traversed) == list(h_again.traversed)
+
+
+@pytest.mark.parametrize("N,T,CS,per", [(128, 4, 4, 6000), (100, 5, 4, 3000), (256, 8, 4, 40000), (64, 2, 4, 0)])
+def test_faithful_refs_concurrent_equals_per_reference_calls(N, T, CS, per):
+    """Packed-word (N % 8 == 0) and (key, sink) pair (N=100) shapes, longer lists, an empty
+    list: the concurrent call equals one faithful_hist call per reference."""
+    torch = pytest.importorskip("torch")
+    c = cfg(N, T, CS, mode="faithful")
+    counts = [min(per, (N - 1) ** 2) if r < 2 else per for r in range(6)]
+    if per:
+        counts[4] = per // 3  # unequal lengths
+    parts = [P.expand_samples(c, 0x5EED0100 + N, r, 0, n) if n else np.zeros(0, np.uint64)
+             for r, n in enumerate(counts)]
+    s = np.concatenate(parts).astype(np.uint64)
+    h, h_one, h_again = _faithful_refs_vs_calls(c, s, counts, torch.cuda.current_stream().cuda_stream)
+    assert h.bins == h_one.bins == h_again.bins
+    assert list(h.traversed) == list(h_one.traversed) == list(h_again.traversed)
+    assert h.total() == h_one.total()

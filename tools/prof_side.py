@@ -23,16 +23,21 @@ with P.Context(P.SamplerConfig(n=N, threads=T)) as ctx:
         ctx.expand(0x5EED0001, r, 0, c, buf.data_ptr() + 8 * off, s.cuda_stream)
         off += c
 torch.cuda.synchronize()
+mode = os.environ.get("PROF_FAITH", "serial")  # serial: one faithful_hist per reference; concurrent: faithful_hist_refs
 with P.Context(P.SamplerConfig(n=N, threads=T, mode="faithful")) as ctx:
-    for rep in range(2):
+    for rep in range(3):
         ctx.reset(s.cuda_stream)
-        t = time.perf_counter()
-        off = 0
-        for r, c in enumerate(counts):
-            ctx.faithful_hist(r, buf.data_ptr() + 8 * off, c, s.cuda_stream)
-            off += c
         torch.cuda.synchronize()
-        print(f"faithful 2^24: {(time.perf_counter() - t) * 1e3:.3f} ms", flush=True)
+        t = time.perf_counter()
+        if mode == "concurrent":
+            ctx.faithful_hist_refs(buf.data_ptr(), counts, s.cuda_stream)
+        else:
+            off = 0
+            for r, c in enumerate(counts):
+                ctx.faithful_hist(r, buf.data_ptr() + 8 * off, c, s.cuda_stream)
+                off += c
+        torch.cuda.synchronize()
+        print(f"faithful 2^24 ({mode}): {(time.perf_counter() - t) * 1e3:.3f} ms", flush=True)
 with P.Context(P.SamplerConfig(n=512, threads=4, thr_variant="v1")) as ctx:
     for rep in range(2):
         t = time.perf_counter()
