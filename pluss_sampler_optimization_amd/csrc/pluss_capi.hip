@@ -175,11 +175,17 @@ int pluss_ctx_destroy(pluss_ctx* c) {
                   c->fb.scal, c->fb.st};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
-  for (const auto& f : c->fbr) {
-    void* fr[] = {f.keys, f.sinks, f.keys_s, f.sinks_s, f.pmax, f.nstart, f.tmp, f.scal, f.st};
+  auto free_bufs = [](const pluss::FaithfulBufs& f, bool core) {
+    void* fr[] = {core ? nullptr : f.keys, core ? nullptr : f.sinks, core ? nullptr : f.keys_s,
+                  core ? nullptr : f.sinks_s, core ? nullptr : f.pmax, core ? nullptr : f.nstart,
+                  core ? nullptr : f.tmp, core ? nullptr : f.scal, core ? nullptr : f.st,
+                  f.bc, f.bo, f.bm, f.bst, f.bpart};
     for (void* p : fr)
       if (p) (void)hipFree(p);
-  }
+  };
+  free_bufs(c->fb, true);  // its core buffers are freed above
+  for (const auto& f : c->fbr) free_bufs(f, false);
+  if (c->hmx) (void)hipHostFree(c->hmx);
   for (int r = 0; r < 6; ++r)
     if (c->fst[r]) (void)hipStreamDestroy(c->fst[r]);
   for (int e = 0; e < 7; ++e)

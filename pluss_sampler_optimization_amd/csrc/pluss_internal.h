@@ -64,6 +64,11 @@ struct FaithfulBufs {
   size_t tmp_bytes = 0;
   unsigned long long* scal = nullptr;  // [0] cut, [1] cold, [2] traversed, [3] shard size, [4] scan tile counter
   unsigned long long* st = nullptr;    // look-back status words of the one-GPU scan (2 per tile)
+  // bucket path (pluss_faithful.hip, one GPU, packed words): per bucket the
+  // count (then the scatter cursor), the offset (nb + 1), the smallest word
+  // (relative to the bucket base), look-back words (2 per bucket), partials
+  unsigned int *bc = nullptr, *bo = nullptr, *bm = nullptr;
+  unsigned long long *bst = nullptr, *bpart = nullptr;
 };
 
 // state of a key-range shard between the phases of pluss_dev_faithful_shard_*
@@ -90,6 +95,7 @@ struct pluss_ctx {
   pluss::FaithfulBufs fbr[6];  // per-reference buffers of pluss_dev_faithful_hist_refs
   hipStream_t fst[6];          // ... and its streams (created on first use)
   hipEvent_t fev[7];           // fork / join events
+  unsigned long long* hmx;     // pinned: largest bucket per reference (faithful bucket path)
   hipStream_t last;   // stream of the most recent launch (fetch orders after it)
   bool tables_dirty;  // hash tables may hold counts (GENERIC / faithful launches since the last reset)
 };

@@ -744,3 +744,72 @@ def test_faithful_refs_concurrent_equals_per_reference_calls(N, T, CS, per):
     assert h.bins == h_one.bins == h_again.bins
     assert list(h.traversed) == list(h_one.traversed) == list(h_again.traversed)
     assert h.total() == h_one.total()
+
+
+def _faithful_both_paths(c, s, counts):
+    """Faithful histograms of one list: bucket path (PLUSS_FAITH_BUCKET=1), radix-sort
+    path (the default), each through one call per reference and through the
+    concurrent six-reference call."""
+    torch = pytest.importorskip("torch")
+    t = torch.from_numpy(np.ascontiguousarray(s).view(np.int64)).cuda()
+    stream = torch.cuda.current_stream().cuda_stream
+    out = {}
+    for path in ("bucket", "sorted"):
+        os.environ["PLUSS_FAITH_BUCKET"] = "1" if path == "bucket" else "0"
+        try:
+            with P.Context(c) as ctx:
+                ctx.reset(stream)
+                off = 0
+                for r, n in enumerate(counts):
+                    if n:
+                        ctx.faithful_hist(r, t.data_ptr() + 8 * off, n, stream)
+                    off += n
+                out[path] = ctx.fetch()
+                ctx.reset(stream)
+                ctx.faithful_hist_refs(t.data_ptr(), counts, stream)
+                out[path + "_refs"] = ctx.fetch()
+        finally:
+            os.environ.pop("PLUSS_FAITH_BUCKET", None)
+    return out
+
+
+def _assert_same(hs):
+    first = next(iter(hs.values()))
+    for k, h in hs.items():
+        assert h.bins == first.bins, k
+        assert list(h.traversed) == list(first.traversed), k
+
+
+@pytest.mark.parametrize("N,T,per", [(1024, 8, 300000), (2048, 8, 200000), (256, 4, 40000), (128, 4, 1)])
+def test_faithful_bucket_path_equals_radix_sort_path(N, T, per):
+    """The bucket path (per-bucket LDS sort + fused scan) equals the device-wide
+    radix-sort path: 32-bit words (N=1024: 128 buckets), 64-bit words (N=2048),
+    a one-bucket list (N=256 ... 40000 per reference: 16 buckets) and one sample."""
+    c = cfg(N, T, mode="faithful")
+    counts = [min(per, (N - 1) ** 2) if r < 2 else per for r in range(6)]
+    s = np.concatenate([P.expand_samples(c, 0x5EED0200 + N, r, 0, n) for r, n in enumerate(counts)]).astype(np.uint64)
+    hs = _faithful_both_paths(c, s, counts)
+    _assert_same(hs)
+    assert hs["bucket"].total() > 0
+
+
+def test_faithful_skewed_list_falls_back_to_radix_sort(orc):
+    """A list crowded into one bucket (rows c0 < 2*T*CS: all in bucket 0 of 8,
+    20000 > the 8192-word tile) takes the radix-sort path; results equal the
+    radix-sort path, the oracle, and the bucket path for the uncrowded references."""
+    N, T = 256, 4
+    c = cfg(N, T, mode="faithful")
+    rng = np.random.default_rng(7)
+    idx = rng.choice(32 * 255 * 255, 20000, replace=False)
+    c0, rest = idx // (255 * 255), idx % (255 * 255)
+    c1, c2 = rest // 255, rest % 255
+    crowded = (np.uint64(P.REF_ID["B0"]) << np.uint64(60)) | (c0.astype(np.uint64) << np.uint64(40)) \
+        | (c1.astype(np.uint64) << np.uint64(20)) | c2.astype(np.uint64)
+    counts = [300, 300, 5000, 20000, 5000, 5000]
+    parts = [P.expand_samples(c, 0x5EED0300, r, 0, n) if r != 3 else crowded for r, n in enumerate(counts)]
+    s = np.concatenate(parts).astype(np.uint64)
+    hs = _faithful_both_paths(c, s, counts)
+    _assert_same(hs)
+    want, trav = orc.faithful(orc.cfg(N, T), "B0", crowded)
+    assert {k: v for k, v in hs["bucket"].bins.items() if k[0] == "B0"} == want
+    assert hs["bucket"].traversed[P.REF_ID["B0"]] == trav
