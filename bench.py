@@ -349,12 +349,13 @@ def main():
         "data": "synthetic: keyed cycle-walking Feistel sample lists (seed 0x5EED0001), indices in [0,N-2]",
         "config": {"workload": spec["workload"], "N": cfg.n, "threads": cfg.threads, "chunk": 4, "ds": 8,
                    "cls": 64, "mode": "clean", "samples_per_gpu": n_local, "global_samples": total,
-                   "parallelism": f"sample-shard x{world}" + (" + RCCL all_reduce of the dense histogram"
-                                                             if world > 1 else "")},
+                   "parallelism": f"sample-shard x{world}" + (
+                       f" + {'RCCL' if args.backend == 'nccl' else 'gloo'} all_reduce of the dense histogram"
+                       if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(n_local)},
-        "kernel": {"name": "pluss::k_count<true,true,true,TAIL_DENSE,2> (ballot counting, nt buffer loads, "
-                           "dense tail)",
+        "kernel": {"name": "pluss::k_count<true,true,true,TAIL_DENSE,2> (per-lane integer case tests on full "
+                           "uniform steps, ballots otherwise; nt buffer loads; dense tail)",
                    "avg_ms": kern_ms, "timing": "HIP events on the launch stream around the K timed steps / K"
                    + (" (includes the overlapped all-reduces)" if world > 1 else ""),
                    "bytes_per_launch": BYTES_PER_SAMPLE * n_local},

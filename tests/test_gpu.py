@@ -813,3 +813,47 @@ def test_faithful_skewed_list_falls_back_to_radix_sort(orc):
     want, trav = orc.faithful(orc.cfg(N, T), "B0", crowded)
     assert {k: v for k, v in hs["bucket"].bins.items() if k[0] == "B0"} == want
     assert hs["bucket"].traversed[P.REF_ID["B0"]] == trav
+
+
+@pytest.mark.parametrize("rank", [0, 7])
+def test_dense_pass_config3_shard(rank):
+    """BASELINE config 3 (N=4096, T=8, 2^28 samples over 8 GPUs): one rank's slice
+    (2^25 samples; rank 7 holds B0's +2 remainder) through the bench's step equals
+    the closed-form histogram of that slice, and the eight slices tile the counts."""
+    torch = pytest.importorskip("torch")
+    N, T, world = 4096, 8, 8
+    c = cfg(N, T)
+    counts = P.default_counts(N, 1 << 28)
+    assert sum(counts) == 1 << 28
+    parts = [(cnt * rank // world, cnt * (rank + 1) // world - cnt * rank // world) for cnt in counts]
+    assert sum(sum(cnt * (r + 1) // world - cnt * r // world for r in range(world)) for cnt in counts) == 1 << 28
+    n = sum(k for _, k in parts)
+    buf = torch.empty(n, dtype=torch.int64, device="cuda")
+    d = torch.zeros(P.DENSE_BINS + 1, dtype=torch.int64, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    with P.Context(c) as ctx:
+        off = 0
+        for r, (lo, k) in enumerate(parts):
+            ctx.expand(0x5EED0001, r, lo, k, buf.data_ptr() + 8 * off, stream)
+            off += k
+        for _ in range(2):
+            ctx.sampled_hist_dense(buf.data_ptr(), n, d.data_ptr(), stream)
+        torch.cuda.synchronize()
+    v = d.cpu().numpy()
+    assert v[P.DENSE_BINS] == 0
+    h = P.hist_from_dense(c, v)
+    assert h.total() == n
+    assert h.bins == closed_form_hist(N, T, 4, buf.cpu().numpy().view(np.uint64))
+
+
+def test_faithful_n4096_concurrent_equals_serial():
+    """Faithful mode at the config-3 shape (N=4096: 64-bit packed words), 2^20 samples
+    per 3-D reference: the six-stream call equals six calls, on both sort paths."""
+    N, T = 4096, 8
+    c = cfg(N, T, mode="faithful")
+    counts = [20000, 20000, 1 << 20, 1 << 20, 1 << 20, 1 << 20]
+    s = np.concatenate([P.expand_samples(c, 0x5EED0001, r, 0, k) for r, k in enumerate(counts)]).astype(np.uint64)
+    hs = _faithful_both_paths(c, s, counts)
+    _assert_same(hs)
+    h = hs["sorted"]
+    assert 0 < h.total() - sum(h.cold(r) for r in P.REFS) <= sum(counts)
