@@ -204,7 +204,7 @@ def main():
     ap.add_argument("--graph", type=int, default=20,
                     help="steps per captured HIP graph for the timed region (0: eager launches)")
     ap.add_argument("--allreduce", action="store_true",
-                    help="rehearsal: run the merge all-reduce even at world size 1 (under torch.distributed.run)")
+                    help="rehearsal: run the merge all-reduce even at world size 1 (with or without torch.distributed.run)")
     ap.add_argument("--no-extras", action="store_true", help="skip the full-trace / faithful side measurements")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend (nccl = RCCL over xGMI; gloo only to rehearse N>1 on one GPU)")
@@ -219,6 +219,9 @@ def main():
     local = local % max(1, torch.cuda.device_count())  # rehearsal: several ranks may share one GPU
     torch.cuda.set_device(local)
     if world > 1 or args.allreduce:
+        if world == 1:  # --allreduce without a launcher: a one-rank group on the loopback address
+            for k, v in (("RANK", "0"), ("WORLD_SIZE", "1"), ("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531")):
+                os.environ.setdefault(k, v)
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
