@@ -1157,8 +1157,13 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
     ++d_samples;
     --n;
   }
-  int nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL);
   const Model& m = ctx->m;
+  // Lists past the Infinity Cache stream from HBM, where fewer resident waves per CU
+  // queue fewer requests against the same channels: measured on MI355X with
+  // tools/grid_sweep.py (profiles/r05_grid_sweep.jsonl), 1024 workgroups are best at
+  // 2^24-2^25 samples, 768 at 2^26 (+1.8%), 640 at 2^27-2^28 (+3.4%).
+  const int cap = !m.fast ? MAX_BLOCKS : n >= (1ull << 27) ? 640 : n >= (1ull << 26) ? 768 : MAX_BLOCKS;
+  int nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL, std::min(cap, MAX_BLOCKS));
   const GTable& g = ctx->g;
 #define PLUSS_LAUNCH_HOT(EX, ...)                                                                                  \
   hipLaunchKernelGGL((k_sampled_hist<__VA_ARGS__>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n, head, has_head, g, \

@@ -330,7 +330,7 @@ def test_dense_pass(orc, N, T, CS):
         first = None
         try:
             knobs = ("PLUSS_GRID", "PLUSS_LEGACY", "PLUSS_DROWS", "PLUSS_BS", "PLUSS_LANES")
-            for grid in ("", "1", "3", "64", "65", "200", "1024", "legacy", "drows1", "drows8", "drows64", "bs1024",
+            for grid in ("", "1", "3", "64", "65", "200", "640", "768", "1024", "legacy", "drows1", "drows8", "drows64", "bs1024",
                          "bs1024_3", "ballots"):
                 for k in knobs:
                     os.environ.pop(k, None)
