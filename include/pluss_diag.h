@@ -1,0 +1,35 @@
+/*
+ * pluss_diag.h — diagnostics of libpluss_gpu.so.  NOT part of the drop-in
+ * boundary (include/pluss_gpu.h): nothing in the product path calls these,
+ * and no environment variable changes what a pluss_* entry point computes.
+ * Used by tools/ablate.py (where the hot kernel's time goes) and
+ * tools/grid_sweep.py (workgroup count vs list size).
+ */
+#ifndef PLUSS_DIAG_H
+#define PLUSS_DIAG_H
+
+#include <stdint.h>
+
+#include "pluss_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  PLUSS_DIAG_PRODUCT = 0,    /* the product dense pass (pluss_dev_sampled_hist_dense), d_counts written */
+  PLUSS_DIAG_LOADS_ONLY = 1, /* the same sample loads, nothing counted, nothing written */
+  PLUSS_DIAG_NO_TAIL = 2     /* counted, but no tail: nothing written */
+};
+
+/* One dense pass over a device sample list (N, CLS/DS and chunk powers of two
+   for variants 1 and 2).  max_grid > 0 replaces the launcher's workgroup cap
+   (product variant: the counts are still exact; tests use it to cover grids
+   of 1..16384 workgroups).  Returns PLUSS_OK or PLUSS_ERR_*. */
+int pluss_diag_dense(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t n, uint64_t *d_counts, int32_t variant,
+                     int32_t max_grid, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PLUSS_DIAG_H */

@@ -42,12 +42,13 @@ def lib():
         L = ctypes.CDLL(_LIB_PATH)
         P = ctypes.POINTER
         L.orc_fulltrace.argtypes = [P(OrcCfg), P(OrcEntry), ctypes.c_int64, P(ctypes.c_int64), P(ctypes.c_int64)]
+        L.orc_fulltrace_mt.argtypes = L.orc_fulltrace.argtypes
         L.orc_clean.argtypes = [P(OrcCfg), P(ctypes.c_uint64), ctypes.c_int64, P(ctypes.c_int64), ctypes.c_int]
         L.orc_faithful.argtypes = [P(OrcCfg), ctypes.c_int, P(ctypes.c_uint64), ctypes.c_int64,
                                    P(OrcEntry), ctypes.c_int64, P(ctypes.c_int64), P(ctypes.c_int64)]
         L.orc_expand.argtypes = [P(OrcCfg), ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
                                  P(ctypes.c_uint64)]
-        for f in (L.orc_fulltrace, L.orc_clean, L.orc_faithful, L.orc_expand):
+        for f in (L.orc_fulltrace, L.orc_fulltrace_mt, L.orc_clean, L.orc_faithful, L.orc_expand):
             f.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -78,6 +79,19 @@ def fulltrace(N, T, CS=4, DS=8, CLS=64, thr_variant=1):
     rc = lib().orc_fulltrace(ctypes.byref(c), buf, cap, ctypes.byref(n), ctypes.byref(trav))
     if rc:
         raise RuntimeError(f"orc_fulltrace rc={rc}")
+    return _entries_to_dict(buf, n.value), trav.value
+
+
+def fulltrace_mt(N, T, CS=4, DS=8, CLS=64, thr_variant=1):
+    """orc_fulltrace with one host thread per simulated tid (same result)."""
+    c = cfg(N, T, CS, DS, CLS, thr_variant)
+    cap = 4096
+    buf = (OrcEntry * cap)()
+    n = ctypes.c_int64()
+    trav = ctypes.c_int64()
+    rc = lib().orc_fulltrace_mt(ctypes.byref(c), buf, cap, ctypes.byref(n), ctypes.byref(trav))
+    if rc:
+        raise RuntimeError(f"orc_fulltrace_mt rc={rc}")
     return _entries_to_dict(buf, n.value), trav.value
 
 

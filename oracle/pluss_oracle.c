@@ -13,6 +13,8 @@
  *                    (per-tid LAT per array, count[tid], share test :203,
  *                    cold = |LAT| per tid :305-319).  Static schedule per
  *                    ChunkDispatcher (runtime/pluss_utils.h:298-334, 386-425).
+ *                    orc_fulltrace_mt: the same, one host thread per simulated
+ *                    tid (the shape of rayon_sampler, src/gemm_sampler_rayon.rs:107-126).
  *   orc_faithful   — one `sampler_<REF>` of
  *                    c_lib/test/sampler/gemm-t4-pluss-pro-model-rs-ri-opt-r10.cpp
  *                    (sampler_C3 :135-696 is the template; B0 share test
@@ -187,42 +189,93 @@ static int cfg_ok(const orc_cfg *c) {
 }
 
 /* ------------------------------------------------------------ full trace -- */
+/* One simulated thread's whole stream: per-array LAT (dense by line), raw RI
+   keyed by the SOURCE reference, cold = lines left in a LAT (seq.cpp:305-319). */
+static int fulltrace_tid(const orc_cfg *c, int64_t tid, uint64_t *lat[3], int64_t nlines, omap *h,
+                         int64_t *count_out) {
+    for (int a = 0; a < 3; a++) memset(lat[a], 0, (size_t)nlines * 8);
+    cursor u; memset(&u, 0, sizeof u); u.lb_next = tid * c->CS;
+    cur_next_chunk(c, &u);
+    uint64_t count = 0;
+    while (!u.done) {
+        int arr = REF_ARRAY[u.ref];
+        uint64_t line = addr_of(c, u.ref, u.c0, u.c1, u.c2);
+        uint64_t prev = lat[arr][line];
+        if (prev) {
+            int src = (int)(prev & 7) - 1;
+            int64_t reuse = (int64_t)(count - (prev >> 3));
+            int kind = (u.ref == R_B0 && is_share(c, reuse)) ? 1 : 0;
+            if (hist_add(h, src, kind, reuse, 1)) return -3;
+        }
+        lat[arr][line] = (count << 3) | (uint64_t)(u.ref + 1);  /* LAT value = (count << 3) | (src ref + 1) */
+        count++;
+        cur_step(c, &u);
+    }
+    for (int a = 0; a < 3; a++)
+        for (int64_t l = 0; l < nlines; l++)
+            if (lat[a][l]) { if (hist_add(h, (int)(lat[a][l] & 7) - 1, 0, -1, 1)) return -3; }
+    *count_out = (int64_t)count;
+    return 0;
+}
+
+/* sequential: for tid in 0..T (seq.cpp:68) */
 int orc_fulltrace(const orc_cfg *c, orc_entry *out, int64_t cap, int64_t *n_out,
                   int64_t *traversed) {
     if (!cfg_ok(c)) return -1;
     int64_t nlines = (c->N * c->N * c->DS) / c->CLS + 1;
-    /* LAT value = (count << 3) | (src ref + 1); 0 = absent */
     uint64_t *lat[3];
     for (int a = 0; a < 3; a++) { lat[a] = (uint64_t *)malloc((size_t)nlines * 8); if (!lat[a]) return -3; }
     omap h; if (om_init(&h, 64)) return -3;
     int64_t total = 0;
-    for (int64_t tid = 0; tid < c->T; tid++) {
-        for (int a = 0; a < 3; a++) memset(lat[a], 0, (size_t)nlines * 8);
-        cursor u; memset(&u, 0, sizeof u); u.lb_next = tid * c->CS;
-        cur_next_chunk(c, &u);
-        uint64_t count = 0;
-        while (!u.done) {
-            int arr = REF_ARRAY[u.ref];
-            uint64_t line = addr_of(c, u.ref, u.c0, u.c1, u.c2);
-            uint64_t prev = lat[arr][line];
-            if (prev) {
-                int src = (int)(prev & 7) - 1;
-                int64_t reuse = (int64_t)(count - (prev >> 3));
-                int kind = (u.ref == R_B0 && is_share(c, reuse)) ? 1 : 0;
-                if (hist_add(&h, src, kind, reuse, 1)) return -3;
-            }
-            lat[arr][line] = (count << 3) | (uint64_t)(u.ref + 1);
-            count++;
-            cur_step(c, &u);
-        }
-        /* cold: every line still in a LAT had no later touch (seq.cpp:305-319) */
-        for (int a = 0; a < 3; a++)
-            for (int64_t l = 0; l < nlines; l++)
-                if (lat[a][l]) { if (hist_add(&h, (int)(lat[a][l] & 7) - 1, 0, -1, 1)) return -3; }
-        total += (int64_t)count;
+    int rc = 0;
+    for (int64_t tid = 0; tid < c->T && !rc; tid++) {
+        int64_t cnt = 0;
+        rc = fulltrace_tid(c, tid, lat, nlines, &h, &cnt);
+        total += cnt;
     }
     for (int a = 0; a < 3; a++) free(lat[a]);
-    int rc = hist_export(&h, out, cap, n_out);
+    if (!rc) rc = hist_export(&h, out, cap, n_out);
+    om_free(&h);
+    if (traversed) *traversed = total;
+    return rc;
+}
+
+/* one host thread per simulated tid, as rayon_sampler runs one task per tid
+   (src/gemm_sampler_rayon.rs:107-126): thread-local LATs and histogram, merged
+   after the join.  The CPU baseline of BASELINE configs[0]. */
+typedef struct { const orc_cfg *c; int64_t tid, nlines, count; omap h; int rc; } ft_job;
+static void *ft_worker(void *p) {
+    ft_job *j = (ft_job *)p;
+    uint64_t *lat[3] = {0, 0, 0};
+    j->rc = om_init(&j->h, 64) ? -3 : 0;
+    for (int a = 0; a < 3 && !j->rc; a++) { lat[a] = (uint64_t *)malloc((size_t)j->nlines * 8); if (!lat[a]) j->rc = -3; }
+    if (!j->rc) j->rc = fulltrace_tid(j->c, j->tid, lat, j->nlines, &j->h, &j->count);
+    for (int a = 0; a < 3; a++) free(lat[a]);
+    return 0;
+}
+int orc_fulltrace_mt(const orc_cfg *c, orc_entry *out, int64_t cap, int64_t *n_out, int64_t *traversed) {
+    if (!cfg_ok(c) || c->T > 4096) return -1;
+    int64_t nlines = (c->N * c->N * c->DS) / c->CLS + 1;
+    ft_job *jb = (ft_job *)calloc((size_t)c->T, sizeof(ft_job));
+    pthread_t *th = (pthread_t *)calloc((size_t)c->T, sizeof(pthread_t));
+    if (!jb || !th) { free(jb); free(th); return -3; }
+    for (int64_t t = 0; t < c->T; t++) {
+        jb[t].c = c; jb[t].tid = t; jb[t].nlines = nlines;
+        pthread_create(&th[t], 0, ft_worker, &jb[t]);
+    }
+    omap h; int rc = om_init(&h, 64) ? -3 : 0;
+    int64_t total = 0;
+    for (int64_t t = 0; t < c->T; t++) {
+        pthread_join(th[t], 0);
+        if (jb[t].rc) rc = jb[t].rc;
+        total += jb[t].count;
+        if (!rc)
+            for (size_t i = 0; i < jb[t].h.cap; i++)
+                if (jb[t].h.k[i]) { uint64_t *sl = om_put(&h, jb[t].h.k[i]); if (!sl) rc = -3; else *sl += jb[t].h.v[i]; }
+        om_free(&jb[t].h);
+    }
+    free(jb); free(th);
+    if (!rc) rc = hist_export(&h, out, cap, n_out);
     om_free(&h);
     if (traversed) *traversed = total;
     return rc;

@@ -27,6 +27,8 @@ EXPORTS = [
     "pluss_dev_faithful_shard_starts", "pluss_dev_faithful_shard_cut", "pluss_dev_faithful_shard_hist",
     "pluss_dense_keys", "pluss_dev_sampled_hist_dense",
 ]
+# include/pluss_diag.h (diagnostics, not the drop-in boundary)
+DIAG_EXPORTS = ["pluss_diag_dense"]
 
 
 class PlussCfg(ctypes.Structure):
@@ -110,6 +112,7 @@ def lib():
         "pluss_dev_faithful_shard_hist": (ctypes.c_int, [vp, u64, u64, i32, vp]),
         "pluss_dense_keys": (ctypes.c_int, [cfgp, P(u64)]),
         "pluss_dev_sampled_hist_dense": (ctypes.c_int, [vp, vp, u64, vp, vp]),
+        "pluss_diag_dense": (ctypes.c_int, [vp, vp, u64, vp, i32, i32, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -270,6 +270,11 @@ class Context:
         check(lib().pluss_dev_sampled_hist_dense(self._h, d_samples, n, d_counts, stream),
               "pluss_dev_sampled_hist_dense")
 
+    def diag_dense(self, d_samples, n, d_counts, variant=0, max_grid=0, stream=None):
+        """Diagnostics (include/pluss_diag.h): a dense pass with an ablation variant
+        (0 product, 1 loads only, 2 no tail) and/or a workgroup cap."""
+        check(lib().pluss_diag_dense(self._h, d_samples, n, d_counts, variant, max_grid, stream), "pluss_diag_dense")
+
     # faithful mode over key-range shards: the four phases of
     # pluss_dev_faithful_shard_* (the caller exchanges the summaries; see dist.py)
     def faithful_shard_keys(self, ref, d_samples, n, key_lo, key_hi, stream=None):

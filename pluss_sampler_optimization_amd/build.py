@@ -41,7 +41,8 @@ def build(verbose=False, force=False):
     os.makedirs(OBJDIR, exist_ok=True)
     hipcc = _hipcc()
     inc = os.path.join(HERE, "..", "include")
-    common_deps = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(inc, "pluss_gpu.h"), __file__]
+    common_deps = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(inc, "pluss_gpu.h"),
+                                                              os.path.join(inc, "pluss_diag.h"), __file__]
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", inc, "-I", CSRC,
              "-Wall", "-Wno-unused-result"]
     jobs = []

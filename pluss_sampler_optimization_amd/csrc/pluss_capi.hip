@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/pluss_diag.h"
 #include "pluss_internal.h"
 
 namespace pluss {
@@ -175,17 +176,11 @@ int pluss_ctx_destroy(pluss_ctx* c) {
                   c->fb.scal, c->fb.st};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
-  auto free_bufs = [](const pluss::FaithfulBufs& f, bool core) {
-    void* fr[] = {core ? nullptr : f.keys, core ? nullptr : f.sinks, core ? nullptr : f.keys_s,
-                  core ? nullptr : f.sinks_s, core ? nullptr : f.pmax, core ? nullptr : f.nstart,
-                  core ? nullptr : f.tmp, core ? nullptr : f.scal, core ? nullptr : f.st,
-                  f.bc, f.bo, f.bm, f.bst, f.bpart};
+  for (const auto& f : c->fbr) {
+    void* fr[] = {f.keys, f.sinks, f.keys_s, f.sinks_s, f.pmax, f.nstart, f.tmp, f.scal, f.st};
     for (void* p : fr)
       if (p) (void)hipFree(p);
-  };
-  free_bufs(c->fb, true);  // its core buffers are freed above
-  for (const auto& f : c->fbr) free_bufs(f, false);
-  if (c->hmx) (void)hipHostFree(c->hmx);
+  }
   for (int r = 0; r < 6; ++r)
     if (c->fst[r]) (void)hipStreamDestroy(c->fst[r]);
   for (int e = 0; e < 7; ++e)
@@ -267,6 +262,12 @@ int pluss_dev_sampled_hist_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint
                                  void* stream) {
   if (!ctx || (!d_samples && n) || !d_counts) return PLUSS_ERR_CONFIG;
   return launch_sampled_hist_dense(ctx, d_samples, n, (unsigned long long*)d_counts, pick(ctx, stream));
+}
+
+int pluss_diag_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, uint64_t* d_counts, int32_t variant,
+                     int32_t max_grid, void* stream) {
+  if (!ctx || (!d_samples && n) || !d_counts) return PLUSS_ERR_CONFIG;
+  return launch_diag_dense(ctx, d_samples, n, (unsigned long long*)d_counts, variant, max_grid, pick(ctx, stream));
 }
 
 int pluss_faithful_key_space(const pluss_cfg* cfg, uint64_t* key_end) {

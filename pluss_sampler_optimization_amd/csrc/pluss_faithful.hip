@@ -35,7 +35,6 @@
 #include <algorithm>
 #include <cstring>
 #include <type_traits>
-#include <rocprim/block/block_radix_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
@@ -711,246 +710,16 @@ __global__ __launch_bounds__(FB) void k_faith_fused(const void* __restrict__ wor
   fused_tile<FM>(src, t, gbase, mt, pv, n, endkey, st, fu_tiles(n), part, scal);
 }
 
-// ---- bucket path (one GPU, packed words, n <= FB_NB * FB_AVG-ish): instead
-// of a device-wide radix sort, the words are distributed into nb = 2^bb
-// buckets by their top bb bits (k_fb_count: sizes and minima; k_fb_offsets:
-// offsets; k_fb_scatter: one pass writing each word into its bucket's range),
-// and k_fb_fused sorts each bucket in LDS (rocPRIM block radix sort over the
-// low sh + 1 bits; the malformed word ~0 becomes 2^sh) and runs the fused
-// scan on it: one bucket = one look-back tile, tiles in bucket order.  A
-// bucket larger than FCHUNK (a skewed list) sends the reference back to the
-// radix-sort path; the host checks the largest bucket before scattering.
-constexpr uint32_t FB_NB = 4096;    // most buckets (LDS counters of the count / scatter passes)
-constexpr uint32_t FB_AVG = 4096;   // target mean bucket size (FCHUNK = 8192 is the capacity)
-constexpr int CB = 1024, CI = 16;   // count / scatter: 1024 threads x 16 words per workgroup
-
-__device__ __forceinline__ uint32_t fb_bucket(uint64_t w, uint32_t sh, uint32_t nb) {
-  const uint64_t b = w >> sh;
-  return b < nb ? (uint32_t)b : nb - 1u;  // the malformed ~0 goes last
-}
-__device__ __forceinline__ uint32_t fb_rel(uint64_t w, uint32_t sh, bool bad) {
-  return bad ? (1u << sh) : (uint32_t)(w & ((1ull << sh) - 1ull));
-}
-
-// bc = 0, bm = ~0, look-back words 0, scal: [0] cut = n, [1] [2] [4] [5] 0
-__global__ void k_fb_init(unsigned int* bc, unsigned int* bm, uint32_t nb, unsigned long long* st,
-                          unsigned long long* scal, uint64_t n) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0) {
-    scal[0] = n;
-    scal[1] = 0;
-    scal[2] = 0;
-    scal[4] = 0;
-    scal[5] = 0;
-  }
-  for (uint32_t j = i; j < nb; j += gridDim.x * blockDim.x) {
-    bc[j] = 0;
-    bm[j] = ~0u;
-    st[2 * j] = 0;
-    st[2 * j + 1] = 0;
-  }
-}
-
-// bucket sizes and smallest (relative) words: LDS counters per workgroup, one
-// global atomic per non-empty bucket
-template <int FM>
-__global__ __launch_bounds__(CB) void k_fb_count(Model m, uint32_t ref, const uint64_t* __restrict__ smp, uint64_t n,
-                                                 uint32_t sh, uint32_t nb, unsigned int* bc, unsigned int* bm,
-                                                 GTable g) {
-  typedef fkey_t<FM> KT;
-  __shared__ unsigned int h[FB_NB], mn[FB_NB];
-  for (uint32_t b = threadIdx.x; b < nb; b += CB) {
-    h[b] = 0;
-    mn[b] = ~0u;
-  }
-  __syncthreads();
-  for (uint64_t base = (uint64_t)blockIdx.x * (CB * CI); base < n; base += (uint64_t)gridDim.x * (CB * CI)) {
-#pragma unroll 4
-    for (int j = 0; j < CI; ++j) {
-      const uint64_t i = base + (uint64_t)j * CB + threadIdx.x;
-      if (i < n) {
-        const KT w = pk_word_of<KT>(m, ref, smp[i], g);
-        const bool bad = w == (KT) ~(KT)0;
-        const uint32_t b = fb_bucket(w, sh, nb);
-        atomicAdd(&h[b], 1u);
-        atomicMin(&mn[b], fb_rel(w, sh, bad));
-      }
-    }
-  }
-  __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nb; b += CB)
-    if (h[b]) {
-      atomicAdd(&bc[b], h[b]);
-      atomicMin(&bm[b], mn[b]);
-    }
-}
-
-// exclusive offsets of the bucket sizes (one workgroup; nb <= FB_NB), the
-// scatter cursors (bc := bo) and the largest bucket (scal[5])
-__global__ __launch_bounds__(1024) void k_fb_offsets(unsigned int* bc, uint32_t nb, unsigned int* bo,
-                                                     unsigned long long* scal) {
-  constexpr int PER = FB_NB / 1024;
-  __shared__ unsigned int ws[16], wm[16];
-  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  unsigned int v[PER], sum = 0, mx = 0;
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const uint32_t b = threadIdx.x * PER + q;
-    v[q] = b < nb ? bc[b] : 0u;
-    sum += v[q];
-    mx = v[q] > mx ? v[q] : mx;
-  }
-  unsigned int inc = sum;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned int y = __shfl_up(inc, o, 64);
-    if (lane >= (uint32_t)o) inc += y;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned int y = __shfl_xor(mx, o, 64);
-    mx = y > mx ? y : mx;
-  }
-  if (lane == 63) ws[wid] = inc;
-  if (lane == 0) wm[wid] = mx;
-  __syncthreads();
-  unsigned int pre = 0, tot = 0, gmx = 0;
-  for (uint32_t x = 0; x < 16; ++x) {
-    if (x < wid) pre += ws[x];
-    tot += ws[x];
-    gmx = wm[x] > gmx ? wm[x] : gmx;
-  }
-  unsigned int off = pre + inc - sum;
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const uint32_t b = threadIdx.x * PER + q;
-    if (b < nb) {
-      bo[b] = off;
-      bc[b] = off;
-    }
-    off += v[q];
-  }
-  if (threadIdx.x == 0) {
-    bo[nb] = tot;
-    scal[5] = gmx;
-  }
-}
-
-// each workgroup: CB*CI words kept in registers, counted per bucket in LDS,
-// one global reservation per non-empty bucket, then written out
-template <int FM>
-__global__ __launch_bounds__(CB) void k_fb_scatter(Model m, uint32_t ref, const uint64_t* __restrict__ smp, uint64_t n,
-                                                   uint32_t sh, uint32_t nb, unsigned int* cur,
-                                                   void* __restrict__ out_words, GTable g) {
-  typedef fkey_t<FM> KT;  // (void* parameters: no anonymous-enum type in the kernel's mangled name)
-  KT* out = static_cast<KT*>(out_words);
-  __shared__ unsigned int h[FB_NB];
-  for (uint32_t b = threadIdx.x; b < nb; b += CB) h[b] = 0;
-  __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * (CB * CI);
-  KT w[CI];
-  uint32_t bk[CI];
-#pragma unroll
-  for (int j = 0; j < CI; ++j) {
-    const uint64_t i = base + (uint64_t)j * CB + threadIdx.x;
-    w[j] = i < n ? pk_word_of<KT>(m, ref, smp[i], g) : (KT)0;
-    bk[j] = fb_bucket(w[j], sh, nb);
-    if (i < n) atomicAdd(&h[bk[j]], 1u);
-  }
-  __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nb; b += CB)
-    if (h[b]) h[b] = atomicAdd(&cur[b], h[b]);
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < CI; ++j) {
-    const uint64_t i = base + (uint64_t)j * CB + threadIdx.x;
-    if (i < n) out[atomicAdd(&h[bk[j]], 1u)] = w[j];
-  }
-}
-
-// a bucket sorted in LDS: relative words, 2^sh = the malformed word
-template <int FM>
-struct LdsTile {
-  static constexpr bool kReload = true;
-  const unsigned int* sk;
-  fkey_t<FM> base;
-  uint32_t sh, mt;
-  unsigned long long next;  // key of the first element after the bucket
-  PkView pv;
-  __device__ fkey_t<FM> word(uint32_t li) const {
-    const unsigned int r = sk[li];
-    return r >> sh ? (fkey_t<FM>) ~(fkey_t<FM>)0 : (fkey_t<FM>)(base | (fkey_t<FM>)r);
-  }
-  __device__ unsigned long long key_after(uint32_t li) const { return li + 1 < mt ? pk_key(word(li + 1), pv) : next; }
-};
-
-// one bucket per workgroup (in arrival order, = its look-back index)
-template <int FM>
-__global__ __launch_bounds__(FB) void k_fb_fused(const void* __restrict__ words, const unsigned int* __restrict__ bo,
-                                                 const unsigned int* __restrict__ bm, uint32_t nb, uint32_t sh,
-                                                 PkView pv, uint64_t n, unsigned long long endkey,
-                                                 unsigned long long* st, unsigned long long* __restrict__ part,
-                                                 unsigned long long* scal, int abl) {
-  typedef fkey_t<FM> KT;
-  const KT* wd = static_cast<const KT*>(words);
-  typedef rocprim::block_radix_sort<unsigned int, FB, FI> Sorter;
-  __shared__ union {
-    typename Sorter::storage_type sort;
-    unsigned int sk[FCHUNK];
-  } u;
-  __shared__ unsigned long long s_tile, s_next;
-  if (threadIdx.x == 0) {
-    const uint32_t t = (uint32_t)atomicAdd(&scal[4], 1ull);
-    s_tile = t;
-    unsigned long long nx = KEY_EMPTY;  // the first word of the next non-empty bucket
-    for (uint32_t b = t + 1; b < nb; ++b)
-      if (bo[b + 1] > bo[b]) {
-        const unsigned int r = bm[b];
-        nx = r >> sh ? KEY_EMPTY : pk_key((KT)(((KT)b << sh) | (KT)r), pv);
-        break;
-      }
-    s_next = nx;
-  }
-  __syncthreads();
-  const uint32_t t = (uint32_t)s_tile;
-  const uint32_t lo = bo[t], mt = bo[t + 1] - lo;
-  const unsigned int pad = 1u << sh;
-  unsigned int kk[FI];
-#pragma unroll
-  for (int j = 0; j < FI; ++j) {  // any arrangement will do: equal values are equal words
-    const uint32_t li = (uint32_t)j * FB + threadIdx.x;
-    if (li < mt) {
-      const KT w = wd[lo + li];
-      kk[j] = fb_rel(w, sh, w == (KT) ~(KT)0);
-    } else {
-      kk[j] = pad;
-    }
-  }
-  if (mt > 1 && abl != 2) Sorter().sort(kk, u.sort, 0, sh + 1);  // abl (diagnostics, PLUSS_FB_ABL): 2 no sort
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < FI; ++j) u.sk[threadIdx.x * FI + j] = kk[j];  // blocked: thread i holds ranks i*FI ...
-  __syncthreads();
-  const LdsTile<FM> src{u.sk, (KT)((KT)t << sh), sh, mt, s_next, pv};
-  if (abl == 1) {  // diagnostics: the sort only
-    if (u.sk[threadIdx.x] == 0x5EED5EEDu) scal[6] = 1;
-    return;
-  }
-  fused_tile<FM>(src, t, lo, mt, pv, n, endkey, st, nb, part, scal);
-}
-
 // Sum the partials of the tiles that start below the cut, then what
 // k_faith_finish does (Q3, the -1 key, traversed) and the case counts.
-// bo: tile offsets (bucket path), or nullptr for FCHUNK-element tiles.
 __global__ __launch_bounds__(BLOCK) void k_faith_fused_finish(uint32_t ref, uint64_t n, PkView pv,
                                                              const unsigned long long* st, uint64_t ntiles,
-                                                             const unsigned int* bo,
                                                              const unsigned long long* part,
                                                              const unsigned long long* scal, GTable g) {
   __shared__ unsigned long long red[BLOCK / 64][FPART];
   const uint64_t cut = scal[0];
   unsigned long long v[FPART] = {0, 0, 0, 0, 0};
-  for (uint64_t t = threadIdx.x; t < ntiles && (bo ? (uint64_t)bo[t] : t * FCHUNK) < cut; t += BLOCK)
+  for (uint64_t t = threadIdx.x; t < ntiles && t * FCHUNK < cut; t += BLOCK)
 #pragma unroll
     for (int f = 0; f < FPART; ++f) v[f] += part[t * FPART + f];
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
@@ -1135,12 +904,6 @@ static int faith_reserve(pluss_ctx* ctx, FaithfulBufs& b, uint64_t n, hipStream_
   if (!b.scal) {
     if (int rc = grow(&b.scal, 8)) return rc;
   }
-  if (!b.bc) {  // the bucket path's per-bucket arrays (fixed size)
-    int rc = 0;
-    if ((rc = grow(&b.bc, FB_NB)) || (rc = grow(&b.bo, FB_NB + 1)) || (rc = grow(&b.bm, FB_NB)) ||
-        (rc = grow(&b.bst, 2 * FB_NB)) || (rc = grow(&b.bpart, (uint64_t)FB_NB * FPART)))
-      return rc;
-  }
   if (n > 0xFFFFFFFFull) {
     set_error("faithful mode: at most 2^32-1 samples per reference");
     return PLUSS_ERR_CONFIG;
@@ -1303,81 +1066,6 @@ static int faith_record(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, uint64_t n
   return PLUSS_OK;
 }
 
-// Bucket bits of the bucket path for n words of a reference, or -1 when it
-// does not apply (pair keys, more than FB_NB buckets) or is not selected.
-// sh = pk_bits - bb <= 30 keeps the in-bucket part (plus the malformed
-// marker 2^sh) in a 32-bit sort key.
-//
-// Opt-in (PLUSS_FAITH_BUCKET=1): measured on MI355X at config 2 (4,189,071
-// words per reference, 1024 buckets) it is slower than the radix-sort path,
-// 213 us vs 236 us per reference serially but 1.22 ms vs 0.93 ms for the six
-// references on their streams: k_fb_fused runs one 1024-thread workgroup per
-// CU, whose LDS sort (~100 us over the 4 rounds of tiles) and look-back waits
-// (~130 us) add up instead of overlapping (tools/fb_ablate.sh).
-static int fb_bits(const Model& m, uint64_t n) {
-  if (faith_fm(m) == FM_PAIRS) return -1;
-  const char* e = getenv("PLUSS_FAITH_BUCKET");
-  if (!e || e[0] != '1') return -1;
-  const int pb = (int)pk_bits(m);
-  int bb = 0;
-  while ((n >> bb) > FB_AVG) ++bb;
-  if (pb - bb > 30) bb = pb - 30;
-  if (bb > pb) bb = pb;
-  return bb < 31 && (1u << bb) <= FB_NB ? bb : -1;
-}
-
-// bucket path, first half: sizes, minima and offsets of the buckets; the
-// largest size goes to *hslot (pinned) once stream s has run
-static int fb_phase1(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, const uint64_t* d_samples, uint64_t n, int bb,
-                     unsigned long long* hslot, hipStream_t s) {
-  const Model& m = ctx->m;
-  const uint32_t nb = 1u << bb, sh = pk_bits(m) - (uint32_t)bb;
-  hipLaunchKernelGGL(k_fb_init, dim3((nb + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, b.bc, b.bm, nb, b.bst, b.scal, n);
-  const uint64_t chunks = (n + CB * CI - 1) / (CB * CI);
-  const unsigned grid = (unsigned)std::min<uint64_t>(chunks, 256);
-  if (faith_fm(m) == FM_PK32)
-    hipLaunchKernelGGL(k_fb_count<FM_PK32>, dim3(grid), dim3(CB), 0, s, m, (uint32_t)ref, d_samples, n, sh, nb, b.bc,
-                       b.bm, ctx->g);
-  else
-    hipLaunchKernelGGL(k_fb_count<FM_PK64>, dim3(grid), dim3(CB), 0, s, m, (uint32_t)ref, d_samples, n, sh, nb, b.bc,
-                       b.bm, ctx->g);
-  hipLaunchKernelGGL(k_fb_offsets, dim3(1), dim3(1024), 0, s, b.bc, nb, b.bo, b.scal);
-  PLUSS_HIP_CHECK(hipGetLastError());
-  PLUSS_HIP_CHECK(hipMemcpyAsync(hslot, b.scal + 5, 8, hipMemcpyDeviceToHost, s));
-  return PLUSS_OK;
-}
-
-// bucket path, second half (every bucket fits a tile): scatter, per-bucket
-// sort + fused scan, finish
-static int fb_phase2(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, const uint64_t* d_samples, uint64_t n, int bb,
-                     hipStream_t s) {
-  const Model& m = ctx->m;
-  const uint32_t nb = 1u << bb, sh = pk_bits(m) - (uint32_t)bb;
-  const unsigned chunks = (unsigned)((n + CB * CI - 1) / (CB * CI));
-  const PkView pv = make_pkview(m, (uint32_t)ref);
-  const unsigned long long endkey = m.A * m.T;
-  const char* ablv = getenv("PLUSS_FB_ABL");
-  const int abl = ablv ? atoi(ablv) : 0;
-  if (faith_fm(m) == FM_PK32) {
-    uint32_t* wd = (uint32_t*)b.keys_s;
-    hipLaunchKernelGGL(k_fb_scatter<FM_PK32>, dim3(chunks), dim3(CB), 0, s, m, (uint32_t)ref, d_samples, n, sh, nb,
-                       b.bc, wd, ctx->g);
-    hipLaunchKernelGGL(k_fb_fused<FM_PK32>, dim3(nb), dim3(FB), 0, s, wd, b.bo, b.bm, nb, sh, pv, n, endkey, b.bst,
-                       b.bpart, b.scal, abl);
-  } else {
-    unsigned long long* wd = b.keys_s;
-    hipLaunchKernelGGL(k_fb_scatter<FM_PK64>, dim3(chunks), dim3(CB), 0, s, m, (uint32_t)ref, d_samples, n, sh, nb,
-                       b.bc, wd, ctx->g);
-    hipLaunchKernelGGL(k_fb_fused<FM_PK64>, dim3(nb), dim3(FB), 0, s, wd, b.bo, b.bm, nb, sh, pv, n, endkey, b.bst,
-                       b.bpart, b.scal, abl);
-  }
-  hipLaunchKernelGGL(k_faith_fused_finish, dim3(1), dim3(BLOCK), 0, s, (uint32_t)ref, n, pv, b.bst, (uint64_t)nb,
-                     b.bo, b.bpart, b.scal, ctx->g);
-  PLUSS_HIP_CHECK(hipGetLastError());
-  ctx->tables_dirty = true;
-  return PLUSS_OK;
-}
-
 // the radix-sort pipeline of one sampler_<REF> over its buffer set, on stream s
 static int faith_pipeline_sorted(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, const uint64_t* d_samples, uint64_t n,
                                  hipStream_t s) {
@@ -1398,8 +1086,8 @@ static int faith_pipeline_sorted(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, c
     else
       hipLaunchKernelGGL(k_faith_fused<FM_PK64>, dim3((unsigned)nt), dim3(FB), 0, s, (const void*)b.keys_s, pv, n,
                          endkey, b.st, part, b.scal);
-    hipLaunchKernelGGL(k_faith_fused_finish, dim3(1), dim3(BLOCK), 0, s, (uint32_t)ref, n, pv, b.st, nt,
-                       (const unsigned int*)nullptr, part, b.scal, ctx->g);
+    hipLaunchKernelGGL(k_faith_fused_finish, dim3(1), dim3(BLOCK), 0, s, (uint32_t)ref, n, pv, b.st, nt, part,
+                       b.scal, ctx->g);
     PLUSS_HIP_CHECK(hipGetLastError());
     ctx->tables_dirty = true;
     return PLUSS_OK;
@@ -1419,37 +1107,17 @@ static int faith_pipeline_sorted(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, c
   return faith_record(ctx, b, ref, n, 0, 0, 0, n, 1, s);
 }
 
-static int faith_hslots(pluss_ctx* ctx) {
-  if (!ctx->hmx && hipHostMalloc((void**)&ctx->hmx, 8 * sizeof(unsigned long long)) != hipSuccess) {
-    ctx->hmx = nullptr;
-    set_error("hipHostMalloc failed for the faithful bucket check");
-    return PLUSS_ERR_ALLOC;
-  }
-  return PLUSS_OK;
-}
-
-// One sampler_<REF>.  Bucket path when it applies: the largest bucket is
-// read back (one stream synchronisation) to choose between the per-bucket
-// LDS sort and the device-wide radix sort.
+// One sampler_<REF>: keys, radix sort, fused scan.
 int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s) {
   if (int rc = faith_check_shape(ctx)) return rc;
   FaithfulBufs& b = ctx->fb;
   if (int rc = faith_reserve(ctx, b, n, s)) return rc;
-  const int bb = n ? fb_bits(ctx->m, n) : -1;
-  if (bb >= 0) {
-    if (int rc = faith_hslots(ctx)) return rc;
-    if (int rc = fb_phase1(ctx, b, ref, d_samples, n, bb, &ctx->hmx[0], s)) return rc;
-    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
-    if (ctx->hmx[0] <= FCHUNK) return fb_phase2(ctx, b, ref, d_samples, n, bb, s);
-  }
   return faith_pipeline_sorted(ctx, b, ref, d_samples, n, s);
 }
 
 // All six sampler_<REF> of one list at once, like r10's main, which runs
 // each on its own thread (r10:3203-3257): reference r's pipeline runs on its
 // own stream with its own buffers, forked from s and joined back into it.
-// With the bucket path the first halves run first, then one wait on their
-// bucket checks, then the second halves.
 int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t* counts, hipStream_t s) {
   if (int rc = faith_check_shape(ctx)) return rc;
   uint64_t off[6], total = 0;
@@ -1461,14 +1129,11 @@ int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64
     set_error("pluss_dev_faithful_hist_refs: null sample list");
     return PLUSS_ERR_CONFIG;
   }
-  int bb[6];
   for (int r = 0; r < 6; ++r) {  // every allocation before the fork
-    bb[r] = counts[r] ? fb_bits(ctx->m, counts[r]) : -1;
     if (!counts[r]) continue;
     if (int rc = faith_reserve(ctx, ctx->fbr[r], counts[r], s)) return rc;
     if (int rc = faith_tmp(ctx, ctx->fbr[r], counts[r], s)) return rc;
   }
-  if (int rc = faith_hslots(ctx)) return rc;
   if (!ctx->fst[0]) {
     for (int r = 0; r < 6; ++r) PLUSS_HIP_CHECK(hipStreamCreateWithFlags(&ctx->fst[r], hipStreamNonBlocking));
     for (int e = 0; e < 7; ++e) PLUSS_HIP_CHECK(hipEventCreateWithFlags(&ctx->fev[e], hipEventDisableTiming));
@@ -1477,22 +1142,7 @@ int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64
   for (int r = 0; r < 6; ++r) {
     if (!counts[r]) continue;
     PLUSS_HIP_CHECK(hipStreamWaitEvent(ctx->fst[r], ctx->fev[6], 0));
-    if (bb[r] >= 0) {
-      if (int rc = fb_phase1(ctx, ctx->fbr[r], r, d_samples + off[r], counts[r], bb[r], &ctx->hmx[r], ctx->fst[r]))
-        return rc;
-    } else if (int rc = faith_pipeline_sorted(ctx, ctx->fbr[r], r, d_samples + off[r], counts[r], ctx->fst[r])) {
-      return rc;
-    }
-  }
-  for (int r = 0; r < 6; ++r) {
-    if (!counts[r]) continue;
-    if (bb[r] >= 0) {
-      PLUSS_HIP_CHECK(hipStreamSynchronize(ctx->fst[r]));
-      const int rc = ctx->hmx[r] <= FCHUNK
-                         ? fb_phase2(ctx, ctx->fbr[r], r, d_samples + off[r], counts[r], bb[r], ctx->fst[r])
-                         : faith_pipeline_sorted(ctx, ctx->fbr[r], r, d_samples + off[r], counts[r], ctx->fst[r]);
-      if (rc) return rc;
-    }
+    if (int rc = faith_pipeline_sorted(ctx, ctx->fbr[r], r, d_samples + off[r], counts[r], ctx->fst[r])) return rc;
     PLUSS_HIP_CHECK(hipEventRecord(ctx->fev[r], ctx->fst[r]));
     PLUSS_HIP_CHECK(hipStreamWaitEvent(s, ctx->fev[r], 0));
   }

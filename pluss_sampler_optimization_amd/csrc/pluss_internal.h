@@ -17,7 +17,6 @@ constexpr uint32_t NREP = 8;           // global replica tables (one per XCD-siz
 constexpr uint32_t RCAP = 256;         // slots per replica (power of two)
 constexpr int MAX_BLOCKS = 1024;       // 256 CUs x 4 workgroups
 constexpr int UNROLL = 2;              // 16-byte sample pairs per lane per step (tools/ablate.py)
-constexpr bool HOT_NT = true;          // non-temporal sample loads: streamed once (tools/ablate.py, r01k)
 constexpr unsigned long long KEY_NONE = 0;  // free table slot (histogram keys are never 0)
 
 constexpr uint32_t NBROW = 64;         // rows of direct (ref, case) counters (workgroup -> row blockIdx % 64)
@@ -29,7 +28,7 @@ constexpr uint32_t BARRIVE = 31;
 // (arrivals << DARR_SHIFT | count) so the last adder of a word knows its total
 // from the value its add returned.  dbins: NBROW rows, dtot: one row.
 constexpr uint32_t DBINS = 19;
-constexpr uint32_t DENSE_ROWS = 32;  // first-level rows of the dense tail (tools/ablate.py, PLUSS_DROWS)
+constexpr uint32_t DENSE_ROWS = 32;  // first-level rows of the dense tail (r02 sweep of 1..64 rows, tools/ablate.py)
 constexpr int DARR_SHIFT = 44;
 constexpr unsigned long long DCNT_MASK = (1ull << DARR_SHIFT) - 1;
 
@@ -64,11 +63,6 @@ struct FaithfulBufs {
   size_t tmp_bytes = 0;
   unsigned long long* scal = nullptr;  // [0] cut, [1] cold, [2] traversed, [3] shard size, [4] scan tile counter
   unsigned long long* st = nullptr;    // look-back status words of the one-GPU scan (2 per tile)
-  // bucket path (pluss_faithful.hip, one GPU, packed words): per bucket the
-  // count (then the scatter cursor), the offset (nb + 1), the smallest word
-  // (relative to the bucket base), look-back words (2 per bucket), partials
-  unsigned int *bc = nullptr, *bo = nullptr, *bm = nullptr;
-  unsigned long long *bst = nullptr, *bpart = nullptr;
 };
 
 // state of a key-range shard between the phases of pluss_dev_faithful_shard_*
@@ -95,7 +89,6 @@ struct pluss_ctx {
   pluss::FaithfulBufs fbr[6];  // per-reference buffers of pluss_dev_faithful_hist_refs
   hipStream_t fst[6];          // ... and its streams (created on first use)
   hipEvent_t fev[7];           // fork / join events
-  unsigned long long* hmx;     // pinned: largest bucket per reference (faithful bucket path)
   hipStream_t last;   // stream of the most recent launch (fetch orders after it)
   bool tables_dirty;  // hash tables may hold counts (GENERIC / faithful launches since the last reset)
 };
@@ -132,6 +125,9 @@ int launch_sampled_hist_export(pluss_ctx* ctx, const uint64_t* d_samples, uint64
 // count a sample list into a caller-owned dense vector of DBINS counts (FAST shapes), one launch
 int launch_sampled_hist_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, unsigned long long* d_counts,
                               hipStream_t s);
+// diagnostics (include/pluss_diag.h): a dense pass with an ablation variant and/or a workgroup cap
+int launch_diag_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, unsigned long long* d_counts,
+                      int variant, int max_grid, hipStream_t s);
 int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s);
 int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t* counts, hipStream_t s);
 int faith_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, uint64_t lo, uint64_t hi,

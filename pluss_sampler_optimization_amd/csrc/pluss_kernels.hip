@@ -1,13 +1,16 @@
 // pluss_kernels.hip — gfx950 kernels of the PLUSS reuse-interval hot path.
 //
-//   k_sampled_hist  (HOT)  one lane per sampled access: decode the packed
-//                   sample, jump to its next same-line touch on the simulated
-//                   static schedule (pluss_model.h), and count the exact
-//                   (ref, noshare/share, RI) key (pluss_device.h: wave ballot
-//                   -> scalar cache -> LDS table -> replica table).  Replaces
-//                   the replay loop of r10 sampler_<REF> (r10:275-654) and
+//   k_count         (HOT, N % W == 0: every BASELINE shape) one pass over the
+//                   packed sample list: each sample's (ref, case) is decided
+//                   by 0-3 integer tests (pluss_model.h, case_fast) and counted
+//                   by wave ballots / per-lane counters; one of three tails
+//                   (accumulate, fused export, dense vector).  Replaces the
+//                   replay loop of r10 sampler_<REF> (r10:275-654) and
 //                   pluss_parallel_histogram_update (pluss_utils.h:726-729).
-//   k_fulltrace     every access of the nest, indices generated in-kernel (no
+//   k_sampled_hist  the same for other shapes: exact RIs by line-element
+//                   enumeration, keys through the wave cache (pluss_device.h).
+//   k_fulltrace_count / k_fulltrace
+//                   every access of the nest, indices generated in-kernel (no
 //                   HBM input); replaces seq.cpp:37-333 / rayon.rs:186-378.
 //   k_export        folds the replicas into a canonical sorted table.
 //   k_ri_dump       per-sample (RI, sink key) parity dump.
@@ -15,158 +18,92 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 
 #include "pluss_device.h"
 
 namespace pluss {
 
-// Kernel variants: GENERIC (any shape: line-element enumeration), FAST
-// (N % W == 0: case index + key table), FAST_P2 (also W, CS powers of two).
-enum : int { GENERIC = 0, FAST = 1, FAST_P2 = 2 };
-
-template <int MODE>
-__device__ __forceinline__ uint64_t key_of(const Model& m, const unsigned long long* ktab, uint32_t ref, uint32_t c0,
-                                           uint32_t c1, uint32_t c2) {
-  if (MODE == GENERIC) {
-    const int64_t ri = ri_generic(m, ref, c0, c1, c2);
-    return make_key(ref, share_kind(m, ref, ri), ri);
-  }
-  return ktab[ref * 3 + case_fast<MODE == FAST_P2>(m, ref, c0, c1, c2)];
+// Exact key of an access on any shape (line-element enumeration).
+__device__ __forceinline__ uint64_t key_generic(const Model& m, uint32_t ref, uint32_t c0, uint32_t c1, uint32_t c2) {
+  const int64_t ri = ri_generic(m, ref, c0, c1, c2);
+  return make_key(ref, share_kind(m, ref, ri), ri);
 }
 
-template <int MODE>
-__device__ __forceinline__ uint64_t sample_key(const Model& m, const unsigned long long* ktab, uint64_t x, bool* bad) {
+__device__ __forceinline__ uint64_t sample_key(const Model& m, uint64_t x, bool* bad) {
   const Sample s = unpack(x);
   const bool b = s.ref > 5 || s.c0 >= m.N || s.c1 >= m.N || s.c2 >= m.N;
   *bad = b;
-  if (MODE == GENERIC && b) return KEY_NONE;  // the generic rules loop over line elements: skip bad input
-  // fast paths: evaluate branch-free on clamped fields, the caller masks bad lanes
-  return key_of<MODE>(m, ktab, s.ref > 5 ? 5u : s.ref, s.c0, s.c1, s.c2);
+  if (b) return KEY_NONE;  // the generic rules loop over line elements: skip bad input
+  return key_generic(m, s.ref, s.c0, s.c1, s.c2);
 }
 
-__device__ __forceinline__ void ktab_init(const Model& m, unsigned long long* ktab) {
-  if (threadIdx.x < 18) ktab[threadIdx.x] = m.keytab[threadIdx.x];
-}
+// ------------------------------------------------------- GENERIC shapes --
+// k_sampled_hist: shapes with N % W != 0, where a line can span two rows and
+// a sample's RI is not one of a few closed forms.  One lane per sampled
+// access: exact RI by line-element enumeration (ri_generic), keys counted
+// through the wave-aggregated cache path (pluss_device.h).  Grid-stride over
+// 16-byte sample pairs, UNROLL pairs per lane per step, the next step's loads
+// issued before the current step's samples are counted.
+constexpr int BIN_BAD = 18;  // dense vector slot of the malformed-sample count
 
-// ------------------------------------------------------------------ HOT --
-// Grid-stride over 16-byte sample pairs, UNR pairs per lane per step, the
-// next step's loads issued before the current step's samples are counted.
-//
-// FAST / FAST_P2 (N % W == 0): a sample's key is one of 18 (ref, case) keys
-// (Model::keytab), so counting is one conflict-free `ds_add_u32` into the
-// lane's own LDS counter for that bin (bank = lane); the block reduces its
-// counters once at the end.  GENERIC: arbitrary exact keys, counted through
-// the wave-aggregated cache path (pluss_device.h).
-constexpr int NBINS = 20;  // 18 (ref, case) bins + 1 malformed-sample bin + 1 masked-lane bin
-constexpr int BIN_BAD = 18, BIN_OFF = 19;
+__global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t* __restrict__ smp, uint64_t n,
+                                                        const uint64_t* __restrict__ head, int has_head, GTable g) {
+  __shared__ unsigned long long tk[TCAP];
+  __shared__ unsigned int tc[TCAP];
+  const BlockTable bt{tk, tc};
+  WaveCache wc;
+  bt_init(bt);
+  wc_init(wc);
+  __syncthreads();
 
-// Per-sample bin for any mix of references (selects only).
-template <bool P2>
-__device__ __forceinline__ uint32_t sample_bin_any(const Model& m, uint64_t x, bool ok) {
-  const Sample s = unpack(x);
-  const bool bad = s.ref > 5 || s.c0 >= m.N || s.c1 >= m.N || s.c2 >= m.N;
-  const uint32_t ref = s.ref > 5 ? 5u : s.ref;
-  const uint32_t bin = ref * 3 + case_fast<P2>(m, ref, s.c0, s.c1, s.c2);
-  return ok ? (bad ? (uint32_t)BIN_BAD : bin) : (uint32_t)BIN_OFF;
-}
-
-// Per-sample bin when every active lane holds the same reference `ref`
-// (wave-uniform, so the rule is chosen by a scalar branch and only the
-// compares that reference needs are evaluated).
-// (ref, case) bin of an access whose reference is wave-uniform.
-template <bool P2>
-__device__ __forceinline__ uint32_t bin_uniform(const Model& m, uint32_t ref, uint32_t c0, uint32_t c1, uint32_t c2) {
-  const uint32_t Wm1 = m.W - 1;
-  uint32_t cs = 0;
-  if (ref == C3) {
-    const bool c1last = (P2 ? (c1 & m.wmask) : fmod_(c1, m.dW)) == Wm1;
-    cs = (c2 + 1 < m.N) ? 0u : (c1last ? 2u : 1u);
-  } else if (ref == A0) {
-    const bool c2last = (P2 ? (c2 & m.wmask) : fmod_(c2, m.dW)) == Wm1;
-    cs = !c2last ? 0u : (c1 + 1 < m.N ? 1u : 2u);
-  } else if (ref == B0) {
-    const bool c1last = (P2 ? (c1 & m.wmask) : fmod_(c1, m.dW)) == Wm1;
-    const uint32_t p = P2 ? (c0 & m.csmask) : fmod_(c0, m.dCS);
-    const uint32_t nxt = c0 + 1 + (p + 1 == m.CS ? (m.T - 1) * m.CS : 0u);
-    cs = !c1last ? 0u : (nxt < m.N ? 1u : 2u);
-  }
-  return ref * 3 + cs;
-}
-
-template <bool P2>
-__device__ __forceinline__ uint32_t sample_bin_ref(const Model& m, uint32_t ref, uint64_t x, bool ok) {
-  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-  const uint32_t c2 = lo & 0xFFFFFu;
-  const uint32_t c1 = __builtin_amdgcn_alignbit(hi, lo, 20) & 0xFFFFFu;
-  const uint32_t c0 = (hi >> 8) & 0xFFFFFu;
-  const uint32_t mx = c0 > c1 ? (c0 > c2 ? c0 : c2) : (c1 > c2 ? c1 : c2);
-  const bool bad = mx >= m.N;
-  const uint32_t bin = bin_uniform<P2>(m, ref, c0, c1, c2);
-  return ok ? (bad ? (uint32_t)BIN_BAD : bin) : (uint32_t)BIN_OFF;
-}
-
-template <bool P2>
-__device__ __forceinline__ uint32_t sample_bin(const Model& m, uint64_t x, bool ok) {
-  const uint32_t r = (uint32_t)(x >> 60);
-  const uint32_t r0 = __builtin_amdgcn_readfirstlane(r);
-  if (r0 <= 5 && __ballot(ok && r != r0) == 0) {
-    switch (r0) {  // scalar branch on the wave's reference
-      case C3: return sample_bin_ref<P2>(m, C3, x, ok);
-      case A0: return sample_bin_ref<P2>(m, A0, x, ok);
-      case B0: return sample_bin_ref<P2>(m, B0, x, ok);
-      default: return sample_bin_ref<P2>(m, r0, x, ok);  // C0, C1, C2: case 0
+  const uint64_t npairs = n >> 1;
+  const ulonglong2* __restrict__ v = reinterpret_cast<const ulonglong2*>(smp);
+  const uint64_t step = (uint64_t)gridDim.x * BLOCK * UNROLL;
+  bool anybad = false;
+  uint64_t base = (uint64_t)blockIdx.x * BLOCK * UNROLL;
+  const uint64_t last = npairs ? npairs - 1 : 0;  // loads are clamped, lanes past the end are masked
+  ulonglong2 x[UNROLL];
+  if (npairs) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint64_t i = base + (uint64_t)u * BLOCK + threadIdx.x;
+      x[u] = v[i < last ? i : last];
     }
   }
-  return sample_bin_any<P2>(m, x, ok);
-}
-
-// Bins of the K samples a lane holds in one step.  The reference check and
-// the scalar branch are paid once for all K (a wave almost always holds one
-// reference: lists are per-reference blocks); a mixed step falls back to the
-// all-reference select chain.
-template <bool P2, int K>
-__device__ __forceinline__ void sample_bins(const Model& m, const uint64_t (&xs)[K], const bool (&ok)[K],
-                                            uint32_t (&bin)[K]) {
-  const uint32_t r0 = __builtin_amdgcn_readfirstlane((uint32_t)(xs[0] >> 60));
-  bool mixed = false;
+  for (; base < npairs; base += step) {
+    ulonglong2 y[UNROLL];
+    const uint64_t nb = base + step;
 #pragma unroll
-  for (int k = 0; k < K; ++k) mixed |= ok[k] && (uint32_t)(xs[k] >> 60) != r0;
-  if (r0 <= 5 && __ballot(mixed) == 0) {
-    switch (r0) {  // scalar branch on the wave's reference
-#define PLUSS_BIN_CASE(R)                                                              \
-  case R:                                                                              \
-    _Pragma("unroll") for (int k = 0; k < K; ++k) bin[k] = sample_bin_ref<P2>(m, R, xs[k], ok[k]); \
-    return;
-      PLUSS_BIN_CASE(C3)
-      PLUSS_BIN_CASE(A0)
-      PLUSS_BIN_CASE(B0)
-#undef PLUSS_BIN_CASE
-      default:  // C0, C1, C2: case 0
-#pragma unroll
-        for (int k = 0; k < K; ++k) bin[k] = sample_bin_ref<P2>(m, r0, xs[k], ok[k]);
-        return;
+    for (int u = 0; u < UNROLL; ++u) {  // prefetch the next step
+      const uint64_t i = nb + (uint64_t)u * BLOCK + threadIdx.x;
+      y[u] = v[i < last ? i : last];
     }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const bool ok = base + (uint64_t)u * BLOCK + threadIdx.x < npairs;
+      bool b0, b1;
+      const uint64_t k0 = sample_key(m, x[u].x, &b0);
+      const uint64_t k1 = sample_key(m, x[u].y, &b1);
+      anybad |= ok && (b0 || b1);
+      wave_count(wc, bt, g, k0, ok && !b0);
+      wave_count(wc, bt, g, k1, ok && !b1);
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) x[u] = y[u];
   }
-#pragma unroll
-  for (int k = 0; k < K; ++k) bin[k] = sample_bin_any<P2>(m, xs[k], ok[k]);
-}
-
-// Workgroup totals of the DBINS bins (18 (ref, case) bins + malformed) from
-// the per-lane LDS counters of k_sampled_hist.
-template <int PCS>
-__device__ __forceinline__ void reduce_lane_counters(unsigned int (*pc)[NBINS][64], unsigned long long* tot) {
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int b = wave; b < (int)DBINS; b += BLOCK / 64) {
-    unsigned long long v = 0;
-#pragma unroll
-    for (int w = 0; w < PCS; ++w) v += pc[w][b][lane];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) tot[b] = v;
+  if (((n & 1) || has_head) && blockIdx.x == 0 && threadIdx.x < 64) {
+    // odd tail (lane 0) and, for an 8-byte-aligned list, its first sample (lane 1).
+    // `head` always points at valid memory, so a speculated load cannot fault.
+    const bool mine = (threadIdx.x == 0 && (n & 1)) || (threadIdx.x == 1 && has_head);
+    const uint64_t* src = (threadIdx.x == 0 && n) ? smp + (n - 1) : head;
+    const uint64_t xs = mine ? *src : 0;
+    bool b = false;
+    const uint64_t k = mine ? sample_key(m, xs, &b) : KEY_NONE;
+    anybad |= mine && b;
+    wave_count(wc, bt, g, k, mine && !b);
   }
-  __syncthreads();
+  if (anybad) atomicOr(&g.flags[1], 1u);
+  bt_finish(wc, bt, g);
 }
 
 // Accumulating tail: each bin with a count is added to its direct counter in
@@ -351,146 +288,8 @@ __device__ __forceinline__ void tail_export(const Model& m, GTable g, const Expo
   if (amlast) bins_export_tail(m, g, ex.keys, ex.counts, ex.cap, ex.nout);
 }
 
-// PCS: sets of lane counters per workgroup (waves share a set: ds_add is
-// atomic and a wave's 64 lanes still hit 64 distinct banks), so LDS per
-// workgroup is PCS * 5 KiB.
-template <int MODE, int ABL = 0, int UNR = UNROLL, bool NT = false, int TAIL = TAIL_NONE, int PCS = 1>
-__global__ __launch_bounds__(BLOCK) void k_sampled_hist(Model m, const uint64_t* __restrict__ smp, uint64_t n,
-                                                        const uint64_t* __restrict__ head, int has_head, GTable g,
-                                                        ExportArgs ex) {
-  static_assert(TAIL == TAIL_NONE || MODE != GENERIC, "fused export and dense output need the direct bins");
-  constexpr bool BINS = MODE != GENERIC;
-  __shared__ unsigned long long tk[BINS ? 1 : TCAP];
-  __shared__ unsigned int tc[BINS ? 1 : TCAP];
-  __shared__ unsigned int pc[BINS ? PCS : 1][NBINS][64];
-  const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) % PCS;
-  const BlockTable bt{tk, tc};
-  WaveCache wc;
-  if (BINS) {
-    for (int i = threadIdx.x; i < PCS * NBINS * 64; i += BLOCK) (&pc[0][0][0])[i] = 0;
-  } else {
-    bt_init(bt);
-    wc_init(wc);
-  }
-  __syncthreads();
-
-  const uint64_t npairs = n >> 1;
-  const ulonglong2* __restrict__ v = reinterpret_cast<const ulonglong2*>(smp);
-  const uint64_t step = (uint64_t)gridDim.x * BLOCK * UNR;
-  bool anybad = false;
-  uint64_t sink = 0;
-  uint64_t base = (uint64_t)blockIdx.x * BLOCK * UNR;
-  const uint64_t last = npairs ? npairs - 1 : 0;  // loads are clamped, lanes past the end are masked
-  auto ld = [&](uint64_t i) -> ulonglong2 {
-    if (NT) {  // streamed once: non-temporal hint
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(v + i));
-      return ulonglong2{((unsigned long long)q.y << 32) | q.x, ((unsigned long long)q.w << 32) | q.z};
-    }
-    return v[i];
-  };
-  ulonglong2 x[UNR];
-  if (npairs) {
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const uint64_t i = base + (uint64_t)u * BLOCK + threadIdx.x;
-      x[u] = ld(i < last ? i : last);
-    }
-  }
-  for (; base < npairs; base += step) {
-    ulonglong2 y[UNR];
-    const uint64_t nb = base + step;
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {  // prefetch the next step
-      const uint64_t i = nb + (uint64_t)u * BLOCK + threadIdx.x;
-      y[u] = ld(i < last ? i : last);
-    }
-    if (BINS && ABL != 2) {  // all 2*UNR samples of the step binned under one reference check
-      uint64_t xs[2 * UNR];
-      bool oks[2 * UNR];
-      uint32_t bin[2 * UNR];
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        xs[2 * u] = x[u].x;
-        xs[2 * u + 1] = x[u].y;
-        oks[2 * u] = oks[2 * u + 1] = base + (uint64_t)u * BLOCK + threadIdx.x < npairs;
-      }
-      sample_bins<MODE == FAST_P2>(m, xs, oks, bin);
-#pragma unroll
-      for (int k = 0; k < 2 * UNR; ++k) {
-        if (ABL == 1) sink += bin[k] << (k & 7);
-        else atomicAdd(&pc[wave][bin[k]][lane], 1u);
-      }
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) x[u] = y[u];
-      continue;
-    }
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const bool ok = base + (uint64_t)u * BLOCK + threadIdx.x < npairs;
-      if (ABL == 2) {
-        sink ^= ok ? (x[u].x ^ x[u].y) : 0;
-        continue;
-      }
-      if (BINS) {
-        const uint32_t b0 = sample_bin<MODE == FAST_P2>(m, x[u].x, ok);
-        const uint32_t b1 = sample_bin<MODE == FAST_P2>(m, x[u].y, ok);
-        if (ABL == 1) {
-          sink += b0 ^ (b1 << 5);
-          continue;
-        }
-        atomicAdd(&pc[wave][b0][lane], 1u);
-        atomicAdd(&pc[wave][b1][lane], 1u);
-      } else {
-        bool b0, b1;
-        const uint64_t k0 = sample_key<MODE>(m, nullptr, x[u].x, &b0);
-        const uint64_t k1 = sample_key<MODE>(m, nullptr, x[u].y, &b1);
-        anybad |= ok && (b0 || b1);
-        if (ABL == 1) {
-          sink += ok ? (k0 ^ k1) : 0;
-          continue;
-        }
-        wave_count(wc, bt, g, k0, ok && !b0);
-        wave_count(wc, bt, g, k1, ok && !b1);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) x[u] = y[u];
-  }
-  if (((n & 1) || has_head) && blockIdx.x == 0 && threadIdx.x < 64) {
-    // odd tail (lane 0) and, for an 8-byte-aligned list, its first sample (lane 1).
-    // `head` always points at valid memory, so a speculated load cannot fault.
-    const bool mine = (threadIdx.x == 0 && (n & 1)) || (threadIdx.x == 1 && has_head);
-    const uint64_t* src = (threadIdx.x == 0 && n) ? smp + (n - 1) : head;
-    const uint64_t xs = mine ? *src : 0;
-    if (BINS) {
-      const uint32_t bin = sample_bin_any<MODE == FAST_P2>(m, xs, mine);
-      if (ABL == 0) atomicAdd(&pc[0][bin][lane], 1u);
-    } else {
-      bool b = false;
-      const uint64_t k = mine ? sample_key<MODE>(m, nullptr, xs, &b) : KEY_NONE;
-      anybad |= mine && b;
-      if (ABL == 0) wave_count(wc, bt, g, k, mine && !b);
-    }
-  }
-  if (anybad) atomicOr(&g.flags[1], 1u);
-  if (ABL) {
-    if (sink == 0x5EED5EED5EED5EEDull) atomicOr(&g.flags[2], 1u);  // keeps the ablated work alive
-    return;
-  }
-  if (BINS) {
-    __shared__ unsigned long long tot[DBINS];
-    reduce_lane_counters<PCS>(pc, tot);
-    if (TAIL == TAIL_DENSE) tail_dense(tot, g, ex.dense, ex.drows);
-    else tail_accumulate(tot, g);
-  } else {
-    bt_finish(wc, bt, g);
-  }
-  if (TAIL == TAIL_EXPORT) tail_export(m, g, ex);
-}
-
 // --------------------------------------------------- HOT (FAST shapes) --
-// k_count: the same pass as k_sampled_hist's FAST path, counted by ballots.
+// k_count: the sampled pass for N % W == 0 shapes (every BASELINE shape).
 // A "slot" is one sample per lane (64 per wave).  The wave finds the
 // references present in the slot (almost always one: lists are per-reference
 // blocks), and for each one evaluates only that reference's case conditions
@@ -773,25 +572,22 @@ __device__ __forceinline__ void flush_counts(uint32_t& acc, unsigned long long* 
   acc = 0;
 }
 
-// ABL (diagnostics, tools/ablate.py): 0 product; 1 loads only (PLUSS_ABLATE=3); 2 count without the tail (=4)
-// XAUX >= 0 (diagnostics, PLUSS_AUX): that cache-policy immediate for the sample loads instead of NT's
-// LANES: full uniform steps counted by count_step_lanes (P2 && NP2 shapes); false = ballots only (PLUSS_LANES=0)
-// PREF: steps of sample loads in flight ahead of the step being counted (PLUSS_PREF=2: two)
-template <bool P2, bool NP2, bool NT, int TAIL, int UNR = UNROLL, int ABL = 0, int BS = BLOCK, int XAUX = -1,
-          bool LANES = true, int PREF = 1>
-__global__ __launch_bounds__(BS) void k_count(Model m, const uint64_t* __restrict__ smp, uint64_t n,
-                                              const uint64_t* __restrict__ head, int has_head, GTable g,
-                                              ExportArgs ex) {
-  static_assert(BS == BLOCK || TAIL != TAIL_EXPORT, "the export tail assumes BLOCK threads");
+// ABL: 0 = the product kernel; diagnostics only (pluss_diag_dense, include/pluss_diag.h):
+// 1 = the same loads, nothing counted; 2 = counted, no tail (nothing written).
+// Sample loads are non-temporal (aux 2): the list is streamed once per pass.
+template <bool P2, bool NP2, int TAIL, int ABL = 0>
+__global__ __launch_bounds__(BLOCK) void k_count(Model m, const uint64_t* __restrict__ smp, uint64_t n,
+                                                 const uint64_t* __restrict__ head, int has_head, GTable g,
+                                                 ExportArgs ex) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  constexpr int UNR = UNROLL, AUX = 2;
   __shared__ unsigned long long tot[DBINS];
   if (threadIdx.x < DBINS) tot[threadIdx.x] = 0;  // the barrier before the first flush orders this
   uint32_t acc = 0;  // lane b: count of bin b
   LaneCounts lc;     // the vector fast path's counters (count_step_lanes)
   lc_init(lc);
   const uint64_t npairs = n >> 1;
-  const uint32_t step = gridDim.x * (uint32_t)(BS * UNR);
-  constexpr int AUX = XAUX >= 0 ? XAUX : (NT ? 2 : 0);  // nt: the list is streamed once per pass
+  const uint32_t step = gridDim.x * (uint32_t)(BLOCK * UNR);
   for (uint64_t w0 = 0; w0 < npairs; w0 += CWIN) {
     const uint32_t wn = (uint32_t)(npairs - w0 < CWIN ? npairs - w0 : CWIN);
     const uint64_t* wp = smp + 2 * w0;
@@ -799,45 +595,39 @@ __global__ __launch_bounds__(BS) void k_count(Model m, const uint64_t* __restric
     const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)wp >> 32));
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(((uintptr_t)phi << 32) | plo), 0, (int)__builtin_amdgcn_readfirstlane(wn * 16u), 0x00020000);
-    uint32_t base = blockIdx.x * (uint32_t)(BS * UNR);
-    u32x4 x[PREF][UNR];  // x[0]: this step's pairs; x[j]: step j ahead
+    uint32_t base = blockIdx.x * (uint32_t)(BLOCK * UNR);
+    u32x4 x[UNR];  // this step's pairs
 #pragma unroll
-    for (int j = 0; j < PREF; ++j)
-#pragma unroll
-      for (int u = 0; u < UNR; ++u)
-        x[j][u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                rs, (int)((base + j * step + u * BS + threadIdx.x) * 16u), 0, AUX));
+    for (int u = 0; u < UNR; ++u)
+      x[u] = __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((base + u * BLOCK + threadIdx.x) * 16u), 0, AUX));
     for (; base < wn; base += step) {
       u32x4 y[UNR];
 #pragma unroll
-      for (int u = 0; u < UNR; ++u)  // the pairs PREF steps ahead (past the window: zeros)
+      for (int u = 0; u < UNR; ++u)  // the next step's pairs (past the window: zeros)
         y[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             rs, (int)((base + PREF * step + u * BS + threadIdx.x) * 16u), 0, AUX));
+                                             rs, (int)((base + step + u * BLOCK + threadIdx.x) * 16u), 0, AUX));
       uint32_t lo[2 * UNR], hi[2 * UNR];
       uint64_t okm[UNR];
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        lo[2 * u] = x[0][u].x;
-        hi[2 * u] = x[0][u].y;
-        lo[2 * u + 1] = x[0][u].z;
-        hi[2 * u + 1] = x[0][u].w;
-        okm[u] = __ballot(base + u * BS + threadIdx.x < wn);
+        lo[2 * u] = x[u].x;
+        hi[2 * u] = x[u].y;
+        lo[2 * u + 1] = x[u].z;
+        hi[2 * u + 1] = x[u].w;
+        okm[u] = __ballot(base + u * BLOCK + threadIdx.x < wn);
       }
       if (ABL == 1) {  // diagnostics: the same loads, nothing counted
 #pragma unroll
         for (int k = 0; k < 2 * UNR; ++k) acc ^= lo[k] ^ hi[k];
-      } else if (!(P2 && NP2 && LANES && base + (uint32_t)(UNR * BS) <= wn && count_step_lanes<UNR>(m, lo, hi, lc))) {
+      } else if (!(P2 && NP2 && base + (uint32_t)(UNR * BLOCK) <= wn && count_step_lanes<UNR>(m, lo, hi, lc))) {
         count_step<P2, NP2, UNR>(m, lo, hi, okm, acc);
       }
 #pragma unroll
-      for (int j = 0; j + 1 < PREF; ++j)
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) x[j][u] = x[j + 1][u];
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) x[PREF - 1][u] = y[u];
+      for (int u = 0; u < UNR; ++u) x[u] = y[u];
     }
     if (ABL != 1) {  // per window: keeps the 32-bit lane counters from overflowing
-      if (P2 && NP2 && LANES) lc_flush(lc, acc);
+      if (P2 && NP2) lc_flush(lc, acc);
       __syncthreads();
       flush_counts(acc, tot);
     }
@@ -862,66 +652,40 @@ __global__ __launch_bounds__(BS) void k_count(Model m, const uint64_t* __restric
 }
 
 // ----------------------------------------------------------- full trace --
-// One wave per (c0, c1) pair: C0, C1, then the c2 loop 64 iterations at a time;
-// the reference is uniform in each inner step.  FAST modes count into the
-// lane-private LDS bins (one ds_add per access), GENERIC through the key cache.
-template <int MODE>
+// GENERIC shapes (N % W != 0): one wave per (c0, c1) pair: C0, C1, then the
+// c2 loop 64 iterations at a time, exact keys through the wave cache.
 __global__ __launch_bounds__(BLOCK) void k_fulltrace(Model m, GTable g) {
-  constexpr bool BINS = MODE != GENERIC;
-  __shared__ unsigned long long tk[BINS ? 1 : TCAP];
-  __shared__ unsigned int tc[BINS ? 1 : TCAP];
-  __shared__ unsigned int pc[BINS ? 1 : 1][NBINS][64];  // one counter set shared by the waves
+  __shared__ unsigned long long tk[TCAP];
+  __shared__ unsigned int tc[TCAP];
   const BlockTable bt{tk, tc};
   WaveCache wc;
-  const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6, cw = 0;
-  if (BINS) {
-    for (int i = threadIdx.x; i < NBINS * 64; i += BLOCK) (&pc[0][0][0])[i] = 0;
-  } else {
-    bt_init(bt);
-    wc_init(wc);
-  }
+  const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
+  bt_init(bt);
+  wc_init(wc);
   __syncthreads();
   const uint64_t nwaves = (uint64_t)gridDim.x * (BLOCK / 64);
   const uint64_t npairs = (uint64_t)m.N * m.N;
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g.trav[0], npairs * m.S);  // accesses traversed
   for (uint64_t pr = (uint64_t)blockIdx.x * (BLOCK / 64) + wave; pr < npairs; pr += nwaves) {
     const uint32_t c0 = (uint32_t)(pr / m.N), c1 = (uint32_t)(pr - (uint64_t)c0 * m.N);
-    if (BINS) {
-      if (lane < 2) atomicAdd(&pc[cw][lane * 3][lane], 1u);  // C0, C1: case 0
-      for (uint32_t c2b = 0; c2b < m.N; c2b += 64) {
-        const uint32_t c2 = c2b + lane;
-        if (c2 < m.N) {
+    {
+      const bool v = lane < 2;
+      uint64_t key = KEY_NONE;
+      if (v) key = key_generic(m, lane, c0, c1, 0);
+      wave_count(wc, bt, g, key, v);
+    }
+    for (uint32_t c2b = 0; c2b < m.N; c2b += 64) {
+      const uint32_t c2 = c2b + lane;
+      const bool v = c2 < m.N;
 #pragma unroll
-          for (uint32_t ref = A0; ref <= C3; ++ref)
-            atomicAdd(&pc[cw][bin_uniform<MODE == FAST_P2>(m, ref, c0, c1, c2)][lane], 1u);
-        }
-      }
-    } else {
-      {
-        const bool v = lane < 2;
+      for (uint32_t ref = A0; ref <= C3; ++ref) {
         uint64_t key = KEY_NONE;
-        if (v) key = key_of<MODE>(m, nullptr, lane, c0, c1, 0);
+        if (v) key = key_generic(m, ref, c0, c1, c2);
         wave_count(wc, bt, g, key, v);
-      }
-      for (uint32_t c2b = 0; c2b < m.N; c2b += 64) {
-        const uint32_t c2 = c2b + lane;
-        const bool v = c2 < m.N;
-#pragma unroll
-        for (uint32_t ref = A0; ref <= C3; ++ref) {
-          uint64_t key = KEY_NONE;
-          if (v) key = key_of<MODE>(m, nullptr, ref, c0, c1, c2);
-          wave_count(wc, bt, g, key, v);
-        }
       }
     }
   }
-  if (BINS) {
-    __shared__ unsigned long long tot[DBINS];
-    reduce_lane_counters<1>(pc, tot);
-    tail_accumulate(tot, g);
-  } else {
-    bt_finish(wc, bt, g);
-  }
+  bt_finish(wc, bt, g);
 }
 
 // Full trace for N % W == 0 shapes, counted by ballots.  One wave per
@@ -1141,10 +905,24 @@ int launch_table_reset(pluss_ctx* ctx, hipStream_t s) {
   return PLUSS_OK;
 }
 
+// Workgroups of a dense pass (k_count, TAIL_DENSE, the bench step).  Lists
+// past the Infinity Cache stream from HBM, where fewer resident waves per CU
+// queue fewer requests on the same channels.  Measured on MI355X with
+// tools/grid_sweep.py (profiles/r05_grid_sweep.jsonl, N=1024 lists, median
+// of 5): 1024 workgroups at 2^24 samples (20.73 us; 768: 20.78); 768 at 2^25
+// (39.23 us; 1024: 39.54, 640: 39.48) and 2^26 (75.7 us; 1024: 77.1); 640 at
+// 2^27 (149.2 us; 768: 150.0) and 2^28 (296.2 us; 768: 299.1).  The other
+// tails keep MAX_BLOCKS (not swept).
+static int dense_grid_cap(uint64_t n) {
+  return n >= (1ull << 27) ? 640 : n >= (1ull << 25) ? 768 : MAX_BLOCKS;
+}
+
 // `fuse` != null: FAST shapes only, the launch also exports and resets (the
-// caller checked pluss_ctx::tables_dirty); n may then be 0.
+// caller checked pluss_ctx::tables_dirty) or writes the dense vector; n may
+// then be 0.  The shape alone picks the kernel.  diag (pluss_diag_dense
+// only): ABL variant and a workgroup cap instead of the product's.
 static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hipStream_t s, const ExportArgs* fuse,
-                      const char* api) {
+                      const char* api, int abl = 0, int grid_cap = 0) {
   if (n == 0 && !fuse) return PLUSS_OK;
   if (((uintptr_t)d_samples & 7u) != 0) {
     set_error(std::string(api) + ": sample buffer must be 8-byte aligned");
@@ -1158,149 +936,44 @@ static int hot_launch(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, hip
     --n;
   }
   const Model& m = ctx->m;
-  // Lists past the Infinity Cache stream from HBM, where fewer resident waves per CU
-  // queue fewer requests against the same channels: measured on MI355X with
-  // tools/grid_sweep.py (profiles/r05_grid_sweep.jsonl), 1024 workgroups are best at
-  // 2^24-2^25 samples, 768 at 2^26 (+1.8%), 640 at 2^27-2^28 (+3.4%).
-  const int cap = !m.fast ? MAX_BLOCKS : n >= (1ull << 27) ? 640 : n >= (1ull << 26) ? 768 : MAX_BLOCKS;
-  int nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL, std::min(cap, MAX_BLOCKS));
-  const GTable& g = ctx->g;
-#define PLUSS_LAUNCH_HOT(EX, ...)                                                                                  \
-  hipLaunchKernelGGL((k_sampled_hist<__VA_ARGS__>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n, head, has_head, g, \
-                     EX)
-  // diagnostics only (tools/ablate.py): PLUSS_ABLATE=1|2 (loads + bins / loads only, lane-counter kernel),
-  // PLUSS_ABLATE=3|4 (k_count: loads only | count without the tail),
-  // PLUSS_LEGACY=1 (the lane-counter kernel k_sampled_hist for FAST shapes), PLUSS_UNROLL=1|4,
-  // PLUSS_NT=0|1, PLUSS_GRID=<max blocks>, PLUSS_PCS=4 (legacy: a counter set per wave)
-  const char* abl = getenv("PLUSS_ABLATE");
-  const char* unr = getenv("PLUSS_UNROLL");
-  const char* ntv = getenv("PLUSS_NT");
-  const char* grd = getenv("PLUSS_GRID");
-  const char* pcs = getenv("PLUSS_PCS");
-  const char* leg = getenv("PLUSS_LEGACY");
-  if (grd && atoi(grd) > 0) nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL, std::min(atoi(grd), 16384));
-  const int a = abl ? atoi(abl) : 0, u = unr ? atoi(unr) : UNROLL;
-  const bool nt = ntv ? ntv[0] == '1' : HOT_NT;
-  const bool pc4 = pcs && pcs[0] == '4';
   const ExportArgs none{nullptr, nullptr, 0, nullptr, nullptr, 0};
-  const bool legacy = (leg && leg[0] == '1') || a == 1 || a == 2 || pc4;
-  if ((a == 3 || a == 4) && m.fast && m.p2 && m.np2 && !fuse) {  // k_count ablations (no output)
-    if (a == 3)
-      hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_NONE, UNROLL, 1>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples,
-                         n, head, has_head, g, none);
-    else
-      hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_NONE, UNROLL, 2>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples,
-                         n, head, has_head, g, none);
-    PLUSS_HIP_CHECK(hipGetLastError());
-    return PLUSS_OK;
-  }
   const ExportArgs& ex = fuse ? *fuse : none;
   const int tail = fuse ? (fuse->dense ? TAIL_DENSE : TAIL_EXPORT) : TAIL_NONE;
-  if (m.fast && !legacy) {
-#define PLUSS_LAUNCH_COUNT(P2, NP2, NT, UNR)                                                                      \
-  do {                                                                                                           \
-    if (tail == TAIL_DENSE)                                                                                      \
-      hipLaunchKernelGGL((k_count<P2, NP2, NT, TAIL_DENSE, UNR>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n,  \
-                         head, has_head, g, ex);                                                                 \
-    else if (tail == TAIL_EXPORT)                                                                                \
-      hipLaunchKernelGGL((k_count<P2, NP2, NT, TAIL_EXPORT, UNR>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n, \
-                         head, has_head, g, ex);                                                                 \
-    else                                                                                                         \
-      hipLaunchKernelGGL((k_count<P2, NP2, NT, TAIL_NONE, UNR>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n,   \
-                         head, has_head, g, ex);                                                                 \
+  int cap = grid_cap > 0 ? grid_cap : (m.fast && tail == TAIL_DENSE ? dense_grid_cap(n) : MAX_BLOCKS);
+  const int nb = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)BLOCK * UNROLL, std::min(cap, 16384));
+  const GTable& g = ctx->g;
+  if (!m.fast) {
+    ctx->tables_dirty = true;
+    hipLaunchKernelGGL(k_sampled_hist, dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n, head, has_head, g);
+    PLUSS_HIP_CHECK(hipGetLastError());
+    return PLUSS_OK;
+  }
+#define PLUSS_LAUNCH_COUNT(P2, NP2, TL, AB)                                                                        \
+  hipLaunchKernelGGL((k_count<P2, NP2, TL, AB>), dim3(nb), dim3(BLOCK), 0, s, m, d_samples, n, head, has_head, g, ex)
+#define PLUSS_LAUNCH_TAIL(P2, NP2)                                                        \
+  do {                                                                                    \
+    if (tail == TAIL_DENSE) PLUSS_LAUNCH_COUNT(P2, NP2, TAIL_DENSE, 0);                   \
+    else if (tail == TAIL_EXPORT) PLUSS_LAUNCH_COUNT(P2, NP2, TAIL_EXPORT, 0);            \
+    else PLUSS_LAUNCH_COUNT(P2, NP2, TAIL_NONE, 0);                                       \
   } while (0)
-    const char* lanesv = getenv("PLUSS_LANES");
-    if (m.p2 && m.np2 && tail == TAIL_DENSE && lanesv && lanesv[0] == '0') {  // diagnostics: ballot counting only
-      hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_DENSE, UNROLL, 0, BLOCK, -1, false>), dim3(nb), dim3(BLOCK),
-                         0, s, m, d_samples, n, head, has_head, g, ex);
-      PLUSS_HIP_CHECK(hipGetLastError());
-      return PLUSS_OK;
+  if (abl) {  // diagnostics: every BASELINE shape is P2 && NP2
+    if (!(m.p2 && m.np2)) {
+      set_error(std::string(api) + ": the ablation variants need N, CLS/DS and chunk powers of two");
+      return PLUSS_ERR_CONFIG;
     }
-    const char* prefv = getenv("PLUSS_PREF");
-    if (m.p2 && m.np2 && tail == TAIL_DENSE && prefv && prefv[0] == '2') {  // diagnostics: two steps in flight
-      hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_DENSE, UNROLL, 0, BLOCK, -1, true, 2>), dim3(nb),
-                         dim3(BLOCK), 0, s, m, d_samples, n, head, has_head, g, ex);
-      PLUSS_HIP_CHECK(hipGetLastError());
-      return PLUSS_OK;
-    }
-    if (m.p2 && m.np2 && tail == TAIL_DENSE && prefv && prefv[0] == '3') {  // diagnostics: UNROLL 1, two steps in flight
-      hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_DENSE, 1, 0, BLOCK, -1, true, 2>), dim3(nb),
-                         dim3(BLOCK), 0, s, m, d_samples, n, head, has_head, g, ex);
-      PLUSS_HIP_CHECK(hipGetLastError());
-      return PLUSS_OK;
-    }
-    const char* auxv = getenv("PLUSS_AUX");
-    if (m.p2 && m.np2 && tail == TAIL_DENSE && auxv) {  // diagnostics: cache-policy bits of the sample loads
-#define PLUSS_AUX_CASE(V)                                                                                          \
-  case V:                                                                                                          \
-    hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_DENSE, UNROLL, 0, BLOCK, V>), dim3(nb), dim3(BLOCK), 0, s, \
-                       m, d_samples, n, head, has_head, g, ex);                                                    \
-    break;
-      switch (atoi(auxv)) {
-        PLUSS_AUX_CASE(0)
-        PLUSS_AUX_CASE(1)
-        PLUSS_AUX_CASE(2)
-        PLUSS_AUX_CASE(3)
-        PLUSS_AUX_CASE(16)
-        PLUSS_AUX_CASE(17)
-        PLUSS_AUX_CASE(18)
-        PLUSS_AUX_CASE(19)
-        default:
-          set_error("PLUSS_AUX: one of 0 1 2 3 16 17 18 19");
-          return PLUSS_ERR_CONFIG;
-      }
-#undef PLUSS_AUX_CASE
-      PLUSS_HIP_CHECK(hipGetLastError());
-      return PLUSS_OK;
-    }
-    const char* bsv = getenv("PLUSS_BS");
-    if (m.p2 && m.np2 && tail == TAIL_DENSE && bsv && atoi(bsv) == 1024) {  // diagnostics: 1024-thread workgroups
-      int nb4 = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)1024 * UNROLL, MAX_BLOCKS / 4);
-      if (grd && atoi(grd) > 0) nb4 = grid_for((n >> 1) ? (n >> 1) : 1, (uint64_t)1024 * UNROLL, std::min(atoi(grd), 4096));
-      hipLaunchKernelGGL((k_count<true, true, HOT_NT, TAIL_DENSE, UNROLL, false, 1024>), dim3(nb4), dim3(1024), 0, s, m,
-                         d_samples, n, head, has_head, g, ex);
-    } else if (m.p2 && m.np2 && (nt != HOT_NT || u != UNROLL)) {  // diagnostics
-      if (u == 1) PLUSS_LAUNCH_COUNT(true, true, HOT_NT, 1);
-      else if (u == 4) PLUSS_LAUNCH_COUNT(true, true, HOT_NT, 4);
-      else PLUSS_LAUNCH_COUNT(true, true, !HOT_NT, UNROLL);
-    } else if (m.p2 && m.np2) {
-      PLUSS_LAUNCH_COUNT(true, true, HOT_NT, UNROLL);
-    } else if (m.p2) {
-      PLUSS_LAUNCH_COUNT(true, false, HOT_NT, UNROLL);
-    } else if (m.np2) {
-      PLUSS_LAUNCH_COUNT(false, true, HOT_NT, UNROLL);
-    } else {
-      PLUSS_LAUNCH_COUNT(false, false, HOT_NT, UNROLL);
-    }
-#undef PLUSS_LAUNCH_COUNT
-    PLUSS_HIP_CHECK(hipGetLastError());
-    return PLUSS_OK;
-  }
-  if (tail == TAIL_DENSE) {  // legacy lane-counter kernel (diagnostics)
-    if (m.p2) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, HOT_NT, TAIL_DENSE);
-    else PLUSS_LAUNCH_HOT(ex, FAST, 0, UNROLL, HOT_NT, TAIL_DENSE);
-    PLUSS_HIP_CHECK(hipGetLastError());
-    return PLUSS_OK;
-  }
-  if (tail == TAIL_EXPORT) {
-    if (m.p2) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, HOT_NT, TAIL_EXPORT);
-    else PLUSS_LAUNCH_HOT(ex, FAST, 0, UNROLL, HOT_NT, TAIL_EXPORT);
-    PLUSS_HIP_CHECK(hipGetLastError());
-    return PLUSS_OK;
-  }
-  if (!m.fast) ctx->tables_dirty = true;
-  if (m.fast && m.p2 && (a || pc4)) {
-    if (pc4) PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, false, TAIL_NONE, 4);
-    else if (a == 1) PLUSS_LAUNCH_HOT(ex, FAST_P2, 1, UNROLL, false);
-    else PLUSS_LAUNCH_HOT(ex, FAST_P2, 2, UNROLL, false);
-  } else if (m.fast && m.p2) {
-    PLUSS_LAUNCH_HOT(ex, FAST_P2, 0, UNROLL, HOT_NT);
-  } else if (m.fast) {
-    PLUSS_LAUNCH_HOT(ex, FAST, 0, UNROLL, HOT_NT);
+    if (abl == 1) PLUSS_LAUNCH_COUNT(true, true, TAIL_NONE, 1);
+    else PLUSS_LAUNCH_COUNT(true, true, TAIL_NONE, 2);
+  } else if (m.p2 && m.np2) {
+    PLUSS_LAUNCH_TAIL(true, true);
+  } else if (m.p2) {
+    PLUSS_LAUNCH_TAIL(true, false);
+  } else if (m.np2) {
+    PLUSS_LAUNCH_TAIL(false, true);
   } else {
-    PLUSS_LAUNCH_HOT(ex, GENERIC);
+    PLUSS_LAUNCH_TAIL(false, false);
   }
-#undef PLUSS_LAUNCH_HOT
+#undef PLUSS_LAUNCH_TAIL
+#undef PLUSS_LAUNCH_COUNT
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }
@@ -1319,44 +992,49 @@ int launch_sampled_hist_export(pluss_ctx* ctx, const uint64_t* d_samples, uint64
   return launch_export(ctx, d_keys, d_counts, cap, s, true);
 }
 
-int launch_sampled_hist_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, unsigned long long* d_counts,
-                              hipStream_t s) {
+static int dense_check(pluss_ctx* ctx, unsigned long long* d_counts, const char* api) {
   if (!ctx->m.fast) {
-    set_error("pluss_dev_sampled_hist_dense: needs N % (cls/ds) == 0 (a dense (ref, case) histogram)");
+    set_error(std::string(api) + ": needs N % (cls/ds) == 0 (a dense (ref, case) histogram)");
     return PLUSS_ERR_CONFIG;
   }
   if (((uintptr_t)d_counts & 7u) != 0) {
-    set_error("pluss_dev_sampled_hist_dense: counts buffer must be 8-byte aligned");
+    set_error(std::string(api) + ": counts buffer must be 8-byte aligned");
     return PLUSS_ERR_INPUT;
   }
-  const char* dr = getenv("PLUSS_DROWS");  // diagnostics: first-level rows of the dense tail
-  uint32_t drows = DENSE_ROWS;
-  if (dr && atoi(dr) > 0) {
-    drows = 1;
-    while (drows * 2 <= (uint32_t)atoi(dr) && drows * 2 <= NBROW) drows *= 2;
-  }
-  const ExportArgs ex{nullptr, nullptr, 0, nullptr, d_counts, drows};
+  return PLUSS_OK;
+}
+
+int launch_sampled_hist_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, unsigned long long* d_counts,
+                              hipStream_t s) {
+  if (int rc = dense_check(ctx, d_counts, "pluss_dev_sampled_hist_dense")) return rc;
+  const ExportArgs ex{nullptr, nullptr, 0, nullptr, d_counts, DENSE_ROWS};
   return hot_launch(ctx, d_samples, n, s, &ex, "pluss_dev_sampled_hist_dense");
 }
 
+int launch_diag_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, unsigned long long* d_counts,
+                      int variant, int max_grid, hipStream_t s) {
+  if (variant < 0 || variant > 2 || max_grid < 0) {
+    set_error("pluss_diag_dense: variant must be 0, 1 or 2 and max_grid >= 0");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (int rc = dense_check(ctx, d_counts, "pluss_diag_dense")) return rc;
+  const ExportArgs ex{nullptr, nullptr, 0, nullptr, d_counts, DENSE_ROWS};
+  return hot_launch(ctx, d_samples, n, s, &ex, "pluss_diag_dense", variant, max_grid);
+}
+
 int launch_fulltrace(pluss_ctx* ctx, hipStream_t s) {
-  if (!ctx->m.fast) ctx->tables_dirty = true;
   const uint64_t npairs = (uint64_t)ctx->m.N * ctx->m.N;
-  const int nb = grid_for(npairs, BLOCK / 64 * 8);
-  const char* leg = getenv("PLUSS_LEGACY");  // diagnostics: the lane-counter full trace
-  const bool legacy = leg && leg[0] == '1';
-  // the ballot kernel's waves are short dependency chains: 8 waves per SIMD (2048 workgroups) hide them
-  const int nbc = grid_for(npairs, BLOCK / 64 * 8, 2048);
-  if (ctx->m.fast && !legacy && ctx->m.p2)
-    hipLaunchKernelGGL(k_fulltrace_count<true>, dim3(nbc), dim3(BLOCK), 0, s, ctx->m, ctx->g);
-  else if (ctx->m.fast && !legacy)
-    hipLaunchKernelGGL(k_fulltrace_count<false>, dim3(nbc), dim3(BLOCK), 0, s, ctx->m, ctx->g);
-  else if (ctx->m.fast && ctx->m.p2)
-    hipLaunchKernelGGL(k_fulltrace<FAST_P2>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ctx->g);
-  else if (ctx->m.fast)
-    hipLaunchKernelGGL(k_fulltrace<FAST>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ctx->g);
-  else
-    hipLaunchKernelGGL(k_fulltrace<GENERIC>, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ctx->g);
+  if (!ctx->m.fast) {
+    ctx->tables_dirty = true;
+    hipLaunchKernelGGL(k_fulltrace, dim3(grid_for(npairs, BLOCK / 64 * 8)), dim3(BLOCK), 0, s, ctx->m, ctx->g);
+  } else {
+    // the ballot kernel's waves are short dependency chains: 8 waves per SIMD (2048 workgroups) hide them
+    const int nbc = grid_for(npairs, BLOCK / 64 * 8, 2048);
+    if (ctx->m.p2)
+      hipLaunchKernelGGL(k_fulltrace_count<true>, dim3(nbc), dim3(BLOCK), 0, s, ctx->m, ctx->g);
+    else
+      hipLaunchKernelGGL(k_fulltrace_count<false>, dim3(nbc), dim3(BLOCK), 0, s, ctx->m, ctx->g);
+  }
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }

@@ -25,7 +25,7 @@ the scan state across shards (include/pluss_gpu.h, pluss_dev_faithful_shard_*).
 """
 import numpy as np
 
-from ._lib import DENSE_BINS
+from ._lib import DENSE_BINS, PlussError
 from .api import REFS, Context, Histogram, faithful_key_space, hist_from_dense, hist_from_tables
 
 TABLE_CAP = 4096
@@ -61,9 +61,25 @@ def allgather_tables(keys_t, counts_t, group=None):
     return merge_tables(gk.cpu().numpy(), gc.cpu().numpy())
 
 
+def raise_together(err, group=None, device=None):
+    """Every rank learns whether any rank failed (one all-reduce of an error
+    word) and all raise together, so no rank is left waiting in a later
+    collective.  `err` is this rank's exception or None."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if err is not None else 0], dtype=torch.int64, device=device or "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    if err is not None:
+        raise err
+    if int(t.item()):
+        raise PlussError("another rank's sampler pass failed (malformed samples or table overflow)")
+
+
 def sharded_clean_hist(cfg, seed, counts, group=None, stream=None):
     """Every rank: expand its shard on its GPU, histogram it, merge across ranks.
-    Returns the merged Histogram (identical on all ranks)."""
+    Returns the merged Histogram (identical on all ranks).  Malformed samples
+    and table overflow on any rank raise PlussError on every rank before the
+    tables are exchanged."""
     import torch
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
@@ -83,7 +99,14 @@ def sharded_clean_hist(cfg, seed, counts, group=None, stream=None):
         ctx.sampled_hist(samples.data_ptr(), n, sp)
         ctx.export(keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
         torch.cuda.synchronize(dev)
-    if dist.get_backend(group) == "gloo":  # e.g. several ranks sharing one GPU in tests
+        err = None
+        try:
+            ctx.fetch()  # the handle's flags: malformed samples, table or export overflow
+        except PlussError as e:
+            err = e
+    gloo = dist.get_backend(group) == "gloo"  # e.g. several ranks sharing one GPU in tests
+    raise_together(err, group, None if gloo else dev)
+    if gloo:
         keys, cnts = keys.cpu(), cnts.cpu()
     return allgather_tables(keys, cnts, group)
 

@@ -109,3 +109,80 @@ def closed_form_ri(N, T, CS, W, refs, c0, c1, c2):
     ri[m] = np.where(c1[m] % W != W - 1, S, np.where(more_rows[m], N * S - (W - 1) * S, -1))
     assert (ri != -9).all()
     return ri
+
+
+def closed_form_counts(N, T, CS, samples, W=8, chunk=1 << 22):
+    """{(ref, kind, ri): count} of a (large) list from the closed forms, in chunks
+    (N % W == 0 shapes, r10 share threshold)."""
+    from collections import Counter
+    refs_names = ["C0", "C1", "A0", "B0", "C2", "C3"]
+    acc = Counter()
+    for a in range(0, len(samples), chunk):
+        s = np.asarray(samples[a:a + chunk], dtype=np.uint64)
+        m = np.uint64(0xFFFFF)
+        refs = (s >> np.uint64(60)).astype(np.int64)
+        c0 = ((s >> np.uint64(40)) & m).astype(np.int64)
+        c1 = ((s >> np.uint64(20)) & m).astype(np.int64)
+        c2 = (s & m).astype(np.int64)
+        ri = closed_form_ri(N, T, CS, W, refs, c0, c1, c2)
+        kind = ((refs == 3) & (ri > 0) & (2 * ri > (4 * N + 2) * N)).astype(np.int64)
+        keys = (refs * 4 + kind) * (1 << 40) + (ri + 2)
+        u, cnt = np.unique(keys, return_counts=True)
+        for k, n in zip(u.tolist(), cnt.tolist()):
+            acc[(refs_names[k >> 42], (k >> 40) & 3, (k & ((1 << 40) - 1)) - 2)] += n
+    return dict(acc)
+
+
+def edge_samples_gemm(N, T, CS=4, W=8, per=8):
+    """Crafted edge samples of an N % (CS*T) == 0 GEMM shape (packed u64), for the
+    oracle checks at BASELINE sizes: every thread's last row, c1 % W == W-1
+    (B0 across rows, B0 cold in a last row), c2 % W == W-1 (A0 next sweep),
+    c2 = N-2 / N-1 (C3 within / past the c2 loop), c1 = N-1, B0 share samples,
+    and the first and last iteration of every row kind.  Indices stay in
+    [0, N-1]; distinct."""
+    rng = np.random.default_rng(N * 131 + T)
+    out = set()
+    last_rows = [((r * T + t) * CS + CS - 1) for t in range(T) for r in [N // (CS * T) - 1]]
+    any_rows = [0, CS - 1, CS, N - 1] + last_rows[:per]
+
+    def pk(ref, c0, c1, c2=0):
+        return (ref << 60) | (int(c0) << 40) | (int(c1) << 20) | int(c2)
+    for c0 in any_rows:
+        for c1 in [0, W - 1, 2 * W - 1, N - 1, N - W, int(rng.integers(0, N // W)) * W + W - 1]:
+            for c2 in [0, W - 1, N - 2, N - 1, int(rng.integers(0, N))]:
+                for ref in (2, 3, 4, 5):
+                    out.add(pk(ref, c0, c1, c2))
+            out.add(pk(0, c0, c1))
+            out.add(pk(1, c0, c1))
+    return np.array(sorted(out), dtype=np.uint64)
+
+
+def oracle_subset(N, T, CS, samples, budget_steps, W=8, seed=0):
+    """The samples the stepping oracle (orc_clean) can check within about
+    `budget_steps` access steps: its cost per sample is the RI, or for a cold
+    sample the rest of its thread's stream (N % (CS*T) == 0 shapes).  Cheap
+    samples are all kept; the expensive ones (B0 across rows, cold samples) are
+    kept in random order while the budget lasts."""
+    s = np.asarray(samples, dtype=np.uint64)
+    m = np.uint64(0xFFFFF)
+    refs = (s >> np.uint64(60)).astype(np.int64)
+    c0 = ((s >> np.uint64(40)) & m).astype(np.int64)
+    c1 = ((s >> np.uint64(20)) & m).astype(np.int64)
+    c2 = (s & m).astype(np.int64)
+    ri = closed_form_ri(N, T, CS, W, refs, c0, c1, c2)
+    S = 4 * N + 2
+    R = N * S
+    q = (c0 // (CS * T)) * CS + c0 % CS
+    off = np.where(refs < 2, refs, refs + 4 * np.where(refs < 2, 0, c2))
+    pos = q * R + c1 * S + off
+    cost = np.where(ri > 0, ri, (N // T) * R - pos).astype(np.float64)
+    cheap = cost <= 1e5
+    keep = cheap.copy()
+    spent = cost[cheap].sum()
+    rng = np.random.default_rng(seed)
+    for i in rng.permutation(np.nonzero(~cheap)[0]):
+        if spent + cost[i] > budget_steps:
+            continue
+        keep[i] = True
+        spent += cost[i]
+    return s[keep]

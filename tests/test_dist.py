@@ -161,3 +161,40 @@ def test_dense_allreduce_equals_whole_list(orc, world):
     assert sum(n for _, _, n in res) == len(whole)
     for _, bins, _ in res:
         assert bins == want
+
+
+def _raise_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from pluss_sampler_optimization_amd import PlussError
+    from pluss_sampler_optimization_amd import dist as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = []
+    for bad_rank in (None, 1):
+        err = PlussError("malformed sample") if rank == bad_rank else None
+        try:
+            D.raise_together(err)
+            out.append("ok")
+        except PlussError as e:
+            out.append("raised:" + ("other" if "another rank" in str(e) else "own"))
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, out))
+
+
+def test_flag_errors_raise_on_every_rank():
+    """A rank whose pass flagged malformed samples / overflow raises, and so do
+    the others (one all-reduce of an error word), before any table exchange."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_raise_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res[0] == ["ok", "raised:other"]
+    assert res[1] == ["ok", "raised:own"]

@@ -87,18 +87,13 @@ def test_ri_dump_generic_path_equals_oracle(orc, model_host, shape):
                                               (20, 2, 3, 4, 64, 1), (33, 4, 2, 8, 64, 0), (256, 4, 4, 8, 64, 1),
                                               (96, 3, 3, 8, 64, 1), (72, 5, 2, 8, 64, 0), (40, 2, 4, 8, 32, 1)])
 def test_fulltrace_gpu_equals_oracle(orc, N, T, CS, DS, CLS, thr):
-    """Full trace (sampling rate 1.0) == seq.cpp sampler() restated (per-source-ref raw bins);
-    the ballot kernel (N % W == 0) also equals the lane-counter kernel."""
+    """Full trace (sampling rate 1.0) == seq.cpp sampler() restated (per-source-ref raw bins):
+    the ballot kernel (N % W == 0) and the exact-key kernel (other shapes)."""
     c = cfg(N, T, CS, DS, CLS, thr_variant="v1" if thr else "r10")
     h = P.fulltrace_hist(c)
     want, trav = orc.fulltrace(N, T, CS, DS, CLS, thr_variant=thr)
     assert h.bins == want
     assert h.traversed[0] == trav
-    os.environ["PLUSS_LEGACY"] = "1"
-    try:
-        assert P.fulltrace_hist(c).bins == want
-    finally:
-        os.environ.pop("PLUSS_LEGACY", None)
 
 
 def test_fulltrace_kat_n128(orc):
@@ -299,9 +294,9 @@ def test_fused_count_and_export(orc, N, T, CS):
 def test_dense_pass(orc, N, T, CS):
     """pluss_dev_sampled_hist_dense (one launch, dense (ref, case) counts) ==
     the oracle, pass after pass (the in-kernel state is left zeroed), over
-    grids of 1..1024 workgroups (1..64 bin rows, uneven rows), unaligned and
-    odd-length lists, an empty list, malformed samples; and it leaves the
-    handle's accumulating histogram alone."""
+    grids of 1..1024 workgroups (pluss_diag_dense's cap: 1..64 bin rows,
+    uneven rows), unaligned and odd-length lists, an empty list, malformed
+    samples; and it leaves the handle's accumulating histogram alone."""
     torch = pytest.importorskip("torch")
     c = cfg(N, T, CS)
     counts = P.default_counts(N, 400000)  # 391 workgroups by default: 64 rows of 6-7
@@ -316,9 +311,12 @@ def test_dense_pass(orc, N, T, CS):
     def out():
         return torch.full((P.DENSE_BINS + 2,), 7, dtype=torch.int64, device="cuda")
 
-    def run(ctx, ptr, n):
+    def run(ctx, ptr, n, grid=None):
         d = out()
-        ctx.sampled_hist_dense(ptr, n, d.data_ptr(), stream)
+        if grid is None:
+            ctx.sampled_hist_dense(ptr, n, d.data_ptr(), stream)
+        else:
+            ctx.diag_dense(ptr, n, d.data_ptr(), 0, grid, stream)
         torch.cuda.synchronize()
         v = d.cpu().numpy()
         assert v[P.DENSE_BINS + 1] == 7  # nothing written past the vector
@@ -328,33 +326,13 @@ def test_dense_pass(orc, N, T, CS):
         ctx.reset(stream)
         ctx.sampled_hist(buf.data_ptr() + 8, 1000, stream)  # accumulating histogram: untouched by dense passes
         first = None
-        try:
-            knobs = ("PLUSS_GRID", "PLUSS_LEGACY", "PLUSS_DROWS", "PLUSS_BS", "PLUSS_LANES")
-            for grid in ("", "1", "3", "64", "65", "200", "640", "768", "1024", "legacy", "drows1", "drows8", "drows64", "bs1024",
-                         "bs1024_3", "ballots"):
-                for k in knobs:
-                    os.environ.pop(k, None)
-                if grid == "legacy":  # the lane-counter kernel (k_sampled_hist) agrees
-                    os.environ["PLUSS_LEGACY"] = "1"
-                elif grid.startswith("drows"):  # first-level rows of the dense tail
-                    os.environ["PLUSS_DROWS"] = grid[5:]
-                elif grid == "ballots":  # k_count without its vector fast path
-                    os.environ["PLUSS_LANES"] = "0"
-                elif grid.startswith("bs1024"):  # 1024-thread workgroups (diagnostic variant)
-                    os.environ["PLUSS_BS"] = "1024"
-                    if grid == "bs1024_3":
-                        os.environ["PLUSS_GRID"] = "3"
-                elif grid:
-                    os.environ["PLUSS_GRID"] = grid
-                for _ in range(2):
-                    v = run(ctx, buf.data_ptr() + 8, total)
-                    assert v[P.DENSE_BINS] == 0
-                    assert P.hist_from_dense(c, v).bins == want, grid
-                    first = v if first is None else first
-                    assert (v == first).all()
-        finally:
-            for k in knobs:
-                os.environ.pop(k, None)
+        for grid in (None, 1, 3, 64, 65, 200, 391):
+            for _ in range(2):
+                v = run(ctx, buf.data_ptr() + 8, total, grid)
+                assert v[P.DENSE_BINS] == 0
+                assert P.hist_from_dense(c, v).bins == want, grid
+                first = v if first is None else first
+                assert (v == first).all()
         v = run(ctx, buf.data_ptr(), total + 1)  # 8-byte aligned (peeled head), odd length
         assert P.hist_from_dense(c, v).total() == total + 1
         for n in (0, 1, 2, 3):
@@ -746,75 +724,6 @@ def test_faithful_refs_concurrent_equals_per_reference_calls(N, T, CS, per):
     assert h.total() == h_one.total()
 
 
-def _faithful_both_paths(c, s, counts):
-    """Faithful histograms of one list: bucket path (PLUSS_FAITH_BUCKET=1), radix-sort
-    path (the default), each through one call per reference and through the
-    concurrent six-reference call."""
-    torch = pytest.importorskip("torch")
-    t = torch.from_numpy(np.ascontiguousarray(s).view(np.int64)).cuda()
-    stream = torch.cuda.current_stream().cuda_stream
-    out = {}
-    for path in ("bucket", "sorted"):
-        os.environ["PLUSS_FAITH_BUCKET"] = "1" if path == "bucket" else "0"
-        try:
-            with P.Context(c) as ctx:
-                ctx.reset(stream)
-                off = 0
-                for r, n in enumerate(counts):
-                    if n:
-                        ctx.faithful_hist(r, t.data_ptr() + 8 * off, n, stream)
-                    off += n
-                out[path] = ctx.fetch()
-                ctx.reset(stream)
-                ctx.faithful_hist_refs(t.data_ptr(), counts, stream)
-                out[path + "_refs"] = ctx.fetch()
-        finally:
-            os.environ.pop("PLUSS_FAITH_BUCKET", None)
-    return out
-
-
-def _assert_same(hs):
-    first = next(iter(hs.values()))
-    for k, h in hs.items():
-        assert h.bins == first.bins, k
-        assert list(h.traversed) == list(first.traversed), k
-
-
-@pytest.mark.parametrize("N,T,per", [(1024, 8, 300000), (2048, 8, 200000), (256, 4, 40000), (128, 4, 1)])
-def test_faithful_bucket_path_equals_radix_sort_path(N, T, per):
-    """The bucket path (per-bucket LDS sort + fused scan) equals the device-wide
-    radix-sort path: 32-bit words (N=1024: 128 buckets), 64-bit words (N=2048),
-    a one-bucket list (N=256 ... 40000 per reference: 16 buckets) and one sample."""
-    c = cfg(N, T, mode="faithful")
-    counts = [min(per, (N - 1) ** 2) if r < 2 else per for r in range(6)]
-    s = np.concatenate([P.expand_samples(c, 0x5EED0200 + N, r, 0, n) for r, n in enumerate(counts)]).astype(np.uint64)
-    hs = _faithful_both_paths(c, s, counts)
-    _assert_same(hs)
-    assert hs["bucket"].total() > 0
-
-
-def test_faithful_skewed_list_falls_back_to_radix_sort(orc):
-    """A list crowded into one bucket (rows c0 < 2*T*CS: all in bucket 0 of 8,
-    20000 > the 8192-word tile) takes the radix-sort path; results equal the
-    radix-sort path, the oracle, and the bucket path for the uncrowded references."""
-    N, T = 256, 4
-    c = cfg(N, T, mode="faithful")
-    rng = np.random.default_rng(7)
-    idx = rng.choice(32 * 255 * 255, 20000, replace=False)
-    c0, rest = idx // (255 * 255), idx % (255 * 255)
-    c1, c2 = rest // 255, rest % 255
-    crowded = (np.uint64(P.REF_ID["B0"]) << np.uint64(60)) | (c0.astype(np.uint64) << np.uint64(40)) \
-        | (c1.astype(np.uint64) << np.uint64(20)) | c2.astype(np.uint64)
-    counts = [300, 300, 5000, 20000, 5000, 5000]
-    parts = [P.expand_samples(c, 0x5EED0300, r, 0, n) if r != 3 else crowded for r, n in enumerate(counts)]
-    s = np.concatenate(parts).astype(np.uint64)
-    hs = _faithful_both_paths(c, s, counts)
-    _assert_same(hs)
-    want, trav = orc.faithful(orc.cfg(N, T), "B0", crowded)
-    assert {k: v for k, v in hs["bucket"].bins.items() if k[0] == "B0"} == want
-    assert hs["bucket"].traversed[P.REF_ID["B0"]] == trav
-
-
 @pytest.mark.parametrize("rank", [0, 7])
 def test_dense_pass_config3_shard(rank):
     """BASELINE config 3 (N=4096, T=8, 2^28 samples over 8 GPUs): one rank's slice
@@ -848,12 +757,60 @@ def test_dense_pass_config3_shard(rank):
 
 def test_faithful_n4096_concurrent_equals_serial():
     """Faithful mode at the config-3 shape (N=4096: 64-bit packed words), 2^20 samples
-    per 3-D reference: the six-stream call equals six calls, on both sort paths."""
+    per 3-D reference: the six-stream call equals six calls."""
+    torch = pytest.importorskip("torch")
     N, T = 4096, 8
     c = cfg(N, T, mode="faithful")
     counts = [20000, 20000, 1 << 20, 1 << 20, 1 << 20, 1 << 20]
     s = np.concatenate([P.expand_samples(c, 0x5EED0001, r, 0, k) for r, k in enumerate(counts)]).astype(np.uint64)
-    hs = _faithful_both_paths(c, s, counts)
-    _assert_same(hs)
-    h = hs["sorted"]
+    h, h_one, h_again = _faithful_refs_vs_calls(c, s, counts, torch.cuda.current_stream().cuda_stream)
+    assert h.bins == h_one.bins == h_again.bins
+    assert list(h.traversed) == list(h_one.traversed) == list(h_again.traversed)
     assert 0 < h.total() - sum(h.cold(r) for r in P.REFS) <= sum(counts)
+
+
+_ENV_PROBE = r'''
+import json, sys
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[1])
+import pluss_sampler_optimization_amd as P
+c = P.SamplerConfig(n=256, threads=4)
+counts = P.default_counts(256, 300000)
+s = np.concatenate([P.expand_samples(c, 0x5EED0006, r, 0, counts[r]) for r in range(6)])
+t = torch.from_numpy(s.view(np.int64)).cuda()
+d = torch.zeros(P.DENSE_BINS + 1, dtype=torch.int64, device="cuda")
+with P.Context(c) as ctx:
+    ctx.sampled_hist_dense(t.data_ptr(), len(s), d.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+out = {"dense": d.cpu().tolist(),
+       "hist": sorted([list(k) + [v] for k, v in P.sampled_hist(c, s).bins.items()]),
+       "faithful": sorted([list(k) + [v] for k, v in
+                           P.sampled_hist(P.SamplerConfig(n=256, threads=4, mode="faithful"), s).bins.items()]),
+       "full": sorted([list(k) + [v] for k, v in P.fulltrace_hist(c).bins.items()])}
+print(json.dumps(out))
+'''
+
+
+def test_environment_cannot_change_results(tmp_path):
+    """The product entry points read no environment variable: the round-1
+    diagnostic knobs (ablation, grid, legacy kernels, bucket path ...) set in
+    the environment change nothing that pluss_dev_* / pluss_gemm_* return."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    probe = tmp_path / "probe.py"
+    probe.write_text(_ENV_PROBE)
+    knobs = {"PLUSS_ABLATE": "3", "PLUSS_GRID": "1", "PLUSS_LEGACY": "1", "PLUSS_LANES": "0", "PLUSS_DROWS": "1",
+             "PLUSS_BS": "1024", "PLUSS_FAITH_BUCKET": "1", "PLUSS_AUX": "3", "PLUSS_PREF": "2", "PLUSS_NT": "0",
+             "PLUSS_UNROLL": "4", "PLUSS_PCS": "4", "PLUSS_FB_ABL": "1"}
+    runs = []
+    for extra in ({}, knobs):
+        env = {k: v for k, v in os.environ.items() if not k.startswith("PLUSS_")}
+        env.update(extra)
+        r = subprocess.run([sys.executable, str(probe), root], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    assert runs[0] == runs[1]
+    assert sum(runs[0]["dense"][:P.DENSE_BINS]) == 300000

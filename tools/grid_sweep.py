@@ -1,5 +1,6 @@
-"""Diagnostics: k_count (dense tail) time vs workgroup count (PLUSS_GRID), interleaved
-repeats so clock drift does not favour one setting.  One JSON line per (size, grid)."""
+"""Diagnostics: k_count (dense tail) time vs workgroup cap (pluss_diag_dense's
+max_grid; 0 = the launcher's default), interleaved repeats so clock drift
+does not favour one setting.  One JSON line per (size, grid)."""
 import json
 import os
 import sys
@@ -15,10 +16,11 @@ def main():
     dev = torch.device("cuda", 0)
     s = torch.cuda.Stream(dev)
     torch.cuda.set_stream(s)
-    cfg = P.SamplerConfig(n=1024, threads=8)
-    grids = [int(g) for g in os.environ.get("SWEEP", "0,768,896,1024,1152,1280,1536,2048").split(",")]
-    for total in [1 << int(b) for b in os.environ.get("SIZES", "24,26").split(",")]:
-        counts = P.default_counts(1024, total)
+    N = int(os.environ.get("SWEEP_N", 4096))
+    cfg = P.SamplerConfig(n=N, threads=8)
+    grids = [int(g) for g in os.environ.get("SWEEP", "0,512,640,768,1024").split(",")]
+    for total in [1 << int(b) for b in os.environ.get("SIZES", "24,26,28").split(",")]:
+        counts = P.default_counts(N, total)
         buf = torch.empty(total, dtype=torch.int64, device=dev)
         ctx = P.Context(cfg)
         off = 0
@@ -29,18 +31,15 @@ def main():
         res = {g: [] for g in grids}
         for _ in range(5):
             for g in grids:
-                if g:
-                    os.environ["PLUSS_GRID"] = str(g)
-                else:
-                    os.environ.pop("PLUSS_GRID", None)
-                res[g].append(timeit(lambda: ctx.sampled_hist_dense(buf.data_ptr(), total, dense.data_ptr(),
-                                                                    s.cuda_stream), s, reps=100))
-        os.environ.pop("PLUSS_GRID", None)
+                res[g].append(timeit(lambda: ctx.diag_dense(buf.data_ptr(), total, dense.data_ptr(), 0, g,
+                                                             s.cuda_stream), s, reps=20))
         for g in grids:
-            ms = min(res[g])
-            print(json.dumps({"samples": total, "grid": g or "default", "min_ms": ms,
-                              "median_ms": sorted(res[g])[2], "GBps": 8 * total / ms / 1e6}), flush=True)
+            v = sorted(res[g])
+            print(json.dumps({"samples": total, "grid": g or "default", "min_ms": v[0], "median_ms": v[2],
+                              "GBps": 8 * total / v[2] / 1e6}), flush=True)
         ctx.close()
+        del buf
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":

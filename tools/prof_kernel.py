@@ -1,5 +1,6 @@
-"""Minimal driver for rocprofv3 counter passes: expand the config-2 sample list
-once, then launch the hot kernel a few times."""
+"""Minimal driver for rocprofv3 counter passes: expand the bench's sample list
+(config 3: N=4096, T=8, 2^28 samples on one GPU; PROF_N / PROF_T / PROF_LOG2
+override) once, then launch the hot kernel a few times."""
 import os
 import sys
 
@@ -8,7 +9,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import pluss_sampler_optimization_amd as P  # noqa: E402
 
-N, T, total = 1024, 8, 1 << 24
+N, T = int(os.environ.get("PROF_N", 4096)), int(os.environ.get("PROF_T", 8))
+total = 1 << int(os.environ.get("PROF_LOG2", 28))
 dev = torch.device("cuda", 0)
 s = torch.cuda.Stream(dev)
 torch.cuda.set_stream(s)
