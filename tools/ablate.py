@@ -1,7 +1,7 @@
 """Where the hot kernel's time goes (diagnostics, include/pluss_diag.h):
 the product dense pass (k_count, TAIL_DENSE), the same sample loads with
 nothing counted (variant 1), counting without the tail (variant 2), and a
-torch copy and read of the same buffer for bandwidth references.  Config-3
+torch copy of the same buffer for a bandwidth reference.  Config-3
 shape (N=4096, T=8) at 2^24 / 2^26 / 2^28 samples.  One JSON line per
 variant."""
 import json
@@ -53,7 +53,7 @@ def main():
         print(json.dumps({"samples": total, "variant": "torch_copy", "ms": ms, "GBps_rd+wr": 16 * total / ms / 1e6}),
               flush=True)
         del dst
-        ms = timeit(lambda: buf.view(torch.int32).sum(dtype=torch.int64), s)
+        ctx.close()
         del buf
         torch.cuda.empty_cache()
 
