@@ -232,48 +232,101 @@ def fulltrace_bench(P, torch, device, stream):
 
 
 def faithful_bench(P, torch, device, stream):
-    """FAITHFUL mode (r10 queue semantics: sort + scans) over the config-2 list
-    (N=1024, T=8, 2^24 samples): the six sampler_<REF> at once
-    (pluss_dev_faithful_hist_refs, one stream per reference, as r10 runs one
-    thread per reference), and one after another."""
+    """FAITHFUL mode (r10 queue semantics) at config 2 (N=1024, T=8, 2^24
+    samples), the six sampler_<REF> at once (one stream per reference, as r10
+    runs one thread per reference):
+      radix:     the Feistel list (arbitrary order): keys -> rocPRIM radix sort ->
+                 fused look-back scan (pluss_dev_faithful_hist_refs);
+      sorted:    the key-order list (pluss_dev_expand_sorted) read once, no sort
+                 (pluss_dev_faithful_hist_sorted_refs): 8 B per sample;
+      generated: the same key-order lists generated inside the pass, no input
+                 (pluss_dev_gen_faithful_refs)."""
     fcfg = P.SamplerConfig(n=1024, threads=8, mode="faithful", device=device)
     total = 1 << 24
     counts = P.default_counts(1024, total)
-    samples = torch.empty(total, dtype=torch.int64, device=torch.device("cuda", device))
-    out = {"workload": "GEMM N=1024, T=8, 2^24 samples (config 2 list), faithful", "samples": total}
+    dev = torch.device("cuda", device)
+    feistel = torch.empty(total, dtype=torch.int64, device=dev)
+    keyord = torch.empty(total, dtype=torch.int64, device=dev)
+    sp = stream.cuda_stream
+    out = {"workload": "GEMM N=1024, T=8, 2^24 samples (config 2 budget), faithful, six references concurrently",
+           "samples": total}
     with P.Context(fcfg) as ctx:
         off = 0
         for r, c in enumerate(counts):
-            ctx.expand(SEED, r, 0, c, samples.data_ptr() + 8 * off, stream.cuda_stream)
+            ctx.expand(SEED, r, 0, c, feistel.data_ptr() + 8 * off, sp)
+            ctx.expand_sorted(SEED, r, c, 0, c, keyord.data_ptr() + 8 * off, sp)
             off += c
-
-        def concurrent():
-            ctx.reset(stream.cuda_stream)
-            ctx.faithful_hist_refs(samples.data_ptr(), counts, stream.cuda_stream)
-
-        def serial():
-            ctx.reset(stream.cuda_stream)
-            off = 0
-            for r, c in enumerate(counts):
-                ctx.faithful_hist(r, samples.data_ptr() + 8 * off, c, stream.cuda_stream)
-                off += c
+        runs = {"radix": lambda: ctx.faithful_hist_refs(feistel.data_ptr(), counts, sp),
+                "sorted": lambda: ctx.faithful_hist_sorted_refs(keyord.data_ptr(), counts, sp),
+                "generated": lambda: ctx.gen_faithful_refs(SEED, counts, sp)}
         hs = {}
-        for name, run in (("concurrent", concurrent), ("serial", serial)):
+        for name, run in runs.items():
+            ctx.reset(sp)
             run()
             torch.cuda.synchronize()
+            hs[name] = ctx.fetch()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            for _ in range(5):
+            for _ in range(10):
                 run()
             e1.record(stream)
             torch.cuda.synchronize()
-            out[name + "_ms"] = e0.elapsed_time(e1) / 5
-            hs[name] = ctx.fetch()
-    h = hs["concurrent"]
-    assert h.bins == hs["serial"].bins and list(h.traversed) == list(hs["serial"].traversed)
-    out.update({"ms": out["concurrent_ms"], "samples_per_s": total / (out["concurrent_ms"] * 1e-3),
-                "recorded": h.total() - sum(h.cold(r) for r in P.REFS), "max_traversed": max(h.traversed),
-                "path": "keys -> rocPRIM radix sort -> fused look-back scan (arbitrary input order)"})
+            ms = e0.elapsed_time(e1) / 10
+            out[name] = {"ms": ms, "samples_per_s": total / (ms * 1e-3)}
+    # the key-order list through both of its paths gives one histogram
+    assert hs["sorted"].bins == hs["generated"].bins and list(hs["sorted"].traversed) == list(hs["generated"].traversed)
+    out["sorted"]["hbm_GBps"] = 8 * total / (out["sorted"]["ms"] * 1e-3) / 1e9
+    out["sorted"]["recorded"] = hs["sorted"].total() - sum(hs["sorted"].cold(r) for r in P.REFS)
+    out["radix"]["recorded"] = hs["radix"].total() - sum(hs["radix"].cold(r) for r in P.REFS)
+    out["note"] = ("radix = arbitrary-order input (sort inside the pass); sorted = input already in r10's pop "
+                   "order, checked in-kernel; generated = the key-order list made inside the pass")
+    return out
+
+
+def end_to_end_bench(P, torch, cfg, counts, parts, stream, steps=20):
+    """Sample generation inside the timed unit, as in r10 (r10:156-185 within the
+    timer r10:3199): this rank's slices of the six key-order lists generated and
+    counted in one launch (pluss_dev_gen_count_dense; the samples never touch
+    memory), and, for comparison, generated into HBM and then counted."""
+    dev = torch.device("cuda", cfg.device)
+    sp = stream.cuda_stream
+    first = [lo for lo, _ in parts]
+    n = [k for _, k in parts]
+    n_local = sum(n)
+    d = torch.zeros(P.DENSE_BINS + 1, dtype=torch.int64, device=dev)
+    d2 = torch.zeros_like(d)
+    buf = torch.empty(n_local, dtype=torch.int64, device=dev)
+    out = {}
+    with P.Context(cfg) as ctx:
+        def fused():
+            ctx.gen_count_dense(SEED, counts, first, n, d.data_ptr(), sp)
+
+        def expand():
+            off = 0
+            for r in range(6):
+                ctx.expand_sorted(SEED, r, counts[r], first[r], n[r], buf.data_ptr() + 8 * off, sp)
+                off += n[r]
+
+        def count():
+            ctx.sampled_hist_dense(buf.data_ptr(), n_local, d2.data_ptr(), sp)
+        for name, fn in (("gen_count_fused", fused), ("expand_sorted", expand), ("count", count)):
+            fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(steps):
+                fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            out[name + "_ms"] = e0.elapsed_time(e1) / steps
+    assert (d.cpu() == d2.cpu()).all(), "fused generate+count differs from expand + count"
+    assert int(d[:P.DENSE_BINS].sum()) == n_local
+    out["samples_per_gpu"] = n_local
+    out["fused_samples_per_s"] = n_local / (out["gen_count_fused_ms"] * 1e-3)
+    out["expand_then_count_samples_per_s"] = n_local / ((out["expand_sorted_ms"] + out["count_ms"]) * 1e-3)
+    out["fused_over_count"] = out["gen_count_fused_ms"] / out["count_ms"]
+    out["note"] = ("key-order stratified lists (pluss_expand_sorted, same per-reference budget and seed); "
+                   "fused = one launch, generation + counting; count = the headline kernel over the materialised list")
     return out
 
 
@@ -472,13 +525,12 @@ def main():
                    + (" (includes the overlapped all-reduces)" if collective else ""),
                    "bytes_per_launch": BYTES_PER_SAMPLE * n_local,
                    "loads_only_ms": loads_ms},
-        "end_to_end": {"expand_ms": expand_ms, "count_ms": kern_ms,
-                       "samples_per_s": n_local / ((expand_ms + kern_ms) * 1e-3),
-                       "note": "sample generation (pluss_dev_expand, Feistel bijection) + one counting pass, "
-                               "per rank; the reference's timer covers generation (r10:156-185 inside r10:3199)"},
+        "feistel_expand_ms": expand_ms,
         "launch": launch_mode,
         "histogram_bins": len(h.bins),
     }
+    if not args.no_extras:
+        result["end_to_end"] = end_to_end_bench(P, torch, cfg, counts, parts, stream)
     if rank == 0 and not args.no_extras:
         result["mrc"] = mrc_vs_reference(local)
     if rank == 0 and world == 1 and not args.no_extras:

@@ -94,6 +94,15 @@ int pluss_gemm_sampled_ri(const pluss_cfg *cfg, const uint64_t *samples, uint64_
 int pluss_expand_samples(const pluss_cfg *cfg, uint64_t seed, int32_t ref, uint64_t first, uint64_t n,
                          uint64_t *out);
 int pluss_default_counts(int64_t n, uint64_t total, uint64_t counts[6]);
+/* Key-order stratified list: samples [first, first+n) of the
+   `total` samples of reference `ref`, generated directly in the order r10's
+   priority queue pops them (IterationComp, runtime/pluss_utils.h:175-267; key
+   a*T+tid), one per stratum of the key-ordered iteration space at a keyed
+   pseudo-random offset: distinct, strictly increasing in key, random access
+   by index.  The list pluss_dev_faithful_hist_sorted consumes without a sort.
+   Needs N % (chunk*threads) == 0 and 1 <= total <= min(span^d, 2^32-1). */
+int pluss_expand_sorted(const pluss_cfg *cfg, uint64_t seed, int32_t ref, uint64_t total, uint64_t first, uint64_t n,
+                        uint64_t *out);
 
 /* --- handle API: device-resident inputs, explicit streams ----------------
    `stream` is a hipStream_t (NULL = the handle's own stream).  Device
@@ -103,6 +112,8 @@ int pluss_ctx_destroy(pluss_ctx *ctx);
 void *pluss_ctx_stream(pluss_ctx *ctx);
 int pluss_dev_expand(pluss_ctx *ctx, uint64_t seed, int32_t ref, uint64_t first, uint64_t n, uint64_t *d_out,
                      void *stream);
+int pluss_dev_expand_sorted(pluss_ctx *ctx, uint64_t seed, int32_t ref, uint64_t total, uint64_t first, uint64_t n,
+                            uint64_t *d_out, void *stream);
 int pluss_dev_hist_reset(pluss_ctx *ctx, void *stream);
 /* clean mode: accumulate every sample of a mixed-reference list */
 int pluss_dev_sampled_hist(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t n, void *stream);
@@ -114,6 +125,20 @@ int pluss_dev_faithful_hist(pluss_ctx *ctx, int32_t ref, const uint64_t *d_sampl
    pluss_dev_faithful_hist calls.  The references run on streams of their
    own, joined back into `stream`. */
 int pluss_dev_faithful_hist_refs(pluss_ctx *ctx, const uint64_t *d_samples, const uint64_t counts[6], void *stream);
+/* faithful mode over a list ALREADY IN KEY ORDER (strictly increasing a*T+tid,
+   e.g. pluss_dev_expand_sorted's): no sort, one pass reading 8 B per sample.
+   Same result as pluss_dev_faithful_hist on any permutation of the list; a
+   list that is not in key order is reported as PLUSS_ERR_INPUT at the next
+   fetch.  N % (cls/ds) == 0 shapes (PLUSS_ERR_CONFIG otherwise). */
+int pluss_dev_faithful_hist_sorted(pluss_ctx *ctx, int32_t ref, const uint64_t *d_samples, uint64_t n, void *stream);
+int pluss_dev_faithful_hist_sorted_refs(pluss_ctx *ctx, const uint64_t *d_samples, const uint64_t counts[6],
+                                        void *stream);
+/* the six sampler_<REF> over generated key-order lists: equal to
+   pluss_dev_expand_sorted(seed, r, totals[r], 0, totals[r]) for every r
+   followed by pluss_dev_faithful_hist_sorted_refs, without the lists ever
+   being written to memory (r10 generates its samples inside its timer,
+   r10:156-185). */
+int pluss_dev_gen_faithful_refs(pluss_ctx *ctx, uint64_t seed, const uint64_t totals[6], void *stream);
 /* full trace: every access of the nest (sampling rate 1.0); accumulates like
    the other passes, and adds the N*N*(4N+2) accesses to traversed[0] */
 int pluss_dev_fulltrace_hist(pluss_ctx *ctx, void *stream);
@@ -150,6 +175,14 @@ int pluss_dev_sampled_hist_export(pluss_ctx *ctx, const uint64_t *d_samples, uin
 int pluss_dense_keys(const pluss_cfg *cfg, uint64_t keys[PLUSS_DENSE_BINS]);
 int pluss_dev_sampled_hist_dense(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t n, uint64_t *d_counts,
                                  void *stream);
+/* generation and counting in one launch: samples [first[r], first[r]+n[r])
+   of every reference's key-order list of totals[r] samples (seed as in
+   pluss_expand_sorted), counted into d_counts like the dense pass, without
+   the list ever being written to memory -- the whole r10 pass, sample
+   generation (r10:156-185) included.  Equal to pluss_dev_expand_sorted of
+   each slice followed by pluss_dev_sampled_hist_dense. */
+int pluss_dev_gen_count_dense(pluss_ctx *ctx, uint64_t seed, const uint64_t totals[6], const uint64_t first[6],
+                              const uint64_t n[6], uint64_t *d_counts, void *stream);
 
 /* --- faithful mode over key-range shards (multi-GPU) ----------------------
    One r10 sampler_<REF> (r10:135-696 and its five twins) split over ranks by

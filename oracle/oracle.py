@@ -48,6 +48,9 @@ def lib():
                                    P(OrcEntry), ctypes.c_int64, P(ctypes.c_int64), P(ctypes.c_int64)]
         L.orc_expand.argtypes = [P(OrcCfg), ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
                                  P(ctypes.c_uint64)]
+        L.orc_expand_sorted.argtypes = [P(OrcCfg), ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
+                                        ctypes.c_uint64, P(ctypes.c_uint64)]
+        L.orc_expand_sorted.restype = ctypes.c_int
         for f in (L.orc_fulltrace, L.orc_fulltrace_mt, L.orc_clean, L.orc_faithful, L.orc_expand):
             f.restype = ctypes.c_int
         _lib = L
@@ -130,6 +133,33 @@ def expand(c, seed, ref, first, n):
     if rc:
         raise RuntimeError(f"orc_expand rc={rc}")
     return out
+
+
+def expand_sorted(c, seed, ref, total, first, n):
+    """Samples [first, first+n) of the key-order stratified list of `total`
+    samples of reference `ref`."""
+    out = np.empty(n, dtype=np.uint64)
+    rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
+    rc = lib().orc_expand_sorted(ctypes.byref(c), seed, rid, total, first, n,
+                                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+    if rc:
+        raise RuntimeError(f"orc_expand_sorted rc={rc}")
+    return out
+
+
+def sort_key(N, T, CS, samples):
+    """Faithful sort key a*T + tid of packed samples, numpy."""
+    s = np.asarray(samples, dtype=np.uint64)
+    m = np.uint64(0xFFFFF)
+    ref = (s >> np.uint64(60)).astype(np.int64)
+    c0 = ((s >> np.uint64(40)) & m).astype(np.int64)
+    c1 = ((s >> np.uint64(20)) & m).astype(np.int64)
+    c2 = (s & m).astype(np.int64)
+    k = c0 // CS
+    t, q = k % T, (k // T) * CS + c0 % CS
+    off = np.where(ref < 2, ref, ref + 4 * c2)
+    S = 4 * N + 2
+    return ((q * N * S + c1 * S + off) * T + t).astype(np.uint64)
 
 
 def pack(ref, c0, c1, c2=0):

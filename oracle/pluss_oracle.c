@@ -31,6 +31,8 @@
  *   orc_expand     — the sample-list bijection (spec in DESIGN.md §4).  Written
  *                    independently of the device implementation so the two
  *                    can be compared.
+ *   orc_expand_sorted — the key-order stratified list (spec in DESIGN.md §4),
+ *                    plain 128-bit arithmetic, for the same comparison.
  *
  * Reference ids (access order inside one c1 iteration, pluss seq.cpp:102-288):
  *   0=C0 C[c0][c1]  1=C1 C[c0][c1]  2=A0 A[c0][c2]  3=B0 B[c2][c1]
@@ -547,6 +549,63 @@ int orc_expand(const orc_cfg *c, uint64_t seed, int ref, uint64_t first, uint64_
         if (dim3) { c2 = y % m; y /= m; }
         c1 = y % m; c0 = y / m;
         out[i] = ((uint64_t)ref << 60) | (c0 << 40) | (c1 << 20) | c2;
+    }
+    return 0;
+}
+
+/* --------------------------------------- key-order stratified lists -- */
+/* the valid points of reference `ref` in key order (q, c1, c2,
+   tid; block A: q < QA, all tids; block B: q = Q-1, tid < T-1 when span < N),
+   S samples split in proportion to the block sizes, one per stratum at a keyed
+   offset.  Needs N % (CS*T) == 0, 1 <= S <= span^d, S < 2^32. */
+static uint32_t lowbias32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16; return x;
+}
+int orc_expand_sorted(const orc_cfg *c, uint64_t seed, int ref, uint64_t S, uint64_t first, uint64_t n,
+                      uint64_t *out) {
+    if (!cfg_ok(c) || ref < 0 || ref > 5 || c->N % (c->CS * c->T)) return -1;
+    const int dim3 = !(ref == R_C0 || ref == R_C1);
+    const uint64_t span = c->range_full ? (uint64_t)c->N : (uint64_t)c->N - 1;
+    const uint64_t T = (uint64_t)c->T, Q = (uint64_t)(c->N / c->T);
+    const uint64_t M = dim3 ? span * span : span;
+    const uint64_t QA = c->range_full ? Q : Q - 1;
+    const uint64_t DA = QA * M * T, DB = c->range_full ? 0 : M * (T - 1), D = DA + DB;
+    if (S < 1 || S > D || S >= (1ull << 32) || first + n > S) return -2;
+    const uint64_t SA = (uint64_t)(((unsigned __int128)S * DA) / D);
+    const uint64_t h = mix64(seed ^ ((uint64_t)(ref + 1) * 0x9E3779B97F4A7C15ull) ^ 0xA5A5A5A55A5A5A5Aull);
+    const uint32_t k0 = (uint32_t)h, k1 = (uint32_t)(h >> 32);
+    uint64_t lenmax = 0;
+    for (int b = 0; b < 2; b++) {
+        uint64_t SX = b ? S - SA : SA, DX = b ? DB : DA;
+        if (!SX) continue;
+        uint64_t len = DX / SX + (DX % SX ? 1 : 0);
+        if (len > lenmax) lenmax = len;
+    }
+    const int wide = lenmax > (1ull << 32);
+    for (uint64_t x = 0; x < n; x++) {
+        const uint64_t i = first + x;
+        const int b = i >= SA;
+        const uint64_t j = b ? i - SA : i, SX = b ? S - SA : SA, DX = b ? DB : DA;
+        const uint64_t g = DX / SX, rr = DX % SX;
+        const uint64_t lo = j * g + (j < rr ? j : rr), len = g + (j < rr);
+        const uint32_t uh = lowbias32((uint32_t)i ^ k0);
+        uint64_t off;
+        if (wide) {
+            const uint64_t u = ((uint64_t)uh << 32) | lowbias32((uint32_t)i ^ k1);
+            off = (uint64_t)(((unsigned __int128)u * len) >> 64);
+        } else {
+            off = ((uint64_t)uh * len) >> 32;
+        }
+        uint64_t p = lo + off;
+        const uint64_t tr = b ? T - 1 : T;
+        const uint64_t tid = p % tr;
+        p /= tr;
+        uint64_t c2 = 0;
+        if (dim3) { c2 = p % span; p /= span; }
+        const uint64_t c1 = p % span;
+        const uint64_t q = b ? Q - 1 : p / span;
+        const uint64_t c0 = ((q / c->CS) * T + tid) * c->CS + q % c->CS;
+        out[x] = ((uint64_t)ref << 60) | (c0 << 40) | (c1 << 20) | c2;
     }
     return 0;
 }

@@ -19,13 +19,15 @@ ERRORS = {-1: "PLUSS_ERR_CONFIG", -2: "PLUSS_ERR_HIP", -3: "PLUSS_ERR_ALLOC", -4
 EXPORTS = [
     "pluss_last_error", "pluss_device_count", "pluss_version",
     "pluss_gemm_sampled_hist", "pluss_gemm_fulltrace_hist", "pluss_gemm_sampled_ri", "pluss_expand_samples",
-    "pluss_default_counts",
+    "pluss_default_counts", "pluss_expand_sorted", "pluss_dev_expand_sorted",
     "pluss_ctx_create", "pluss_ctx_destroy", "pluss_ctx_stream", "pluss_dev_expand", "pluss_dev_hist_reset",
-    "pluss_dev_sampled_hist", "pluss_dev_faithful_hist", "pluss_dev_faithful_hist_refs", "pluss_dev_fulltrace_hist", "pluss_dev_sampled_ri",
+    "pluss_dev_sampled_hist", "pluss_dev_faithful_hist", "pluss_dev_faithful_hist_refs",
+    "pluss_dev_faithful_hist_sorted", "pluss_dev_faithful_hist_sorted_refs", "pluss_dev_gen_faithful_refs",
+    "pluss_dev_fulltrace_hist", "pluss_dev_sampled_ri",
     "pluss_dev_hist_export", "pluss_dev_hist_export_reset", "pluss_dev_sampled_hist_export", "pluss_hist_fetch",
     "pluss_hist_from_tables", "pluss_faithful_key_space", "pluss_dev_faithful_shard_keys",
     "pluss_dev_faithful_shard_starts", "pluss_dev_faithful_shard_cut", "pluss_dev_faithful_shard_hist",
-    "pluss_dense_keys", "pluss_dev_sampled_hist_dense",
+    "pluss_dense_keys", "pluss_dev_sampled_hist_dense", "pluss_dev_gen_count_dense",
 ]
 # include/pluss_diag.h (diagnostics, not the drop-in boundary)
 DIAG_EXPORTS = ["pluss_diag_dense"]
@@ -90,6 +92,8 @@ def lib():
         "pluss_gemm_sampled_ri": (ctypes.c_int, [cfgp, vp, u64, vp, vp]),
         "pluss_expand_samples": (ctypes.c_int, [cfgp, u64, i32, u64, u64, vp]),
         "pluss_default_counts": (ctypes.c_int, [i64, u64, P(u64)]),
+        "pluss_expand_sorted": (ctypes.c_int, [cfgp, u64, i32, u64, u64, u64, vp]),
+        "pluss_dev_expand_sorted": (ctypes.c_int, [vp, u64, i32, u64, u64, u64, vp, vp]),
         "pluss_ctx_create": (ctypes.c_int, [cfgp, P(vp)]),
         "pluss_ctx_destroy": (ctypes.c_int, [vp]),
         "pluss_ctx_stream": (vp, [vp]),
@@ -98,6 +102,9 @@ def lib():
         "pluss_dev_sampled_hist": (ctypes.c_int, [vp, vp, u64, vp]),
         "pluss_dev_faithful_hist": (ctypes.c_int, [vp, i32, vp, u64, vp]),
         "pluss_dev_faithful_hist_refs": (ctypes.c_int, [vp, vp, ctypes.POINTER(ctypes.c_uint64), vp]),
+        "pluss_dev_faithful_hist_sorted": (ctypes.c_int, [vp, i32, vp, u64, vp]),
+        "pluss_dev_faithful_hist_sorted_refs": (ctypes.c_int, [vp, vp, ctypes.POINTER(ctypes.c_uint64), vp]),
+        "pluss_dev_gen_faithful_refs": (ctypes.c_int, [vp, u64, ctypes.POINTER(ctypes.c_uint64), vp]),
         "pluss_dev_fulltrace_hist": (ctypes.c_int, [vp, vp]),
         "pluss_dev_sampled_ri": (ctypes.c_int, [vp, vp, u64, vp, vp, vp]),
         "pluss_dev_hist_export": (ctypes.c_int, [vp, vp, vp, u64, vp]),
@@ -112,6 +119,7 @@ def lib():
         "pluss_dev_faithful_shard_hist": (ctypes.c_int, [vp, u64, u64, i32, vp]),
         "pluss_dense_keys": (ctypes.c_int, [cfgp, P(u64)]),
         "pluss_dev_sampled_hist_dense": (ctypes.c_int, [vp, vp, u64, vp, vp]),
+        "pluss_dev_gen_count_dense": (ctypes.c_int, [vp, u64, P(u64), P(u64), P(u64), vp, vp]),
         "pluss_diag_dense": (ctypes.c_int, [vp, vp, u64, vp, i32, i32, vp]),
     }
     for name, (res, args) in sig.items():

@@ -159,6 +159,17 @@ def expand_samples(cfg, seed, ref, first, n):
     return out
 
 
+def expand_sorted(cfg, seed, ref, total, first, n):
+    """Samples [first, first+n) of reference `ref`'s key-order stratified list of
+    `total` samples (generated in r10's pop order: no sort needed in faithful mode)."""
+    out = np.empty(n, dtype=np.uint64)
+    c = cfg.to_c()
+    rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
+    check(lib().pluss_expand_sorted(ctypes.byref(c), seed, rid, total, first, n, out.ctypes.data_as(ctypes.c_void_p)),
+          "pluss_expand_sorted")
+    return out
+
+
 def default_counts(n, total):
     counts = (ctypes.c_uint64 * 6)()
     check(lib().pluss_default_counts(n, total, counts), "pluss_default_counts")
@@ -233,6 +244,11 @@ class Context:
         rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
         check(lib().pluss_dev_expand(self._h, seed, rid, first, n, d_out, stream), "pluss_dev_expand")
 
+    def expand_sorted(self, seed, ref, total, first, n, d_out, stream=None):
+        rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
+        check(lib().pluss_dev_expand_sorted(self._h, seed, rid, total, first, n, d_out, stream),
+              "pluss_dev_expand_sorted")
+
     def sampled_hist(self, d_samples, n, stream=None):
         check(lib().pluss_dev_sampled_hist(self._h, d_samples, n, stream), "pluss_dev_sampled_hist")
 
@@ -246,6 +262,21 @@ class Context:
         reference 1, ...  Same result as six faithful_hist calls."""
         c = (ctypes.c_uint64 * 6)(*[int(x) for x in counts])
         check(lib().pluss_dev_faithful_hist_refs(self._h, d_samples, c, stream), "pluss_dev_faithful_hist_refs")
+
+    def faithful_hist_sorted(self, ref, d_samples, n, stream=None):
+        """faithful_hist over a list already in key order (no sort; checked)."""
+        rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
+        check(lib().pluss_dev_faithful_hist_sorted(self._h, rid, d_samples, n, stream), "pluss_dev_faithful_hist_sorted")
+
+    def faithful_hist_sorted_refs(self, d_samples, counts, stream=None):
+        c = (ctypes.c_uint64 * 6)(*[int(x) for x in counts])
+        check(lib().pluss_dev_faithful_hist_sorted_refs(self._h, d_samples, c, stream),
+              "pluss_dev_faithful_hist_sorted_refs")
+
+    def gen_faithful_refs(self, seed, totals, stream=None):
+        """The six samplers over generated key-order lists (never materialised)."""
+        c = (ctypes.c_uint64 * 6)(*[int(x) for x in totals])
+        check(lib().pluss_dev_gen_faithful_refs(self._h, seed, c, stream), "pluss_dev_gen_faithful_refs")
 
     def fulltrace(self, stream=None):
         check(lib().pluss_dev_fulltrace_hist(self._h, stream), "pluss_dev_fulltrace_hist")
@@ -269,6 +300,13 @@ class Context:
         """One launch: this pass's dense counts (DENSE_BINS + 1 u64 at d_counts; see dense_keys)."""
         check(lib().pluss_dev_sampled_hist_dense(self._h, d_samples, n, d_counts, stream),
               "pluss_dev_sampled_hist_dense")
+
+    def gen_count_dense(self, seed, totals, first, n, d_counts, stream=None):
+        """Generate slices [first[r], first[r]+n[r]) of the six key-order lists and
+        count them (dense vector) in one launch; the lists never touch memory."""
+        a = [(ctypes.c_uint64 * 6)(*[int(x) for x in v]) for v in (totals, first, n)]
+        check(lib().pluss_dev_gen_count_dense(self._h, seed, a[0], a[1], a[2], d_counts, stream),
+              "pluss_dev_gen_count_dense")
 
     def diag_dense(self, d_samples, n, d_counts, variant=0, max_grid=0, stream=None):
         """Diagnostics (include/pluss_diag.h): a dense pass with an ablation variant

@@ -173,11 +173,11 @@ int pluss_ctx_destroy(pluss_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->d_table,  c->d_exp_keys, c->d_exp_counts, c->d_exp_n, c->fb.keys,  c->fb.sinks,
                   c->fb.keys_s, c->fb.sinks_s, c->fb.pmax,      c->fb.nstart, c->fb.tmp,
-                  c->fb.scal, c->fb.st};
+                  c->fb.scal, c->fb.st, c->fb.dst, c->fb.dpart};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (const auto& f : c->fbr) {
-    void* fr[] = {f.keys, f.sinks, f.keys_s, f.sinks_s, f.pmax, f.nstart, f.tmp, f.scal, f.st};
+    void* fr[] = {f.keys, f.sinks, f.keys_s, f.sinks_s, f.pmax, f.nstart, f.tmp, f.scal, f.st, f.dst, f.dpart};
     for (void* p : fr)
       if (p) (void)hipFree(p);
   }
@@ -212,6 +212,22 @@ int pluss_dev_faithful_hist_refs(pluss_ctx* ctx, const uint64_t* d_samples, cons
   return launch_faithful_refs(ctx, d_samples, counts, pick(ctx, stream));
 }
 
+int pluss_dev_faithful_hist_sorted(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, void* stream) {
+  if (!ctx || (!d_samples && n) || ref < 0 || ref > 5) return PLUSS_ERR_CONFIG;
+  return launch_faithful_sorted(ctx, ref, d_samples, n, pick(ctx, stream));
+}
+
+int pluss_dev_faithful_hist_sorted_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t counts[6],
+                                        void* stream) {
+  if (!ctx || !counts) return PLUSS_ERR_CONFIG;
+  return launch_faithful_sorted_refs(ctx, d_samples, counts, pick(ctx, stream));
+}
+
+int pluss_dev_gen_faithful_refs(pluss_ctx* ctx, uint64_t seed, const uint64_t totals[6], void* stream) {
+  if (!ctx || !totals) return PLUSS_ERR_CONFIG;
+  return launch_gen_faithful_refs(ctx, seed, totals, pick(ctx, stream));
+}
+
 int pluss_dev_fulltrace_hist(pluss_ctx* ctx, void* stream) {
   if (!ctx) return PLUSS_ERR_CONFIG;
   return launch_fulltrace(ctx, pick(ctx, stream));  // the kernel also adds N*N*(4N+2) to traversed[0]
@@ -227,6 +243,12 @@ int pluss_dev_expand(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t first,
                      void* stream) {
   if (!ctx || ref < 0 || ref > 5 || (n && !d_out)) return PLUSS_ERR_CONFIG;
   return launch_expand(ctx, seed, ref, first, n, d_out, pick(ctx, stream));
+}
+
+int pluss_dev_expand_sorted(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t total, uint64_t first, uint64_t n,
+                            uint64_t* d_out, void* stream) {
+  if (!ctx || ref < 0 || ref > 5 || (n && !d_out)) return PLUSS_ERR_CONFIG;
+  return launch_expand_sorted(ctx, seed, ref, total, first, n, d_out, pick(ctx, stream));
 }
 
 int pluss_dev_hist_export(pluss_ctx* ctx, uint64_t* d_keys, uint64_t* d_counts, uint64_t cap, void* stream) {
@@ -262,6 +284,12 @@ int pluss_dev_sampled_hist_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint
                                  void* stream) {
   if (!ctx || (!d_samples && n) || !d_counts) return PLUSS_ERR_CONFIG;
   return launch_sampled_hist_dense(ctx, d_samples, n, (unsigned long long*)d_counts, pick(ctx, stream));
+}
+
+int pluss_dev_gen_count_dense(pluss_ctx* ctx, uint64_t seed, const uint64_t totals[6], const uint64_t first[6],
+                              const uint64_t n[6], uint64_t* d_counts, void* stream) {
+  if (!ctx || !totals || !first || !n || !d_counts) return PLUSS_ERR_CONFIG;
+  return launch_gen_count_dense(ctx, seed, totals, first, n, (unsigned long long*)d_counts, pick(ctx, stream));
 }
 
 int pluss_diag_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, uint64_t* d_counts, int32_t variant,
@@ -434,6 +462,22 @@ int pluss_expand_samples(const pluss_cfg* cfg, uint64_t seed, int32_t ref, uint6
   PLUSS_HIP_CHECK(hipMalloc((void**)&d, n * 8));
   sc.bufs.push_back(d);
   if (int rc = launch_expand(sc.ctx, seed, ref, first, n, d, sc.ctx->stream)) return rc;
+  PLUSS_HIP_CHECK(hipStreamSynchronize(sc.ctx->stream));
+  PLUSS_HIP_CHECK(hipMemcpy(out, d, n * 8, hipMemcpyDeviceToHost));
+  return PLUSS_OK;
+}
+
+int pluss_expand_sorted(const pluss_cfg* cfg, uint64_t seed, int32_t ref, uint64_t total, uint64_t first, uint64_t n,
+                        uint64_t* out) {
+  if ((n && !out) || ref < 0 || ref > 5) return PLUSS_ERR_CONFIG;
+  Scoped sc;
+  if (int rc = pluss_ctx_create(cfg, &sc.ctx)) return rc;
+  if (int rc = keygen_check(sc.ctx, ref, total, first, n, "pluss_expand_sorted")) return rc;
+  if (!n) return PLUSS_OK;
+  uint64_t* d = nullptr;
+  PLUSS_HIP_CHECK(hipMalloc((void**)&d, n * 8));
+  sc.bufs.push_back(d);
+  if (int rc = launch_expand_sorted(sc.ctx, seed, ref, total, first, n, d, sc.ctx->stream)) return rc;
   PLUSS_HIP_CHECK(hipStreamSynchronize(sc.ctx->stream));
   PLUSS_HIP_CHECK(hipMemcpy(out, d, n * 8, hipMemcpyDeviceToHost));
   return PLUSS_OK;

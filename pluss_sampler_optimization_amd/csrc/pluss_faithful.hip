@@ -531,6 +531,9 @@ __device__ __forceinline__ unsigned long long fu_chain(unsigned long long* st, u
 // gbase + li, li in [0, mt); src.word(li) is element li's packed word and
 // src.key_after(li) the key of the global element after it (KEY_EMPTY past
 // the end).  t is the tile's look-back index (tiles in global order).
+// Src::kCheck: the source is a caller's list that must be in key order;
+// an element whose successor's key is not larger is reported through
+// src.unordered() (the bad-input flag).
 // scal: [0] cut (= n beforehand); st: 2 * ntiles zeroed words; part: FPART
 // words per tile (written, not accumulated).
 template <int FM, class Src>
@@ -543,8 +546,6 @@ __device__ __forceinline__ void fused_tile(const Src& src, uint32_t t, uint64_t 
   __shared__ unsigned long long s_w[NW], s_inm, s_inc, s_red[NW][FPART];
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
   const uint32_t lbase = wid * (64 * FI);
-  // Src::kReload (the tile sits in LDS): words and keys are re-read where
-  // needed instead of being held in registers across the look-backs
   KT w[FI];
   unsigned long long tm = 0;
 #pragma unroll
@@ -554,7 +555,6 @@ __device__ __forceinline__ void fused_tile(const Src& src, uint32_t t, uint64_t 
     const unsigned long long sk = li < mt ? pk_sink(w[k], pv) : 0ull;
     tm = sk > tm ? sk : tm;
   }
-  auto word_at = [&](int k, uint32_t li) -> KT { return Src::kReload ? (li < mt ? src.word(li) : (KT)0) : w[k]; };
   // prefix max of sinks
   {
     const unsigned long long wagg = sc_wave_red<true>(st_cap(tm));
@@ -577,13 +577,13 @@ __device__ __forceinline__ void fused_tile(const Src& src, uint32_t t, uint64_t 
     const uint32_t li = lbase + (uint32_t)k * 64 + lane;
     const uint64_t i = gbase + li;
     const bool valid = li < mt;
-    const KT wk = word_at(k, li);
+    const KT wk = w[k];
     unsigned long long inc = sc_wave_scan<true>(valid ? pk_sink(wk, pv) : 0ull, lane);
     inc = inc > carry ? inc : carry;
     const unsigned long long up = __shfl_up(inc, 1, 64);
     const unsigned long long before = lane ? up : carry;
     const unsigned long long kk = valid ? pk_key(wk, pv) : KEY_EMPTY;
-    if (!Src::kReload) key[k] = kk;
+    key[k] = kk;
     fmask[k] = __ballot(valid && (i == 0 || kk > before));
     wcnt += (uint32_t)__popcll(fmask[k]);
     pm[k] = inc;
@@ -628,25 +628,22 @@ __device__ __forceinline__ void fused_tile(const Src& src, uint32_t t, uint64_t 
   // record the tile's elements below its own cut
   unsigned long long cold = 0, trav = 0;
   uint32_t nc0 = 0, nc1 = 0, nc2 = 0;
+  bool unordered = false;
 #pragma unroll
   for (int k = 0; k < FI; ++k) {
     const uint32_t li = lbase + (uint32_t)k * 64 + lane;
     const uint64_t i = gbase + li;
-    const KT wk = word_at(k, li);
-    const unsigned long long kk = Src::kReload ? (li < mt ? pk_key(wk, pv) : KEY_EMPTY) : key[k];
+    const KT wk = w[k];
+    const unsigned long long kk = key[k];
     // the next element's key: the next lane, the next round's lane 0, or (the wave's last element) the source
-    unsigned long long kn;
-    if (Src::kReload) {
+    unsigned long long kn = __shfl_down(kk, 1, 64);
+    if (k + 1 < FI) {
+      const unsigned long long k0 = __shfl(key[k + 1], 0, 64);
+      if (lane == 63) kn = k0;
+    } else if (lane == 63) {
       kn = li < mt ? src.key_after(li) : KEY_EMPTY;
-    } else {
-      kn = __shfl_down(kk, 1, 64);
-      if (k + 1 < FI) {
-        const unsigned long long k0 = __shfl(key[k + 1], 0, 64);
-        if (lane == 63) kn = k0;
-      } else if (lane == 63) {
-        kn = li < mt ? src.key_after(li) : KEY_EMPTY;
-      }
     }
+    if (Src::kCheck && li < mt && i + 1 < n && !(kn > kk)) unordered = true;
     uint32_t c = 3;
     bool rec = false;
     if (li < mt && i < cut) {
@@ -661,6 +658,7 @@ __device__ __forceinline__ void fused_tile(const Src& src, uint32_t t, uint64_t 
     nc1 += (uint32_t)__popcll(__ballot(rec && c == 1));
     nc2 += (uint32_t)__popcll(__ballot(rec && c == 2));
   }
+  if (Src::kCheck && __ballot(unordered) && lane == 0) src.unordered();
   cold = sc_wave_red<false>(cold);
   trav = sc_wave_red<false>(trav);
   if (lane == 0) {
@@ -682,7 +680,7 @@ __device__ __forceinline__ void fused_tile(const Src& src, uint32_t t, uint64_t 
 // Tiles of FCHUNK consecutive sorted words (the rocPRIM-sorted array).
 template <int FM>
 struct GlobalTile {
-  static constexpr bool kReload = false;
+  static constexpr bool kCheck = false;
   const fkey_t<FM>* wd;
   uint64_t gbase, n;
   PkView pv;
@@ -691,6 +689,47 @@ struct GlobalTile {
     const uint64_t i = gbase + li + 1;
     return i < n ? pk_key(wd[i], pv) : KEY_EMPTY;
   }
+  __device__ void unordered() const {}
+};
+
+// Tiles of FCHUNK consecutive samples of a caller's list that is already in
+// key order (pluss_dev_faithful_hist_sorted): each sample's packed word is
+// made where it is read -- no keys pass, no sort -- and the order is checked.
+template <int FM>
+struct SampleTile {
+  static constexpr bool kCheck = true;
+  const uint64_t* smp;
+  uint64_t gbase, n;
+  const Model* m;
+  uint32_t ref;
+  PkView pv;
+  GTable g;
+  __device__ fkey_t<FM> word(uint32_t li) const { return pk_word_of<fkey_t<FM>>(*m, ref, smp[gbase + li], g); }
+  __device__ unsigned long long key_after(uint32_t li) const {
+    const uint64_t i = gbase + li + 1;
+    return i < n ? pk_key(pk_word_of<fkey_t<FM>>(*m, ref, smp[i], g), pv) : KEY_EMPTY;
+  }
+  __device__ void unordered() const { atomicOr(&g.flags[1], 1u); }
+};
+
+// Tiles of a generated key-order list (pluss_dev_gen_faithful_refs): the
+// samples never exist in memory.
+template <int FM>
+struct GenTile {
+  static constexpr bool kCheck = false;
+  const KeyGen* k;
+  uint64_t gbase, n;
+  const Model* m;
+  PkView pv;
+  GTable g;
+  __device__ fkey_t<FM> word(uint32_t li) const {
+    return pk_word_of<fkey_t<FM>>(*m, k->ref, keygen_sample(*k, gbase + li), g);
+  }
+  __device__ unsigned long long key_after(uint32_t li) const {
+    const uint64_t i = gbase + li + 1;
+    return i < n ? pk_key(pk_word_of<fkey_t<FM>>(*m, k->ref, keygen_sample(*k, i), g), pv) : KEY_EMPTY;
+  }
+  __device__ void unordered() const {}
 };
 
 // scal: [0] cut (= n beforehand), [4] tile counter; st: 2 * fu_tiles(n) zeroed words;
@@ -708,6 +747,29 @@ __global__ __launch_bounds__(FB) void k_faith_fused(const void* __restrict__ wor
   const uint32_t mt = (uint32_t)(n - gbase < FCHUNK ? n - gbase : FCHUNK);
   const GlobalTile<FM> src{static_cast<const fkey_t<FM>*>(words), gbase, n, pv};
   fused_tile<FM>(src, t, gbase, mt, pv, n, endkey, st, fu_tiles(n), part, scal);
+}
+
+// The same pass straight over a key-ordered sample list (GEN = false) or a
+// generated key-order list (GEN = true, `smp` unused).
+template <int FM, bool GEN>
+__global__ __launch_bounds__(FB) void k_faith_fused_direct(Model m, uint32_t ref, const uint64_t* __restrict__ smp,
+                                                           KeyGen kg, PkView pv, uint64_t n, unsigned long long endkey,
+                                                           unsigned long long* st,
+                                                           unsigned long long* __restrict__ part,
+                                                           unsigned long long* scal, GTable g) {
+  __shared__ unsigned long long s_tile;
+  if (threadIdx.x == 0) s_tile = atomicAdd(&scal[4], 1ull);
+  __syncthreads();
+  const uint32_t t = (uint32_t)s_tile;
+  const uint64_t gbase = (uint64_t)t * FCHUNK;
+  const uint32_t mt = (uint32_t)(n - gbase < FCHUNK ? n - gbase : FCHUNK);
+  if (GEN) {
+    const GenTile<FM> src{&kg, gbase, n, &m, pv, g};
+    fused_tile<FM>(src, t, gbase, mt, pv, n, endkey, st, fu_tiles(n), part, scal);
+  } else {
+    const SampleTile<FM> src{smp, gbase, n, &m, ref, pv, g};
+    fused_tile<FM>(src, t, gbase, mt, pv, n, endkey, st, fu_tiles(n), part, scal);
+  }
 }
 
 // Sum the partials of the tiles that start below the cut, then what
@@ -1115,9 +1177,93 @@ int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint
   return faith_pipeline_sorted(ctx, b, ref, d_samples, n, s);
 }
 
-// All six sampler_<REF> of one list at once, like r10's main, which runs
-// each on its own thread (r10:3203-3257): reference r's pipeline runs on its
-// own stream with its own buffers, forked from s and joined back into it.
+// ---- direct passes over key-ordered lists: no keys pass, no sort.  One
+// launch of k_faith_fused_direct (FCHUNK-element tiles chained by decoupled
+// look-back) and the finish kernel.
+static int faith_direct_shape(const pluss_ctx* ctx, const char* api) {
+  if (int rc = faith_check_shape(ctx)) return rc;
+  if (!ctx->m.fast) {
+    set_error(std::string(api) + ": needs N % (cls/ds) == 0 (packed words); use pluss_dev_faithful_hist");
+    return PLUSS_ERR_CONFIG;
+  }
+  return PLUSS_OK;
+}
+
+static int faith_reserve_direct(FaithfulBufs& b, uint64_t n, hipStream_t s) {
+  if (!b.scal) {
+    if (int rc = grow(&b.scal, 8)) return rc;
+  }
+  if (n > 0xFFFFFFFFull) {
+    set_error("faithful mode: at most 2^32-1 samples per reference");
+    return PLUSS_ERR_CONFIG;
+  }
+  const uint64_t nt = fu_tiles(n);
+  if (nt > b.dcap) {
+    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+    int rc = 0;
+    if ((rc = grow(&b.dst, 2 * nt)) || (rc = grow(&b.dpart, nt * FPART))) return rc;
+    b.dcap = nt;
+  }
+  return PLUSS_OK;
+}
+
+// kg == nullptr: the samples are read from d_samples (checked to be in key order)
+static int faith_pipeline_direct(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, const uint64_t* d_samples,
+                                 const KeyGen* kg, uint64_t n, hipStream_t s) {
+  if (n == 0) return PLUSS_OK;
+  const Model& m = ctx->m;
+  const uint64_t nt = fu_tiles(n);
+  hipLaunchKernelGGL(k_faith_scan_init, dim3((unsigned)std::min<uint64_t>((2 * nt + BLOCK - 1) / BLOCK + 1, 64)),
+                     dim3(BLOCK), 0, s, b.scal, n, b.dst, 2 * nt);
+  const PkView pv = make_pkview(m, (uint32_t)ref);
+  const unsigned long long endkey = m.A * m.T;
+  const KeyGen k = kg ? *kg : KeyGen{};
+  const bool pk32 = faith_fm(m) == FM_PK32;
+#define PLUSS_DIRECT(FMV, GENV)                                                                                  \
+  hipLaunchKernelGGL((k_faith_fused_direct<FMV, GENV>), dim3((unsigned)nt), dim3(FB), 0, s, m, (uint32_t)ref, \
+                     d_samples, k, pv, n, endkey, b.dst, b.dpart, b.scal, ctx->g)
+  if (kg) {
+    if (pk32) PLUSS_DIRECT(FM_PK32, true);
+    else PLUSS_DIRECT(FM_PK64, true);
+  } else {
+    if (pk32) PLUSS_DIRECT(FM_PK32, false);
+    else PLUSS_DIRECT(FM_PK64, false);
+  }
+#undef PLUSS_DIRECT
+  hipLaunchKernelGGL(k_faith_fused_finish, dim3(1), dim3(BLOCK), 0, s, (uint32_t)ref, n, pv, b.dst, nt, b.dpart,
+                     b.scal, ctx->g);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  ctx->tables_dirty = true;
+  return PLUSS_OK;
+}
+
+int launch_faithful_sorted(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s) {
+  if (int rc = faith_direct_shape(ctx, "pluss_dev_faithful_hist_sorted")) return rc;
+  if (int rc = faith_reserve_direct(ctx->fb, n, s)) return rc;
+  return faith_pipeline_direct(ctx, ctx->fb, ref, d_samples, nullptr, n, s);
+}
+
+// The six references' pipelines on streams of their own, forked from s and
+// joined back into it, as r10's main runs one thread per reference
+// (r10:3203-3257).  per_ref(r, buffers, stream) enqueues reference r.
+template <class F>
+static int fork_refs(pluss_ctx* ctx, const uint64_t* counts, hipStream_t s, F&& per_ref) {
+  if (!ctx->fst[0]) {
+    for (int r = 0; r < 6; ++r) PLUSS_HIP_CHECK(hipStreamCreateWithFlags(&ctx->fst[r], hipStreamNonBlocking));
+    for (int e = 0; e < 7; ++e) PLUSS_HIP_CHECK(hipEventCreateWithFlags(&ctx->fev[e], hipEventDisableTiming));
+  }
+  PLUSS_HIP_CHECK(hipEventRecord(ctx->fev[6], s));
+  for (int r = 0; r < 6; ++r) {
+    if (!counts[r]) continue;
+    PLUSS_HIP_CHECK(hipStreamWaitEvent(ctx->fst[r], ctx->fev[6], 0));
+    if (int rc = per_ref(r, ctx->fbr[r], ctx->fst[r])) return rc;
+    PLUSS_HIP_CHECK(hipEventRecord(ctx->fev[r], ctx->fst[r]));
+    PLUSS_HIP_CHECK(hipStreamWaitEvent(s, ctx->fev[r], 0));
+  }
+  return PLUSS_OK;
+}
+
+// All six sampler_<REF> of one list at once (radix-sort pipeline).
 int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t* counts, hipStream_t s) {
   if (int rc = faith_check_shape(ctx)) return rc;
   uint64_t off[6], total = 0;
@@ -1134,19 +1280,45 @@ int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64
     if (int rc = faith_reserve(ctx, ctx->fbr[r], counts[r], s)) return rc;
     if (int rc = faith_tmp(ctx, ctx->fbr[r], counts[r], s)) return rc;
   }
-  if (!ctx->fst[0]) {
-    for (int r = 0; r < 6; ++r) PLUSS_HIP_CHECK(hipStreamCreateWithFlags(&ctx->fst[r], hipStreamNonBlocking));
-    for (int e = 0; e < 7; ++e) PLUSS_HIP_CHECK(hipEventCreateWithFlags(&ctx->fev[e], hipEventDisableTiming));
-  }
-  PLUSS_HIP_CHECK(hipEventRecord(ctx->fev[6], s));
+  return fork_refs(ctx, counts, s, [&](int r, FaithfulBufs& b, hipStream_t rs) {
+    return faith_pipeline_sorted(ctx, b, r, d_samples + off[r], counts[r], rs);
+  });
+}
+
+// All six over a key-ordered list (each reference's block in key order).
+int launch_faithful_sorted_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t* counts, hipStream_t s) {
+  if (int rc = faith_direct_shape(ctx, "pluss_dev_faithful_hist_sorted_refs")) return rc;
+  uint64_t off[6], total = 0;
   for (int r = 0; r < 6; ++r) {
-    if (!counts[r]) continue;
-    PLUSS_HIP_CHECK(hipStreamWaitEvent(ctx->fst[r], ctx->fev[6], 0));
-    if (int rc = faith_pipeline_sorted(ctx, ctx->fbr[r], r, d_samples + off[r], counts[r], ctx->fst[r])) return rc;
-    PLUSS_HIP_CHECK(hipEventRecord(ctx->fev[r], ctx->fst[r]));
-    PLUSS_HIP_CHECK(hipStreamWaitEvent(s, ctx->fev[r], 0));
+    off[r] = total;
+    total += counts[r];
   }
-  return PLUSS_OK;
+  if (total && !d_samples) {
+    set_error("pluss_dev_faithful_hist_sorted_refs: null sample list");
+    return PLUSS_ERR_CONFIG;
+  }
+  for (int r = 0; r < 6; ++r)
+    if (counts[r])
+      if (int rc = faith_reserve_direct(ctx->fbr[r], counts[r], s)) return rc;
+  return fork_refs(ctx, counts, s, [&](int r, FaithfulBufs& b, hipStream_t rs) {
+    return faith_pipeline_direct(ctx, b, r, d_samples + off[r], nullptr, counts[r], rs);
+  });
+}
+
+// All six over generated key-order lists (pluss_expand_sorted's lists of
+// totals[r] samples, never written to memory).
+int launch_gen_faithful_refs(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t s) {
+  if (int rc = faith_direct_shape(ctx, "pluss_dev_gen_faithful_refs")) return rc;
+  KeyGen kg[6];
+  for (int r = 0; r < 6; ++r) {
+    if (!totals[r]) continue;
+    if (int rc = keygen_check(ctx, r, totals[r], 0, totals[r], "pluss_dev_gen_faithful_refs")) return rc;
+    kg[r] = keygen_of(ctx, seed, r, totals[r]);
+    if (int rc = faith_reserve_direct(ctx->fbr[r], totals[r], s)) return rc;
+  }
+  return fork_refs(ctx, totals, s, [&](int r, FaithfulBufs& b, hipStream_t rs) {
+    return faith_pipeline_direct(ctx, b, r, nullptr, &kg[r], totals[r], rs);
+  });
 }
 
 // ---- key-range shards (multi-GPU faithful mode; the caller exchanges the

@@ -63,6 +63,9 @@ struct FaithfulBufs {
   size_t tmp_bytes = 0;
   unsigned long long* scal = nullptr;  // [0] cut, [1] cold, [2] traversed, [3] shard size, [4] scan tile counter
   unsigned long long* st = nullptr;    // look-back status words of the one-GPU scan (2 per tile)
+  // direct passes over key-ordered / generated lists: look-back words and partials per FCHUNK tile
+  uint64_t dcap = 0;
+  unsigned long long *dst = nullptr, *dpart = nullptr;
 };
 
 // state of a key-range shard between the phases of pluss_dev_faithful_shard_*
@@ -116,6 +119,14 @@ int launch_ri_dump(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, int64_
                    hipStream_t s);
 int launch_expand(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t first, uint64_t n, uint64_t* d_out,
                   hipStream_t s);
+// key-order stratified lists (pluss_model.h KeyGen)
+int keygen_check(const pluss_ctx* ctx, int32_t ref, uint64_t total, uint64_t first, uint64_t n, const char* api);
+KeyGen keygen_of(const pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t total);
+int launch_expand_sorted(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t total, uint64_t first, uint64_t n,
+                         uint64_t* d_out, hipStream_t s);
+// generated key-order lists counted without materialising them (dense vector)
+int launch_gen_count_dense(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, const uint64_t* first,
+                           const uint64_t* n, unsigned long long* d_counts, hipStream_t s);
 int launch_export(pluss_ctx* ctx, unsigned long long* d_keys, unsigned long long* d_counts, uint64_t cap,
                   hipStream_t s, bool consume = false);
 // count a sample list and export-and-reset in one launch when only the direct
@@ -130,6 +141,10 @@ int launch_diag_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, uns
                       int variant, int max_grid, hipStream_t s);
 int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s);
 int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t* counts, hipStream_t s);
+// faithful mode over key-ordered lists (no sort) and generated key-order lists (no input)
+int launch_faithful_sorted(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s);
+int launch_faithful_sorted_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t* counts, hipStream_t s);
+int launch_gen_faithful_refs(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t s);
 int faith_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, uint64_t lo, uint64_t hi,
                      pluss_faith_shard* out, hipStream_t s);
 int faith_shard_starts(pluss_ctx* ctx, uint64_t j_off, uint64_t pmax_in, pluss_faith_shard* out, hipStream_t s);

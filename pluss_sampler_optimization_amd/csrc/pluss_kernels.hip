@@ -376,29 +376,30 @@ __device__ __forceinline__ void count_slot(const Model& m, uint64_t x, bool ok, 
   }
 }
 
-// All 2*UNR slots of a step (lane-pair u holds slots 2u, 2u+1; okm[u] = its
-// live lanes).  When every live sample of the step has the reference of the
+// All 2*UNR slots of a step (okm[k] = the live lanes of slot k; in k_count
+// lane-pair u holds slots 2u and 2u+1).  A lane whose slot k is live has its
+// slot 0 live too.  When every live sample of the step has the reference of the
 // first live lane (almost always), that reference's conditions are evaluated
 // for all slots in one straight-line block -- independent ballots the
 // scheduler interleaves -- and the counts are summed in scalar registers
 // before one lane-indexed add per bin.  Otherwise slot by slot.
 template <bool P2, bool NP2, int UNR>
 __device__ __forceinline__ void count_step(const Model& m, const uint32_t (&lo)[2 * UNR], const uint32_t (&hi)[2 * UNR],
-                                           const uint64_t (&okm)[UNR], uint32_t& acc) {
+                                           const uint64_t (&okm)[2 * UNR], uint32_t& acc) {
   constexpr int K = 2 * UNR;
   uint64_t any = 0;
 #pragma unroll
-  for (int u = 0; u < UNR; ++u) any |= okm[u];
+  for (int k = 0; k < 2 * UNR; ++k) any |= okm[k];
   if (any == 0) return;
   const int l0 = (int)__builtin_ctzll(any);
   const uint32_t r0 = __builtin_amdgcn_readlane(hi[0] >> 28, l0);  // slot 0 is live wherever any slot is
   uint64_t mixed = 0;
 #pragma unroll
-  for (int k = 0; k < K; ++k) mixed |= __ballot((hi[k] >> 28) != r0) & okm[k / 2];
+  for (int k = 0; k < K; ++k) mixed |= __ballot((hi[k] >> 28) != r0) & okm[k];
   if (r0 > 5 || mixed) {
 #pragma unroll
     for (int k = 0; k < K; ++k)
-      count_slot<P2, NP2>(m, ((uint64_t)hi[k] << 32) | lo[k], (okm[k / 2] >> __lane_id()) & 1, acc);
+      count_slot<P2, NP2>(m, ((uint64_t)hi[k] << 32) | lo[k], (okm[k] >> __lane_id()) & 1, acc);
     return;
   }
   uint32_t nbad = 0, ng = 0, na = 0, nb = 0;
@@ -413,8 +414,8 @@ __device__ __forceinline__ void count_step(const Model& m, const uint32_t (&lo)[
       const uint32_t c1 = __builtin_amdgcn_alignbit(hi[k], lo[k], 20) & 0xFFFFFu;
       bad = (c0 > c1 ? (c0 > c2 ? c0 : c2) : (c1 > c2 ? c1 : c2)) >= m.N;
     }
-    const uint64_t mb = __ballot(bad) & okm[k / 2];
-    good[k] = okm[k / 2] & ~mb;
+    const uint64_t mb = __ballot(bad) & okm[k];
+    good[k] = okm[k] & ~mb;
     nbad += (uint32_t)__popcll(mb);
     ng += (uint32_t)__popcll(good[k]);
   }
@@ -608,14 +609,14 @@ __global__ __launch_bounds__(BLOCK) void k_count(Model m, const uint64_t* __rest
         y[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                              rs, (int)((base + step + u * BLOCK + threadIdx.x) * 16u), 0, AUX));
       uint32_t lo[2 * UNR], hi[2 * UNR];
-      uint64_t okm[UNR];
+      uint64_t okm[2 * UNR];
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         lo[2 * u] = x[u].x;
         hi[2 * u] = x[u].y;
         lo[2 * u + 1] = x[u].z;
         hi[2 * u + 1] = x[u].w;
-        okm[u] = __ballot(base + u * BLOCK + threadIdx.x < wn);
+        okm[2 * u] = okm[2 * u + 1] = __ballot(base + u * BLOCK + threadIdx.x < wn);
       }
       if (ABL == 1) {  // diagnostics: the same loads, nothing counted
 #pragma unroll
@@ -649,6 +650,60 @@ __global__ __launch_bounds__(BLOCK) void k_count(Model m, const uint64_t* __rest
   if (TAIL == TAIL_DENSE) tail_dense(tot, g, ex.dense, ex.drows);
   else tail_accumulate(tot, g);
   if (TAIL == TAIL_EXPORT) tail_export(m, g, ex);
+}
+
+// ------------------------------------------------ generated and counted --
+// k_gen_count: the key-order lists of the six references (pluss_model.h
+// KeyGen) counted while they are generated -- the samples never touch
+// memory; = pluss_dev_expand_sorted of every slice + one dense pass.  A wave
+// step is GK = 2*UNROLL rounds of 64 consecutive samples of one reference
+// (lane l: samples base + 64k + l); each reference's slice is padded to whole
+// wave steps, so the reference, its generator and its case tests are
+// wave-uniform.  Counting and tail are k_count's.
+struct GenArgs {
+  KeyGen k[6];
+  uint64_t first[6], n[6];
+  uint64_t wbeg[7];  // first wave step of each reference; wbeg[6] = all steps
+};
+constexpr uint32_t GK = 2 * UNROLL;
+
+template <bool P2, bool NP2>
+__global__ __launch_bounds__(BLOCK) void k_gen_count(Model m, GenArgs ga, GTable g, ExportArgs ex) {
+  __shared__ unsigned long long tot[DBINS];
+  if (threadIdx.x < DBINS) tot[threadIdx.x] = 0;
+  uint32_t acc = 0;
+  LaneCounts lc;
+  lc_init(lc);
+  const uint32_t lane = __lane_id();
+  const uint64_t nw = (uint64_t)gridDim.x * (BLOCK / 64);
+  const uint64_t w0 = (uint64_t)blockIdx.x * (BLOCK / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (uint64_t ws = w0; ws < ga.wbeg[6]; ws += nw) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int x = 1; x < 6; ++x) r += ws >= ga.wbeg[x] ? 1u : 0u;
+    r = __builtin_amdgcn_readfirstlane(r);
+    const KeyGen& kg = ga.k[r];
+    const uint64_t rel = (ws - ga.wbeg[r]) * (GK * 64);  // this step's first sample within the slice
+    const uint64_t nr = ga.n[r];
+    uint32_t lo[GK], hi[GK];
+    uint64_t okm[GK];
+#pragma unroll
+    for (int k = 0; k < (int)GK; ++k) {
+      const uint64_t j = rel + (uint64_t)k * 64 + lane;
+      const bool ok = j < nr;
+      const uint64_t x = ok ? keygen_sample(kg, ga.first[r] + j) : 0ull;
+      lo[k] = (uint32_t)x;
+      hi[k] = (uint32_t)(x >> 32);
+      okm[k] = __ballot(ok);
+    }
+    if (!(P2 && NP2 && rel + GK * 64 <= nr && count_step_lanes<UNROLL>(m, lo, hi, lc)))
+      count_step<P2, NP2, UNROLL>(m, lo, hi, okm, acc);
+  }
+  if (P2 && NP2) lc_flush(lc, acc);
+  __syncthreads();
+  flush_counts(acc, tot);
+  __syncthreads();
+  tail_dense(tot, g, ex.dense, ex.drows);
 }
 
 // ----------------------------------------------------------- full trace --
@@ -891,6 +946,15 @@ __global__ __launch_bounds__(BLOCK) void k_expand(Perm p, uint32_t ref, uint64_t
   }
 }
 
+// ---------------------------------------------------- key-order lists --
+// Samples [first, first + n) of a reference's key-order stratified list
+// (pluss_model.h KeyGen), one lane per sample, coalesced stores.
+__global__ __launch_bounds__(BLOCK) void k_expand_sorted(KeyGen k, uint64_t first, uint64_t n,
+                                                         uint64_t* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK)
+    out[i] = keygen_sample(k, first + i);
+}
+
 // ------------------------------------------------------------ launchers --
 static int grid_for(uint64_t work, uint64_t per_block, int max_blocks = MAX_BLOCKS) {
   uint64_t b = (work + per_block - 1) / per_block;
@@ -1067,6 +1131,72 @@ int launch_expand(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t first, ui
   }
   const int nb = grid_for(n, BLOCK * 4, 4096);
   hipLaunchKernelGGL(k_expand, dim3(nb), dim3(BLOCK), 0, s, p, (uint32_t)ref, first, n, d_out);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  return PLUSS_OK;
+}
+
+int keygen_check(const pluss_ctx* ctx, int32_t ref, uint64_t total, uint64_t first, uint64_t n, const char* api) {
+  const pluss_cfg& c = ctx->cfg;
+  if ((uint64_t)c.n % ((uint64_t)c.chunk * (uint64_t)c.threads) != 0) {
+    set_error(std::string(api) + ": key-order lists need N % (chunk*threads) == 0");
+    return PLUSS_ERR_CONFIG;
+  }
+  const uint64_t span = c.range_full ? (uint64_t)c.n : (uint64_t)c.n - 1;
+  const uint64_t d = (ref == C0 || ref == C1) ? span * span : span * span * span;
+  if (total < 1 || total > d || total >= (1ull << 32)) {
+    set_error(std::string(api) + ": total must be in [1, min(span^d, 2^32 - 1)]");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (first > total || n > total - first) {
+    set_error(std::string(api) + ": [first, first + n) exceeds the list");
+    return PLUSS_ERR_CONFIG;
+  }
+  return PLUSS_OK;
+}
+
+KeyGen keygen_of(const pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t total) {
+  const pluss_cfg& c = ctx->cfg;
+  return make_keygen((uint64_t)c.n, (uint64_t)c.threads, (uint64_t)c.chunk, c.range_full != 0, seed, (uint32_t)ref,
+                     total);
+}
+
+int launch_expand_sorted(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t total, uint64_t first, uint64_t n,
+                         uint64_t* d_out, hipStream_t s) {
+  if (int rc = keygen_check(ctx, ref, total, first, n, "pluss_expand_sorted")) return rc;
+  if (n == 0) return PLUSS_OK;
+  const KeyGen k = keygen_of(ctx, seed, ref, total);
+  hipLaunchKernelGGL(k_expand_sorted, dim3(grid_for(n, BLOCK * 4, 4096)), dim3(BLOCK), 0, s, k, first, n, d_out);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  return PLUSS_OK;
+}
+
+int launch_gen_count_dense(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, const uint64_t* first,
+                           const uint64_t* n, unsigned long long* d_counts, hipStream_t s) {
+  if (int rc = dense_check(ctx, d_counts, "pluss_dev_gen_count_dense")) return rc;
+  GenArgs ga;
+  ga.wbeg[0] = 0;
+  for (int r = 0; r < 6; ++r) {
+    ga.first[r] = first[r];
+    ga.n[r] = n[r];
+    ga.k[r] = KeyGen{};
+    if (n[r]) {
+      if (int rc = keygen_check(ctx, r, totals[r], first[r], n[r], "pluss_dev_gen_count_dense")) return rc;
+      ga.k[r] = keygen_of(ctx, seed, r, totals[r]);
+    }
+    ga.wbeg[r + 1] = ga.wbeg[r] + (n[r] + GK * 64 - 1) / (GK * 64);
+  }
+  const ExportArgs ex{nullptr, nullptr, 0, nullptr, d_counts, DENSE_ROWS};
+  // ALU-bound: 8 waves per SIMD
+  const int nb = grid_for(ga.wbeg[6] ? ga.wbeg[6] : 1, BLOCK / 64, 2048);
+  const Model& m = ctx->m;
+  if (m.p2 && m.np2)
+    hipLaunchKernelGGL((k_gen_count<true, true>), dim3(nb), dim3(BLOCK), 0, s, m, ga, ctx->g, ex);
+  else if (m.p2)
+    hipLaunchKernelGGL((k_gen_count<true, false>), dim3(nb), dim3(BLOCK), 0, s, m, ga, ctx->g, ex);
+  else if (m.np2)
+    hipLaunchKernelGGL((k_gen_count<false, true>), dim3(nb), dim3(BLOCK), 0, s, m, ga, ctx->g, ex);
+  else
+    hipLaunchKernelGGL((k_gen_count<false, false>), dim3(nb), dim3(BLOCK), 0, s, m, ga, ctx->g, ex);
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }

@@ -314,4 +314,129 @@ PM_HD uint64_t perm_apply(const Perm& p, uint64_t y) {
   return y;
 }
 
+// ---- key-order stratified sample lists ----------------------
+// A reference's list generated directly in the order r10 pops its samples
+// (IterationComp, pluss_utils.h:175-267 = key a*T+tid when N % (CS*T) == 0),
+// so faithful mode needs no sort and the list can be counted while it is
+// generated.  The valid iteration points (indices in [0, span)) are
+// enumerated in key order -- (q, c1, c2, tid), tid fastest -- in two blocks:
+//   A: q in [0, QA), tid in [0, T)          QA = Q-1 if span < N, else Q
+//   B: q = Q-1,      tid in [0, T-1)        only if span < N (c0 = N-1 is out)
+// with Q = N/T local rows per thread.  S samples are split SA = floor(S*DA/D),
+// SB = S - SA; inside a block of DX points and SX samples, sample j owns the
+// stratum [j*g + min(j, rr), +g + (j < rr)) (g = DX / SX, rr = DX % SX) and
+// sits at a keyed pseudo-random offset in it: distinct, strictly increasing
+// keys, random access by sample index (any rank can generate any slice).
+
+// 64-bit division by a run-time invariant d >= 1 (round-up multiplier, any
+// 64-bit numerator; Granlund-Montgomery).
+struct Div64 {
+  uint64_t d, m;
+  uint32_t s, one;  // one: d == 1
+};
+inline Div64 make_div64(uint64_t d) {
+  Div64 f;
+  f.d = d;
+  f.one = d == 1 ? 1u : 0u;
+  uint32_t l = 0;
+  while (l < 64 && (1ull << l) < d) ++l;  // 2^(l-1) < d <= 2^l
+  if (d <= 1) l = 1;
+  f.s = l;
+  const unsigned __int128 two_l = (unsigned __int128)1 << l;
+  f.m = (uint64_t)((((unsigned __int128)1 << 64) * (two_l - d)) / d + 1);
+  return f;
+}
+PM_HD uint64_t mulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul64hi(a, b);
+#else
+  return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+PM_HD uint64_t div64(uint64_t n, const Div64& f) {
+  const uint64_t q = mulhi64(n, f.m);
+  const uint64_t t = ((n - q) >> 1) + q;
+  return f.one ? n : t >> (f.s - 1);
+}
+
+PM_HD uint32_t lowbias32(uint32_t x) {  // 32-bit integer hash (xorshift-multiply)
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+struct KeyGen {
+  uint32_t ref, dim3, N, T, CS, span, Q, k0, k1, wide;
+  uint64_t S, SA;    // samples of this reference; of them in block A
+  uint64_t g[2];     // stratum size in block A / B
+  uint64_t rr[2];    // strata of size g+1 (the first rr of the block)
+  Div64 dt[2], dspan;  // radix of tid in block A (T) / B (T-1); radix of c1 and c2
+};
+
+// Host: the generator of S samples of reference `ref` (validated: the caller
+// checks N % (CS*T) == 0, 1 <= S <= span^d, S < 2^32).
+inline KeyGen make_keygen(uint64_t N, uint64_t T, uint64_t CS, bool range_full, uint64_t seed, uint32_t ref,
+                          uint64_t S) {
+  KeyGen k;
+  k.ref = ref;
+  k.dim3 = (ref == C0 || ref == C1) ? 0u : 1u;
+  k.N = (uint32_t)N;
+  k.T = (uint32_t)T;
+  k.CS = (uint32_t)CS;
+  k.span = (uint32_t)(range_full ? N : N - 1);
+  k.Q = (uint32_t)(N / T);
+  const uint64_t M = k.dim3 ? (uint64_t)k.span * k.span : (uint64_t)k.span;  // points per (q, tid)
+  const uint64_t QA = range_full ? k.Q : k.Q - 1;
+  const uint64_t DA = QA * M * T, DB = range_full ? 0 : M * (T - 1), D = DA + DB;
+  k.S = S;
+  k.SA = D ? (uint64_t)(((unsigned __int128)S * DA) / D) : 0;
+  const uint64_t SX[2] = {k.SA, S - k.SA}, DX[2] = {DA, DB};
+  uint64_t gmax = 0;
+  for (int b = 0; b < 2; ++b) {
+    k.g[b] = SX[b] ? DX[b] / SX[b] : 0;
+    k.rr[b] = SX[b] ? DX[b] - k.g[b] * SX[b] : 0;
+    const uint64_t len = k.g[b] + (k.rr[b] ? 1 : 0);
+    gmax = len > gmax ? len : gmax;
+  }
+  k.wide = gmax > (1ull << 32) ? 1u : 0u;
+  k.dt[0] = make_div64(T);
+  k.dt[1] = make_div64(T > 1 ? T - 1 : 1);
+  k.dspan = make_div64(k.span ? k.span : 1);
+  const uint64_t h = mix64(seed ^ ((uint64_t)(ref + 1) * 0x9E3779B97F4A7C15ull) ^ 0xA5A5A5A55A5A5A5Aull);
+  k.k0 = (uint32_t)h;
+  k.k1 = (uint32_t)(h >> 32);
+  return k;
+}
+
+// Sample i (0 <= i < S) of the list: packed ref|c0|c1|c2.
+PM_HD uint64_t keygen_sample(const KeyGen& k, uint64_t i) {
+  const uint32_t b = i < k.SA ? 0u : 1u;
+  const uint64_t j = b ? i - k.SA : i;
+  const uint64_t g = k.g[b], rr = k.rr[b];
+  const uint64_t lo = j * g + (j < rr ? j : rr);
+  const uint64_t len = g + (j < rr ? 1u : 0u);
+  const uint32_t uh = lowbias32((uint32_t)i ^ k.k0);
+  uint64_t off;
+  if (k.wide) off = mulhi64(((uint64_t)uh << 32) | lowbias32((uint32_t)i ^ k.k1), len);
+  else off = ((uint64_t)uh * len) >> 32;
+  const uint64_t p = lo + off;
+  const Div64& dt = k.dt[b];
+  uint64_t r = div64(p, dt);
+  const uint32_t tid = (uint32_t)(p - r * dt.d);
+  uint32_t c2 = 0;
+  if (k.dim3) {
+    const uint64_t r2 = div64(r, k.dspan);
+    c2 = (uint32_t)(r - r2 * k.span);
+    r = r2;
+  }
+  const uint64_t r3 = div64(r, k.dspan);
+  const uint32_t c1 = (uint32_t)(r - r3 * k.span);
+  const uint32_t q = b ? k.Q - 1 : (uint32_t)r3;
+  const uint32_t c0 = ((q / k.CS) * k.T + tid) * k.CS + q % k.CS;
+  return pack(k.ref, c0, c1, c2);
+}
+
 }  // namespace pluss

@@ -47,3 +47,12 @@ extern "C" int mh_expand(int64_t N, int range_full, uint64_t seed, int ref, uint
   }
   return 0;
 }
+
+// key-order stratified lists (pluss_model.h KeyGen) and the 64-bit divider
+extern "C" int mh_expand_sorted(int64_t N, int64_t T, int64_t CS, int range_full, uint64_t seed, int ref, uint64_t S,
+                                uint64_t first, uint64_t n, uint64_t* out) {
+  KeyGen k = make_keygen(N, T, CS, range_full != 0, seed, (uint32_t)ref, S);
+  for (uint64_t i = 0; i < n; i++) out[i] = keygen_sample(k, first + i);
+  return 0;
+}
+extern "C" uint64_t mh_div64(uint64_t n, uint64_t d) { Div64 f = make_div64(d); return div64(n, f); }

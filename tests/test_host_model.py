@@ -188,3 +188,57 @@ def test_dense_keys_follow_closed_forms_without_gpu():
             assert k == (b // 3) << 60 | kind << 56 | (ri + 2), (N, ref, case)
     with pytest.raises(PlussError, match="PLUSS_ERR_CONFIG"):
         dense_keys(SamplerConfig(n=100, threads=3, chunk=5))  # N % (cls/ds) != 0
+
+
+KEYGEN_SHAPES = [(128, 4, 4, 0, 2098), (128, 4, 4, 1, 2098), (1024, 8, 4, 0, 4189071), (4096, 8, 4, 0, 67025020),
+                 (2048, 64, 4, 0, 4173354), (64, 2, 1, 0, 5000), (16, 1, 4, 0, 100), (32, 4, 2, 0, 1),
+                 (4096, 8, 4, 0, 3), (256, 4, 4, 1, 255 ** 3), (256, 4, 4, 0, 255 ** 3)]
+
+
+@pytest.mark.parametrize("N,T,CS,rf,S", KEYGEN_SHAPES, ids=[str(s) for s in KEYGEN_SHAPES])
+def test_key_order_lists_host_model_equals_oracle(orc, model_host, N, T, CS, rf, S):
+    """The key-order stratified generator (pluss_model.h keygen_sample, what the
+    kernels run) == its independent restatement in the oracle, on slices at the
+    start, the block A/B seam and the end; the list is distinct, in range and
+    strictly increasing in the faithful sort key (r10's pop order)."""
+    import ctypes
+    L = model_host.lib
+    L.mh_expand_sorted.argtypes = [ctypes.c_int64] * 3 + [ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
+                                                          ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                          ctypes.POINTER(ctypes.c_uint64)]
+    c = orc.cfg(N, T, CS, range_full=rf)
+    for ref in range(6):
+        span = N if rf else N - 1
+        tot = min(S, span ** (3 if ref >= 2 else 2))
+        for first, n in {(0, min(tot, 5000)), (max(0, tot - 5000), min(tot, 5000)),
+                         (max(0, tot // 2 - 2500), min(tot, 5000))}:
+            want = orc.expand_sorted(c, 0x5EED0007, ref, tot, first, n)
+            got = np.empty(n, np.uint64)
+            assert L.mh_expand_sorted(N, T, CS, rf, 0x5EED0007, ref, tot, first, n,
+                                      got.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))) == 0
+            np.testing.assert_array_equal(got, want)
+            key = orc.sort_key(N, T, CS, want)
+            assert (key[1:] > key[:-1]).all()
+            m = np.uint64(0xFFFFF)
+            for sh in (40, 20, 0):
+                assert (((want >> np.uint64(sh)) & m) < span).all()
+            assert ((want >> np.uint64(60)) == ref).all()
+    if S <= 300000:  # the whole list: every sample distinct, spread over the whole key range
+        tot = min(S, (N if rf else N - 1) ** 3)
+        full = orc.expand_sorted(c, 1, "B0", tot, 0, tot)
+        assert len(np.unique(full)) == tot
+
+
+def test_div64_round_up_divider(model_host):
+    import ctypes
+    L = model_host.lib
+    L.mh_div64.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+    L.mh_div64.restype = ctypes.c_uint64
+    rng = np.random.default_rng(3)
+    ds = [1, 2, 3, 7, 8, 1023, 4095, 4096, 65535, (1 << 32) - 1, 1 << 32, (1 << 32) + 1, (1 << 63) - 25, 1 << 63,
+          (1 << 64) - 1] + [int(x) for x in rng.integers(1, 1 << 62, 40)]
+    ns = [0, 1, (1 << 64) - 1, (1 << 63), (1 << 32) - 1] + [int(x) for x in rng.integers(0, 1 << 63, 60)]
+    for d in ds:
+        for n in ns + [d - 1, d, d + 1, 2 * d - 1]:
+            n &= (1 << 64) - 1
+            assert L.mh_div64(n, d) == n // d, (n, d)
