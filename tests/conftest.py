@@ -186,3 +186,22 @@ def oracle_subset(N, T, CS, samples, budget_steps, W=8, seed=0):
         keep[i] = True
         spent += cost[i]
     return s[keep]
+
+
+@pytest.fixture(autouse=True)
+def _torch_stream(request):
+    """GPU tests run with a dedicated (non-null) torch stream as the current
+    stream, so `torch.cuda.current_stream().cuda_stream` handed to the library
+    orders its launches with torch's own fills, copies and adds.  (A null
+    pointer would select the handle's own non-blocking stream instead.)"""
+    if "gpu" not in request.keywords:
+        yield
+        return
+    import torch
+    if not torch.cuda.is_available():
+        yield
+        return
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        yield
+    torch.cuda.synchronize()
