@@ -460,23 +460,26 @@ __global__ void k_faith_scan_init(unsigned long long* scal, uint64_t cut, unsign
   for (uint64_t j = i; j < nw; j += (uint64_t)gridDim.x * blockDim.x) st[j] = 0;
 }
 
-// ---- one-GPU packed-word pass: scan, Q1 cut and record fused.  Chunks of
-// FCHUNK elements (1024 threads x FI) chain their prefix max and start count
-// through decoupled look-back (256 predecessors per round, so the chain
-// over a 2^22-element reference resolves in a couple of rounds), find their
-// own first qualifying start (the chunk's Q1 candidate) and record their
-// elements below it into per-chunk partial sums.  The condition of Q1,
-// j - starts_before_j >= n - j, is monotone in j, so the global cut is the
-// smallest candidate; k_faith_fused_finish adds the partials of the chunks
-// that start below it (the cut's own chunk recorded exactly the elements
-// before it; chunks before it have no candidate and recorded everything).
-// The prefix max is never stored.
-constexpr int FB = 1024, FI = 8;
-constexpr uint32_t FCHUNK = FB * FI;
-constexpr int FPART = 5;  // per chunk: cold (tid 0), traversed, case 0/1/2 counts
-__host__ __device__ inline uint64_t fu_tiles(uint64_t n) { return (n + FCHUNK - 1) / FCHUNK; }
-
-// exclusive prefix of tile t > 0, 4 predecessors per lane (256 per round)
+// ---- the one-GPU scan over key-ordered elements, the six references of a
+// list in ONE pipeline of four launches (whatever the element source: sorted
+// packed words after the radix sort, a caller's key-ordered samples, or
+// samples generated in key order):
+//   k_fa_max     per tile of TILE elements: the largest sink (and, for a
+//                caller's list, the key-order check);
+//   k_fa_prefix  one workgroup per reference: exclusive prefix max of the
+//                tile maxima = the running max of sinks entering each tile;
+//                resets the reference's look-back words and scalars;
+//   k_fa_scan    per tile, in order of a tile counter: prefix max inside the
+//                tile, start flags, start count chained across the
+//                reference's tiles by decoupled look-back (the only chain),
+//                the tile's Q1 candidate, and the records of its elements
+//                below that candidate into per-tile partial sums;
+//   k_fa_finish  one workgroup per reference: the Q1 cut is the smallest
+//                candidate (the condition j - starts_before_j >= n - j is
+//                monotone in j), so the partials of the tiles that start
+//                below it are summed; Q3, the -1 key, traversed, the bins.
+// exclusive prefix of tile t > 0 from the status words of tiles t-1, t-2, ...
+// (one whole wave, 4 predecessors per lane: 256 per round)
 template <bool MAX>
 __device__ unsigned long long sc_lookback4(const unsigned long long* st, uint32_t t, uint32_t lane) {
   unsigned long long acc = 0;
@@ -509,6 +512,8 @@ __device__ unsigned long long sc_lookback4(const unsigned long long* st, uint32_
     hi -= 256;
   }
 }
+// publish the tile's aggregate, resolve its exclusive prefix, publish the
+// inclusive one (wave 0); every thread of the workgroup gets the prefix
 template <bool MAX>
 __device__ __forceinline__ unsigned long long fu_chain(unsigned long long* st, uint32_t t, unsigned long long agg,
                                                        uint32_t lane, unsigned long long* s_in) {
@@ -527,69 +532,208 @@ __device__ __forceinline__ unsigned long long fu_chain(unsigned long long* st, u
   return *s_in;
 }
 
-// One tile of the fused pass.  The tile's elements have global indices
-// gbase + li, li in [0, mt); src.word(li) is element li's packed word and
-// src.key_after(li) the key of the global element after it (KEY_EMPTY past
-// the end).  t is the tile's look-back index (tiles in global order).
-// Src::kCheck: the source is a caller's list that must be in key order;
-// an element whose successor's key is not larger is reported through
-// src.unordered() (the bad-input flag).
-// scal: [0] cut (= n beforehand); st: 2 * ntiles zeroed words; part: FPART
-// words per tile (written, not accumulated).
-template <int FM, class Src>
-__device__ __forceinline__ void fused_tile(const Src& src, uint32_t t, uint64_t gbase, uint32_t mt, const PkView& pv,
-                                           uint64_t n, unsigned long long endkey, unsigned long long* st,
-                                           uint64_t ntiles, unsigned long long* __restrict__ part,
-                                           unsigned long long* scal) {
-  typedef fkey_t<FM> KT;
-  constexpr int NW = FB / 64;
-  __shared__ unsigned long long s_w[NW], s_inm, s_inc, s_red[NW][FPART];
+constexpr int TB = 256, TI = 16;            // threads per tile, elements per thread
+constexpr uint32_t TILE = TB * TI;          // elements per tile
+constexpr int FPART = 5;                    // per tile: cold (tid 0), traversed, case 0/1/2 counts
+constexpr int FA_SCAL = 8;                  // scalars per reference: [0] cut
+constexpr int FA_COUNTER = 6 * FA_SCAL;     // the scan pass's tile counter (all references)
+__host__ __device__ inline uint64_t fa_tiles(uint64_t n) { return (n + TILE - 1) / TILE; }
+
+enum : int { SRC_W32 = 0, SRC_W64 = 1, SRC_SAMPLES = 2, SRC_GEN = 3 };
+
+struct FaRefs {
+  uint64_t n[6];
+  uint64_t toff[7];    // first (global) tile of each reference; toff[6] = all tiles
+  const void* src[6];  // SRC_W*: sorted packed words; SRC_SAMPLES: the key-ordered samples
+  PkView pv[6];
+  KeyGen kg[6];        // SRC_GEN
+};
+
+// key, sink and case of one element (case 3: malformed, flagged)
+struct Elem {
+  unsigned long long key, sink;
+  uint32_t c;
+};
+
+__device__ __forceinline__ Elem elem_of_sample(const Model& m, const PkView& v, uint32_t ref, uint64_t x, GTable g) {
+  const Sample s = unpack(x);
+  if (s.ref != ref || s.c0 >= m.N || s.c1 >= m.N || s.c2 >= m.N) {
+    atomicOr(&g.flags[1], 1u);
+    return Elem{KEY_EMPTY, KEY_EMPTY, 3u};
+  }
+  const uint32_t c2 = (ref == C0 || ref == C1) ? 0u : s.c2;
+  const uint32_t k = fdiv(s.c0, m.dCS), p = s.c0 - k * m.CS;
+  const uint32_t kt = fdiv(k, m.dT), t = k - kt * m.T;
+  const uint64_t q = (uint64_t)kt * m.CS + p;
+  const uint64_t key = (q * m.R + (uint64_t)s.c1 * m.S + ref_off(ref, c2)) * m.T + t;
+  const uint32_t c = case_fast<false>(m, ref, s.c0, s.c1, c2);
+  const int64_t ri = c == 0 ? v.ri[0] : (c == 1 ? v.ri[1] : v.ri[2]);
+  return Elem{key, ri < 0 ? KEY_EMPTY : key + (unsigned long long)ri * m.T, c};
+}
+
+template <int SRC>
+__device__ __forceinline__ Elem fa_elem(const Model& m, const FaRefs& a, uint32_t r, uint64_t i, GTable g) {
+  if (SRC == SRC_W32 || SRC == SRC_W64) {
+    typedef typename std::conditional<SRC == SRC_W32, uint32_t, unsigned long long>::type KT;
+    const KT w = static_cast<const KT*>(a.src[r])[i];
+    const bool bad = w == (KT) ~(KT)0;
+    return Elem{pk_key(w, a.pv[r]), pk_sink(w, a.pv[r]), bad ? 3u : (uint32_t)(w & 3u)};
+  }
+  const uint64_t x = SRC == SRC_GEN ? keygen_sample(a.kg[r], i) : static_cast<const uint64_t*>(a.src[r])[i];
+  return elem_of_sample(m, a.pv[r], r, x, g);
+}
+
+// the tile's reference (wave-uniform) and its place in it
+struct FaTile {
+  uint32_t r;
+  uint64_t lt, base;  // tile index within the reference, its first element
+  uint32_t mt;        // elements in the tile
+};
+__device__ __forceinline__ FaTile fa_tile(const FaRefs& a, uint64_t gt) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int x = 1; x < 6; ++x) r += gt >= a.toff[x] ? 1u : 0u;
+  r = __builtin_amdgcn_readfirstlane(r);
+  FaTile t;
+  t.r = r;
+  t.lt = gt - a.toff[r];
+  t.base = t.lt * TILE;
+  const uint64_t left = a.n[r] - t.base;
+  t.mt = (uint32_t)(left < TILE ? left : TILE);
+  return t;
+}
+
+// Wave w of a tile owns elements [w*64*TI, (w+1)*64*TI), visited as TI rounds
+// of 64 (lane l: element w*64*TI + 64k + l): every load is coalesced and the
+// scans run across the lanes of a round with a carry between rounds.
+template <int SRC, bool CHECK>
+__global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long long* __restrict__ tmax, GTable g) {
+  __shared__ unsigned long long s_w[TB / 64];
+  const FaTile T = fa_tile(a, blockIdx.x);
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  const uint32_t lbase = wid * (64 * FI);
-  KT w[FI];
+  const uint32_t lbase = wid * (64 * TI);
+  unsigned long long tm = 0, prev = 0;  // prev: lane 63's key of the previous round
+  bool prev_v = false, unordered = false;
+#pragma unroll
+  for (int k = 0; k < TI; ++k) {
+    const uint32_t li = lbase + (uint32_t)k * 64 + lane;
+    const bool v = li < T.mt;
+    const Elem e = v ? fa_elem<SRC>(m, a, T.r, T.base + li, g) : Elem{KEY_EMPTY, 0ull, 3u};
+    tm = e.sink > tm ? e.sink : tm;
+    if (CHECK) {  // key order: every element against the next one
+      const unsigned long long kn = __shfl_down(e.key, 1, 64);  // the next lane's
+      if (lane < 63 && v && li + 1 < T.mt) unordered |= !(kn > e.key);
+      const unsigned long long k0 = __shfl(e.key, 0, 64);  // this round's first vs the previous round's last
+      if (lane == 63 && k > 0 && prev_v && lbase + (uint32_t)k * 64 < T.mt) unordered |= !(k0 > prev);
+      prev = e.key;
+      prev_v = v;
+      if (k + 1 == TI && lane == 63 && v && T.base + li + 1 < a.n[T.r])  // the wave's last vs the next element
+        unordered |= !(fa_elem<SRC>(m, a, T.r, T.base + li + 1, g).key > e.key);
+    }
+  }
+  if (CHECK && __ballot(unordered) && lane == 0) atomicOr(&g.flags[1], 1u);
+  tm = sc_wave_red<true>(tm);
+  if (lane == 0) s_w[wid] = tm;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long x = 0;
+#pragma unroll
+    for (int w = 0; w < TB / 64; ++w) x = s_w[w] > x ? s_w[w] : x;
+    tmax[blockIdx.x] = x;
+  }
+}
+
+// One workgroup per reference: pmin[t] = max of tmax over the reference's
+// tiles before t (0 for its first); st of its tiles zeroed; its cut = n.
+constexpr int PB = 1024;
+__global__ __launch_bounds__(PB) void k_fa_prefix(FaRefs a, const unsigned long long* __restrict__ tmax,
+                                                  unsigned long long* __restrict__ pmin, unsigned long long* st,
+                                                  unsigned long long* scal) {
+  __shared__ unsigned long long s_w[PB / 64];
+  const uint32_t r = blockIdx.x;
+  if (r == 0 && threadIdx.x == 0) scal[FA_COUNTER] = 0;
+  if (threadIdx.x == 0) scal[r * FA_SCAL] = a.n[r];
+  const uint64_t t0 = a.toff[r], nt = a.toff[r + 1] - t0;
+  if (nt == 0) return;
+  const uint64_t per = (nt + PB - 1) / PB;
+  const uint64_t lo = t0 + threadIdx.x * per, hi = lo + per < t0 + nt ? lo + per : t0 + nt;
+  unsigned long long mx = 0;
+  for (uint64_t t = lo; t < hi; ++t) mx = tmax[t] > mx ? tmax[t] : mx;
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  const unsigned long long inc = sc_wave_scan<true>(mx, lane);
+  if (lane == 63) s_w[wid] = inc;
+  __syncthreads();
+  unsigned long long pre = 0;
+  for (uint32_t w = 0; w < wid; ++w) pre = s_w[w] > pre ? s_w[w] : pre;
+  const unsigned long long up = __shfl_up(inc, 1, 64);
+  unsigned long long run = lane ? (up > pre ? up : pre) : pre;  // exclusive prefix of this thread's segment
+  for (uint64_t t = lo; t < hi; ++t) {
+    pmin[t] = run;
+    run = tmax[t] > run ? tmax[t] : run;
+    st[t] = 0;
+  }
+}
+
+template <int SRC>
+__global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigned long long* __restrict__ pmin,
+                                                unsigned long long* st, unsigned long long* __restrict__ part,
+                                                unsigned long long* scal, GTable g) {
+  constexpr int NW = TB / 64;
+  __shared__ unsigned long long s_tile, s_w[NW], s_inc, s_red[NW][FPART];
+  if (threadIdx.x == 0) s_tile = atomicAdd(&scal[FA_COUNTER], 1ull);
+  __syncthreads();
+  const uint64_t gt = s_tile;
+  const FaTile T = fa_tile(a, gt);
+  const uint32_t r = T.r;
+  const uint64_t n = a.n[r];
+  const unsigned long long endkey = m.A * m.T;
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  const uint32_t lbase = wid * (64 * TI);
+  // ri*T per case (KEY_EMPTY: cold), to recompute sinks from keys
+  unsigned long long rt[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) rt[c] = a.pv[r].ri[c] < 0 ? KEY_EMPTY : (unsigned long long)a.pv[r].ri[c] * m.T;
+  auto sink_of = [&](unsigned long long key, uint32_t c) -> unsigned long long {
+    const unsigned long long d = c == 0 ? rt[0] : (c == 1 ? rt[1] : rt[2]);
+    return (c > 2 || d == KEY_EMPTY || key == KEY_EMPTY) ? KEY_EMPTY : key + d;
+  };
+  unsigned long long key[TI];
+  uint32_t cases = 0;  // 2 bits per element
   unsigned long long tm = 0;
 #pragma unroll
-  for (int k = 0; k < FI; ++k) {
+  for (int k = 0; k < TI; ++k) {
     const uint32_t li = lbase + (uint32_t)k * 64 + lane;
-    w[k] = li < mt ? src.word(li) : (KT)0;
-    const unsigned long long sk = li < mt ? pk_sink(w[k], pv) : 0ull;
-    tm = sk > tm ? sk : tm;
+    const Elem e = li < T.mt ? fa_elem<SRC>(m, a, r, T.base + li, g) : Elem{KEY_EMPTY, 0ull, 3u};
+    key[k] = e.key;
+    cases |= (e.c & 3u) << (2 * k);
+    if (li < T.mt) tm = e.sink > tm ? e.sink : tm;
   }
-  // prefix max of sinks
-  {
-    const unsigned long long wagg = sc_wave_red<true>(st_cap(tm));
-    if (lane == 0) s_w[wid] = wagg;
-  }
+  // prefix max entering each wave: the tile's incoming max and the earlier waves' maxima
+  tm = sc_wave_red<true>(tm);
+  if (lane == 0) s_w[wid] = tm;
   __syncthreads();
-  unsigned long long pre = 0, agg = 0;
+  unsigned long long carry = pmin[gt];
 #pragma unroll
-  for (int x = 0; x < NW; ++x) {
-    const unsigned long long v = s_w[x];
-    if (x < (int)wid) pre = v > pre ? v : pre;
-    agg = v > agg ? v : agg;
-  }
-  const unsigned long long m_in = fu_chain<true>(st, t, agg, lane, &s_inm);
-  unsigned long long carry = st_uncap(m_in > pre ? m_in : pre);  // prefix max before the wave's first element
-  unsigned long long pm[FI], fmask[FI], key[FI];
+  for (int x = 0; x < NW; ++x)
+    if (x < (int)wid) carry = s_w[x] > carry ? s_w[x] : carry;
+  unsigned long long pm[TI], fmask[TI];
   uint32_t wcnt = 0;
 #pragma unroll
-  for (int k = 0; k < FI; ++k) {
+  for (int k = 0; k < TI; ++k) {
     const uint32_t li = lbase + (uint32_t)k * 64 + lane;
-    const uint64_t i = gbase + li;
-    const bool valid = li < mt;
-    const KT wk = w[k];
-    unsigned long long inc = sc_wave_scan<true>(valid ? pk_sink(wk, pv) : 0ull, lane);
+    const uint64_t i = T.base + li;
+    const bool valid = li < T.mt;
+    const uint32_t c = (cases >> (2 * k)) & 3u;
+    unsigned long long inc = sc_wave_scan<true>(valid ? sink_of(key[k], c) : 0ull, lane);
     inc = inc > carry ? inc : carry;
     const unsigned long long up = __shfl_up(inc, 1, 64);
     const unsigned long long before = lane ? up : carry;
-    const unsigned long long kk = valid ? pk_key(wk, pv) : KEY_EMPTY;
-    key[k] = kk;
-    fmask[k] = __ballot(valid && (i == 0 || kk > before));
+    fmask[k] = __ballot(valid && (i == 0 || key[k] > before));
     wcnt += (uint32_t)__popcll(fmask[k]);
     pm[k] = inc;
     carry = __shfl(inc, 63, 64);
   }
-  // start counts
+  // start counts: this tile's total, chained over the reference's tiles
   __syncthreads();  // s_w is reused
   if (lane == 0) s_w[wid] = wcnt;
   __syncthreads();
@@ -600,20 +744,20 @@ __device__ __forceinline__ void fused_tile(const Src& src, uint32_t t, uint64_t 
     if (x < (int)wid) cpre += v;
     cagg += v;
   }
-  const unsigned long long c_in = fu_chain<false>(st + ntiles, t, cagg, lane, &s_inc);
+  const unsigned long long c_in = fu_chain<false>(st + a.toff[r], (uint32_t)T.lt, cagg, lane, &s_inc);
   // the tile's Q1 candidate: its first start j > 0 with j - starts_before_j >= n - j
   unsigned long long best = KEY_EMPTY;
   {
     uint64_t cb = c_in + cpre;
     const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
-    for (int k = 0; k < FI; ++k) {
+    for (int k = 0; k < TI; ++k) {
       const unsigned long long F = fmask[k];
       if (best == KEY_EMPTY && F) {
-        const uint64_t j = gbase + lbase + (uint64_t)k * 64 + lane;
+        const uint64_t j = T.base + lbase + (uint64_t)k * 64 + lane;
         const uint64_t before_j = cb + (uint64_t)__popcll(F & below);
         const unsigned long long q = __ballot(((F >> lane) & 1ull) && j > 0 && j - before_j >= n - j);
-        if (q) best = gbase + lbase + (uint64_t)k * 64 + (uint64_t)(__ffsll((long long)q) - 1);
+        if (q) best = T.base + lbase + (uint64_t)k * 64 + (uint64_t)(__ffsll((long long)q) - 1);
       }
       cb += (uint64_t)__popcll(F);
     }
@@ -624,31 +768,29 @@ __device__ __forceinline__ void fused_tile(const Src& src, uint32_t t, uint64_t 
   unsigned long long cut = n;
 #pragma unroll
   for (int x = 0; x < NW; ++x) cut = s_w[x] < cut ? s_w[x] : cut;
-  if (threadIdx.x == 0 && cut < n) atomicMin(&scal[0], cut);
-  // record the tile's elements below its own cut
+  if (threadIdx.x == 0 && cut < n) atomicMin(&scal[r * FA_SCAL], cut);
+  // record the tile's elements below its own candidate
   unsigned long long cold = 0, trav = 0;
   uint32_t nc0 = 0, nc1 = 0, nc2 = 0;
-  bool unordered = false;
+  const uint64_t tmask = m.T - 1;
+  const bool tp2 = (m.T & tmask) == 0;
 #pragma unroll
-  for (int k = 0; k < FI; ++k) {
+  for (int k = 0; k < TI; ++k) {
     const uint32_t li = lbase + (uint32_t)k * 64 + lane;
-    const uint64_t i = gbase + li;
-    const KT wk = w[k];
+    const uint64_t i = T.base + li;
     const unsigned long long kk = key[k];
     // the next element's key: the next lane, the next round's lane 0, or (the wave's last element) the source
     unsigned long long kn = __shfl_down(kk, 1, 64);
-    if (k + 1 < FI) {
+    if (k + 1 < TI) {
       const unsigned long long k0 = __shfl(key[k + 1], 0, 64);
       if (lane == 63) kn = k0;
     } else if (lane == 63) {
-      kn = li < mt ? src.key_after(li) : KEY_EMPTY;
+      kn = (li < T.mt && i + 1 < n) ? fa_elem<SRC>(m, a, r, i + 1, g).key : KEY_EMPTY;
     }
-    if (Src::kCheck && li < mt && i + 1 < n && !(kn > kk)) unordered = true;
-    uint32_t c = 3;
+    const uint32_t c = (cases >> (2 * k)) & 3u;
     bool rec = false;
-    if (li < mt && i < cut) {
-      c = (uint32_t)(wk & 3u);
-      if (pk_sink(wk, pv) == KEY_EMPTY) cold += ((pv.p2 ? (kk & (pv.T - 1)) : kk % pv.T) == 0) ? 1u : 0u;
+    if (li < T.mt && i < cut) {
+      if (sink_of(kk, c) == KEY_EMPTY) cold += ((tp2 ? (kk & tmask) : kk % m.T) == 0) ? 1u : 0u;
       else rec = true;
       if ((fmask[k] >> lane) & 1ull) trav -= kk;  // this element starts a replay
       const unsigned long long gm = pm[k];
@@ -658,7 +800,6 @@ __device__ __forceinline__ void fused_tile(const Src& src, uint32_t t, uint64_t 
     nc1 += (uint32_t)__popcll(__ballot(rec && c == 1));
     nc2 += (uint32_t)__popcll(__ballot(rec && c == 2));
   }
-  if (Src::kCheck && __ballot(unordered) && lane == 0) src.unordered();
   cold = sc_wave_red<false>(cold);
   trav = sc_wave_red<false>(trav);
   if (lane == 0) {
@@ -673,117 +814,28 @@ __device__ __forceinline__ void fused_tile(const Src& src, uint32_t t, uint64_t 
     unsigned long long v = 0;
 #pragma unroll
     for (int x = 0; x < NW; ++x) v += s_red[x][threadIdx.x];
-    part[(uint64_t)t * FPART + threadIdx.x] = v;
+    part[gt * FPART + threadIdx.x] = v;
   }
 }
 
-// Tiles of FCHUNK consecutive sorted words (the rocPRIM-sorted array).
-template <int FM>
-struct GlobalTile {
-  static constexpr bool kCheck = false;
-  const fkey_t<FM>* wd;
-  uint64_t gbase, n;
-  PkView pv;
-  __device__ fkey_t<FM> word(uint32_t li) const { return wd[gbase + li]; }
-  __device__ unsigned long long key_after(uint32_t li) const {
-    const uint64_t i = gbase + li + 1;
-    return i < n ? pk_key(wd[i], pv) : KEY_EMPTY;
-  }
-  __device__ void unordered() const {}
-};
-
-// Tiles of FCHUNK consecutive samples of a caller's list that is already in
-// key order (pluss_dev_faithful_hist_sorted): each sample's packed word is
-// made where it is read -- no keys pass, no sort -- and the order is checked.
-template <int FM>
-struct SampleTile {
-  static constexpr bool kCheck = true;
-  const uint64_t* smp;
-  uint64_t gbase, n;
-  const Model* m;
-  uint32_t ref;
-  PkView pv;
-  GTable g;
-  __device__ fkey_t<FM> word(uint32_t li) const { return pk_word_of<fkey_t<FM>>(*m, ref, smp[gbase + li], g); }
-  __device__ unsigned long long key_after(uint32_t li) const {
-    const uint64_t i = gbase + li + 1;
-    return i < n ? pk_key(pk_word_of<fkey_t<FM>>(*m, ref, smp[i], g), pv) : KEY_EMPTY;
-  }
-  __device__ void unordered() const { atomicOr(&g.flags[1], 1u); }
-};
-
-// Tiles of a generated key-order list (pluss_dev_gen_faithful_refs): the
-// samples never exist in memory.
-template <int FM>
-struct GenTile {
-  static constexpr bool kCheck = false;
-  const KeyGen* k;
-  uint64_t gbase, n;
-  const Model* m;
-  PkView pv;
-  GTable g;
-  __device__ fkey_t<FM> word(uint32_t li) const {
-    return pk_word_of<fkey_t<FM>>(*m, k->ref, keygen_sample(*k, gbase + li), g);
-  }
-  __device__ unsigned long long key_after(uint32_t li) const {
-    const uint64_t i = gbase + li + 1;
-    return i < n ? pk_key(pk_word_of<fkey_t<FM>>(*m, k->ref, keygen_sample(*k, i), g), pv) : KEY_EMPTY;
-  }
-  __device__ void unordered() const {}
-};
-
-// scal: [0] cut (= n beforehand), [4] tile counter; st: 2 * fu_tiles(n) zeroed words;
-// part: FPART words per chunk (written, not accumulated)
-template <int FM>
-__global__ __launch_bounds__(FB) void k_faith_fused(const void* __restrict__ words, PkView pv, uint64_t n,
-                                                    unsigned long long endkey, unsigned long long* st,
-                                                    unsigned long long* __restrict__ part,
-                                                    unsigned long long* scal) {
-  __shared__ unsigned long long s_tile;
-  if (threadIdx.x == 0) s_tile = atomicAdd(&scal[4], 1ull);
-  __syncthreads();
-  const uint32_t t = (uint32_t)s_tile;
-  const uint64_t gbase = (uint64_t)t * FCHUNK;
-  const uint32_t mt = (uint32_t)(n - gbase < FCHUNK ? n - gbase : FCHUNK);
-  const GlobalTile<FM> src{static_cast<const fkey_t<FM>*>(words), gbase, n, pv};
-  fused_tile<FM>(src, t, gbase, mt, pv, n, endkey, st, fu_tiles(n), part, scal);
-}
-
-// The same pass straight over a key-ordered sample list (GEN = false) or a
-// generated key-order list (GEN = true, `smp` unused).
-template <int FM, bool GEN>
-__global__ __launch_bounds__(FB) void k_faith_fused_direct(Model m, uint32_t ref, const uint64_t* __restrict__ smp,
-                                                           KeyGen kg, PkView pv, uint64_t n, unsigned long long endkey,
-                                                           unsigned long long* st,
-                                                           unsigned long long* __restrict__ part,
-                                                           unsigned long long* scal, GTable g) {
-  __shared__ unsigned long long s_tile;
-  if (threadIdx.x == 0) s_tile = atomicAdd(&scal[4], 1ull);
-  __syncthreads();
-  const uint32_t t = (uint32_t)s_tile;
-  const uint64_t gbase = (uint64_t)t * FCHUNK;
-  const uint32_t mt = (uint32_t)(n - gbase < FCHUNK ? n - gbase : FCHUNK);
-  if (GEN) {
-    const GenTile<FM> src{&kg, gbase, n, &m, pv, g};
-    fused_tile<FM>(src, t, gbase, mt, pv, n, endkey, st, fu_tiles(n), part, scal);
-  } else {
-    const SampleTile<FM> src{smp, gbase, n, &m, ref, pv, g};
-    fused_tile<FM>(src, t, gbase, mt, pv, n, endkey, st, fu_tiles(n), part, scal);
-  }
-}
-
-// Sum the partials of the tiles that start below the cut, then what
-// k_faith_finish does (Q3, the -1 key, traversed) and the case counts.
-__global__ __launch_bounds__(BLOCK) void k_faith_fused_finish(uint32_t ref, uint64_t n, PkView pv,
-                                                             const unsigned long long* st, uint64_t ntiles,
-                                                             const unsigned long long* part,
-                                                             const unsigned long long* scal, GTable g) {
+// One workgroup per reference with samples: the partials of its tiles that
+// start below its cut; Q3 (nothing dropped: the owner of the final largest
+// sink stays in LAT, +1 cold if it is tid 0); the -1 key (materialised even
+// with 0, r10:196,671), traversed, the (ref, case) bins.
+__global__ __launch_bounds__(BLOCK) void k_fa_finish(Model m, FaRefs a, const unsigned long long* __restrict__ tmax,
+                                                     const unsigned long long* __restrict__ pmin,
+                                                     const unsigned long long* __restrict__ part,
+                                                     const unsigned long long* scal, GTable g) {
   __shared__ unsigned long long red[BLOCK / 64][FPART];
-  const uint64_t cut = scal[0];
+  const uint32_t r = blockIdx.x;
+  const uint64_t n = a.n[r];
+  if (n == 0) return;
+  const uint64_t cut = scal[r * FA_SCAL];
+  const uint64_t t0 = a.toff[r], nt = a.toff[r + 1] - t0;
   unsigned long long v[FPART] = {0, 0, 0, 0, 0};
-  for (uint64_t t = threadIdx.x; t < ntiles && t * FCHUNK < cut; t += BLOCK)
+  for (uint64_t t = threadIdx.x; t < nt && t * TILE < cut; t += BLOCK)
 #pragma unroll
-    for (int f = 0; f < FPART; ++f) v[f] += part[t * FPART + f];
+    for (int f = 0; f < FPART; ++f) v[f] += part[(t0 + t) * FPART + f];
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
 #pragma unroll
   for (int f = 0; f < FPART; ++f) {
@@ -796,17 +848,17 @@ __global__ __launch_bounds__(BLOCK) void k_faith_fused_finish(uint32_t ref, uint
     for (int x = 0; x < BLOCK / 64; ++x)
       for (int f = 0; f < FPART; ++f) tot[f] += red[x][f];
     unsigned long long cold = tot[0];
-    if (n > 0 && cut == n) {  // Q3: nothing dropped; the owner of the largest sink stays in LAT
-      const unsigned long long gm = st_uncap(st[ntiles - 1] & ST_VAL);
-      if (gm != KEY_EMPTY && (pv.p2 ? (gm & (pv.T - 1)) : gm % pv.T) == 0) cold += 1;
+    if (cut == n) {
+      const uint64_t last = t0 + nt - 1;
+      const unsigned long long gm = tmax[last] > pmin[last] ? tmax[last] : pmin[last];
+      if (gm != KEY_EMPTY && gm % m.T == 0) cold += 1;
     }
-    g_add(g, make_key(ref, 0, -1), cold);
-    g.trav[ref] += tot[1];
+    g_add(g, make_key(r, 0, -1), cold);
+    g.trav[r] += tot[1];
     for (int c = 0; c < 3; ++c)
-      if (tot[2 + c]) atomicAdd(&g.bins[ref * 3 + c], tot[2 + c]);
+      if (tot[2 + c]) atomicAdd(&g.bins[r * 3 + c], tot[2 + c]);
   }
 }
-
 
 // Record the shard's samples with global index < cut: RI bins, tid-0 cold
 // samples, and the traversed contributions of the replays that start or end
@@ -1128,121 +1180,6 @@ static int faith_record(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, uint64_t n
   return PLUSS_OK;
 }
 
-// the radix-sort pipeline of one sampler_<REF> over its buffer set, on stream s
-static int faith_pipeline_sorted(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, const uint64_t* d_samples, uint64_t n,
-                                 hipStream_t s) {
-  if (n == 0) return PLUSS_OK;
-  if (int rc = faith_keys(ctx, b, ref, d_samples, n, 0, 0, nullptr, s)) return rc;
-  if (int rc = faith_sort(ctx, b, ref, n, s, false)) return rc;
-  const int fm = faith_fm(ctx->m);
-  if (fm != FM_PAIRS) {
-    const uint64_t nt = fu_tiles(n);
-    hipLaunchKernelGGL(k_faith_scan_init, dim3((unsigned)std::min<uint64_t>((2 * nt + BLOCK - 1) / BLOCK + 1, 64)),
-                       dim3(BLOCK), 0, s, b.scal, n, b.st, 2 * nt);
-    const PkView pv = make_pkview(ctx->m, (uint32_t)ref);
-    const unsigned long long endkey = ctx->m.A * ctx->m.T;
-    unsigned long long* part = b.pmax;  // the prefix max is not stored: its buffer holds the partials
-    if (fm == FM_PK32)
-      hipLaunchKernelGGL(k_faith_fused<FM_PK32>, dim3((unsigned)nt), dim3(FB), 0, s, (const void*)b.keys_s, pv, n,
-                         endkey, b.st, part, b.scal);
-    else
-      hipLaunchKernelGGL(k_faith_fused<FM_PK64>, dim3((unsigned)nt), dim3(FB), 0, s, (const void*)b.keys_s, pv, n,
-                         endkey, b.st, part, b.scal);
-    hipLaunchKernelGGL(k_faith_fused_finish, dim3(1), dim3(BLOCK), 0, s, (uint32_t)ref, n, pv, b.st, nt, part,
-                       b.scal, ctx->g);
-    PLUSS_HIP_CHECK(hipGetLastError());
-    ctx->tables_dirty = true;
-    return PLUSS_OK;
-  }
-  const uint64_t nw = 2 * sc_tiles(n);
-  hipLaunchKernelGGL(k_faith_scan_init, dim3((unsigned)std::min<uint64_t>((nw + BLOCK - 1) / BLOCK + 1, 64)),
-                     dim3(BLOCK), 0, s, b.scal, n, b.st, nw);
-  const FlagArgs fa{b.keys_s, b.pmax, 0, 0, make_pkview(ctx->m, (uint32_t)ref)};
-  const dim3 grid((unsigned)sc_tiles(n));
-  if (fm == FM_PK32)
-    hipLaunchKernelGGL(k_faith_scan<FM_PK32>, grid, dim3(BLOCK), 0, s, fa, b.sinks_s, b.pmax, n, b.st, b.scal);
-  else if (fm == FM_PK64)
-    hipLaunchKernelGGL(k_faith_scan<FM_PK64>, grid, dim3(BLOCK), 0, s, fa, b.sinks_s, b.pmax, n, b.st, b.scal);
-  else
-    hipLaunchKernelGGL(k_faith_scan<FM_PAIRS>, grid, dim3(BLOCK), 0, s, fa, b.sinks_s, b.pmax, n, b.st, b.scal);
-  PLUSS_HIP_CHECK(hipGetLastError());
-  return faith_record(ctx, b, ref, n, 0, 0, 0, n, 1, s);
-}
-
-// One sampler_<REF>: keys, radix sort, fused scan.
-int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s) {
-  if (int rc = faith_check_shape(ctx)) return rc;
-  FaithfulBufs& b = ctx->fb;
-  if (int rc = faith_reserve(ctx, b, n, s)) return rc;
-  return faith_pipeline_sorted(ctx, b, ref, d_samples, n, s);
-}
-
-// ---- direct passes over key-ordered lists: no keys pass, no sort.  One
-// launch of k_faith_fused_direct (FCHUNK-element tiles chained by decoupled
-// look-back) and the finish kernel.
-static int faith_direct_shape(const pluss_ctx* ctx, const char* api) {
-  if (int rc = faith_check_shape(ctx)) return rc;
-  if (!ctx->m.fast) {
-    set_error(std::string(api) + ": needs N % (cls/ds) == 0 (packed words); use pluss_dev_faithful_hist");
-    return PLUSS_ERR_CONFIG;
-  }
-  return PLUSS_OK;
-}
-
-static int faith_reserve_direct(FaithfulBufs& b, uint64_t n, hipStream_t s) {
-  if (!b.scal) {
-    if (int rc = grow(&b.scal, 8)) return rc;
-  }
-  if (n > 0xFFFFFFFFull) {
-    set_error("faithful mode: at most 2^32-1 samples per reference");
-    return PLUSS_ERR_CONFIG;
-  }
-  const uint64_t nt = fu_tiles(n);
-  if (nt > b.dcap) {
-    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
-    int rc = 0;
-    if ((rc = grow(&b.dst, 2 * nt)) || (rc = grow(&b.dpart, nt * FPART))) return rc;
-    b.dcap = nt;
-  }
-  return PLUSS_OK;
-}
-
-// kg == nullptr: the samples are read from d_samples (checked to be in key order)
-static int faith_pipeline_direct(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, const uint64_t* d_samples,
-                                 const KeyGen* kg, uint64_t n, hipStream_t s) {
-  if (n == 0) return PLUSS_OK;
-  const Model& m = ctx->m;
-  const uint64_t nt = fu_tiles(n);
-  hipLaunchKernelGGL(k_faith_scan_init, dim3((unsigned)std::min<uint64_t>((2 * nt + BLOCK - 1) / BLOCK + 1, 64)),
-                     dim3(BLOCK), 0, s, b.scal, n, b.dst, 2 * nt);
-  const PkView pv = make_pkview(m, (uint32_t)ref);
-  const unsigned long long endkey = m.A * m.T;
-  const KeyGen k = kg ? *kg : KeyGen{};
-  const bool pk32 = faith_fm(m) == FM_PK32;
-#define PLUSS_DIRECT(FMV, GENV)                                                                                  \
-  hipLaunchKernelGGL((k_faith_fused_direct<FMV, GENV>), dim3((unsigned)nt), dim3(FB), 0, s, m, (uint32_t)ref, \
-                     d_samples, k, pv, n, endkey, b.dst, b.dpart, b.scal, ctx->g)
-  if (kg) {
-    if (pk32) PLUSS_DIRECT(FM_PK32, true);
-    else PLUSS_DIRECT(FM_PK64, true);
-  } else {
-    if (pk32) PLUSS_DIRECT(FM_PK32, false);
-    else PLUSS_DIRECT(FM_PK64, false);
-  }
-#undef PLUSS_DIRECT
-  hipLaunchKernelGGL(k_faith_fused_finish, dim3(1), dim3(BLOCK), 0, s, (uint32_t)ref, n, pv, b.dst, nt, b.dpart,
-                     b.scal, ctx->g);
-  PLUSS_HIP_CHECK(hipGetLastError());
-  ctx->tables_dirty = true;
-  return PLUSS_OK;
-}
-
-int launch_faithful_sorted(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s) {
-  if (int rc = faith_direct_shape(ctx, "pluss_dev_faithful_hist_sorted")) return rc;
-  if (int rc = faith_reserve_direct(ctx->fb, n, s)) return rc;
-  return faith_pipeline_direct(ctx, ctx->fb, ref, d_samples, nullptr, n, s);
-}
-
 // The six references' pipelines on streams of their own, forked from s and
 // joined back into it, as r10's main runs one thread per reference
 // (r10:3203-3257).  per_ref(r, buffers, stream) enqueues reference r.
@@ -1263,7 +1200,126 @@ static int fork_refs(pluss_ctx* ctx, const uint64_t* counts, hipStream_t s, F&& 
   return PLUSS_OK;
 }
 
-// All six sampler_<REF> of one list at once (radix-sort pipeline).
+// ---- the scan pipeline (k_fa_*) over the references with a.n[r] > 0, on
+// stream s.  Its buffers are the handle's (ctx->fb): tile maxima, prefixes,
+// look-back words and partials, sized by the tiles of all references.
+static int fa_reserve(FaithfulBufs& b, uint64_t tiles, hipStream_t s) {
+  if (!b.fscal) {
+    if (int rc = grow(&b.fscal, 64)) return rc;
+  }
+  if (tiles > b.dcap) {
+    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+    int rc = 0;
+    if ((rc = grow(&b.dst, tiles)) || (rc = grow(&b.dpart, tiles * FPART)) || (rc = grow(&b.tmax, tiles)) ||
+        (rc = grow(&b.pmin, tiles)))
+      return rc;
+    b.dcap = tiles;
+  }
+  return PLUSS_OK;
+}
+
+static int fa_run(pluss_ctx* ctx, FaRefs& a, int src, bool check, hipStream_t s) {
+  const Model& m = ctx->m;
+  uint64_t t = 0;
+  for (int r = 0; r < 6; ++r) {
+    if (a.n[r] > 0xFFFFFFFFull) {
+      set_error("faithful mode: at most 2^32-1 samples per reference");
+      return PLUSS_ERR_CONFIG;
+    }
+    a.toff[r] = t;
+    t += fa_tiles(a.n[r]);
+    a.pv[r] = make_pkview(m, (uint32_t)r);
+  }
+  a.toff[6] = t;
+  if (t == 0) return PLUSS_OK;
+  FaithfulBufs& b = ctx->fb;
+  if (int rc = fa_reserve(b, t, s)) return rc;
+  const GTable& g = ctx->g;
+#define PLUSS_FA(SRCV, CHK)                                                                                       \
+  do {                                                                                                            \
+    hipLaunchKernelGGL((k_fa_max<SRCV, CHK>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.tmax, g);               \
+    hipLaunchKernelGGL(k_fa_prefix, dim3(6), dim3(PB), 0, s, a, b.tmax, b.pmin, b.dst, b.fscal);                  \
+    hipLaunchKernelGGL((k_fa_scan<SRCV>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.pmin, b.dst, b.dpart, b.fscal, \
+                       g);                                                                                        \
+  } while (0)
+  switch (src) {
+    case SRC_W32: PLUSS_FA(SRC_W32, false); break;
+    case SRC_W64: PLUSS_FA(SRC_W64, false); break;
+    case SRC_SAMPLES:
+      if (check) PLUSS_FA(SRC_SAMPLES, true);
+      else PLUSS_FA(SRC_SAMPLES, false);
+      break;
+    default: PLUSS_FA(SRC_GEN, false); break;
+  }
+#undef PLUSS_FA
+  hipLaunchKernelGGL(k_fa_finish, dim3(6), dim3(BLOCK), 0, s, m, a, b.tmax, b.pmin, b.dpart, b.fscal, g);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  ctx->tables_dirty = true;
+  return PLUSS_OK;
+}
+
+static FaRefs fa_none() {
+  FaRefs a;
+  std::memset((void*)&a, 0, sizeof a);
+  return a;
+}
+
+// the radix-sort pipeline's first half for one sampler_<REF>: packed words
+// (or (key, sink) pairs) of its list, sorted into b.keys_s, on stream s
+static int faith_keys_sorted(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, const uint64_t* d_samples, uint64_t n,
+                             hipStream_t s) {
+  if (int rc = faith_keys(ctx, b, ref, d_samples, n, 0, 0, nullptr, s)) return rc;
+  return faith_sort(ctx, b, ref, n, s, faith_fm(ctx->m) == FM_PAIRS);
+}
+
+// (key, sink) pairs (shapes with N % W != 0): the rocPRIM scans and the record pass
+static int faith_pairs_scan(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, uint64_t n, hipStream_t s) {
+  const uint64_t nw = 2 * sc_tiles(n);
+  hipLaunchKernelGGL(k_faith_scan_init, dim3((unsigned)std::min<uint64_t>((nw + BLOCK - 1) / BLOCK + 1, 64)),
+                     dim3(BLOCK), 0, s, b.scal, n, b.st, nw);
+  const FlagArgs fa{b.keys_s, b.pmax, 0, 0, make_pkview(ctx->m, (uint32_t)ref)};
+  hipLaunchKernelGGL(k_faith_scan<FM_PAIRS>, dim3((unsigned)sc_tiles(n)), dim3(BLOCK), 0, s, fa, b.sinks_s, b.pmax, n,
+                     b.st, b.scal);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  return faith_record(ctx, b, ref, n, 0, 0, 0, n, 1, s);
+}
+
+// One sampler_<REF> over a list in any order: keys, radix sort, scan.
+int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s) {
+  if (int rc = faith_check_shape(ctx)) return rc;
+  if (n == 0) return PLUSS_OK;
+  FaithfulBufs& b = ctx->fb;
+  if (int rc = faith_reserve(ctx, b, n, s)) return rc;
+  if (int rc = faith_keys_sorted(ctx, b, ref, d_samples, n, s)) return rc;
+  const int fm = faith_fm(ctx->m);
+  if (fm == FM_PAIRS) return faith_pairs_scan(ctx, b, ref, n, s);
+  FaRefs a = fa_none();
+  a.n[ref] = n;
+  a.src[ref] = b.keys_s;
+  return fa_run(ctx, a, fm == FM_PK32 ? SRC_W32 : SRC_W64, false, s);
+}
+
+static int faith_direct_shape(const pluss_ctx* ctx, const char* api) {
+  if (int rc = faith_check_shape(ctx)) return rc;
+  if (!ctx->m.fast) {
+    set_error(std::string(api) + ": needs N % (cls/ds) == 0 (packed words); use pluss_dev_faithful_hist");
+    return PLUSS_ERR_CONFIG;
+  }
+  return PLUSS_OK;
+}
+
+int launch_faithful_sorted(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s) {
+  if (int rc = faith_direct_shape(ctx, "pluss_dev_faithful_hist_sorted")) return rc;
+  FaRefs a = fa_none();
+  a.n[ref] = n;
+  a.src[ref] = d_samples;
+  return fa_run(ctx, a, SRC_SAMPLES, true, s);
+}
+
+// All six sampler_<REF> of one list in any order: each reference's keys and
+// radix sort on a stream of its own, forked from s and joined back into it
+// (r10's main runs one thread per reference, r10:3203-3257); then one scan
+// pipeline for the six sorted arrays.
 int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t* counts, hipStream_t s) {
   if (int rc = faith_check_shape(ctx)) return rc;
   uint64_t off[6], total = 0;
@@ -1280,45 +1336,57 @@ int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64
     if (int rc = faith_reserve(ctx, ctx->fbr[r], counts[r], s)) return rc;
     if (int rc = faith_tmp(ctx, ctx->fbr[r], counts[r], s)) return rc;
   }
-  return fork_refs(ctx, counts, s, [&](int r, FaithfulBufs& b, hipStream_t rs) {
-    return faith_pipeline_sorted(ctx, b, r, d_samples + off[r], counts[r], rs);
-  });
+  const int fm = faith_fm(ctx->m);
+  if (fm == FM_PAIRS) {  // the pair path scans per reference on its stream
+    return fork_refs(ctx, counts, s, [&](int r, FaithfulBufs& b, hipStream_t rs) {
+      if (int rc = faith_keys_sorted(ctx, b, r, d_samples + off[r], counts[r], rs)) return rc;
+      return faith_pairs_scan(ctx, b, r, counts[r], rs);
+    });
+  }
+  uint64_t tiles = 0;
+  for (int r = 0; r < 6; ++r) tiles += fa_tiles(counts[r]);
+  if (int rc = fa_reserve(ctx->fb, tiles, s)) return rc;
+  if (int rc = fork_refs(ctx, counts, s, [&](int r, FaithfulBufs& b, hipStream_t rs) {
+        return faith_keys_sorted(ctx, b, r, d_samples + off[r], counts[r], rs);
+      }))
+    return rc;
+  FaRefs a = fa_none();
+  for (int r = 0; r < 6; ++r) {
+    a.n[r] = counts[r];
+    a.src[r] = ctx->fbr[r].keys_s;
+  }
+  return fa_run(ctx, a, fm == FM_PK32 ? SRC_W32 : SRC_W64, false, s);
 }
 
 // All six over a key-ordered list (each reference's block in key order).
 int launch_faithful_sorted_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t* counts, hipStream_t s) {
   if (int rc = faith_direct_shape(ctx, "pluss_dev_faithful_hist_sorted_refs")) return rc;
-  uint64_t off[6], total = 0;
+  FaRefs a = fa_none();
+  uint64_t off = 0;
   for (int r = 0; r < 6; ++r) {
-    off[r] = total;
-    total += counts[r];
+    a.n[r] = counts[r];
+    a.src[r] = d_samples ? d_samples + off : nullptr;
+    off += counts[r];
   }
-  if (total && !d_samples) {
+  if (off && !d_samples) {
     set_error("pluss_dev_faithful_hist_sorted_refs: null sample list");
     return PLUSS_ERR_CONFIG;
   }
-  for (int r = 0; r < 6; ++r)
-    if (counts[r])
-      if (int rc = faith_reserve_direct(ctx->fbr[r], counts[r], s)) return rc;
-  return fork_refs(ctx, counts, s, [&](int r, FaithfulBufs& b, hipStream_t rs) {
-    return faith_pipeline_direct(ctx, b, r, d_samples + off[r], nullptr, counts[r], rs);
-  });
+  return fa_run(ctx, a, SRC_SAMPLES, true, s);
 }
 
 // All six over generated key-order lists (pluss_expand_sorted's lists of
 // totals[r] samples, never written to memory).
 int launch_gen_faithful_refs(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t s) {
   if (int rc = faith_direct_shape(ctx, "pluss_dev_gen_faithful_refs")) return rc;
-  KeyGen kg[6];
+  FaRefs a = fa_none();
   for (int r = 0; r < 6; ++r) {
     if (!totals[r]) continue;
     if (int rc = keygen_check(ctx, r, totals[r], 0, totals[r], "pluss_dev_gen_faithful_refs")) return rc;
-    kg[r] = keygen_of(ctx, seed, r, totals[r]);
-    if (int rc = faith_reserve_direct(ctx->fbr[r], totals[r], s)) return rc;
+    a.n[r] = totals[r];
+    a.kg[r] = keygen_of(ctx, seed, r, totals[r]);
   }
-  return fork_refs(ctx, totals, s, [&](int r, FaithfulBufs& b, hipStream_t rs) {
-    return faith_pipeline_direct(ctx, b, r, nullptr, &kg[r], totals[r], rs);
-  });
+  return fa_run(ctx, a, SRC_GEN, false, s);
 }
 
 // ---- key-range shards (multi-GPU faithful mode; the caller exchanges the

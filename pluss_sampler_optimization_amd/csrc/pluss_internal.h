@@ -63,9 +63,10 @@ struct FaithfulBufs {
   size_t tmp_bytes = 0;
   unsigned long long* scal = nullptr;  // [0] cut, [1] cold, [2] traversed, [3] shard size, [4] scan tile counter
   unsigned long long* st = nullptr;    // look-back status words of the one-GPU scan (2 per tile)
-  // direct passes over key-ordered / generated lists: look-back words and partials per FCHUNK tile
+  // the scan pipeline (pluss_faithful.hip k_fa_*): per tile the look-back word, the partials, the
+  // largest sink and the running max entering it; its scalars (cut per reference, tile counter)
   uint64_t dcap = 0;
-  unsigned long long *dst = nullptr, *dpart = nullptr;
+  unsigned long long *dst = nullptr, *dpart = nullptr, *tmax = nullptr, *pmin = nullptr, *fscal = nullptr;
 };
 
 // state of a key-range shard between the phases of pluss_dev_faithful_shard_*
