@@ -284,6 +284,14 @@ __device__ __forceinline__ unsigned long long sc_wave_red(unsigned long long v) 
   for (int o = 32; o > 0; o >>= 1) v = sc_op<MAX>(v, __shfl_xor(v, o, 64));
   return v;
 }
+__device__ __forceinline__ unsigned long long sc_wave_red_min(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long x = __shfl_xor(v, o, 64);
+    v = x < v ? x : v;
+  }
+  return v;
+}
 template <bool MAX>
 __device__ __forceinline__ unsigned long long sc_wave_scan(unsigned long long v, uint32_t lane) {  // inclusive
 #pragma unroll
@@ -603,35 +611,40 @@ __device__ __forceinline__ FaTile fa_tile(const FaRefs& a, uint64_t gt) {
   return t;
 }
 
-// Wave w of a tile owns elements [w*64*TI, (w+1)*64*TI), visited as TI rounds
-// of 64 (lane l: element w*64*TI + 64k + l): every load is coalesced and the
-// scans run across the lanes of a round with a carry between rounds.
+// Lane-contiguous elements: thread x of a tile owns its elements
+// [x*TI, (x+1)*TI); each lane scans its own run sequentially in registers and
+// the lanes are combined by ONE wave scan per quantity (instead of a 64-wide
+// scan per element round).
 template <int SRC, bool CHECK>
 __global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long long* __restrict__ tmax, GTable g) {
   __shared__ unsigned long long s_w[TB / 64];
   const FaTile T = fa_tile(a, blockIdx.x);
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  const uint32_t lbase = wid * (64 * TI);
-  unsigned long long tm = 0, prev = 0;  // prev: lane 63's key of the previous round
-  bool prev_v = false, unordered = false;
+  const uint32_t e0 = threadIdx.x * TI;
+  const uint64_t n = a.n[T.r];
+  unsigned long long tm = 0, prev = 0, first = KEY_EMPTY;
+  bool unordered = false;
 #pragma unroll
   for (int k = 0; k < TI; ++k) {
-    const uint32_t li = lbase + (uint32_t)k * 64 + lane;
-    const bool v = li < T.mt;
-    const Elem e = v ? fa_elem<SRC>(m, a, T.r, T.base + li, g) : Elem{KEY_EMPTY, 0ull, 3u};
-    tm = e.sink > tm ? e.sink : tm;
-    if (CHECK) {  // key order: every element against the next one
-      const unsigned long long kn = __shfl_down(e.key, 1, 64);  // the next lane's
-      if (lane < 63 && v && li + 1 < T.mt) unordered |= !(kn > e.key);
-      const unsigned long long k0 = __shfl(e.key, 0, 64);  // this round's first vs the previous round's last
-      if (lane == 63 && k > 0 && prev_v && lbase + (uint32_t)k * 64 < T.mt) unordered |= !(k0 > prev);
-      prev = e.key;
-      prev_v = v;
-      if (k + 1 == TI && lane == 63 && v && T.base + li + 1 < a.n[T.r])  // the wave's last vs the next element
-        unordered |= !(fa_elem<SRC>(m, a, T.r, T.base + li + 1, g).key > e.key);
+    if (e0 + k < T.mt) {
+      const Elem e = fa_elem<SRC>(m, a, T.r, T.base + e0 + k, g);
+      tm = e.sink > tm ? e.sink : tm;
+      if (CHECK) {
+        if (k == 0) first = e.key;
+        else unordered |= !(e.key > prev);
+        prev = e.key;
+      }
     }
   }
-  if (CHECK && __ballot(unordered) && lane == 0) atomicOr(&g.flags[1], 1u);
+  if (CHECK) {  // the lane's last element against the next lane's first (lane 63: the next element itself)
+    const unsigned long long nf = __shfl_down(first, 1, 64);
+    const uint64_t inext = T.base + e0 + TI;  // the element after this lane's run
+    if (e0 + TI <= T.mt && inext < n) {
+      const unsigned long long kn = (lane < 63 && e0 + TI < T.mt) ? nf : fa_elem<SRC>(m, a, T.r, inext, g).key;
+      unordered |= !(kn > prev);
+    }
+    if (__ballot(unordered) && lane == 0) atomicOr(&g.flags[1], 1u);
+  }
   tm = sc_wave_red<true>(tm);
   if (lane == 0) s_w[wid] = tm;
   __syncthreads();
@@ -679,7 +692,7 @@ __global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigne
                                                 unsigned long long* st, unsigned long long* __restrict__ part,
                                                 unsigned long long* scal, GTable g) {
   constexpr int NW = TB / 64;
-  __shared__ unsigned long long s_tile, s_w[NW], s_inc, s_red[NW][FPART];
+  __shared__ unsigned long long s_tile, s_w[NW], s_c[NW], s_inc, s_red[NW][FPART];
   if (threadIdx.x == 0) s_tile = atomicAdd(&scal[FA_COUNTER], 1ull);
   __syncthreads();
   const uint64_t gt = s_tile;
@@ -688,7 +701,9 @@ __global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigne
   const uint64_t n = a.n[r];
   const unsigned long long endkey = m.A * m.T;
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  const uint32_t lbase = wid * (64 * TI);
+  const uint32_t e0 = threadIdx.x * TI;                             // this lane's run in the tile
+  const uint32_t nv = e0 < T.mt ? (T.mt - e0 < TI ? T.mt - e0 : TI) : 0u;  // its valid elements
+  const uint64_t i0 = T.base + e0;                                  // index of its first element
   // ri*T per case (KEY_EMPTY: cold), to recompute sinks from keys
   unsigned long long rt[3];
 #pragma unroll
@@ -699,69 +714,64 @@ __global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigne
   };
   unsigned long long key[TI];
   uint32_t cases = 0;  // 2 bits per element
-  unsigned long long tm = 0;
+  unsigned long long lmax = 0;
 #pragma unroll
   for (int k = 0; k < TI; ++k) {
-    const uint32_t li = lbase + (uint32_t)k * 64 + lane;
-    const Elem e = li < T.mt ? fa_elem<SRC>(m, a, r, T.base + li, g) : Elem{KEY_EMPTY, 0ull, 3u};
+    Elem e{KEY_EMPTY, 0ull, 3u};
+    if ((uint32_t)k < nv) e = fa_elem<SRC>(m, a, r, i0 + k, g);
     key[k] = e.key;
     cases |= (e.c & 3u) << (2 * k);
-    if (li < T.mt) tm = e.sink > tm ? e.sink : tm;
+    if ((uint32_t)k < nv) lmax = e.sink > lmax ? e.sink : lmax;
   }
-  // prefix max entering each wave: the tile's incoming max and the earlier waves' maxima
-  tm = sc_wave_red<true>(tm);
-  if (lane == 0) s_w[wid] = tm;
+  // running max of sinks entering this lane: the tile's incoming max, the
+  // earlier waves' maxima, the earlier lanes' maxima
+  const unsigned long long linc = sc_wave_scan<true>(lmax, lane);
+  if (lane == 63) s_w[wid] = linc;
   __syncthreads();
   unsigned long long carry = pmin[gt];
 #pragma unroll
   for (int x = 0; x < NW; ++x)
     if (x < (int)wid) carry = s_w[x] > carry ? s_w[x] : carry;
-  unsigned long long pm[TI], fmask[TI];
-  uint32_t wcnt = 0;
-#pragma unroll
-  for (int k = 0; k < TI; ++k) {
-    const uint32_t li = lbase + (uint32_t)k * 64 + lane;
-    const uint64_t i = T.base + li;
-    const bool valid = li < T.mt;
-    const uint32_t c = (cases >> (2 * k)) & 3u;
-    unsigned long long inc = sc_wave_scan<true>(valid ? sink_of(key[k], c) : 0ull, lane);
-    inc = inc > carry ? inc : carry;
-    const unsigned long long up = __shfl_up(inc, 1, 64);
-    const unsigned long long before = lane ? up : carry;
-    fmask[k] = __ballot(valid && (i == 0 || key[k] > before));
-    wcnt += (uint32_t)__popcll(fmask[k]);
-    pm[k] = inc;
-    carry = __shfl(inc, 63, 64);
+  {
+    const unsigned long long up = __shfl_up(linc, 1, 64);
+    if (lane) carry = up > carry ? up : carry;
   }
-  // start counts: this tile's total, chained over the reference's tiles
-  __syncthreads();  // s_w is reused
-  if (lane == 0) s_w[wid] = wcnt;
+  // start flags: key > the running max before it (or the reference's first element)
+  uint32_t flags = 0, lcnt = 0;
+  {
+    unsigned long long run = carry;
+#pragma unroll
+    for (int k = 0; k < TI; ++k) {
+      if ((uint32_t)k < nv) {
+        const bool f = (i0 + k == 0) || key[k] > run;
+        flags |= (f ? 1u : 0u) << k;
+        lcnt += f ? 1u : 0u;
+        const unsigned long long sk = sink_of(key[k], (cases >> (2 * k)) & 3u);
+        run = sk > run ? sk : run;
+      }
+    }
+  }
+  // start counts: lanes, waves, then the chain over the reference's tiles
+  const unsigned long long cinc = sc_wave_scan<false>(lcnt, lane);
+  if (lane == 63) s_c[wid] = cinc;
   __syncthreads();
   unsigned long long cpre = 0, cagg = 0;
 #pragma unroll
   for (int x = 0; x < NW; ++x) {
-    const unsigned long long v = s_w[x];
-    if (x < (int)wid) cpre += v;
-    cagg += v;
+    if (x < (int)wid) cpre += s_c[x];
+    cagg += s_c[x];
   }
   const unsigned long long c_in = fu_chain<false>(st + a.toff[r], (uint32_t)T.lt, cagg, lane, &s_inc);
+  const uint64_t sb0 = c_in + cpre + (cinc - lcnt);  // starts before this lane's first element
   // the tile's Q1 candidate: its first start j > 0 with j - starts_before_j >= n - j
   unsigned long long best = KEY_EMPTY;
-  {
-    uint64_t cb = c_in + cpre;
-    const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
-    for (int k = 0; k < TI; ++k) {
-      const unsigned long long F = fmask[k];
-      if (best == KEY_EMPTY && F) {
-        const uint64_t j = T.base + lbase + (uint64_t)k * 64 + lane;
-        const uint64_t before_j = cb + (uint64_t)__popcll(F & below);
-        const unsigned long long q = __ballot(((F >> lane) & 1ull) && j > 0 && j - before_j >= n - j);
-        if (q) best = T.base + lbase + (uint64_t)k * 64 + (uint64_t)(__ffsll((long long)q) - 1);
-      }
-      cb += (uint64_t)__popcll(F);
-    }
+  for (int k = 0; k < TI; ++k) {
+    const uint64_t j = i0 + k;
+    const uint64_t before_j = sb0 + (uint64_t)__popc(flags & ((1u << k) - 1u));
+    if (best == KEY_EMPTY && ((flags >> k) & 1u) && j > 0 && j - before_j >= n - j) best = j;
   }
+  best = sc_wave_red_min(best);
   __syncthreads();  // s_w is reused
   if (lane == 0) s_w[wid] = best;
   __syncthreads();
@@ -769,52 +779,48 @@ __global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigne
 #pragma unroll
   for (int x = 0; x < NW; ++x) cut = s_w[x] < cut ? s_w[x] : cut;
   if (threadIdx.x == 0 && cut < n) atomicMin(&scal[r * FA_SCAL], cut);
-  // record the tile's elements below its own candidate
+  // record this lane's elements below the tile's candidate
   unsigned long long cold = 0, trav = 0;
   uint32_t nc0 = 0, nc1 = 0, nc2 = 0;
   const uint64_t tmask = m.T - 1;
   const bool tp2 = (m.T & tmask) == 0;
+  // the key after this lane's run: the next lane's first, or (lane 63, or the tile's end) the source's
+  unsigned long long knext = __shfl_down(key[0], 1, 64);
+  if (lane == 63 || e0 + TI >= T.mt) knext = (nv == TI && i0 + TI < n) ? fa_elem<SRC>(m, a, r, i0 + TI, g).key : KEY_EMPTY;
+  {
+    unsigned long long run = carry;
 #pragma unroll
-  for (int k = 0; k < TI; ++k) {
-    const uint32_t li = lbase + (uint32_t)k * 64 + lane;
-    const uint64_t i = T.base + li;
-    const unsigned long long kk = key[k];
-    // the next element's key: the next lane, the next round's lane 0, or (the wave's last element) the source
-    unsigned long long kn = __shfl_down(kk, 1, 64);
-    if (k + 1 < TI) {
-      const unsigned long long k0 = __shfl(key[k + 1], 0, 64);
-      if (lane == 63) kn = k0;
-    } else if (lane == 63) {
-      kn = (li < T.mt && i + 1 < n) ? fa_elem<SRC>(m, a, r, i + 1, g).key : KEY_EMPTY;
+    for (int k = 0; k < TI; ++k) {
+      const uint64_t i = i0 + k;
+      if ((uint32_t)k < nv && i < cut) {
+        const uint32_t c = (cases >> (2 * k)) & 3u;
+        const unsigned long long kk = key[k], sk = sink_of(kk, c);
+        const unsigned long long gm = sk > run ? sk : run;  // inclusive running max at i
+        run = gm;
+        if (sk == KEY_EMPTY) {
+          cold += ((tp2 ? (kk & tmask) : kk % m.T) == 0) ? 1u : 0u;
+        } else {
+          nc0 += c == 0 ? 1u : 0u;
+          nc1 += c == 1 ? 1u : 0u;
+          nc2 += c == 2 ? 1u : 0u;
+        }
+        if ((flags >> k) & 1u) trav -= kk;  // this element starts a replay
+        const unsigned long long kn = k + 1 < TI ? key[k + 1 < TI ? k + 1 : k] : knext;
+        if (i + 1 == cut || (i + 1 < n ? kn > gm : true)) trav += (gm == KEY_EMPTY) ? endkey : gm;  // ends one
+      }
     }
-    const uint32_t c = (cases >> (2 * k)) & 3u;
-    bool rec = false;
-    if (li < T.mt && i < cut) {
-      if (sink_of(kk, c) == KEY_EMPTY) cold += ((tp2 ? (kk & tmask) : kk % m.T) == 0) ? 1u : 0u;
-      else rec = true;
-      if ((fmask[k] >> lane) & 1ull) trav -= kk;  // this element starts a replay
-      const unsigned long long gm = pm[k];
-      if (i + 1 == cut || (i + 1 < n ? kn > gm : true)) trav += (gm == KEY_EMPTY) ? endkey : gm;  // ends one
-    }
-    nc0 += (uint32_t)__popcll(__ballot(rec && c == 0));
-    nc1 += (uint32_t)__popcll(__ballot(rec && c == 1));
-    nc2 += (uint32_t)__popcll(__ballot(rec && c == 2));
   }
-  cold = sc_wave_red<false>(cold);
-  trav = sc_wave_red<false>(trav);
-  if (lane == 0) {
-    s_red[wid][0] = cold;
-    s_red[wid][1] = trav;
-    s_red[wid][2] = nc0;
-    s_red[wid][3] = nc1;
-    s_red[wid][4] = nc2;
-  }
+  const unsigned long long v[FPART] = {sc_wave_red<false>(cold), sc_wave_red<false>(trav),
+                                       sc_wave_red<false>(nc0), sc_wave_red<false>(nc1), sc_wave_red<false>(nc2)};
+  if (lane == 0)
+#pragma unroll
+    for (int f = 0; f < FPART; ++f) s_red[wid][f] = v[f];
   __syncthreads();
   if (threadIdx.x < FPART) {
-    unsigned long long v = 0;
+    unsigned long long x = 0;
 #pragma unroll
-    for (int x = 0; x < NW; ++x) v += s_red[x][threadIdx.x];
-    part[gt * FPART + threadIdx.x] = v;
+    for (int w = 0; w < NW; ++w) x += s_red[w][threadIdx.x];
+    part[gt * FPART + threadIdx.x] = x;
   }
 }
 
