@@ -591,6 +591,39 @@ __device__ __forceinline__ Elem fa_elem(const Model& m, const FaRefs& a, uint32_
   return elem_of_sample(m, a.pv[r], r, x, g);
 }
 
+// A tile's elements as read from memory (raw words / samples), staged in LDS:
+// loaded coalesced (thread x, round k: element k*TB + x), read back by each
+// thread as its contiguous run (x*TI + k).  One padding slot per TI elements
+// keeps the run reads at 2-way bank conflicts.
+template <int SRC>
+using fa_raw_t = typename std::conditional<SRC == SRC_W32, uint32_t, unsigned long long>::type;
+constexpr uint32_t FA_LDS = TILE + TILE / TI;
+__device__ __forceinline__ uint32_t fa_slot(uint32_t e) { return e + e / TI; }
+
+template <int SRC>
+__device__ __forceinline__ void fa_stage(const FaRefs& a, uint32_t r, uint64_t base, uint32_t mt,
+                                         fa_raw_t<SRC>* lds) {
+  if (SRC == SRC_GEN) return;
+  const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(a.src[r]) + base;
+#pragma unroll
+  for (int k = 0; k < TI; ++k) {
+    const uint32_t e = (uint32_t)k * TB + threadIdx.x;
+    if (e < mt) lds[fa_slot(e)] = src[e];
+  }
+  __syncthreads();
+}
+
+// element e of the tile (lane-contiguous read from the staged raw data)
+template <int SRC>
+__device__ __forceinline__ Elem fa_tile_elem(const Model& m, const FaRefs& a, uint32_t r, uint64_t base, uint32_t e,
+                                             const fa_raw_t<SRC>* lds, GTable g) {
+  if (SRC == SRC_GEN) return elem_of_sample(m, a.pv[r], r, keygen_sample(a.kg[r], base + e), g);
+  const fa_raw_t<SRC> w = lds[fa_slot(e)];
+  if (SRC == SRC_SAMPLES) return elem_of_sample(m, a.pv[r], r, w, g);
+  const bool bad = w == (fa_raw_t<SRC>) ~(fa_raw_t<SRC>)0;
+  return Elem{pk_key(w, a.pv[r]), pk_sink(w, a.pv[r]), bad ? 3u : (uint32_t)(w & 3u)};
+}
+
 // the tile's reference (wave-uniform) and its place in it
 struct FaTile {
   uint32_t r;
@@ -618,7 +651,9 @@ __device__ __forceinline__ FaTile fa_tile(const FaRefs& a, uint64_t gt) {
 template <int SRC, bool CHECK>
 __global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long long* __restrict__ tmax, GTable g) {
   __shared__ unsigned long long s_w[TB / 64];
+  __shared__ fa_raw_t<SRC> s_raw[SRC == SRC_GEN ? 1 : FA_LDS];
   const FaTile T = fa_tile(a, blockIdx.x);
+  fa_stage<SRC>(a, T.r, T.base, T.mt, s_raw);
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
   const uint32_t e0 = threadIdx.x * TI;
   const uint64_t n = a.n[T.r];
@@ -627,7 +662,7 @@ __global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long 
 #pragma unroll
   for (int k = 0; k < TI; ++k) {
     if (e0 + k < T.mt) {
-      const Elem e = fa_elem<SRC>(m, a, T.r, T.base + e0 + k, g);
+      const Elem e = fa_tile_elem<SRC>(m, a, T.r, T.base, e0 + k, s_raw, g);
       tm = e.sink > tm ? e.sink : tm;
       if (CHECK) {
         if (k == 0) first = e.key;
@@ -693,10 +728,12 @@ __global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigne
                                                 unsigned long long* scal, GTable g) {
   constexpr int NW = TB / 64;
   __shared__ unsigned long long s_tile, s_w[NW], s_c[NW], s_inc, s_red[NW][FPART];
+  __shared__ fa_raw_t<SRC> s_raw[SRC == SRC_GEN ? 1 : FA_LDS];
   if (threadIdx.x == 0) s_tile = atomicAdd(&scal[FA_COUNTER], 1ull);
   __syncthreads();
   const uint64_t gt = s_tile;
   const FaTile T = fa_tile(a, gt);
+  fa_stage<SRC>(a, T.r, T.base, T.mt, s_raw);
   const uint32_t r = T.r;
   const uint64_t n = a.n[r];
   const unsigned long long endkey = m.A * m.T;
@@ -718,7 +755,7 @@ __global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigne
 #pragma unroll
   for (int k = 0; k < TI; ++k) {
     Elem e{KEY_EMPTY, 0ull, 3u};
-    if ((uint32_t)k < nv) e = fa_elem<SRC>(m, a, r, i0 + k, g);
+    if ((uint32_t)k < nv) e = fa_tile_elem<SRC>(m, a, r, T.base, e0 + k, s_raw, g);
     key[k] = e.key;
     cases |= (e.c & 3u) << (2 * k);
     if ((uint32_t)k < nv) lmax = e.sink > lmax ? e.sink : lmax;
