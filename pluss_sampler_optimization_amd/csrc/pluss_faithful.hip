@@ -563,20 +563,36 @@ struct Elem {
   uint32_t c;
 };
 
+__device__ __forceinline__ Elem elem_of_digits(const Model& m, const PkView& v, uint32_t ref, const KeyDigits& d) {
+  const uint64_t a = ((uint64_t)d.q * m.N + d.c1) * m.S + ref_off(ref, d.c2);
+  const uint64_t key = v.p2 ? ((a << v.tsh) | d.t) : a * m.T + d.t;
+  const uint32_t c = case_of_digits(m, ref, d, (uint32_t)(m.N / m.T));
+  const int64_t ri = c == 0 ? v.ri[0] : (c == 1 ? v.ri[1] : v.ri[2]);
+  const unsigned long long dt = v.p2 ? ((unsigned long long)ri << v.tsh) : (unsigned long long)ri * m.T;
+  return Elem{key, ri < 0 ? KEY_EMPTY : key + dt, c};
+}
+
 __device__ __forceinline__ Elem elem_of_sample(const Model& m, const PkView& v, uint32_t ref, uint64_t x, GTable g) {
   const Sample s = unpack(x);
   if (s.ref != ref || s.c0 >= m.N || s.c1 >= m.N || s.c2 >= m.N) {
     atomicOr(&g.flags[1], 1u);
     return Elem{KEY_EMPTY, KEY_EMPTY, 3u};
   }
-  const uint32_t c2 = (ref == C0 || ref == C1) ? 0u : s.c2;
-  const uint32_t k = fdiv(s.c0, m.dCS), p = s.c0 - k * m.CS;
-  const uint32_t kt = fdiv(k, m.dT), t = k - kt * m.T;
-  const uint64_t q = (uint64_t)kt * m.CS + p;
-  const uint64_t key = (q * m.R + (uint64_t)s.c1 * m.S + ref_off(ref, c2)) * m.T + t;
-  const uint32_t c = case_fast<false>(m, ref, s.c0, s.c1, c2);
-  const int64_t ri = c == 0 ? v.ri[0] : (c == 1 ? v.ri[1] : v.ri[2]);
-  return Elem{key, ri < 0 ? KEY_EMPTY : key + (unsigned long long)ri * m.T, c};
+  KeyDigits d;
+  d.c1 = s.c1;
+  d.c2 = (ref == C0 || ref == C1) ? 0u : s.c2;
+  uint32_t k;
+  if (v.p2 && m.p2) {  // T, N, CS (and W) powers of two
+    k = s.c0 >> m.csshift;
+    d.t = k & (m.T - 1);
+    d.q = ((k >> v.tsh) << m.csshift) | (s.c0 & m.csmask);
+  } else {
+    k = fdiv(s.c0, m.dCS);
+    const uint32_t kt = fdiv(k, m.dT);
+    d.t = k - kt * m.T;
+    d.q = kt * m.CS + (s.c0 - k * m.CS);
+  }
+  return elem_of_digits(m, v, ref, d);
 }
 
 template <int SRC>
@@ -612,6 +628,37 @@ __device__ __forceinline__ void fa_stage(const FaRefs& a, uint32_t r, uint64_t b
   }
   __syncthreads();
 }
+
+// A lane's run of consecutive elements: read from the staged tile, or
+// generated in sequence (keyrun_*: digits carried from one sample to the next).
+template <int SRC>
+struct FaCursor {
+  const Model& m;
+  const FaRefs& a;
+  uint32_t r;
+  uint64_t base;
+  uint32_t e;
+  const fa_raw_t<SRC>* lds;
+  GTable g;
+  KeyRun run;
+  __device__ FaCursor(const Model& m_, const FaRefs& a_, uint32_t r_, uint64_t base_, uint32_t e0,
+                      const fa_raw_t<SRC>* lds_, GTable g_)
+      : m(m_), a(a_), r(r_), base(base_), e(e0), lds(lds_), g(g_) {
+    if (SRC == SRC_GEN) keyrun_start(a.kg[r], run, base + e0);
+  }
+  // the element at the cursor; then the cursor moves on
+  __device__ Elem next() {
+    Elem x;
+    if (SRC == SRC_GEN) {
+      x = elem_of_digits(m, a.pv[r], r, keyrun_digits(a.kg[r], run));
+      keyrun_next(a.kg[r], run);
+    } else {
+      x = fa_tile_elem<SRC>(m, a, r, base, e, lds, g);
+    }
+    ++e;
+    return x;
+  }
+};
 
 // element e of the tile (lane-contiguous read from the staged raw data)
 template <int SRC>
@@ -659,10 +706,11 @@ __global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long 
   const uint64_t n = a.n[T.r];
   unsigned long long tm = 0, prev = 0, first = KEY_EMPTY;
   bool unordered = false;
+  FaCursor<SRC> cur(m, a, T.r, T.base, e0 < T.mt ? e0 : 0u, s_raw, g);
 #pragma unroll
   for (int k = 0; k < TI; ++k) {
     if (e0 + k < T.mt) {
-      const Elem e = fa_tile_elem<SRC>(m, a, T.r, T.base, e0 + k, s_raw, g);
+      const Elem e = cur.next();
       tm = e.sink > tm ? e.sink : tm;
       if (CHECK) {
         if (k == 0) first = e.key;
@@ -752,10 +800,11 @@ __global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigne
   unsigned long long key[TI];
   uint32_t cases = 0;  // 2 bits per element
   unsigned long long lmax = 0;
+  FaCursor<SRC> cur(m, a, r, T.base, nv ? e0 : 0u, s_raw, g);
 #pragma unroll
   for (int k = 0; k < TI; ++k) {
     Elem e{KEY_EMPTY, 0ull, 3u};
-    if ((uint32_t)k < nv) e = fa_tile_elem<SRC>(m, a, r, T.base, e0 + k, s_raw, g);
+    if ((uint32_t)k < nv) e = cur.next();
     key[k] = e.key;
     cases |= (e.c & 3u) << (2 * k);
     if ((uint32_t)k < nv) lmax = e.sink > lmax ? e.sink : lmax;

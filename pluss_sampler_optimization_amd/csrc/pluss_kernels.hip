@@ -656,25 +656,27 @@ __global__ __launch_bounds__(BLOCK) void k_count(Model m, const uint64_t* __rest
 // k_gen_count: the key-order lists of the six references (pluss_model.h
 // KeyGen) counted while they are generated -- the samples never touch
 // memory; = pluss_dev_expand_sorted of every slice + one dense pass.  A wave
-// step is GK = 2*UNROLL rounds of 64 consecutive samples of one reference
-// (lane l: samples base + 64k + l); each reference's slice is padded to whole
-// wave steps, so the reference, its generator and its case tests are
-// wave-uniform.  Counting and tail are k_count's.
+// step is 64 runs of GR consecutive samples of one reference (lane l: samples
+// base + l*GR ... + GR-1, generated incrementally by keyrun_*); each
+// reference's slice is padded to whole wave steps, so the reference, its
+// generator and its case rules are wave-uniform.  A sample's outcome comes
+// straight from its digits (case_of_digits); per-lane counters per
+// (reference, case), folded at the end into k_count's dense tail.
+constexpr uint32_t GR = 16;
 struct GenArgs {
   KeyGen k[6];
   uint64_t first[6], n[6];
   uint64_t wbeg[7];  // first wave step of each reference; wbeg[6] = all steps
 };
-constexpr uint32_t GK = 2 * UNROLL;
 
-template <bool P2, bool NP2>
 __global__ __launch_bounds__(BLOCK) void k_gen_count(Model m, GenArgs ga, GTable g, ExportArgs ex) {
   __shared__ unsigned long long tot[DBINS];
   if (threadIdx.x < DBINS) tot[threadIdx.x] = 0;
-  uint32_t acc = 0;
-  LaneCounts lc;
-  lc_init(lc);
+  uint32_t na[6], nb[6], nt[6];  // per reference: case 0, case 1, all (case 2 = the rest)
+#pragma unroll
+  for (int x = 0; x < 6; ++x) na[x] = nb[x] = nt[x] = 0;
   const uint32_t lane = __lane_id();
+  const uint32_t Q = m.N / m.T;
   const uint64_t nw = (uint64_t)gridDim.x * (BLOCK / 64);
   const uint64_t w0 = (uint64_t)blockIdx.x * (BLOCK / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (uint64_t ws = w0; ws < ga.wbeg[6]; ws += nw) {
@@ -683,23 +685,41 @@ __global__ __launch_bounds__(BLOCK) void k_gen_count(Model m, GenArgs ga, GTable
     for (int x = 1; x < 6; ++x) r += ws >= ga.wbeg[x] ? 1u : 0u;
     r = __builtin_amdgcn_readfirstlane(r);
     const KeyGen& kg = ga.k[r];
-    const uint64_t rel = (ws - ga.wbeg[r]) * (GK * 64);  // this step's first sample within the slice
+    const uint64_t j0 = (ws - ga.wbeg[r]) * (64 * GR) + lane * GR;  // this lane's run within the slice
     const uint64_t nr = ga.n[r];
-    uint32_t lo[GK], hi[GK];
-    uint64_t okm[GK];
+    uint32_t a = 0, b = 0, v = 0;
+    if (j0 < nr) {
+      const uint32_t cnt = nr - j0 < GR ? (uint32_t)(nr - j0) : GR;
+      KeyRun run;
+      keyrun_start(kg, run, ga.first[r] + j0);
 #pragma unroll
-    for (int k = 0; k < (int)GK; ++k) {
-      const uint64_t j = rel + (uint64_t)k * 64 + lane;
-      const bool ok = j < nr;
-      const uint64_t x = ok ? keygen_sample(kg, ga.first[r] + j) : 0ull;
-      lo[k] = (uint32_t)x;
-      hi[k] = (uint32_t)(x >> 32);
-      okm[k] = __ballot(ok);
+      for (uint32_t k = 0; k < GR; ++k) {
+        if (k < cnt) {
+          const uint32_t c = case_of_digits(m, r, keyrun_digits(kg, run), Q);
+          a += c == 0 ? 1u : 0u;
+          b += c == 1 ? 1u : 0u;
+          if (k + 1 < cnt) keyrun_next(kg, run);
+        }
+      }
+      v = cnt;
     }
-    if (!(P2 && NP2 && rel + GK * 64 <= nr && count_step_lanes<UNROLL>(m, lo, hi, lc)))
-      count_step<P2, NP2, UNROLL>(m, lo, hi, okm, acc);
+#pragma unroll
+    for (int x = 0; x < 6; ++x) {  // r is wave-uniform: one scalar branch
+      if (r == (uint32_t)x) {
+        na[x] += a;
+        nb[x] += b;
+        nt[x] += v;
+      }
+    }
   }
-  if (P2 && NP2) lc_flush(lc, acc);
+  uint32_t acc = 0;  // lane b: count of bin b
+#pragma unroll
+  for (int x = 0; x < 6; ++x) {
+    const uint32_t A = wave_sum(na[x]), B = wave_sum(nb[x]), N = wave_sum(nt[x]);
+    acc += lane == (uint32_t)(3 * x) ? A : 0u;
+    acc += lane == (uint32_t)(3 * x + 1) ? B : 0u;
+    acc += lane == (uint32_t)(3 * x + 2) ? N - A - B : 0u;
+  }
   __syncthreads();
   flush_counts(acc, tot);
   __syncthreads();
@@ -948,11 +968,36 @@ __global__ __launch_bounds__(BLOCK) void k_expand(Perm p, uint32_t ref, uint64_t
 
 // ---------------------------------------------------- key-order lists --
 // Samples [first, first + n) of a reference's key-order stratified list
-// (pluss_model.h KeyGen), one lane per sample, coalesced stores.
+// (pluss_model.h KeyGen).  Each thread generates a run of ER
+// consecutive samples incrementally (keyrun_*) into LDS; the block then
+// stores them coalesced.
+constexpr uint32_t ER = 8;
+__device__ __forceinline__ uint32_t er_slot(uint32_t e) { return e + e / ER; }
 __global__ __launch_bounds__(BLOCK) void k_expand_sorted(KeyGen k, uint64_t first, uint64_t n,
                                                          uint64_t* __restrict__ out) {
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK)
-    out[i] = keygen_sample(k, first + i);
+  __shared__ unsigned long long buf[BLOCK * ER + BLOCK];
+  for (uint64_t base = (uint64_t)blockIdx.x * BLOCK * ER; base < n; base += (uint64_t)gridDim.x * BLOCK * ER) {
+    const uint64_t j0 = base + threadIdx.x * ER;
+    if (j0 < n) {
+      const uint32_t cnt = n - j0 < ER ? (uint32_t)(n - j0) : ER;
+      KeyRun run;
+      keyrun_start(k, run, first + j0);
+#pragma unroll
+      for (uint32_t x = 0; x < ER; ++x) {
+        if (x < cnt) {
+          buf[er_slot(threadIdx.x * ER + x)] = keygen_pack(k, keyrun_digits(k, run));
+          if (x + 1 < cnt) keyrun_next(k, run);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t x = 0; x < ER; ++x) {
+      const uint32_t e = x * BLOCK + threadIdx.x;
+      if (base + e < n) out[base + e] = buf[er_slot(e)];
+    }
+    __syncthreads();
+  }
 }
 
 // ------------------------------------------------------------ launchers --
@@ -1165,7 +1210,7 @@ int launch_expand_sorted(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t to
   if (int rc = keygen_check(ctx, ref, total, first, n, "pluss_expand_sorted")) return rc;
   if (n == 0) return PLUSS_OK;
   const KeyGen k = keygen_of(ctx, seed, ref, total);
-  hipLaunchKernelGGL(k_expand_sorted, dim3(grid_for(n, BLOCK * 4, 4096)), dim3(BLOCK), 0, s, k, first, n, d_out);
+  hipLaunchKernelGGL(k_expand_sorted, dim3(grid_for(n, BLOCK * ER, 4096)), dim3(BLOCK), 0, s, k, first, n, d_out);
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }
@@ -1183,20 +1228,12 @@ int launch_gen_count_dense(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals
       if (int rc = keygen_check(ctx, r, totals[r], first[r], n[r], "pluss_dev_gen_count_dense")) return rc;
       ga.k[r] = keygen_of(ctx, seed, r, totals[r]);
     }
-    ga.wbeg[r + 1] = ga.wbeg[r] + (n[r] + GK * 64 - 1) / (GK * 64);
+    ga.wbeg[r + 1] = ga.wbeg[r] + (n[r] + GR * 64 - 1) / (GR * 64);
   }
   const ExportArgs ex{nullptr, nullptr, 0, nullptr, d_counts, DENSE_ROWS};
   // ALU-bound: 8 waves per SIMD
   const int nb = grid_for(ga.wbeg[6] ? ga.wbeg[6] : 1, BLOCK / 64, 2048);
-  const Model& m = ctx->m;
-  if (m.p2 && m.np2)
-    hipLaunchKernelGGL((k_gen_count<true, true>), dim3(nb), dim3(BLOCK), 0, s, m, ga, ctx->g, ex);
-  else if (m.p2)
-    hipLaunchKernelGGL((k_gen_count<true, false>), dim3(nb), dim3(BLOCK), 0, s, m, ga, ctx->g, ex);
-  else if (m.np2)
-    hipLaunchKernelGGL((k_gen_count<false, true>), dim3(nb), dim3(BLOCK), 0, s, m, ga, ctx->g, ex);
-  else
-    hipLaunchKernelGGL((k_gen_count<false, false>), dim3(nb), dim3(BLOCK), 0, s, m, ga, ctx->g, ex);
+  hipLaunchKernelGGL(k_gen_count, dim3(nb), dim3(BLOCK), 0, s, ctx->m, ga, ctx->g, ex);
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }

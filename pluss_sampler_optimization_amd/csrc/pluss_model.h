@@ -370,6 +370,8 @@ PM_HD uint32_t lowbias32(uint32_t x) {  // 32-bit integer hash (xorshift-multipl
 
 struct KeyGen {
   uint32_t ref, dim3, N, T, CS, span, Q, k0, k1, wide;
+  uint32_t fast, tsh;  // run fast path (keyrun_*): T = 2^tsh and block-A strata below T*span
+  uint32_t gd[4];      // block-A stratum size g as digits: t, c2, c1, q (2-D: t, c1, q)
   uint64_t S, SA;    // samples of this reference; of them in block A
   uint64_t g[2];     // stratum size in block A / B
   uint64_t rr[2];    // strata of size g+1 (the first rr of the block)
@@ -405,10 +407,160 @@ inline KeyGen make_keygen(uint64_t N, uint64_t T, uint64_t CS, bool range_full, 
   k.dt[0] = make_div64(T);
   k.dt[1] = make_div64(T > 1 ? T - 1 : 1);
   k.dspan = make_div64(k.span ? k.span : 1);
+  k.tsh = 0;
+  while ((1ull << k.tsh) < T) ++k.tsh;
+  const bool tp2 = (1ull << k.tsh) == T;
+  const uint64_t lenA = k.g[0] + (k.rr[0] ? 1 : 0);
+  k.fast = (tp2 && k.span > 0 && lenA <= (uint64_t)T * k.span && !k.wide) ? 1u : 0u;
+  {  // digits of g (block A radices)
+    uint64_t r = k.g[0];
+    k.gd[0] = (uint32_t)(r % T);
+    r /= T;
+    const uint32_t nd = k.dim3 ? 2u : 1u;
+    for (uint32_t x = 0; x < nd; ++x) {
+      k.gd[1 + x] = (uint32_t)(k.span ? r % k.span : 0);
+      r = k.span ? r / k.span : 0;
+    }
+    k.gd[1 + nd] = (uint32_t)r;
+    if (!k.dim3) k.gd[3] = 0;
+  }
   const uint64_t h = mix64(seed ^ ((uint64_t)(ref + 1) * 0x9E3779B97F4A7C15ull) ^ 0xA5A5A5A55A5A5A5Aull);
   k.k0 = (uint32_t)h;
   k.k1 = (uint32_t)(h >> 32);
   return k;
+}
+
+// ---- the same list as iteration digits, and incrementally along a run ----
+// digits of a point of the key-ordered space: local row q, c1, c2 (0 for 2-D
+// references) and simulated thread t
+struct KeyDigits {
+  uint32_t q, c1, c2, t;
+};
+
+// digits of position p of block b (full decode)
+PM_HD KeyDigits keygen_digits(const KeyGen& k, uint32_t b, uint64_t p) {
+  const Div64& dt = k.dt[b];
+  uint64_t r = div64(p, dt);
+  KeyDigits d;
+  d.t = (uint32_t)(p - r * dt.d);
+  d.c2 = 0;
+  if (k.dim3) {
+    const uint64_t r2 = div64(r, k.dspan);
+    d.c2 = (uint32_t)(r - r2 * k.span);
+    r = r2;
+  }
+  const uint64_t r3 = div64(r, k.dspan);
+  d.c1 = (uint32_t)(r - r3 * k.span);
+  d.q = b ? k.Q - 1 : (uint32_t)r3;
+  return d;
+}
+
+PM_HD uint64_t keygen_offset(const KeyGen& k, uint64_t i, uint64_t len) {
+  const uint32_t uh = lowbias32((uint32_t)i ^ k.k0);
+  if (k.wide) return mulhi64(((uint64_t)uh << 32) | lowbias32((uint32_t)i ^ k.k1), len);
+  return ((uint64_t)uh * len) >> 32;
+}
+
+PM_HD uint64_t keygen_pack(const KeyGen& k, const KeyDigits& d) {
+  const uint32_t c0 = ((d.q / k.CS) * k.T + d.t) * k.CS + d.q % k.CS;
+  return pack(k.ref, c0, d.c1, d.c2);
+}
+
+// A run of consecutive samples i, i+1, ... of one list: the stratum base
+// lo_j is carried as digits and advanced by the stratum size's digits with
+// carries, and the sample's offset (< T*span in block A when the strata are
+// "small", every BASELINE list) is added to them the same way, so a sample
+// costs adds and compares instead of three 64-bit divisions.  Anything else
+// (block B, wide strata) falls back to the full decode.  KeyGen::gd holds the
+// block-A digits of g; fast = T is a power of two and g + 1 <= T*span.
+struct KeyRun {
+  uint64_t i, j, lo;  // sample, its index in its block, its stratum base
+  uint32_t b;         // block
+  KeyDigits ld;       // digits of lo (block A fast path)
+};
+
+PM_HD void keyrun_start(const KeyGen& k, KeyRun& s, uint64_t i) {
+  s.i = i;
+  s.b = i < k.SA ? 0u : 1u;
+  s.j = s.b ? i - k.SA : i;
+  const uint64_t g = k.g[s.b], rr = k.rr[s.b];
+  s.lo = s.j * g + (s.j < rr ? s.j : rr);
+  s.ld = keygen_digits(k, s.b, s.lo);
+}
+
+PM_HD KeyDigits keyrun_digits(const KeyGen& k, const KeyRun& s) {
+  const uint64_t len = k.g[s.b] + (s.j < k.rr[s.b] ? 1u : 0u);
+  const uint64_t off = keygen_offset(k, s.i, len);
+  if (s.b || !k.fast) return keygen_digits(k, s.b, s.lo + off);
+  KeyDigits d = s.ld;
+  const uint32_t ot = (uint32_t)off & (k.T - 1), orest = (uint32_t)(off >> k.tsh);  // orest < span
+  uint32_t t = d.t + ot, c = t >= k.T ? 1u : 0u;
+  d.t = t - (c ? k.T : 0u);
+  if (k.dim3) {
+    uint32_t c2 = d.c2 + orest + c;
+    c = c2 >= k.span ? 1u : 0u;
+    d.c2 = c2 - (c ? k.span : 0u);
+    uint32_t c1 = d.c1 + c;
+    c = c1 >= k.span ? 1u : 0u;
+    d.c1 = c1 - (c ? k.span : 0u);
+  } else {
+    uint32_t c1 = d.c1 + orest + c;
+    c = c1 >= k.span ? 1u : 0u;
+    d.c1 = c1 - (c ? k.span : 0u);
+  }
+  d.q += c;
+  return d;
+}
+
+PM_HD void keyrun_next(const KeyGen& k, KeyRun& s) {
+  const uint64_t step = k.g[s.b] + (s.j < k.rr[s.b] ? 1u : 0u);
+  ++s.i;
+  if (s.i == k.SA) {  // into block B
+    keyrun_start(k, s, s.i);
+    return;
+  }
+  ++s.j;
+  s.lo += step;
+  if (s.b || !k.fast) return;  // the digits are only kept on the fast path
+  KeyDigits& d = s.ld;
+  const uint32_t inc = (uint32_t)(step - k.g[0]);  // 0 or 1
+  uint32_t t = d.t + k.gd[0] + inc, c = t >= k.T ? 1u : 0u;
+  d.t = t - (c ? k.T : 0u);
+  if (k.dim3) {
+    uint32_t c2 = d.c2 + k.gd[1] + c;
+    c = c2 >= k.span ? 1u : 0u;
+    d.c2 = c2 - (c ? k.span : 0u);
+    uint32_t c1 = d.c1 + k.gd[2] + c;
+    c = c1 >= k.span ? 1u : 0u;
+    d.c1 = c1 - (c ? k.span : 0u);
+    d.q += k.gd[3] + c;
+  } else {
+    uint32_t c1 = d.c1 + k.gd[1] + c;
+    c = c1 >= k.span ? 1u : 0u;
+    d.c1 = c1 - (c ? k.span : 0u);
+    d.q += k.gd[2] + c;
+  }
+}
+
+// Faithful sort key a*T + tid of a point given as digits, and
+// its (ref, case) outcome (case_fast's rules; B0's "the thread owns a later
+// row" is q < Q-1 when N % (CS*T) == 0).
+PM_HD uint64_t key_of_digits(const Model& m, uint32_t ref, const KeyDigits& d) {
+  const uint64_t a = ((uint64_t)d.q * m.N + d.c1) * m.S + ref_off(ref, d.c2);
+  return a * m.T + d.t;
+}
+PM_HD uint32_t case_of_digits(const Model& m, uint32_t ref, const KeyDigits& d, uint32_t Q) {
+  const uint32_t Wm1 = m.W - 1;
+  const bool c1last = (m.p2 ? (d.c1 & m.wmask) : fmod_(d.c1, m.dW)) == Wm1;
+  const bool c2last = (m.p2 ? (d.c2 & m.wmask) : fmod_(d.c2, m.dW)) == Wm1;
+  bool a = true, b = true;
+  a = (ref == C3) ? (d.c2 + 1 < m.N) : a;
+  b = (ref == C3) ? !c1last : b;
+  a = (ref == A0) ? !c2last : a;
+  b = (ref == A0) ? (d.c1 + 1 < m.N) : b;
+  a = (ref == B0) ? !c1last : a;
+  b = (ref == B0) ? (d.q + 1 < Q) : b;
+  return a ? 0u : (b ? 1u : 2u);
 }
 
 // Sample i (0 <= i < S) of the list: packed ref|c0|c1|c2.
@@ -418,25 +570,7 @@ PM_HD uint64_t keygen_sample(const KeyGen& k, uint64_t i) {
   const uint64_t g = k.g[b], rr = k.rr[b];
   const uint64_t lo = j * g + (j < rr ? j : rr);
   const uint64_t len = g + (j < rr ? 1u : 0u);
-  const uint32_t uh = lowbias32((uint32_t)i ^ k.k0);
-  uint64_t off;
-  if (k.wide) off = mulhi64(((uint64_t)uh << 32) | lowbias32((uint32_t)i ^ k.k1), len);
-  else off = ((uint64_t)uh * len) >> 32;
-  const uint64_t p = lo + off;
-  const Div64& dt = k.dt[b];
-  uint64_t r = div64(p, dt);
-  const uint32_t tid = (uint32_t)(p - r * dt.d);
-  uint32_t c2 = 0;
-  if (k.dim3) {
-    const uint64_t r2 = div64(r, k.dspan);
-    c2 = (uint32_t)(r - r2 * k.span);
-    r = r2;
-  }
-  const uint64_t r3 = div64(r, k.dspan);
-  const uint32_t c1 = (uint32_t)(r - r3 * k.span);
-  const uint32_t q = b ? k.Q - 1 : (uint32_t)r3;
-  const uint32_t c0 = ((q / k.CS) * k.T + tid) * k.CS + q % k.CS;
-  return pack(k.ref, c0, c1, c2);
+  return keygen_pack(k, keygen_digits(k, b, lo + keygen_offset(k, i, len)));
 }
 
 }  // namespace pluss

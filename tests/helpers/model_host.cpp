@@ -56,3 +56,17 @@ extern "C" int mh_expand_sorted(int64_t N, int64_t T, int64_t CS, int range_full
   return 0;
 }
 extern "C" uint64_t mh_div64(uint64_t n, uint64_t d) { Div64 f = make_div64(d); return div64(n, f); }
+// the same list through the incremental run path (keyrun_*): runs of `run` samples
+extern "C" int mh_expand_sorted_runs(int64_t N, int64_t T, int64_t CS, int range_full, uint64_t seed, int ref,
+                                     uint64_t S, uint64_t first, uint64_t n, uint64_t run, uint64_t* out) {
+  KeyGen k = make_keygen(N, T, CS, range_full != 0, seed, (uint32_t)ref, S);
+  for (uint64_t a = 0; a < n; a += run) {
+    KeyRun s;
+    keyrun_start(k, s, first + a);
+    for (uint64_t x = 0; x < run && a + x < n; ++x) {
+      if (x) keyrun_next(k, s);
+      out[a + x] = keygen_pack(k, keyrun_digits(k, s));
+    }
+  }
+  return (int)k.fast;
+}

@@ -229,6 +229,34 @@ def test_key_order_lists_host_model_equals_oracle(orc, model_host, N, T, CS, rf,
         assert len(np.unique(full)) == tot
 
 
+@pytest.mark.parametrize("N,T,CS,rf,S", KEYGEN_SHAPES, ids=[str(s) for s in KEYGEN_SHAPES])
+def test_key_order_runs_equal_direct(model_host, N, T, CS, rf, S):
+    """The incremental run path (keyrun_*: digits carried along consecutive
+    samples, what the fused kernels use) == the direct per-sample decode, for
+    runs of 1, 16 and 1000 starting anywhere (block A, the A/B seam, block B)."""
+    import ctypes
+    L = model_host.lib
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    L.mh_expand_sorted.argtypes = [ctypes.c_int64] * 3 + [ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
+                                                          ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u64p]
+    L.mh_expand_sorted_runs.argtypes = L.mh_expand_sorted.argtypes[:-1] + [ctypes.c_uint64, u64p]
+    fast_seen = set()
+    for ref in range(6):
+        span = N if rf else N - 1
+        tot = min(S, span ** (3 if ref >= 2 else 2))
+        for first in sorted({0, max(0, tot // 2 - 3000), max(0, tot - 6000), max(0, tot - tot // (N // T) - 3000)}):
+            n = min(6000, tot - first)
+            want = np.empty(n, np.uint64)
+            L.mh_expand_sorted(N, T, CS, rf, 9, ref, tot, first, n, want.ctypes.data_as(u64p))
+            for run in (1, 16, 1000):
+                got = np.empty(n, np.uint64)
+                fast_seen.add(L.mh_expand_sorted_runs(N, T, CS, rf, 9, ref, tot, first, n, run,
+                                                       got.ctypes.data_as(u64p)))
+                np.testing.assert_array_equal(got, want)
+    if (N, T, S) in ((1024, 8, 4189071), (4096, 8, 67025020), (2048, 64, 4173354)):
+        assert 1 in fast_seen  # the BASELINE lists take the fast path
+
+
 def test_div64_round_up_divider(model_host):
     import ctypes
     L = model_host.lib
