@@ -640,18 +640,26 @@ struct FaCursor {
   uint32_t e;
   const fa_raw_t<SRC>* lds;
   GTable g;
-  KeyRun run;
+  bool fast;  // tile-uniform: the whole tile takes keyrunf_* (GEN)
+  KeyRunF run;
   __device__ FaCursor(const Model& m_, const FaRefs& a_, uint32_t r_, uint64_t base_, uint32_t e0,
                       const fa_raw_t<SRC>* lds_, GTable g_)
-      : m(m_), a(a_), r(r_), base(base_), e(e0), lds(lds_), g(g_) {
-    if (SRC == SRC_GEN) keyrun_start(a.kg[r], run, base + e0);
+      : m(m_), a(a_), r(r_), base(base_), e(e0), lds(lds_), g(g_), fast(false) {
+    if (SRC == SRC_GEN) {
+      fast = keyrun_fast_ok(a.kg[r], base, TILE);
+      if (fast) keyrunf_start(a.kg[r], run, base + e0);
+    }
   }
   // the element at the cursor; then the cursor moves on
   __device__ Elem next() {
     Elem x;
     if (SRC == SRC_GEN) {
-      x = elem_of_digits(m, a.pv[r], r, keyrun_digits(a.kg[r], run));
-      keyrun_next(a.kg[r], run);
+      if (fast) {
+        x = elem_of_digits(m, a.pv[r], r, keyrunf_digits(a.kg[r], run));
+        keyrunf_next(a.kg[r], run);
+      } else {
+        x = elem_of_digits(m, a.pv[r], r, keygen_digits_at(a.kg[r], base + e));
+      }
     } else {
       x = fa_tile_elem<SRC>(m, a, r, base, e, lds, g);
     }

@@ -688,18 +688,26 @@ __global__ __launch_bounds__(BLOCK) void k_gen_count(Model m, GenArgs ga, GTable
     const uint64_t j0 = (ws - ga.wbeg[r]) * (64 * GR) + lane * GR;  // this lane's run within the slice
     const uint64_t nr = ga.n[r];
     uint32_t a = 0, b = 0, v = 0;
+    // straight-line 32-bit generation when the wave's whole range is in block A
+    const uint64_t wfirst = ga.first[r] + (ws - ga.wbeg[r]) * (64 * GR);
+    const bool fast = keyrun_fast_ok(kg, wfirst, 64 * GR);
     if (j0 < nr) {
       const uint32_t cnt = nr - j0 < GR ? (uint32_t)(nr - j0) : GR;
-      KeyRun run;
-      keyrun_start(kg, run, ga.first[r] + j0);
+      auto tally = [&](const KeyDigits& d) {
+        const uint32_t c = case_of_digits(m, r, d, Q);
+        a += c == 0 ? 1u : 0u;
+        b += c == 1 ? 1u : 0u;
+      };
+      if (fast) {
+        KeyRunF run;
+        keyrunf_start(kg, run, ga.first[r] + j0);
 #pragma unroll
-      for (uint32_t k = 0; k < GR; ++k) {
-        if (k < cnt) {
-          const uint32_t c = case_of_digits(m, r, keyrun_digits(kg, run), Q);
-          a += c == 0 ? 1u : 0u;
-          b += c == 1 ? 1u : 0u;
-          if (k + 1 < cnt) keyrun_next(kg, run);
+        for (uint32_t k = 0; k < GR; ++k) {
+          if (k < cnt) tally(keyrunf_digits(kg, run));
+          keyrunf_next(kg, run);
         }
+      } else {
+        for (uint32_t k = 0; k < cnt; ++k) tally(keygen_digits_at(kg, ga.first[r] + j0 + k));
       }
       v = cnt;
     }
@@ -980,14 +988,16 @@ __global__ __launch_bounds__(BLOCK) void k_expand_sorted(KeyGen k, uint64_t firs
     const uint64_t j0 = base + threadIdx.x * ER;
     if (j0 < n) {
       const uint32_t cnt = n - j0 < ER ? (uint32_t)(n - j0) : ER;
-      KeyRun run;
-      keyrun_start(k, run, first + j0);
+      if (keyrun_fast_ok(k, first + base, (uint64_t)BLOCK * ER)) {  // block-uniform
+        KeyRunF run;
+        keyrunf_start(k, run, first + j0);
 #pragma unroll
-      for (uint32_t x = 0; x < ER; ++x) {
-        if (x < cnt) {
-          buf[er_slot(threadIdx.x * ER + x)] = keygen_pack(k, keyrun_digits(k, run));
-          if (x + 1 < cnt) keyrun_next(k, run);
+        for (uint32_t x = 0; x < ER; ++x) {
+          if (x < cnt) buf[er_slot(threadIdx.x * ER + x)] = keygen_pack(k, keyrunf_digits(k, run));
+          keyrunf_next(k, run);
         }
+      } else {
+        for (uint32_t x = 0; x < cnt; ++x) buf[er_slot(threadIdx.x * ER + x)] = keygen_sample(k, first + j0 + x);
       }
     }
     __syncthreads();

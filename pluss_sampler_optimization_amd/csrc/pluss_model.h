@@ -372,6 +372,8 @@ struct KeyGen {
   uint32_t ref, dim3, N, T, CS, span, Q, k0, k1, wide;
   uint32_t fast, tsh;  // run fast path (keyrun_*): T = 2^tsh and block-A strata below T*span
   uint32_t gd[4];      // block-A stratum size g as digits: t, c2, c1, q (2-D: t, c1, q)
+  uint32_t g0, rr0;    // block A's g and rr as 32-bit values (fast path)
+  uint32_t cssh, csp2; // CS = 2^cssh (packing by shifts)
   uint64_t S, SA;    // samples of this reference; of them in block A
   uint64_t g[2];     // stratum size in block A / B
   uint64_t rr[2];    // strata of size g+1 (the first rr of the block)
@@ -411,7 +413,12 @@ inline KeyGen make_keygen(uint64_t N, uint64_t T, uint64_t CS, bool range_full, 
   while ((1ull << k.tsh) < T) ++k.tsh;
   const bool tp2 = (1ull << k.tsh) == T;
   const uint64_t lenA = k.g[0] + (k.rr[0] ? 1 : 0);
-  k.fast = (tp2 && k.span > 0 && lenA <= (uint64_t)T * k.span && !k.wide) ? 1u : 0u;
+  k.fast = (tp2 && k.span > 0 && lenA <= (uint64_t)T * k.span && !k.wide && k.SA < (1ull << 32)) ? 1u : 0u;
+  k.g0 = (uint32_t)k.g[0];
+  k.rr0 = (uint32_t)k.rr[0];
+  k.cssh = 0;
+  while ((1ull << k.cssh) < CS) ++k.cssh;
+  k.csp2 = (1ull << k.cssh) == CS ? 1u : 0u;
   {  // digits of g (block A radices)
     uint64_t r = k.g[0];
     k.gd[0] = (uint32_t)(r % T);
@@ -462,8 +469,68 @@ PM_HD uint64_t keygen_offset(const KeyGen& k, uint64_t i, uint64_t len) {
 }
 
 PM_HD uint64_t keygen_pack(const KeyGen& k, const KeyDigits& d) {
-  const uint32_t c0 = ((d.q / k.CS) * k.T + d.t) * k.CS + d.q % k.CS;
+  const uint32_t c0 = (k.csp2 && k.fast) ? (((((d.q >> k.cssh) << k.tsh) | d.t) << k.cssh) | (d.q & (k.CS - 1)))
+                                         : ((d.q / k.CS) * k.T + d.t) * k.CS + d.q % k.CS;
   return pack(k.ref, c0, d.c1, d.c2);
+}
+
+// The fast path of a run as straight-line 32-bit code (KeyGen::fast, the
+// whole run in block A): sample i, its stratum j (= i in block A), the digits
+// of its stratum base.  keyrun_fast_ok() tells whether a run of `len` samples
+// from i0 may take it.
+struct KeyRunF {
+  uint32_t i;
+  KeyDigits ld;
+};
+PM_HD bool keyrun_fast_ok(const KeyGen& k, uint64_t i0, uint64_t len) { return k.fast && i0 + len <= k.SA; }
+PM_HD void keyrunf_start(const KeyGen& k, KeyRunF& s, uint64_t i) {
+  s.i = (uint32_t)i;
+  const uint64_t lo = i * k.g[0] + (i < k.rr[0] ? i : k.rr[0]);
+  s.ld = keygen_digits(k, 0, lo);
+}
+PM_HD KeyDigits keyrunf_digits(const KeyGen& k, const KeyRunF& s) {
+  const uint32_t len = k.g0 + (s.i < k.rr0 ? 1u : 0u);
+  const uint32_t off = umulhi32(lowbias32(s.i ^ k.k0), len);
+  KeyDigits d = s.ld;
+  const uint32_t t = d.t + (off & (k.T - 1));
+  uint32_t c = t >= k.T ? 1u : 0u;
+  d.t = t - (c ? k.T : 0u);
+  const uint32_t orest = off >> k.tsh;
+  if (k.dim3) {
+    const uint32_t c2 = d.c2 + orest + c;
+    c = c2 >= k.span ? 1u : 0u;
+    d.c2 = c2 - (c ? k.span : 0u);
+    const uint32_t c1 = d.c1 + c;
+    c = c1 >= k.span ? 1u : 0u;
+    d.c1 = c1 - (c ? k.span : 0u);
+  } else {
+    const uint32_t c1 = d.c1 + orest + c;
+    c = c1 >= k.span ? 1u : 0u;
+    d.c1 = c1 - (c ? k.span : 0u);
+  }
+  d.q += c;
+  return d;
+}
+PM_HD void keyrunf_next(const KeyGen& k, KeyRunF& s) {
+  KeyDigits& d = s.ld;
+  const uint32_t t = d.t + k.gd[0] + (s.i < k.rr0 ? 1u : 0u);
+  uint32_t c = t >= k.T ? 1u : 0u;
+  d.t = t - (c ? k.T : 0u);
+  if (k.dim3) {
+    const uint32_t c2 = d.c2 + k.gd[1] + c;
+    c = c2 >= k.span ? 1u : 0u;
+    d.c2 = c2 - (c ? k.span : 0u);
+    const uint32_t c1 = d.c1 + k.gd[2] + c;
+    c = c1 >= k.span ? 1u : 0u;
+    d.c1 = c1 - (c ? k.span : 0u);
+    d.q += k.gd[3] + c;
+  } else {
+    const uint32_t c1 = d.c1 + k.gd[1] + c;
+    c = c1 >= k.span ? 1u : 0u;
+    d.c1 = c1 - (c ? k.span : 0u);
+    d.q += k.gd[2] + c;
+  }
+  ++s.i;
 }
 
 // A run of consecutive samples i, i+1, ... of one list: the stratum base
@@ -563,14 +630,15 @@ PM_HD uint32_t case_of_digits(const Model& m, uint32_t ref, const KeyDigits& d, 
   return a ? 0u : (b ? 1u : 2u);
 }
 
-// Sample i (0 <= i < S) of the list: packed ref|c0|c1|c2.
-PM_HD uint64_t keygen_sample(const KeyGen& k, uint64_t i) {
+// Sample i (0 <= i < S) of the list as digits, and packed ref|c0|c1|c2.
+PM_HD KeyDigits keygen_digits_at(const KeyGen& k, uint64_t i) {
   const uint32_t b = i < k.SA ? 0u : 1u;
   const uint64_t j = b ? i - k.SA : i;
   const uint64_t g = k.g[b], rr = k.rr[b];
   const uint64_t lo = j * g + (j < rr ? j : rr);
   const uint64_t len = g + (j < rr ? 1u : 0u);
-  return keygen_pack(k, keygen_digits(k, b, lo + keygen_offset(k, i, len)));
+  return keygen_digits(k, b, lo + keygen_offset(k, i, len));
 }
+PM_HD uint64_t keygen_sample(const KeyGen& k, uint64_t i) { return keygen_pack(k, keygen_digits_at(k, i)); }
 
 }  // namespace pluss

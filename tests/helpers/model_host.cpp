@@ -70,3 +70,24 @@ extern "C" int mh_expand_sorted_runs(int64_t N, int64_t T, int64_t CS, int range
   }
   return (int)k.fast;
 }
+// the 32-bit fast run path (keyrunf_*) where it applies, else the general run
+extern "C" int mh_expand_sorted_fast(int64_t N, int64_t T, int64_t CS, int range_full, uint64_t seed, int ref,
+                                     uint64_t S, uint64_t first, uint64_t n, uint64_t run, uint64_t* out) {
+  KeyGen k = make_keygen(N, T, CS, range_full != 0, seed, (uint32_t)ref, S);
+  int used = 0;
+  for (uint64_t a = 0; a < n; a += run) {
+    const uint64_t len = run < n - a ? run : n - a;
+    if (keyrun_fast_ok(k, first + a, len)) {
+      used = 1;
+      KeyRunF s;
+      keyrunf_start(k, s, first + a);
+      for (uint64_t x = 0; x < len; ++x) {
+        if (x) keyrunf_next(k, s);
+        out[a + x] = keygen_pack(k, keyrunf_digits(k, s));
+      }
+    } else {
+      for (uint64_t x = 0; x < len; ++x) out[a + x] = keygen_sample(k, first + a + x);
+    }
+  }
+  return used;
+}

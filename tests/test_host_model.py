@@ -240,6 +240,7 @@ def test_key_order_runs_equal_direct(model_host, N, T, CS, rf, S):
     L.mh_expand_sorted.argtypes = [ctypes.c_int64] * 3 + [ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
                                                           ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u64p]
     L.mh_expand_sorted_runs.argtypes = L.mh_expand_sorted.argtypes[:-1] + [ctypes.c_uint64, u64p]
+    L.mh_expand_sorted_fast.argtypes = L.mh_expand_sorted_runs.argtypes
     fast_seen = set()
     for ref in range(6):
         span = N if rf else N - 1
@@ -252,6 +253,9 @@ def test_key_order_runs_equal_direct(model_host, N, T, CS, rf, S):
                 got = np.empty(n, np.uint64)
                 fast_seen.add(L.mh_expand_sorted_runs(N, T, CS, rf, 9, ref, tot, first, n, run,
                                                        got.ctypes.data_as(u64p)))
+                np.testing.assert_array_equal(got, want)
+                got[:] = 0
+                L.mh_expand_sorted_fast(N, T, CS, rf, 9, ref, tot, first, n, run, got.ctypes.data_as(u64p))
                 np.testing.assert_array_equal(got, want)
     if (N, T, S) in ((1024, 8, 4189071), (4096, 8, 67025020), (2048, 64, 4173354)):
         assert 1 in fast_seen  # the BASELINE lists take the fast path
