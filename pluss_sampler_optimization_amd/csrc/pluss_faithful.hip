@@ -55,6 +55,7 @@ struct PkView {
   int64_t ri[3];             // RI of case 0/1/2 (-1: cold)
   uint64_t T, N, R, S;
   uint32_t ref, p2, tsh, nsh;  // p2: N and T powers of two (shifts)
+  uint32_t Q;                  // local rows per simulated thread, N / T
 };
 inline PkView make_pkview(const Model& m, uint32_t ref) {
   PkView v;
@@ -68,6 +69,7 @@ inline PkView make_pkview(const Model& m, uint32_t ref) {
   while ((1ull << v.tsh) < v.T) ++v.tsh;
   while ((1ull << v.nsh) < v.N) ++v.nsh;
   v.p2 = ((1ull << v.tsh) == v.T && (1ull << v.nsh) == v.N) ? 1u : 0u;
+  v.Q = (uint32_t)(v.N / v.T);
   return v;
 }
 // the key a*T + tid of a packed word (KEY_EMPTY for the malformed marker ~0)
@@ -557,62 +559,92 @@ struct FaRefs {
   KeyGen kg[6];        // SRC_GEN
 };
 
-// key, sink and case of one element (case 3: malformed, flagged)
+// key, sink, case (3: malformed, flagged) and tid == 0 of one element.  P2:
+// N, T, CS and CLS/DS powers of two (every BASELINE shape) -- decoded with
+// shifts; the general decode is a separate instantiation, so no division is
+// ever evaluated on the P2 path.
 struct Elem {
   unsigned long long key, sink;
-  uint32_t c;
+  uint32_t c, t0;
 };
 
+template <bool P2>
 __device__ __forceinline__ Elem elem_of_digits(const Model& m, const PkView& v, uint32_t ref, const KeyDigits& d) {
   const uint64_t a = ((uint64_t)d.q * m.N + d.c1) * m.S + ref_off(ref, d.c2);
-  const uint64_t key = v.p2 ? ((a << v.tsh) | d.t) : a * m.T + d.t;
-  const uint32_t c = case_of_digits(m, ref, d, (uint32_t)(m.N / m.T));
+  const uint64_t key = P2 ? ((a << v.tsh) | d.t) : a * m.T + d.t;
+  const uint32_t c = case_of_digits(m, ref, d, v.Q);
   const int64_t ri = c == 0 ? v.ri[0] : (c == 1 ? v.ri[1] : v.ri[2]);
-  const unsigned long long dt = v.p2 ? ((unsigned long long)ri << v.tsh) : (unsigned long long)ri * m.T;
-  return Elem{key, ri < 0 ? KEY_EMPTY : key + dt, c};
+  const unsigned long long dt = P2 ? ((unsigned long long)ri << v.tsh) : (unsigned long long)ri * m.T;
+  return Elem{key, ri < 0 ? KEY_EMPTY : key + dt, c, d.t == 0 ? 1u : 0u};
 }
 
+template <bool P2>
 __device__ __forceinline__ Elem elem_of_sample(const Model& m, const PkView& v, uint32_t ref, uint64_t x, GTable g) {
   const Sample s = unpack(x);
   if (s.ref != ref || s.c0 >= m.N || s.c1 >= m.N || s.c2 >= m.N) {
     atomicOr(&g.flags[1], 1u);
-    return Elem{KEY_EMPTY, KEY_EMPTY, 3u};
+    return Elem{KEY_EMPTY, KEY_EMPTY, 3u, 0u};
   }
   KeyDigits d;
   d.c1 = s.c1;
   d.c2 = (ref == C0 || ref == C1) ? 0u : s.c2;
-  uint32_t k;
-  if (v.p2 && m.p2) {  // T, N, CS (and W) powers of two
-    k = s.c0 >> m.csshift;
+  if (P2) {
+    const uint32_t k = s.c0 >> m.csshift;
     d.t = k & (m.T - 1);
     d.q = ((k >> v.tsh) << m.csshift) | (s.c0 & m.csmask);
   } else {
-    k = fdiv(s.c0, m.dCS);
-    const uint32_t kt = fdiv(k, m.dT);
+    const uint32_t k = fdiv(s.c0, m.dCS), kt = fdiv(k, m.dT);
     d.t = k - kt * m.T;
     d.q = kt * m.CS + (s.c0 - k * m.CS);
   }
-  return elem_of_digits(m, v, ref, d);
+  return elem_of_digits<P2>(m, v, ref, d);
+}
+
+// a packed sort word (rank << 2 | case), rank = ((q*N + c1)*N + c2)*T + tid
+template <bool P2, typename KT>
+__device__ __forceinline__ Elem elem_of_word(const Model& m, const PkView& v, uint32_t ref, KT w) {
+  if (w == (KT) ~(KT)0) return Elem{KEY_EMPTY, KEY_EMPTY, 3u, 0u};
+  uint64_t r = (uint64_t)(w >> 2);
+  KeyDigits d;
+  if (P2) {
+    d.t = (uint32_t)(r & (v.T - 1));
+    r >>= v.tsh;
+    d.c2 = (uint32_t)(r & (v.N - 1));
+    r >>= v.nsh;
+    d.c1 = (uint32_t)(r & (v.N - 1));
+    d.q = (uint32_t)(r >> v.nsh);
+  } else {
+    d.t = (uint32_t)(r % v.T);
+    r /= v.T;
+    d.c2 = (uint32_t)(r % v.N);
+    r /= v.N;
+    d.c1 = (uint32_t)(r % v.N);
+    d.q = (uint32_t)(r / v.N);
+  }
+  const uint32_t c = (uint32_t)(w & 3u);
+  const uint64_t a = ((uint64_t)d.q * m.N + d.c1) * m.S + ref_off(ref, d.c2);
+  const uint64_t key = P2 ? ((a << v.tsh) | d.t) : a * m.T + d.t;
+  const int64_t ri = c == 0 ? v.ri[0] : (c == 1 ? v.ri[1] : v.ri[2]);
+  const unsigned long long dt = P2 ? ((unsigned long long)ri << v.tsh) : (unsigned long long)ri * m.T;
+  return Elem{key, (c == 3 || ri < 0) ? KEY_EMPTY : key + dt, c, d.t == 0 ? 1u : 0u};
 }
 
 template <int SRC>
+using fa_raw_t = typename std::conditional<SRC == SRC_W32, uint32_t, unsigned long long>::type;
+
+// element i of reference r read straight from the source (global memory)
+template <int SRC, bool P2>
 __device__ __forceinline__ Elem fa_elem(const Model& m, const FaRefs& a, uint32_t r, uint64_t i, GTable g) {
-  if (SRC == SRC_W32 || SRC == SRC_W64) {
-    typedef typename std::conditional<SRC == SRC_W32, uint32_t, unsigned long long>::type KT;
-    const KT w = static_cast<const KT*>(a.src[r])[i];
-    const bool bad = w == (KT) ~(KT)0;
-    return Elem{pk_key(w, a.pv[r]), pk_sink(w, a.pv[r]), bad ? 3u : (uint32_t)(w & 3u)};
-  }
-  const uint64_t x = SRC == SRC_GEN ? keygen_sample(a.kg[r], i) : static_cast<const uint64_t*>(a.src[r])[i];
-  return elem_of_sample(m, a.pv[r], r, x, g);
+  if (SRC == SRC_GEN) return elem_of_digits<P2>(m, a.pv[r], r, keygen_digits_at(a.kg[r], i));
+  const fa_raw_t<SRC> w = static_cast<const fa_raw_t<SRC>*>(a.src[r])[i];
+  if (SRC == SRC_SAMPLES) return elem_of_sample<P2>(m, a.pv[r], r, (uint64_t)w, g);
+  return elem_of_word<P2>(m, a.pv[r], r, w);
 }
 
 // A tile's elements as read from memory (raw words / samples), staged in LDS:
 // loaded coalesced (thread x, round k: element k*TB + x), read back by each
 // thread as its contiguous run (x*TI + k).  One padding slot per TI elements
 // keeps the run reads at 2-way bank conflicts.
-template <int SRC>
-using fa_raw_t = typename std::conditional<SRC == SRC_W32, uint32_t, unsigned long long>::type;
 constexpr uint32_t FA_LDS = TILE + TILE / TI;
 __device__ __forceinline__ uint32_t fa_slot(uint32_t e) { return e + e / TI; }
 
@@ -630,8 +662,9 @@ __device__ __forceinline__ void fa_stage(const FaRefs& a, uint32_t r, uint64_t b
 }
 
 // A lane's run of consecutive elements: read from the staged tile, or
-// generated in sequence (keyrun_*: digits carried from one sample to the next).
-template <int SRC>
+// generated in sequence (GEN: keyrunf_* when the whole tile lies in block A
+// with small strata -- tile-uniform -- else one direct decode per sample).
+template <int SRC, bool P2>
 struct FaCursor {
   const Model& m;
   const FaRefs& a;
@@ -640,7 +673,7 @@ struct FaCursor {
   uint32_t e;
   const fa_raw_t<SRC>* lds;
   GTable g;
-  bool fast;  // tile-uniform: the whole tile takes keyrunf_* (GEN)
+  bool fast;
   KeyRunF run;
   __device__ FaCursor(const Model& m_, const FaRefs& a_, uint32_t r_, uint64_t base_, uint32_t e0,
                       const fa_raw_t<SRC>* lds_, GTable g_)
@@ -655,29 +688,20 @@ struct FaCursor {
     Elem x;
     if (SRC == SRC_GEN) {
       if (fast) {
-        x = elem_of_digits(m, a.pv[r], r, keyrunf_digits(a.kg[r], run));
+        x = elem_of_digits<P2>(m, a.pv[r], r, keyrunf_digits(a.kg[r], run));
         keyrunf_next(a.kg[r], run);
       } else {
-        x = elem_of_digits(m, a.pv[r], r, keygen_digits_at(a.kg[r], base + e));
+        x = elem_of_digits<P2>(m, a.pv[r], r, keygen_digits_at(a.kg[r], base + e));
       }
     } else {
-      x = fa_tile_elem<SRC>(m, a, r, base, e, lds, g);
+      const fa_raw_t<SRC> w = lds[fa_slot(e)];
+      if (SRC == SRC_SAMPLES) x = elem_of_sample<P2>(m, a.pv[r], r, (uint64_t)w, g);
+      else x = elem_of_word<P2>(m, a.pv[r], r, w);
     }
     ++e;
     return x;
   }
 };
-
-// element e of the tile (lane-contiguous read from the staged raw data)
-template <int SRC>
-__device__ __forceinline__ Elem fa_tile_elem(const Model& m, const FaRefs& a, uint32_t r, uint64_t base, uint32_t e,
-                                             const fa_raw_t<SRC>* lds, GTable g) {
-  if (SRC == SRC_GEN) return elem_of_sample(m, a.pv[r], r, keygen_sample(a.kg[r], base + e), g);
-  const fa_raw_t<SRC> w = lds[fa_slot(e)];
-  if (SRC == SRC_SAMPLES) return elem_of_sample(m, a.pv[r], r, w, g);
-  const bool bad = w == (fa_raw_t<SRC>) ~(fa_raw_t<SRC>)0;
-  return Elem{pk_key(w, a.pv[r]), pk_sink(w, a.pv[r]), bad ? 3u : (uint32_t)(w & 3u)};
-}
 
 // the tile's reference (wave-uniform) and its place in it
 struct FaTile {
@@ -703,7 +727,7 @@ __device__ __forceinline__ FaTile fa_tile(const FaRefs& a, uint64_t gt) {
 // [x*TI, (x+1)*TI); each lane scans its own run sequentially in registers and
 // the lanes are combined by ONE wave scan per quantity (instead of a 64-wide
 // scan per element round).
-template <int SRC, bool CHECK>
+template <int SRC, bool CHECK, bool P2>
 __global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long long* __restrict__ tmax, GTable g) {
   __shared__ unsigned long long s_w[TB / 64];
   __shared__ fa_raw_t<SRC> s_raw[SRC == SRC_GEN ? 1 : FA_LDS];
@@ -714,7 +738,7 @@ __global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long 
   const uint64_t n = a.n[T.r];
   unsigned long long tm = 0, prev = 0, first = KEY_EMPTY;
   bool unordered = false;
-  FaCursor<SRC> cur(m, a, T.r, T.base, e0 < T.mt ? e0 : 0u, s_raw, g);
+  FaCursor<SRC, P2> cur(m, a, T.r, T.base, e0 < T.mt ? e0 : 0u, s_raw, g);
 #pragma unroll
   for (int k = 0; k < TI; ++k) {
     if (e0 + k < T.mt) {
@@ -731,7 +755,7 @@ __global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long 
     const unsigned long long nf = __shfl_down(first, 1, 64);
     const uint64_t inext = T.base + e0 + TI;  // the element after this lane's run
     if (e0 + TI <= T.mt && inext < n) {
-      const unsigned long long kn = (lane < 63 && e0 + TI < T.mt) ? nf : fa_elem<SRC>(m, a, T.r, inext, g).key;
+      const unsigned long long kn = (lane < 63 && e0 + TI < T.mt) ? nf : fa_elem<SRC, P2>(m, a, T.r, inext, g).key;
       unordered |= !(kn > prev);
     }
     if (__ballot(unordered) && lane == 0) atomicOr(&g.flags[1], 1u);
@@ -778,7 +802,7 @@ __global__ __launch_bounds__(PB) void k_fa_prefix(FaRefs a, const unsigned long 
   }
 }
 
-template <int SRC>
+template <int SRC, bool P2>
 __global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigned long long* __restrict__ pmin,
                                                 unsigned long long* st, unsigned long long* __restrict__ part,
                                                 unsigned long long* scal, GTable g) {
@@ -806,15 +830,16 @@ __global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigne
     return (c > 2 || d == KEY_EMPTY || key == KEY_EMPTY) ? KEY_EMPTY : key + d;
   };
   unsigned long long key[TI];
-  uint32_t cases = 0;  // 2 bits per element
+  uint32_t cases = 0, t0s = 0;  // 2 bits per element; tid == 0 per element
   unsigned long long lmax = 0;
-  FaCursor<SRC> cur(m, a, r, T.base, nv ? e0 : 0u, s_raw, g);
+  FaCursor<SRC, P2> cur(m, a, r, T.base, nv ? e0 : 0u, s_raw, g);
 #pragma unroll
   for (int k = 0; k < TI; ++k) {
     Elem e{KEY_EMPTY, 0ull, 3u};
     if ((uint32_t)k < nv) e = cur.next();
     key[k] = e.key;
     cases |= (e.c & 3u) << (2 * k);
+    t0s |= e.t0 << k;
     if ((uint32_t)k < nv) lmax = e.sink > lmax ? e.sink : lmax;
   }
   // running max of sinks entering this lane: the tile's incoming max, the
@@ -876,11 +901,9 @@ __global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigne
   // record this lane's elements below the tile's candidate
   unsigned long long cold = 0, trav = 0;
   uint32_t nc0 = 0, nc1 = 0, nc2 = 0;
-  const uint64_t tmask = m.T - 1;
-  const bool tp2 = (m.T & tmask) == 0;
   // the key after this lane's run: the next lane's first, or (lane 63, or the tile's end) the source's
   unsigned long long knext = __shfl_down(key[0], 1, 64);
-  if (lane == 63 || e0 + TI >= T.mt) knext = (nv == TI && i0 + TI < n) ? fa_elem<SRC>(m, a, r, i0 + TI, g).key : KEY_EMPTY;
+  if (lane == 63 || e0 + TI >= T.mt) knext = (nv == TI && i0 + TI < n) ? fa_elem<SRC, P2>(m, a, r, i0 + TI, g).key : KEY_EMPTY;
   {
     unsigned long long run = carry;
 #pragma unroll
@@ -892,7 +915,7 @@ __global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigne
         const unsigned long long gm = sk > run ? sk : run;  // inclusive running max at i
         run = gm;
         if (sk == KEY_EMPTY) {
-          cold += ((tp2 ? (kk & tmask) : kk % m.T) == 0) ? 1u : 0u;
+          cold += (t0s >> k) & 1u;
         } else {
           nc0 += c == 0 ? 1u : 0u;
           nc1 += c == 1 ? 1u : 0u;
@@ -1335,12 +1358,18 @@ static int fa_run(pluss_ctx* ctx, FaRefs& a, int src, bool check, hipStream_t s)
   FaithfulBufs& b = ctx->fb;
   if (int rc = fa_reserve(b, t, s)) return rc;
   const GTable& g = ctx->g;
-#define PLUSS_FA(SRCV, CHK)                                                                                       \
+  const bool p2 = m.p2 && a.pv[0].p2;  // N, T, CS, CLS/DS powers of two: shift decoding
+#define PLUSS_FA3(SRCV, CHK, P2V)                                                                                 \
   do {                                                                                                            \
-    hipLaunchKernelGGL((k_fa_max<SRCV, CHK>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.tmax, g);               \
+    hipLaunchKernelGGL((k_fa_max<SRCV, CHK, P2V>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.tmax, g);          \
     hipLaunchKernelGGL(k_fa_prefix, dim3(6), dim3(PB), 0, s, a, b.tmax, b.pmin, b.dst, b.fscal);                  \
-    hipLaunchKernelGGL((k_fa_scan<SRCV>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.pmin, b.dst, b.dpart, b.fscal, \
-                       g);                                                                                        \
+    hipLaunchKernelGGL((k_fa_scan<SRCV, P2V>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.pmin, b.dst, b.dpart,  \
+                       b.fscal, g);                                                                               \
+  } while (0)
+#define PLUSS_FA(SRCV, CHK)            \
+  do {                                 \
+    if (p2) PLUSS_FA3(SRCV, CHK, true); \
+    else PLUSS_FA3(SRCV, CHK, false);   \
   } while (0)
   switch (src) {
     case SRC_W32: PLUSS_FA(SRC_W32, false); break;
@@ -1352,6 +1381,7 @@ static int fa_run(pluss_ctx* ctx, FaRefs& a, int src, bool check, hipStream_t s)
     default: PLUSS_FA(SRC_GEN, false); break;
   }
 #undef PLUSS_FA
+#undef PLUSS_FA3
   hipLaunchKernelGGL(k_fa_finish, dim3(6), dim3(BLOCK), 0, s, m, a, b.tmax, b.pmin, b.dpart, b.fscal, g);
   PLUSS_HIP_CHECK(hipGetLastError());
   ctx->tables_dirty = true;
