@@ -18,9 +18,17 @@ namespace {
 
 using Hist = std::map<long, double>;
 
+// log |Gamma(x)| without touching glibc's global `signgam` (std::lgamma writes
+// it: a data race when two threads run the pipeline, found by the TSan build
+// in tests/test_sanitizers.py)
+double lgam(double x) {
+  int sign = 0;
+  return ::lgamma_r(x, &sign);
+}
+
 // gsl_ran_negative_binomial_pdf(k, p, n) (GSL randist/nbinomial.c form)
 double nbd_pdf(unsigned int k, double p, double n) {
-  const double f = std::lgamma((double)k + n), a = std::lgamma(n), b = std::lgamma((double)k + 1.0);
+  const double f = lgam((double)k + n), a = lgam(n), b = lgam((double)k + 1.0);
   return std::exp(f - a - b + n * std::log(p) + (double)k * std::log1p(-p));
 }
 
