@@ -276,6 +276,21 @@ def faithful_bench(P, torch, device, stream):
     # the key-order list through both of its paths gives one histogram
     assert hs["sorted"].bins == hs["generated"].bins and list(hs["sorted"].traversed) == list(hs["generated"].traversed)
     out["sorted"]["hbm_GBps"] = 8 * total / (out["sorted"]["ms"] * 1e-3) / 1e9
+    # the sorted pass reads its 8 B per sample once (algorithmic bytes); HBM
+    # traffic per pass from the committed PMC summary (tools/pmc_faithful_summary.py)
+    traffic = None
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_faithful.json")))
+        if d.get("samples_per_pass") == total:
+            traffic = d.get("hbm_bytes_per_pass")
+    except (OSError, ValueError):
+        pass
+    ach = out["sorted"]["hbm_GBps"]
+    out["sorted"]["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+                                 "note": "achieved = 8 B x samples / pass time (four launches, six references); "
+                                         "traffic includes the 4-8 B per sample word buffer written by the first "
+                                         "launch and read by the scan"}
     out["sorted"]["recorded"] = hs["sorted"].total() - sum(hs["sorted"].cold(r) for r in P.REFS)
     out["radix"]["recorded"] = hs["radix"].total() - sum(hs["radix"].cold(r) for r in P.REFS)
     out["note"] = ("radix = arbitrary-order input (sort inside the pass); sorted = input already in r10's pop "

@@ -566,16 +566,19 @@ struct FaRefs {
 struct Elem {
   unsigned long long key, sink;
   uint32_t c, t0;
+  unsigned long long w;  // the packed sort word rank << 2 | case (~0: malformed)
 };
 
 template <bool P2>
 __device__ __forceinline__ Elem elem_of_digits(const Model& m, const PkView& v, uint32_t ref, const KeyDigits& d) {
   const uint64_t a = ((uint64_t)d.q * m.N + d.c1) * m.S + ref_off(ref, d.c2);
   const uint64_t key = P2 ? ((a << v.tsh) | d.t) : a * m.T + d.t;
-  const uint32_t c = case_of_digits(m, ref, d, v.Q);
+  const uint32_t c = case_of_digits<P2>(m, ref, d, v.Q);
   const int64_t ri = c == 0 ? v.ri[0] : (c == 1 ? v.ri[1] : v.ri[2]);
   const unsigned long long dt = P2 ? ((unsigned long long)ri << v.tsh) : (unsigned long long)ri * m.T;
-  return Elem{key, ri < 0 ? KEY_EMPTY : key + dt, c, d.t == 0 ? 1u : 0u};
+  const uint64_t qc = (uint64_t)d.q * m.N + d.c1;  // rank = ((q*N + c1)*N + c2)*T + t
+  const uint64_t rank = P2 ? ((((qc << v.nsh) | d.c2) << v.tsh) | d.t) : (qc * m.N + d.c2) * m.T + d.t;
+  return Elem{key, ri < 0 ? KEY_EMPTY : key + dt, c, d.t == 0 ? 1u : 0u, (rank << 2) | c};
 }
 
 template <bool P2>
@@ -583,7 +586,7 @@ __device__ __forceinline__ Elem elem_of_sample(const Model& m, const PkView& v, 
   const Sample s = unpack(x);
   if (s.ref != ref || s.c0 >= m.N || s.c1 >= m.N || s.c2 >= m.N) {
     atomicOr(&g.flags[1], 1u);
-    return Elem{KEY_EMPTY, KEY_EMPTY, 3u, 0u};
+    return Elem{KEY_EMPTY, KEY_EMPTY, 3u, 0u, ~0ull};
   }
   KeyDigits d;
   d.c1 = s.c1;
@@ -603,7 +606,7 @@ __device__ __forceinline__ Elem elem_of_sample(const Model& m, const PkView& v, 
 // a packed sort word (rank << 2 | case), rank = ((q*N + c1)*N + c2)*T + tid
 template <bool P2, typename KT>
 __device__ __forceinline__ Elem elem_of_word(const Model& m, const PkView& v, uint32_t ref, KT w) {
-  if (w == (KT) ~(KT)0) return Elem{KEY_EMPTY, KEY_EMPTY, 3u, 0u};
+  if (w == (KT) ~(KT)0) return Elem{KEY_EMPTY, KEY_EMPTY, 3u, 0u, ~0ull};
   uint64_t r = (uint64_t)(w >> 2);
   KeyDigits d;
   if (P2) {
@@ -626,7 +629,7 @@ __device__ __forceinline__ Elem elem_of_word(const Model& m, const PkView& v, ui
   const uint64_t key = P2 ? ((a << v.tsh) | d.t) : a * m.T + d.t;
   const int64_t ri = c == 0 ? v.ri[0] : (c == 1 ? v.ri[1] : v.ri[2]);
   const unsigned long long dt = P2 ? ((unsigned long long)ri << v.tsh) : (unsigned long long)ri * m.T;
-  return Elem{key, (c == 3 || ri < 0) ? KEY_EMPTY : key + dt, c, d.t == 0 ? 1u : 0u};
+  return Elem{key, (c == 3 || ri < 0) ? KEY_EMPTY : key + dt, c, d.t == 0 ? 1u : 0u, (unsigned long long)w};
 }
 
 template <int SRC>
@@ -727,15 +730,22 @@ __device__ __forceinline__ FaTile fa_tile(const FaRefs& a, uint64_t gt) {
 // [x*TI, (x+1)*TI); each lane scans its own run sequentially in registers and
 // the lanes are combined by ONE wave scan per quantity (instead of a 64-wide
 // scan per element round).
-template <int SRC, bool CHECK, bool P2>
-__global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long long* __restrict__ tmax, GTable g) {
+// WK (0: none, 4 or 8 bytes): also write each element's packed sort word at
+// words + its global tile offset, so the scan pass reads words and decodes
+// the source only once.
+template <int SRC, bool CHECK, bool P2, int WK>
+__global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long long* __restrict__ tmax, void* words,
+                                               GTable g) {
+  using wk_t = typename std::conditional<WK == 8, unsigned long long, uint32_t>::type;
   __shared__ unsigned long long s_w[TB / 64];
   __shared__ fa_raw_t<SRC> s_raw[SRC == SRC_GEN ? 1 : FA_LDS];
+  __shared__ wk_t s_wd[(WK != 0 && SRC == SRC_GEN) ? FA_LDS : 1];
   const FaTile T = fa_tile(a, blockIdx.x);
   fa_stage<SRC>(a, T.r, T.base, T.mt, s_raw);
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
   const uint32_t e0 = threadIdx.x * TI;
   const uint64_t n = a.n[T.r];
+  wk_t wv[TI];
   unsigned long long tm = 0, prev = 0, first = KEY_EMPTY;
   bool unordered = false;
   FaCursor<SRC, P2> cur(m, a, T.r, T.base, e0 < T.mt ? e0 : 0u, s_raw, g);
@@ -744,6 +754,7 @@ __global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long 
     if (e0 + k < T.mt) {
       const Elem e = cur.next();
       tm = e.sink > tm ? e.sink : tm;
+      if (WK) wv[k] = (wk_t)e.w;
       if (CHECK) {
         if (k == 0) first = e.key;
         else unordered |= !(e.key > prev);
@@ -759,6 +770,20 @@ __global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long 
       unordered |= !(kn > prev);
     }
     if (__ballot(unordered) && lane == 0) atomicOr(&g.flags[1], 1u);
+  }
+  if (WK) {  // words through LDS (the samples' staging buffer once it is consumed): coalesced stores
+    wk_t* buf = SRC == SRC_GEN ? s_wd : reinterpret_cast<wk_t*>(s_raw);
+    if (SRC != SRC_GEN) __syncthreads();
+#pragma unroll
+    for (int k = 0; k < TI; ++k)
+      if (e0 + k < T.mt) buf[fa_slot(e0 + k)] = wv[k];
+    __syncthreads();
+    wk_t* out = static_cast<wk_t*>(words) + blockIdx.x * (uint64_t)TILE;
+#pragma unroll
+    for (int k = 0; k < TI; ++k) {
+      const uint32_t e = k * TB + threadIdx.x;
+      if (e < T.mt) out[e] = buf[fa_slot(e)];
+    }
   }
   tm = sc_wave_red<true>(tm);
   if (lane == 0) s_w[wid] = tm;
@@ -835,7 +860,7 @@ __global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigne
   FaCursor<SRC, P2> cur(m, a, r, T.base, nv ? e0 : 0u, s_raw, g);
 #pragma unroll
   for (int k = 0; k < TI; ++k) {
-    Elem e{KEY_EMPTY, 0ull, 3u};
+    Elem e{KEY_EMPTY, 0ull, 3u, 0u, ~0ull};
     if ((uint32_t)k < nv) e = cur.next();
     key[k] = e.key;
     cases |= (e.c & 3u) << (2 * k);
@@ -1359,21 +1384,46 @@ static int fa_run(pluss_ctx* ctx, FaRefs& a, int src, bool check, hipStream_t s)
   if (int rc = fa_reserve(b, t, s)) return rc;
   const GTable& g = ctx->g;
   const bool p2 = m.p2 && a.pv[0].p2;  // N, T, CS, CLS/DS powers of two: shift decoding
-#define PLUSS_FA3(SRCV, CHK, P2V)                                                                                 \
-  do {                                                                                                            \
-    hipLaunchKernelGGL((k_fa_max<SRCV, CHK, P2V>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.tmax, g);          \
-    hipLaunchKernelGGL(k_fa_prefix, dim3(6), dim3(PB), 0, s, a, b.tmax, b.pmin, b.dst, b.fscal);                  \
-    hipLaunchKernelGGL((k_fa_scan<SRCV, P2V>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.pmin, b.dst, b.dpart,  \
-                       b.fscal, g);                                                                               \
+  // samples / generated lists: the first pass writes the packed sort words
+  // (4 or 8 bytes, as the radix path sorts them) and the scan reads those
+  const bool w32 = pk_bits(m) <= 32;
+  FaRefs aw = a;
+  if (src == SRC_SAMPLES || src == SRC_GEN) {
+    const size_t need = t * (size_t)TILE * (w32 ? 4 : 8);
+    if (need > b.words_bytes) {
+      PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+      if (b.words) (void)hipFree(b.words);
+      b.words = nullptr;
+      b.words_bytes = 0;
+      if (hipMalloc(&b.words, need) != hipSuccess) {
+        set_error("hipMalloc failed for the faithful scan's word buffer");
+        return PLUSS_ERR_ALLOC;
+      }
+      b.words_bytes = need;
+    }
+    for (int r = 0; r < 6; ++r)
+      aw.src[r] = static_cast<char*>(b.words) + a.toff[r] * (uint64_t)TILE * (w32 ? 4 : 8);
+  }
+#define PLUSS_FA3(SRCV, CHK, P2V, WKV, SCANV)                                                                      \
+  do {                                                                                                             \
+    hipLaunchKernelGGL((k_fa_max<SRCV, CHK, P2V, WKV>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.tmax, b.words, g); \
+    hipLaunchKernelGGL(k_fa_prefix, dim3(6), dim3(PB), 0, s, a, b.tmax, b.pmin, b.dst, b.fscal);                   \
+    hipLaunchKernelGGL((k_fa_scan<SCANV, P2V>), dim3((unsigned)t), dim3(TB), 0, s, m, aw, b.pmin, b.dst, b.dpart, \
+                       b.fscal, g);                                                                                \
   } while (0)
-#define PLUSS_FA(SRCV, CHK)            \
-  do {                                 \
-    if (p2) PLUSS_FA3(SRCV, CHK, true); \
-    else PLUSS_FA3(SRCV, CHK, false);   \
+#define PLUSS_FA2(SRCV, CHK, WKV, SCANV)            \
+  do {                                              \
+    if (p2) PLUSS_FA3(SRCV, CHK, true, WKV, SCANV); \
+    else PLUSS_FA3(SRCV, CHK, false, WKV, SCANV);   \
+  } while (0)
+#define PLUSS_FA(SRCV, CHK)                                    \
+  do {                                                         \
+    if (w32) PLUSS_FA2(SRCV, CHK, 4, SRC_W32);                 \
+    else PLUSS_FA2(SRCV, CHK, 8, SRC_W64);                     \
   } while (0)
   switch (src) {
-    case SRC_W32: PLUSS_FA(SRC_W32, false); break;
-    case SRC_W64: PLUSS_FA(SRC_W64, false); break;
+    case SRC_W32: PLUSS_FA2(SRC_W32, false, 0, SRC_W32); break;
+    case SRC_W64: PLUSS_FA2(SRC_W64, false, 0, SRC_W64); break;
     case SRC_SAMPLES:
       if (check) PLUSS_FA(SRC_SAMPLES, true);
       else PLUSS_FA(SRC_SAMPLES, false);
@@ -1381,6 +1431,7 @@ static int fa_run(pluss_ctx* ctx, FaRefs& a, int src, bool check, hipStream_t s)
     default: PLUSS_FA(SRC_GEN, false); break;
   }
 #undef PLUSS_FA
+#undef PLUSS_FA2
 #undef PLUSS_FA3
   hipLaunchKernelGGL(k_fa_finish, dim3(6), dim3(BLOCK), 0, s, m, a, b.tmax, b.pmin, b.dpart, b.fscal, g);
   PLUSS_HIP_CHECK(hipGetLastError());

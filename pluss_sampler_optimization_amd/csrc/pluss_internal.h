@@ -67,6 +67,8 @@ struct FaithfulBufs {
   // largest sink and the running max entering it; its scalars (cut per reference, tile counter)
   uint64_t dcap = 0;
   unsigned long long *dst = nullptr, *dpart = nullptr, *tmax = nullptr, *pmin = nullptr, *fscal = nullptr;
+  void* words = nullptr;  // packed sort words written by the first pass (sample / generated sources)
+  size_t words_bytes = 0;
 };
 
 // state of a key-range shard between the phases of pluss_dev_faithful_shard_*

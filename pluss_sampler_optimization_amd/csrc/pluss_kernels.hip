@@ -694,7 +694,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_count(Model m, GenArgs ga, GTable
     if (j0 < nr) {
       const uint32_t cnt = nr - j0 < GR ? (uint32_t)(nr - j0) : GR;
       auto tally = [&](const KeyDigits& d) {
-        const uint32_t c = case_of_digits(m, r, d, Q);
+        const uint32_t c = m.p2 ? case_of_digits<true>(m, r, d, Q) : case_of_digits<false>(m, r, d, Q);
         a += c == 0 ? 1u : 0u;
         b += c == 1 ? 1u : 0u;
       };

@@ -616,10 +616,11 @@ PM_HD uint64_t key_of_digits(const Model& m, uint32_t ref, const KeyDigits& d) {
   const uint64_t a = ((uint64_t)d.q * m.N + d.c1) * m.S + ref_off(ref, d.c2);
   return a * m.T + d.t;
 }
+template <bool P2 = false>
 PM_HD uint32_t case_of_digits(const Model& m, uint32_t ref, const KeyDigits& d, uint32_t Q) {
-  const uint32_t Wm1 = m.W - 1;
-  const bool c1last = (m.p2 ? (d.c1 & m.wmask) : fmod_(d.c1, m.dW)) == Wm1;
-  const bool c2last = (m.p2 ? (d.c2 & m.wmask) : fmod_(d.c2, m.dW)) == Wm1;
+  const uint32_t Wm1 = m.W - 1;  // P2: W a power of two (a mask; no division evaluated)
+  const bool c1last = (P2 ? (d.c1 & m.wmask) : fmod_(d.c1, m.dW)) == Wm1;
+  const bool c2last = (P2 ? (d.c2 & m.wmask) : fmod_(d.c2, m.dW)) == Wm1;
   bool a = true, b = true;
   a = (ref == C3) ? (d.c2 + 1 < m.N) : a;
   b = (ref == C3) ? !c1last : b;

@@ -1,0 +1,37 @@
+"""Minimal driver for rocprofv3 passes over the faithful (r10 queue semantics)
+pipeline: config 2's budget (N=1024, T=8, 2^24 samples, six references in one
+pass).  PROF_FAITH=sorted (key-order list in HBM, read once) or generated (the
+same lists generated inside the pass); PROF_REPS passes."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import pluss_sampler_optimization_amd as P  # noqa: E402
+
+SEED = 0x5EED0001
+mode = os.environ.get("PROF_FAITH", "sorted")
+dev = torch.device("cuda", 0)
+s = torch.cuda.Stream(dev)
+torch.cuda.set_stream(s)
+sp = s.cuda_stream
+cfg = P.SamplerConfig(n=1024, threads=8, mode="faithful")
+total = 1 << 24
+counts = P.default_counts(1024, total)
+buf = torch.empty(total, dtype=torch.int64, device=dev)
+ctx = P.Context(cfg)
+off = 0
+for r, c in enumerate(counts):
+    ctx.expand_sorted(SEED, r, c, 0, c, buf.data_ptr() + 8 * off, sp)
+    off += c
+for _ in range(int(os.environ.get("PROF_REPS", 5))):
+    ctx.reset(sp)
+    if mode == "sorted":
+        ctx.faithful_hist_sorted_refs(buf.data_ptr(), counts, sp)
+    else:
+        ctx.gen_faithful_refs(SEED, counts, sp)
+torch.cuda.synchronize()
+h = ctx.fetch()
+assert h.total() > 0
+print("ok", mode, h.total())
