@@ -474,79 +474,22 @@ __global__ void k_faith_scan_init(unsigned long long* scal, uint64_t cut, unsign
 // list in ONE pipeline of four launches (whatever the element source: sorted
 // packed words after the radix sort, a caller's key-ordered samples, or
 // samples generated in key order):
-//   k_fa_max     per tile of TILE elements: the largest sink (and, for a
-//                caller's list, the key-order check);
+//   k_fa_max     per tile of TILE elements: the largest sink (a caller's list:
+//                the key-order check; samples / generated lists: the packed
+//                sort word of every element, written once for the scan);
 //   k_fa_prefix  one workgroup per reference: exclusive prefix max of the
 //                tile maxima = the running max of sinks entering each tile;
-//                resets the reference's look-back words and scalars;
-//   k_fa_scan    per tile, in order of a tile counter: prefix max inside the
-//                tile, start flags, start count chained across the
-//                reference's tiles by decoupled look-back (the only chain),
-//                the tile's Q1 candidate, and the records of its elements
-//                below that candidate into per-tile partial sums;
-//   k_fa_finish  one workgroup per reference: the Q1 cut is the smallest
-//                candidate (the condition j - starts_before_j >= n - j is
-//                monotone in j), so the partials of the tiles that start
-//                below it are summed; Q3, the -1 key, traversed, the bins.
-// exclusive prefix of tile t > 0 from the status words of tiles t-1, t-2, ...
-// (one whole wave, 4 predecessors per lane: 256 per round)
-template <bool MAX>
-__device__ unsigned long long sc_lookback4(const unsigned long long* st, uint32_t t, uint32_t lane) {
-  unsigned long long acc = 0;
-  int64_t hi = (int64_t)t - 1;
-  while (true) {
-    unsigned long long w[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t j = hi - (int64_t)(q * 64 + lane);
-      w[q] = j >= 0 ? st_ld(&st[j]) : ST_INC;
-    }
-    while (__ballot((w[0] >> 62) == 0 || (w[1] >> 62) == 0 || (w[2] >> 62) == 0 || (w[3] >> 62) == 0) != 0) {
-      __builtin_amdgcn_s_sleep(1);  // back off: the spinning waves share L2 with the publishers
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int64_t j = hi - (int64_t)(q * 64 + lane);
-        if ((w[q] >> 62) == 0) w[q] = st_ld(&st[j]);
-      }
-    }
-    bool done = false;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (done) break;
-      const unsigned long long inc = __ballot((w[q] >> 62) == 2);
-      const uint32_t stop = inc ? (uint32_t)(__ffsll((long long)inc) - 1) : 64u;
-      acc = sc_op<MAX>(acc, sc_wave_red<MAX>(lane <= stop ? (w[q] & ST_VAL) : 0ull));
-      done = inc != 0;
-    }
-    if (done) return acc;
-    hi -= 256;
-  }
-}
-// publish the tile's aggregate, resolve its exclusive prefix, publish the
-// inclusive one (wave 0); every thread of the workgroup gets the prefix
-template <bool MAX>
-__device__ __forceinline__ unsigned long long fu_chain(unsigned long long* st, uint32_t t, unsigned long long agg,
-                                                       uint32_t lane, unsigned long long* s_in) {
-  if (threadIdx.x < 64) {
-    unsigned long long in = 0;
-    if (t == 0) {
-      if (lane == 0) st_st(&st[0], ST_INC | st_cap(agg));
-    } else {
-      if (lane == 0) st_st(&st[t], ST_AGG | st_cap(agg));
-      in = sc_lookback4<MAX>(st, t, lane);
-      if (lane == 0) st_st(&st[t], ST_INC | st_cap(sc_op<MAX>(in, agg)));
-    }
-    if (lane == 0) *s_in = in;
-  }
-  __syncthreads();
-  return *s_in;
-}
-
+//   k_fa_scan    every tile independently (no chain across tiles): prefix
+//                max inside the tile, start flags, the tile's start count,
+//                its Q1 bound (hmax) and the records of all its elements;
+//   k_fa_finish  one workgroup per reference: the exclusive sum of the start
+//                counts locates the tile holding the Q1 cut (the condition
+//                j - starts_before_j >= n - j is monotone in j), the tiles
+//                before it are summed, that tile is scanned again below the
+//                cut; Q3, the -1 key, traversed, the bins.
 constexpr int TB = 256, TI = 16;            // threads per tile, elements per thread
 constexpr uint32_t TILE = TB * TI;          // elements per tile
 constexpr int FPART = 5;                    // per tile: cold (tid 0), traversed, case 0/1/2 counts
-constexpr int FA_SCAL = 8;                  // scalars per reference: [0] cut
-constexpr int FA_COUNTER = 6 * FA_SCAL;     // the scan pass's tile counter (all references)
 __host__ __device__ inline uint64_t fa_tiles(uint64_t n) { return (n + TILE - 1) / TILE; }
 
 enum : int { SRC_W32 = 0, SRC_W64 = 1, SRC_SAMPLES = 2, SRC_GEN = 3 };
@@ -726,64 +669,63 @@ __device__ __forceinline__ FaTile fa_tile(const FaRefs& a, uint64_t gt) {
   return t;
 }
 
-// Lane-contiguous elements: thread x of a tile owns its elements
-// [x*TI, (x+1)*TI); each lane scans its own run sequentially in registers and
-// the lanes are combined by ONE wave scan per quantity (instead of a 64-wide
-// scan per element round).
-// WK (0: none, 4 or 8 bytes): also write each element's packed sort word at
-// words + its global tile offset, so the scan pass reads words and decodes
-// the source only once.
+// ---- pass 1 (k_fa_max*): per tile, the largest sink; for a caller's list
+// the key-order check; for sample / generated sources also the packed sort
+// word of every element (written once, read by the scan).
+//
+// Lists in memory (sorted words, a caller's samples): element-strided, thread
+// x round k holds element k*TB + x, so every load and word store is coalesced
+// and no LDS staging is needed (occupancy is not capped by LDS).
 template <int SRC, bool CHECK, bool P2, int WK>
 __global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long long* __restrict__ tmax, void* words,
                                                GTable g) {
+  static_assert(SRC != SRC_GEN, "generated lists: k_fa_max_gen");
   using wk_t = typename std::conditional<WK == 8, unsigned long long, uint32_t>::type;
-  __shared__ unsigned long long s_w[TB / 64];
-  __shared__ fa_raw_t<SRC> s_raw[SRC == SRC_GEN ? 1 : FA_LDS];
-  __shared__ wk_t s_wd[(WK != 0 && SRC == SRC_GEN) ? FA_LDS : 1];
+  constexpr int NW = TB / 64;
+  __shared__ unsigned long long s_w[NW];
+  __shared__ unsigned long long s_first[CHECK ? TI : 1][NW], s_last[CHECK ? TI : 1][NW];
   const FaTile T = fa_tile(a, blockIdx.x);
-  fa_stage<SRC>(a, T.r, T.base, T.mt, s_raw);
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  const uint32_t e0 = threadIdx.x * TI;
-  const uint64_t n = a.n[T.r];
-  wk_t wv[TI];
-  unsigned long long tm = 0, prev = 0, first = KEY_EMPTY;
-  bool unordered = false;
-  FaCursor<SRC, P2> cur(m, a, T.r, T.base, e0 < T.mt ? e0 : 0u, s_raw, g);
+  const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(a.src[T.r]) + T.base;
+  wk_t* out = static_cast<wk_t*>(words) + blockIdx.x * (uint64_t)TILE;
+  fa_raw_t<SRC> raw[TI];
+#pragma unroll
+  for (int k = 0; k < TI; ++k) {  // every load in flight before the first decode
+    const uint32_t e = (uint32_t)k * TB + threadIdx.x;
+    raw[k] = e < T.mt ? src[e] : (fa_raw_t<SRC>)0;
+  }
+  unsigned long long tm = 0;
+  bool bad = false;
 #pragma unroll
   for (int k = 0; k < TI; ++k) {
-    if (e0 + k < T.mt) {
-      const Elem e = cur.next();
-      tm = e.sink > tm ? e.sink : tm;
-      if (WK) wv[k] = (wk_t)e.w;
-      if (CHECK) {
-        if (k == 0) first = e.key;
-        else unordered |= !(e.key > prev);
-        prev = e.key;
+    const uint32_t e = (uint32_t)k * TB + threadIdx.x;
+    const bool v = e < T.mt;
+    Elem x{KEY_EMPTY, 0ull, 3u, 0u, ~0ull};
+    if (v) {
+      if (SRC == SRC_SAMPLES) x = elem_of_sample<P2>(m, a.pv[T.r], T.r, (uint64_t)raw[k], g);
+      else x = elem_of_word<P2>(m, a.pv[T.r], T.r, raw[k]);
+      tm = x.sink > tm ? x.sink : tm;
+      if (WK) out[e] = (wk_t)x.w;
+    }
+    if (CHECK) {  // strictly increasing keys: against the previous lane here, across waves/rounds below
+      const unsigned long long up = __shfl_up(x.key, 1, 64);
+      bad |= v && lane > 0 && !(x.key > up);
+      if (lane == 0) s_first[k][wid] = x.key;
+      if (lane == 63) s_last[k][wid] = x.key;
+    }
+  }
+  if (CHECK) {
+    __syncthreads();
+    if (threadIdx.x < TI * NW) {  // the first element of (round k, wave w) against the element before it
+      const uint32_t k = threadIdx.x / NW, w = threadIdx.x % NW;
+      const uint32_t e = k * TB + w * 64;
+      if (e < T.mt && (e > 0 || T.base > 0)) {
+        const unsigned long long prev =
+            e > 0 ? (w > 0 ? s_last[k][w - 1] : s_last[k - 1][NW - 1]) : fa_elem<SRC, P2>(m, a, T.r, T.base - 1, g).key;
+        bad |= !(s_first[k][w] > prev);
       }
     }
-  }
-  if (CHECK) {  // the lane's last element against the next lane's first (lane 63: the next element itself)
-    const unsigned long long nf = __shfl_down(first, 1, 64);
-    const uint64_t inext = T.base + e0 + TI;  // the element after this lane's run
-    if (e0 + TI <= T.mt && inext < n) {
-      const unsigned long long kn = (lane < 63 && e0 + TI < T.mt) ? nf : fa_elem<SRC, P2>(m, a, T.r, inext, g).key;
-      unordered |= !(kn > prev);
-    }
-    if (__ballot(unordered) && lane == 0) atomicOr(&g.flags[1], 1u);
-  }
-  if (WK) {  // words through LDS (the samples' staging buffer once it is consumed): coalesced stores
-    wk_t* buf = SRC == SRC_GEN ? s_wd : reinterpret_cast<wk_t*>(s_raw);
-    if (SRC != SRC_GEN) __syncthreads();
-#pragma unroll
-    for (int k = 0; k < TI; ++k)
-      if (e0 + k < T.mt) buf[fa_slot(e0 + k)] = wv[k];
-    __syncthreads();
-    wk_t* out = static_cast<wk_t*>(words) + blockIdx.x * (uint64_t)TILE;
-#pragma unroll
-    for (int k = 0; k < TI; ++k) {
-      const uint32_t e = k * TB + threadIdx.x;
-      if (e < T.mt) out[e] = buf[fa_slot(e)];
-    }
+    if (__ballot(bad) && lane == 0) atomicOr(&g.flags[1], 1u);
   }
   tm = sc_wave_red<true>(tm);
   if (lane == 0) s_w[wid] = tm;
@@ -791,21 +733,58 @@ __global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long 
   if (threadIdx.x == 0) {
     unsigned long long x = 0;
 #pragma unroll
-    for (int w = 0; w < TB / 64; ++w) x = s_w[w] > x ? s_w[w] : x;
+    for (int w = 0; w < NW; ++w) x = s_w[w] > x ? s_w[w] : x;
+    tmax[blockIdx.x] = x;
+  }
+}
+
+// Generated lists: each lane generates its run of TI consecutive elements
+// (incremental key-order digits), the words go out through LDS (coalesced).
+template <bool P2, int WK>
+__global__ __launch_bounds__(TB) void k_fa_max_gen(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
+                                                   void* words, GTable g) {
+  using wk_t = typename std::conditional<WK == 8, unsigned long long, uint32_t>::type;
+  constexpr int NW = TB / 64;
+  __shared__ unsigned long long s_w[NW];
+  __shared__ wk_t s_wd[FA_LDS];
+  const FaTile T = fa_tile(a, blockIdx.x);
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  const uint32_t e0 = threadIdx.x * TI;
+  unsigned long long tm = 0;
+  FaCursor<SRC_GEN, P2> cur(m, a, T.r, T.base, e0 < T.mt ? e0 : 0u, nullptr, g);
+#pragma unroll
+  for (int k = 0; k < TI; ++k) {
+    if (e0 + k < T.mt) {
+      const Elem e = cur.next();
+      tm = e.sink > tm ? e.sink : tm;
+      s_wd[fa_slot(e0 + k)] = (wk_t)e.w;
+    }
+  }
+  __syncthreads();
+  wk_t* out = static_cast<wk_t*>(words) + blockIdx.x * (uint64_t)TILE;
+#pragma unroll
+  for (int k = 0; k < TI; ++k) {
+    const uint32_t e = k * TB + threadIdx.x;
+    if (e < T.mt) out[e] = s_wd[fa_slot(e)];
+  }
+  tm = sc_wave_red<true>(tm);
+  if (lane == 0) s_w[wid] = tm;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long x = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) x = s_w[w] > x ? s_w[w] : x;
     tmax[blockIdx.x] = x;
   }
 }
 
 // One workgroup per reference: pmin[t] = max of tmax over the reference's
-// tiles before t (0 for its first); st of its tiles zeroed; its cut = n.
+// tiles before t (0 for its first).
 constexpr int PB = 1024;
 __global__ __launch_bounds__(PB) void k_fa_prefix(FaRefs a, const unsigned long long* __restrict__ tmax,
-                                                  unsigned long long* __restrict__ pmin, unsigned long long* st,
-                                                  unsigned long long* scal) {
+                                                  unsigned long long* __restrict__ pmin) {
   __shared__ unsigned long long s_w[PB / 64];
   const uint32_t r = blockIdx.x;
-  if (r == 0 && threadIdx.x == 0) scal[FA_COUNTER] = 0;
-  if (threadIdx.x == 0) scal[r * FA_SCAL] = a.n[r];
   const uint64_t t0 = a.toff[r], nt = a.toff[r + 1] - t0;
   if (nt == 0) return;
   const uint64_t per = (nt + PB - 1) / PB;
@@ -823,178 +802,319 @@ __global__ __launch_bounds__(PB) void k_fa_prefix(FaRefs a, const unsigned long 
   for (uint64_t t = lo; t < hi; ++t) {
     pmin[t] = run;
     run = tmax[t] > run ? tmax[t] : run;
-    st[t] = 0;
   }
 }
 
-template <int SRC, bool P2>
-__global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigned long long* __restrict__ pmin,
-                                                unsigned long long* st, unsigned long long* __restrict__ part,
-                                                unsigned long long* scal, GTable g) {
+// ---- pass 2: the scan of one tile of packed words (TB threads; thread x
+// owns the run [x*TI, (x+1)*TI), staged through LDS).  carry = the largest
+// sink before the tile (pmin).  The start counts need no chain across tiles:
+//   CUT = false (k_fa_scan, all tiles at once): the tile's start count, its
+//     hmax = 2j - (starts of the tile before j) at its last start j > 0, and
+//     the records of ALL its elements.  Q1's condition j - before_j >= n - j
+//     is 2j - before_j >= n, increasing in j; with c_in starts before the
+//     tile it holds at the tile's last start iff hmax >= n + c_in, so the cut
+//     lies in the first tile where that holds, and every earlier tile is
+//     recorded whole;
+//   CUT = true (k_fa_finish, that one tile, c_in known): the cut and the
+//     records below it.
+// sh.out[0, FPART): cold, traversed, case 0/1/2 counts; sh.out[FPART]: the
+// start count (CUT: the cut); sh.out[FPART + 1]: hmax.  (Results go through
+// LDS: a store through a generic pointer here would keep the kernels' FaRefs
+// argument copied to scratch.)
+constexpr int FPW = FPART + 2;
+template <int SRC>
+struct FaScanLds {
+  unsigned long long w[TB / 64], c[TB / 64], red[TB / 64][FPW], out[FPW];
+  fa_raw_t<SRC> raw[FA_LDS];
+};
+
+// the one reference a scanned tile belongs to (copied out of FaRefs by the
+// kernel, so the body never indexes the kernel argument itself)
+struct FaOne {
+  FaTile T;
+  uint64_t n;
+  const void* src;
+  PkView pv;
+};
+__device__ __forceinline__ FaOne fa_one(const FaRefs& a, uint64_t gt) {
+  FaOne o;
+  o.T = fa_tile(a, gt);
+  o.n = a.n[o.T.r];
+  o.src = a.src[o.T.r];
+  o.pv = a.pv[o.T.r];
+  return o;
+}
+
+template <int SRC, bool P2, bool CUT>
+__device__ __forceinline__ void fa_tile_scan(const Model& m, const FaOne& o, unsigned long long carry_in,
+                                             uint64_t c_in, FaScanLds<SRC>& sh) {
+  static_assert(SRC == SRC_W32 || SRC == SRC_W64, "the scan reads packed words");
+  using raw_t = fa_raw_t<SRC>;
   constexpr int NW = TB / 64;
-  __shared__ unsigned long long s_tile, s_w[NW], s_c[NW], s_inc, s_red[NW][FPART];
-  __shared__ fa_raw_t<SRC> s_raw[SRC == SRC_GEN ? 1 : FA_LDS];
-  if (threadIdx.x == 0) s_tile = atomicAdd(&scal[FA_COUNTER], 1ull);
-  __syncthreads();
-  const uint64_t gt = s_tile;
-  const FaTile T = fa_tile(a, gt);
-  fa_stage<SRC>(a, T.r, T.base, T.mt, s_raw);
+  const FaTile& T = o.T;
+  const bool full = T.mt == TILE;  // tile-uniform: no per-element bounds in the loops below
+  {
+    const raw_t* src = static_cast<const raw_t*>(o.src) + T.base;
+#pragma unroll
+    for (int k = 0; k < TI; ++k) {
+      const uint32_t e = (uint32_t)k * TB + threadIdx.x;
+      if (full || e < T.mt) sh.raw[fa_slot(e)] = src[e];
+    }
+    __syncthreads();
+  }
   const uint32_t r = T.r;
-  const uint64_t n = a.n[r];
+  const uint64_t n = o.n;
   const unsigned long long endkey = m.A * m.T;
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  const uint32_t e0 = threadIdx.x * TI;                             // this lane's run in the tile
+  const uint32_t e0 = threadIdx.x * TI;                                       // this lane's run in the tile
   const uint32_t nv = e0 < T.mt ? (T.mt - e0 < TI ? T.mt - e0 : TI) : 0u;  // its valid elements
-  const uint64_t i0 = T.base + e0;                                  // index of its first element
-  // ri*T per case (KEY_EMPTY: cold), to recompute sinks from keys
-  unsigned long long rt[3];
+  const uint64_t i0 = T.base + e0;                                            // index of its first element
+  // ri*T per case (KEY_EMPTY: a cold case; case 3 = a malformed word, already flagged)
+  unsigned long long rt[4];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) rt[c] = a.pv[r].ri[c] < 0 ? KEY_EMPTY : (unsigned long long)a.pv[r].ri[c] * m.T;
-  auto sink_of = [&](unsigned long long key, uint32_t c) -> unsigned long long {
-    const unsigned long long d = c == 0 ? rt[0] : (c == 1 ? rt[1] : rt[2]);
-    return (c > 2 || d == KEY_EMPTY || key == KEY_EMPTY) ? KEY_EMPTY : key + d;
-  };
-  unsigned long long key[TI];
-  uint32_t cases = 0, t0s = 0;  // 2 bits per element; tid == 0 per element
+  for (int c = 0; c < 3; ++c) rt[c] = o.pv.ri[c] < 0 ? KEY_EMPTY : (unsigned long long)o.pv.ri[c] * m.T;
+  rt[3] = KEY_EMPTY;
+  // decode: keys and sinks in registers, cases (2 bits) and tid == 0 (at bit 2k) per element
+  unsigned long long key[TI], snk[TI];
+  uint32_t cases = 0, t0s = 0;
   unsigned long long lmax = 0;
-  FaCursor<SRC, P2> cur(m, a, r, T.base, nv ? e0 : 0u, s_raw, g);
 #pragma unroll
   for (int k = 0; k < TI; ++k) {
-    Elem e{KEY_EMPTY, 0ull, 3u, 0u, ~0ull};
-    if ((uint32_t)k < nv) e = cur.next();
-    key[k] = e.key;
-    cases |= (e.c & 3u) << (2 * k);
-    t0s |= e.t0 << k;
-    if ((uint32_t)k < nv) lmax = e.sink > lmax ? e.sink : lmax;
+    key[k] = KEY_EMPTY;
+    snk[k] = 0;
+    if (full || (uint32_t)k < nv) {
+      const raw_t w = sh.raw[fa_slot(e0 + k)];
+      uint32_t c, t;
+      unsigned long long kk;
+      if (P2) {  // rank = ((q*N + c1)*N + c2)*T + tid; q*N + c1 < 2^32 (fa_run)
+        c = (uint32_t)w & 3u;
+        const raw_t rk = w >> 2;
+        t = (uint32_t)rk & (uint32_t)(o.pv.T - 1);
+        const uint32_t c2 = (uint32_t)(rk >> o.pv.tsh) & (uint32_t)(o.pv.N - 1);
+        const uint32_t qc = (uint32_t)(rk >> (o.pv.tsh + o.pv.nsh));
+        const uint64_t a = (uint64_t)qc * (uint32_t)m.S + ref_off(r, c2);
+        kk = (a << o.pv.tsh) | t;
+      } else {
+        const Elem e = elem_of_word<false>(m, o.pv, r, w);
+        kk = e.key;
+        c = e.c;
+        t = e.t0 ? 0u : 1u;
+      }
+      const unsigned long long d = c == 0 ? rt[0] : (c == 1 ? rt[1] : (c == 2 ? rt[2] : rt[3]));
+      const unsigned long long sk = d == KEY_EMPTY ? KEY_EMPTY : kk + d;
+      key[k] = kk;
+      snk[k] = sk;
+      lmax = sk > lmax ? sk : lmax;
+      cases |= c << (2 * k);
+      t0s |= (t == 0 ? 1u : 0u) << (2 * k);
+    }
   }
   // running max of sinks entering this lane: the tile's incoming max, the
   // earlier waves' maxima, the earlier lanes' maxima
   const unsigned long long linc = sc_wave_scan<true>(lmax, lane);
-  if (lane == 63) s_w[wid] = linc;
+  if (lane == 63) sh.w[wid] = linc;
   __syncthreads();
-  unsigned long long carry = pmin[gt];
+  unsigned long long carry = carry_in;
 #pragma unroll
   for (int x = 0; x < NW; ++x)
-    if (x < (int)wid) carry = s_w[x] > carry ? s_w[x] : carry;
+    if (x < (int)wid) carry = sh.w[x] > carry ? sh.w[x] : carry;
   {
     const unsigned long long up = __shfl_up(linc, 1, 64);
     if (lane) carry = up > carry ? up : carry;
   }
-  // start flags: key > the running max before it (or the reference's first element)
-  uint32_t flags = 0, lcnt = 0;
-  {
+  // Start flags (key > the running max before it; the reference's first
+  // element) and, for the elements below lim, traversed: a replay starting
+  // at p subtracts key_p; the replay ending at p - 1 adds the running max
+  // there when p starts one, p == cut or p == n.  The end of a tile's last
+  // element is counted by the next tile (its first element's boundary).
+  uint32_t flags = 0;
+  unsigned long long tpos = 0, tneg = 0;
+  auto scan = [&](uint64_t lim, bool rec) {
     unsigned long long run = carry;
+    flags = 0;
 #pragma unroll
     for (int k = 0; k < TI; ++k) {
-      if ((uint32_t)k < nv) {
-        const bool f = (i0 + k == 0) || key[k] > run;
+      if (full || (uint32_t)k < nv) {
+        const uint64_t p = i0 + k;
+        bool f = key[k] > run;
+        if (k == 0) f = f || i0 == 0;
         flags |= (f ? 1u : 0u) << k;
-        lcnt += f ? 1u : 0u;
-        const unsigned long long sk = sink_of(key[k], (cases >> (2 * k)) & 3u);
-        run = sk > run ? sk : run;
+        if (rec) {
+          if (p < lim) {
+            if (f) {
+              tneg += key[k];
+              if (p != 0) tpos += run;  // f implies run is a sink (not KEY_EMPTY)
+            }
+          } else if (CUT && p == lim) {
+            tpos += run == KEY_EMPTY ? endkey : run;
+          }
+        }
+        run = snk[k] > run ? snk[k] : run;
       }
     }
-  }
-  // start counts: lanes, waves, then the chain over the reference's tiles
-  const unsigned long long cinc = sc_wave_scan<false>(lcnt, lane);
-  if (lane == 63) s_c[wid] = cinc;
+    if (rec && nv && i0 + nv == n && n <= lim) tpos += run == KEY_EMPTY ? endkey : run;  // the last element ends
+  };
+  if (!CUT) scan(n, true);
+  else scan(n, false);
+  // start counts: lanes, then waves (the tile's total)
+  const uint32_t lcnt = (uint32_t)__popc(flags);
+  const uint32_t cinc = (uint32_t)sc_wave_scan<false>(lcnt, lane);
+  if (lane == 63) sh.c[wid] = cinc;
   __syncthreads();
-  unsigned long long cpre = 0, cagg = 0;
+  uint64_t cpre = 0, cagg = 0;
 #pragma unroll
   for (int x = 0; x < NW; ++x) {
-    if (x < (int)wid) cpre += s_c[x];
-    cagg += s_c[x];
+    if (x < (int)wid) cpre += sh.c[x];
+    cagg += sh.c[x];
   }
-  const unsigned long long c_in = fu_chain<false>(st + a.toff[r], (uint32_t)T.lt, cagg, lane, &s_inc);
-  const uint64_t sb0 = c_in + cpre + (cinc - lcnt);  // starts before this lane's first element
-  // the tile's Q1 candidate: its first start j > 0 with j - starts_before_j >= n - j
-  unsigned long long best = KEY_EMPTY;
-#pragma unroll
-  for (int k = 0; k < TI; ++k) {
-    const uint64_t j = i0 + k;
-    const uint64_t before_j = sb0 + (uint64_t)__popc(flags & ((1u << k) - 1u));
-    if (best == KEY_EMPTY && ((flags >> k) & 1u) && j > 0 && j - before_j >= n - j) best = j;
-  }
-  best = sc_wave_red_min(best);
-  __syncthreads();  // s_w is reused
-  if (lane == 0) s_w[wid] = best;
-  __syncthreads();
-  unsigned long long cut = n;
-#pragma unroll
-  for (int x = 0; x < NW; ++x) cut = s_w[x] < cut ? s_w[x] : cut;
-  if (threadIdx.x == 0 && cut < n) atomicMin(&scal[r * FA_SCAL], cut);
-  // record this lane's elements below the tile's candidate
-  unsigned long long cold = 0, trav = 0;
-  uint32_t nc0 = 0, nc1 = 0, nc2 = 0;
-  // the key after this lane's run: the next lane's first, or (lane 63, or the tile's end) the source's
-  unsigned long long knext = __shfl_down(key[0], 1, 64);
-  if (lane == 63 || e0 + TI >= T.mt) knext = (nv == TI && i0 + TI < n) ? fa_elem<SRC, P2>(m, a, r, i0 + TI, g).key : KEY_EMPTY;
-  {
-    unsigned long long run = carry;
+  const uint64_t lb = cpre + (cinc - lcnt);  // starts of the tile before this lane's first element
+  uint64_t cut = n;
+  unsigned long long hl = 0;
+  if (CUT) {  // the first start j > 0 with j - before_j >= n - j; then the records below it
+    unsigned long long best = KEY_EMPTY;
 #pragma unroll
     for (int k = 0; k < TI; ++k) {
-      const uint64_t i = i0 + k;
-      if ((uint32_t)k < nv && i < cut) {
-        const uint32_t c = (cases >> (2 * k)) & 3u;
-        const unsigned long long kk = key[k], sk = sink_of(kk, c);
-        const unsigned long long gm = sk > run ? sk : run;  // inclusive running max at i
-        run = gm;
-        if (sk == KEY_EMPTY) {
-          cold += (t0s >> k) & 1u;
-        } else {
-          nc0 += c == 0 ? 1u : 0u;
-          nc1 += c == 1 ? 1u : 0u;
-          nc2 += c == 2 ? 1u : 0u;
-        }
-        if ((flags >> k) & 1u) trav -= kk;  // this element starts a replay
-        const unsigned long long kn = k + 1 < TI ? key[k + 1 < TI ? k + 1 : k] : knext;
-        if (i + 1 == cut || (i + 1 < n ? kn > gm : true)) trav += (gm == KEY_EMPTY) ? endkey : gm;  // ends one
-      }
+      const uint64_t j = i0 + k;
+      const uint64_t before_j = c_in + lb + (uint64_t)__popc(flags & ((1u << k) - 1u));
+      if (best == KEY_EMPTY && ((flags >> k) & 1u) && j > 0 && j - before_j >= n - j) best = j;
     }
+    best = sc_wave_red_min(best);
+    if (lane == 0) sh.red[wid][0] = best;
+    __syncthreads();
+#pragma unroll
+    for (int x = 0; x < NW; ++x) cut = sh.red[x][0] < cut ? sh.red[x][0] : cut;
+    __syncthreads();  // sh.red is reused below
+    scan(cut, true);
+  } else if (flags) {
+    const int k = 31 - __clz(flags);
+    const uint64_t j = i0 + k;
+    if (j > 0) hl = 2 * j - (lb + (uint64_t)__popc(flags & ((1u << k) - 1u)));
   }
-  const unsigned long long v[FPART] = {sc_wave_red<false>(cold), sc_wave_red<false>(trav),
-                                       sc_wave_red<false>(nc0), sc_wave_red<false>(nc1), sc_wave_red<false>(nc2)};
+  // recorded elements (below the cut) per case: recorded, or cold (tid 0 only)
+  const uint64_t nrec = cut <= i0 ? 0 : (cut - i0 < nv ? cut - i0 : nv);
+  const uint32_t rec2 = nrec >= 16 ? 0x55555555u : (uint32_t)((1ull << (2 * nrec)) - 1) & 0x55555555u;
+  const uint32_t lo = cases & rec2, hi = (cases >> 1) & rec2;
+  const uint32_t mc[3] = {rec2 & ~lo & ~hi, lo & ~hi, hi & ~lo};
+  unsigned long long packed = 0;  // cold | case 0 << 16 | case 1 << 32 | case 2 << 48 (each <= TILE per tile)
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    if (rt[c] == KEY_EMPTY) packed += (unsigned long long)__popc(mc[c] & t0s);
+    else packed += (unsigned long long)__popc(mc[c]) << (16 * (c + 1));
+  }
+  const unsigned long long v[3] = {sc_wave_red<false>(packed), sc_wave_red<false>(tpos - tneg),
+                                   CUT ? 0ull : sc_wave_red<true>(hl)};
   if (lane == 0)
 #pragma unroll
-    for (int f = 0; f < FPART; ++f) s_red[wid][f] = v[f];
+    for (int f = 0; f < 3; ++f) sh.red[wid][f] = v[f];
   __syncthreads();
-  if (threadIdx.x < FPART) {
+  if (threadIdx.x < FPW) {
     unsigned long long x = 0;
+    const uint32_t f = threadIdx.x;
+    if (f == FPART) {
+      x = CUT ? cut : cagg;
+    } else if (f == FPART + 1) {
 #pragma unroll
-    for (int w = 0; w < NW; ++w) x += s_red[w][threadIdx.x];
-    part[gt * FPART + threadIdx.x] = x;
+      for (int w = 0; w < NW; ++w) x = sh.red[w][2] > x ? sh.red[w][2] : x;
+    } else if (f == 1) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) x += sh.red[w][1];
+    } else {  // 0 cold, 2..4 case counts
+      const uint32_t sh16 = f == 0 ? 0u : 16u * (f - 1);
+#pragma unroll
+      for (int w = 0; w < NW; ++w) x += (sh.red[w][0] >> sh16) & 0xFFFFull;
+    }
+    sh.out[f] = x;
   }
+  __syncthreads();
 }
 
-// One workgroup per reference with samples: the partials of its tiles that
-// start below its cut; Q3 (nothing dropped: the owner of the final largest
-// sink stays in LAT, +1 cold if it is tid 0); the -1 key (materialised even
-// with 0, r10:196,671), traversed, the (ref, case) bins.
-__global__ __launch_bounds__(BLOCK) void k_fa_finish(Model m, FaRefs a, const unsigned long long* __restrict__ tmax,
-                                                     const unsigned long long* __restrict__ pmin,
-                                                     const unsigned long long* __restrict__ part,
-                                                     const unsigned long long* scal, GTable g) {
-  __shared__ unsigned long long red[BLOCK / 64][FPART];
+template <int SRC, bool P2>
+__global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigned long long* __restrict__ pmin,
+                                                unsigned long long* __restrict__ part, GTable g) {
+  __shared__ FaScanLds<SRC> sh;
+  const FaOne o = fa_one(a, blockIdx.x);
+  fa_tile_scan<SRC, P2, false>(m, o, pmin[blockIdx.x], 0, sh);
+  if (threadIdx.x < FPW) part[blockIdx.x * (uint64_t)FPW + threadIdx.x] = sh.out[threadIdx.x];
+}
+
+// ---- pass 3, one workgroup per reference with samples: the exclusive sum of
+// its tiles' start counts locates the tile holding the Q1 cut (the first with
+// hmax >= n + starts before it); the tiles before it are summed whole, that
+// tile is scanned again with its incoming start count (CUT); then Q3 (nothing
+// dropped: the owner of the final largest sink stays in LAT, +1 cold if it is
+// tid 0), the -1 key (materialised even with 0, r10:196,671), traversed and
+// the (ref, case) bins.
+template <int SRC, bool P2>
+__global__ __launch_bounds__(TB) void k_fa_finish(Model m, FaRefs a, const unsigned long long* __restrict__ tmax,
+                                                  const unsigned long long* __restrict__ pmin,
+                                                  const unsigned long long* __restrict__ part, GTable g) {
+  constexpr int NW = TB / 64;
+  __shared__ FaScanLds<SRC> sh;
+  __shared__ unsigned long long s_ct[2], s_red[NW][FPART];
   const uint32_t r = blockIdx.x;
   const uint64_t n = a.n[r];
   if (n == 0) return;
-  const uint64_t cut = scal[r * FA_SCAL];
   const uint64_t t0 = a.toff[r], nt = a.toff[r + 1] - t0;
-  unsigned long long v[FPART] = {0, 0, 0, 0, 0};
-  for (uint64_t t = threadIdx.x; t < nt && t * TILE < cut; t += BLOCK)
-#pragma unroll
-    for (int f = 0; f < FPART; ++f) v[f] += part[(t0 + t) * FPART + f];
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  // 1. the cut tile
+  uint64_t ct = nt, cin = 0, c = 0;
+  for (uint64_t b0 = 0; b0 < nt; b0 += TB) {
+    const uint64_t t = b0 + threadIdx.x;
+    const unsigned long long cnt = t < nt ? part[(t0 + t) * FPW + FPART] : 0ull;
+    const unsigned long long h = t < nt ? part[(t0 + t) * FPW + FPART + 1] : 0ull;
+    const unsigned long long inc = sc_wave_scan<false>(cnt, lane);
+    if (lane == 63) sh.c[wid] = inc;
+    __syncthreads();
+    unsigned long long pre = c, tot = 0;
+#pragma unroll
+    for (int x = 0; x < NW; ++x) {
+      if (x < (int)wid) pre += sh.c[x];
+      tot += sh.c[x];
+    }
+    const unsigned long long excl = pre + inc - cnt;
+    const bool hit = t < nt && h >= n + excl;
+    const unsigned long long cand = sc_wave_red_min(hit ? t : KEY_EMPTY);
+    if (lane == 0) sh.w[wid] = cand;
+    __syncthreads();
+    unsigned long long best = KEY_EMPTY;
+#pragma unroll
+    for (int x = 0; x < NW; ++x) best = sh.w[x] < best ? sh.w[x] : best;
+    if (best != KEY_EMPTY) {  // block-uniform
+      if (t == best) s_ct[0] = excl;
+      __syncthreads();
+      ct = best;
+      cin = s_ct[0];
+      break;
+    }
+    c += tot;
+    __syncthreads();  // sh.c / sh.w are rewritten by the next chunk
+  }
+  // 2. the tiles before it, whole
+  unsigned long long v[FPART] = {0, 0, 0, 0, 0};
+  for (uint64_t t = threadIdx.x; t < ct; t += TB)
+#pragma unroll
+    for (int f = 0; f < FPART; ++f) v[f] += part[(t0 + t) * FPW + f];
 #pragma unroll
   for (int f = 0; f < FPART; ++f) {
     v[f] = sc_wave_red<false>(v[f]);
-    if (lane == 0) red[wid][f] = v[f];
+    if (lane == 0) s_red[wid][f] = v[f];
+  }
+  // 3. the cut tile, below the cut
+  uint64_t cut = n;
+  if (ct < nt) {
+    __syncthreads();
+    const FaOne o = fa_one(a, t0 + ct);
+    fa_tile_scan<SRC, P2, true>(m, o, pmin[t0 + ct], cin, sh);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long tot[FPART] = {0, 0, 0, 0, 0};
-    for (int x = 0; x < BLOCK / 64; ++x)
-      for (int f = 0; f < FPART; ++f) tot[f] += red[x][f];
+    for (int x = 0; x < NW; ++x)
+      for (int f = 0; f < FPART; ++f) tot[f] += s_red[x][f];
+    if (ct < nt) {
+      for (int f = 0; f < FPART; ++f) tot[f] += sh.out[f];
+      cut = sh.out[FPART];
+    }
     unsigned long long cold = tot[0];
     if (cut == n) {
       const uint64_t last = t0 + nt - 1;
@@ -1003,8 +1123,8 @@ __global__ __launch_bounds__(BLOCK) void k_fa_finish(Model m, FaRefs a, const un
     }
     g_add(g, make_key(r, 0, -1), cold);
     g.trav[r] += tot[1];
-    for (int c = 0; c < 3; ++c)
-      if (tot[2 + c]) atomicAdd(&g.bins[r * 3 + c], tot[2 + c]);
+    for (int x = 0; x < 3; ++x)
+      if (tot[2 + x]) atomicAdd(&g.bins[r * 3 + x], tot[2 + x]);
   }
 }
 
@@ -1349,17 +1469,13 @@ static int fork_refs(pluss_ctx* ctx, const uint64_t* counts, hipStream_t s, F&& 
 }
 
 // ---- the scan pipeline (k_fa_*) over the references with a.n[r] > 0, on
-// stream s.  Its buffers are the handle's (ctx->fb): tile maxima, prefixes,
-// look-back words and partials, sized by the tiles of all references.
+// stream s.  Its buffers are the handle's (ctx->fb): tile maxima, prefixes
+// and per-tile partials, sized by the tiles of all references.
 static int fa_reserve(FaithfulBufs& b, uint64_t tiles, hipStream_t s) {
-  if (!b.fscal) {
-    if (int rc = grow(&b.fscal, 64)) return rc;
-  }
   if (tiles > b.dcap) {
     PLUSS_HIP_CHECK(hipStreamSynchronize(s));
     int rc = 0;
-    if ((rc = grow(&b.dst, tiles)) || (rc = grow(&b.dpart, tiles * FPART)) || (rc = grow(&b.tmax, tiles)) ||
-        (rc = grow(&b.pmin, tiles)))
+    if ((rc = grow(&b.dpart, tiles * FPW)) || (rc = grow(&b.tmax, tiles)) || (rc = grow(&b.pmin, tiles)))
       return rc;
     b.dcap = tiles;
   }
@@ -1383,7 +1499,9 @@ static int fa_run(pluss_ctx* ctx, FaRefs& a, int src, bool check, hipStream_t s)
   FaithfulBufs& b = ctx->fb;
   if (int rc = fa_reserve(b, t, s)) return rc;
   const GTable& g = ctx->g;
-  const bool p2 = m.p2 && a.pv[0].p2;  // N, T, CS, CLS/DS powers of two: shift decoding
+  // N, T, CS, CLS/DS powers of two: shift decoding (the scan's word decode
+  // also keeps q*N + c1 < N*N/T in 32 bits)
+  const bool p2 = m.p2 && a.pv[0].p2 && (uint64_t)m.N * m.N / m.T < (1ull << 32);
   // samples / generated lists: the first pass writes the packed sort words
   // (4 or 8 bytes, as the radix path sorts them) and the scan reads those
   const bool w32 = pk_bits(m) <= 32;
@@ -1406,20 +1524,24 @@ static int fa_run(pluss_ctx* ctx, FaRefs& a, int src, bool check, hipStream_t s)
   }
 #define PLUSS_FA3(SRCV, CHK, P2V, WKV, SCANV)                                                                      \
   do {                                                                                                             \
-    hipLaunchKernelGGL((k_fa_max<SRCV, CHK, P2V, WKV>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.tmax, b.words, g); \
-    hipLaunchKernelGGL(k_fa_prefix, dim3(6), dim3(PB), 0, s, a, b.tmax, b.pmin, b.dst, b.fscal);                   \
-    hipLaunchKernelGGL((k_fa_scan<SCANV, P2V>), dim3((unsigned)t), dim3(TB), 0, s, m, aw, b.pmin, b.dst, b.dpart, \
-                       b.fscal, g);                                                                                \
+    if constexpr (SRCV == SRC_GEN)                                                                                 \
+      hipLaunchKernelGGL((k_fa_max_gen<P2V, WKV>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.tmax, b.words, g);   \
+    else                                                                                                           \
+      hipLaunchKernelGGL((k_fa_max<SRCV, CHK, P2V, WKV>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.tmax, b.words, \
+                         g);                                                                                       \
+    hipLaunchKernelGGL(k_fa_prefix, dim3(6), dim3(PB), 0, s, a, b.tmax, b.pmin);                                   \
+    hipLaunchKernelGGL((k_fa_scan<SCANV, P2V>), dim3((unsigned)t), dim3(TB), 0, s, m, aw, b.pmin, b.dpart, g);    \
+    hipLaunchKernelGGL((k_fa_finish<SCANV, P2V>), dim3(6), dim3(TB), 0, s, m, aw, b.tmax, b.pmin, b.dpart, g);    \
   } while (0)
 #define PLUSS_FA2(SRCV, CHK, WKV, SCANV)            \
   do {                                              \
     if (p2) PLUSS_FA3(SRCV, CHK, true, WKV, SCANV); \
     else PLUSS_FA3(SRCV, CHK, false, WKV, SCANV);   \
   } while (0)
-#define PLUSS_FA(SRCV, CHK)                                    \
-  do {                                                         \
-    if (w32) PLUSS_FA2(SRCV, CHK, 4, SRC_W32);                 \
-    else PLUSS_FA2(SRCV, CHK, 8, SRC_W64);                     \
+#define PLUSS_FA(SRCV, CHK)                    \
+  do {                                         \
+    if (w32) PLUSS_FA2(SRCV, CHK, 4, SRC_W32); \
+    else PLUSS_FA2(SRCV, CHK, 8, SRC_W64);     \
   } while (0)
   switch (src) {
     case SRC_W32: PLUSS_FA2(SRC_W32, false, 0, SRC_W32); break;
@@ -1433,7 +1555,6 @@ static int fa_run(pluss_ctx* ctx, FaRefs& a, int src, bool check, hipStream_t s)
 #undef PLUSS_FA
 #undef PLUSS_FA2
 #undef PLUSS_FA3
-  hipLaunchKernelGGL(k_fa_finish, dim3(6), dim3(BLOCK), 0, s, m, a, b.tmax, b.pmin, b.dpart, b.fscal, g);
   PLUSS_HIP_CHECK(hipGetLastError());
   ctx->tables_dirty = true;
   return PLUSS_OK;

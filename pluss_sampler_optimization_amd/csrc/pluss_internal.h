@@ -63,10 +63,10 @@ struct FaithfulBufs {
   size_t tmp_bytes = 0;
   unsigned long long* scal = nullptr;  // [0] cut, [1] cold, [2] traversed, [3] shard size, [4] scan tile counter
   unsigned long long* st = nullptr;    // look-back status words of the one-GPU scan (2 per tile)
-  // the scan pipeline (pluss_faithful.hip k_fa_*): per tile the look-back word, the partials, the
-  // largest sink and the running max entering it; its scalars (cut per reference, tile counter)
+  // the scan pipeline (pluss_faithful.hip k_fa_*): per tile the partials, the largest sink and the
+  // running max entering it
   uint64_t dcap = 0;
-  unsigned long long *dst = nullptr, *dpart = nullptr, *tmax = nullptr, *pmin = nullptr, *fscal = nullptr;
+  unsigned long long *dpart = nullptr, *tmax = nullptr, *pmin = nullptr;
   void* words = nullptr;  // packed sort words written by the first pass (sample / generated sources)
   size_t words_bytes = 0;
 };

@@ -89,7 +89,8 @@ def test_faithful_sorted_on_reference_samples(orc, name, d, smp):
     assert h.bins == h1.bins and list(h.traversed) == list(h1.traversed)
 
 
-@pytest.mark.parametrize("N,T,per", [(128, 4, 2098), (256, 4, 6000), (512, 4, 3000), (128, 8, 9000)])
+@pytest.mark.parametrize("N,T,per", [(128, 4, 2098), (256, 4, 6000), (512, 4, 3000), (128, 8, 9000),
+                                     (96, 4, 3000), (120, 3, 3000)])  # the last two: non-power-of-two decode
 def test_faithful_sorted_and_generated_equal_oracle(orc, N, T, per):
     """Key-order lists: the no-sort path, the generated path and the radix-sort
     path (on a shuffled copy) all equal the stepping r10 oracle."""
