@@ -55,6 +55,27 @@ __device__ __noinline__ bool g_add_cap(unsigned long long* keys, unsigned long l
   return false;
 }
 
+// The main-table slot of `key`, inserted with count 0 when absent (so it is
+// materialised even if nothing is added later); ~0 when the table is full
+// (overflow flagged).
+__device__ __noinline__ unsigned long long g_slot(GTable g, uint64_t key) {
+  atomicOr(&g.flags[3], 1u);  // main table in use: k_export must scan it
+  uint32_t s = slot_hash(key, GCAP);
+#pragma unroll 1
+  for (uint32_t p = 0; p < GCAP; ++p) {
+    const unsigned long long k = __hip_atomic_load(&g.keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k == KEY_NONE) {
+      const unsigned long long prev = atomicCAS(&g.keys[s], KEY_NONE, (unsigned long long)key);
+      if (prev == KEY_NONE || prev == key) return s;
+    } else if (k == key) {
+      return s;
+    }
+    s = (s + 1) & (GCAP - 1);
+  }
+  atomicOr(&g.flags[0], 1u);
+  return ~0ull;
+}
+
 __device__ __forceinline__ void g_add(GTable g, uint64_t key, uint64_t cnt) {
   atomicOr(&g.flags[3], 1u);  // main table in use: k_export must scan it
   if (!g_add_cap(g.keys, g.counts, GCAP, key, cnt)) atomicOr(&g.flags[0], 1u);

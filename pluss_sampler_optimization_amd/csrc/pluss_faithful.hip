@@ -514,12 +514,14 @@ struct Elem {
 
 template <bool P2>
 __device__ __forceinline__ Elem elem_of_digits(const Model& m, const PkView& v, uint32_t ref, const KeyDigits& d) {
-  const uint64_t a = ((uint64_t)d.q * m.N + d.c1) * m.S + ref_off(ref, d.c2);
+  // P2: q*N + c1 < N*N/T < 2^32 (fa_run), so one 32x32->64 multiply
+  const uint64_t qc = P2 ? (uint64_t)((d.q << v.nsh) | d.c1) : (uint64_t)d.q * m.N + d.c1;
+  const uint64_t a = (P2 ? (uint64_t)(uint32_t)qc * (uint32_t)m.S : qc * m.S) + ref_off(ref, d.c2);
   const uint64_t key = P2 ? ((a << v.tsh) | d.t) : a * m.T + d.t;
   const uint32_t c = case_of_digits<P2>(m, ref, d, v.Q);
   const int64_t ri = c == 0 ? v.ri[0] : (c == 1 ? v.ri[1] : v.ri[2]);
   const unsigned long long dt = P2 ? ((unsigned long long)ri << v.tsh) : (unsigned long long)ri * m.T;
-  const uint64_t qc = (uint64_t)d.q * m.N + d.c1;  // rank = ((q*N + c1)*N + c2)*T + t
+  // rank = ((q*N + c1)*N + c2)*T + t
   const uint64_t rank = P2 ? ((((qc << v.nsh) | d.c2) << v.tsh) | d.t) : (qc * m.N + d.c2) * m.T + d.t;
   return Elem{key, ri < 0 ? KEY_EMPTY : key + dt, c, d.t == 0 ? 1u : 0u, (rank << 2) | c};
 }
@@ -669,47 +671,94 @@ __device__ __forceinline__ FaTile fa_tile(const FaRefs& a, uint64_t gt) {
   return t;
 }
 
+// the one reference a scanned tile belongs to (copied out of FaRefs by the
+// kernel, so the body never indexes the kernel argument itself)
+struct FaOne {
+  FaTile T;
+  uint64_t n;
+  const void* src;
+  PkView pv;
+};
+__device__ __forceinline__ FaOne fa_one(const FaRefs& a, uint64_t gt) {
+  FaOne o;
+  o.T = fa_tile(a, gt);
+  o.n = a.n[o.T.r];
+  o.src = a.src[o.T.r];
+  o.pv = a.pv[o.T.r];
+  return o;
+}
+
 // ---- pass 1 (k_fa_max*): per tile, the largest sink; for a caller's list
 // the key-order check; for sample / generated sources also the packed sort
 // word of every element (written once, read by the scan).
 //
 // Lists in memory (sorted words, a caller's samples): element-strided, thread
 // x round k holds element k*TB + x, so every load and word store is coalesced
-// and no LDS staging is needed (occupancy is not capped by LDS).
-template <int SRC, bool CHECK, bool P2, int WK>
-__global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long long* __restrict__ tmax, void* words,
-                                               GTable g) {
-  static_assert(SRC != SRC_GEN, "generated lists: k_fa_max_gen");
+// and no LDS staging is needed (occupancy is not capped by LDS).  The body is
+// instantiated per reference (tile-uniform switch), so the decode and the
+// case rules fold to the reference's own few instructions.
+template <uint32_t REF, bool P2>
+__device__ __forceinline__ Elem elem_of_sample_ref(const Model& m, const PkView& v, uint64_t x, bool& bad) {
+  const Sample s = unpack(x);
+  const uint32_t mx = s.c0 > s.c1 ? s.c0 : s.c1;
+  const bool ok = s.ref == REF && (mx > s.c2 ? mx : s.c2) < m.N;
+  bad |= !ok;
+  KeyDigits d;
+  d.c1 = s.c1;
+  d.c2 = (REF == C0 || REF == C1) ? 0u : s.c2;
+  if (P2) {
+    const uint32_t k = s.c0 >> m.csshift;
+    d.t = k & (m.T - 1);
+    d.q = ((k >> v.tsh) << m.csshift) | (s.c0 & m.csmask);
+  } else {
+    const uint32_t k = fdiv(s.c0, m.dCS), kt = fdiv(k, m.dT);
+    d.t = k - kt * m.T;
+    d.q = kt * m.CS + (s.c0 - k * m.CS);
+  }
+  Elem e = elem_of_digits<P2>(m, v, REF, d);
+  if (!ok) e = Elem{KEY_EMPTY, KEY_EMPTY, 3u, 0u, ~0ull};
+  return e;
+}
+
+template <int SRC, bool P2, uint32_t REF>
+__device__ __forceinline__ Elem fa_decode_ref(const Model& m, const PkView& v, fa_raw_t<SRC> w, bool& bad) {
+  if constexpr (SRC == SRC_SAMPLES) return elem_of_sample_ref<REF, P2>(m, v, (uint64_t)w, bad);
+  else return elem_of_word<P2>(m, v, REF, w);
+}
+
+template <int SRC, bool CHECK, bool P2, int WK, uint32_t REF>
+__device__ __forceinline__ void fa_max_tile(const Model& m, const FaOne& o, unsigned long long* __restrict__ tmax,
+                                            void* words, GTable g, unsigned long long* s_w,
+                                            unsigned long long (*s_first)[TB / 64],
+                                            unsigned long long (*s_last)[TB / 64]) {
   using wk_t = typename std::conditional<WK == 8, unsigned long long, uint32_t>::type;
   constexpr int NW = TB / 64;
-  __shared__ unsigned long long s_w[NW];
-  __shared__ unsigned long long s_first[CHECK ? TI : 1][NW], s_last[CHECK ? TI : 1][NW];
-  const FaTile T = fa_tile(a, blockIdx.x);
+  const FaTile& T = o.T;
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(a.src[T.r]) + T.base;
+  const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(o.src) + T.base;
   wk_t* out = static_cast<wk_t*>(words) + blockIdx.x * (uint64_t)TILE;
+  const bool full = T.mt == TILE;
   fa_raw_t<SRC> raw[TI];
 #pragma unroll
   for (int k = 0; k < TI; ++k) {  // every load in flight before the first decode
     const uint32_t e = (uint32_t)k * TB + threadIdx.x;
-    raw[k] = e < T.mt ? src[e] : (fa_raw_t<SRC>)0;
+    raw[k] = (full || e < T.mt) ? src[e] : (fa_raw_t<SRC>)0;
   }
   unsigned long long tm = 0;
-  bool bad = false;
+  bool bad = false, unordered = false;
 #pragma unroll
   for (int k = 0; k < TI; ++k) {
     const uint32_t e = (uint32_t)k * TB + threadIdx.x;
-    const bool v = e < T.mt;
+    const bool v = full || e < T.mt;
     Elem x{KEY_EMPTY, 0ull, 3u, 0u, ~0ull};
     if (v) {
-      if (SRC == SRC_SAMPLES) x = elem_of_sample<P2>(m, a.pv[T.r], T.r, (uint64_t)raw[k], g);
-      else x = elem_of_word<P2>(m, a.pv[T.r], T.r, raw[k]);
+      x = fa_decode_ref<SRC, P2, REF>(m, o.pv, raw[k], bad);
       tm = x.sink > tm ? x.sink : tm;
       if (WK) out[e] = (wk_t)x.w;
     }
     if (CHECK) {  // strictly increasing keys: against the previous lane here, across waves/rounds below
       const unsigned long long up = __shfl_up(x.key, 1, 64);
-      bad |= v && lane > 0 && !(x.key > up);
+      unordered |= v && lane > 0 && !(x.key > up);
       if (lane == 0) s_first[k][wid] = x.key;
       if (lane == 63) s_last[k][wid] = x.key;
     }
@@ -720,13 +769,14 @@ __global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long 
       const uint32_t k = threadIdx.x / NW, w = threadIdx.x % NW;
       const uint32_t e = k * TB + w * 64;
       if (e < T.mt && (e > 0 || T.base > 0)) {
+        bool b2 = false;
         const unsigned long long prev =
-            e > 0 ? (w > 0 ? s_last[k][w - 1] : s_last[k - 1][NW - 1]) : fa_elem<SRC, P2>(m, a, T.r, T.base - 1, g).key;
-        bad |= !(s_first[k][w] > prev);
+            e > 0 ? (w > 0 ? s_last[k][w - 1] : s_last[k - 1][NW - 1]) : fa_decode_ref<SRC, P2, REF>(m, o.pv, src[-1], b2).key;
+        unordered |= !(s_first[k][w] > prev);
       }
     }
-    if (__ballot(bad) && lane == 0) atomicOr(&g.flags[1], 1u);
   }
+  if (__ballot(bad || unordered) && lane == 0) atomicOr(&g.flags[1], 1u);
   tm = sc_wave_red<true>(tm);
   if (lane == 0) s_w[wid] = tm;
   __syncthreads();
@@ -738,26 +788,65 @@ __global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long 
   }
 }
 
-// Generated lists: each lane generates its run of TI consecutive elements
-// (incremental key-order digits), the words go out through LDS (coalesced).
-template <bool P2, int WK>
-__global__ __launch_bounds__(TB) void k_fa_max_gen(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
-                                                   void* words, GTable g) {
-  using wk_t = typename std::conditional<WK == 8, unsigned long long, uint32_t>::type;
+// the reference's first tile also materialises its -1 (cold) key in the main
+// table and keeps the slot, so the finish pass only adds the count
+__device__ __forceinline__ void fa_cold_slot(const FaTile& T, GTable g, unsigned long long* slots) {
+  if (T.lt == 0 && threadIdx.x == 0) slots[T.r] = g_slot(g, make_key(T.r, 0, -1));
+}
+
+template <int SRC, bool CHECK, bool P2, int WK>
+__global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long long* __restrict__ tmax, void* words,
+                                               unsigned long long* slots, GTable g) {
+  static_assert(SRC != SRC_GEN, "generated lists: k_fa_max_gen");
   constexpr int NW = TB / 64;
   __shared__ unsigned long long s_w[NW];
-  __shared__ wk_t s_wd[FA_LDS];
-  const FaTile T = fa_tile(a, blockIdx.x);
+  __shared__ unsigned long long s_first[CHECK ? TI : 1][NW], s_last[CHECK ? TI : 1][NW];
+  const FaOne o = fa_one(a, blockIdx.x);
+  fa_cold_slot(o.T, g, slots);
+#define PLUSS_FA_MAX(R) fa_max_tile<SRC, CHECK, P2, WK, R>(m, o, tmax, words, g, s_w, s_first, s_last)
+  switch (o.T.r) {
+    case C0: PLUSS_FA_MAX(C0); break;
+    case C1: PLUSS_FA_MAX(C1); break;
+    case A0: PLUSS_FA_MAX(A0); break;
+    case B0: PLUSS_FA_MAX(B0); break;
+    case C2: PLUSS_FA_MAX(C2); break;
+    default: PLUSS_FA_MAX(C3); break;
+  }
+#undef PLUSS_FA_MAX
+}
+
+// Generated lists: each lane generates its run of TI consecutive elements
+// (incremental key-order digits: keyrunf_* when the whole tile lies in block A
+// with small strata -- tile-uniform -- else one direct decode per sample), the
+// words go out through LDS (coalesced).  Instantiated per reference.
+template <bool P2, int WK, uint32_t REF>
+__device__ __forceinline__ void fa_gen_tile(const Model& m, const KeyGen& kg, const PkView& pv, const FaTile& T,
+                                            unsigned long long* __restrict__ tmax, void* words,
+                                            unsigned long long* s_w, void* s_wd_) {
+  using wk_t = typename std::conditional<WK == 8, unsigned long long, uint32_t>::type;
+  wk_t* s_wd = static_cast<wk_t*>(s_wd_);
+  constexpr int NW = TB / 64;
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
   const uint32_t e0 = threadIdx.x * TI;
   unsigned long long tm = 0;
-  FaCursor<SRC_GEN, P2> cur(m, a, T.r, T.base, e0 < T.mt ? e0 : 0u, nullptr, g);
+  if (keyrun_fast_ok(kg, T.base, TILE)) {  // the whole tile: every lane's run is in range
+    KeyRunF run;
+    keyrunf_start(kg, run, T.base + e0);
 #pragma unroll
-  for (int k = 0; k < TI; ++k) {
-    if (e0 + k < T.mt) {
-      const Elem e = cur.next();
+    for (int k = 0; k < TI; ++k) {
+      const Elem e = elem_of_digits<P2>(m, pv, REF, keyrunf_digits(kg, run));
+      keyrunf_next(kg, run);
       tm = e.sink > tm ? e.sink : tm;
       s_wd[fa_slot(e0 + k)] = (wk_t)e.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < TI; ++k) {
+      if (e0 + k < T.mt) {
+        const Elem e = elem_of_digits<P2>(m, pv, REF, keygen_digits_at(kg, T.base + e0 + k));
+        tm = e.sink > tm ? e.sink : tm;
+        s_wd[fa_slot(e0 + k)] = (wk_t)e.w;
+      }
     }
   }
   __syncthreads();
@@ -776,6 +865,33 @@ __global__ __launch_bounds__(TB) void k_fa_max_gen(Model m, FaRefs a, unsigned l
     for (int w = 0; w < NW; ++w) x = s_w[w] > x ? s_w[w] : x;
     tmax[blockIdx.x] = x;
   }
+}
+
+template <bool P2, int WK>
+__global__ __launch_bounds__(TB) void k_fa_max_gen(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
+                                                   void* words, unsigned long long* slots, GTable g) {
+  using wk_t = typename std::conditional<WK == 8, unsigned long long, uint32_t>::type;
+  __shared__ unsigned long long s_w[TB / 64];
+  __shared__ wk_t s_wd[FA_LDS];
+  const FaTile T = fa_tile(a, blockIdx.x);
+  fa_cold_slot(T, g, slots);
+  // (the reference's generator and view copied out first: the kernel argument
+  // itself is never passed down, which would put a copy of it in scratch)
+#define PLUSS_FA_GEN(R)                                               \
+  {                                                                   \
+    const KeyGen kg = a.kg[R];                                        \
+    const PkView pv = a.pv[R];                                        \
+    fa_gen_tile<P2, WK, R>(m, kg, pv, T, tmax, words, s_w, s_wd);     \
+  }
+  switch (T.r) {
+    case C0: PLUSS_FA_GEN(C0); break;
+    case C1: PLUSS_FA_GEN(C1); break;
+    case A0: PLUSS_FA_GEN(A0); break;
+    case B0: PLUSS_FA_GEN(B0); break;
+    case C2: PLUSS_FA_GEN(C2); break;
+    default: PLUSS_FA_GEN(C3); break;
+  }
+#undef PLUSS_FA_GEN
 }
 
 // One workgroup per reference: pmin[t] = max of tmax over the reference's
@@ -822,43 +938,31 @@ __global__ __launch_bounds__(PB) void k_fa_prefix(FaRefs a, const unsigned long 
 // LDS: a store through a generic pointer here would keep the kernels' FaRefs
 // argument copied to scratch.)
 constexpr int FPW = FPART + 2;
-template <int SRC>
+template <int SRC, int NT = TB, int EPT = TI>
 struct FaScanLds {
-  unsigned long long w[TB / 64], c[TB / 64], red[TB / 64][FPW], out[FPW];
-  fa_raw_t<SRC> raw[FA_LDS];
+  unsigned long long w[NT / 64], c[NT / 64], red[NT / 64][FPW], out[FPW];
+  fa_raw_t<SRC> raw[TILE + TILE / EPT];
 };
+// LDS slot of tile element e for runs of EPT elements per thread (one pad per run)
+template <int EPT>
+__device__ __forceinline__ uint32_t fa_slot_n(uint32_t e) { return e + e / EPT; }
 
-// the one reference a scanned tile belongs to (copied out of FaRefs by the
-// kernel, so the body never indexes the kernel argument itself)
-struct FaOne {
-  FaTile T;
-  uint64_t n;
-  const void* src;
-  PkView pv;
-};
-__device__ __forceinline__ FaOne fa_one(const FaRefs& a, uint64_t gt) {
-  FaOne o;
-  o.T = fa_tile(a, gt);
-  o.n = a.n[o.T.r];
-  o.src = a.src[o.T.r];
-  o.pv = a.pv[o.T.r];
-  return o;
-}
 
-template <int SRC, bool P2, bool CUT>
+template <int SRC, bool P2, bool CUT, int NT = TB, int EPT = TI>
 __device__ __forceinline__ void fa_tile_scan(const Model& m, const FaOne& o, unsigned long long carry_in,
-                                             uint64_t c_in, FaScanLds<SRC>& sh) {
+                                             uint64_t c_in, FaScanLds<SRC, NT, EPT>& sh) {
+  static_assert(NT * EPT == (int)TILE && EPT <= 16, "a tile is NT threads x EPT elements");
   static_assert(SRC == SRC_W32 || SRC == SRC_W64, "the scan reads packed words");
   using raw_t = fa_raw_t<SRC>;
-  constexpr int NW = TB / 64;
+  constexpr int NW = NT / 64;
   const FaTile& T = o.T;
   const bool full = T.mt == TILE;  // tile-uniform: no per-element bounds in the loops below
   {
     const raw_t* src = static_cast<const raw_t*>(o.src) + T.base;
 #pragma unroll
-    for (int k = 0; k < TI; ++k) {
-      const uint32_t e = (uint32_t)k * TB + threadIdx.x;
-      if (full || e < T.mt) sh.raw[fa_slot(e)] = src[e];
+    for (int k = 0; k < EPT; ++k) {
+      const uint32_t e = (uint32_t)k * NT + threadIdx.x;
+      if (full || e < T.mt) sh.raw[fa_slot_n<EPT>(e)] = src[e];
     }
     __syncthreads();
   }
@@ -866,24 +970,29 @@ __device__ __forceinline__ void fa_tile_scan(const Model& m, const FaOne& o, uns
   const uint64_t n = o.n;
   const unsigned long long endkey = m.A * m.T;
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  const uint32_t e0 = threadIdx.x * TI;                                       // this lane's run in the tile
-  const uint32_t nv = e0 < T.mt ? (T.mt - e0 < TI ? T.mt - e0 : TI) : 0u;  // its valid elements
+  const uint32_t e0 = threadIdx.x * EPT;                                      // this lane's run in the tile
+  const uint32_t nv = e0 < T.mt ? (T.mt - e0 < EPT ? T.mt - e0 : EPT) : 0u;  // its valid elements
   const uint64_t i0 = T.base + e0;                                            // index of its first element
   // ri*T per case (KEY_EMPTY: a cold case; case 3 = a malformed word, already flagged)
   unsigned long long rt[4];
 #pragma unroll
   for (int c = 0; c < 3; ++c) rt[c] = o.pv.ri[c] < 0 ? KEY_EMPTY : (unsigned long long)o.pv.ri[c] * m.T;
   rt[3] = KEY_EMPTY;
-  // decode: keys and sinks in registers, cases (2 bits) and tid == 0 (at bit 2k) per element
-  unsigned long long key[TI], snk[TI];
+  // decode: keys in registers, cases (2 bits) and tid == 0 (at bit 2k) per
+  // element; sinks are recomputed from key and case where needed (registers
+  // for occupancy: this pass waits on its tile loads)
+  unsigned long long key[EPT];
+  auto sink_of = [&](unsigned long long kk, uint32_t c) -> unsigned long long {
+    const unsigned long long d = c == 0 ? rt[0] : (c == 1 ? rt[1] : (c == 2 ? rt[2] : rt[3]));
+    return d == KEY_EMPTY ? KEY_EMPTY : kk + d;
+  };
   uint32_t cases = 0, t0s = 0;
   unsigned long long lmax = 0;
 #pragma unroll
-  for (int k = 0; k < TI; ++k) {
+  for (int k = 0; k < EPT; ++k) {
     key[k] = KEY_EMPTY;
-    snk[k] = 0;
     if (full || (uint32_t)k < nv) {
-      const raw_t w = sh.raw[fa_slot(e0 + k)];
+      const raw_t w = sh.raw[fa_slot_n<EPT>(e0 + k)];
       uint32_t c, t;
       unsigned long long kk;
       if (P2) {  // rank = ((q*N + c1)*N + c2)*T + tid; q*N + c1 < 2^32 (fa_run)
@@ -900,10 +1009,8 @@ __device__ __forceinline__ void fa_tile_scan(const Model& m, const FaOne& o, uns
         c = e.c;
         t = e.t0 ? 0u : 1u;
       }
-      const unsigned long long d = c == 0 ? rt[0] : (c == 1 ? rt[1] : (c == 2 ? rt[2] : rt[3]));
-      const unsigned long long sk = d == KEY_EMPTY ? KEY_EMPTY : kk + d;
+      const unsigned long long sk = sink_of(kk, c);
       key[k] = kk;
-      snk[k] = sk;
       lmax = sk > lmax ? sk : lmax;
       cases |= c << (2 * k);
       t0s |= (t == 0 ? 1u : 0u) << (2 * k);
@@ -933,7 +1040,7 @@ __device__ __forceinline__ void fa_tile_scan(const Model& m, const FaOne& o, uns
     unsigned long long run = carry;
     flags = 0;
 #pragma unroll
-    for (int k = 0; k < TI; ++k) {
+    for (int k = 0; k < EPT; ++k) {
       if (full || (uint32_t)k < nv) {
         const uint64_t p = i0 + k;
         bool f = key[k] > run;
@@ -949,7 +1056,8 @@ __device__ __forceinline__ void fa_tile_scan(const Model& m, const FaOne& o, uns
             tpos += run == KEY_EMPTY ? endkey : run;
           }
         }
-        run = snk[k] > run ? snk[k] : run;
+        const unsigned long long sk = sink_of(key[k], (cases >> (2 * k)) & 3u);
+        run = sk > run ? sk : run;
       }
     }
     if (rec && nv && i0 + nv == n && n <= lim) tpos += run == KEY_EMPTY ? endkey : run;  // the last element ends
@@ -973,7 +1081,7 @@ __device__ __forceinline__ void fa_tile_scan(const Model& m, const FaOne& o, uns
   if (CUT) {  // the first start j > 0 with j - before_j >= n - j; then the records below it
     unsigned long long best = KEY_EMPTY;
 #pragma unroll
-    for (int k = 0; k < TI; ++k) {
+    for (int k = 0; k < EPT; ++k) {
       const uint64_t j = i0 + k;
       const uint64_t before_j = c_in + lb + (uint64_t)__popc(flags & ((1u << k) - 1u));
       if (best == KEY_EMPTY && ((flags >> k) & 1u) && j > 0 && j - before_j >= n - j) best = j;
@@ -1037,31 +1145,40 @@ __global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigne
   if (threadIdx.x < FPW) part[blockIdx.x * (uint64_t)FPW + threadIdx.x] = sh.out[threadIdx.x];
 }
 
-// ---- pass 3, one workgroup per reference with samples: the exclusive sum of
-// its tiles' start counts locates the tile holding the Q1 cut (the first with
-// hmax >= n + starts before it); the tiles before it are summed whole, that
-// tile is scanned again with its incoming start count (CUT); then Q3 (nothing
-// dropped: the owner of the final largest sink stays in LAT, +1 cold if it is
-// tid 0), the -1 key (materialised even with 0, r10:196,671), traversed and
-// the (ref, case) bins.
+// ---- pass 3, one workgroup of FT threads per reference with samples: the
+// exclusive sum of its tiles' start counts locates the tile holding the Q1
+// cut (the first with hmax >= n + starts before it); the tiles before it are
+// summed whole, that tile is scanned again with its incoming start count
+// (CUT; FT threads x TILE/FT elements); then Q3 (nothing dropped: the owner
+// of the final largest sink stays in LAT, +1 cold if it is tid 0), the -1
+// key (materialised even with 0, r10:196,671), traversed and the bins.
+constexpr int FT = 1024;
 template <int SRC, bool P2>
-__global__ __launch_bounds__(TB) void k_fa_finish(Model m, FaRefs a, const unsigned long long* __restrict__ tmax,
+__global__ __launch_bounds__(FT) void k_fa_finish(Model m, FaRefs a, const unsigned long long* __restrict__ tmax,
                                                   const unsigned long long* __restrict__ pmin,
-                                                  const unsigned long long* __restrict__ part, GTable g) {
-  constexpr int NW = TB / 64;
-  __shared__ FaScanLds<SRC> sh;
-  __shared__ unsigned long long s_ct[2], s_red[NW][FPART];
+                                                  const unsigned long long* __restrict__ part,
+                                                  const unsigned long long* __restrict__ slots, GTable g) {
+  constexpr int NW = FT / 64;
+  __shared__ FaScanLds<SRC, FT, TILE / FT> sh;
+  __shared__ unsigned long long s_ct, s_red[NW][FPART];
   const uint32_t r = blockIdx.x;
   const uint64_t n = a.n[r];
   if (n == 0) return;
   const uint64_t t0 = a.toff[r], nt = a.toff[r + 1] - t0;
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  // 1. the cut tile
+  // read early (latency): the cold key's slot, the last tile's sinks (Q3)
+  const unsigned long long slot = slots[r];
+  const unsigned long long gl = tmax[t0 + nt - 1] > pmin[t0 + nt - 1] ? tmax[t0 + nt - 1] : pmin[t0 + nt - 1];
+  // 1. the cut tile, one tile per thread and chunk; the partials of the tiles
+  // before it are summed on the way
   uint64_t ct = nt, cin = 0, c = 0;
-  for (uint64_t b0 = 0; b0 < nt; b0 += TB) {
+  unsigned long long v[FPART] = {0, 0, 0, 0, 0};
+  for (uint64_t b0 = 0; b0 < nt; b0 += FT) {
     const uint64_t t = b0 + threadIdx.x;
-    const unsigned long long cnt = t < nt ? part[(t0 + t) * FPW + FPART] : 0ull;
-    const unsigned long long h = t < nt ? part[(t0 + t) * FPW + FPART + 1] : 0ull;
+    unsigned long long pw[FPW];
+#pragma unroll
+    for (int f = 0; f < FPW; ++f) pw[f] = t < nt ? part[(t0 + t) * FPW + f] : 0ull;
+    const unsigned long long cnt = pw[FPART], h = pw[FPART + 1];
     const unsigned long long inc = sc_wave_scan<false>(cnt, lane);
     if (lane == 63) sh.c[wid] = inc;
     __syncthreads();
@@ -1079,52 +1196,50 @@ __global__ __launch_bounds__(TB) void k_fa_finish(Model m, FaRefs a, const unsig
     unsigned long long best = KEY_EMPTY;
 #pragma unroll
     for (int x = 0; x < NW; ++x) best = sh.w[x] < best ? sh.w[x] : best;
+    if (best == KEY_EMPTY || t < best)
+#pragma unroll
+      for (int f = 0; f < FPART; ++f) v[f] += pw[f];
     if (best != KEY_EMPTY) {  // block-uniform
-      if (t == best) s_ct[0] = excl;
+      if (t == best) s_ct = excl;
       __syncthreads();
       ct = best;
-      cin = s_ct[0];
+      cin = s_ct;
       break;
     }
     c += tot;
     __syncthreads();  // sh.c / sh.w are rewritten by the next chunk
   }
-  // 2. the tiles before it, whole
-  unsigned long long v[FPART] = {0, 0, 0, 0, 0};
-  for (uint64_t t = threadIdx.x; t < ct; t += TB)
-#pragma unroll
-    for (int f = 0; f < FPART; ++f) v[f] += part[(t0 + t) * FPW + f];
 #pragma unroll
   for (int f = 0; f < FPART; ++f) {
     v[f] = sc_wave_red<false>(v[f]);
     if (lane == 0) s_red[wid][f] = v[f];
   }
-  // 3. the cut tile, below the cut
+  // 2. the cut tile, below the cut
   uint64_t cut = n;
   if (ct < nt) {
     __syncthreads();
     const FaOne o = fa_one(a, t0 + ct);
-    fa_tile_scan<SRC, P2, true>(m, o, pmin[t0 + ct], cin, sh);
+    fa_tile_scan<SRC, P2, true, FT, TILE / FT>(m, o, pmin[t0 + ct], cin, sh);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long tot[FPART] = {0, 0, 0, 0, 0};
-    for (int x = 0; x < NW; ++x)
-      for (int f = 0; f < FPART; ++f) tot[f] += s_red[x][f];
+  if (threadIdx.x < FPART) {  // one sum per thread, then plain no-return atomics
+    const uint32_t f = threadIdx.x;
+    unsigned long long x = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) x += s_red[w][f];
     if (ct < nt) {
-      for (int f = 0; f < FPART; ++f) tot[f] += sh.out[f];
+      x += sh.out[f];
       cut = sh.out[FPART];
     }
-    unsigned long long cold = tot[0];
-    if (cut == n) {
-      const uint64_t last = t0 + nt - 1;
-      const unsigned long long gm = tmax[last] > pmin[last] ? tmax[last] : pmin[last];
-      if (gm != KEY_EMPTY && gm % m.T == 0) cold += 1;
+    if (f == 0) {  // cold; Q3: +1 when nothing was cut and the final largest sink's owner is tid 0
+      const unsigned long long tid = P2 ? (gl & (m.T - 1)) : gl % m.T;
+      if (cut == n && gl != KEY_EMPTY && tid == 0) x += 1;
+      if (slot != ~0ull && x) atomicAdd(&g.counts[slot], x);
+    } else if (f == 1) {
+      atomicAdd(&g.trav[r], x);
+    } else if (x) {
+      atomicAdd(&g.bins[r * 3 + (f - 2)], x);
     }
-    g_add(g, make_key(r, 0, -1), cold);
-    g.trav[r] += tot[1];
-    for (int x = 0; x < 3; ++x)
-      if (tot[2 + x]) atomicAdd(&g.bins[r * 3 + x], tot[2 + x]);
   }
 }
 
@@ -1472,6 +1587,9 @@ static int fork_refs(pluss_ctx* ctx, const uint64_t* counts, hipStream_t s, F&& 
 // stream s.  Its buffers are the handle's (ctx->fb): tile maxima, prefixes
 // and per-tile partials, sized by the tiles of all references.
 static int fa_reserve(FaithfulBufs& b, uint64_t tiles, hipStream_t s) {
+  if (!b.fslot) {
+    if (int rc = grow(&b.fslot, 8)) return rc;
+  }
   if (tiles > b.dcap) {
     PLUSS_HIP_CHECK(hipStreamSynchronize(s));
     int rc = 0;
@@ -1525,13 +1643,14 @@ static int fa_run(pluss_ctx* ctx, FaRefs& a, int src, bool check, hipStream_t s)
 #define PLUSS_FA3(SRCV, CHK, P2V, WKV, SCANV)                                                                      \
   do {                                                                                                             \
     if constexpr (SRCV == SRC_GEN)                                                                                 \
-      hipLaunchKernelGGL((k_fa_max_gen<P2V, WKV>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.tmax, b.words, g);   \
+      hipLaunchKernelGGL((k_fa_max_gen<P2V, WKV>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.tmax, b.words, b.fslot, g);   \
     else                                                                                                           \
       hipLaunchKernelGGL((k_fa_max<SRCV, CHK, P2V, WKV>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.tmax, b.words, \
-                         g);                                                                                       \
+                         b.fslot, g);                                                                                       \
     hipLaunchKernelGGL(k_fa_prefix, dim3(6), dim3(PB), 0, s, a, b.tmax, b.pmin);                                   \
     hipLaunchKernelGGL((k_fa_scan<SCANV, P2V>), dim3((unsigned)t), dim3(TB), 0, s, m, aw, b.pmin, b.dpart, g);    \
-    hipLaunchKernelGGL((k_fa_finish<SCANV, P2V>), dim3(6), dim3(TB), 0, s, m, aw, b.tmax, b.pmin, b.dpart, g);    \
+    hipLaunchKernelGGL((k_fa_finish<SCANV, P2V>), dim3(6), dim3(FT), 0, s, m, aw, b.tmax, b.pmin, b.dpart, b.fslot, \
+                       g);    \
   } while (0)
 #define PLUSS_FA2(SRCV, CHK, WKV, SCANV)            \
   do {                                              \

@@ -67,6 +67,7 @@ struct FaithfulBufs {
   // running max entering it
   uint64_t dcap = 0;
   unsigned long long *dpart = nullptr, *tmax = nullptr, *pmin = nullptr;
+  unsigned long long* fslot = nullptr;  // per reference: the main-table slot of its -1 (cold) key
   void* words = nullptr;  // packed sort words written by the first pass (sample / generated sources)
   size_t words_bytes = 0;
 };
