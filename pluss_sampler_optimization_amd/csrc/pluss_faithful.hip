@@ -941,6 +941,7 @@ constexpr int FPW = FPART + 2;
 template <int SRC, int NT = TB, int EPT = TI>
 struct FaScanLds {
   unsigned long long w[NT / 64], c[NT / 64], red[NT / 64][FPW], out[FPW];
+  unsigned long long rt[4];  // ri*T per case (KEY_EMPTY: cold; case 3: malformed)
   fa_raw_t<SRC> raw[TILE + TILE / EPT];
 };
 // LDS slot of tile element e for runs of EPT elements per thread (one pad per run)
@@ -948,15 +949,21 @@ template <int EPT>
 __device__ __forceinline__ uint32_t fa_slot_n(uint32_t e) { return e + e / EPT; }
 
 
-template <int SRC, bool P2, bool CUT, int NT = TB, int EPT = TI>
-__device__ __forceinline__ void fa_tile_scan(const Model& m, const FaOne& o, unsigned long long carry_in,
-                                             uint64_t c_in, FaScanLds<SRC, NT, EPT>& sh) {
+template <int SRC, bool P2, bool CUT, int NT, int EPT, bool FULLT>
+__device__ __forceinline__ void fa_tile_scan_t(const Model& m, const FaOne& o, unsigned long long carry_in,
+                                               uint64_t c_in, FaScanLds<SRC, NT, EPT>& sh) {
   static_assert(NT * EPT == (int)TILE && EPT <= 16, "a tile is NT threads x EPT elements");
   static_assert(SRC == SRC_W32 || SRC == SRC_W64, "the scan reads packed words");
   using raw_t = fa_raw_t<SRC>;
   constexpr int NW = NT / 64;
   const FaTile& T = o.T;
-  const bool full = T.mt == TILE;  // tile-uniform: no per-element bounds in the loops below
+  constexpr bool full = FULLT;  // a whole tile: no per-element bounds in the loops below
+  // ri*T per case (KEY_EMPTY: a cold case; case 3 = a malformed word, already flagged)
+  unsigned long long rt[4];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) rt[c] = o.pv.ri[c] < 0 ? KEY_EMPTY : (unsigned long long)o.pv.ri[c] * m.T;
+  rt[3] = KEY_EMPTY;
+  if (threadIdx.x < 4) sh.rt[threadIdx.x] = rt[threadIdx.x & 3];
   {
     const raw_t* src = static_cast<const raw_t*>(o.src) + T.base;
 #pragma unroll
@@ -973,18 +980,14 @@ __device__ __forceinline__ void fa_tile_scan(const Model& m, const FaOne& o, uns
   const uint32_t e0 = threadIdx.x * EPT;                                      // this lane's run in the tile
   const uint32_t nv = e0 < T.mt ? (T.mt - e0 < EPT ? T.mt - e0 : EPT) : 0u;  // its valid elements
   const uint64_t i0 = T.base + e0;                                            // index of its first element
-  // ri*T per case (KEY_EMPTY: a cold case; case 3 = a malformed word, already flagged)
-  unsigned long long rt[4];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) rt[c] = o.pv.ri[c] < 0 ? KEY_EMPTY : (unsigned long long)o.pv.ri[c] * m.T;
-  rt[3] = KEY_EMPTY;
   // decode: keys in registers, cases (2 bits) and tid == 0 (at bit 2k) per
   // element; sinks are recomputed from key and case where needed (registers
   // for occupancy: this pass waits on its tile loads)
   unsigned long long key[EPT];
   auto sink_of = [&](unsigned long long kk, uint32_t c) -> unsigned long long {
-    const unsigned long long d = c == 0 ? rt[0] : (c == 1 ? rt[1] : (c == 2 ? rt[2] : rt[3]));
-    return d == KEY_EMPTY ? KEY_EMPTY : kk + d;
+    const unsigned long long d = sh.rt[c];  // an LDS table: no divergent selects
+    const unsigned long long x = kk + d;    // d == KEY_EMPTY wraps below d: the max keeps KEY_EMPTY
+    return x > d ? x : d;
   };
   uint32_t cases = 0, t0s = 0;
   unsigned long long lmax = 0;
@@ -1134,6 +1137,13 @@ __device__ __forceinline__ void fa_tile_scan(const Model& m, const FaOne& o, uns
     sh.out[f] = x;
   }
   __syncthreads();
+}
+
+template <int SRC, bool P2, bool CUT, int NT = TB, int EPT = TI>
+__device__ __forceinline__ void fa_tile_scan(const Model& m, const FaOne& o, unsigned long long carry_in,
+                                             uint64_t c_in, FaScanLds<SRC, NT, EPT>& sh) {
+  if (o.T.mt == TILE) fa_tile_scan_t<SRC, P2, CUT, NT, EPT, true>(m, o, carry_in, c_in, sh);
+  else fa_tile_scan_t<SRC, P2, CUT, NT, EPT, false>(m, o, carry_in, c_in, sh);
 }
 
 template <int SRC, bool P2>
