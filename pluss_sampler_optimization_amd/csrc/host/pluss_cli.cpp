@@ -6,6 +6,9 @@
 //   pluss_cli replay FILE     like `sample`, on a given list of "SAMPLE <REF> c0 c1 [c2]" lines
 //
 // opts: --n N --threads T --chunk CS --ds DS --cls CLS --seed S --total K --device D
+//       --trace FILE  (sample / replay) one line per sample: "ref c0 c1 c2 ri sink_key"
+//                     (the RI and sink the reference derives at r10:333/558; ri -1 = cold)
+//       --json FILE   the same results as one machine-readable JSON object
 // Output formats are the reference's (_pluss_histogram_print, pluss_print_mrc).
 #include <chrono>
 #include <cstdio>
@@ -71,12 +74,21 @@ struct Opts {
   pluss_cfg cfg{128, 4, 4, 8, 64, PLUSS_MODE_CLEAN, PLUSS_THR_R10, 0, 0};
   uint64_t seed = 0x5EED0001;
   uint64_t total = 0;  // 0: the reference's counts (164 / 2098 at any N)
+  std::string trace, json;
 };
 
 Opts parse(int argc, char** argv, int first) {
   Opts o;
   for (int i = first; i + 1 < argc; i += 2) {
     std::string k = argv[i];
+    if (k == "--trace") {
+      o.trace = argv[i + 1];
+      continue;
+    }
+    if (k == "--json") {
+      o.json = argv[i + 1];
+      continue;
+    }
     long long v = std::strtoll(argv[i + 1], nullptr, 0);
     if (k == "--n") o.cfg.n = v;
     else if (k == "--threads") o.cfg.threads = v;
@@ -88,6 +100,57 @@ Opts parse(int argc, char** argv, int first) {
     else if (k == "--device") o.cfg.device = (int32_t)v;
   }
   return o;
+}
+
+// ---- machine-readable output: {"histograms": {name: [[key, value], ...]}, "mrc": [[c, mr], ...], ...}
+std::string json_kv(const std::vector<pluss_kv>& v) {
+  std::ostringstream o;
+  o.precision(17);
+  o << "[";
+  for (size_t i = 0; i < v.size(); ++i) o << (i ? ", " : "") << "[" << v[i].key << ", " << v[i].value << "]";
+  o << "]";
+  return o.str();
+}
+
+void write_json(const std::string& path, const Opts& o, const char* mode,
+                const std::vector<std::pair<std::string, std::vector<pluss_kv>>>& hists, const std::vector<pluss_kv>& mrc,
+                const std::vector<uint64_t>& traversed, double seconds) {
+  std::ofstream f(path);
+  if (!f) {
+    std::cerr << "cannot write " << path << "\n";
+    std::exit(1);
+  }
+  f.precision(17);
+  f << "{\"mode\": \"" << mode << "\", \"n\": " << o.cfg.n << ", \"threads\": " << o.cfg.threads
+    << ", \"chunk\": " << o.cfg.chunk << ", \"ds\": " << o.cfg.ds << ", \"cls\": " << o.cfg.cls
+    << ", \"seconds\": " << seconds << ",\n \"histograms\": {";
+  for (size_t i = 0; i < hists.size(); ++i)
+    f << (i ? ",\n  " : "\n  ") << "\"" << hists[i].first << "\": " << json_kv(hists[i].second);
+  f << "},\n \"mrc\": " << json_kv(mrc) << ",\n \"traversed\": [";
+  for (size_t i = 0; i < traversed.size(); ++i) f << (i ? ", " : "") << traversed[i];
+  f << "]}\n";
+}
+
+// per-sample RI / sink dump (--trace)
+void write_trace(const std::string& path, const pluss_cfg& cfg, const std::vector<uint64_t>& samples) {
+  pluss_cfg c = cfg;
+  c.mode = PLUSS_MODE_CLEAN;
+  std::vector<int64_t> ri(samples.size());
+  std::vector<uint64_t> sink(samples.size());
+  if (!samples.empty())
+    if (int rc = pluss_gemm_sampled_ri(&c, samples.data(), samples.size(), ri.data(), sink.data()))
+      die("pluss_gemm_sampled_ri", rc);
+  std::ofstream f(path);
+  if (!f) {
+    std::cerr << "cannot write " << path << "\n";
+    std::exit(1);
+  }
+  const uint64_t M = (1ull << 20) - 1;
+  for (size_t i = 0; i < samples.size(); ++i) {
+    const uint64_t x = samples[i];
+    f << REFNAME[(x >> 60) & 7] << " " << ((x >> 40) & M) << " " << ((x >> 20) & M) << " " << (x & M) << " " << ri[i]
+      << " " << (int64_t)sink[i] << "\n";
+  }
 }
 
 double now() {
@@ -133,6 +196,8 @@ int run_acc(const Opts& o) {
   std::cout << text_hist("Start to dump reuse time", rih);
   std::cout << text_mrc(mrc);
   std::cout << "max iteration traversed\n" << trav << "\n\n";
+  if (!o.json.empty())
+    write_json(o.json, o, "acc", {{"noshare", vns}, {"share", vsh}, {"reuse", rih}}, mrc, {trav}, t1 - t0);
   return 0;
 }
 
@@ -193,6 +258,15 @@ int run_samplers(const Opts& o, const std::vector<uint64_t>* given) {
   uint64_t mx = 0;
   for (int r = 0; r < 6; ++r) mx = h.traversed[r] > mx ? h.traversed[r] : mx;
   std::cout << "max iteration traversed\n" << mx << "\n";
+  const double t1 = now();
+  if (!o.json.empty()) {
+    std::vector<std::pair<std::string, std::vector<pluss_kv>>> hs;
+    for (int r = 0; r < 6; ++r) hs.push_back({REFNAME[r], per[r]});
+    hs.push_back({"reuse", rih});
+    write_json(o.json, o, given ? "replay" : "sample", hs, mrc, std::vector<uint64_t>(h.traversed, h.traversed + 6),
+               t1 - t0);
+  }
+  if (!o.trace.empty()) write_trace(o.trace, cfg, samples);
   return 0;
 }
 

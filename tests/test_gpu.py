@@ -814,3 +814,35 @@ def test_environment_cannot_change_results(tmp_path):
         runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
     assert runs[0] == runs[1]
     assert sum(runs[0]["dense"][:P.DENSE_BINS]) == 300000
+
+
+@pytest.mark.parametrize("name,d,smp", GOLD[:2], ids=[g[0] for g in GOLD[:2]])
+def test_cli_trace_and_json(tmp_path, orc, name, d, smp):
+    """`pluss_cli replay --trace F --json J`: the trace has one line per sample
+    whose RI equals the stepping oracle's per-sample replay; the JSON holds the
+    same per-reference histograms, reuse histogram and MRC as the printout
+    (itself checked against the reference above) and the traversed counts."""
+    import json
+    import subprocess
+    f = tmp_path / "samples.txt"
+    rows = []
+    with open(f, "w") as fh:
+        for ref in orc.REFS:
+            for row in smp[ref]:
+                fh.write(f"SAMPLE {ref} {row[0]} {row[1]} {row[2]}\n")
+                rows.append((ref, int(row[0]), int(row[1]), int(row[2])))
+    tr, js = tmp_path / "trace.txt", tmp_path / "out.json"
+    out = subprocess.run([CLI, "replay", str(f), "--n", str(d["N"]), "--threads", str(d["T"]), "--trace", str(tr),
+                          "--json", str(js)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    j = json.load(open(js))
+    assert j["mode"] == "replay" and j["n"] == d["N"] and j["threads"] == d["T"]
+    for ref in ("C3", "C2", "A0", "C0", "B0", "C1"):
+        assert j["histograms"][ref] == d["printed"]["per_ref"][ref], ref
+    assert j["histograms"]["reuse"] == d["printed"]["reuse"]
+    assert max(j["traversed"]) == d["printed"]["max_traversed"]
+    lines = [l.split() for l in open(tr).read().splitlines()]
+    assert [(l[0], int(l[1]), int(l[2]), int(l[3])) for l in lines] == rows
+    packed = np.array([P.pack(r, a, b, c) for r, a, b, c in rows], dtype=np.uint64)
+    want = orc.clean_ri(orc.cfg(d["N"], d["T"]), packed)
+    assert [int(l[4]) for l in lines] == want.tolist()
