@@ -298,6 +298,51 @@ def faithful_bench(P, torch, device, stream):
     return out
 
 
+def faithful_config3_bench(P, torch, device, stream, reps=5):
+    """FAITHFUL mode (r10's queue semantics, bit-exact with the reference's
+    sampler_<REF> on the same sample list) at the headline shape: N=4096,
+    T=8, 2^28 samples on one GPU, six references concurrently.  sorted = the
+    key-order list resident in HBM, read once per pass (8 B per sample);
+    generated = the same lists generated inside the pass."""
+    N, T, total = 4096, 8, 1 << 28
+    counts = P.default_counts(N, total)
+    fcfg = P.SamplerConfig(n=N, threads=T, mode="faithful", device=device)
+    buf = torch.empty(total, dtype=torch.int64, device=torch.device("cuda", device))
+    sp = stream.cuda_stream
+    out = {"workload": "GEMM N=4096, T=8, 2^28 samples (config 3 on one GPU), faithful, six references",
+           "samples": total}
+    with P.Context(fcfg) as ctx:
+        off = 0
+        for r, c in enumerate(counts):
+            ctx.expand_sorted(SEED, r, c, 0, c, buf.data_ptr() + 8 * off, sp)
+            off += c
+        runs = {"sorted": lambda: ctx.faithful_hist_sorted_refs(buf.data_ptr(), counts, sp),
+                "generated": lambda: ctx.gen_faithful_refs(SEED, counts, sp)}
+        hs = {}
+        for name, run in runs.items():
+            ctx.reset(sp)
+            run()
+            torch.cuda.synchronize()
+            hs[name] = ctx.fetch()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                run()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            out[name] = {"ms": ms, "samples_per_s": total / (ms * 1e-3)}
+    del buf
+    assert hs["sorted"].bins == hs["generated"].bins and list(hs["sorted"].traversed) == list(hs["generated"].traversed)
+    ach = 8 * total / (out["sorted"]["ms"] * 1e-3) / 1e9
+    out["sorted"]["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                                 "note": "achieved = 8 B x samples / pass time (four launches, six references)"}
+    out["recorded"] = hs["sorted"].total() - sum(hs["sorted"].cold(r) for r in P.REFS)
+    out["traversed"] = list(hs["sorted"].traversed)
+    return out
+
+
 def end_to_end_bench(P, torch, cfg, counts, parts, stream, steps=20):
     """Sample generation inside the timed unit, as in r10 (r10:156-185 within the
     timer r10:3199): this rank's slices of the six key-order lists generated and
@@ -551,6 +596,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras:
         result["fulltrace"] = fulltrace_bench(P, torch, local, stream)
         result["faithful"] = faithful_bench(P, torch, local, stream)
+        try:  # a side line: its failure must not cost the headline line
+            result["faithful_config3"] = faithful_config3_bench(P, torch, local, stream)
+        except Exception as e:  # noqa: BLE001
+            result["faithful_config3"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         host = samples.cpu().numpy().view(np.uint64)
 

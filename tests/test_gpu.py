@@ -837,9 +837,16 @@ def test_cli_trace_and_json(tmp_path, orc, name, d, smp):
     assert out.returncode == 0, out.stderr
     j = json.load(open(js))
     assert j["mode"] == "replay" and j["n"] == d["N"] and j["threads"] == d["T"]
+    def same(got, printed):  # printed rows: key, value (6 significant digits), fraction
+        assert [k for k, _ in got] == [r[0] for r in printed]
+        assert np.allclose([v for _, v in got], [r[1] for r in printed], rtol=5e-6, atol=0)
+
     for ref in ("C3", "C2", "A0", "C0", "B0", "C1"):
-        assert j["histograms"][ref] == d["printed"]["per_ref"][ref], ref
-    assert j["histograms"]["reuse"] == d["printed"]["reuse"]
+        same(j["histograms"][ref], d["printed"]["per_ref"][ref])
+    same(j["histograms"]["reuse"], d["printed"]["reuse"])
+    mrc = dict((k, v) for k, v in j["mrc"])  # every printed (plateau-compressed) MRC row is in the JSON curve
+    for c, mr in d["printed"]["mrc"]:
+        assert c in mrc and abs(mrc[c] - mr) <= 5e-6 * max(abs(mr), 1e-6), (c, mr)
     assert max(j["traversed"]) == d["printed"]["max_traversed"]
     lines = [l.split() for l in open(tr).read().splitlines()]
     assert [(l[0], int(l[1]), int(l[2]), int(l[3])) for l in lines] == rows

@@ -120,7 +120,8 @@ def test_faithful_sorted_and_generated_equal_oracle(orc, N, T, per):
         assert h.bins == h_sorted.bins and list(h.traversed) == list(h_sorted.traversed)
 
 
-@pytest.mark.parametrize("N,T,total", [(1024, 8, 1 << 24), (4096, 8, 1 << 22), (2048, 64, 1 << 22)])
+@pytest.mark.parametrize("N,T,total", [(1024, 8, 1 << 24), (4096, 8, 1 << 22), (2048, 64, 1 << 22),
+                                       (4096, 8, 1 << 28)])  # the last: config 3's whole budget on one GPU
 def test_faithful_sorted_and_generated_at_baseline_shapes(N, T, total):
     """At BASELINE shapes (32-bit words at N=1024, 64-bit at 2048/4096) the
     three pipelines agree: no-sort over the materialised key-order list,
