@@ -183,6 +183,43 @@ def faithful_key_space(cfg):
     return int(out.value)
 
 
+def faithful_key(cfg, sample):
+    """The faithful-mode sort key a*T + tid of one packed sample (r10's pop
+    order, IterationComp, pluss_utils.h:175-267): a = q*R + c1*S + off is the
+    sample's thread-local position (S = 4N+2, R = N*S, q its thread-local row,
+    off C0:0 C1:1 A0:2+4c2 B0:3+4c2 C2:4+4c2 C3:5+4c2).  Needs N % (CS*T) == 0
+    (the lockstep interleaving order faithful mode requires)."""
+    x = int(sample)
+    ref, c0, c1, c2 = x >> 60, (x >> 40) & 0xFFFFF, (x >> 20) & 0xFFFFF, x & 0xFFFFF
+    N, T, CS = cfg.n, cfg.threads, cfg.chunk
+    S = 4 * N + 2
+    k = c0 // CS
+    tid, q = k % T, (k // T) * CS + c0 % CS
+    off = ref if ref < 2 else ref + 4 * c2
+    return ((q * N + c1) * S + off) * T + tid
+
+
+def keyorder_index_range(cfg, seed, ref, total, key_lo, key_hi, sample_at=None):
+    """[i_lo, i_hi): the samples of the key-order list (expand_sorted, keys
+    strictly increasing in the index) whose faithful keys lie in
+    [key_lo, key_hi) -- two binary searches, one host sample per probe
+    (sample_at(i) -> packed sample i; default: expand_sorted)."""
+    if sample_at is None:
+        def sample_at(i):
+            return expand_sorted(cfg, seed, ref, total, i, 1)[0]
+
+    def first_at_least(key):
+        lo, hi = 0, total
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if faithful_key(cfg, sample_at(mid)) >= key:
+                hi = mid
+            else:
+                lo = mid + 1
+        return lo
+    return first_at_least(key_lo), first_at_least(key_hi)
+
+
 def dense_keys(cfg):
     """Keys of the PLUSS_DENSE_BINS dense bins (bin = ref*3 + case) of a shape with N % (cls/ds) == 0."""
     out = (ctypes.c_uint64 * DENSE_BINS)()

@@ -26,7 +26,8 @@ the scan state across shards (include/pluss_gpu.h, pluss_dev_faithful_shard_*).
 import numpy as np
 
 from ._lib import DENSE_BINS, PlussError
-from .api import REFS, Context, Histogram, faithful_key_space, hist_from_dense, hist_from_tables
+from .api import (REFS, Context, Histogram, faithful_key_space, hist_from_dense, hist_from_tables,
+                  keyorder_index_range)
 
 TABLE_CAP = 4096
 KEY_EMPTY = (1 << 64) - 1
@@ -204,6 +205,44 @@ def sharded_faithful_hist(cfg, samples_by_ref, group=None, stream=None):
         ctx.reset(sp)
         for ref, t in samples_by_ref.items():
             faithful_shard_protocol(ctx, ref, t.data_ptr(), t.numel(), lo, hi, rank, ag, sp)
+        ctx.export(keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
+        torch.cuda.synchronize(dev)
+        trav = ctx.fetch().traversed
+    tsum = [sum(col) % (1 << 64) for col in zip(*ag(trav))]
+    if not nccl:
+        keys, cnts = keys.cpu(), cnts.cpu()
+    h = allgather_tables(keys, cnts, group)
+    return Histogram(h.bins, tsum)
+
+
+def sharded_faithful_gen_hist(cfg, seed, totals, group=None, stream=None):
+    """Faithful mode over key-range shards of the key-order lists
+    (pluss_dev_expand_sorted's lists of totals[r] samples): each rank
+    generates only the samples whose keys fall in its range -- an index slice,
+    since the lists are in key order and random access -- so no rank reads or
+    holds the whole list; then the same four-phase protocol as
+    sharded_faithful_hist.  Returns the merged Histogram (identical on every
+    rank)."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    nccl = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", cfg.device)
+    ag = torch_allgather(group, dev if nccl else "cpu")
+    lo, hi = key_range(faithful_key_space(cfg), rank, world)
+    sp = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    keys = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
+    cnts = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
+    slices = [keyorder_index_range(cfg, seed, r, int(t), lo, hi) if t else (0, 0) for r, t in enumerate(totals)]
+    buf = torch.empty(max([b - a for a, b in slices] + [1]), dtype=torch.int64, device=dev)
+    with Context(cfg) as ctx:
+        ctx.reset(sp)
+        for ref, (t, (a, b)) in enumerate(zip(totals, slices)):
+            if t == 0:
+                continue
+            if b > a:
+                ctx.expand_sorted(seed, ref, int(t), a, b - a, buf.data_ptr(), sp)
+            faithful_shard_protocol(ctx, ref, buf.data_ptr(), b - a, lo, hi, rank, ag, sp)
         ctx.export(keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
         torch.cuda.synchronize(dev)
         trav = ctx.fetch().traversed

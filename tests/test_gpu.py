@@ -853,3 +853,48 @@ def test_cli_trace_and_json(tmp_path, orc, name, d, smp):
     packed = np.array([P.pack(r, a, b, c) for r, a, b, c in rows], dtype=np.uint64)
     want = orc.clean_ri(orc.cfg(d["N"], d["T"]), packed)
     assert [int(l[4]) for l in lines] == want.tolist()
+
+
+def _faith_gen_dist_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import torch.distributed as dist
+    import pluss_sampler_optimization_amd as P2
+    from pluss_sampler_optimization_amd import dist as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = P2.SamplerConfig(n=512, threads=8, mode="faithful")
+    h = D.sharded_faithful_gen_hist(c, 0x5EED0001, P2.default_counts(512, 1 << 20))
+    q.put((rank, h.bins, h.traversed))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_faithful_generated_lists_on_one_gpu(world):
+    """dist.sharded_faithful_gen_hist: each rank generates only the slice of the
+    key-order lists inside its key range (no rank holds a whole list), the
+    four-phase shard protocol over gloo; equals one GPU's gen_faithful_refs."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_faith_gen_dist_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    c = P.SamplerConfig(n=512, threads=8, mode="faithful")
+    with P.Context(c) as one:
+        one.gen_faithful_refs(0x5EED0001, P.default_counts(512, 1 << 20))
+        want = one.fetch()
+    for _, bins, trav in res:
+        assert bins == want.bins
+        assert list(trav) == list(want.traversed)

@@ -274,3 +274,29 @@ def test_div64_round_up_divider(model_host):
         for n in ns + [d - 1, d, d + 1, 2 * d - 1]:
             n &= (1 << 64) - 1
             assert L.mh_div64(n, d) == n // d, (n, d)
+
+
+@pytest.mark.parametrize("N,T,CS", [(64, 4, 4), (96, 3, 4), (1024, 8, 4), (4096, 8, 4), (2048, 64, 4)])
+def test_keyorder_index_range_selects_a_key_range(orc, N, T, CS):
+    """faithful_key (the host key of dist.sharded_faithful_gen_hist) equals the
+    oracle's sort key; keyorder_index_range's binary searches over a key-order
+    list give exactly the indices whose keys fall in the range (what a rank of
+    the generated-list faithful shards generates)."""
+    import pluss_sampler_optimization_amd as P
+    c = orc.cfg(N, T, CS)
+    pc = P.SamplerConfig(n=N, threads=T, chunk=CS, mode="faithful")
+    for ref in range(6):
+        tot = min(3000, (N - 1) ** (3 if ref >= 2 else 2))
+        s = orc.expand_sorted(c, 0x5EED0003, ref, tot, 0, tot)
+        key = orc.sort_key(N, T, CS, s)
+        assert [P.faithful_key(pc, x) for x in s] == [int(k) for k in key]
+        at = lambda i: s[i]  # noqa: E731
+        hi_key = int(key[-1]) + 1
+        for lo, hi in ((0, hi_key), (hi_key // 3, 2 * hi_key // 3), (int(key[7]), int(key[7]) + 1),
+                       (int(key[7]) + 1, int(key[8])), (hi_key, 2 * hi_key)):
+            a, b = P.keyorder_index_range(pc, 0, ref, tot, lo, hi, sample_at=at)
+            inside = np.nonzero((key >= lo) & (key < hi))[0]
+            if len(inside):
+                assert (a, b) == (inside[0], inside[-1] + 1)
+            else:
+                assert a == b
