@@ -350,9 +350,18 @@ def faithful_config3_bench(P, torch, device, stream, reps=5):
     del buf
     assert hs["sorted"].bins == hs["generated"].bins and list(hs["sorted"].traversed) == list(hs["generated"].traversed)
     ach = 8 * total / (out["sorted"]["ms"] * 1e-3) / 1e9
+    traffic = None  # HBM bytes per pass from the committed PMC summary (tools/gpu_pmc_faithful.sh, PROF_SHAPE=config3)
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_faithful_config3.json")))
+        if d.get("samples_per_pass") == total:
+            traffic = d.get("hbm_bytes_per_pass")
+    except (OSError, ValueError):
+        pass
     out["sorted"]["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": ach / HBM_PEAK_GBS, "traffic": None,
-                                 "note": "achieved = 8 B x samples / pass time (four launches, six references)"}
+                                 "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+                                 "note": "achieved = 8 B x samples / pass time (four launches, six references); "
+                                         "traffic = samples read + 8 B words written by the first launch and read "
+                                         "by the scan"}
     out["recorded"] = hs["sorted"].total() - sum(hs["sorted"].cold(r) for r in P.REFS)
     out["traversed"] = list(hs["sorted"].traversed)
     return out

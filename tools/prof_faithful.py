@@ -16,9 +16,10 @@ dev = torch.device("cuda", 0)
 s = torch.cuda.Stream(dev)
 torch.cuda.set_stream(s)
 sp = s.cuda_stream
-cfg = P.SamplerConfig(n=1024, threads=8, mode="faithful")
-total = 1 << 24
-counts = P.default_counts(1024, total)
+# PROF_SHAPE=config3: N=4096, T=8, 2^28 samples (the headline shape on one GPU)
+N, total = (4096, 1 << 28) if os.environ.get("PROF_SHAPE") == "config3" else (1024, 1 << 24)
+cfg = P.SamplerConfig(n=N, threads=8, mode="faithful")
+counts = P.default_counts(N, total)
 buf = torch.empty(total, dtype=torch.int64, device=dev)
 ctx = P.Context(cfg)
 off = 0
