@@ -898,3 +898,48 @@ def test_sharded_faithful_generated_lists_on_one_gpu(world):
     for _, bins, trav in res:
         assert bins == want.bins
         assert list(trav) == list(want.traversed)
+
+
+def _random_shapes(seed, k):
+    """k random GEMM shapes (fixed seed): N, T, CS, DS, CLS with CLS a multiple
+    of DS; faithful ones also with N % (CS*T) == 0."""
+    rng = np.random.default_rng(seed)
+    out = []
+    while len(out) < k:
+        T = int(rng.choice([1, 2, 3, 4, 5, 8, 16]))
+        CS = int(rng.choice([1, 2, 3, 4, 8]))
+        DS = int(rng.choice([4, 8]))
+        CLS = DS * int(rng.choice([1, 2, 4, 8, 16]))
+        N = int(rng.integers(8, 200))
+        if len(out) % 2:  # every other shape in r10's lockstep order (faithful mode too)
+            N = CS * T * max(1, N // (CS * T))
+        if N // (CS * T) < 1 or N < 8:
+            continue
+        out.append((N, T, CS, DS, CLS))
+    return out
+
+
+RANDOM_SHAPES = _random_shapes(20261017, 24)
+
+
+@pytest.mark.parametrize("shape", RANDOM_SHAPES, ids=[str(s) for s in RANDOM_SHAPES])
+def test_random_shapes_clean_and_faithful_equal_oracle(orc, shape):
+    """A fixed-seed sweep of random shapes (any N, T, CS, DS, CLS; lines that
+    span rows; N % (CS*T) != 0): clean mode == the stepping oracle's per-sample
+    replay histogram; where N % (CS*T) == 0 (r10's lockstep order), faithful
+    mode == the oracle's r10 sampler on the same lists, with traversed."""
+    N, T, CS, DS, CLS = shape
+    c = cfg(N, T, CS, DS, CLS)
+    span = N - 1
+    per = [min(800, span ** (2 if r < 2 else 3)) for r in range(6)]
+    s = np.concatenate([P.expand_samples(c, 0x5EED0100 + N, r, 0, n) for r, n in enumerate(per) if n > 0])
+    oc = orc.cfg(N, T, CS, DS, CLS)
+    assert P.sampled_hist(c, s).bins == oracle_clean_hist(orc, oc, s)
+    if N % (CS * T) == 0:
+        cf = cfg(N, T, CS, DS, CLS, mode="faithful")
+        h = P.sampled_hist(cf, s)
+        for ref in orc.REFS:
+            part = s[(s >> np.uint64(60)) == np.uint64(P.REF_ID[ref])]
+            want, trav = orc.faithful(oc, ref, part)
+            assert {k: v for k, v in h.bins.items() if k[0] == ref} == want, (shape, ref)
+            assert h.traversed[P.REF_ID[ref]] == trav, (shape, ref)
