@@ -17,7 +17,7 @@ Run on an MI355X:  python -m pytest tests -m gpu -x -q
 import numpy as np
 import pytest
 
-from conftest import closed_form_counts, edge_samples_gemm, oracle_subset
+from conftest import closed_form_counts, closed_form_ri, edge_samples_gemm, oracle_subset
 
 pytestmark = pytest.mark.gpu
 
@@ -153,3 +153,54 @@ def test_faithful_large_n_vs_oracle(orc, N, T, refs):
         want, trav = orc.faithful(oc, ref, s)
         assert {k: v for k, v in h.bins.items() if k[0] == ref} == want, (N, ref)
         assert h.traversed[P.REF_ID[ref]] == trav, (N, ref)
+
+
+def test_largest_n_clean_and_faithful():
+    """The largest N the 20-bit sample fields allow (N = 2^20 - 32, T=8, CS=4):
+    thread-local positions near 2^42, B0 reuses near 2^42 accesses, faithful
+    sort keys near 2^62 and 62-bit packed words.  Clean mode and the per-sample
+    RI dump equal the closed forms sample by sample; faithful mode
+    gives one histogram from the key-order list (no sort), the generated lists
+    and the radix path over a shuffled copy."""
+    N, T, CS = (1 << 20) - 32, 8, 4
+    c = P.SamplerConfig(n=N, threads=T, chunk=CS)
+    per = 40000
+    s = np.concatenate([P.expand_samples(c, 0x5EED0042, r, 0, per) for r in range(6)])
+    m = np.uint64(0xFFFFF)
+    refs = (s >> np.uint64(60)).astype(np.int64)
+    c0, c1, c2 = [((s >> np.uint64(sh)) & m).astype(np.int64) for sh in (40, 20, 0)]
+    want_ri = closed_form_ri(N, T, CS, 8, refs, c0, c1, c2)
+    ri, _ = P.sampled_ri(c, s)
+    np.testing.assert_array_equal(ri, want_ri)
+    S = 4 * N + 2
+    kind = ((refs == 3) & (want_ri > 0) & (2 * want_ri > S * N)).astype(np.int64)
+    want = {}
+    for r, k, x in zip(refs.tolist(), kind.tolist(), want_ri.tolist()):
+        key = (P.REFS[r], k, x)
+        want[key] = want.get(key, 0) + 1
+    assert P.sampled_hist(c, s).bins == want
+    # faithful: three sources, one histogram
+    cf = P.SamplerConfig(n=N, threads=T, chunk=CS, mode="faithful")
+    totals = [per] * 6
+    buf = torch.empty(6 * per, dtype=torch.int64, device="cuda")
+    with P.Context(cf) as ctx:
+        for r in range(6):
+            ctx.expand_sorted(0x5EED0042, r, per, 0, per, buf.data_ptr() + 8 * r * per, stream())
+        rng = np.random.default_rng(5)
+        host = buf.cpu().numpy()
+        shuf = np.concatenate([host[r * per:(r + 1) * per][rng.permutation(per)] for r in range(6)])
+        ts = torch.from_numpy(shuf).cuda()
+        hs = []
+        for run in (lambda: ctx.faithful_hist_sorted_refs(buf.data_ptr(), totals, stream()),
+                    lambda: ctx.gen_faithful_refs(0x5EED0042, totals, stream()),
+                    lambda: ctx.faithful_hist_refs(ts.data_ptr(), totals, stream())):
+            ctx.reset(stream())
+            run()
+            hs.append(ctx.fetch())
+    for h in hs[1:]:
+        assert h.bins == hs[0].bins and list(h.traversed) == list(hs[0].traversed)
+    assert 0 < hs[0].total() <= 6 * per + 6
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
