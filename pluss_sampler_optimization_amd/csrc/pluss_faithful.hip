@@ -1179,11 +1179,72 @@ __global__ __launch_bounds__(FT) void k_fa_finish(Model m, FaRefs a, const unsig
   // read early (latency): the cold key's slot, the last tile's sinks (Q3)
   const unsigned long long slot = slots[r];
   const unsigned long long gl = tmax[t0 + nt - 1] > pmin[t0 + nt - 1] ? tmax[t0 + nt - 1] : pmin[t0 + nt - 1];
-  // 1. the cut tile, one tile per thread and chunk; the partials of the tiles
-  // before it are summed on the way
+  // 1. the cut tile; the partials of the tiles before it are summed on the way
   uint64_t ct = nt, cin = 0, c = 0;
   unsigned long long v[FPART] = {0, 0, 0, 0, 0};
-  for (uint64_t b0 = 0; b0 < nt; b0 += FT) {
+  if (nt > FT) {  // many tiles (2^24+ samples per reference): each thread a contiguous run of them
+    const uint64_t per = (nt + FT - 1) / FT;
+    const uint64_t lo = threadIdx.x * per < nt ? threadIdx.x * per : nt, hi = lo + per < nt ? lo + per : nt;
+    const unsigned long long* pt = part + t0 * FPW;
+    constexpr int FB = 8;  // loads of a batch in flight together
+    unsigned long long cs = 0;
+    for (uint64_t t = lo; t < hi; t += FB) {
+      unsigned long long x[FB];
+#pragma unroll
+      for (int k = 0; k < FB; ++k) x[k] = t + k < hi ? pt[(t + k) * FPW + FPART] : 0ull;
+#pragma unroll
+      for (int k = 0; k < FB; ++k) cs += x[k];
+    }
+    const unsigned long long inc = sc_wave_scan<false>(cs, lane);
+    if (lane == 63) sh.c[wid] = inc;
+    __syncthreads();
+    unsigned long long run = inc - cs;
+#pragma unroll
+    for (int x = 0; x < NW; ++x)
+      if (x < (int)wid) run += sh.c[x];
+    unsigned long long hit = KEY_EMPTY, hcin = 0;
+    for (uint64_t t = lo; t < hi; t += FB) {
+      unsigned long long x[FB], h[FB];
+#pragma unroll
+      for (int k = 0; k < FB; ++k) {
+        x[k] = t + k < hi ? pt[(t + k) * FPW + FPART] : 0ull;
+        h[k] = t + k < hi ? pt[(t + k) * FPW + FPART + 1] : 0ull;
+      }
+#pragma unroll
+      for (int k = 0; k < FB; ++k) {
+        if (hit == KEY_EMPTY && t + k < hi && h[k] >= n + run) {
+          hit = t + k;
+          hcin = run;
+        }
+        run += x[k];
+      }
+    }
+    const unsigned long long cand = sc_wave_red_min(hit);
+    if (lane == 0) sh.w[wid] = cand;
+    __syncthreads();
+    unsigned long long best = KEY_EMPTY;
+#pragma unroll
+    for (int x = 0; x < NW; ++x) best = sh.w[x] < best ? sh.w[x] : best;
+    if (best != KEY_EMPTY && hit == best) s_ct = hcin;
+    __syncthreads();
+    if (best != KEY_EMPTY) {  // block-uniform
+      ct = best;
+      cin = s_ct;
+    }
+    const uint64_t hi2 = hi < ct ? hi : ct;
+    for (uint64_t t = lo; t < hi2; t += FB / 2) {
+      unsigned long long x[FB / 2][FPART];
+#pragma unroll
+      for (int k = 0; k < FB / 2; ++k)
+#pragma unroll
+        for (int f = 0; f < FPART; ++f) x[k][f] = t + k < hi2 ? pt[(t + k) * FPW + f] : 0ull;
+#pragma unroll
+      for (int k = 0; k < FB / 2; ++k)
+#pragma unroll
+        for (int f = 0; f < FPART; ++f) v[f] += x[k][f];
+    }
+  } else
+  for (uint64_t b0 = 0; b0 < nt; b0 += FT) {  // one chunk: one tile per thread
     const uint64_t t = b0 + threadIdx.x;
     unsigned long long pw[FPW];
 #pragma unroll

@@ -538,10 +538,13 @@ def test_faithful_key_range_shards_equal_reference_dumps(orc, name, d, smp):
         assert trav[P.REF_ID[ref]] == etrav, (name, ref)
 
 
-@pytest.mark.parametrize("N,T,per,nshards", [(128, 8, 20000, 2), (256, 4, 60000, 5), (64, 2, 30000, 8)])
+@pytest.mark.parametrize("N,T,per,nshards", [(128, 8, 20000, 2), (256, 4, 60000, 5), (64, 2, 30000, 8),
+                                             (1024, 8, 5000000, 2)])
 def test_faithful_key_range_shards_equal_one_gpu(N, T, per, nshards):
     """Longer lists (many replays, Q1 drops, cold samples): the sharded phases
-    equal one-handle faithful mode exactly, traversed included."""
+    equal one-handle faithful mode exactly, traversed included.  The last case
+    gives the 3-D references 1221 tiles each (the finish kernel's many-tile
+    path), checked against the independent shard kernels."""
     torch = pytest.importorskip("torch")
     c = cfg(N, T, mode="faithful")
     ks = P.faithful_key_space(c)
