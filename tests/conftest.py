@@ -188,6 +188,53 @@ def oracle_subset(N, T, CS, samples, budget_steps, W=8, seed=0):
     return s[keep]
 
 
+def _key_sorted(N, T, CS, s):
+    import oracle as orc
+    return s[np.argsort(orc.sort_key(N, T, CS, s), kind="stable")]
+
+
+def window_list(N, T, CS, ref, n, qs, c1_hi, seed):
+    """Up to n distinct samples of `ref` drawn uniformly from a window of the
+    iteration space -- the rows with thread-local row index q in `qs` (every
+    simulated thread), c1 < c1_hi for 3-D references, every c2 -- in key order.
+    Dense windows make r10's replays chain across many samples (and scan
+    tiles) while the stepping oracle's cost stays bounded by the window's key
+    span (cold B0 samples only in a thread's last row q = N/T - 1)."""
+    import oracle as orc
+    rng = np.random.default_rng(seed)
+    rid = orc.REF_ID[ref]
+    span = N - 1  # rand() % (N-1) (Q4)
+    c0s = np.array([c for c in (((q // CS) * T + t) * CS + q % CS for q in qs for t in range(T)) if c < span],
+                   np.int64)
+    dims = (len(c0s), span) if rid < 2 else (len(c0s), min(c1_hi, span), span)
+    tot = int(np.prod(dims))
+    idx = rng.choice(tot, size=min(n, tot), replace=False)
+    pts = np.unravel_index(idx, dims)
+    arr = np.stack([c0s[pts[0]]] + [np.asarray(p, np.int64) for p in pts[1:]], 1)
+    return _key_sorted(N, T, CS, orc.pack_array(ref, arr))
+
+
+def all_tids_list(N, T, CS, ref, points, qs, seed):
+    """`points` distinct (q, c1, c2) points of the rows `qs`, each sampled by
+    every simulated thread (T samples per point, adjacent keys): every replay
+    meets the other T-1 threads' samples, so r10's Q1 exit fires about half way
+    through the list.  Key order."""
+    import oracle as orc
+    rng = np.random.default_rng(seed)
+    span = N - 1
+    dims = (len(qs), span, span) if orc.REF_ID[ref] >= 2 else (len(qs), span)
+    idx = rng.choice(int(np.prod(dims)), size=points, replace=False)
+    pts = np.unravel_index(idx, dims)
+    q = np.asarray(qs, np.int64)[pts[0]]
+    rows = []
+    for t in range(T):
+        c0 = ((q // CS) * T + t) * CS + q % CS
+        rows.append(np.stack([c0] + [np.asarray(p, np.int64) for p in pts[1:]], 1))
+    arr = np.concatenate(rows)
+    arr = arr[arr[:, 0] < span]
+    return _key_sorted(N, T, CS, orc.pack_array(ref, arr))
+
+
 @pytest.fixture(autouse=True)
 def _torch_stream(request):
     """GPU tests run with a dedicated (non-null) torch stream as the current
