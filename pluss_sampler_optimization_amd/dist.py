@@ -91,19 +91,19 @@ def sharded_clean_hist(cfg, seed, counts, group=None, stream=None):
     keys = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
     cnts = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
     sp = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    err = None
     with Context(cfg) as ctx:
-        off = 0
-        for ref, (first, c) in zip(range(len(REFS)), parts):
-            ctx.expand(seed, ref, first, c, samples.data_ptr() + 8 * off, sp)
-            off += c
-        ctx.reset(sp)
-        ctx.sampled_hist(samples.data_ptr(), n, sp)
-        ctx.export(keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
-        torch.cuda.synchronize(dev)
-        err = None
-        try:
+        try:  # any failure of the local pass is raised on every rank, before the exchange
+            off = 0
+            for ref, (first, c) in zip(range(len(REFS)), parts):
+                ctx.expand(seed, ref, first, c, samples.data_ptr() + 8 * off, sp)
+                off += c
+            ctx.reset(sp)
+            ctx.sampled_hist(samples.data_ptr(), n, sp)
+            ctx.export(keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
+            torch.cuda.synchronize(dev)
             ctx.fetch()  # the handle's flags: malformed samples, table or export overflow
-        except PlussError as e:
+        except Exception as e:  # noqa: BLE001
             err = e
     gloo = dist.get_backend(group) == "gloo"  # e.g. several ranks sharing one GPU in tests
     raise_together(err, group, None if gloo else dev)
@@ -132,14 +132,20 @@ def sharded_clean_dense(cfg, seed, counts, group=None, stream=None):
     samples = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
     dense = torch.zeros(DENSE_BINS + 1, dtype=torch.int64, device=dev)
     sp = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    err = None
     with Context(cfg) as ctx:
-        off = 0
-        for ref, (first, c) in zip(range(len(REFS)), parts):
-            ctx.expand(seed, ref, first, c, samples.data_ptr() + 8 * off, sp)
-            off += c
-        ctx.sampled_hist_dense(samples.data_ptr(), n, dense.data_ptr(), sp)
-        torch.cuda.synchronize(dev)
-    if dist.get_backend(group) == "gloo":  # e.g. several ranks sharing one GPU in tests
+        try:  # a failed local pass raises on every rank, before the all-reduce
+            off = 0
+            for ref, (first, c) in zip(range(len(REFS)), parts):
+                ctx.expand(seed, ref, first, c, samples.data_ptr() + 8 * off, sp)
+                off += c
+            ctx.sampled_hist_dense(samples.data_ptr(), n, dense.data_ptr(), sp)
+            torch.cuda.synchronize(dev)
+        except Exception as e:  # noqa: BLE001
+            err = e
+    gloo = dist.get_backend(group) == "gloo"  # e.g. several ranks sharing one GPU in tests
+    raise_together(err, group, None if gloo else dev)
+    if gloo:
         dense = dense.cpu()
     v = allreduce_dense(dense, group).cpu().numpy()
     if v[DENSE_BINS]:
@@ -166,23 +172,59 @@ def torch_allgather(group=None, device=None):
     return allgather
 
 
-def faithful_shard_protocol(shard, ref, d_samples, n, key_lo, key_hi, rank, allgather, stream=None):
+def faithful_shard_protocol(shard, ref, d_samples, n, key_lo, key_hi, rank, allgather, stream=None, err=None):
     """The four phases of a key-range-sharded faithful sampler on `shard` (a
     Context, or any object with the same faithful_shard_* methods), exchanging
-    the per-shard summaries with `allgather`.  Returns (n_total, cut)."""
-    m, first, mx = shard.faithful_shard_keys(ref, d_samples, n, key_lo, key_hi, stream)
-    g = allgather([m, first, mx])
+    the per-shard summaries with `allgather`.  Returns (n_total, cut).
+
+    Every exchange carries an error word: a rank whose phase raised (or that
+    enters with `err`, e.g. from generating its slice) still takes part in the
+    exchange, and then every rank raises at that same exchange -- no rank is
+    left waiting in a later collective."""
+    def exchange(vals):
+        nonlocal err
+        g = allgather([1 if err is not None else 0] + list(vals))
+        if err is not None:
+            raise err
+        if any(x[0] for x in g):
+            raise PlussError("another rank's faithful shard pass failed")
+        return [x[1:] for x in g]
+
+    def phase(fn, *args, default):
+        nonlocal err
+        if err is not None:
+            return default
+        try:
+            return fn(*args)
+        except Exception as e:  # noqa: BLE001 -- re-raised at the next exchange, on every rank
+            err = e
+            return default
+    m, first, mx = phase(shard.faithful_shard_keys, ref, d_samples, n, key_lo, key_hi, stream,
+                         default=(0, KEY_EMPTY, 0))
+    g = exchange([m, first, mx])
     j_off = sum(x[0] for x in g[:rank])
     n_total = sum(x[0] for x in g)
     pmax_in = max([x[2] for x in g[:rank] if x[0] > 0], default=0)
     later = [x for x in g[rank + 1:] if x[0] > 0]
     next_first = later[0][1] if later else KEY_EMPTY
-    ns = shard.faithful_shard_starts(j_off, pmax_in, stream)
-    s_off = sum(x[0] for x in allgather([ns])[:rank])
-    c = shard.faithful_shard_cut(s_off, n_total, stream)
-    cut = min(x[0] for x in allgather([c]))
-    shard.faithful_shard_hist(cut, next_first, not later, stream)
+    ns = phase(shard.faithful_shard_starts, j_off, pmax_in, stream, default=0)
+    s_off = sum(x[0] for x in exchange([ns])[:rank])
+    c = phase(shard.faithful_shard_cut, s_off, n_total, stream, default=n_total)
+    cut = min(x[0] for x in exchange([c]))
+    phase(shard.faithful_shard_hist, cut, next_first, not later, stream, default=None)
+    exchange([])  # the last phase's error, before the caller's merge collectives
     return n_total, cut
+
+
+def _export_fetch(ctx, keys, cnts, sp, dev):
+    """Export the handle's canonical table and read its flags: (traversed, error or None)."""
+    import torch
+    try:
+        ctx.export(keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
+        torch.cuda.synchronize(dev)
+        return ctx.fetch().traversed, None
+    except Exception as e:  # noqa: BLE001 -- raised on every rank by raise_together
+        return [0] * 6, e
 
 
 def sharded_faithful_hist(cfg, samples_by_ref, group=None, stream=None):
@@ -205,9 +247,8 @@ def sharded_faithful_hist(cfg, samples_by_ref, group=None, stream=None):
         ctx.reset(sp)
         for ref, t in samples_by_ref.items():
             faithful_shard_protocol(ctx, ref, t.data_ptr(), t.numel(), lo, hi, rank, ag, sp)
-        ctx.export(keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
-        torch.cuda.synchronize(dev)
-        trav = ctx.fetch().traversed
+        trav, err = _export_fetch(ctx, keys, cnts, sp, dev)
+    raise_together(err, group, dev if nccl else None)
     tsum = [sum(col) % (1 << 64) for col in zip(*ag(trav))]
     if not nccl:
         keys, cnts = keys.cpu(), cnts.cpu()
@@ -240,12 +281,15 @@ def sharded_faithful_gen_hist(cfg, seed, totals, group=None, stream=None):
         for ref, (t, (a, b)) in enumerate(zip(totals, slices)):
             if t == 0:
                 continue
-            if b > a:
-                ctx.expand_sorted(seed, ref, int(t), a, b - a, buf.data_ptr(), sp)
-            faithful_shard_protocol(ctx, ref, buf.data_ptr(), b - a, lo, hi, rank, ag, sp)
-        ctx.export(keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
-        torch.cuda.synchronize(dev)
-        trav = ctx.fetch().traversed
+            err = None
+            try:
+                if b > a:
+                    ctx.expand_sorted(seed, ref, int(t), a, b - a, buf.data_ptr(), sp)
+            except Exception as e:  # noqa: BLE001 -- raised on every rank by the protocol's first exchange
+                err = e
+            faithful_shard_protocol(ctx, ref, buf.data_ptr(), b - a, lo, hi, rank, ag, sp, err=err)
+        trav, err = _export_fetch(ctx, keys, cnts, sp, dev)
+    raise_together(err, group, dev if nccl else None)
     tsum = [sum(col) % (1 << 64) for col in zip(*ag(trav))]
     if not nccl:
         keys, cnts = keys.cpu(), cnts.cpu()

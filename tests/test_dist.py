@@ -133,7 +133,7 @@ def _dense_worker(rank, world, port, samples_per_ref, N, T, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_dense_allreduce_equals_whole_list(orc, world):
     """The dense multi-GPU merge (bench step for N>1): per-rank (ref, case)
     vectors summed by one all-reduce == the oracle histogram of the whole list."""
@@ -198,3 +198,72 @@ def test_flag_errors_raise_on_every_rank():
         p.join(timeout=60)
     assert res[0] == ["ok", "raised:other"]
     assert res[1] == ["ok", "raised:own"]
+
+
+def _dense8_worker(rank, world, port, q):
+    """Config 3's shape at the node's size: rank `rank` of 8 takes its slice of
+    every reference's config-3 index range (default_counts(4096, 2^28)), a
+    strided subset of which is counted into the dense (ref, case) vector by the
+    closed forms; the vectors are merged by dist.allreduce_dense."""
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+    import oracle as orc
+    import pluss_sampler_optimization_amd as P
+    from conftest import closed_form_ri
+    from pluss_sampler_optimization_amd import dist as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    N, T = 4096, 8
+    c = orc.cfg(N, T)
+    cfg = P.SamplerConfig(n=N, threads=T)
+    keys = np.array(P.dense_keys(cfg), dtype=np.uint64)
+    counts = P.default_counts(N, 1 << 28)
+    v = np.zeros(P.DENSE_BINS + 1, np.int64)
+    mine = []
+    for r, (first, n) in enumerate(D.shard_ranges(counts, rank, world)):
+        idx = np.arange(first, first + n, 4096, dtype=np.uint64)
+        s = np.concatenate([orc.expand(c, 0x5EED0001, r, int(i), 1) for i in idx[:64]] +
+                           [orc.expand(c, 0x5EED0001, r, int(first), min(n, 2000))])
+        mine.append(s)
+    mine = np.unique(np.concatenate(mine))
+    refs, c0, c1, c2 = P.unpack_array(mine)
+    ri = closed_form_ri(N, T, 4, 8, refs, c0, c1, c2)
+    kind = ((refs == 3) & (ri > 0) & (2 * ri > (4 * N + 2) * N)).astype(np.int64)
+    key = (refs.astype(np.uint64) << np.uint64(60)) | (kind.astype(np.uint64) << np.uint64(56)) | (ri + 2).astype(np.uint64)
+    for b in range(P.DENSE_BINS):  # C0/C1/C2 have one key for all three cases: its first bin
+        if keys[b] not in keys[:b]:
+            v[b] = int((key == keys[b]).sum())
+    assert v.sum() == len(mine)
+    merged = D.allreduce_dense(torch.from_numpy(v)).numpy()
+    q.put((rank, merged.tolist(), mine.tolist()))
+    dist.destroy_process_group()
+
+
+def test_dense_allreduce_config3_world8(orc):
+    """World size 8 (config 3's node) with config-3 vectors (N=4096, T=8, each
+    rank's slice of the 2^28 budget): the all-reduced vector == the closed-form
+    histogram of the union of the ranks' samples, identical on every rank."""
+    import pluss_sampler_optimization_amd as P
+    from conftest import closed_form_counts
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dense8_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    allmine = np.concatenate([np.array(m, np.uint64) for _, _, m in res])
+    assert len(np.unique(allmine)) == len(allmine)  # the slices are disjoint
+    want = closed_form_counts(4096, 8, 4, allmine)
+    cfg = P.SamplerConfig(n=4096, threads=8)
+    for _, merged, _ in res:
+        assert merged == res[0][1]
+        assert P.hist_from_dense(cfg, np.array(merged, np.int64)).bins == want

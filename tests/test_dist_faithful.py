@@ -151,7 +151,7 @@ def _worker(rank, world, port, N, T, per, q):
 
 
 @pytest.mark.parametrize("world,N,T,per", [(1, 64, 4, 3000), (2, 64, 4, 3000), (3, 128, 8, 4000),
-                                           (4, 64, 2, 2500)])
+                                           (4, 64, 2, 2500), (8, 128, 8, 4000)])
 def test_key_range_shards_equal_sequential_sampler(orc, world, N, T, per):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -211,3 +211,75 @@ def test_key_range_shards_on_reference_dumps(orc, name, d, smp):
         assert got == exp, (name, ref)
         assert trav == etrav, (name, ref)
         assert D.KEY_EMPTY == KEY_EMPTY
+
+
+class FailingShard(HostShard):
+    """A shard whose phase `phase` raises (as a device phase does on malformed
+    samples or a HIP error)."""
+
+    def __init__(self, *a, phase):
+        super().__init__(*a)
+        self.phase = phase
+
+    def faithful_shard_starts(self, *a, **k):
+        if self.phase == "starts":
+            raise RuntimeError("injected failure in phase 2")
+        return super().faithful_shard_starts(*a, **k)
+
+    def faithful_shard_hist(self, *a, **k):
+        if self.phase == "hist":
+            raise RuntimeError("injected failure in phase 4")
+        return super().faithful_shard_hist(*a, **k)
+
+
+def _fail_worker(rank, world, port, bad, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    import oracle as orc
+    from pluss_sampler_optimization_amd import PlussError
+    from pluss_sampler_optimization_amd import dist as D
+    from test_dist_faithful import FailingShard, keys_and_sinks
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    N, T = 64, 4
+    c = orc.cfg(N, T)
+    ag = D.torch_allgather(None, "cpu")
+    lo, hi = D.key_range((N // T) * N * (4 * N + 2) * T, rank, world)
+    s = orc.expand(c, 0x5EED0040, 2, 0, 2000)
+    keys, sinks, _ = keys_and_sinks(orc, c, N, T, 4, "A0", s)
+    out = []
+    for phase in ("starts", "hist", None):
+        sh = FailingShard(N, T, keys, sinks, "A0", phase=phase if rank == bad else None)
+        try:
+            D.faithful_shard_protocol(sh, 2, None, len(s), lo, hi, rank, ag)
+            out.append("ok")
+        except PlussError as e:
+            out.append("other" if "another rank" in str(e) else "?")
+        except RuntimeError as e:
+            out.append("own" if "injected" in str(e) else "?")
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, out))
+
+
+def test_failing_rank_raises_on_every_rank():
+    """A rank whose shard phase raises still takes part in the protocol's next
+    exchange, so every rank raises there instead of waiting forever; the next
+    protocol run on the same process group works."""
+    world, bad = 4, 1
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_fail_worker, args=(r, world, port, bad, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        want = "own" if r == bad else "other"
+        assert res[r] == [want, want, "ok"], (r, res[r])
