@@ -526,6 +526,12 @@ static uint64_t mix64(uint64_t z) { /* splitmix64 finaliser */
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
 }
+static uint32_t lowbias32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16; return x;
+}
+/* Sample list bijection: cycle-walking 4-round Feistel over
+   [0, 2^2h) onto [0, D), D = span^d; round R' = L ^ (lowbias32(R ^ k_r) & mask)
+   with 32-bit round keys from splitmix64(seed, ref, round). */
 int orc_expand(const orc_cfg *c, uint64_t seed, int ref, uint64_t first, uint64_t n, uint64_t *out) {
     if (!cfg_ok(c) || ref < 0 || ref > 5) return -1;
     int dim3 = !(ref == R_C0 || ref == R_C1);
@@ -534,16 +540,16 @@ int orc_expand(const orc_cfg *c, uint64_t seed, int ref, uint64_t first, uint64_
     uint64_t D = dim3 ? m * m * m : m * m;
     if (first + n > D) return -2;
     int h = 1; while ((1ULL << (2 * h)) < D) h++;
-    uint64_t M = (1ULL << h) - 1;
-    uint64_t key[4];
+    uint32_t M = (uint32_t)((1ULL << h) - 1);
+    uint32_t key[4];
     for (int r = 0; r < 4; r++)
-        key[r] = mix64(seed ^ ((uint64_t)(ref + 1) * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)(r + 1) * 0xD1B54A32D192ED03ULL));
+        key[r] = (uint32_t)mix64(seed ^ ((uint64_t)(ref + 1) * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)(r + 1) * 0xD1B54A32D192ED03ULL));
     for (uint64_t i = 0; i < n; i++) {
         uint64_t y = first + i;
         do {
-            uint64_t L = y >> h, R = y & M;
-            for (int r = 0; r < 4; r++) { uint64_t t = R; R = L ^ (mix64(key[r] ^ R) & M); L = t; }
-            y = (L << h) | R;
+            uint32_t L = (uint32_t)(y >> h), R = (uint32_t)y & M;
+            for (int r = 0; r < 4; r++) { uint32_t t = R; R = L ^ (lowbias32(R ^ key[r]) & M); L = t; }
+            y = ((uint64_t)L << h) | R;
         } while (y >= D);
         uint64_t c0, c1, c2 = 0;
         if (dim3) { c2 = y % m; y /= m; }
@@ -558,9 +564,6 @@ int orc_expand(const orc_cfg *c, uint64_t seed, int ref, uint64_t first, uint64_
    tid; block A: q < QA, all tids; block B: q = Q-1, tid < T-1 when span < N),
    S samples split in proportion to the block sizes, one per stratum at a keyed
    offset.  Needs N % (CS*T) == 0, 1 <= S <= span^d, S < 2^32. */
-static uint32_t lowbias32(uint32_t x) {
-    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16; return x;
-}
 int orc_expand_sorted(const orc_cfg *c, uint64_t seed, int ref, uint64_t S, uint64_t first, uint64_t n,
                       uint64_t *out) {
     if (!cfg_ok(c) || ref < 0 || ref > 5 || c->N % (c->CS * c->T)) return -1;

@@ -1,0 +1,12 @@
+// pluss_fa_w64.hip — the faithful scan pipeline (pluss_faithful.h) instantiated
+// for one element source, in a translation unit of its own.
+#include "pluss_faithful.h"
+
+namespace pluss {
+
+void fa_launch_w64(const FaLaunch& L) {
+  if (L.p2) fa_launch_t<SRC_W64, false, true>(L);
+  else fa_launch_t<SRC_W64, false, false>(L);
+}
+
+}  // namespace pluss

@@ -40,86 +40,9 @@
 #include <rocprim/iterator/counting_iterator.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
 
-#include "pluss_device.h"
+#include "pluss_faithful.h"
 
 namespace pluss {
-
-// Faithful-mode key storage: FM_PAIRS = 64-bit (key, sink) pairs (any
-// shape); FM_PK64 / FM_PK32 = packed (rank << 2 | case) words of 64 / 32 bits.
-enum : int { FM_PAIRS = 0, FM_PK64 = 1, FM_PK32 = 2 };
-template <int FM>
-using fkey_t = typename std::conditional<FM == FM_PK32, uint32_t, unsigned long long>::type;
-
-// Decoding of packed words for one reference.
-struct PkView {
-  int64_t ri[3];             // RI of case 0/1/2 (-1: cold)
-  uint64_t T, N, R, S;
-  uint32_t ref, p2, tsh, nsh;  // p2: N and T powers of two (shifts)
-  uint32_t Q;                  // local rows per simulated thread, N / T
-};
-inline PkView make_pkview(const Model& m, uint32_t ref) {
-  PkView v;
-  for (int c = 0; c < 3; ++c) v.ri[c] = key_ri(m.keytab[ref * 3 + c]);
-  v.T = m.T;
-  v.N = m.N;
-  v.R = m.R;
-  v.S = m.S;
-  v.ref = ref;
-  v.tsh = v.nsh = 0;
-  while ((1ull << v.tsh) < v.T) ++v.tsh;
-  while ((1ull << v.nsh) < v.N) ++v.nsh;
-  v.p2 = ((1ull << v.tsh) == v.T && (1ull << v.nsh) == v.N) ? 1u : 0u;
-  v.Q = (uint32_t)(v.N / v.T);
-  return v;
-}
-// the key a*T + tid of a packed word (KEY_EMPTY for the malformed marker ~0)
-template <typename KT>
-__host__ __device__ __forceinline__ unsigned long long pk_key(KT pk, const PkView& v) {
-  if (pk == (KT) ~(KT)0) return KEY_EMPTY;
-  uint64_t r = (uint64_t)(pk >> 2), t, c2, c1, q;
-  if (v.p2) {
-    t = r & (v.T - 1);
-    r >>= v.tsh;
-    c2 = r & (v.N - 1);
-    r >>= v.nsh;
-    c1 = r & (v.N - 1);
-    q = r >> v.nsh;
-  } else {
-    t = r % v.T;
-    r /= v.T;
-    c2 = r % v.N;
-    r /= v.N;
-    c1 = r % v.N;
-    q = r / v.N;
-  }
-  const uint64_t off = v.ref < 2 ? v.ref : v.ref + 4 * c2;
-  return (q * v.R + c1 * v.S + off) * v.T + t;
-}
-template <typename KT>
-__device__ __forceinline__ unsigned long long pk_sink(KT pk, const PkView& v) {
-  const uint32_t c = (uint32_t)(pk & 3u);
-  if (pk == (KT) ~(KT)0 || c == 3) return KEY_EMPTY;
-  const int64_t ri = c == 0 ? v.ri[0] : (c == 1 ? v.ri[1] : v.ri[2]);
-  return ri < 0 ? KEY_EMPTY : pk_key(pk, v) + (unsigned long long)ri * v.T;
-}
-// key / sink of sorted element i
-template <int FM>
-__device__ __forceinline__ unsigned long long key_at(const void* keys, uint64_t i, const PkView& v) {
-  if (FM == FM_PAIRS) return static_cast<const unsigned long long*>(keys)[i];
-  return pk_key(static_cast<const fkey_t<FM>*>(keys)[i], v);
-}
-template <int FM>
-__device__ __forceinline__ unsigned long long sink_at(const void* keys, const unsigned long long* sinks, uint64_t i,
-                                                      const PkView& v) {
-  if (FM == FM_PAIRS) return sinks[i];
-  return pk_sink(static_cast<const fkey_t<FM>*>(keys)[i], v);
-}
-template <typename KT>
-struct PkSinkOp {  // rocprim transform: packed word -> sink
-  PkView v;
-  __device__ unsigned long long operator()(KT pk) const { return pk_sink(pk, v); }
-};
-
 // Packed word (rank << 2 | case) of sample x of reference `ref`; ~0 (and the
 // bad-input flag) for a sample of another reference or out of range.
 template <typename KT>
@@ -275,33 +198,6 @@ __device__ __forceinline__ unsigned long long st_ld(const unsigned long long* p)
 }
 __device__ __forceinline__ void st_st(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <bool MAX>
-__device__ __forceinline__ unsigned long long sc_op(unsigned long long a, unsigned long long b) {
-  return MAX ? (a > b ? a : b) : a + b;
-}
-template <bool MAX>
-__device__ __forceinline__ unsigned long long sc_wave_red(unsigned long long v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = sc_op<MAX>(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ unsigned long long sc_wave_red_min(unsigned long long v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long x = __shfl_xor(v, o, 64);
-    v = x < v ? x : v;
-  }
-  return v;
-}
-template <bool MAX>
-__device__ __forceinline__ unsigned long long sc_wave_scan(unsigned long long v, uint32_t lane) {  // inclusive
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long y = __shfl_up(v, o, 64);
-    if (lane >= (uint32_t)o) v = sc_op<MAX>(v, y);
-  }
-  return v;
 }
 // Exclusive prefix of tile t > 0 from the status words of tiles t-1, t-2, ...
 // (one whole wave, 64 predecessors per round).  Every predecessor took its
@@ -470,849 +366,6 @@ __global__ void k_faith_scan_init(unsigned long long* scal, uint64_t cut, unsign
   for (uint64_t j = i; j < nw; j += (uint64_t)gridDim.x * blockDim.x) st[j] = 0;
 }
 
-// ---- the one-GPU scan over key-ordered elements, the six references of a
-// list in ONE pipeline of four launches (whatever the element source: sorted
-// packed words after the radix sort, a caller's key-ordered samples, or
-// samples generated in key order):
-//   k_fa_max     per tile of TILE elements: the largest sink (a caller's list:
-//                the key-order check; samples / generated lists: the packed
-//                sort word of every element, written once for the scan);
-//   k_fa_prefix  one workgroup per reference: exclusive prefix max of the
-//                tile maxima = the running max of sinks entering each tile;
-//   k_fa_scan    every tile independently (no chain across tiles): prefix
-//                max inside the tile, start flags, the tile's start count,
-//                its Q1 bound (hmax) and the records of all its elements;
-//   k_fa_finish  one workgroup per reference: the exclusive sum of the start
-//                counts locates the tile holding the Q1 cut (the condition
-//                j - starts_before_j >= n - j is monotone in j), the tiles
-//                before it are summed, that tile is scanned again below the
-//                cut; Q3, the -1 key, traversed, the bins.
-constexpr int TB = 256, TI = 16;            // threads per tile, elements per thread
-constexpr uint32_t TILE = TB * TI;          // elements per tile
-constexpr int FPART = 5;                    // per tile: cold (tid 0), traversed, case 0/1/2 counts
-__host__ __device__ inline uint64_t fa_tiles(uint64_t n) { return (n + TILE - 1) / TILE; }
-
-enum : int { SRC_W32 = 0, SRC_W64 = 1, SRC_SAMPLES = 2, SRC_GEN = 3 };
-
-struct FaRefs {
-  uint64_t n[6];
-  uint64_t toff[7];    // first (global) tile of each reference; toff[6] = all tiles
-  const void* src[6];  // SRC_W*: sorted packed words; SRC_SAMPLES: the key-ordered samples
-  PkView pv[6];
-  KeyGen kg[6];        // SRC_GEN
-};
-
-// key, sink, case (3: malformed, flagged) and tid == 0 of one element.  P2:
-// N, T, CS and CLS/DS powers of two (every BASELINE shape) -- decoded with
-// shifts; the general decode is a separate instantiation, so no division is
-// ever evaluated on the P2 path.
-struct Elem {
-  unsigned long long key, sink;
-  uint32_t c, t0;
-  unsigned long long w;  // the packed sort word rank << 2 | case (~0: malformed)
-};
-
-template <bool P2>
-__device__ __forceinline__ Elem elem_of_digits(const Model& m, const PkView& v, uint32_t ref, const KeyDigits& d) {
-  // P2: q*N + c1 < N*N/T < 2^32 (fa_run), so one 32x32->64 multiply
-  const uint64_t qc = P2 ? (uint64_t)((d.q << v.nsh) | d.c1) : (uint64_t)d.q * m.N + d.c1;
-  const uint64_t a = (P2 ? (uint64_t)(uint32_t)qc * (uint32_t)m.S : qc * m.S) + ref_off(ref, d.c2);
-  const uint64_t key = P2 ? ((a << v.tsh) | d.t) : a * m.T + d.t;
-  const uint32_t c = case_of_digits<P2>(m, ref, d, v.Q);
-  const int64_t ri = c == 0 ? v.ri[0] : (c == 1 ? v.ri[1] : v.ri[2]);
-  const unsigned long long dt = P2 ? ((unsigned long long)ri << v.tsh) : (unsigned long long)ri * m.T;
-  // rank = ((q*N + c1)*N + c2)*T + t
-  const uint64_t rank = P2 ? ((((qc << v.nsh) | d.c2) << v.tsh) | d.t) : (qc * m.N + d.c2) * m.T + d.t;
-  return Elem{key, ri < 0 ? KEY_EMPTY : key + dt, c, d.t == 0 ? 1u : 0u, (rank << 2) | c};
-}
-
-template <bool P2>
-__device__ __forceinline__ Elem elem_of_sample(const Model& m, const PkView& v, uint32_t ref, uint64_t x, GTable g) {
-  const Sample s = unpack(x);
-  if (s.ref != ref || s.c0 >= m.N || s.c1 >= m.N || s.c2 >= m.N) {
-    atomicOr(&g.flags[1], 1u);
-    return Elem{KEY_EMPTY, KEY_EMPTY, 3u, 0u, ~0ull};
-  }
-  KeyDigits d;
-  d.c1 = s.c1;
-  d.c2 = (ref == C0 || ref == C1) ? 0u : s.c2;
-  if (P2) {
-    const uint32_t k = s.c0 >> m.csshift;
-    d.t = k & (m.T - 1);
-    d.q = ((k >> v.tsh) << m.csshift) | (s.c0 & m.csmask);
-  } else {
-    const uint32_t k = fdiv(s.c0, m.dCS), kt = fdiv(k, m.dT);
-    d.t = k - kt * m.T;
-    d.q = kt * m.CS + (s.c0 - k * m.CS);
-  }
-  return elem_of_digits<P2>(m, v, ref, d);
-}
-
-// a packed sort word (rank << 2 | case), rank = ((q*N + c1)*N + c2)*T + tid
-template <bool P2, typename KT>
-__device__ __forceinline__ Elem elem_of_word(const Model& m, const PkView& v, uint32_t ref, KT w) {
-  if (w == (KT) ~(KT)0) return Elem{KEY_EMPTY, KEY_EMPTY, 3u, 0u, ~0ull};
-  uint64_t r = (uint64_t)(w >> 2);
-  KeyDigits d;
-  if (P2) {
-    d.t = (uint32_t)(r & (v.T - 1));
-    r >>= v.tsh;
-    d.c2 = (uint32_t)(r & (v.N - 1));
-    r >>= v.nsh;
-    d.c1 = (uint32_t)(r & (v.N - 1));
-    d.q = (uint32_t)(r >> v.nsh);
-  } else {
-    d.t = (uint32_t)(r % v.T);
-    r /= v.T;
-    d.c2 = (uint32_t)(r % v.N);
-    r /= v.N;
-    d.c1 = (uint32_t)(r % v.N);
-    d.q = (uint32_t)(r / v.N);
-  }
-  const uint32_t c = (uint32_t)(w & 3u);
-  const uint64_t a = ((uint64_t)d.q * m.N + d.c1) * m.S + ref_off(ref, d.c2);
-  const uint64_t key = P2 ? ((a << v.tsh) | d.t) : a * m.T + d.t;
-  const int64_t ri = c == 0 ? v.ri[0] : (c == 1 ? v.ri[1] : v.ri[2]);
-  const unsigned long long dt = P2 ? ((unsigned long long)ri << v.tsh) : (unsigned long long)ri * m.T;
-  return Elem{key, (c == 3 || ri < 0) ? KEY_EMPTY : key + dt, c, d.t == 0 ? 1u : 0u, (unsigned long long)w};
-}
-
-template <int SRC>
-using fa_raw_t = typename std::conditional<SRC == SRC_W32, uint32_t, unsigned long long>::type;
-
-// element i of reference r read straight from the source (global memory)
-template <int SRC, bool P2>
-__device__ __forceinline__ Elem fa_elem(const Model& m, const FaRefs& a, uint32_t r, uint64_t i, GTable g) {
-  if (SRC == SRC_GEN) return elem_of_digits<P2>(m, a.pv[r], r, keygen_digits_at(a.kg[r], i));
-  const fa_raw_t<SRC> w = static_cast<const fa_raw_t<SRC>*>(a.src[r])[i];
-  if (SRC == SRC_SAMPLES) return elem_of_sample<P2>(m, a.pv[r], r, (uint64_t)w, g);
-  return elem_of_word<P2>(m, a.pv[r], r, w);
-}
-
-// A tile's elements as read from memory (raw words / samples), staged in LDS:
-// loaded coalesced (thread x, round k: element k*TB + x), read back by each
-// thread as its contiguous run (x*TI + k).  One padding slot per TI elements
-// keeps the run reads at 2-way bank conflicts.
-constexpr uint32_t FA_LDS = TILE + TILE / TI;
-__device__ __forceinline__ uint32_t fa_slot(uint32_t e) { return e + e / TI; }
-
-template <int SRC>
-__device__ __forceinline__ void fa_stage(const FaRefs& a, uint32_t r, uint64_t base, uint32_t mt,
-                                         fa_raw_t<SRC>* lds) {
-  if (SRC == SRC_GEN) return;
-  const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(a.src[r]) + base;
-#pragma unroll
-  for (int k = 0; k < TI; ++k) {
-    const uint32_t e = (uint32_t)k * TB + threadIdx.x;
-    if (e < mt) lds[fa_slot(e)] = src[e];
-  }
-  __syncthreads();
-}
-
-// A lane's run of consecutive elements: read from the staged tile, or
-// generated in sequence (GEN: keyrunf_* when the whole tile lies in block A
-// with small strata -- tile-uniform -- else one direct decode per sample).
-template <int SRC, bool P2>
-struct FaCursor {
-  const Model& m;
-  const FaRefs& a;
-  uint32_t r;
-  uint64_t base;
-  uint32_t e;
-  const fa_raw_t<SRC>* lds;
-  GTable g;
-  bool fast;
-  KeyRunF run;
-  __device__ FaCursor(const Model& m_, const FaRefs& a_, uint32_t r_, uint64_t base_, uint32_t e0,
-                      const fa_raw_t<SRC>* lds_, GTable g_)
-      : m(m_), a(a_), r(r_), base(base_), e(e0), lds(lds_), g(g_), fast(false) {
-    if (SRC == SRC_GEN) {
-      fast = keyrun_fast_ok(a.kg[r], base, TILE);
-      if (fast) keyrunf_start(a.kg[r], run, base + e0);
-    }
-  }
-  // the element at the cursor; then the cursor moves on
-  __device__ Elem next() {
-    Elem x;
-    if (SRC == SRC_GEN) {
-      if (fast) {
-        x = elem_of_digits<P2>(m, a.pv[r], r, keyrunf_digits(a.kg[r], run));
-        keyrunf_next(a.kg[r], run);
-      } else {
-        x = elem_of_digits<P2>(m, a.pv[r], r, keygen_digits_at(a.kg[r], base + e));
-      }
-    } else {
-      const fa_raw_t<SRC> w = lds[fa_slot(e)];
-      if (SRC == SRC_SAMPLES) x = elem_of_sample<P2>(m, a.pv[r], r, (uint64_t)w, g);
-      else x = elem_of_word<P2>(m, a.pv[r], r, w);
-    }
-    ++e;
-    return x;
-  }
-};
-
-// the tile's reference (wave-uniform) and its place in it
-struct FaTile {
-  uint32_t r;
-  uint64_t lt, base;  // tile index within the reference, its first element
-  uint32_t mt;        // elements in the tile
-};
-__device__ __forceinline__ FaTile fa_tile(const FaRefs& a, uint64_t gt) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int x = 1; x < 6; ++x) r += gt >= a.toff[x] ? 1u : 0u;
-  r = __builtin_amdgcn_readfirstlane(r);
-  FaTile t;
-  t.r = r;
-  t.lt = gt - a.toff[r];
-  t.base = t.lt * TILE;
-  const uint64_t left = a.n[r] - t.base;
-  t.mt = (uint32_t)(left < TILE ? left : TILE);
-  return t;
-}
-
-// the one reference a scanned tile belongs to (copied out of FaRefs by the
-// kernel, so the body never indexes the kernel argument itself)
-struct FaOne {
-  FaTile T;
-  uint64_t n;
-  const void* src;
-  PkView pv;
-};
-__device__ __forceinline__ FaOne fa_one(const FaRefs& a, uint64_t gt) {
-  FaOne o;
-  o.T = fa_tile(a, gt);
-  o.n = a.n[o.T.r];
-  o.src = a.src[o.T.r];
-  o.pv = a.pv[o.T.r];
-  return o;
-}
-
-// ---- pass 1 (k_fa_max*): per tile, the largest sink; for a caller's list
-// the key-order check; for sample / generated sources also the packed sort
-// word of every element (written once, read by the scan).
-//
-// Lists in memory (sorted words, a caller's samples): element-strided, thread
-// x round k holds element k*TB + x, so every load and word store is coalesced
-// and no LDS staging is needed (occupancy is not capped by LDS).  The body is
-// instantiated per reference (tile-uniform switch), so the decode and the
-// case rules fold to the reference's own few instructions.
-template <uint32_t REF, bool P2>
-__device__ __forceinline__ Elem elem_of_sample_ref(const Model& m, const PkView& v, uint64_t x, bool& bad) {
-  const Sample s = unpack(x);
-  const uint32_t mx = s.c0 > s.c1 ? s.c0 : s.c1;
-  const bool ok = s.ref == REF && (mx > s.c2 ? mx : s.c2) < m.N;
-  bad |= !ok;
-  KeyDigits d;
-  d.c1 = s.c1;
-  d.c2 = (REF == C0 || REF == C1) ? 0u : s.c2;
-  if (P2) {
-    const uint32_t k = s.c0 >> m.csshift;
-    d.t = k & (m.T - 1);
-    d.q = ((k >> v.tsh) << m.csshift) | (s.c0 & m.csmask);
-  } else {
-    const uint32_t k = fdiv(s.c0, m.dCS), kt = fdiv(k, m.dT);
-    d.t = k - kt * m.T;
-    d.q = kt * m.CS + (s.c0 - k * m.CS);
-  }
-  Elem e = elem_of_digits<P2>(m, v, REF, d);
-  if (!ok) e = Elem{KEY_EMPTY, KEY_EMPTY, 3u, 0u, ~0ull};
-  return e;
-}
-
-template <int SRC, bool P2, uint32_t REF>
-__device__ __forceinline__ Elem fa_decode_ref(const Model& m, const PkView& v, fa_raw_t<SRC> w, bool& bad) {
-  if constexpr (SRC == SRC_SAMPLES) return elem_of_sample_ref<REF, P2>(m, v, (uint64_t)w, bad);
-  else return elem_of_word<P2>(m, v, REF, w);
-}
-
-template <int SRC, bool CHECK, bool P2, int WK, uint32_t REF>
-__device__ __forceinline__ void fa_max_tile(const Model& m, const FaOne& o, unsigned long long* __restrict__ tmax,
-                                            void* words, GTable g, unsigned long long* s_w,
-                                            unsigned long long (*s_first)[TB / 64],
-                                            unsigned long long (*s_last)[TB / 64]) {
-  using wk_t = typename std::conditional<WK == 8, unsigned long long, uint32_t>::type;
-  constexpr int NW = TB / 64;
-  const FaTile& T = o.T;
-  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(o.src) + T.base;
-  wk_t* out = static_cast<wk_t*>(words) + blockIdx.x * (uint64_t)TILE;
-  const bool full = T.mt == TILE;
-  fa_raw_t<SRC> raw[TI];
-#pragma unroll
-  for (int k = 0; k < TI; ++k) {  // every load in flight before the first decode
-    const uint32_t e = (uint32_t)k * TB + threadIdx.x;
-    raw[k] = (full || e < T.mt) ? src[e] : (fa_raw_t<SRC>)0;
-  }
-  unsigned long long tm = 0;
-  bool bad = false, unordered = false;
-#pragma unroll
-  for (int k = 0; k < TI; ++k) {
-    const uint32_t e = (uint32_t)k * TB + threadIdx.x;
-    const bool v = full || e < T.mt;
-    Elem x{KEY_EMPTY, 0ull, 3u, 0u, ~0ull};
-    if (v) {
-      x = fa_decode_ref<SRC, P2, REF>(m, o.pv, raw[k], bad);
-      tm = x.sink > tm ? x.sink : tm;
-      if (WK) out[e] = (wk_t)x.w;
-    }
-    if (CHECK) {  // strictly increasing keys: against the previous lane here, across waves/rounds below
-      const unsigned long long up = __shfl_up(x.key, 1, 64);
-      unordered |= v && lane > 0 && !(x.key > up);
-      if (lane == 0) s_first[k][wid] = x.key;
-      if (lane == 63) s_last[k][wid] = x.key;
-    }
-  }
-  if (CHECK) {
-    __syncthreads();
-    if (threadIdx.x < TI * NW) {  // the first element of (round k, wave w) against the element before it
-      const uint32_t k = threadIdx.x / NW, w = threadIdx.x % NW;
-      const uint32_t e = k * TB + w * 64;
-      if (e < T.mt && (e > 0 || T.base > 0)) {
-        bool b2 = false;
-        const unsigned long long prev =
-            e > 0 ? (w > 0 ? s_last[k][w - 1] : s_last[k - 1][NW - 1]) : fa_decode_ref<SRC, P2, REF>(m, o.pv, src[-1], b2).key;
-        unordered |= !(s_first[k][w] > prev);
-      }
-    }
-  }
-  if (__ballot(bad || unordered) && lane == 0) atomicOr(&g.flags[1], 1u);
-  tm = sc_wave_red<true>(tm);
-  if (lane == 0) s_w[wid] = tm;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long x = 0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) x = s_w[w] > x ? s_w[w] : x;
-    tmax[blockIdx.x] = x;
-  }
-}
-
-// the reference's first tile also materialises its -1 (cold) key in the main
-// table and keeps the slot, so the finish pass only adds the count
-__device__ __forceinline__ void fa_cold_slot(const FaTile& T, GTable g, unsigned long long* slots) {
-  if (T.lt == 0 && threadIdx.x == 0) slots[T.r] = g_slot(g, make_key(T.r, 0, -1));
-}
-
-template <int SRC, bool CHECK, bool P2, int WK>
-__global__ __launch_bounds__(TB) void k_fa_max(Model m, FaRefs a, unsigned long long* __restrict__ tmax, void* words,
-                                               unsigned long long* slots, GTable g) {
-  static_assert(SRC != SRC_GEN, "generated lists: k_fa_max_gen");
-  constexpr int NW = TB / 64;
-  __shared__ unsigned long long s_w[NW];
-  __shared__ unsigned long long s_first[CHECK ? TI : 1][NW], s_last[CHECK ? TI : 1][NW];
-  const FaOne o = fa_one(a, blockIdx.x);
-  fa_cold_slot(o.T, g, slots);
-#define PLUSS_FA_MAX(R) fa_max_tile<SRC, CHECK, P2, WK, R>(m, o, tmax, words, g, s_w, s_first, s_last)
-  switch (o.T.r) {
-    case C0: PLUSS_FA_MAX(C0); break;
-    case C1: PLUSS_FA_MAX(C1); break;
-    case A0: PLUSS_FA_MAX(A0); break;
-    case B0: PLUSS_FA_MAX(B0); break;
-    case C2: PLUSS_FA_MAX(C2); break;
-    default: PLUSS_FA_MAX(C3); break;
-  }
-#undef PLUSS_FA_MAX
-}
-
-// Generated lists: each lane generates its run of TI consecutive elements
-// (incremental key-order digits: keyrunf_* when the whole tile lies in block A
-// with small strata -- tile-uniform -- else one direct decode per sample), the
-// words go out through LDS (coalesced).  Instantiated per reference.
-template <bool P2, int WK, uint32_t REF>
-__device__ __forceinline__ void fa_gen_tile(const Model& m, const KeyGen& kg, const PkView& pv, const FaTile& T,
-                                            unsigned long long* __restrict__ tmax, void* words,
-                                            unsigned long long* s_w, void* s_wd_) {
-  using wk_t = typename std::conditional<WK == 8, unsigned long long, uint32_t>::type;
-  wk_t* s_wd = static_cast<wk_t*>(s_wd_);
-  constexpr int NW = TB / 64;
-  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  const uint32_t e0 = threadIdx.x * TI;
-  unsigned long long tm = 0;
-  if (keyrun_fast_ok(kg, T.base, TILE)) {  // the whole tile: every lane's run is in range
-    KeyRunF run;
-    keyrunf_start(kg, run, T.base + e0);
-#pragma unroll
-    for (int k = 0; k < TI; ++k) {
-      const Elem e = elem_of_digits<P2>(m, pv, REF, keyrunf_digits(kg, run));
-      keyrunf_next(kg, run);
-      tm = e.sink > tm ? e.sink : tm;
-      s_wd[fa_slot(e0 + k)] = (wk_t)e.w;
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < TI; ++k) {
-      if (e0 + k < T.mt) {
-        const Elem e = elem_of_digits<P2>(m, pv, REF, keygen_digits_at(kg, T.base + e0 + k));
-        tm = e.sink > tm ? e.sink : tm;
-        s_wd[fa_slot(e0 + k)] = (wk_t)e.w;
-      }
-    }
-  }
-  __syncthreads();
-  wk_t* out = static_cast<wk_t*>(words) + blockIdx.x * (uint64_t)TILE;
-#pragma unroll
-  for (int k = 0; k < TI; ++k) {
-    const uint32_t e = k * TB + threadIdx.x;
-    if (e < T.mt) out[e] = s_wd[fa_slot(e)];
-  }
-  tm = sc_wave_red<true>(tm);
-  if (lane == 0) s_w[wid] = tm;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long x = 0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) x = s_w[w] > x ? s_w[w] : x;
-    tmax[blockIdx.x] = x;
-  }
-}
-
-template <bool P2, int WK>
-__global__ __launch_bounds__(TB) void k_fa_max_gen(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
-                                                   void* words, unsigned long long* slots, GTable g) {
-  using wk_t = typename std::conditional<WK == 8, unsigned long long, uint32_t>::type;
-  __shared__ unsigned long long s_w[TB / 64];
-  __shared__ wk_t s_wd[FA_LDS];
-  const FaTile T = fa_tile(a, blockIdx.x);
-  fa_cold_slot(T, g, slots);
-  // (the reference's generator and view copied out first: the kernel argument
-  // itself is never passed down, which would put a copy of it in scratch)
-#define PLUSS_FA_GEN(R)                                               \
-  {                                                                   \
-    const KeyGen kg = a.kg[R];                                        \
-    const PkView pv = a.pv[R];                                        \
-    fa_gen_tile<P2, WK, R>(m, kg, pv, T, tmax, words, s_w, s_wd);     \
-  }
-  switch (T.r) {
-    case C0: PLUSS_FA_GEN(C0); break;
-    case C1: PLUSS_FA_GEN(C1); break;
-    case A0: PLUSS_FA_GEN(A0); break;
-    case B0: PLUSS_FA_GEN(B0); break;
-    case C2: PLUSS_FA_GEN(C2); break;
-    default: PLUSS_FA_GEN(C3); break;
-  }
-#undef PLUSS_FA_GEN
-}
-
-// One workgroup per reference: pmin[t] = max of tmax over the reference's
-// tiles before t (0 for its first).
-constexpr int PB = 1024;
-__global__ __launch_bounds__(PB) void k_fa_prefix(FaRefs a, const unsigned long long* __restrict__ tmax,
-                                                  unsigned long long* __restrict__ pmin) {
-  __shared__ unsigned long long s_w[PB / 64];
-  const uint32_t r = blockIdx.x;
-  const uint64_t t0 = a.toff[r], nt = a.toff[r + 1] - t0;
-  if (nt == 0) return;
-  const uint64_t per = (nt + PB - 1) / PB;
-  const uint64_t lo = t0 + threadIdx.x * per, hi = lo + per < t0 + nt ? lo + per : t0 + nt;
-  unsigned long long mx = 0;
-  for (uint64_t t = lo; t < hi; ++t) mx = tmax[t] > mx ? tmax[t] : mx;
-  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  const unsigned long long inc = sc_wave_scan<true>(mx, lane);
-  if (lane == 63) s_w[wid] = inc;
-  __syncthreads();
-  unsigned long long pre = 0;
-  for (uint32_t w = 0; w < wid; ++w) pre = s_w[w] > pre ? s_w[w] : pre;
-  const unsigned long long up = __shfl_up(inc, 1, 64);
-  unsigned long long run = lane ? (up > pre ? up : pre) : pre;  // exclusive prefix of this thread's segment
-  for (uint64_t t = lo; t < hi; ++t) {
-    pmin[t] = run;
-    run = tmax[t] > run ? tmax[t] : run;
-  }
-}
-
-// ---- pass 2: the scan of one tile of packed words (TB threads; thread x
-// owns the run [x*TI, (x+1)*TI), staged through LDS).  carry = the largest
-// sink before the tile (pmin).  The start counts need no chain across tiles:
-//   CUT = false (k_fa_scan, all tiles at once): the tile's start count, its
-//     hmax = 2j - (starts of the tile before j) at its last start j > 0, and
-//     the records of ALL its elements.  Q1's condition j - before_j >= n - j
-//     is 2j - before_j >= n, increasing in j; with c_in starts before the
-//     tile it holds at the tile's last start iff hmax >= n + c_in, so the cut
-//     lies in the first tile where that holds, and every earlier tile is
-//     recorded whole;
-//   CUT = true (k_fa_finish, that one tile, c_in known): the cut and the
-//     records below it.
-// sh.out[0, FPART): cold, traversed, case 0/1/2 counts; sh.out[FPART]: the
-// start count (CUT: the cut); sh.out[FPART + 1]: hmax.  (Results go through
-// LDS: a store through a generic pointer here would keep the kernels' FaRefs
-// argument copied to scratch.)
-constexpr int FPW = FPART + 2;
-template <int SRC, int NT = TB, int EPT = TI>
-struct FaScanLds {
-  unsigned long long w[NT / 64], c[NT / 64], red[NT / 64][FPW], out[FPW];
-  unsigned long long rt[4];  // ri*T per case (KEY_EMPTY: cold; case 3: malformed)
-  fa_raw_t<SRC> raw[TILE + TILE / EPT];
-};
-// LDS slot of tile element e for runs of EPT elements per thread (one pad per run)
-template <int EPT>
-__device__ __forceinline__ uint32_t fa_slot_n(uint32_t e) { return e + e / EPT; }
-
-
-template <int SRC, bool P2, bool CUT, int NT, int EPT, bool FULLT>
-__device__ __forceinline__ void fa_tile_scan_t(const Model& m, const FaOne& o, unsigned long long carry_in,
-                                               uint64_t c_in, FaScanLds<SRC, NT, EPT>& sh) {
-  static_assert(NT * EPT == (int)TILE && EPT <= 16, "a tile is NT threads x EPT elements");
-  static_assert(SRC == SRC_W32 || SRC == SRC_W64, "the scan reads packed words");
-  using raw_t = fa_raw_t<SRC>;
-  constexpr int NW = NT / 64;
-  const FaTile& T = o.T;
-  constexpr bool full = FULLT;  // a whole tile: no per-element bounds in the loops below
-  // ri*T per case (KEY_EMPTY: a cold case; case 3 = a malformed word, already flagged)
-  unsigned long long rt[4];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) rt[c] = o.pv.ri[c] < 0 ? KEY_EMPTY : (unsigned long long)o.pv.ri[c] * m.T;
-  rt[3] = KEY_EMPTY;
-  if (threadIdx.x < 4) sh.rt[threadIdx.x] = rt[threadIdx.x & 3];
-  {
-    const raw_t* src = static_cast<const raw_t*>(o.src) + T.base;
-#pragma unroll
-    for (int k = 0; k < EPT; ++k) {
-      const uint32_t e = (uint32_t)k * NT + threadIdx.x;
-      if (full || e < T.mt) sh.raw[fa_slot_n<EPT>(e)] = src[e];
-    }
-    __syncthreads();
-  }
-  const uint32_t r = T.r;
-  const uint64_t n = o.n;
-  const unsigned long long endkey = m.A * m.T;
-  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  const uint32_t e0 = threadIdx.x * EPT;                                      // this lane's run in the tile
-  const uint32_t nv = e0 < T.mt ? (T.mt - e0 < EPT ? T.mt - e0 : EPT) : 0u;  // its valid elements
-  const uint64_t i0 = T.base + e0;                                            // index of its first element
-  // decode: keys in registers, cases (2 bits) and tid == 0 (at bit 2k) per
-  // element; sinks are recomputed from key and case where needed (registers
-  // for occupancy: this pass waits on its tile loads)
-  unsigned long long key[EPT];
-  auto sink_of = [&](unsigned long long kk, uint32_t c) -> unsigned long long {
-    const unsigned long long d = sh.rt[c];  // an LDS table: no divergent selects
-    const unsigned long long x = kk + d;    // d == KEY_EMPTY wraps below d: the max keeps KEY_EMPTY
-    return x > d ? x : d;
-  };
-  uint32_t cases = 0, t0s = 0;
-  unsigned long long lmax = 0;
-#pragma unroll
-  for (int k = 0; k < EPT; ++k) {
-    key[k] = KEY_EMPTY;
-    if (full || (uint32_t)k < nv) {
-      const raw_t w = sh.raw[fa_slot_n<EPT>(e0 + k)];
-      uint32_t c, t;
-      unsigned long long kk;
-      if (P2) {  // rank = ((q*N + c1)*N + c2)*T + tid; q*N + c1 < 2^32 (fa_run)
-        c = (uint32_t)w & 3u;
-        const raw_t rk = w >> 2;
-        t = (uint32_t)rk & (uint32_t)(o.pv.T - 1);
-        const uint32_t c2 = (uint32_t)(rk >> o.pv.tsh) & (uint32_t)(o.pv.N - 1);
-        const uint32_t qc = (uint32_t)(rk >> (o.pv.tsh + o.pv.nsh));
-        const uint64_t a = (uint64_t)qc * (uint32_t)m.S + ref_off(r, c2);
-        kk = (a << o.pv.tsh) | t;
-      } else {
-        const Elem e = elem_of_word<false>(m, o.pv, r, w);
-        kk = e.key;
-        c = e.c;
-        t = e.t0 ? 0u : 1u;
-      }
-      const unsigned long long sk = sink_of(kk, c);
-      key[k] = kk;
-      lmax = sk > lmax ? sk : lmax;
-      cases |= c << (2 * k);
-      t0s |= (t == 0 ? 1u : 0u) << (2 * k);
-    }
-  }
-  // running max of sinks entering this lane: the tile's incoming max, the
-  // earlier waves' maxima, the earlier lanes' maxima
-  const unsigned long long linc = sc_wave_scan<true>(lmax, lane);
-  if (lane == 63) sh.w[wid] = linc;
-  __syncthreads();
-  unsigned long long carry = carry_in;
-#pragma unroll
-  for (int x = 0; x < NW; ++x)
-    if (x < (int)wid) carry = sh.w[x] > carry ? sh.w[x] : carry;
-  {
-    const unsigned long long up = __shfl_up(linc, 1, 64);
-    if (lane) carry = up > carry ? up : carry;
-  }
-  // Start flags (key > the running max before it; the reference's first
-  // element) and, for the elements below lim, traversed: a replay starting
-  // at p subtracts key_p; the replay ending at p - 1 adds the running max
-  // there when p starts one, p == cut or p == n.  The end of a tile's last
-  // element is counted by the next tile (its first element's boundary).
-  uint32_t flags = 0;
-  unsigned long long tpos = 0, tneg = 0;
-  auto scan = [&](uint64_t lim, bool rec) {
-    unsigned long long run = carry;
-    flags = 0;
-#pragma unroll
-    for (int k = 0; k < EPT; ++k) {
-      if (full || (uint32_t)k < nv) {
-        const uint64_t p = i0 + k;
-        bool f = key[k] > run;
-        if (k == 0) f = f || i0 == 0;
-        flags |= (f ? 1u : 0u) << k;
-        if (rec) {
-          if (p < lim) {
-            if (f) {
-              tneg += key[k];
-              if (p != 0) tpos += run;  // f implies run is a sink (not KEY_EMPTY)
-            }
-          } else if (CUT && p == lim) {
-            tpos += run == KEY_EMPTY ? endkey : run;
-          }
-        }
-        const unsigned long long sk = sink_of(key[k], (cases >> (2 * k)) & 3u);
-        run = sk > run ? sk : run;
-      }
-    }
-    if (rec && nv && i0 + nv == n && n <= lim) tpos += run == KEY_EMPTY ? endkey : run;  // the last element ends
-  };
-  if (!CUT) scan(n, true);
-  else scan(n, false);
-  // start counts: lanes, then waves (the tile's total)
-  const uint32_t lcnt = (uint32_t)__popc(flags);
-  const uint32_t cinc = (uint32_t)sc_wave_scan<false>(lcnt, lane);
-  if (lane == 63) sh.c[wid] = cinc;
-  __syncthreads();
-  uint64_t cpre = 0, cagg = 0;
-#pragma unroll
-  for (int x = 0; x < NW; ++x) {
-    if (x < (int)wid) cpre += sh.c[x];
-    cagg += sh.c[x];
-  }
-  const uint64_t lb = cpre + (cinc - lcnt);  // starts of the tile before this lane's first element
-  uint64_t cut = n;
-  unsigned long long hl = 0;
-  if (CUT) {  // the first start j > 0 with j - before_j >= n - j; then the records below it
-    unsigned long long best = KEY_EMPTY;
-#pragma unroll
-    for (int k = 0; k < EPT; ++k) {
-      const uint64_t j = i0 + k;
-      const uint64_t before_j = c_in + lb + (uint64_t)__popc(flags & ((1u << k) - 1u));
-      if (best == KEY_EMPTY && ((flags >> k) & 1u) && j > 0 && j - before_j >= n - j) best = j;
-    }
-    best = sc_wave_red_min(best);
-    if (lane == 0) sh.red[wid][0] = best;
-    __syncthreads();
-#pragma unroll
-    for (int x = 0; x < NW; ++x) cut = sh.red[x][0] < cut ? sh.red[x][0] : cut;
-    __syncthreads();  // sh.red is reused below
-    scan(cut, true);
-  } else if (flags) {
-    const int k = 31 - __clz(flags);
-    const uint64_t j = i0 + k;
-    if (j > 0) hl = 2 * j - (lb + (uint64_t)__popc(flags & ((1u << k) - 1u)));
-  }
-  // recorded elements (below the cut) per case: recorded, or cold (tid 0 only)
-  const uint64_t nrec = cut <= i0 ? 0 : (cut - i0 < nv ? cut - i0 : nv);
-  const uint32_t rec2 = nrec >= 16 ? 0x55555555u : (uint32_t)((1ull << (2 * nrec)) - 1) & 0x55555555u;
-  const uint32_t lo = cases & rec2, hi = (cases >> 1) & rec2;
-  const uint32_t mc[3] = {rec2 & ~lo & ~hi, lo & ~hi, hi & ~lo};
-  unsigned long long packed = 0;  // cold | case 0 << 16 | case 1 << 32 | case 2 << 48 (each <= TILE per tile)
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    if (rt[c] == KEY_EMPTY) packed += (unsigned long long)__popc(mc[c] & t0s);
-    else packed += (unsigned long long)__popc(mc[c]) << (16 * (c + 1));
-  }
-  const unsigned long long v[3] = {sc_wave_red<false>(packed), sc_wave_red<false>(tpos - tneg),
-                                   CUT ? 0ull : sc_wave_red<true>(hl)};
-  if (lane == 0)
-#pragma unroll
-    for (int f = 0; f < 3; ++f) sh.red[wid][f] = v[f];
-  __syncthreads();
-  if (threadIdx.x < FPW) {
-    unsigned long long x = 0;
-    const uint32_t f = threadIdx.x;
-    if (f == FPART) {
-      x = CUT ? cut : cagg;
-    } else if (f == FPART + 1) {
-#pragma unroll
-      for (int w = 0; w < NW; ++w) x = sh.red[w][2] > x ? sh.red[w][2] : x;
-    } else if (f == 1) {
-#pragma unroll
-      for (int w = 0; w < NW; ++w) x += sh.red[w][1];
-    } else {  // 0 cold, 2..4 case counts
-      const uint32_t sh16 = f == 0 ? 0u : 16u * (f - 1);
-#pragma unroll
-      for (int w = 0; w < NW; ++w) x += (sh.red[w][0] >> sh16) & 0xFFFFull;
-    }
-    sh.out[f] = x;
-  }
-  __syncthreads();
-}
-
-template <int SRC, bool P2, bool CUT, int NT = TB, int EPT = TI>
-__device__ __forceinline__ void fa_tile_scan(const Model& m, const FaOne& o, unsigned long long carry_in,
-                                             uint64_t c_in, FaScanLds<SRC, NT, EPT>& sh) {
-  if (o.T.mt == TILE) fa_tile_scan_t<SRC, P2, CUT, NT, EPT, true>(m, o, carry_in, c_in, sh);
-  else fa_tile_scan_t<SRC, P2, CUT, NT, EPT, false>(m, o, carry_in, c_in, sh);
-}
-
-template <int SRC, bool P2>
-__global__ __launch_bounds__(TB) void k_fa_scan(Model m, FaRefs a, const unsigned long long* __restrict__ pmin,
-                                                unsigned long long* __restrict__ part, GTable g) {
-  __shared__ FaScanLds<SRC> sh;
-  const FaOne o = fa_one(a, blockIdx.x);
-  fa_tile_scan<SRC, P2, false>(m, o, pmin[blockIdx.x], 0, sh);
-  if (threadIdx.x < FPW) part[blockIdx.x * (uint64_t)FPW + threadIdx.x] = sh.out[threadIdx.x];
-}
-
-// ---- pass 3, one workgroup of FT threads per reference with samples: the
-// exclusive sum of its tiles' start counts locates the tile holding the Q1
-// cut (the first with hmax >= n + starts before it); the tiles before it are
-// summed whole, that tile is scanned again with its incoming start count
-// (CUT; FT threads x TILE/FT elements); then Q3 (nothing dropped: the owner
-// of the final largest sink stays in LAT, +1 cold if it is tid 0), the -1
-// key (materialised even with 0, r10:196,671), traversed and the bins.
-constexpr int FT = 1024;
-template <int SRC, bool P2>
-__global__ __launch_bounds__(FT) void k_fa_finish(Model m, FaRefs a, const unsigned long long* __restrict__ tmax,
-                                                  const unsigned long long* __restrict__ pmin,
-                                                  const unsigned long long* __restrict__ part,
-                                                  const unsigned long long* __restrict__ slots, GTable g) {
-  constexpr int NW = FT / 64;
-  __shared__ FaScanLds<SRC, FT, TILE / FT> sh;
-  __shared__ unsigned long long s_ct, s_red[NW][FPART];
-  const uint32_t r = blockIdx.x;
-  const uint64_t n = a.n[r];
-  if (n == 0) return;
-  const uint64_t t0 = a.toff[r], nt = a.toff[r + 1] - t0;
-  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  // read early (latency): the cold key's slot, the last tile's sinks (Q3)
-  const unsigned long long slot = slots[r];
-  const unsigned long long gl = tmax[t0 + nt - 1] > pmin[t0 + nt - 1] ? tmax[t0 + nt - 1] : pmin[t0 + nt - 1];
-  // 1. the cut tile; the partials of the tiles before it are summed on the way
-  uint64_t ct = nt, cin = 0, c = 0;
-  unsigned long long v[FPART] = {0, 0, 0, 0, 0};
-  if (nt > FT) {  // many tiles (2^24+ samples per reference): each thread a contiguous run of them
-    const uint64_t per = (nt + FT - 1) / FT;
-    const uint64_t lo = threadIdx.x * per < nt ? threadIdx.x * per : nt, hi = lo + per < nt ? lo + per : nt;
-    const unsigned long long* pt = part + t0 * FPW;
-    constexpr int FB = 8;  // loads of a batch in flight together
-    unsigned long long cs = 0;
-    for (uint64_t t = lo; t < hi; t += FB) {
-      unsigned long long x[FB];
-#pragma unroll
-      for (int k = 0; k < FB; ++k) x[k] = t + k < hi ? pt[(t + k) * FPW + FPART] : 0ull;
-#pragma unroll
-      for (int k = 0; k < FB; ++k) cs += x[k];
-    }
-    const unsigned long long inc = sc_wave_scan<false>(cs, lane);
-    if (lane == 63) sh.c[wid] = inc;
-    __syncthreads();
-    unsigned long long run = inc - cs;
-#pragma unroll
-    for (int x = 0; x < NW; ++x)
-      if (x < (int)wid) run += sh.c[x];
-    unsigned long long hit = KEY_EMPTY, hcin = 0;
-    for (uint64_t t = lo; t < hi; t += FB) {
-      unsigned long long x[FB], h[FB];
-#pragma unroll
-      for (int k = 0; k < FB; ++k) {
-        x[k] = t + k < hi ? pt[(t + k) * FPW + FPART] : 0ull;
-        h[k] = t + k < hi ? pt[(t + k) * FPW + FPART + 1] : 0ull;
-      }
-#pragma unroll
-      for (int k = 0; k < FB; ++k) {
-        if (hit == KEY_EMPTY && t + k < hi && h[k] >= n + run) {
-          hit = t + k;
-          hcin = run;
-        }
-        run += x[k];
-      }
-    }
-    const unsigned long long cand = sc_wave_red_min(hit);
-    if (lane == 0) sh.w[wid] = cand;
-    __syncthreads();
-    unsigned long long best = KEY_EMPTY;
-#pragma unroll
-    for (int x = 0; x < NW; ++x) best = sh.w[x] < best ? sh.w[x] : best;
-    if (best != KEY_EMPTY && hit == best) s_ct = hcin;
-    __syncthreads();
-    if (best != KEY_EMPTY) {  // block-uniform
-      ct = best;
-      cin = s_ct;
-    }
-    const uint64_t hi2 = hi < ct ? hi : ct;
-    for (uint64_t t = lo; t < hi2; t += FB / 2) {
-      unsigned long long x[FB / 2][FPART];
-#pragma unroll
-      for (int k = 0; k < FB / 2; ++k)
-#pragma unroll
-        for (int f = 0; f < FPART; ++f) x[k][f] = t + k < hi2 ? pt[(t + k) * FPW + f] : 0ull;
-#pragma unroll
-      for (int k = 0; k < FB / 2; ++k)
-#pragma unroll
-        for (int f = 0; f < FPART; ++f) v[f] += x[k][f];
-    }
-  } else
-  for (uint64_t b0 = 0; b0 < nt; b0 += FT) {  // one chunk: one tile per thread
-    const uint64_t t = b0 + threadIdx.x;
-    unsigned long long pw[FPW];
-#pragma unroll
-    for (int f = 0; f < FPW; ++f) pw[f] = t < nt ? part[(t0 + t) * FPW + f] : 0ull;
-    const unsigned long long cnt = pw[FPART], h = pw[FPART + 1];
-    const unsigned long long inc = sc_wave_scan<false>(cnt, lane);
-    if (lane == 63) sh.c[wid] = inc;
-    __syncthreads();
-    unsigned long long pre = c, tot = 0;
-#pragma unroll
-    for (int x = 0; x < NW; ++x) {
-      if (x < (int)wid) pre += sh.c[x];
-      tot += sh.c[x];
-    }
-    const unsigned long long excl = pre + inc - cnt;
-    const bool hit = t < nt && h >= n + excl;
-    const unsigned long long cand = sc_wave_red_min(hit ? t : KEY_EMPTY);
-    if (lane == 0) sh.w[wid] = cand;
-    __syncthreads();
-    unsigned long long best = KEY_EMPTY;
-#pragma unroll
-    for (int x = 0; x < NW; ++x) best = sh.w[x] < best ? sh.w[x] : best;
-    if (best == KEY_EMPTY || t < best)
-#pragma unroll
-      for (int f = 0; f < FPART; ++f) v[f] += pw[f];
-    if (best != KEY_EMPTY) {  // block-uniform
-      if (t == best) s_ct = excl;
-      __syncthreads();
-      ct = best;
-      cin = s_ct;
-      break;
-    }
-    c += tot;
-    __syncthreads();  // sh.c / sh.w are rewritten by the next chunk
-  }
-#pragma unroll
-  for (int f = 0; f < FPART; ++f) {
-    v[f] = sc_wave_red<false>(v[f]);
-    if (lane == 0) s_red[wid][f] = v[f];
-  }
-  // 2. the cut tile, below the cut
-  uint64_t cut = n;
-  if (ct < nt) {
-    __syncthreads();
-    const FaOne o = fa_one(a, t0 + ct);
-    fa_tile_scan<SRC, P2, true, FT, TILE / FT>(m, o, pmin[t0 + ct], cin, sh);
-  }
-  __syncthreads();
-  if (threadIdx.x < FPART) {  // one sum per thread, then plain no-return atomics
-    const uint32_t f = threadIdx.x;
-    unsigned long long x = 0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) x += s_red[w][f];
-    if (ct < nt) {
-      x += sh.out[f];
-      cut = sh.out[FPART];
-    }
-    if (f == 0) {  // cold; Q3: +1 when nothing was cut and the final largest sink's owner is tid 0
-      const unsigned long long tid = P2 ? (gl & (m.T - 1)) : gl % m.T;
-      if (cut == n && gl != KEY_EMPTY && tid == 0) x += 1;
-      if (slot != ~0ull && x) atomicAdd(&g.counts[slot], x);
-    } else if (f == 1) {
-      atomicAdd(&g.trav[r], x);
-    } else if (x) {
-      atomicAdd(&g.bins[r * 3 + (f - 2)], x);
-    }
-  }
-}
 
 // Record the shard's samples with global index < cut: RI bins, tid-0 cold
 // samples, and the traversed contributions of the replays that start or end
@@ -1664,7 +717,8 @@ static int fa_reserve(FaithfulBufs& b, uint64_t tiles, hipStream_t s) {
   if (tiles > b.dcap) {
     PLUSS_HIP_CHECK(hipStreamSynchronize(s));
     int rc = 0;
-    if ((rc = grow(&b.dpart, tiles * FPW)) || (rc = grow(&b.tmax, tiles)) || (rc = grow(&b.pmin, tiles)))
+    if ((rc = grow(&b.dpart, tiles * FPW)) || (rc = grow(&b.tmax, tiles)) || (rc = grow(&b.pmin, tiles)) ||
+        (rc = grow(&b.klist, tiles * 2 * KL)) || (rc = grow(&b.queue, tiles + 1)))
       return rc;
     b.dcap = tiles;
   }
@@ -1685,66 +739,23 @@ static int fa_run(pluss_ctx* ctx, FaRefs& a, int src, bool check, hipStream_t s)
   }
   a.toff[6] = t;
   if (t == 0) return PLUSS_OK;
+  if (src == SRC_SAMPLES && !check) {
+    set_error("faithful mode: a caller's list is always order-checked");
+    return PLUSS_ERR_CONFIG;
+  }
   FaithfulBufs& b = ctx->fb;
   if (int rc = fa_reserve(b, t, s)) return rc;
   const GTable& g = ctx->g;
-  // N, T, CS, CLS/DS powers of two: shift decoding (the scan's word decode
-  // also keeps q*N + c1 < N*N/T in 32 bits)
+  // N, T, CS, CLS/DS powers of two: shift decoding (the word decode also
+  // keeps q*N + c1 < N*N/T in 32 bits)
   const bool p2 = m.p2 && a.pv[0].p2 && (uint64_t)m.N * m.N / m.T < (1ull << 32);
-  // samples / generated lists: the first pass writes the packed sort words
-  // (4 or 8 bytes, as the radix path sorts them) and the scan reads those
-  const bool w32 = pk_bits(m) <= 32;
-  FaRefs aw = a;
-  if (src == SRC_SAMPLES || src == SRC_GEN) {
-    const size_t need = t * (size_t)TILE * (w32 ? 4 : 8);
-    if (need > b.words_bytes) {
-      PLUSS_HIP_CHECK(hipStreamSynchronize(s));
-      if (b.words) (void)hipFree(b.words);
-      b.words = nullptr;
-      b.words_bytes = 0;
-      if (hipMalloc(&b.words, need) != hipSuccess) {
-        set_error("hipMalloc failed for the faithful scan's word buffer");
-        return PLUSS_ERR_ALLOC;
-      }
-      b.words_bytes = need;
-    }
-    for (int r = 0; r < 6; ++r)
-      aw.src[r] = static_cast<char*>(b.words) + a.toff[r] * (uint64_t)TILE * (w32 ? 4 : 8);
-  }
-#define PLUSS_FA3(SRCV, CHK, P2V, WKV, SCANV)                                                                      \
-  do {                                                                                                             \
-    if constexpr (SRCV == SRC_GEN)                                                                                 \
-      hipLaunchKernelGGL((k_fa_max_gen<P2V, WKV>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.tmax, b.words, b.fslot, g);   \
-    else                                                                                                           \
-      hipLaunchKernelGGL((k_fa_max<SRCV, CHK, P2V, WKV>), dim3((unsigned)t), dim3(TB), 0, s, m, a, b.tmax, b.words, \
-                         b.fslot, g);                                                                                       \
-    hipLaunchKernelGGL(k_fa_prefix, dim3(6), dim3(PB), 0, s, a, b.tmax, b.pmin);                                   \
-    hipLaunchKernelGGL((k_fa_scan<SCANV, P2V>), dim3((unsigned)t), dim3(TB), 0, s, m, aw, b.pmin, b.dpart, g);    \
-    hipLaunchKernelGGL((k_fa_finish<SCANV, P2V>), dim3(6), dim3(FT), 0, s, m, aw, b.tmax, b.pmin, b.dpart, b.fslot, \
-                       g);    \
-  } while (0)
-#define PLUSS_FA2(SRCV, CHK, WKV, SCANV)            \
-  do {                                              \
-    if (p2) PLUSS_FA3(SRCV, CHK, true, WKV, SCANV); \
-    else PLUSS_FA3(SRCV, CHK, false, WKV, SCANV);   \
-  } while (0)
-#define PLUSS_FA(SRCV, CHK)                    \
-  do {                                         \
-    if (w32) PLUSS_FA2(SRCV, CHK, 4, SRC_W32); \
-    else PLUSS_FA2(SRCV, CHK, 8, SRC_W64);     \
-  } while (0)
+  const FaLaunch L{m, a, g, &b, p2, t, s};
   switch (src) {
-    case SRC_W32: PLUSS_FA2(SRC_W32, false, 0, SRC_W32); break;
-    case SRC_W64: PLUSS_FA2(SRC_W64, false, 0, SRC_W64); break;
-    case SRC_SAMPLES:
-      if (check) PLUSS_FA(SRC_SAMPLES, true);
-      else PLUSS_FA(SRC_SAMPLES, false);
-      break;
-    default: PLUSS_FA(SRC_GEN, false); break;
+    case SRC_W32: fa_launch_w32(L); break;
+    case SRC_W64: fa_launch_w64(L); break;
+    case SRC_SAMPLES: fa_launch_smp(L); break;
+    default: fa_launch_gen(L); break;
   }
-#undef PLUSS_FA
-#undef PLUSS_FA2
-#undef PLUSS_FA3
   PLUSS_HIP_CHECK(hipGetLastError());
   ctx->tables_dirty = true;
   return PLUSS_OK;

@@ -63,13 +63,12 @@ struct FaithfulBufs {
   size_t tmp_bytes = 0;
   unsigned long long* scal = nullptr;  // [0] cut, [1] cold, [2] traversed, [3] shard size, [4] scan tile counter
   unsigned long long* st = nullptr;    // look-back status words of the one-GPU scan (2 per tile)
-  // the scan pipeline (pluss_faithful.hip k_fa_*): per tile the partials, the largest sink and the
-  // running max entering it
+  // the scan pipeline (pluss_faithful.hip k_fa_*): per tile the partials, the largest sink, the
+  // running max entering it, its first local starts; the queue of tiles to scan again
   uint64_t dcap = 0;
-  unsigned long long *dpart = nullptr, *tmax = nullptr, *pmin = nullptr;
+  unsigned long long *dpart = nullptr, *tmax = nullptr, *pmin = nullptr, *klist = nullptr;
+  unsigned int* queue = nullptr;
   unsigned long long* fslot = nullptr;  // per reference: the main-table slot of its -1 (cold) key
-  void* words = nullptr;  // packed sort words written by the first pass (sample / generated sources)
-  size_t words_bytes = 0;
 };
 
 // state of a key-range shard between the phases of pluss_dev_faithful_shard_*

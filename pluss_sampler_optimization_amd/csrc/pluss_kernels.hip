@@ -963,14 +963,7 @@ __global__ __launch_bounds__(BLOCK) void k_ri_dump(Model m, const uint64_t* __re
 __global__ __launch_bounds__(BLOCK) void k_expand(Perm p, uint32_t ref, uint64_t first, uint64_t n,
                                                   uint64_t* __restrict__ out) {
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
-    uint64_t y = perm_apply(p, first + i);
-    uint64_t c2 = 0;
-    if (p.dim3) {
-      c2 = y % p.span;
-      y /= p.span;
-    }
-    const uint64_t c1 = y % p.span, c0 = y / p.span;
-    out[i] = pack(ref, (uint32_t)c0, (uint32_t)c1, (uint32_t)c2);
+    out[i] = perm_sample(p, ref, perm_apply(p, first + i));
   }
 }
 

@@ -276,44 +276,6 @@ PM_HD void position(const Model& m, uint32_t ref, uint32_t c0, uint32_t c1, uint
   *tid = t;
 }
 
-// ---- sample-list bijection (cycle-walking 4-round Feistel; DESIGN.md §4) ----
-PM_HD uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-struct Perm {
-  uint64_t key[4];
-  uint64_t D, mask, span;  // domain size, half mask, radix
-  uint32_t h, dim3;
-};
-inline Perm make_perm(uint64_t seed, uint32_t ref, uint64_t span, bool dim3) {
-  Perm p;
-  p.dim3 = dim3;
-  p.span = span;
-  p.D = dim3 ? span * span * span : span * span;
-  uint32_t h = 1;
-  while ((1ull << (2 * h)) < p.D) ++h;
-  p.h = h;
-  p.mask = (1ull << h) - 1;
-  for (int r = 0; r < 4; ++r)
-    p.key[r] = mix64(seed ^ ((uint64_t)(ref + 1) * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)(r + 1) * 0xD1B54A32D192ED03ull));
-  return p;
-}
-PM_HD uint64_t perm_apply(const Perm& p, uint64_t y) {
-  do {
-    uint64_t L = y >> p.h, R = y & p.mask;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      uint64_t t = R;
-      R = L ^ (mix64(p.key[r] ^ R) & p.mask);
-      L = t;
-    }
-    y = (L << p.h) | R;
-  } while (y >= p.D);
-  return y;
-}
-
 // ---- key-order stratified sample lists ----------------------
 // A reference's list generated directly in the order r10 pops its samples
 // (IterationComp, pluss_utils.h:175-267 = key a*T+tid when N % (CS*T) == 0),
@@ -327,6 +289,12 @@ PM_HD uint64_t perm_apply(const Perm& p, uint64_t y) {
 // stratum [j*g + min(j, rr), +g + (j < rr)) (g = DX / SX, rr = DX % SX) and
 // sits at a keyed pseudo-random offset in it: distinct, strictly increasing
 // keys, random access by sample index (any rank can generate any slice).
+
+PM_HD uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
 
 // 64-bit division by a run-time invariant d >= 1 (round-up multiplier, any
 // 64-bit numerator; Granlund-Montgomery).
@@ -366,6 +334,60 @@ PM_HD uint32_t lowbias32(uint32_t x) {  // 32-bit integer hash (xorshift-multipl
   x *= 0x846ca68bu;
   x ^= x >> 16;
   return x;
+}
+
+// ---- sample-list bijection (cycle-walking 4-round Feistel; DESIGN.md §4) ----
+// Sample i of reference r is decode(F(i)), F a Feistel permutation of
+// [0, 2^2h) walked until it lands in [0, D), D = span^d.  D <= 2^60, so each
+// half is at most 30 bits and a round is 32-bit integer work: R' = L ^
+// (lowbias32(R ^ k_r) & mask), with 32-bit round keys from splitmix64 of
+// (seed, ref, round).  The index -> (c0, c1, c2) decode divides by span
+// with a precomputed multiplier.
+struct Perm {
+  uint32_t key[4];
+  uint64_t D, mask, span;  // domain size, half mask, radix
+  uint32_t h, dim3;
+  Div64 dspan;
+};
+inline Perm make_perm(uint64_t seed, uint32_t ref, uint64_t span, bool dim3) {
+  Perm p;
+  p.dim3 = dim3;
+  p.span = span;
+  p.D = dim3 ? span * span * span : span * span;
+  uint32_t h = 1;
+  while ((1ull << (2 * h)) < p.D) ++h;
+  p.h = h;
+  p.mask = (1ull << h) - 1;
+  for (int r = 0; r < 4; ++r)
+    p.key[r] = (uint32_t)mix64(seed ^ ((uint64_t)(ref + 1) * 0x9E3779B97F4A7C15ull) ^
+                               ((uint64_t)(r + 1) * 0xD1B54A32D192ED03ull));
+  p.dspan = make_div64(span ? span : 1);
+  return p;
+}
+PM_HD uint64_t perm_apply(const Perm& p, uint64_t y) {
+  const uint32_t mask = (uint32_t)p.mask;
+  do {
+    uint32_t L = (uint32_t)(y >> p.h), R = (uint32_t)y & mask;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t t = R;
+      R = L ^ (lowbias32(R ^ p.key[r]) & mask);
+      L = t;
+    }
+    y = ((uint64_t)L << p.h) | R;
+  } while (y >= p.D);
+  return y;
+}
+// packed sample of permuted index y (mixed radix span: c0, c1[, c2])
+PM_HD uint64_t perm_sample(const Perm& p, uint32_t ref, uint64_t y) {
+  uint64_t c2 = 0;
+  if (p.dim3) {
+    const uint64_t q = div64(y, p.dspan);
+    c2 = y - q * p.span;
+    y = q;
+  }
+  const uint64_t c0 = div64(y, p.dspan), c1 = y - c0 * p.span;
+  return pack(ref, (uint32_t)c0, (uint32_t)c1, (uint32_t)c2);
 }
 
 struct KeyGen {
