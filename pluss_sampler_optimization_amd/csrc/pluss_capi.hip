@@ -174,11 +174,11 @@ int pluss_ctx_destroy(pluss_ctx* c) {
   void* bufs[] = {c->d_table,  c->d_exp_keys, c->d_exp_counts, c->d_exp_n, c->fb.keys,  c->fb.sinks,
                   c->fb.keys_s, c->fb.sinks_s, c->fb.pmax,      c->fb.nstart, c->fb.tmp,
                   c->fb.scal, c->fb.st, c->fb.dpart, c->fb.tmax, c->fb.pmin, c->fb.fslot,
-                  c->fb.klist, c->fb.queue};
+                  c->fb.klist, c->fb.queue, c->fb.slowq};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (const auto& f : c->fbr) {
-    void* fr[] = {f.keys, f.sinks, f.keys_s, f.sinks_s, f.pmax, f.nstart, f.tmp, f.scal, f.st, f.dpart, f.tmax, f.pmin, f.fslot, f.klist, f.queue};
+    void* fr[] = {f.keys, f.sinks, f.keys_s, f.sinks_s, f.pmax, f.nstart, f.tmp, f.scal, f.st, f.dpart, f.tmax, f.pmin, f.fslot, f.klist, f.queue, f.slowq};
     for (void* p : fr)
       if (p) (void)hipFree(p);
   }

@@ -158,6 +158,7 @@ struct FaRefs {
   const void* src[6];  // SRC_W*: sorted packed words; SRC_SAMPLES: the key-ordered samples
   PkView pv[6];
   KeyGen kg[6];        // SRC_GEN
+  uint32_t fast;       // the local pass's fast path applies to the shape (fa_run)
 };
 
 // key, sink, case (3: malformed, flagged) and tid == 0 of one element.  P2:
@@ -281,10 +282,14 @@ __device__ __forceinline__ void fa_cold_slot(const FaTile& T, GTable g, unsigned
 constexpr int PB = 1024;
 template <int SRC>  // (instantiated in each source's translation unit)
 __global__ __launch_bounds__(PB) void k_fa_prefix(FaRefs a, const unsigned long long* __restrict__ tmax,
-                                                  unsigned long long* __restrict__ pmin, unsigned int* queue) {
+                                                  unsigned long long* __restrict__ pmin, unsigned int* queue,
+                                                  unsigned int* slowq) {
   __shared__ unsigned long long s_w[PB / 64];
   const uint32_t r = blockIdx.x;
-  if (r == 0 && threadIdx.x == 0) queue[0] = 0;
+  if (r == 0 && threadIdx.x == 0) {  // the rescan queue starts empty; the slow-tile queue is left empty (it was read)
+    queue[0] = 0;
+    slowq[0] = 0;
+  }
   const uint64_t t0 = a.toff[r], nt = a.toff[r + 1] - t0;
   if (nt == 0) return;
   const uint64_t per = (nt + PB - 1) / PB;
@@ -738,16 +743,307 @@ __device__ __forceinline__ void fa_scan_local32(const FaOne& o, const unsigned l
   __syncthreads();
 }
 
-// ---- pass 1: every tile as if nothing entered it
+// ---- the local pass's fast path: a full tile of a shape with N, T, CS and
+// CLS/DS powers of two and q*N + c1, S below 2^24 (every BASELINE shape),
+// whose keys and non-cold sinks lie within 2^32 - 1 of its first key (every
+// dense tile).  Each element is decoded straight from its bits to the low 32
+// bits of its key (one 24-bit multiply-add), its case flags and tid == 0;
+// everything after that is 32-bit: offsets from the tile's first key, cold
+// sinks saturated to 0xFFFFFFFF, counts accumulated per thread, wave scans
+// by DPP.
+template <int SRC>
+__device__ __forceinline__ fa_raw_t<SRC> src_at(const FaOne& o, uint32_t e) {
+  return static_cast<const fa_raw_t<SRC>*>(o.src)[o.T.base + e];
+}
+
+struct FaDec {
+  uint32_t lk;             // low 32 bits of the key a*T + tid
+  bool a, b, t0;           // case 0 = a, case 1 = !a && b, case 2 = neither; tid == 0
+  unsigned long long key;  // the whole key (CHECK: the order check)
+};
+
+template <uint32_t REF, bool KEY64>
+__device__ __forceinline__ FaDec fa_dec_digits(const Model& m, const PkView& v, uint32_t q, uint32_t c1, uint32_t c2,
+                                               uint32_t t) {
+  FaDec d;
+  const uint32_t qc = (q << v.nsh) | c1;
+  const uint32_t off = ref_off(REF, c2);
+  if (KEY64) {
+    d.key = ((((uint64_t)qc * m.S) + off) << v.tsh) | t;
+    d.lk = (uint32_t)d.key;
+  } else {
+    d.key = 0;
+    d.lk = ((__umul24(qc, m.S) + off) << v.tsh) | t;
+  }
+  const uint32_t Wm1 = m.W - 1;
+  d.a = true;
+  d.b = true;
+  if (REF == C3) {
+    d.a = c2 + 1 < m.N;
+    d.b = (c1 & Wm1) != Wm1;
+  } else if (REF == A0) {
+    d.a = (c2 & Wm1) != Wm1;
+    d.b = c1 + 1 < m.N;
+  } else if (REF == B0) {
+    d.a = (c1 & Wm1) != Wm1;
+    d.b = q + 1 < v.Q;
+  }
+  d.t0 = t == 0;
+  return d;
+}
+
+// a caller's packed sample ref(4)|c0(20)|c1(20)|c2(20); `odd` collects the
+// bits of another reference or of an index >= N (N a power of two)
+template <uint32_t REF, bool KEY64>
+__device__ __forceinline__ FaDec fa_dec_sample(const Model& m, const PkView& v, uint64_t x, uint32_t& odd) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  odd |= ((hi ^ (REF << 28)) & (0xF0000000u | m.badhi)) | (lo & m.badlo);
+  const uint32_t c2 = (REF == C0 || REF == C1) ? 0u : (lo & 0xFFFFFu);
+  const uint32_t c1 = __builtin_amdgcn_alignbit(hi, lo, 20) & 0xFFFFFu;
+  const uint32_t cs = m.csshift, ts = v.tsh;
+  const uint32_t t = __builtin_amdgcn_ubfe(hi, 8 + cs, ts);
+  const uint32_t q = (__builtin_amdgcn_ubfe(hi, 8 + cs + ts, 20 - cs - ts) << cs) | __builtin_amdgcn_ubfe(hi, 8, cs);
+  return fa_dec_digits<REF, KEY64>(m, v, q, c1, c2, t);
+}
+
+// a packed sort word rank << 2 | case, rank = ((q*N + c1)*N + c2)*T + tid
+template <uint32_t REF, typename KT>
+__device__ __forceinline__ FaDec fa_dec_word(const Model& m, const PkView& v, KT w) {
+  const uint32_t c = (uint32_t)w & 3u;
+  const uint32_t t = ((uint32_t)w >> 2) & (uint32_t)(v.T - 1);
+  const uint32_t c2 = (uint32_t)(w >> (2 + v.tsh)) & (uint32_t)(v.N - 1);
+  const uint32_t qc = (uint32_t)(w >> (2 + v.tsh + v.nsh));
+  FaDec d;
+  d.key = 0;
+  d.lk = ((__umul24(qc, m.S) + ref_off(REF, c2)) << v.tsh) | t;
+  d.a = c == 0;
+  d.b = c == 1;
+  d.t0 = t == 0;
+  return d;
+}
+
+// inclusive 32-bit wave scan (identity 0), Hillis-Steele by DPP: row_shr
+// 1/2/4/8 inside rows of 16 lanes, then row_bcast 15 and 31 across rows
+template <bool MAX>
+__device__ __forceinline__ uint32_t dpp_op(uint32_t a, uint32_t b) { return MAX ? (a > b ? a : b) : a + b; }
+template <bool MAX>
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
+  v = dpp_op<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+  v = dpp_op<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+  v = dpp_op<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+  v = dpp_op<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+  v = dpp_op<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+  v = dpp_op<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+  return v;
+}
+// the previous lane's value (lane 0: 0)
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(v), 63);
+}
+
+template <int SRC, bool CHECK, uint32_t REF>
+__device__ __forceinline__ void fa_local_fast(const Model& m, const FaOne& o, const KeyGen& kg,
+                                              FaLds<SRC, TB, TI>& sh, unsigned long long base, const uint32_t (&r)[3],
+                                              unsigned long long* __restrict__ klist, GTable g) {
+  constexpr int NW = TB / 64;
+  const FaTile& T = o.T;
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  const uint32_t e0 = threadIdx.x * TI;
+  const uint64_t i0 = T.base + e0;
+  const uint32_t b32 = (uint32_t)base;
+  uint32_t rk[TI], sk[TI], lmax = 0, n0 = 0, n1 = 0, nc = 0, odd = 0;
+  bool unordered = false;
+  unsigned long long kfirst = 0, kprev = 0;
+  KeyRunF run;
+  if constexpr (SRC == SRC_GEN) keyrunf_start(kg, run, T.base + e0);
+#pragma unroll
+  for (int k = 0; k < TI; ++k) {
+    FaDec d;
+    if constexpr (SRC == SRC_SAMPLES) {
+      d = fa_dec_sample<REF, CHECK>(m, o.pv, sh.raw[fa_slot_n<TI>(e0 + k)], odd);
+    } else if constexpr (SRC == SRC_GEN) {
+      const KeyDigits dg = keyrunf_digits(kg, run);
+      keyrunf_next(kg, run);
+      d = fa_dec_digits<REF, false>(m, o.pv, dg.q, dg.c1, dg.c2, dg.t);
+    } else {
+      d = fa_dec_word<REF>(m, o.pv, sh.raw[fa_slot_n<TI>(e0 + k)]);
+    }
+    if (CHECK) {
+      if (k == 0) kfirst = d.key;
+      else unordered |= !(d.key > kprev);
+      kprev = d.key;
+    }
+    rk[k] = d.lk - b32;
+    const uint32_t dd = d.a ? r[0] : (d.b ? r[1] : r[2]);
+    const uint32_t x = rk[k] + dd;  // dd = 0xFFFFFFFF (cold) wraps below dd: the max keeps it
+    sk[k] = x > dd ? x : dd;
+    lmax = sk[k] > lmax ? sk[k] : lmax;
+    n0 += d.a ? 1u : 0u;
+    n1 += (!d.a && d.b) ? 1u : 0u;
+    nc += (!d.a && !d.b && d.t0) ? 1u : 0u;
+  }
+  if (CHECK) {  // across lanes, waves and the tile's start (the element before it)
+    const unsigned long long up = __shfl_up(kprev, 1, 64);
+    if (lane > 0) unordered |= !(kfirst > up);
+    if (lane == 63) sh.klast[wid] = kprev;
+  }
+  // running max of sinks entering this lane
+  const uint32_t linc = wave_scan_dpp<true>(lmax);
+  if (lane == 63) sh.w[wid] = linc;
+  __syncthreads();
+  if (CHECK) {
+    if (lane == 0 && wid > 0) unordered |= !(kfirst > sh.klast[wid - 1]);
+    if (threadIdx.x == 0 && T.base > 0) {
+      bool b2 = false;
+      const fa_raw_t<SRC> w = static_cast<const fa_raw_t<SRC>*>(o.src)[T.base - 1];
+      unordered |= !(kfirst > fa_decode_ref<SRC, true, REF>(m, o.pv, w, b2).key);
+    }
+    if (__ballot(odd != 0 || unordered) && lane == 0) atomicOr(&g.flags[1], 1u);
+  }
+  uint32_t carry = wave_shr1(linc), tm = 0;
+#pragma unroll
+  for (int x = 0; x < NW; ++x) {
+    const uint32_t w = (uint32_t)sh.w[x];
+    if (x < (int)wid) carry = w > carry ? w : carry;
+    tm = w > tm ? w : tm;
+  }
+  uint32_t flags = 0, dsum = 0;  // dsum: key - run over the starts (the tile's first excluded)
+  {
+    uint32_t rn = carry;
+#pragma unroll
+    for (int k = 0; k < TI; ++k) {
+      const bool f = rk[k] > rn || (k == 0 && e0 == 0);
+      flags |= (f ? 1u : 0u) << k;
+      dsum += __builtin_elementwise_sub_sat(rk[k], rn);  // key - run of a start, 0 otherwise (and for the tile's first)
+      rn = sk[k] > rn ? sk[k] : rn;
+    }
+  }
+  const uint32_t lcnt = (uint32_t)__popc(flags);
+  const uint32_t cinc = wave_scan_dpp<false>(lcnt);
+  // the wave's last start: its global index (the tile's last start has every other start of the tile before it)
+  const unsigned long long hasf = __ballot(flags != 0);
+  unsigned long long jl = 0;
+  if (hasf) {
+    const int ll = 63 - __builtin_clzll(hasf);
+    const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)flags, ll);
+    jl = T.base + (uint64_t)(wid * 64 + ll) * TI + (31 - __clz(fl)) + 1;  // + 1: 0 = none
+  }
+  // per-thread records -> wave sums (DPP), then LDS
+  const uint32_t s0 = wave_sum_dpp(n0), s1 = wave_sum_dpp(n1), sc = wave_sum_dpp(nc), sd = wave_sum_dpp(dsum);
+  if (lane == 63) {
+    sh.c[wid] = cinc;
+    sh.red[wid][0] = s0;
+    sh.red[wid][1] = s1;
+    sh.red[wid][2] = sc;
+    sh.red[wid][3] = sd;
+    sh.red[wid][4] = jl;
+  }
+  __syncthreads();
+  uint64_t cpre = 0, cagg = 0;
+#pragma unroll
+  for (int x = 0; x < NW; ++x) {
+    if (x < (int)wid) cpre += sh.c[x];
+    cagg += sh.c[x];
+  }
+  const uint64_t lb = cpre + (cinc - lcnt);
+  if (lb < (uint64_t)KL && flags) {  // the tile's first KL local starts (absolute key, running max before it)
+    uint64_t rank = lb;
+    uint32_t rn = carry;
+#pragma unroll
+    for (int k = 0; k < TI; ++k) {
+      if (((flags >> k) & 1u) && rank < (uint64_t)KL) {
+        klist[2 * rank] = base + rk[k];
+        klist[2 * rank + 1] = (k == 0 && e0 == 0) ? 0ull : base + rn;
+      }
+      rank += (flags >> k) & 1u;
+      rn = sk[k] > rn ? sk[k] : rn;
+    }
+  }
+  if (threadIdx.x < FPW + 1) {
+    const uint32_t f = threadIdx.x;
+    unsigned long long x = 0;
+    if (f == FPART) {
+      x = cagg;
+    } else if (f == FPART + 1) {  // hmax = 2j - (starts before j) at the last start j > 0
+      unsigned long long j = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) j = sh.red[w][4] > j ? sh.red[w][4] : j;
+      x = j > 1 ? 2 * (j - 1) - (cagg - 1) : 0ull;
+    } else if (f == FPW) {
+      x = tm == 0xFFFFFFFFu ? KEY_EMPTY : base + tm;
+    } else if (f == 1) {  // traversed: -base (the first start, nothing before it) - sum(key - run)
+#pragma unroll
+      for (int w = 0; w < NW; ++w) x += sh.red[w][3];
+      x = 0ull - base - x;
+    } else {  // 0: cold (tid 0) of case 2 when it is cold; 2..4: case 0/1/2 counts (case 2 when not cold)
+      unsigned long long a0 = 0, a1 = 0, ac = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        a0 += sh.red[w][0];
+        a1 += sh.red[w][1];
+        ac += sh.red[w][2];
+      }
+      const bool cold2 = r[2] == 0xFFFFFFFFu;
+      x = f == 0 ? (cold2 ? ac : 0ull) : f == 2 ? a0 : f == 3 ? a1 : (cold2 ? 0ull : TILE - a0 - a1);
+    }
+    sh.out[f] = x;
+  }
+  __syncthreads();
+}
+
+// ---- pass 1: every tile as if nothing entered it.  The fast path (a full
+// tile of a shape with FaRefs::fast whose keys lie within 2^32 - 1 minus the
+// longest reuse of its first key; tile-uniform) in k_fa_local_fast; the tiles
+// it leaves (partial or wide ones) and shapes without it in k_fa_local.
+template <int SRC, bool CHECK, uint32_t REF>
+__device__ __forceinline__ bool fa_local_try_fast(const Model& m, const FaOne& o, const KeyGen& kg,
+                                                  FaLds<SRC, TB, TI>& sh, unsigned long long* __restrict__ klist,
+                                                  GTable g) {
+  fa_rt(m, o.pv, sh);
+  if constexpr (SRC != SRC_GEN) {
+    const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(o.src) + o.T.base;
+#pragma unroll
+    for (int k = 0; k < TI; ++k) sh.raw[fa_slot_n<TI>((uint32_t)k * TB + threadIdx.x)] = src[k * TB + threadIdx.x];
+  }
+  if (threadIdx.x < 2) {  // the first and the last key, in 64 bits
+    const uint32_t e = threadIdx.x ? TILE - 1 : 0;
+    bool b2 = false;
+    if constexpr (SRC == SRC_GEN)
+      sh.kb[threadIdx.x] = elem_of_digits<true>(m, o.pv, REF, keygen_digits_at(kg, o.T.base + e)).key;
+    else
+      sh.kb[threadIdx.x] = fa_decode_ref<SRC, true, REF>(m, o.pv, src_at<SRC>(o, e), b2).key;
+  }
+  __syncthreads();
+  const unsigned long long base = sh.kb[0], kl = sh.kb[1];
+  uint32_t r[3];
+  unsigned long long rmax = 0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const unsigned long long x = sh.rt[c];
+    r[c] = x == KEY_EMPTY ? 0xFFFFFFFFu : (uint32_t)x;
+    rmax = x != KEY_EMPTY && x > rmax ? x : rmax;
+  }
+  if (kl >= base && kl - base < 0xFFFFFFFFull - rmax && r[0] != 0xFFFFFFFFu && r[1] != 0xFFFFFFFFu &&
+      (SRC != SRC_GEN || keyrun_fast_ok(kg, o.T.base, TILE))) {
+    fa_local_fast<SRC, CHECK, REF>(m, o, kg, sh, base, r, klist + blockIdx.x * (uint64_t)(2 * KL), g);
+    return true;
+  }
+  return false;
+}
+
 template <int SRC, bool P2, bool CHECK, uint32_t REF, bool FULLT>
-__device__ __forceinline__ void fa_local_tile(const Model& m, const FaOne& o, const KeyGen& kg,
+__device__ __forceinline__ void fa_local_tile(const Model& m, const FaOne& o, const KeyGen& kg, uint64_t gt,
                                               FaLds<SRC, TB, TI>& sh, unsigned long long* __restrict__ tmax,
                                               unsigned long long* __restrict__ part,
                                               unsigned long long* __restrict__ klist, GTable g) {
+  unsigned long long* kl_out = klist + gt * (uint64_t)(2 * KL);
+  fa_rt(m, o.pv, sh);
   unsigned long long key[TI];
   uint32_t cases, t0s;
   bool bad = false;
-  fa_rt(m, o.pv, sh);
   fa_load_run<SRC, P2, REF, TB, TI, FULLT>(m, o, kg, sh, key, cases, t0s, bad);
   bool unordered = false;
   if constexpr (CHECK) unordered = fa_unordered<SRC, P2, REF, TB, TI, FULLT>(m, o, key, sh, bad);
@@ -768,13 +1064,12 @@ __device__ __forceinline__ void fa_local_tile(const Model& m, const FaOne& o, co
   unsigned long long rmax = 0;
 #pragma unroll
   for (int c = 0; c < 3; ++c) rmax = sh.rt[c] != KEY_EMPTY && sh.rt[c] > rmax ? sh.rt[c] : rmax;
-  unsigned long long* kl_out = klist + blockIdx.x * (uint64_t)(2 * KL);
   if (kl >= base && kl - base < 0xFFFFFFFFull - rmax)  // (a flagged list's result is never read)
     fa_scan_local32<SRC, TB, TI, FULLT>(o, key, cases, t0s, base, sh, kl_out);
   else
     fa_scan<FA_LOCAL, SRC, TB, TI, FULLT>(m, o, key, cases, t0s, 0, 0, sh, kl_out);
-  if (threadIdx.x < FPW) part[blockIdx.x * (uint64_t)FPW + threadIdx.x] = sh.out[threadIdx.x];
-  if (threadIdx.x == FPW) tmax[blockIdx.x] = sh.out[FPW];
+  if (threadIdx.x < FPW) part[gt * FPW + threadIdx.x] = sh.out[threadIdx.x];
+  if (threadIdx.x == FPW) tmax[gt] = sh.out[FPW];
 }
 
 // Per-reference dispatch (tile-uniform switch; the reference's view, source
@@ -798,22 +1093,57 @@ __device__ __forceinline__ FaOne fa_one_ref(const FaRefs& a, const FaTile& T) {
   return o;
 }
 
-template <int SRC, bool P2, bool CHECK>
+// Tiles: every tile (list == nullptr), or the tiles queued in list (list[0]
+// = count, then tile indices; a grid of resident workgroups over it).
+template <int SRC, bool P2, bool CHECK, bool LIST>
 __global__ __launch_bounds__(TB) void k_fa_local(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
                                                  unsigned long long* __restrict__ part,
                                                  unsigned long long* __restrict__ klist, unsigned long long* slots,
-                                                 GTable g) {
+                                                 const unsigned int* list, GTable g) {
+  __shared__ FaLds<SRC, TB, TI> sh;
+  const uint32_t nl = LIST ? list[0] : 1u;
+  for (uint32_t q = LIST ? blockIdx.x : 0u; q < nl; q += gridDim.x) {
+    const uint64_t gt = LIST ? list[1 + q] : blockIdx.x;
+    const FaTile T = fa_tile(a, gt);
+    if (!LIST) fa_cold_slot(T, g, slots);
+#define PLUSS_FA_LOCAL(R)                                                                                 \
+  const FaOne o = fa_one_ref<SRC, R>(a, T);                                                               \
+  KeyGen kg;                                                                                              \
+  if constexpr (SRC == SRC_GEN) kg = a.kg[R];                                                             \
+  if (T.mt == TILE) fa_local_tile<SRC, P2, CHECK, R, true>(m, o, kg, gt, sh, tmax, part, klist, g);       \
+  else fa_local_tile<SRC, P2, CHECK, R, false>(m, o, kg, gt, sh, tmax, part, klist, g);
+    PLUSS_FA_REFS(PLUSS_FA_LOCAL)
+#undef PLUSS_FA_LOCAL
+    __syncthreads();  // sh is reused by the next queued tile
+  }
+}
+
+// The fast path over every tile (shapes with FaRefs::fast); the tiles it
+// cannot take are queued in slowq for k_fa_local.
+template <int SRC, bool CHECK>
+__global__ __launch_bounds__(TB) void k_fa_local_fast(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
+                                                      unsigned long long* __restrict__ part,
+                                                      unsigned long long* __restrict__ klist,
+                                                      unsigned long long* slots, unsigned int* slowq, GTable g) {
   __shared__ FaLds<SRC, TB, TI> sh;
   const FaTile T = fa_tile(a, blockIdx.x);
   fa_cold_slot(T, g, slots);
-#define PLUSS_FA_LOCAL(R)                                                                              \
-  const FaOne o = fa_one_ref<SRC, R>(a, T);                                                            \
-  KeyGen kg;                                                                                           \
-  if constexpr (SRC == SRC_GEN) kg = a.kg[R];                                                          \
-  if (T.mt == TILE) fa_local_tile<SRC, P2, CHECK, R, true>(m, o, kg, sh, tmax, part, klist, g);        \
-  else fa_local_tile<SRC, P2, CHECK, R, false>(m, o, kg, sh, tmax, part, klist, g);
-  PLUSS_FA_REFS(PLUSS_FA_LOCAL)
-#undef PLUSS_FA_LOCAL
+  bool done = false;
+  if (T.mt == TILE) {
+#define PLUSS_FA_FAST(R)                                            \
+  const FaOne o = fa_one_ref<SRC, R>(a, T);                         \
+  KeyGen kg;                                                        \
+  if constexpr (SRC == SRC_GEN) kg = a.kg[R];                       \
+  done = fa_local_try_fast<SRC, CHECK, R>(m, o, kg, sh, klist, g);
+    PLUSS_FA_REFS(PLUSS_FA_FAST)
+#undef PLUSS_FA_FAST
+  }
+  if (done) {
+    if (threadIdx.x < FPW) part[blockIdx.x * (uint64_t)FPW + threadIdx.x] = sh.out[threadIdx.x];
+    if (threadIdx.x == FPW) tmax[blockIdx.x] = sh.out[FPW];
+  } else if (threadIdx.x == 0) {
+    slowq[1 + atomicAdd(&slowq[0], 1u)] = (unsigned int)blockIdx.x;
+  }
 }
 
 // ---- pass 3: the carry entering each tile applied to its local results (one
@@ -1086,9 +1416,16 @@ inline void fa_launch_t(const FaLaunch& L) {
   const unsigned t = (unsigned)L.t;
   const unsigned nfix = (unsigned)((L.t + FIXB / 64 - 1) / (FIXB / 64));
   const unsigned nres = t < 512 ? t : 512u;
-  hipLaunchKernelGGL((k_fa_local<SRC, P2, CHK>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
-                     b.fslot, L.g);
-  hipLaunchKernelGGL(k_fa_prefix<SRC>, dim3(6), dim3(PB), 0, L.s, L.a, b.tmax, b.pmin, b.queue);
+  if (P2 && L.a.fast) {  // fast tiles, then the queued rest
+    hipLaunchKernelGGL((k_fa_local_fast<SRC, CHK>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
+                       b.fslot, b.slowq, L.g);
+    hipLaunchKernelGGL((k_fa_local<SRC, P2, CHK, true>), dim3(nres), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart,
+                       b.klist, b.fslot, (const unsigned int*)b.slowq, L.g);
+  } else {
+    hipLaunchKernelGGL((k_fa_local<SRC, P2, CHK, false>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
+                       b.fslot, (const unsigned int*)nullptr, L.g);
+  }
+  hipLaunchKernelGGL(k_fa_prefix<SRC>, dim3(6), dim3(PB), 0, L.s, L.a, b.tmax, b.pmin, b.queue, b.slowq);
   hipLaunchKernelGGL(k_fa_fix<SRC>, dim3(nfix), dim3(FIXB), 0, L.s, L.a, b.pmin, b.dpart, b.klist, b.queue);
   hipLaunchKernelGGL((k_fa_rescan<SRC, P2>), dim3(nres), dim3(TB), 0, L.s, L.m, L.a, b.pmin, b.dpart, b.queue);
   hipLaunchKernelGGL((k_fa_finish<SRC, P2>), dim3(6), dim3(FT), 0, L.s, L.m, L.a, b.tmax, b.pmin, b.dpart, b.fslot,

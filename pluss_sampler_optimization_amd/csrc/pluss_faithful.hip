@@ -718,8 +718,9 @@ static int fa_reserve(FaithfulBufs& b, uint64_t tiles, hipStream_t s) {
     PLUSS_HIP_CHECK(hipStreamSynchronize(s));
     int rc = 0;
     if ((rc = grow(&b.dpart, tiles * FPW)) || (rc = grow(&b.tmax, tiles)) || (rc = grow(&b.pmin, tiles)) ||
-        (rc = grow(&b.klist, tiles * 2 * KL)) || (rc = grow(&b.queue, tiles + 1)))
+        (rc = grow(&b.klist, tiles * 2 * KL)) || (rc = grow(&b.queue, tiles + 1)) || (rc = grow(&b.slowq, tiles + 1)))
       return rc;
+    PLUSS_HIP_CHECK(hipMemsetAsync(b.slowq, 0, 4, s));  // k_fa_prefix empties it after every pass
     b.dcap = tiles;
   }
   return PLUSS_OK;
@@ -749,6 +750,9 @@ static int fa_run(pluss_ctx* ctx, FaRefs& a, int src, bool check, hipStream_t s)
   // N, T, CS, CLS/DS powers of two: shift decoding (the word decode also
   // keeps q*N + c1 < N*N/T in 32 bits)
   const bool p2 = m.p2 && a.pv[0].p2 && (uint64_t)m.N * m.N / m.T < (1ull << 32);
+  // the local pass's fast path: 24-bit multiplies (q*N + c1 < N*N/T and S
+  // below 2^24) and the range check by bit masks (N a power of two)
+  a.fast = (p2 && m.np2 && (uint64_t)m.N * m.N / m.T < (1ull << 24) && m.S < (1u << 24)) ? 1u : 0u;
   const FaLaunch L{m, a, g, &b, p2, t, s};
   switch (src) {
     case SRC_W32: fa_launch_w32(L); break;

@@ -67,7 +67,8 @@ struct FaithfulBufs {
   // running max entering it, its first local starts; the queue of tiles to scan again
   uint64_t dcap = 0;
   unsigned long long *dpart = nullptr, *tmax = nullptr, *pmin = nullptr, *klist = nullptr;
-  unsigned int* queue = nullptr;
+  unsigned int* queue = nullptr;  // tiles to scan again with their carry: [0] count, then indices
+  unsigned int* slowq = nullptr;  // tiles the local fast path left (zero count between passes)
   unsigned long long* fslot = nullptr;  // per reference: the main-table slot of its -1 (cold) key
 };
 
