@@ -148,19 +148,19 @@ def cpu_baseline(cfg, host, ri_gpu_fn, budget_s):
     import pluss_sampler_optimization_amd as P
     threads = host_cores()
     oc = orc.cfg(cfg.n, cfg.threads, cfg.chunk, cfg.ds, cfg.cls)
-    # a pilot on a strided sub-sample sizes the timed one (~budget/5 per run, 5
-    # runs); the size is a power of two, so the timed sub-sample is always one
-    # of a few fixed strided sets of the list
+    # a pilot on a strided sub-sample sizes the timed one (~budget/10 per run,
+    # 10 runs, median: SURVEY §8d); the size is a power of two, so the timed
+    # sub-sample is always one of a few fixed strided sets of the list
     pilot = host[:: max(1, len(host) // 512)][:512]
     t = time.perf_counter()
     orc.clean_ri(oc, pilot, nthreads=threads)
     per = (time.perf_counter() - t) / len(pilot)
-    n = 1 << max(8, int(np.log2(max(2.0, budget_s / 5 / max(per, 1e-9)))))
+    n = 1 << max(8, int(np.log2(max(2.0, budget_s / 10 / max(per, 1e-9)))))
     n = min(n, 1 << 20, len(host))
     stride = max(1, len(host) // n)
     sub = np.ascontiguousarray(host[::stride][:n])
     out = {}
-    med, ts = median_time(lambda: out.__setitem__("ri", orc.clean_ri(oc, sub, nthreads=threads)), 5)
+    med, ts = median_time(lambda: out.__setitem__("ri", orc.clean_ri(oc, sub, nthreads=threads)), 10)
     ri_gpu = ri_gpu_fn(sub)
     assert np.array_equal(out["ri"], ri_gpu), "CPU oracle RIs differ from the device RI dump"
     return {"value": len(sub) / med, "unit": "sampled accesses/s", "cores": threads, "kind": "port",
@@ -251,7 +251,7 @@ def faithful_bench(P, torch, device, stream):
     samples), the six sampler_<REF> at once (one stream per reference, as r10
     runs one thread per reference):
       radix:     the Feistel list (arbitrary order): keys -> rocPRIM radix sort ->
-                 fused look-back scan (pluss_dev_faithful_hist_refs);
+                 the single-read scan pipeline (pluss_dev_faithful_hist_refs);
       sorted:    the key-order list (pluss_dev_expand_sorted) read once, no sort
                  (pluss_dev_faithful_hist_sorted_refs): 8 B per sample;
       generated: the same key-order lists generated inside the pass, no input
@@ -303,9 +303,8 @@ def faithful_bench(P, torch, device, stream):
     ach = out["sorted"]["hbm_GBps"]
     out["sorted"]["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
-                                 "note": "achieved = 8 B x samples / pass time (four launches, six references); "
-                                         "traffic includes the 4-8 B per sample word buffer written by the first "
-                                         "launch and read by the scan"}
+                                 "note": "achieved = 8 B x samples / pass time (the whole pipeline, six references); "
+                                         "traffic = HBM bytes of one pass (PMC)"}
     out["sorted"]["recorded"] = hs["sorted"].total() - sum(hs["sorted"].cold(r) for r in P.REFS)
     out["radix"]["recorded"] = hs["radix"].total() - sum(hs["radix"].cold(r) for r in P.REFS)
     out["note"] = ("radix = arbitrary-order input (sort inside the pass); sorted = input already in r10's pop "
@@ -318,11 +317,15 @@ def faithful_config3_bench(P, torch, device, stream, reps=5):
     sampler_<REF> on the same sample list) at the headline shape: N=4096,
     T=8, 2^28 samples on one GPU, six references concurrently.  sorted = the
     key-order list resident in HBM, read once per pass (8 B per sample);
-    generated = the same lists generated inside the pass."""
+    generated = the same lists generated inside the pass; radix = r10's real
+    input, a list in arbitrary order (the keyed Feistel lists, as rand() draws
+    them, r10:156-185), sorted inside the pass."""
     N, T, total = 4096, 8, 1 << 28
     counts = P.default_counts(N, total)
     fcfg = P.SamplerConfig(n=N, threads=T, mode="faithful", device=device)
-    buf = torch.empty(total, dtype=torch.int64, device=torch.device("cuda", device))
+    dev = torch.device("cuda", device)
+    buf = torch.empty(total, dtype=torch.int64, device=dev)
+    fe = torch.empty(total, dtype=torch.int64, device=dev)
     sp = stream.cuda_stream
     out = {"workload": "GEMM N=4096, T=8, 2^28 samples (config 3 on one GPU), faithful, six references",
            "samples": total}
@@ -330,24 +333,28 @@ def faithful_config3_bench(P, torch, device, stream, reps=5):
         off = 0
         for r, c in enumerate(counts):
             ctx.expand_sorted(SEED, r, c, 0, c, buf.data_ptr() + 8 * off, sp)
+            ctx.expand(SEED, r, 0, c, fe.data_ptr() + 8 * off, sp)
             off += c
-        runs = {"sorted": lambda: ctx.faithful_hist_sorted_refs(buf.data_ptr(), counts, sp),
-                "generated": lambda: ctx.gen_faithful_refs(SEED, counts, sp)}
+        runs = {"sorted": (lambda: ctx.faithful_hist_sorted_refs(buf.data_ptr(), counts, sp), reps),
+                "generated": (lambda: ctx.gen_faithful_refs(SEED, counts, sp), reps),
+                "radix": (lambda: ctx.faithful_hist_refs(fe.data_ptr(), counts, sp), 2)}
         hs = {}
-        for name, run in runs.items():
+        for name, (run, k) in runs.items():
             ctx.reset(sp)
             run()
             torch.cuda.synchronize()
             hs[name] = ctx.fetch()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            for _ in range(reps):
+            for _ in range(k):
                 run()
             e1.record(stream)
             torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / reps
+            ms = e0.elapsed_time(e1) / k
             out[name] = {"ms": ms, "samples_per_s": total / (ms * 1e-3)}
-    del buf
+    out["radix"]["recorded"] = hs["radix"].total() - sum(hs["radix"].cold(r) for r in P.REFS)
+    out["radix"]["over_sorted"] = out["radix"]["ms"] / out["sorted"]["ms"]
+    del buf, fe
     assert hs["sorted"].bins == hs["generated"].bins and list(hs["sorted"].traversed) == list(hs["generated"].traversed)
     ach = 8 * total / (out["sorted"]["ms"] * 1e-3) / 1e9
     traffic = None  # HBM bytes per pass from the committed PMC summary (tools/gpu_pmc_faithful.sh, PROF_SHAPE=config3)
@@ -359,9 +366,9 @@ def faithful_config3_bench(P, torch, device, stream, reps=5):
         pass
     out["sorted"]["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
-                                 "note": "achieved = 8 B x samples / pass time (four launches, six references); "
-                                         "traffic = samples read + 8 B words written by the first launch and read "
-                                         "by the scan"}
+                                 "note": "achieved = 8 B x samples / pass time (the whole pipeline, six references); "
+                                         "traffic = HBM bytes of one pass: the samples read once plus the per-tile "
+                                         "summaries and local-start lists"}
     out["recorded"] = hs["sorted"].total() - sum(hs["sorted"].cold(r) for r in P.REFS)
     out["traversed"] = list(hs["sorted"].traversed)
     return out
@@ -412,6 +419,68 @@ def end_to_end_bench(P, torch, cfg, counts, parts, stream, steps=20):
     out["note"] = ("key-order stratified lists (pluss_expand_sorted, same per-reference budget and seed); "
                    "fused = one launch, generation + counting; count = the headline kernel over the materialised list")
     return out
+
+
+def collective_costs(args, torch, dist, ctx, samples, n_local, dense, stream, reps=20):
+    """N>1: the step's parts measured apart -- the kernel alone (K launches,
+    no collective, HIP events on the launch stream) and one all-reduce of the
+    dense vector issued eagerly and waited for (median of `reps`, host clock,
+    every rank in step by a barrier first)."""
+    sp = stream.cuda_stream
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(args.steps):
+        ctx.sampled_hist_dense(samples.data_ptr(), n_local, dense[0].data_ptr(), sp)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    kernel_ms = e0.elapsed_time(e1) / args.steps
+    t = dense[1] if args.backend == "nccl" else dense[1].cpu()
+    ts = []
+    for _ in range(reps):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dist.all_reduce(t)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return {"kernel_only_ms": kernel_ms, "allreduce_eager_us": ts[len(ts) // 2] * 1e6,
+            "allreduce_words": int(t.numel()), "backend": args.backend,
+            "note": "kernel_only_ms: the K timed launches without their all-reduces (HIP events); "
+                    "allreduce_eager_us: one eager all-reduce of the dense vector and its wait, median; in the timed "
+                    "steps the all-reduces run asynchronously from HIP graphs, overlapped with the next launch"}
+
+
+def faithful_sharded_bench(P, torch, dist, device, stream, world, reps=3):
+    """N>1: FAITHFUL mode at config 3 (N=4096, T=8, 2^28 samples in total)
+    over key-range shards, one per rank (dist.sharded_faithful_gen_hist): each
+    rank generates the samples of its key range inside its single-read pass,
+    three six-word all-gathers carry the scan across the ranks, the tables are
+    merged.  Time per pass: max over ranks."""
+    from pluss_sampler_optimization_amd import dist as D
+    N, T, total = 4096, 8, 1 << 28
+    counts = P.default_counts(N, total)
+    fcfg = P.SamplerConfig(n=N, threads=T, mode="faithful", device=device)
+    h = D.sharded_faithful_gen_hist(fcfg, SEED, counts, stream=stream)  # warm-up
+    ts = []
+    for _ in range(reps):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        h = D.sharded_faithful_gen_hist(fcfg, SEED, counts, stream=stream)
+        torch.cuda.synchronize()
+        nccl = dist.get_backend() == "nccl"
+        dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                          device=torch.device("cuda", device) if nccl else "cpu")
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        ts.append(float(dt.item()))
+    ms = sorted(ts)[len(ts) // 2] * 1e3
+    return {"workload": "GEMM N=4096, T=8, 2^28 samples in total (config 3), faithful, key-range shards, "
+                        "lists generated inside the pass", "ranks": world, "ms": ms,
+            "samples_per_s": total / (ms * 1e-3), "recorded": h.total() - sum(h.cold(r) for r in P.REFS),
+            "note": "host clock around the whole sharded pass (4 phases, 3 all-gathers, table merge); median of "
+                    f"{reps}, max over ranks"}
 
 
 def pmc_traffic(samples_per_launch):
@@ -579,6 +648,16 @@ def main():
     torch.cuda.synchronize()
     loads_ms = e2.elapsed_time(e3) / 20
 
+    collective_info = None
+    if collective:
+        collective_info = collective_costs(args, torch, dist, ctx, samples, n_local, dense, stream)
+    faithful_shards = None
+    if world > 1 and not args.no_extras:
+        try:  # a side line: its failure must not cost the headline line
+            faithful_shards = faithful_sharded_bench(P, torch, dist, local, stream, world)
+        except Exception as e:  # noqa: BLE001
+            faithful_shards = {"error": repr(e)}
+
     achieved = BYTES_PER_SAMPLE * n_local / (kern_ms * 1e-3) / 1e9
     stream_peak = BYTES_PER_SAMPLE * n_local / (loads_ms * 1e-3) / 1e9
     result = {
@@ -613,6 +692,10 @@ def main():
         "launch": launch_mode,
         "histogram_bins": len(h.bins),
     }
+    if collective_info is not None:
+        result["collective"] = collective_info
+    if faithful_shards is not None:
+        result["faithful_sharded"] = faithful_shards
     if not args.no_extras:
         result["end_to_end"] = end_to_end_bench(P, torch, cfg, counts, parts, stream)
     if rank == 0 and not args.no_extras:

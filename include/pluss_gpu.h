@@ -213,6 +213,39 @@ typedef struct pluss_faith_shard {
 
 /* keys of this shape lie in [0, *key_end) (= accesses per thread * threads) */
 int pluss_faithful_key_space(const pluss_cfg *cfg, uint64_t *key_end);
+
+/* Faithful mode over key-range shards, all six references at once, on the
+   single-read scan pipeline (multi-GPU: one shard per rank; the shards of a
+   reference partition its list in key order).  r10's sampler_<REF> is one
+   sequential pass over the whole list (r10:187-695); the caller exchanges
+   three per-reference summaries between the four phases:
+     1. local: this shard's slices -- n[r] samples of reference r from index
+        first[r] of its list of totals[r] samples: d_samples (key-ordered,
+        reference blocks back to back) or, d_samples == NULL, generated
+        (pluss_expand_sorted's lists, seed); out: the largest sink per
+        reference (0: none);
+     2. carry: carry_in[r] = the largest sink of the earlier shards (max of
+        their phase-1 outputs); out: this shard's replay-start counts;
+     3. cut: starts_before[r] = the earlier shards' start counts summed; out:
+        this shard's first Q1 cut candidate (global index; totals[r]: none);
+     4. hist: cut[r] = the smallest candidate over all shards; is_last[r] =
+        this is the last shard with samples of reference r: this shard's part
+        of the histograms and traversed is added to the handle (the tables of
+        the shards are then summed, e.g. by all-gathering the exports).
+   Needs N % (chunk*threads) == 0 and N % (cls/ds) == 0. */
+int pluss_dev_faithful_shards_local(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t seed, const uint64_t *totals,
+                                    const uint64_t *first, const uint64_t *n, uint64_t *max_sink, void *stream);
+int pluss_dev_faithful_shards_carry(pluss_ctx *ctx, const uint64_t *carry_in, uint64_t *starts, void *stream);
+int pluss_dev_faithful_shards_cut(pluss_ctx *ctx, const uint64_t *starts_before, uint64_t *cut, void *stream);
+int pluss_dev_faithful_shards_hist(pluss_ctx *ctx, const uint64_t *cut, const int32_t *is_last, void *stream);
+
+/* Host only (no device): [*i_lo, *i_hi) = the indices of the samples of the
+   key-order list of `total` samples of reference `ref` (pluss_expand_sorted's
+   list) whose faithful keys lie in [key_lo, key_hi) -- the list is in key
+   order, so two binary searches of the host generator.  A key-range shard of
+   faithful mode generates exactly that slice (dist.sharded_faithful_gen_hist). */
+int pluss_keyorder_index_range(const pluss_cfg *cfg, uint64_t seed, int32_t ref, uint64_t total, uint64_t key_lo,
+                               uint64_t key_hi, uint64_t *i_lo, uint64_t *i_hi);
 int pluss_dev_faithful_shard_keys(pluss_ctx *ctx, int32_t ref, const uint64_t *d_samples, uint64_t n,
                                   uint64_t key_lo, uint64_t key_hi, pluss_faith_shard *out, void *stream);
 int pluss_dev_faithful_shard_starts(pluss_ctx *ctx, uint64_t j_off, uint64_t pmax_in, pluss_faith_shard *out,

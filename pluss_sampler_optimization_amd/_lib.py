@@ -25,9 +25,11 @@ EXPORTS = [
     "pluss_dev_faithful_hist_sorted", "pluss_dev_faithful_hist_sorted_refs", "pluss_dev_gen_faithful_refs",
     "pluss_dev_fulltrace_hist", "pluss_dev_sampled_ri",
     "pluss_dev_hist_export", "pluss_dev_hist_export_reset", "pluss_dev_sampled_hist_export", "pluss_hist_fetch",
-    "pluss_hist_from_tables", "pluss_faithful_key_space", "pluss_dev_faithful_shard_keys",
+    "pluss_hist_from_tables", "pluss_faithful_key_space", "pluss_keyorder_index_range", "pluss_dev_faithful_shard_keys",
     "pluss_dev_faithful_shard_starts", "pluss_dev_faithful_shard_cut", "pluss_dev_faithful_shard_hist",
     "pluss_dense_keys", "pluss_dev_sampled_hist_dense", "pluss_dev_gen_count_dense",
+    "pluss_dev_faithful_shards_local", "pluss_dev_faithful_shards_carry", "pluss_dev_faithful_shards_cut",
+    "pluss_dev_faithful_shards_hist",
 ]
 # include/pluss_diag.h (diagnostics, not the drop-in boundary)
 DIAG_EXPORTS = ["pluss_diag_dense"]
@@ -113,6 +115,7 @@ def lib():
         "pluss_hist_fetch": (ctypes.c_int, [vp, histp]),
         "pluss_hist_from_tables": (ctypes.c_int, [vp, vp, u64, histp]),
         "pluss_faithful_key_space": (ctypes.c_int, [cfgp, P(u64)]),
+        "pluss_keyorder_index_range": (ctypes.c_int, [cfgp, u64, i32, u64, u64, u64, P(u64), P(u64)]),
         "pluss_dev_faithful_shard_keys": (ctypes.c_int, [vp, i32, vp, u64, u64, u64, P(PlussFaithShard), vp]),
         "pluss_dev_faithful_shard_starts": (ctypes.c_int, [vp, u64, u64, P(PlussFaithShard), vp]),
         "pluss_dev_faithful_shard_cut": (ctypes.c_int, [vp, u64, u64, P(PlussFaithShard), vp]),
@@ -121,6 +124,10 @@ def lib():
         "pluss_dev_sampled_hist_dense": (ctypes.c_int, [vp, vp, u64, vp, vp]),
         "pluss_dev_gen_count_dense": (ctypes.c_int, [vp, u64, P(u64), P(u64), P(u64), vp, vp]),
         "pluss_diag_dense": (ctypes.c_int, [vp, vp, u64, vp, i32, i32, vp]),
+        "pluss_dev_faithful_shards_local": (ctypes.c_int, [vp, vp, u64, P(u64), P(u64), P(u64), P(u64), vp]),
+        "pluss_dev_faithful_shards_carry": (ctypes.c_int, [vp, P(u64), P(u64), vp]),
+        "pluss_dev_faithful_shards_cut": (ctypes.c_int, [vp, P(u64), P(u64), vp]),
+        "pluss_dev_faithful_shards_hist": (ctypes.c_int, [vp, P(u64), P(i32), vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -202,11 +202,15 @@ def faithful_key(cfg, sample):
 def keyorder_index_range(cfg, seed, ref, total, key_lo, key_hi, sample_at=None):
     """[i_lo, i_hi): the samples of the key-order list (expand_sorted, keys
     strictly increasing in the index) whose faithful keys lie in
-    [key_lo, key_hi) -- two binary searches, one host sample per probe
-    (sample_at(i) -> packed sample i; default: expand_sorted)."""
+    [key_lo, key_hi) -- two binary searches of the host generator
+    (pluss_keyorder_index_range; no device).  sample_at(i) -> packed sample i
+    replaces the generator (tests)."""
+    rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
     if sample_at is None:
-        def sample_at(i):
-            return expand_sorted(cfg, seed, ref, total, i, 1)[0]
+        lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib().pluss_keyorder_index_range(ctypes.byref(cfg.to_c()), seed, rid, total, key_lo, key_hi,
+                                               ctypes.byref(lo), ctypes.byref(hi)), "pluss_keyorder_index_range")
+        return int(lo.value), int(hi.value)
 
     def first_at_least(key):
         lo, hi = 0, total
@@ -378,6 +382,39 @@ class Context:
         """Phase 4: accumulate this shard's part of the sampler's histogram."""
         check(lib().pluss_dev_faithful_shard_hist(self._h, cut, next_first_key, 1 if is_last else 0, stream),
               "pluss_dev_faithful_shard_hist")
+
+    # faithful mode over key-range shards of the single-read pipeline, all six
+    # references at once (pluss_dev_faithful_shards_*; dist.sharded_faithful_gen_hist)
+    def faithful_shards_local(self, d_samples, seed, totals, first, n, stream=None):
+        """Phase 1 -> the largest sink of this shard per reference.  d_samples None: generated slices."""
+        u6 = ctypes.c_uint64 * 6
+        out = u6()
+        check(lib().pluss_dev_faithful_shards_local(self._h, d_samples, seed, u6(*map(int, totals)),
+                                                    u6(*map(int, first)), u6(*map(int, n)), out, stream),
+              "pluss_dev_faithful_shards_local")
+        return [int(x) for x in out]
+
+    def faithful_shards_carry(self, carry_in, stream=None):
+        """Phase 2 -> this shard's replay-start counts per reference."""
+        u6 = ctypes.c_uint64 * 6
+        out = u6()
+        check(lib().pluss_dev_faithful_shards_carry(self._h, u6(*map(int, carry_in)), out, stream),
+              "pluss_dev_faithful_shards_carry")
+        return [int(x) for x in out]
+
+    def faithful_shards_cut(self, starts_before, stream=None):
+        """Phase 3 -> this shard's first Q1 cut candidate per reference (global index; the list length: none)."""
+        u6 = ctypes.c_uint64 * 6
+        out = u6()
+        check(lib().pluss_dev_faithful_shards_cut(self._h, u6(*map(int, starts_before)), out, stream),
+              "pluss_dev_faithful_shards_cut")
+        return [int(x) for x in out]
+
+    def faithful_shards_hist(self, cut, is_last, stream=None):
+        """Phase 4: add this shard's part of the histograms (global cut per reference)."""
+        check(lib().pluss_dev_faithful_shards_hist(self._h, (ctypes.c_uint64 * 6)(*map(int, cut)),
+                                                   (ctypes.c_int32 * 6)(*[1 if x else 0 for x in is_last]), stream),
+              "pluss_dev_faithful_shards_hist")
 
     def fetch(self):
         h, keep = _hist_buf()

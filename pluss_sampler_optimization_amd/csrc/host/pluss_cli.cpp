@@ -121,7 +121,11 @@ void write_json(const std::string& path, const Opts& o, const char* mode,
     std::exit(1);
   }
   f.precision(17);
-  f << "{\"mode\": \"" << mode << "\", \"n\": " << o.cfg.n << ", \"threads\": " << o.cfg.threads
+  // sampler: which semantics the histograms follow (acc: the full trace; sample/replay: r10's
+  // queue semantics -- samples after its Q1 exit are not recorded, colds count for tid 0 only)
+  const bool full = std::string(mode) == "acc";
+  f << "{\"mode\": \"" << mode << "\", \"sampler\": \"" << (full ? "full trace" : "faithful (r10 queue semantics)")
+    << "\", \"n\": " << o.cfg.n << ", \"threads\": " << o.cfg.threads
     << ", \"chunk\": " << o.cfg.chunk << ", \"ds\": " << o.cfg.ds << ", \"cls\": " << o.cfg.cls
     << ", \"seconds\": " << seconds << ",\n \"histograms\": {";
   for (size_t i = 0; i < hists.size(); ++i)
@@ -145,6 +149,12 @@ void write_trace(const std::string& path, const pluss_cfg& cfg, const std::vecto
     std::cerr << "cannot write " << path << "\n";
     std::exit(1);
   }
+  // The RI of each sample is its own next reuse (clean mode).  In a faithful
+  // (r10) run the histograms leave out the samples after r10's Q1 exit and
+  // count cold samples of tid 0 only, so the trace says so in its header.
+  if (cfg.mode == PLUSS_MODE_FAITHFUL)
+    f << "# ref c0 c1 c2 ri sink_key: per-sample reuse (clean); the faithful histograms skip samples after r10's "
+         "Q1 exit and count cold samples of tid 0 only\n";
   const uint64_t M = (1ull << 20) - 1;
   for (size_t i = 0; i < samples.size(); ++i) {
     const uint64_t x = samples[i];

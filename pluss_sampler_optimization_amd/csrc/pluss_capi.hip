@@ -174,11 +174,11 @@ int pluss_ctx_destroy(pluss_ctx* c) {
   void* bufs[] = {c->d_table,  c->d_exp_keys, c->d_exp_counts, c->d_exp_n, c->fb.keys,  c->fb.sinks,
                   c->fb.keys_s, c->fb.sinks_s, c->fb.pmax,      c->fb.nstart, c->fb.tmp,
                   c->fb.scal, c->fb.st, c->fb.dpart, c->fb.tmax, c->fb.pmin, c->fb.fslot,
-                  c->fb.klist, c->fb.queue, c->fb.slowq};
+                  c->fb.klist, c->fb.slowq, c->fb.cval, c->fb.crec, c->fb.cflag, c->fb.shrec};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (const auto& f : c->fbr) {
-    void* fr[] = {f.keys, f.sinks, f.keys_s, f.sinks_s, f.pmax, f.nstart, f.tmp, f.scal, f.st, f.dpart, f.tmax, f.pmin, f.fslot, f.klist, f.queue, f.slowq};
+    void* fr[] = {f.keys, f.sinks, f.keys_s, f.sinks_s, f.pmax, f.nstart, f.tmp, f.scal, f.st, f.dpart, f.tmax, f.pmin, f.fslot, f.klist, f.slowq, f.cval, f.crec, f.cflag};
     for (void* p : fr)
       if (p) (void)hipFree(p);
   }
@@ -187,6 +187,7 @@ int pluss_ctx_destroy(pluss_ctx* c) {
   for (int e = 0; e < 7; ++e)
     if (c->fev[e]) (void)hipEventDestroy(c->fev[e]);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  faith_shards_free(c);
   delete c;
   return PLUSS_OK;
 }
@@ -308,6 +309,52 @@ int pluss_faithful_key_space(const pluss_cfg* cfg, uint64_t* key_end) {
     return PLUSS_ERR_CONFIG;
   }
   *key_end = m.A * m.T;
+  return PLUSS_OK;
+}
+
+int pluss_dev_faithful_shards_local(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t seed, const uint64_t* totals,
+                                    const uint64_t* first, const uint64_t* n, uint64_t* max_sink, void* stream) {
+  if (!ctx || !totals || !first || !n || !max_sink) return PLUSS_ERR_CONFIG;
+  return faith_shards_local(ctx, d_samples, seed, totals, first, n, max_sink, pick(ctx, stream));
+}
+
+int pluss_dev_faithful_shards_carry(pluss_ctx* ctx, const uint64_t* carry_in, uint64_t* starts, void* stream) {
+  if (!ctx || !carry_in || !starts) return PLUSS_ERR_CONFIG;
+  return faith_shards_carry(ctx, carry_in, starts, pick(ctx, stream));
+}
+
+int pluss_dev_faithful_shards_cut(pluss_ctx* ctx, const uint64_t* starts_before, uint64_t* cut, void* stream) {
+  if (!ctx || !starts_before || !cut) return PLUSS_ERR_CONFIG;
+  return faith_shards_cut(ctx, starts_before, cut, pick(ctx, stream));
+}
+
+int pluss_dev_faithful_shards_hist(pluss_ctx* ctx, const uint64_t* cut, const int32_t* is_last, void* stream) {
+  if (!ctx || !cut || !is_last) return PLUSS_ERR_CONFIG;
+  return faith_shards_hist(ctx, cut, is_last, pick(ctx, stream));
+}
+
+int pluss_keyorder_index_range(const pluss_cfg* cfg, uint64_t seed, int32_t ref, uint64_t total, uint64_t key_lo,
+                               uint64_t key_hi, uint64_t* i_lo, uint64_t* i_hi) {
+  Model m;
+  if (!i_lo || !i_hi || ref < 0 || ref > 5 || key_lo > key_hi) return PLUSS_ERR_CONFIG;
+  if (int rc = validate_cfg(cfg, &m)) return rc;
+  pluss_ctx probe;  // keygen_check / keygen_of read only the configuration
+  probe.cfg = *cfg;
+  probe.m = m;
+  if (int rc = keygen_check(&probe, ref, total, 0, total, "pluss_keyorder_index_range")) return rc;
+  const KeyGen k = keygen_of(&probe, seed, ref, total);
+  // keys increase with the index (the list is in key order): two binary searches on the host
+  auto first_at_least = [&](uint64_t key) {
+    uint64_t lo = 0, hi = total;
+    while (lo < hi) {
+      const uint64_t mid = lo + (hi - lo) / 2;
+      if (key_of_digits(m, (uint32_t)ref, keygen_digits_at(k, mid)) >= key) hi = mid;
+      else lo = mid + 1;
+    }
+    return lo;
+  };
+  *i_lo = first_at_least(key_lo);
+  *i_hi = first_at_least(key_hi);
   return PLUSS_OK;
 }
 

@@ -124,23 +124,15 @@ __device__ __forceinline__ unsigned long long sc_wave_scan(unsigned long long v,
 //                sink, the start count, the Q1 bound hmax, the records of all
 //                its elements, the traversed sum, and its first KL local starts
 //                (key, running max of sinks before it);
-//   k_fa_prefix  one workgroup per reference: exclusive prefix max of the tile
-//                maxima = the running max c entering each tile;
-//   k_fa_fix     per tile: with c entering, element i starts iff key_i >
-//                max(c, lp_{i-1}) (lp: the tile's own running max).  A local
-//                start stays a start iff key_i > c, a local non-start stays one,
-//                and keys increase, so c absorbs exactly the first m local
-//                starts; the first surviving start's replay-before term becomes
-//                max(c, lp) and every later running max is the local one.  So
-//                the start count, hmax and traversed follow from the stored
-//                list; a tile whose whole list is absorbed while it has more
-//                starts is queued;
-//   k_fa_rescan  the queued tiles (rare) scanned again with their carry;
+//   k_fa_chunk   per chunk of CH tiles: the running max c entering each tile
+//                (the chunk's maxima published and looked back at, then a scan
+//                inside the chunk), the fix-up of each tile's results for its
+//                c (below), and the chunk's summary;
 //   k_fa_finish  one workgroup per reference: the exclusive sum of the start
-//                counts locates the tile holding the Q1 cut (the condition
-//                j - starts_before_j >= n - j is monotone in j), the tiles
-//                before it are summed, that tile is scanned again below the
-//                cut; Q3, the -1 key, traversed, the bins.
+//                counts over chunks, then tiles, locates the tile holding the
+//                Q1 cut (the condition j - starts_before_j >= n - j is monotone
+//                in j), everything before it is summed, that tile is scanned
+//                again below the cut; Q3, the -1 key, traversed, the bins.
 // HBM traffic: the elements once, plus per tile a few words and its list.
 constexpr int TB = 256, TI = 16;            // threads per tile, elements per thread
 constexpr uint32_t TILE = TB * TI;          // elements per tile
@@ -155,6 +147,12 @@ enum : int { FA_LOCAL = 0, FA_FULL = 1, FA_CUT = 2 };
 struct FaRefs {
   uint64_t n[6];
   uint64_t toff[7];    // first (global) tile of each reference; toff[6] = all tiles
+  uint64_t coff[7];    // first chunk (CH tiles) of each reference; coff[6] = all chunks
+  // key-range shards (multi-GPU; one GPU: joff 0, ntot = n, cin 0, soff 0): the global
+  // index of this shard's element 0 in the reference's list, the list's length, the
+  // running max of sinks entering the shard, the starts before it
+  uint64_t joff[6], ntot[6], soff[6];
+  unsigned long long cin[6];
   const void* src[6];  // SRC_W*: sorted packed words; SRC_SAMPLES: the key-ordered samples
   PkView pv[6];
   KeyGen kg[6];        // SRC_GEN
@@ -222,7 +220,9 @@ using fa_raw_t = typename std::conditional<SRC == SRC_W32, uint32_t, unsigned lo
 // the tile's reference (wave-uniform) and its place in it
 struct FaTile {
   uint32_t r;
-  uint64_t lt, base;  // tile index within the reference, its first element
+  uint64_t gt;        // tile index over all references
+  uint64_t lt, base;  // tile index within the reference (shard), its first element (in memory)
+  uint64_t gbase;     // the global index of its first element (base + the shard's joff)
   uint32_t mt;        // elements in the tile
 };
 __device__ __forceinline__ FaTile fa_tile(const FaRefs& a, uint64_t gt) {
@@ -232,8 +232,10 @@ __device__ __forceinline__ FaTile fa_tile(const FaRefs& a, uint64_t gt) {
   r = __builtin_amdgcn_readfirstlane(r);
   FaTile t;
   t.r = r;
+  t.gt = gt;
   t.lt = gt - a.toff[r];
   t.base = t.lt * TILE;
+  t.gbase = a.joff[r] + t.base;
   const uint64_t left = a.n[r] - t.base;
   t.mt = (uint32_t)(left < TILE ? left : TILE);
   return t;
@@ -275,39 +277,6 @@ __device__ __forceinline__ Elem fa_decode_ref(const Model& m, const PkView& v, f
 // table and keeps the slot, so the finish pass only adds the count
 __device__ __forceinline__ void fa_cold_slot(const FaTile& T, GTable g, unsigned long long* slots) {
   if (T.lt == 0 && threadIdx.x == 0) slots[T.r] = g_slot(g, make_key(T.r, 0, -1));
-}
-
-// One workgroup per reference: pmin[t] = max of tmax over the reference's
-// tiles before t (0 for its first).  Also empties the rescan queue.
-constexpr int PB = 1024;
-template <int SRC>  // (instantiated in each source's translation unit)
-__global__ __launch_bounds__(PB) void k_fa_prefix(FaRefs a, const unsigned long long* __restrict__ tmax,
-                                                  unsigned long long* __restrict__ pmin, unsigned int* queue,
-                                                  unsigned int* slowq) {
-  __shared__ unsigned long long s_w[PB / 64];
-  const uint32_t r = blockIdx.x;
-  if (r == 0 && threadIdx.x == 0) {  // the rescan queue starts empty; the slow-tile queue is left empty (it was read)
-    queue[0] = 0;
-    slowq[0] = 0;
-  }
-  const uint64_t t0 = a.toff[r], nt = a.toff[r + 1] - t0;
-  if (nt == 0) return;
-  const uint64_t per = (nt + PB - 1) / PB;
-  const uint64_t lo = t0 + threadIdx.x * per, hi = lo + per < t0 + nt ? lo + per : t0 + nt;
-  unsigned long long mx = 0;
-  for (uint64_t t = lo; t < hi; ++t) mx = tmax[t] > mx ? tmax[t] : mx;
-  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  const unsigned long long inc = sc_wave_scan<true>(mx, lane);
-  if (lane == 63) s_w[wid] = inc;
-  __syncthreads();
-  unsigned long long pre = 0;
-  for (uint32_t w = 0; w < wid; ++w) pre = s_w[w] > pre ? s_w[w] : pre;
-  const unsigned long long up = __shfl_up(inc, 1, 64);
-  unsigned long long run = lane ? (up > pre ? up : pre) : pre;  // exclusive prefix of this thread's segment
-  for (uint64_t t = lo; t < hi; ++t) {
-    pmin[t] = run;
-    run = tmax[t] > run ? tmax[t] : run;
-  }
 }
 
 // ---- the tile scan (NT threads; thread x owns the run [x*EPT, (x+1)*EPT) of
@@ -374,9 +343,9 @@ __device__ __forceinline__ void fa_load_run(const Model& m, const FaOne& o, cons
       }
     }
   } else {
-    if (keyrun_fast_ok(kg, T.base, TILE)) {  // a whole tile: every run is in range
+    if (keyrun_fast_ok(kg, T.gbase, TILE)) {  // a whole tile: every run is in range
       KeyRunF run;
-      keyrunf_start(kg, run, T.base + e0);
+      keyrunf_start(kg, run, T.gbase + e0);
 #pragma unroll
       for (int k = 0; k < EPT; ++k) {
         const Elem x = elem_of_digits<P2>(m, o.pv, REF, keyrunf_digits(kg, run));
@@ -390,7 +359,7 @@ __device__ __forceinline__ void fa_load_run(const Model& m, const FaOne& o, cons
       for (int k = 0; k < EPT; ++k) {
         key[k] = KEY_EMPTY;
         if (FULLT || e0 + k < T.mt) {
-          const Elem x = elem_of_digits<P2>(m, o.pv, REF, keygen_digits_at(kg, T.base + e0 + k));
+          const Elem x = elem_of_digits<P2>(m, o.pv, REF, keygen_digits_at(kg, T.gbase + e0 + k));
           key[k] = x.key;
           cases |= x.c << (2 * k);
           t0s |= x.t0 << (2 * k);
@@ -416,7 +385,7 @@ __device__ __forceinline__ void fa_scan(const Model& m, const FaOne& o, const un
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
   const uint32_t e0 = threadIdx.x * EPT;                                        // this lane's run in the tile
   const uint32_t nv = FULLT ? EPT : (e0 < T.mt ? (T.mt - e0 < EPT ? T.mt - e0 : EPT) : 0u);  // its valid elements
-  const uint64_t i0 = T.base + e0;                                              // index of its first element
+  const uint64_t i0 = T.gbase + e0;                                             // global index of its first element
   auto sink_of = [&](unsigned long long kk, uint32_t c) -> unsigned long long {
     const unsigned long long d = sh.rt[c];  // an LDS table: no divergent selects
     const unsigned long long x = kk + d;    // d == KEY_EMPTY wraps below d: the max keeps KEY_EMPTY
@@ -629,7 +598,7 @@ __device__ __forceinline__ void fa_scan_local32(const FaOne& o, const unsigned l
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
   const uint32_t e0 = threadIdx.x * EPT;
   const uint32_t nv = FULLT ? EPT : (e0 < T.mt ? (T.mt - e0 < EPT ? T.mt - e0 : EPT) : 0u);
-  const uint64_t i0 = T.base + e0;
+  const uint64_t i0 = T.gbase + e0;
   uint32_t rt32[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) rt32[c] = sh.rt[c] == KEY_EMPTY ? 0xFFFFFFFFu : (uint32_t)sh.rt[c];
@@ -759,22 +728,16 @@ __device__ __forceinline__ fa_raw_t<SRC> src_at(const FaOne& o, uint32_t e) {
 struct FaDec {
   uint32_t lk;             // low 32 bits of the key a*T + tid
   bool a, b, t0;           // case 0 = a, case 1 = !a && b, case 2 = neither; tid == 0
-  unsigned long long key;  // the whole key (CHECK: the order check)
+  unsigned long long ord;  // (q*N + c1) << 32 | c2 << tsh | tid: increasing with the key (CHECK)
 };
 
-template <uint32_t REF, bool KEY64>
+template <uint32_t REF>
 __device__ __forceinline__ FaDec fa_dec_digits(const Model& m, const PkView& v, uint32_t q, uint32_t c1, uint32_t c2,
                                                uint32_t t) {
   FaDec d;
   const uint32_t qc = (q << v.nsh) | c1;
-  const uint32_t off = ref_off(REF, c2);
-  if (KEY64) {
-    d.key = ((((uint64_t)qc * m.S) + off) << v.tsh) | t;
-    d.lk = (uint32_t)d.key;
-  } else {
-    d.key = 0;
-    d.lk = ((__umul24(qc, m.S) + off) << v.tsh) | t;
-  }
+  d.lk = ((__umul24(qc, m.S) + ref_off(REF, c2)) << v.tsh) | t;
+  d.ord = ((unsigned long long)qc << 32) | ((c2 << v.tsh) | t);
   const uint32_t Wm1 = m.W - 1;
   d.a = true;
   d.b = true;
@@ -794,7 +757,7 @@ __device__ __forceinline__ FaDec fa_dec_digits(const Model& m, const PkView& v, 
 
 // a caller's packed sample ref(4)|c0(20)|c1(20)|c2(20); `odd` collects the
 // bits of another reference or of an index >= N (N a power of two)
-template <uint32_t REF, bool KEY64>
+template <uint32_t REF>
 __device__ __forceinline__ FaDec fa_dec_sample(const Model& m, const PkView& v, uint64_t x, uint32_t& odd) {
   const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
   odd |= ((hi ^ (REF << 28)) & (0xF0000000u | m.badhi)) | (lo & m.badlo);
@@ -803,7 +766,7 @@ __device__ __forceinline__ FaDec fa_dec_sample(const Model& m, const PkView& v, 
   const uint32_t cs = m.csshift, ts = v.tsh;
   const uint32_t t = __builtin_amdgcn_ubfe(hi, 8 + cs, ts);
   const uint32_t q = (__builtin_amdgcn_ubfe(hi, 8 + cs + ts, 20 - cs - ts) << cs) | __builtin_amdgcn_ubfe(hi, 8, cs);
-  return fa_dec_digits<REF, KEY64>(m, v, q, c1, c2, t);
+  return fa_dec_digits<REF>(m, v, q, c1, c2, t);
 }
 
 // a packed sort word rank << 2 | case, rank = ((q*N + c1)*N + c2)*T + tid
@@ -814,7 +777,7 @@ __device__ __forceinline__ FaDec fa_dec_word(const Model& m, const PkView& v, KT
   const uint32_t c2 = (uint32_t)(w >> (2 + v.tsh)) & (uint32_t)(v.N - 1);
   const uint32_t qc = (uint32_t)(w >> (2 + v.tsh + v.nsh));
   FaDec d;
-  d.key = 0;
+  d.ord = 0;
   d.lk = ((__umul24(qc, m.S) + ref_off(REF, c2)) << v.tsh) | t;
   d.a = c == 0;
   d.b = c == 1;
@@ -844,62 +807,56 @@ __device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(v), 63);
 }
 
-template <int SRC, bool CHECK, uint32_t REF>
-__device__ __forceinline__ void fa_local_fast(const Model& m, const FaOne& o, const KeyGen& kg,
-                                              FaLds<SRC, TB, TI>& sh, unsigned long long base, const uint32_t (&r)[3],
+// The scan of one tile by the fast path (mt elements: FULLT, or a partial
+// tile's elements at e < mt).  `el(k)` decodes this thread's element k.
+template <int SRC, bool CHECK, uint32_t REF, bool FULLT, class EL>
+__device__ __forceinline__ void fa_local_fast(const Model& m, const FaOne& o, FaLds<SRC, TB, TI>& sh,
+                                              unsigned long long base, const uint32_t (&r)[3], EL&& el,
                                               unsigned long long* __restrict__ klist, GTable g) {
   constexpr int NW = TB / 64;
   const FaTile& T = o.T;
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
   const uint32_t e0 = threadIdx.x * TI;
-  const uint64_t i0 = T.base + e0;
+  const uint32_t nv = FULLT ? TI : (e0 < T.mt ? (T.mt - e0 < TI ? T.mt - e0 : TI) : 0u);
+  const uint64_t i0 = T.gbase + e0;
   const uint32_t b32 = (uint32_t)base;
-  uint32_t rk[TI], sk[TI], lmax = 0, n0 = 0, n1 = 0, nc = 0, odd = 0;
+  uint32_t rk[TI], sk[TI], lmax = 0, odd = 0;
+  uint32_t w0 = 0, w1 = 0, wc = 0;  // wave counts (ballots): case 0, case 1, case 2 of tid 0
   bool unordered = false;
-  unsigned long long kfirst = 0, kprev = 0;
-  KeyRunF run;
-  if constexpr (SRC == SRC_GEN) keyrunf_start(kg, run, T.base + e0);
+  unsigned long long ofirst = 0, oprev = 0;
 #pragma unroll
   for (int k = 0; k < TI; ++k) {
-    FaDec d;
-    if constexpr (SRC == SRC_SAMPLES) {
-      d = fa_dec_sample<REF, CHECK>(m, o.pv, sh.raw[fa_slot_n<TI>(e0 + k)], odd);
-    } else if constexpr (SRC == SRC_GEN) {
-      const KeyDigits dg = keyrunf_digits(kg, run);
-      keyrunf_next(kg, run);
-      d = fa_dec_digits<REF, false>(m, o.pv, dg.q, dg.c1, dg.c2, dg.t);
-    } else {
-      d = fa_dec_word<REF>(m, o.pv, sh.raw[fa_slot_n<TI>(e0 + k)]);
+    const bool v = FULLT || (uint32_t)k < nv;
+    const FaDec d = el(k, odd);
+    if (CHECK && v) {
+      if (k == 0) ofirst = d.ord;
+      else unordered |= !(d.ord > oprev);
+      oprev = d.ord;
     }
-    if (CHECK) {
-      if (k == 0) kfirst = d.key;
-      else unordered |= !(d.key > kprev);
-      kprev = d.key;
-    }
-    rk[k] = d.lk - b32;
+    rk[k] = v ? d.lk - b32 : 0u;
     const uint32_t dd = d.a ? r[0] : (d.b ? r[1] : r[2]);
     const uint32_t x = rk[k] + dd;  // dd = 0xFFFFFFFF (cold) wraps below dd: the max keeps it
-    sk[k] = x > dd ? x : dd;
+    sk[k] = v ? (x > dd ? x : dd) : 0u;
     lmax = sk[k] > lmax ? sk[k] : lmax;
-    n0 += d.a ? 1u : 0u;
-    n1 += (!d.a && d.b) ? 1u : 0u;
-    nc += (!d.a && !d.b && d.t0) ? 1u : 0u;
+    w0 += (uint32_t)__popcll(__ballot(v && d.a));
+    w1 += (uint32_t)__popcll(__ballot(v && !d.a && d.b));
+    wc += (uint32_t)__popcll(__ballot(v && !d.a && !d.b && d.t0));
   }
   if (CHECK) {  // across lanes, waves and the tile's start (the element before it)
-    const unsigned long long up = __shfl_up(kprev, 1, 64);
-    if (lane > 0) unordered |= !(kfirst > up);
-    if (lane == 63) sh.klast[wid] = kprev;
+    const unsigned long long up = __shfl_up(oprev, 1, 64);
+    if (lane > 0 && nv) unordered |= !(ofirst > up);
+    if (lane == 63) sh.klast[wid] = oprev;
   }
   // running max of sinks entering this lane
   const uint32_t linc = wave_scan_dpp<true>(lmax);
   if (lane == 63) sh.w[wid] = linc;
   __syncthreads();
   if (CHECK) {
-    if (lane == 0 && wid > 0) unordered |= !(kfirst > sh.klast[wid - 1]);
+    if (lane == 0 && wid > 0 && nv) unordered |= !(ofirst > sh.klast[wid - 1]);
     if (threadIdx.x == 0 && T.base > 0) {
-      bool b2 = false;
+      uint32_t o2 = 0;
       const fa_raw_t<SRC> w = static_cast<const fa_raw_t<SRC>*>(o.src)[T.base - 1];
-      unordered |= !(kfirst > fa_decode_ref<SRC, true, REF>(m, o.pv, w, b2).key);
+      unordered |= !(ofirst > fa_dec_sample<REF>(m, o.pv, (uint64_t)w, o2).ord);
     }
     if (__ballot(odd != 0 || unordered) && lane == 0) atomicOr(&g.flags[1], 1u);
   }
@@ -929,15 +886,14 @@ __device__ __forceinline__ void fa_local_fast(const Model& m, const FaOne& o, co
   if (hasf) {
     const int ll = 63 - __builtin_clzll(hasf);
     const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)flags, ll);
-    jl = T.base + (uint64_t)(wid * 64 + ll) * TI + (31 - __clz(fl)) + 1;  // + 1: 0 = none
+    jl = T.gbase + (uint64_t)(wid * 64 + ll) * TI + (31 - __clz(fl)) + 1;  // + 1: 0 = none
   }
-  // per-thread records -> wave sums (DPP), then LDS
-  const uint32_t s0 = wave_sum_dpp(n0), s1 = wave_sum_dpp(n1), sc = wave_sum_dpp(nc), sd = wave_sum_dpp(dsum);
+  const uint32_t sd = wave_sum_dpp(dsum);
   if (lane == 63) {
     sh.c[wid] = cinc;
-    sh.red[wid][0] = s0;
-    sh.red[wid][1] = s1;
-    sh.red[wid][2] = sc;
+    sh.red[wid][0] = w0;
+    sh.red[wid][1] = w1;
+    sh.red[wid][2] = wc;
     sh.red[wid][3] = sd;
     sh.red[wid][4] = jl;
   }
@@ -987,32 +943,50 @@ __device__ __forceinline__ void fa_local_fast(const Model& m, const FaOne& o, co
         ac += sh.red[w][2];
       }
       const bool cold2 = r[2] == 0xFFFFFFFFu;
-      x = f == 0 ? (cold2 ? ac : 0ull) : f == 2 ? a0 : f == 3 ? a1 : (cold2 ? 0ull : TILE - a0 - a1);
+      x = f == 0 ? (cold2 ? ac : 0ull) : f == 2 ? a0 : f == 3 ? a1 : (cold2 ? 0ull : T.mt - a0 - a1);
     }
     sh.out[f] = x;
   }
   __syncthreads();
 }
 
-// ---- pass 1: every tile as if nothing entered it.  The fast path (a full
-// tile of a shape with FaRefs::fast whose keys lie within 2^32 - 1 minus the
-// longest reuse of its first key; tile-uniform) in k_fa_local_fast; the tiles
-// it leaves (partial or wide ones) and shapes without it in k_fa_local.
+template <int SRC>
+__device__ __forceinline__ const void* fa_src_of(const FaRefs& a, uint32_t r) {
+  switch (r) {
+    case 0: return a.src[0];
+    case 1: return a.src[1];
+    case 2: return a.src[2];
+    case 3: return a.src[3];
+    case 4: return a.src[4];
+    default: return a.src[5];
+  }
+}
+
+// One tile by the fast path: its elements staged to LDS (memory sources),
+// the first and last keys in 64 bits, then the scan if the tile qualifies.
+// Returns whether the fast path took the tile (tile-uniform).
 template <int SRC, bool CHECK, uint32_t REF>
-__device__ __forceinline__ bool fa_local_try_fast(const Model& m, const FaOne& o, const KeyGen& kg,
-                                                  FaLds<SRC, TB, TI>& sh, unsigned long long* __restrict__ klist,
-                                                  GTable g) {
+__device__ __forceinline__ bool fa_fast_tile(const Model& m, const FaRefs& a, const FaTile& T,
+                                             FaLds<SRC, TB, TI>& sh, unsigned long long* __restrict__ klist,
+                                             GTable g) {
+  const FaOne o = fa_one_ref<SRC, REF>(a, T);
+  KeyGen kg;
+  if constexpr (SRC == SRC_GEN) kg = a.kg[REF];
   fa_rt(m, o.pv, sh);
+  const bool full = T.mt == TILE;
   if constexpr (SRC != SRC_GEN) {
-    const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(o.src) + o.T.base;
+    const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(o.src) + T.base;
 #pragma unroll
-    for (int k = 0; k < TI; ++k) sh.raw[fa_slot_n<TI>((uint32_t)k * TB + threadIdx.x)] = src[k * TB + threadIdx.x];
+    for (int k = 0; k < TI; ++k) {
+      const uint32_t e = (uint32_t)k * TB + threadIdx.x;
+      if (full || e < T.mt) sh.raw[fa_slot_n<TI>(e)] = src[e];
+    }
   }
   if (threadIdx.x < 2) {  // the first and the last key, in 64 bits
-    const uint32_t e = threadIdx.x ? TILE - 1 : 0;
+    const uint32_t e = threadIdx.x ? T.mt - 1 : 0;
     bool b2 = false;
     if constexpr (SRC == SRC_GEN)
-      sh.kb[threadIdx.x] = elem_of_digits<true>(m, o.pv, REF, keygen_digits_at(kg, o.T.base + e)).key;
+      sh.kb[threadIdx.x] = elem_of_digits<true>(m, o.pv, REF, keygen_digits_at(kg, T.gbase + e)).key;
     else
       sh.kb[threadIdx.x] = fa_decode_ref<SRC, true, REF>(m, o.pv, src_at<SRC>(o, e), b2).key;
   }
@@ -1026,14 +1000,37 @@ __device__ __forceinline__ bool fa_local_try_fast(const Model& m, const FaOne& o
     r[c] = x == KEY_EMPTY ? 0xFFFFFFFFu : (uint32_t)x;
     rmax = x != KEY_EMPTY && x > rmax ? x : rmax;
   }
-  if (kl >= base && kl - base < 0xFFFFFFFFull - rmax && r[0] != 0xFFFFFFFFu && r[1] != 0xFFFFFFFFu &&
-      (SRC != SRC_GEN || keyrun_fast_ok(kg, o.T.base, TILE))) {
-    fa_local_fast<SRC, CHECK, REF>(m, o, kg, sh, base, r, klist + blockIdx.x * (uint64_t)(2 * KL), g);
-    return true;
+  if (!(kl >= base && kl - base < 0xFFFFFFFFull - rmax && r[0] != 0xFFFFFFFFu && r[1] != 0xFFFFFFFFu &&
+        (SRC != SRC_GEN || keyrun_fast_ok(kg, T.gbase, T.mt))))
+    return false;
+  unsigned long long* kl_out = klist + T.gt * (uint64_t)(2 * KL);
+  const uint32_t e0 = threadIdx.x * TI;
+  if constexpr (SRC == SRC_GEN) {
+    KeyRunF run;
+    keyrunf_start(kg, run, T.gbase + (e0 < T.mt ? e0 : 0u));
+    auto el = [&](int, uint32_t&) -> FaDec {
+      const KeyDigits dg = keyrunf_digits(kg, run);
+      keyrunf_next(kg, run);
+      return fa_dec_digits<REF>(m, o.pv, dg.q, dg.c1, dg.c2, dg.t);
+    };
+    if (full) fa_local_fast<SRC, CHECK, REF, true>(m, o, sh, base, r, el, kl_out, g);
+    else fa_local_fast<SRC, CHECK, REF, false>(m, o, sh, base, r, el, kl_out, g);
+  } else {
+    auto el = [&](int k, uint32_t& odd) -> FaDec {
+      const fa_raw_t<SRC> w = sh.raw[fa_slot_n<TI>(e0 + k)];
+      if constexpr (SRC == SRC_SAMPLES) return fa_dec_sample<REF>(m, o.pv, (uint64_t)w, odd);
+      else return fa_dec_word<REF>(m, o.pv, w);
+    };
+    if (full) fa_local_fast<SRC, CHECK, REF, true>(m, o, sh, base, r, el, kl_out, g);
+    else fa_local_fast<SRC, CHECK, REF, false>(m, o, sh, base, r, el, kl_out, g);
   }
-  return false;
+  return true;
 }
 
+// ---- pass 1: every tile as if nothing entered it.  The fast path (a full
+// tile of a shape with FaRefs::fast whose keys lie within 2^32 - 1 minus the
+// longest reuse of its first key; tile-uniform) in k_fa_local_fast; the tiles
+// it leaves (partial or wide ones) and shapes without it in k_fa_local.
 template <int SRC, bool P2, bool CHECK, uint32_t REF, bool FULLT>
 __device__ __forceinline__ void fa_local_tile(const Model& m, const FaOne& o, const KeyGen& kg, uint64_t gt,
                                               FaLds<SRC, TB, TI>& sh, unsigned long long* __restrict__ tmax,
@@ -1087,7 +1084,7 @@ template <int SRC, uint32_t R>
 __device__ __forceinline__ FaOne fa_one_ref(const FaRefs& a, const FaTile& T) {
   FaOne o;
   o.T = T;
-  o.n = a.n[R];
+  o.n = a.ntot[R];  // the reference's whole list (all shards)
   o.src = a.src[R];
   o.pv = a.pv[R];
   return o;
@@ -1099,7 +1096,7 @@ template <int SRC, bool P2, bool CHECK, bool LIST>
 __global__ __launch_bounds__(TB) void k_fa_local(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
                                                  unsigned long long* __restrict__ part,
                                                  unsigned long long* __restrict__ klist, unsigned long long* slots,
-                                                 const unsigned int* list, GTable g) {
+                                                 unsigned int* list, GTable g) {
   __shared__ FaLds<SRC, TB, TI> sh;
   const uint32_t nl = LIST ? list[0] : 1u;
   for (uint32_t q = LIST ? blockIdx.x : 0u; q < nl; q += gridDim.x) {
@@ -1129,15 +1126,9 @@ __global__ __launch_bounds__(TB) void k_fa_local_fast(Model m, FaRefs a, unsigne
   const FaTile T = fa_tile(a, blockIdx.x);
   fa_cold_slot(T, g, slots);
   bool done = false;
-  if (T.mt == TILE) {
-#define PLUSS_FA_FAST(R)                                            \
-  const FaOne o = fa_one_ref<SRC, R>(a, T);                         \
-  KeyGen kg;                                                        \
-  if constexpr (SRC == SRC_GEN) kg = a.kg[R];                       \
-  done = fa_local_try_fast<SRC, CHECK, R>(m, o, kg, sh, klist, g);
-    PLUSS_FA_REFS(PLUSS_FA_FAST)
+#define PLUSS_FA_FAST(R) done = fa_fast_tile<SRC, CHECK, R>(m, a, T, sh, klist, g);
+  PLUSS_FA_REFS(PLUSS_FA_FAST)
 #undef PLUSS_FA_FAST
-  }
   if (done) {
     if (threadIdx.x < FPW) part[blockIdx.x * (uint64_t)FPW + threadIdx.x] = sh.out[threadIdx.x];
     if (threadIdx.x == FPW) tmax[blockIdx.x] = sh.out[FPW];
@@ -1146,57 +1137,312 @@ __global__ __launch_bounds__(TB) void k_fa_local_fast(Model m, FaRefs a, unsigne
   }
 }
 
-// ---- pass 3: the carry entering each tile applied to its local results (one
-// wave per tile).  A tile whose KL stored starts are all absorbed while it has
-// more is queued for k_fa_rescan (queue[0] = count, then tile indices).
-constexpr int FIXB = 256;
-template <int SRC>  // (instantiated in each source's translation unit)
-__global__ __launch_bounds__(FIXB) void k_fa_fix(FaRefs a, const unsigned long long* __restrict__ pmin,
+// ---- pass 2, one workgroup per chunk of CH tiles (thread i: tile i of the
+// chunk): the chunk's largest sink is published at once (cval, cflag = this
+// pass's epoch), the running max entering the chunk is the max over the
+// reference's earlier chunks (a look-back over published values that never
+// waits on anything but those publications), and the exclusive max scan over
+// the chunk's tiles gives each tile's carry c (pmin).  Then the fix-up: with c
+// entering, element i starts iff key_i > max(c, lp_{i-1}) (lp: the tile's own
+// running max).  A local start stays a start iff key_i > c, a local non-start
+// stays one, and keys increase, so c absorbs exactly the tile's first m local
+// starts; the first surviving start's replay-before term becomes max(c, lp)
+// and every later running max is the local one.  So the start count, hmax
+// and traversed follow from the stored list; a tile whose whole stored list is
+// absorbed while it has more starts is scanned again here by the workgroup
+// (rare).  Last, the chunk's record for the finish: its start count, the
+// largest hmax - (the chunk's starts before that tile), the records and
+// traversed summed.
+constexpr int CH = 256;  // tiles per chunk (== TB: the workgroup rescans a tile with the same threads)
+constexpr int CW = 7;    // words of a chunk record: start count, h', cold, traversed, case 0/1/2 counts
+static_assert(CH == TB, "a chunk workgroup is a tile workgroup");
+__host__ __device__ inline uint64_t fa_chunks(uint64_t tiles) { return (tiles + CH - 1) / CH; }
+
+__device__ __forceinline__ uint32_t fa_chunk_ref(const FaRefs& a, uint64_t c) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int x = 1; x < 6; ++x) r += c >= a.coff[x] ? 1u : 0u;
+  return __builtin_amdgcn_readfirstlane(r);
+}
+
+// block-wide (CH threads) inclusive scan of one value per thread; returns (inclusive, aggregate)
+template <bool MAX>
+__device__ __forceinline__ void fa_block_scan(unsigned long long v, unsigned long long* sw, unsigned long long& inc,
+                                              unsigned long long& agg) {
+  constexpr int NW = CH / 64;
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  const unsigned long long w = sc_wave_scan<MAX>(v, lane);
+  __syncthreads();  // sw is reused
+  if (lane == 63) sw[wid] = w;
+  __syncthreads();
+  unsigned long long pre = 0, all = 0;
+#pragma unroll
+  for (int x = 0; x < NW; ++x) {
+    if (x < (int)wid) pre = sc_op<MAX>(pre, sw[x]);
+    all = sc_op<MAX>(all, sw[x]);
+  }
+  inc = sc_op<MAX>(pre, w);
+  agg = all;
+}
+
+template <int SRC, bool P2>
+__global__ __launch_bounds__(CH) void k_fa_chunk(Model m, FaRefs a, const unsigned long long* __restrict__ tmax,
+                                                 unsigned long long* __restrict__ pmin,
                                                  unsigned long long* __restrict__ part,
-                                                 const unsigned long long* __restrict__ klist, unsigned int* queue) {
-  const uint32_t lane = __lane_id();
-  const uint64_t t = (uint64_t)blockIdx.x * (FIXB / 64) + (threadIdx.x >> 6);
-  if (t >= a.toff[6]) return;                 // wave-uniform
-  const FaTile T = fa_tile(a, t);
-  if (T.lt == 0) return;                      // the reference's first tile: nothing enters it
-  const unsigned long long c = pmin[t];
+                                                 const unsigned long long* __restrict__ klist,
+                                                 unsigned long long* __restrict__ cval, unsigned int* cflag,
+                                                 unsigned long long* __restrict__ crec, uint32_t epoch,
+                                                 unsigned int* slowq, GTable g) {
+  __shared__ FaLds<SRC, TB, TI> sh;
+  __shared__ unsigned long long sw[CH / 64], s_p;
+  __shared__ unsigned int s_next;
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  const uint64_t c = blockIdx.x;
+  if (c == 0 && threadIdx.x == 0) slowq[0] = 0;  // the local pass's queue was read: empty for the next pass
+  const uint32_t r = fa_chunk_ref(a, c);
+  const uint64_t c0 = a.coff[r], lc = c - c0;
+  const uint64_t t0 = a.toff[r], nt = a.toff[r + 1] - t0;
+  const uint64_t tl = lc * CH + threadIdx.x;  // tile within the reference
+  const bool valid = tl < nt;
+  const uint64_t t = t0 + tl;
+  const unsigned long long tm = valid ? tmax[t] : 0ull;
+  // 1. the chunk's largest sink, published; 2. the max over the earlier chunks
+  unsigned long long inc, cmax;
+  fa_block_scan<true>(tm, sw, inc, cmax);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&cval[c], cmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&cflag[c], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (wid == 0) {
+    unsigned long long p = a.cin[r];  // what entered this shard (earlier shards' sinks)
+    for (int64_t hi = (int64_t)lc - 1; hi >= 0; hi -= 64) {
+      const int64_t j = hi - (int64_t)lane;
+      uint32_t spins = 0;
+      while (__ballot(j >= 0 && __hip_atomic_load(&cflag[c0 + j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch)) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 24)) {  // a predecessor never published: flag it and stop waiting
+          if (lane == 0) atomicOr(&g.flags[0], 2u);
+          break;
+        }
+      }
+      const unsigned long long v =
+          j >= 0 ? __hip_atomic_load(&cval[c0 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+      p = sc_op<true>(p, sc_wave_red<true>(v));
+    }
+    if (lane == 0) s_p = p;
+  }
+  __syncthreads();
+  // 3. the carry entering each tile: the chunk's incoming max and the tiles before it in the chunk
+  const unsigned long long up = __shfl_up(inc, 1, 64);
+  unsigned long long cy = s_p;
+  {
+    unsigned long long w = 0;  // sw: the waves' maxima
+    for (int x = 0; x < (int)wid; ++x) w = sw[x] > w ? sw[x] : w;
+    const unsigned long long ex = lane ? (up > w ? up : w) : w;
+    cy = ex > cy ? ex : cy;
+  }
+  if (valid) pmin[t] = cy;
+  // 4. the fix-up
   unsigned long long* pt = part + t * FPW;
-  const uint64_t cnt = pt[FPART];
-  const uint32_t nl = cnt < (uint64_t)KL ? (uint32_t)cnt : (uint32_t)KL;
-  const unsigned long long* kl = klist + t * (uint64_t)(2 * KL);
-  unsigned long long k = KEY_EMPTY, lp = 0;
-  if (lane < nl) {
-    k = kl[2 * lane];
-    lp = kl[2 * lane + 1];
+  unsigned long long pv[FPW];
+#pragma unroll
+  for (int f = 0; f < FPW; ++f) pv[f] = valid ? pt[f] : 0ull;
+  bool resc = false;
+  if (valid && (tl > 0 || a.joff[r] > 0)) {  // (nothing enters the list's first tile)
+    const uint64_t cnt = pv[FPART];
+    const uint32_t nl = cnt < (uint64_t)KL ? (uint32_t)cnt : (uint32_t)KL;
+    const unsigned long long* kl = klist + t * (uint64_t)(2 * KL);
+    uint32_t mm = 0;
+    unsigned long long dsum = 0, lpm = 0;
+    for (; mm < nl; ++mm) {
+      const unsigned long long k = kl[2 * mm], lp = kl[2 * mm + 1];
+      if (k > cy) {
+        lpm = lp;
+        break;
+      }
+      dsum += lp - k;
+    }
+    if (mm == nl && cnt > nl) {
+      resc = true;
+    } else {
+      const bool any = mm < cnt;
+      pv[1] = pv[1] - dsum + (any ? (cy > lpm ? cy : lpm) - lpm : 0ull);
+      pv[FPART] = cnt - mm;
+      pv[FPART + 1] = any ? pv[FPART + 1] + mm : 0ull;
+    }
   }
-  const bool absorbed = lane < nl && k <= c;
-  const uint32_t mm = (uint32_t)__popcll(__ballot(absorbed));  // keys increase: the absorbed starts are a prefix
-  if (mm == nl && cnt > nl) {
-    if (lane == 0) queue[1 + atomicAdd(&queue[0], 1u)] = (unsigned int)t;
-    return;
+  // tiles whose stored starts ran out: scanned again by the whole workgroup, one by one
+  while (__syncthreads_or(resc)) {
+    if (threadIdx.x == 0) s_next = CH;
+    __syncthreads();
+    if (resc) atomicMin(&s_next, threadIdx.x);
+    __syncthreads();
+    const uint32_t who = s_next;
+    const FaTile T = fa_tile(a, t0 + lc * CH + who);
+#define PLUSS_FA_RESCAN(R)                                                                                  \
+  const FaOne o = fa_one_ref<SRC, R>(a, T);                                                                 \
+  KeyGen kg;                                                                                                \
+  if constexpr (SRC == SRC_GEN) kg = a.kg[R];                                                               \
+  unsigned long long key[TI];                                                                               \
+  uint32_t cases, t0s;                                                                                      \
+  bool bad = false;                                                                                         \
+  const unsigned long long cin = pmin[T.gt];                                                                \
+  fa_rt(m, o.pv, sh);                                                                                       \
+  if (T.mt == TILE) {                                                                                       \
+    fa_load_run<SRC, P2, R, TB, TI, true>(m, o, kg, sh, key, cases, t0s, bad);                              \
+    fa_scan<FA_FULL, SRC, TB, TI, true>(m, o, key, cases, t0s, cin, 0, sh, nullptr);                        \
+  } else {                                                                                                  \
+    fa_load_run<SRC, P2, R, TB, TI, false>(m, o, kg, sh, key, cases, t0s, bad);                             \
+    fa_scan<FA_FULL, SRC, TB, TI, false>(m, o, key, cases, t0s, cin, 0, sh, nullptr);                       \
   }
-  const unsigned long long dsum = sc_wave_red<false>(absorbed ? lp - k : 0ull);
-  const unsigned long long lpm = __shfl(lp, (int)(mm < 64 ? mm : 0), 64);  // the first surviving start's
-  if (lane == 0) {
-    const bool any = mm < cnt;
-    pt[1] = pt[1] - dsum + (any ? (c > lpm ? c : lpm) - lpm : 0ull);
-    pt[FPART] = cnt - mm;
-    pt[FPART + 1] = any ? pt[FPART + 1] + mm : 0ull;
+    __threadfence_block();  // pmin of the tile (written above) is read by every thread
+    __syncthreads();
+    PLUSS_FA_REFS(PLUSS_FA_RESCAN)
+#undef PLUSS_FA_RESCAN
+    if (threadIdx.x == who) {
+      pv[1] = sh.out[1];
+      pv[FPART] = sh.out[FPART];
+      pv[FPART + 1] = sh.out[FPART + 1];
+      resc = false;
+    }
+    __syncthreads();  // sh is reused
+  }
+  if (valid) {
+    pt[1] = pv[1];
+    pt[FPART] = pv[FPART];
+    pt[FPART + 1] = pv[FPART + 1];
+  }
+  // 5. the chunk's record
+  unsigned long long cinc, ctot;
+  fa_block_scan<false>(pv[FPART], sw, cinc, ctot);
+  const unsigned long long hp = pv[FPART + 1] ? pv[FPART + 1] - (cinc - pv[FPART]) : 0ull;
+  const unsigned long long red[6] = {sc_wave_red<true>(hp), sc_wave_red<false>(pv[0]), sc_wave_red<false>(pv[1]),
+                                     sc_wave_red<false>(pv[2]), sc_wave_red<false>(pv[3]), sc_wave_red<false>(pv[4])};
+  __shared__ unsigned long long s_red[CH / 64][6];
+  if (lane == 0)
+#pragma unroll
+    for (int f = 0; f < 6; ++f) s_red[wid][f] = red[f];
+  __syncthreads();
+  if (threadIdx.x < CW) {
+    const uint32_t f = threadIdx.x;
+    unsigned long long x = 0;
+    if (f == 0) {
+      x = ctot;
+    } else {
+#pragma unroll
+      for (int w = 0; w < CH / 64; ++w) x = f == 1 ? (s_red[w][0] > x ? s_red[w][0] : x) : x + s_red[w][f - 1];
+    }
+    crec[c * CW + f] = x;
   }
 }
 
-// ---- pass 4: the queued tiles scanned again with the running max entering
-// them (a grid of resident workgroups over the queue; empty queue: nothing)
-template <int SRC, bool P2>
-__global__ __launch_bounds__(TB) void k_fa_rescan(Model m, FaRefs a, const unsigned long long* __restrict__ pmin,
-                                                  unsigned long long* __restrict__ part, const unsigned int* queue) {
+// ---- pass 3, one workgroup per reference with samples: the exclusive sum of
+// the chunks' start counts locates the chunk holding the Q1 cut (the first
+// whose h' >= n + starts before it: the condition j - starts_before_j >= n -
+// j is monotone in j), then the tile inside it the same way; the chunks and
+// tiles before it are summed, that tile is scanned again with its incoming
+// start count (FA_CUT); then Q3 (nothing dropped: the owner of the final
+// largest sink stays in LAT, +1 cold if it is tid 0), the -1 key
+// (materialised even with 0, r10:196,671), traversed (+ the end of the last
+// replay when nothing was cut) and the bins.
+//
+// STORE (a key-range shard, pass 3 of 4): the shard's first cut candidate
+// (global index; the list's length if none), the sums below it (or of the
+// whole shard) and the shard's final running max go to shrec[r]; the global
+// cut decides later what is recorded (k_fa_shard_apply).
+constexpr int SRW = FPART + 2;  // shard record: sums (cold, traversed, case 0/1/2), the cut candidate, the final max
+template <int SRC, bool P2, bool STORE>
+__global__ __launch_bounds__(CH) void k_fa_finish(Model m, FaRefs a, const unsigned long long* __restrict__ tmax,
+                                                  const unsigned long long* __restrict__ pmin,
+                                                  const unsigned long long* __restrict__ part,
+                                                  const unsigned long long* __restrict__ crec,
+                                                  const unsigned long long* __restrict__ slots,
+                                                  unsigned long long* __restrict__ shrec, GTable g) {
+  constexpr int NW = CH / 64;
   __shared__ FaLds<SRC, TB, TI> sh;
-  const uint32_t nq = queue[0];
-  for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
-    const uint64_t gt = queue[1 + q];
-    const FaTile T = fa_tile(a, gt);
-    const unsigned long long c = pmin[gt];
-#define PLUSS_FA_RESCAN(R)                                                                                  \
+  __shared__ unsigned long long sw[NW], s_best, s_cin, s_red[NW][FPART];
+  const uint32_t r = blockIdx.x;
+  if (a.n[r] == 0) return;
+  const uint64_t n = a.ntot[r];  // the Q1 condition is on the whole list
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  const uint64_t t0 = a.toff[r], nt = a.toff[r + 1] - t0;
+  const uint64_t c0 = a.coff[r], nc = a.coff[r + 1] - c0;
+  const unsigned long long slot = slots[r];
+  const unsigned long long gl = tmax[t0 + nt - 1] > pmin[t0 + nt - 1] ? tmax[t0 + nt - 1] : pmin[t0 + nt - 1];
+  unsigned long long v[FPART] = {0, 0, 0, 0, 0};  // this thread's sums: cold, traversed, case 0/1/2
+  // 1. the cut chunk (blocks of CH chunks); run: starts before (earlier shards' included)
+  uint64_t run = a.soff[r], cc = nc, ccin = 0;
+  for (uint64_t b0 = 0; b0 < nc && cc == nc; b0 += CH) {
+    const uint64_t i = b0 + threadIdx.x;
+    const bool ok = i < nc;
+    unsigned long long rec[CW];
+#pragma unroll
+    for (int f = 0; f < CW; ++f) rec[f] = ok ? crec[(c0 + i) * CW + f] : 0ull;
+    unsigned long long inc, tot;
+    fa_block_scan<false>(rec[0], sw, inc, tot);
+    const unsigned long long ex = run + inc - rec[0];
+    const bool hit = ok && rec[1] >= n + ex;
+    const unsigned long long cand = sc_wave_red_min(hit ? i : KEY_EMPTY);
+    __syncthreads();
+    if (threadIdx.x == 0) s_best = KEY_EMPTY;
+    __syncthreads();
+    if (lane == 0 && cand != KEY_EMPTY) atomicMin(&s_best, cand);
+    __syncthreads();
+    const unsigned long long best = s_best;
+    if (hit && i == best) s_cin = ex;
+    if (ok && (best == KEY_EMPTY || i < best)) {
+      v[0] += rec[2];
+      v[1] += rec[3];
+      v[2] += rec[4];
+      v[3] += rec[5];
+      v[4] += rec[6];
+    }
+    __syncthreads();
+    if (best != KEY_EMPTY) {  // block-uniform
+      cc = best;
+      ccin = s_cin;
+    }
+    run += tot;
+  }
+  // 2. the cut tile inside the cut chunk
+  uint64_t ct = nt, cin = 0;
+  if (cc < nc) {
+    const uint64_t tl = cc * CH + threadIdx.x;
+    const bool ok = tl < nt;
+    unsigned long long pw[FPW];
+#pragma unroll
+    for (int f = 0; f < FPW; ++f) pw[f] = ok ? part[(t0 + tl) * FPW + f] : 0ull;
+    unsigned long long inc, tot;
+    fa_block_scan<false>(pw[FPART], sw, inc, tot);
+    const unsigned long long ex = ccin + inc - pw[FPART];
+    const bool hit = ok && pw[FPART + 1] >= n + ex;
+    const unsigned long long cand = sc_wave_red_min(hit ? tl : KEY_EMPTY);
+    __syncthreads();
+    if (threadIdx.x == 0) s_best = KEY_EMPTY;
+    __syncthreads();
+    if (lane == 0 && cand != KEY_EMPTY) atomicMin(&s_best, cand);
+    __syncthreads();
+    const unsigned long long best = s_best;  // the chunk holds a tile that qualifies
+    if (hit && tl == best) s_cin = ex;
+    if (ok && tl < best)
+#pragma unroll
+      for (int f = 0; f < FPART; ++f) v[f] += pw[f];
+    __syncthreads();
+    ct = best;
+    cin = s_cin;
+  }
+#pragma unroll
+  for (int f = 0; f < FPART; ++f) {
+    v[f] = sc_wave_red<false>(v[f]);
+    if (lane == 0) s_red[wid][f] = v[f];
+  }
+  // 3. the cut tile, below the cut
+  uint64_t cut = n;
+  if (ct < nt) {
+    __syncthreads();
+    const FaTile T = fa_tile(a, t0 + ct);
+    const unsigned long long carry = pmin[t0 + ct];
+#define PLUSS_FA_CUT(R)                                                                                     \
   const FaOne o = fa_one_ref<SRC, R>(a, T);                                                                 \
   KeyGen kg;                                                                                                \
   if constexpr (SRC == SRC_GEN) kg = a.kg[R];                                                               \
@@ -1206,175 +1452,30 @@ __global__ __launch_bounds__(TB) void k_fa_rescan(Model m, FaRefs a, const unsig
   fa_rt(m, o.pv, sh);                                                                                       \
   if (T.mt == TILE) {                                                                                       \
     fa_load_run<SRC, P2, R, TB, TI, true>(m, o, kg, sh, key, cases, t0s, bad);                              \
-    fa_scan<FA_FULL, SRC, TB, TI, true>(m, o, key, cases, t0s, c, 0, sh, nullptr);                          \
+    fa_scan<FA_CUT, SRC, TB, TI, true>(m, o, key, cases, t0s, carry, cin, sh, nullptr);                     \
   } else {                                                                                                  \
     fa_load_run<SRC, P2, R, TB, TI, false>(m, o, kg, sh, key, cases, t0s, bad);                             \
-    fa_scan<FA_FULL, SRC, TB, TI, false>(m, o, key, cases, t0s, c, 0, sh, nullptr);                         \
-  }
-    PLUSS_FA_REFS(PLUSS_FA_RESCAN)
-#undef PLUSS_FA_RESCAN
-    if (threadIdx.x < FPW) part[gt * FPW + threadIdx.x] = sh.out[threadIdx.x];
-    __syncthreads();  // sh is reused by the next queued tile
-  }
-}
-
-// ---- pass 5, one workgroup of FT threads per reference with samples: the
-// exclusive sum of its tiles' start counts locates the tile holding the Q1
-// cut (the first with hmax >= n + starts before it); the tiles before it are
-// summed whole, that tile is scanned again with its incoming start count
-// (FA_CUT; FT threads x TILE/FT elements); then Q3 (nothing dropped: the owner
-// of the final largest sink stays in LAT, +1 cold if it is tid 0), the -1
-// key (materialised even with 0, r10:196,671), traversed (+ the end of the
-// last replay when nothing was cut) and the bins.
-constexpr int FT = 1024;
-template <int SRC, bool P2>
-__global__ __launch_bounds__(FT) void k_fa_finish(Model m, FaRefs a, const unsigned long long* __restrict__ tmax,
-                                                  const unsigned long long* __restrict__ pmin,
-                                                  const unsigned long long* __restrict__ part,
-                                                  const unsigned long long* __restrict__ slots, GTable g) {
-  constexpr int NW = FT / 64;
-  __shared__ FaLds<SRC, FT, TILE / FT> sh;
-  __shared__ unsigned long long s_ct, s_red[NW][FPART];
-  const uint32_t r = blockIdx.x;
-  const uint64_t n = a.n[r];
-  if (n == 0) return;
-  const uint64_t t0 = a.toff[r], nt = a.toff[r + 1] - t0;
-  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  // read early (latency): the cold key's slot, the last tile's sinks (Q3)
-  const unsigned long long slot = slots[r];
-  const unsigned long long gl = tmax[t0 + nt - 1] > pmin[t0 + nt - 1] ? tmax[t0 + nt - 1] : pmin[t0 + nt - 1];
-  // 1. the cut tile; the partials of the tiles before it are summed on the way
-  uint64_t ct = nt, cin = 0, c = 0;
-  unsigned long long v[FPART] = {0, 0, 0, 0, 0};
-  if (nt > FT) {  // many tiles (2^24+ samples per reference): each thread a contiguous run of them
-    const uint64_t per = (nt + FT - 1) / FT;
-    const uint64_t lo = threadIdx.x * per < nt ? threadIdx.x * per : nt, hi = lo + per < nt ? lo + per : nt;
-    const unsigned long long* pt = part + t0 * FPW;
-    constexpr int FB = 8;  // loads of a batch in flight together
-    unsigned long long cs = 0;
-    for (uint64_t t = lo; t < hi; t += FB) {
-      unsigned long long x[FB];
-#pragma unroll
-      for (int k = 0; k < FB; ++k) x[k] = t + k < hi ? pt[(t + k) * FPW + FPART] : 0ull;
-#pragma unroll
-      for (int k = 0; k < FB; ++k) cs += x[k];
-    }
-    const unsigned long long inc = sc_wave_scan<false>(cs, lane);
-    if (lane == 63) sh.c[wid] = inc;
-    __syncthreads();
-    unsigned long long run = inc - cs;
-#pragma unroll
-    for (int x = 0; x < NW; ++x)
-      if (x < (int)wid) run += sh.c[x];
-    unsigned long long hit = KEY_EMPTY, hcin = 0;
-    for (uint64_t t = lo; t < hi; t += FB) {
-      unsigned long long x[FB], h[FB];
-#pragma unroll
-      for (int k = 0; k < FB; ++k) {
-        x[k] = t + k < hi ? pt[(t + k) * FPW + FPART] : 0ull;
-        h[k] = t + k < hi ? pt[(t + k) * FPW + FPART + 1] : 0ull;
-      }
-#pragma unroll
-      for (int k = 0; k < FB; ++k) {
-        if (hit == KEY_EMPTY && t + k < hi && h[k] >= n + run) {
-          hit = t + k;
-          hcin = run;
-        }
-        run += x[k];
-      }
-    }
-    const unsigned long long cand = sc_wave_red_min(hit);
-    if (lane == 0) sh.w[wid] = cand;
-    __syncthreads();
-    unsigned long long best = KEY_EMPTY;
-#pragma unroll
-    for (int x = 0; x < NW; ++x) best = sh.w[x] < best ? sh.w[x] : best;
-    if (best != KEY_EMPTY && hit == best) s_ct = hcin;
-    __syncthreads();
-    if (best != KEY_EMPTY) {  // block-uniform
-      ct = best;
-      cin = s_ct;
-    }
-    const uint64_t hi2 = hi < ct ? hi : ct;
-    for (uint64_t t = lo; t < hi2; t += FB / 2) {
-      unsigned long long x[FB / 2][FPART];
-#pragma unroll
-      for (int k = 0; k < FB / 2; ++k)
-#pragma unroll
-        for (int f = 0; f < FPART; ++f) x[k][f] = t + k < hi2 ? pt[(t + k) * FPW + f] : 0ull;
-#pragma unroll
-      for (int k = 0; k < FB / 2; ++k)
-#pragma unroll
-        for (int f = 0; f < FPART; ++f) v[f] += x[k][f];
-    }
-  } else
-  for (uint64_t b0 = 0; b0 < nt; b0 += FT) {  // one chunk: one tile per thread
-    const uint64_t t = b0 + threadIdx.x;
-    unsigned long long pw[FPW];
-#pragma unroll
-    for (int f = 0; f < FPW; ++f) pw[f] = t < nt ? part[(t0 + t) * FPW + f] : 0ull;
-    const unsigned long long cnt = pw[FPART], h = pw[FPART + 1];
-    const unsigned long long inc = sc_wave_scan<false>(cnt, lane);
-    if (lane == 63) sh.c[wid] = inc;
-    __syncthreads();
-    unsigned long long pre = c, tot = 0;
-#pragma unroll
-    for (int x = 0; x < NW; ++x) {
-      if (x < (int)wid) pre += sh.c[x];
-      tot += sh.c[x];
-    }
-    const unsigned long long excl = pre + inc - cnt;
-    const bool hit = t < nt && h >= n + excl;
-    const unsigned long long cand = sc_wave_red_min(hit ? t : KEY_EMPTY);
-    if (lane == 0) sh.w[wid] = cand;
-    __syncthreads();
-    unsigned long long best = KEY_EMPTY;
-#pragma unroll
-    for (int x = 0; x < NW; ++x) best = sh.w[x] < best ? sh.w[x] : best;
-    if (best == KEY_EMPTY || t < best)
-#pragma unroll
-      for (int f = 0; f < FPART; ++f) v[f] += pw[f];
-    if (best != KEY_EMPTY) {  // block-uniform
-      if (t == best) s_ct = excl;
-      __syncthreads();
-      ct = best;
-      cin = s_ct;
-      break;
-    }
-    c += tot;
-    __syncthreads();  // sh.c / sh.w are rewritten by the next chunk
-  }
-#pragma unroll
-  for (int f = 0; f < FPART; ++f) {
-    v[f] = sc_wave_red<false>(v[f]);
-    if (lane == 0) s_red[wid][f] = v[f];
-  }
-  // 2. the cut tile, below the cut
-  uint64_t cut = n;
-  if (ct < nt) {
-    __syncthreads();
-    const FaTile T = fa_tile(a, t0 + ct);
-    const unsigned long long carry = pmin[t0 + ct];
-    constexpr int FE = TILE / FT;
-#define PLUSS_FA_CUT(R)                                                                                     \
-  const FaOne o = fa_one_ref<SRC, R>(a, T);                                                                 \
-  KeyGen kg;                                                                                                \
-  if constexpr (SRC == SRC_GEN) kg = a.kg[R];                                                               \
-  unsigned long long key[FE];                                                                               \
-  uint32_t cases, t0s;                                                                                      \
-  bool bad = false;                                                                                         \
-  fa_rt(m, o.pv, sh);                                                                                       \
-  if (T.mt == TILE) {                                                                                       \
-    fa_load_run<SRC, P2, R, FT, FE, true>(m, o, kg, sh, key, cases, t0s, bad);                              \
-    fa_scan<FA_CUT, SRC, FT, FE, true>(m, o, key, cases, t0s, carry, cin, sh, nullptr);                     \
-  } else {                                                                                                  \
-    fa_load_run<SRC, P2, R, FT, FE, false>(m, o, kg, sh, key, cases, t0s, bad);                             \
-    fa_scan<FA_CUT, SRC, FT, FE, false>(m, o, key, cases, t0s, carry, cin, sh, nullptr);                    \
+    fa_scan<FA_CUT, SRC, TB, TI, false>(m, o, key, cases, t0s, carry, cin, sh, nullptr);                    \
   }
     PLUSS_FA_REFS(PLUSS_FA_CUT)
 #undef PLUSS_FA_CUT
   }
   __syncthreads();
+  if (STORE) {
+    if (threadIdx.x < FPART) {
+      const uint32_t f = threadIdx.x;
+      unsigned long long x = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) x += s_red[w][f];
+      if (ct < nt) x += sh.out[f];
+      shrec[r * SRW + f] = x;
+    } else if (threadIdx.x == FPART) {
+      shrec[r * SRW + FPART] = ct < nt ? sh.out[FPART] : n;
+    } else if (threadIdx.x == FPART + 1) {
+      shrec[r * SRW + FPART + 1] = gl;
+    }
+    return;
+  }
   if (threadIdx.x < FPART) {  // one sum per thread, then plain no-return atomics
     const uint32_t f = threadIdx.x;
     unsigned long long x = 0;
@@ -1396,6 +1497,55 @@ __global__ __launch_bounds__(FT) void k_fa_finish(Model m, FaRefs a, const unsig
     }
   }
 }
+// pass 4 of a key-range shard: with the global cut of each reference (the
+// smallest candidate over the shards), record this shard's part: nothing if
+// the cut lies before it; its sums below the cut if it holds the cut; all of
+// it otherwise, and, on the list's last shard with nothing cut, Q3 and the end
+// of the last replay (as k_fa_finish does on one GPU).
+struct FaShardCut {
+  uint64_t cut[6];  // the global cut of each reference (its list's length: none)
+  int32_t last[6];  // this shard is the reference's last with samples
+};
+template <int X = 0>  // (a template: instantiated only where launched)
+__global__ void k_fa_shard_apply(Model m, FaRefs a, const unsigned long long* __restrict__ shrec, FaShardCut c,
+                                 const unsigned long long* __restrict__ slots, GTable g) {
+  const uint32_t r = threadIdx.x;
+  if (r >= 6 || a.n[r] == 0) return;
+  const unsigned long long* sr = shrec + r * SRW;
+  const uint64_t G = c.cut[r], start = a.joff[r], n = a.ntot[r];
+  if (G < start) return;  // dropped by Q1 in an earlier shard
+  unsigned long long cold = sr[0], trav = sr[1];
+  if (G == n && c.last[r]) {
+    const unsigned long long gl = sr[FPART + 1];
+    if (gl != KEY_EMPTY && gl % m.T == 0) cold += 1;
+    trav += gl == KEY_EMPTY ? m.A * m.T : gl;
+  }
+  if (slots[r] != ~0ull && cold) atomicAdd(&g.counts[slots[r]], cold);
+  atomicAdd(&g.trav[r], trav);
+  for (int c = 0; c < 3; ++c)
+    if (sr[2 + c]) atomicAdd(&g.bins[r * 3 + c], sr[2 + c]);
+}
+
+// per reference: the largest of its tiles' sinks (max_out[r]) and the sum of
+// its chunks' start counts (starts_out[r]); either pointer may be null
+template <int X = 0>  // (a template: instantiated only where launched)
+__global__ void k_fa_shard_sums(FaRefs a, const unsigned long long* __restrict__ tmax,
+                                const unsigned long long* __restrict__ crec, unsigned long long* max_out,
+                                unsigned long long* starts_out) {
+  const uint32_t r = blockIdx.x, lane = __lane_id();
+  unsigned long long mx = 0, st = 0;
+  if (max_out)
+    for (uint64_t t = a.toff[r] + lane; t < a.toff[r + 1]; t += 64) mx = tmax[t] > mx ? tmax[t] : mx;
+  if (starts_out)
+    for (uint64_t c = a.coff[r] + lane; c < a.coff[r + 1]; c += 64) st += crec[c * CW];
+  mx = sc_wave_red<true>(mx);
+  st = sc_wave_red<false>(st);
+  if (lane == 0) {
+    if (max_out) max_out[r] = mx;
+    if (starts_out) starts_out[r] = st;
+  }
+}
+
 #undef PLUSS_FA_REFS
 
 // ---- launching the pipeline for one element source (each source's kernels
@@ -1405,32 +1555,56 @@ struct FaLaunch {
   FaRefs a;
   GTable g;
   FaithfulBufs* b;
-  bool p2;      // shift decoding (fa_run)
-  uint64_t t;   // tiles of all references
+  bool p2;        // shift decoding (fa_run)
+  uint64_t t;     // tiles of all references
+  uint32_t epoch; // this pass's chunk-publication epoch
+  int phase;      // FA_PH_*
   hipStream_t s;
 };
+
+// phases of the pipeline: 1 local pass, 2 chunks (carry, fix-up), 3 finish
+// (one GPU: the bins; a shard: its record), 4 a shard's record applied
+enum : int { FA_PH_ALL = 0, FA_PH_LOCAL = 1, FA_PH_CHUNK = 2, FA_PH_CUT = 3, FA_PH_APPLY = 4 };
 
 template <int SRC, bool CHK, bool P2>
 inline void fa_launch_t(const FaLaunch& L) {
   FaithfulBufs& b = *L.b;
   const unsigned t = (unsigned)L.t;
-  const unsigned nfix = (unsigned)((L.t + FIXB / 64 - 1) / (FIXB / 64));
   const unsigned nres = t < 512 ? t : 512u;
-  if (P2 && L.a.fast) {  // fast tiles, then the queued rest
-    hipLaunchKernelGGL((k_fa_local_fast<SRC, CHK>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
-                       b.fslot, b.slowq, L.g);
-    hipLaunchKernelGGL((k_fa_local<SRC, P2, CHK, true>), dim3(nres), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart,
-                       b.klist, b.fslot, (const unsigned int*)b.slowq, L.g);
-  } else {
-    hipLaunchKernelGGL((k_fa_local<SRC, P2, CHK, false>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
-                       b.fslot, (const unsigned int*)nullptr, L.g);
+  const int ph = L.phase;
+  if (ph == FA_PH_ALL || ph == FA_PH_LOCAL) {
+    bool fast = false;
+    if constexpr (P2) {  // fast tiles, then the queued rest (an empty queue: the workgroups return at once)
+      if (L.a.fast) {
+        hipLaunchKernelGGL((k_fa_local_fast<SRC, CHK>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
+                           b.fslot, b.slowq, L.g);
+        hipLaunchKernelGGL((k_fa_local<SRC, P2, CHK, true>), dim3(nres), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart,
+                           b.klist, b.fslot, b.slowq, L.g);
+        fast = true;
+      }
+    }
+    if (!fast) {
+      hipLaunchKernelGGL((k_fa_local<SRC, P2, CHK, false>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart,
+                         b.klist, b.fslot, (unsigned int*)nullptr, L.g);
+    }
   }
-  hipLaunchKernelGGL(k_fa_prefix<SRC>, dim3(6), dim3(PB), 0, L.s, L.a, b.tmax, b.pmin, b.queue, b.slowq);
-  hipLaunchKernelGGL(k_fa_fix<SRC>, dim3(nfix), dim3(FIXB), 0, L.s, L.a, b.pmin, b.dpart, b.klist, b.queue);
-  hipLaunchKernelGGL((k_fa_rescan<SRC, P2>), dim3(nres), dim3(TB), 0, L.s, L.m, L.a, b.pmin, b.dpart, b.queue);
-  hipLaunchKernelGGL((k_fa_finish<SRC, P2>), dim3(6), dim3(FT), 0, L.s, L.m, L.a, b.tmax, b.pmin, b.dpart, b.fslot,
-                     L.g);
+  if (ph == FA_PH_ALL || ph == FA_PH_CHUNK)
+    hipLaunchKernelGGL((k_fa_chunk<SRC, P2>), dim3((unsigned)L.a.coff[6]), dim3(CH), 0, L.s, L.m, L.a, b.tmax,
+                       b.pmin, b.dpart, b.klist, b.cval, b.cflag, b.crec, L.epoch, b.slowq, L.g);
+  if (ph == FA_PH_ALL)
+    hipLaunchKernelGGL((k_fa_finish<SRC, P2, false>), dim3(6), dim3(CH), 0, L.s, L.m, L.a, b.tmax, b.pmin, b.dpart,
+                       b.crec, b.fslot, b.shrec, L.g);
+  if (ph == FA_PH_CUT)
+    hipLaunchKernelGGL((k_fa_finish<SRC, P2, true>), dim3(6), dim3(CH), 0, L.s, L.m, L.a, b.tmax, b.pmin, b.dpart,
+                       b.crec, b.fslot, b.shrec, L.g);
 }
+
+// a key-range shard's pass between its phases (pluss_dev_faithful_shards_*)
+struct FaShards {
+  FaLaunch L;
+  int src = SRC_GEN;
+  int phase = 0;  // last completed phase (1 local, 2 carry, 3 cut)
+};
 
 // the four sources (pluss_fa_w32.hip, pluss_fa_w64.hip, pluss_fa_smp.hip, pluss_fa_gen.hip)
 void fa_launch_w32(const FaLaunch& L);

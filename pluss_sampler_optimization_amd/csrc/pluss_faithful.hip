@@ -710,7 +710,7 @@ static int fork_refs(pluss_ctx* ctx, const uint64_t* counts, hipStream_t s, F&& 
 // ---- the scan pipeline (k_fa_*) over the references with a.n[r] > 0, on
 // stream s.  Its buffers are the handle's (ctx->fb): tile maxima, prefixes
 // and per-tile partials, sized by the tiles of all references.
-static int fa_reserve(FaithfulBufs& b, uint64_t tiles, hipStream_t s) {
+static int fa_reserve(FaithfulBufs& b, uint64_t tiles, uint64_t chunks, hipStream_t s) {
   if (!b.fslot) {
     if (int rc = grow(&b.fslot, 8)) return rc;
   }
@@ -718,15 +718,26 @@ static int fa_reserve(FaithfulBufs& b, uint64_t tiles, hipStream_t s) {
     PLUSS_HIP_CHECK(hipStreamSynchronize(s));
     int rc = 0;
     if ((rc = grow(&b.dpart, tiles * FPW)) || (rc = grow(&b.tmax, tiles)) || (rc = grow(&b.pmin, tiles)) ||
-        (rc = grow(&b.klist, tiles * 2 * KL)) || (rc = grow(&b.queue, tiles + 1)) || (rc = grow(&b.slowq, tiles + 1)))
+        (rc = grow(&b.klist, tiles * 2 * KL)) || (rc = grow(&b.slowq, tiles + 1)))
       return rc;
-    PLUSS_HIP_CHECK(hipMemsetAsync(b.slowq, 0, 4, s));  // k_fa_prefix empties it after every pass
+    PLUSS_HIP_CHECK(hipMemsetAsync(b.slowq, 0, 4, s));  // k_fa_chunk empties it after every pass
     b.dcap = tiles;
+  }
+  if (chunks > b.ccap) {
+    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+    int rc = 0;
+    if ((rc = grow(&b.cval, chunks)) || (rc = grow(&b.crec, chunks * CW)) || (rc = grow(&b.cflag, chunks))) return rc;
+    PLUSS_HIP_CHECK(hipMemsetAsync(b.cflag, 0, chunks * sizeof(unsigned int), s));
+    b.epoch = 0;
+    b.ccap = chunks;
   }
   return PLUSS_OK;
 }
 
-static int fa_run(pluss_ctx* ctx, FaRefs& a, int src, bool check, hipStream_t s) {
+// Tile and chunk offsets, buffers and the launch description of one pass
+// over `a` (a.n set; one GPU: the whole lists, ntot = n; a key-range shard:
+// joff, ntot set by the caller).  *L.t == 0: nothing to do.
+static int fa_prepare(pluss_ctx* ctx, FaRefs& a, int src, bool check, bool shard, hipStream_t s, FaLaunch* out) {
   const Model& m = ctx->m;
   uint64_t t = 0;
   for (int r = 0; r < 6; ++r) {
@@ -734,35 +745,64 @@ static int fa_run(pluss_ctx* ctx, FaRefs& a, int src, bool check, hipStream_t s)
       set_error("faithful mode: at most 2^32-1 samples per reference");
       return PLUSS_ERR_CONFIG;
     }
+    if (!shard) {
+      a.ntot[r] = a.n[r];
+      a.joff[r] = 0;
+      a.soff[r] = 0;
+      a.cin[r] = 0;
+    }
     a.toff[r] = t;
     t += fa_tiles(a.n[r]);
     a.pv[r] = make_pkview(m, (uint32_t)r);
   }
   a.toff[6] = t;
-  if (t == 0) return PLUSS_OK;
+  uint64_t c = 0;
+  for (int r = 0; r < 6; ++r) {
+    a.coff[r] = c;
+    c += fa_chunks(a.toff[r + 1] - a.toff[r]);
+  }
+  a.coff[6] = c;
   if (src == SRC_SAMPLES && !check) {
     set_error("faithful mode: a caller's list is always order-checked");
     return PLUSS_ERR_CONFIG;
   }
   FaithfulBufs& b = ctx->fb;
-  if (int rc = fa_reserve(b, t, s)) return rc;
-  const GTable& g = ctx->g;
   // N, T, CS, CLS/DS powers of two: shift decoding (the word decode also
   // keeps q*N + c1 < N*N/T in 32 bits)
   const bool p2 = m.p2 && a.pv[0].p2 && (uint64_t)m.N * m.N / m.T < (1ull << 32);
   // the local pass's fast path: 24-bit multiplies (q*N + c1 < N*N/T and S
   // below 2^24) and the range check by bit masks (N a power of two)
   a.fast = (p2 && m.np2 && (uint64_t)m.N * m.N / m.T < (1ull << 24) && m.S < (1u << 24)) ? 1u : 0u;
-  const FaLaunch L{m, a, g, &b, p2, t, s};
+  *out = FaLaunch{m, a, ctx->g, &b, p2, t, 0, FA_PH_ALL, s};
+  if (t == 0) return PLUSS_OK;
+  if (int rc = fa_reserve(b, t, c, s)) return rc;
+  if (!b.shrec) {
+    if (int rc = grow(&b.shrec, 6 * SRW + 16)) return rc;
+  }
+  if (++b.epoch == 0) ++b.epoch;  // (0: never published)
+  out->epoch = b.epoch;
+  return PLUSS_OK;
+}
+
+static int fa_launch(pluss_ctx* ctx, const FaLaunch& L, int src, int phase) {
+  FaLaunch l = L;
+  l.phase = phase;
   switch (src) {
-    case SRC_W32: fa_launch_w32(L); break;
-    case SRC_W64: fa_launch_w64(L); break;
-    case SRC_SAMPLES: fa_launch_smp(L); break;
-    default: fa_launch_gen(L); break;
+    case SRC_W32: fa_launch_w32(l); break;
+    case SRC_W64: fa_launch_w64(l); break;
+    case SRC_SAMPLES: fa_launch_smp(l); break;
+    default: fa_launch_gen(l); break;
   }
   PLUSS_HIP_CHECK(hipGetLastError());
   ctx->tables_dirty = true;
   return PLUSS_OK;
+}
+
+static int fa_run(pluss_ctx* ctx, FaRefs& a, int src, bool check, hipStream_t s) {
+  FaLaunch L;
+  if (int rc = fa_prepare(ctx, a, src, check, false, s, &L)) return rc;
+  if (L.t == 0) return PLUSS_OK;
+  return fa_launch(ctx, L, src, FA_PH_ALL);
 }
 
 static FaRefs fa_none() {
@@ -850,9 +890,12 @@ int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64
       return faith_pairs_scan(ctx, b, r, counts[r], rs);
     });
   }
-  uint64_t tiles = 0;
-  for (int r = 0; r < 6; ++r) tiles += fa_tiles(counts[r]);
-  if (int rc = fa_reserve(ctx->fb, tiles, s)) return rc;
+  uint64_t tiles = 0, chunks = 0;
+  for (int r = 0; r < 6; ++r) {
+    tiles += fa_tiles(counts[r]);
+    chunks += fa_chunks(fa_tiles(counts[r]));
+  }
+  if (int rc = fa_reserve(ctx->fb, tiles, chunks, s)) return rc;
   if (int rc = fork_refs(ctx, counts, s, [&](int r, FaithfulBufs& b, hipStream_t rs) {
         return faith_keys_sorted(ctx, b, r, d_samples + off[r], counts[r], rs);
       }))
@@ -993,6 +1036,127 @@ int faith_shard_hist(pluss_ctx* ctx, uint64_t cut, uint64_t next_first_key, int 
   hipLaunchKernelGGL(k_faith_init, dim3(1), dim3(1), 0, s, b.scal, cut);
   f.phase = 0;
   return faith_record(ctx, b, f.ref, f.n, f.j_off, f.pmax_in, next_start, f.n_total, is_last, s);
+}
+
+// ---- key-range shards of the single-read pipeline (multi-GPU faithful mode;
+// dist.sharded_faithful_gen_hist): the caller exchanges the per-reference
+// summaries between the four phases
+int faith_shards_local(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t seed, const uint64_t* totals,
+                       const uint64_t* first, const uint64_t* n, uint64_t* max_sink, hipStream_t s) {
+  if (int rc = faith_direct_shape(ctx, "pluss_dev_faithful_shards_local")) return rc;
+  FaRefs a = fa_none();
+  uint64_t off = 0;
+  for (int r = 0; r < 6; ++r) {
+    a.n[r] = n[r];
+    a.ntot[r] = totals[r];
+    a.joff[r] = first[r];
+    if (first[r] > totals[r] || n[r] > totals[r] - first[r]) {
+      set_error("pluss_dev_faithful_shards_local: [first, first + n) exceeds the list");
+      return PLUSS_ERR_CONFIG;
+    }
+    if (d_samples) {
+      a.src[r] = d_samples + off;
+      off += n[r];
+    } else if (n[r]) {
+      if (int rc = keygen_check(ctx, r, totals[r], first[r], n[r], "pluss_dev_faithful_shards_local")) return rc;
+      a.kg[r] = keygen_of(ctx, seed, r, totals[r]);
+    }
+  }
+  if (off && !d_samples) {
+    set_error("pluss_dev_faithful_shards_local: null sample list");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (!ctx->fsh2) ctx->fsh2 = new FaShards();
+  FaShards& f = *ctx->fsh2;
+  f = FaShards{};
+  f.src = d_samples ? SRC_SAMPLES : SRC_GEN;
+  if (int rc = fa_prepare(ctx, a, f.src, true, true, s, &f.L)) return rc;
+  for (int r = 0; r < 6; ++r) max_sink[r] = 0;
+  if (f.L.t) {
+    if (int rc = fa_launch(ctx, f.L, f.src, FA_PH_LOCAL)) return rc;
+    FaithfulBufs& b = ctx->fb;
+    hipLaunchKernelGGL(k_fa_shard_sums<0>, dim3(6), dim3(64), 0, s, f.L.a, b.tmax, b.crec, b.shrec + 6 * SRW,
+                       (unsigned long long*)nullptr);
+    PLUSS_HIP_CHECK(hipGetLastError());
+    PLUSS_HIP_CHECK(hipMemcpyAsync(max_sink, b.shrec + 6 * SRW, 6 * 8, hipMemcpyDeviceToHost, s));
+    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  f.phase = 1;
+  return PLUSS_OK;
+}
+
+int faith_shards_carry(pluss_ctx* ctx, const uint64_t* carry_in, uint64_t* starts, hipStream_t s) {
+  if (!ctx->fsh2) ctx->fsh2 = new FaShards();
+  FaShards& f = *ctx->fsh2;
+  if (f.phase != 1) {
+    set_error("pluss_dev_faithful_shards_carry: call pluss_dev_faithful_shards_local first");
+    return PLUSS_ERR_CONFIG;
+  }
+  for (int r = 0; r < 6; ++r) {
+    f.L.a.cin[r] = carry_in[r];
+    starts[r] = 0;
+  }
+  if (f.L.t) {
+    if (int rc = fa_launch(ctx, f.L, f.src, FA_PH_CHUNK)) return rc;
+    FaithfulBufs& b = ctx->fb;
+    hipLaunchKernelGGL(k_fa_shard_sums<0>, dim3(6), dim3(64), 0, s, f.L.a, b.tmax, b.crec, (unsigned long long*)nullptr,
+                       b.shrec + 6 * SRW + 8);
+    PLUSS_HIP_CHECK(hipGetLastError());
+    PLUSS_HIP_CHECK(hipMemcpyAsync(starts, b.shrec + 6 * SRW + 8, 6 * 8, hipMemcpyDeviceToHost, s));
+    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  f.phase = 2;
+  return PLUSS_OK;
+}
+
+int faith_shards_cut(pluss_ctx* ctx, const uint64_t* starts_before, uint64_t* cut, hipStream_t s) {
+  if (!ctx->fsh2) ctx->fsh2 = new FaShards();
+  FaShards& f = *ctx->fsh2;
+  if (f.phase != 2) {
+    set_error("pluss_dev_faithful_shards_cut: call pluss_dev_faithful_shards_carry first");
+    return PLUSS_ERR_CONFIG;
+  }
+  for (int r = 0; r < 6; ++r) {
+    f.L.a.soff[r] = starts_before[r];
+    cut[r] = f.L.a.ntot[r];
+  }
+  if (f.L.t) {
+    if (int rc = fa_launch(ctx, f.L, f.src, FA_PH_CUT)) return rc;
+    FaithfulBufs& b = ctx->fb;
+    unsigned long long rec[6 * SRW];
+    PLUSS_HIP_CHECK(hipMemcpyAsync(rec, b.shrec, sizeof rec, hipMemcpyDeviceToHost, s));
+    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+    for (int r = 0; r < 6; ++r)
+      if (f.L.a.n[r]) cut[r] = rec[r * SRW + FPART];
+  }
+  f.phase = 3;
+  return PLUSS_OK;
+}
+
+int faith_shards_hist(pluss_ctx* ctx, const uint64_t* cut, const int32_t* is_last, hipStream_t s) {
+  if (!ctx->fsh2) ctx->fsh2 = new FaShards();
+  FaShards& f = *ctx->fsh2;
+  if (f.phase != 3) {
+    set_error("pluss_dev_faithful_shards_hist: call pluss_dev_faithful_shards_cut first");
+    return PLUSS_ERR_CONFIG;
+  }
+  f.phase = 0;
+  if (!f.L.t) return PLUSS_OK;
+  FaShardCut c;
+  for (int r = 0; r < 6; ++r) {
+    c.cut[r] = cut[r];
+    c.last[r] = is_last[r];
+  }
+  FaithfulBufs& b = ctx->fb;
+  hipLaunchKernelGGL(k_fa_shard_apply<0>, dim3(1), dim3(64), 0, s, f.L.m, f.L.a, b.shrec, c, b.fslot, f.L.g);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  ctx->tables_dirty = true;
+  return PLUSS_OK;
+}
+
+void faith_shards_free(pluss_ctx* ctx) {
+  delete ctx->fsh2;
+  ctx->fsh2 = nullptr;
 }
 
 }  // namespace pluss

@@ -67,8 +67,12 @@ struct FaithfulBufs {
   // running max entering it, its first local starts; the queue of tiles to scan again
   uint64_t dcap = 0;
   unsigned long long *dpart = nullptr, *tmax = nullptr, *pmin = nullptr, *klist = nullptr;
-  unsigned int* queue = nullptr;  // tiles to scan again with their carry: [0] count, then indices
-  unsigned int* slowq = nullptr;  // tiles the local fast path left (zero count between passes)
+  unsigned int* slowq = nullptr;  // tiles the local fast path left: [0] count (zero between passes), then indices
+  uint64_t ccap = 0;              // chunks (of k_fa_chunk's CH tiles) the buffers below hold
+  unsigned long long *cval = nullptr, *crec = nullptr;  // per chunk: its largest sink; its summary for the finish
+  unsigned int* cflag = nullptr;  // per chunk: the epoch of the pass that published cval (zeroed once)
+  uint32_t epoch = 0;             // passes run on these buffers
+  unsigned long long* shrec = nullptr;  // key-range shards: per reference the pass-3 record; staging words
   unsigned long long* fslot = nullptr;  // per reference: the main-table slot of its -1 (cold) key
 };
 
@@ -79,6 +83,8 @@ struct FaithShard {
   uint64_t n = 0, j_off = 0, n_total = 0;
   unsigned long long pmax_in = 0, max_sink = 0;
 };
+
+struct FaShards;  // a key-range shard's state between the phases of pluss_dev_faithful_shards_* (pluss_faithful.h)
 
 }  // namespace pluss
 
@@ -93,6 +99,7 @@ struct pluss_ctx {
   unsigned int* d_exp_n;
   pluss::FaithfulBufs fb;
   pluss::FaithShard fsh;
+  pluss::FaShards* fsh2;  // created on first use (faith_shards_local), freed by faith_shards_free
   pluss::FaithfulBufs fbr[6];  // per-reference buffers of pluss_dev_faithful_hist_refs
   hipStream_t fst[6];          // ... and its streams (created on first use)
   hipEvent_t fev[7];           // fork / join events
@@ -154,5 +161,12 @@ int faith_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uin
 int faith_shard_starts(pluss_ctx* ctx, uint64_t j_off, uint64_t pmax_in, pluss_faith_shard* out, hipStream_t s);
 int faith_shard_cut(pluss_ctx* ctx, uint64_t s_off, uint64_t n_total, pluss_faith_shard* out, hipStream_t s);
 int faith_shard_hist(pluss_ctx* ctx, uint64_t cut, uint64_t next_first_key, int is_last, hipStream_t s);
+// key-range shards of the single-read pipeline (all six references at once)
+int faith_shards_local(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t seed, const uint64_t* totals,
+                       const uint64_t* first, const uint64_t* n, uint64_t* max_sink, hipStream_t s);
+int faith_shards_carry(pluss_ctx* ctx, const uint64_t* carry_in, uint64_t* starts, hipStream_t s);
+int faith_shards_cut(pluss_ctx* ctx, const uint64_t* starts_before, uint64_t* cut, hipStream_t s);
+int faith_shards_hist(pluss_ctx* ctx, const uint64_t* cut, const int32_t* is_last, hipStream_t s);
+void faith_shards_free(pluss_ctx* ctx);
 
 }  // namespace pluss

@@ -256,14 +256,60 @@ def sharded_faithful_hist(cfg, samples_by_ref, group=None, stream=None):
     return Histogram(h.bins, tsum)
 
 
+def faithful_shards_protocol(shard, d_samples, seed, totals, first, n, rank, allgather, stream=None, err=None):
+    """Faithful mode over key-range shards of the single-read pipeline, all six
+    references at once (pluss_dev_faithful_shards_*): `shard` (a Context, or
+    any object with the same faithful_shards_* methods) holds this rank's
+    slices [first[r], first[r] + n[r]) of the six key-ordered lists of
+    totals[r] samples (d_samples; None: generated), and three exchanges of
+    six-word summaries carry the scan across the ranks:
+      1. (n, largest sink) -> the largest sink of the earlier ranks = the carry;
+      2. the start counts -> the starts before this rank;
+      3. the first Q1 cut candidates -> the global cut (their minimum).
+    Every exchange carries an error word, as in faithful_shard_protocol.
+    Returns the global cuts."""
+    def exchange(vals):
+        nonlocal err
+        g = allgather([1 if err is not None else 0] + [int(v) for v in vals])
+        if err is not None:
+            raise err
+        if any(x[0] for x in g):
+            raise PlussError("another rank's faithful shard pass failed")
+        return [x[1:] for x in g]
+
+    def phase(fn, *args, default):
+        nonlocal err
+        if err is not None:
+            return default
+        try:
+            return fn(*args)
+        except Exception as e:  # noqa: BLE001 -- re-raised at the next exchange, on every rank
+            err = e
+            return default
+    mx = phase(shard.faithful_shards_local, d_samples, seed, totals, first, n, stream, default=[0] * 6)
+    g = exchange(list(n) + list(mx))
+    carry = [max([x[6 + r] for x in g[:rank] if x[r] > 0], default=0) for r in range(6)]
+    last = [not any(x[r] > 0 for x in g[rank + 1:]) for r in range(6)]
+    st = phase(shard.faithful_shards_carry, carry, stream, default=[0] * 6)
+    g = exchange(st)
+    before = [sum(x[r] for x in g[:rank]) for r in range(6)]
+    cand = phase(shard.faithful_shards_cut, before, stream, default=list(totals))
+    g = exchange(cand)
+    cut = [min(x[r] for x in g) for r in range(6)]
+    phase(shard.faithful_shards_hist, cut, last, stream, default=None)
+    exchange([])  # the last phase's error, before the caller's merge collectives
+    return cut
+
+
 def sharded_faithful_gen_hist(cfg, seed, totals, group=None, stream=None):
     """Faithful mode over key-range shards of the key-order lists
-    (pluss_dev_expand_sorted's lists of totals[r] samples): each rank
-    generates only the samples whose keys fall in its range -- an index slice,
-    since the lists are in key order and random access -- so no rank reads or
-    holds the whole list; then the same four-phase protocol as
-    sharded_faithful_hist.  Returns the merged Histogram (identical on every
-    rank)."""
+    (pluss_dev_expand_sorted's lists of totals[r] samples): each rank takes the
+    samples whose keys fall in its range -- an index slice, found by the host
+    search pluss_keyorder_index_range, since the lists are in key order and
+    random access -- and generates them inside its single-read pass; no rank
+    reads or holds a whole list.  Then the three-exchange protocol of
+    faithful_shards_protocol.  Returns the merged Histogram (identical on
+    every rank)."""
     import torch
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
@@ -274,20 +320,18 @@ def sharded_faithful_gen_hist(cfg, seed, totals, group=None, stream=None):
     sp = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
     keys = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
     cnts = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
-    slices = [keyorder_index_range(cfg, seed, r, int(t), lo, hi) if t else (0, 0) for r, t in enumerate(totals)]
-    buf = torch.empty(max([b - a for a, b in slices] + [1]), dtype=torch.int64, device=dev)
+    err = None
+    first, n = [0] * 6, [0] * 6
+    try:
+        for r, t in enumerate(totals):
+            if t:
+                a, b = keyorder_index_range(cfg, seed, r, int(t), lo, hi)
+                first[r], n[r] = a, b - a
+    except Exception as e:  # noqa: BLE001 -- raised on every rank by the protocol's first exchange
+        err = e
     with Context(cfg) as ctx:
         ctx.reset(sp)
-        for ref, (t, (a, b)) in enumerate(zip(totals, slices)):
-            if t == 0:
-                continue
-            err = None
-            try:
-                if b > a:
-                    ctx.expand_sorted(seed, ref, int(t), a, b - a, buf.data_ptr(), sp)
-            except Exception as e:  # noqa: BLE001 -- raised on every rank by the protocol's first exchange
-                err = e
-            faithful_shard_protocol(ctx, ref, buf.data_ptr(), b - a, lo, hi, rank, ag, sp, err=err)
+        faithful_shards_protocol(ctx, None, seed, [int(t) for t in totals], first, n, rank, ag, sp, err=err)
         trav, err = _export_fetch(ctx, keys, cnts, sp, dev)
     raise_together(err, group, dev if nccl else None)
     tsum = [sum(col) % (1 << 64) for col in zip(*ag(trav))]

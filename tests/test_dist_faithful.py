@@ -283,3 +283,144 @@ def test_failing_rank_raises_on_every_rank():
     for r in range(world):
         want = "own" if r == bad else "other"
         assert res[r] == [want, want, "ok"], (r, res[r])
+
+
+class HostShards:
+    """Host emulation of the four pluss_dev_faithful_shards_* phases (all six
+    references at once; the single-read pipeline's key-range shards) on the
+    oracle's keys and sinks of each reference's key-ordered list."""
+
+    def __init__(self, N, T, ks):  # ks[r] = (keys, sinks) of reference r's whole list, key order
+        self.N, self.T, self.ks = N, T, ks
+        self.bins, self.trav = {}, [0] * 6
+
+    def faithful_shards_local(self, d, seed, totals, first, n, stream=None):
+        self.tot, self.first, self.n = list(totals), list(first), list(n)
+        out = []
+        for r in range(6):
+            s = self.ks[r][1][first[r]:first[r] + n[r]]
+            out.append(int(max(int(x) for x in s)) if len(s) else 0)
+        return out
+
+    def _walk(self, r):  # (flag, run before) of each element of the slice
+        k, s = self.ks[r]
+        run, out = self.carry[r], []
+        for i in range(self.first[r], self.first[r] + self.n[r]):
+            f = i == 0 or int(k[i]) > run
+            out.append((f, run))
+            run = max(run, int(s[i]))
+        return out, run
+
+    def faithful_shards_carry(self, carry, stream=None):
+        self.carry = list(carry)
+        return [sum(f for f, _ in self._walk(r)[0]) for r in range(6)]
+
+    def faithful_shards_cut(self, before, stream=None):
+        out = []
+        for r in range(6):
+            c, nb = self.tot[r], before[r]
+            for i, (f, _) in enumerate(self._walk(r)[0]):
+                j = self.first[r] + i
+                if f and j > 0 and j - nb >= self.tot[r] - j:
+                    c = j
+                    break
+                nb += f
+            out.append(c)
+        return out
+
+    def faithful_shards_hist(self, cut, last, stream=None):
+        N, T = self.N, self.T
+        thr = (4 * N + 2) * N
+        endkey = (N // T) * N * (4 * N + 2) * T
+        for r, ref in enumerate(REFS):
+            if self.n[r] == 0 or cut[r] < self.first[r]:
+                continue
+            k, s = self.ks[r]
+            walk, final = self._walk(r)
+            cold, trav = 0, 0
+            for i, (f, run) in enumerate(walk):
+                j = self.first[r] + i
+                if j == cut[r]:
+                    trav += endkey if run == KEY_EMPTY else run  # the replay ends at the cut
+                    break
+                kk, ss = int(k[j]), int(s[j])
+                if ss == KEY_EMPTY:
+                    cold += kk % T == 0
+                else:
+                    ri = (ss - kk) // T
+                    kind = 1 if (ref == "B0" and ri > 0 and 2 * ri > thr) else 0
+                    self.bins[(ref, kind, ri)] = self.bins.get((ref, kind, ri), 0) + 1
+                if f:
+                    trav += run - kk
+            if cut[r] == self.tot[r] and last[r]:
+                if final != KEY_EMPTY and final % T == 0:
+                    cold += 1
+                trav += endkey if final == KEY_EMPTY else final
+            key = (ref, 0, -1)
+            self.bins[key] = self.bins.get(key, 0) + cold
+            self.trav[r] = trav % (1 << 64)
+
+
+REFS = ["C0", "C1", "A0", "B0", "C2", "C3"]
+
+
+def _shards_worker(rank, world, port, N, T, per, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    import oracle as orc
+    from pluss_sampler_optimization_amd import dist as D
+    from test_dist_faithful import HostShards, keys_and_sinks
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = orc.cfg(N, T)
+    ag = D.torch_allgather(None, "cpu")
+    key_space = (N // T) * N * (4 * N + 2) * T
+    lo, hi = D.key_range(key_space, rank, world)
+    ks, totals, first, n = [], [], [], []
+    for r, ref in enumerate(orc.REFS):
+        cnt = min(per, (N - 1) ** (2 if r < 2 else 3))
+        s = orc.expand_sorted(c, 0x5EED0000 + N, r, cnt, 0, cnt)
+        keys, sinks, _ = keys_and_sinks(orc, c, N, T, 4, ref, s)
+        ks.append((keys, sinks))
+        inside = np.nonzero((keys >= np.uint64(lo)) & (keys < np.uint64(hi)))[0]
+        totals.append(cnt)
+        first.append(int(inside[0]) if len(inside) else 0)
+        n.append(len(inside))
+    sh = HostShards(N, T, ks)
+    D.faithful_shards_protocol(sh, None, 0, totals, first, n, rank, ag)
+    q.put((rank, sh.bins, sh.trav))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N,T,per", [(1, 64, 4, 3000), (2, 64, 4, 3000), (3, 128, 8, 4000), (8, 128, 8, 4000)])
+def test_single_read_shards_equal_sequential_sampler(orc, world, N, T, per):
+    """dist.faithful_shards_protocol (the three six-word exchanges of the
+    single-read pipeline's key-range shards) over gloo, with host-emulated
+    shards: merged over ranks == the oracle's sequential r10 sampler of each
+    reference's whole key-order list."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shards_worker, args=(r, world, port, N, T, per, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    c = orc.cfg(N, T)
+    for r, ref in enumerate(orc.REFS):
+        cnt = min(per, (N - 1) ** (2 if r < 2 else 3))
+        s = orc.expand_sorted(c, 0x5EED0000 + N, r, cnt, 0, cnt)
+        want, wtrav = orc.faithful(c, ref, s)
+        got, trav = {}, 0
+        for _, bins, tr in res:
+            for k, v in bins.items():
+                if k[0] == ref:
+                    got[k] = got.get(k, 0) + v
+            trav = (trav + tr[r]) % (1 << 64)
+        assert got == want, (world, ref)
+        assert trav == wtrav, (world, ref)

@@ -851,7 +851,10 @@ def test_cli_trace_and_json(tmp_path, orc, name, d, smp):
     for c, mr in d["printed"]["mrc"]:
         assert c in mrc and abs(mrc[c] - mr) <= 5e-6 * max(abs(mr), 1e-6), (c, mr)
     assert max(j["traversed"]) == d["printed"]["max_traversed"]
-    lines = [l.split() for l in open(tr).read().splitlines()]
+    assert j["sampler"].startswith("faithful")
+    text = open(tr).read().splitlines()
+    assert text[0].startswith("# ref c0 c1 c2 ri sink_key")  # faithful run: the header says what the RIs are
+    lines = [l.split() for l in text if not l.startswith("#")]
     assert [(l[0], int(l[1]), int(l[2]), int(l[3])) for l in lines] == rows
     packed = np.array([P.pack(r, a, b, c) for r, a, b, c in rows], dtype=np.uint64)
     want = orc.clean_ri(orc.cfg(d["N"], d["T"]), packed)

@@ -71,6 +71,9 @@ def oracle_parity(orc, c, N, T, host, n_sub, budget_steps):
     for r, k, x in zip(refs.tolist(), kind.tolist(), want.tolist()):
         exp[(P.REFS[r], k, x)] = exp.get((P.REFS[r], k, x), 0) + 1
     assert h.bins == exp
+    # the bench's kernel itself (the dense pass, k_count's dense tail) on the oracle's sub-sample
+    t = torch.from_numpy(np.ascontiguousarray(sub).view(np.int64)).cuda()
+    assert dense_pass(c, t, len(sub)).bins == exp
     return sub, want
 
 

@@ -119,3 +119,67 @@ def test_words64_over_1024_tiles(orc, kind):
         assert 0.3 * n < rec < 0.7 * n  # the Q1 cut lies inside the list
     else:
         assert rec >= n - 8  # sparse: at most Q1's exit at the very end drops a sample
+
+
+def shards_by_hand(c, splits, totals, lists=None, seed=None):
+    """The four phases of pluss_dev_faithful_shards_* on one GPU, one handle
+    per shard, the summaries exchanged here: splits[r] = the index boundaries
+    of reference r's list over the shards (uneven, empty shards allowed).
+    lists: key-ordered sample lists (each shard gets its slices); None: the
+    generated key-order lists of `seed`.  Returns the merged Histogram."""
+    S = len(splits[0]) - 1
+    first = [[splits[r][k] for r in range(6)] for k in range(S)]
+    n = [[splits[r][k + 1] - splits[r][k] for r in range(6)] for k in range(S)]
+    ctxs = [P.Context(c) for _ in range(S)]
+    bufs = []
+    for k, ctx in enumerate(ctxs):
+        ctx.reset(stream())
+        if lists is not None:
+            sl = np.concatenate([lists[r][first[k][r]:first[k][r] + n[k][r]] for r in range(6)]).astype(np.uint64)
+            bufs.append(torch.from_numpy(sl.view(np.int64)).cuda() if len(sl) else None)
+        else:
+            bufs.append(None)
+    ptr = [b.data_ptr() if b is not None else None for b in bufs]
+    mx = [ctx.faithful_shards_local(ptr[k], seed or 0, totals, first[k], n[k], stream()) for k, ctx in enumerate(ctxs)]
+    carry = [[max([mx[j][r] for j in range(k) if n[j][r] > 0], default=0) for r in range(6)] for k in range(S)]
+    st = [ctx.faithful_shards_carry(carry[k], stream()) for k, ctx in enumerate(ctxs)]
+    before = [[sum(st[j][r] for j in range(k)) for r in range(6)] for k in range(S)]
+    cand = [ctx.faithful_shards_cut(before[k], stream()) for k, ctx in enumerate(ctxs)]
+    cut = [min(cand[k][r] for k in range(S)) for r in range(6)]
+    bins, trav = {}, [0] * 6
+    for k, ctx in enumerate(ctxs):
+        last = [not any(n[j][r] > 0 for j in range(k + 1, S)) for r in range(6)]
+        ctx.faithful_shards_hist(cut, last, stream())
+        h = ctx.fetch()
+        for key, v in h.bins.items():
+            bins[key] = bins.get(key, 0) + v
+        trav = [(a + b) % (1 << 64) for a, b in zip(trav, h.traversed)]
+        ctx.close()
+    return P.Histogram(bins, trav)
+
+
+@pytest.mark.parametrize("kind", ["generated", "windows"])
+def test_key_range_shards_equal_one_gpu(orc, kind):
+    """The key-range-sharded single-read pipeline (multi-GPU faithful mode) run
+    by hand as 5 uneven shards (one empty) at N=4096: equal to one GPU.
+    `windows`: dense first/last-row lists whose replays chain across the shard
+    boundaries and whose Q1 cuts fall inside a middle shard; also equal to the
+    stepping oracle."""
+    N, T = 4096, 8
+    c = P.SamplerConfig(n=N, threads=T, mode="faithful")
+    if kind == "generated":
+        totals = P.default_counts(N, 1 << 22)
+        lists = None
+        with P.Context(c) as ctx:
+            ctx.gen_faithful_refs(SEED, totals, stream())
+            want = ctx.fetch()
+    else:
+        lists = [window_list(N, T, 4, ref, 10000, [0, N // T - 1], 16, 7 + r) for r, ref in enumerate(P.REFS)]
+        totals = [len(x) for x in lists]
+        want = three_sources(c, lists)["sorted"]
+    fr = [0.0, 0.13, 0.13, 0.5, 0.61, 1.0]  # shard 1 is empty
+    splits = [[int(round(f * t)) for f in fr] for t in totals]
+    got = shards_by_hand(c, splits, totals, lists=lists, seed=SEED if lists is None else None)
+    assert got.bins == want.bins and list(got.traversed) == list(want.traversed)
+    if kind == "windows":
+        check_vs_oracle(orc, c, {"shards": got}, lists, [r for r in P.REFS if r != "B0"])

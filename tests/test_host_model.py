@@ -295,6 +295,8 @@ def test_keyorder_index_range_selects_a_key_range(orc, N, T, CS):
         for lo, hi in ((0, hi_key), (hi_key // 3, 2 * hi_key // 3), (int(key[7]), int(key[7]) + 1),
                        (int(key[7]) + 1, int(key[8])), (hi_key, 2 * hi_key)):
             a, b = P.keyorder_index_range(pc, 0, ref, tot, lo, hi, sample_at=at)
+            # the library's host-only search (pluss_keyorder_index_range: no device) over its own generator
+            assert P.keyorder_index_range(pc, 0x5EED0003, ref, tot, lo, hi) == (a, b)
             inside = np.nonzero((key >= lo) & (key < hi))[0]
             if len(inside):
                 assert (a, b) == (inside[0], inside[-1] + 1)
