@@ -827,7 +827,9 @@ __device__ __forceinline__ void fa_local_fast(const Model& m, const FaOne& o, Fa
 #pragma unroll
   for (int k = 0; k < TI; ++k) {
     const bool v = FULLT || (uint32_t)k < nv;
-    const FaDec d = el(k, odd);
+    uint32_t oddk = 0;  // a partial tile's LDS slots past its end hold stale words: not checked
+    const FaDec d = el(k, oddk);
+    odd |= v ? oddk : 0u;
     if (CHECK && v) {
       if (k == 0) ofirst = d.ord;
       else unordered |= !(d.ord > oprev);
