@@ -2,8 +2,8 @@
  * pluss_diag.h — diagnostics of libpluss_gpu.so.  NOT part of the drop-in
  * boundary (include/pluss_gpu.h): nothing in the product path calls these,
  * and no environment variable changes what a pluss_* entry point computes.
- * Used by tools/ablate.py (where the hot kernel's time goes) and
- * tools/grid_sweep.py (workgroup count vs list size).
+ * Used by tools/ablate.py (where the hot kernel's time goes),
+ * tools/grid_sweep.py (workgroup count vs list size) and the sort tests.
  */
 #ifndef PLUSS_DIAG_H
 #define PLUSS_DIAG_H
@@ -28,6 +28,13 @@ enum {
    of 1..16384 workgroups).  Returns PLUSS_OK or PLUSS_ERR_*. */
 int pluss_diag_dense(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t n, uint64_t *d_counts, int32_t variant,
                      int32_t max_grid, void *stream);
+
+/* The faithful radix source's sort alone (pluss_sort.h): the n samples of
+   reference `ref` (any order) -> their packed sort words (rank << 2 | case) in
+   ascending order, copied to d_words.  *word_bytes is set to 4 (N <= 1024) or
+   8.  Needs N % (cls/ds) == 0.  Tests compare it with a host sort. */
+int pluss_diag_sort_words(pluss_ctx *ctx, int32_t ref, const uint64_t *d_samples, uint64_t n, void *d_words,
+                          int32_t *word_bytes, void *stream);
 
 #ifdef __cplusplus
 }

@@ -32,7 +32,7 @@ EXPORTS = [
     "pluss_dev_faithful_shards_hist",
 ]
 # include/pluss_diag.h (diagnostics, not the drop-in boundary)
-DIAG_EXPORTS = ["pluss_diag_dense"]
+DIAG_EXPORTS = ["pluss_diag_dense", "pluss_diag_sort_words"]
 
 
 class PlussCfg(ctypes.Structure):
@@ -124,6 +124,7 @@ def lib():
         "pluss_dev_sampled_hist_dense": (ctypes.c_int, [vp, vp, u64, vp, vp]),
         "pluss_dev_gen_count_dense": (ctypes.c_int, [vp, u64, P(u64), P(u64), P(u64), vp, vp]),
         "pluss_diag_dense": (ctypes.c_int, [vp, vp, u64, vp, i32, i32, vp]),
+        "pluss_diag_sort_words": (ctypes.c_int, [vp, i32, vp, u64, vp, ctypes.POINTER(i32), vp]),
         "pluss_dev_faithful_shards_local": (ctypes.c_int, [vp, vp, u64, P(u64), P(u64), P(u64), P(u64), vp]),
         "pluss_dev_faithful_shards_carry": (ctypes.c_int, [vp, P(u64), P(u64), vp]),
         "pluss_dev_faithful_shards_cut": (ctypes.c_int, [vp, P(u64), P(u64), vp]),

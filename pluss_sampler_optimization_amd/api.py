@@ -354,6 +354,16 @@ class Context:
         (0 product, 1 loads only, 2 no tail) and/or a workgroup cap."""
         check(lib().pluss_diag_dense(self._h, d_samples, n, d_counts, variant, max_grid, stream), "pluss_diag_dense")
 
+    def diag_sort_words(self, ref, d_samples, n, d_words, stream=None):
+        """Diagnostics (include/pluss_diag.h): the faithful radix source's bucket
+        sort alone -- reference `ref`'s n samples (any order) -> its packed sort
+        words, ascending, into d_words.  Returns the word size in bytes (4 or 8)."""
+        rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
+        wb = ctypes.c_int32(0)
+        check(lib().pluss_diag_sort_words(self._h, rid, d_samples, n, d_words, ctypes.byref(wb), stream),
+              "pluss_diag_sort_words")
+        return int(wb.value)
+
     # faithful mode over key-range shards: the four phases of
     # pluss_dev_faithful_shard_* (the caller exchanges the summaries; see dist.py)
     def faithful_shard_keys(self, ref, d_samples, n, key_lo, key_hi, stream=None):

@@ -174,11 +174,14 @@ int pluss_ctx_destroy(pluss_ctx* c) {
   void* bufs[] = {c->d_table,  c->d_exp_keys, c->d_exp_counts, c->d_exp_n, c->fb.keys,  c->fb.sinks,
                   c->fb.keys_s, c->fb.sinks_s, c->fb.pmax,      c->fb.nstart, c->fb.tmp,
                   c->fb.scal, c->fb.st, c->fb.dpart, c->fb.tmax, c->fb.pmin, c->fb.fslot,
-                  c->fb.klist, c->fb.slowq, c->fb.cval, c->fb.crec, c->fb.cflag, c->fb.shrec};
+                  c->fb.klist, c->fb.slowq, c->fb.cval, c->fb.crec, c->fb.cflag, c->fb.shrec,
+                  c->fb.sbuf};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (const auto& f : c->fbr) {
-    void* fr[] = {f.keys, f.sinks, f.keys_s, f.sinks_s, f.pmax, f.nstart, f.tmp, f.scal, f.st, f.dpart, f.tmax, f.pmin, f.fslot, f.klist, f.slowq, f.cval, f.crec, f.cflag};
+    void* fr[] = {f.keys,  f.sinks, f.keys_s, f.sinks_s, f.pmax,  f.nstart, f.tmp,   f.scal,  f.st,
+                  f.dpart, f.tmax,  f.pmin,   f.fslot,   f.klist, f.slowq,  f.cval,  f.crec,  f.cflag,
+                  f.shrec, f.sbuf};
     for (void* p : fr)
       if (p) (void)hipFree(p);
   }
@@ -298,6 +301,12 @@ int pluss_diag_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, uint
                      int32_t max_grid, void* stream) {
   if (!ctx || (!d_samples && n) || !d_counts) return PLUSS_ERR_CONFIG;
   return launch_diag_dense(ctx, d_samples, n, (unsigned long long*)d_counts, variant, max_grid, pick(ctx, stream));
+}
+
+int pluss_diag_sort_words(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, void* d_words,
+                          int32_t* word_bytes, void* stream) {
+  if (!ctx || (!d_samples && n) || (!d_words && n) || !word_bytes || ref < 0 || ref > 5) return PLUSS_ERR_CONFIG;
+  return diag_sort_words(ctx, ref, d_samples, n, d_words, word_bytes, pick(ctx, stream));
 }
 
 int pluss_faithful_key_space(const pluss_cfg* cfg, uint64_t* key_end) {

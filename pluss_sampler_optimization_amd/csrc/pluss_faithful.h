@@ -326,11 +326,15 @@ __device__ __forceinline__ void fa_load_run(const Model& m, const FaOne& o, cons
   t0s = 0;
   if constexpr (SRC != SRC_GEN) {
     const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(o.src) + T.base;
+    fa_raw_t<SRC> v[EPT];  // every load issued before the first wait (partial tiles: clamped, no branch)
+    const uint32_t last = T.mt - 1;
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
       const uint32_t e = (uint32_t)k * NT + threadIdx.x;
-      if (FULLT || e < T.mt) sh.raw[fa_slot_n<EPT>(e)] = src[e];
+      v[k] = src[FULLT ? e : (e < last ? e : last)];
     }
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) sh.raw[fa_slot_n<EPT>((uint32_t)k * NT + threadIdx.x)] = v[k];
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
@@ -807,18 +811,23 @@ __device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(v), 63);
 }
 
+// ri*T per case in 32 bits (0xFFFFFFFF: cold), as three fields: never an
+// indexed array, which the compiler may place in scratch
+struct FaRi {
+  uint32_t r0, r1, r2;
+};
+
 // The scan of one tile by the fast path (mt elements: FULLT, or a partial
 // tile's elements at e < mt).  `el(k)` decodes this thread's element k.
 template <int SRC, bool CHECK, uint32_t REF, bool FULLT, class EL>
 __device__ __forceinline__ void fa_local_fast(const Model& m, const FaOne& o, FaLds<SRC, TB, TI>& sh,
-                                              unsigned long long base, const uint32_t (&r)[3], EL&& el,
+                                              unsigned long long base, const FaRi r, EL&& el,
                                               unsigned long long* __restrict__ klist, GTable g) {
   constexpr int NW = TB / 64;
   const FaTile& T = o.T;
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
   const uint32_t e0 = threadIdx.x * TI;
   const uint32_t nv = FULLT ? TI : (e0 < T.mt ? (T.mt - e0 < TI ? T.mt - e0 : TI) : 0u);
-  const uint64_t i0 = T.gbase + e0;
   const uint32_t b32 = (uint32_t)base;
   uint32_t rk[TI], sk[TI], lmax = 0, odd = 0;
   uint32_t w0 = 0, w1 = 0, wc = 0;  // wave counts (ballots): case 0, case 1, case 2 of tid 0
@@ -836,7 +845,7 @@ __device__ __forceinline__ void fa_local_fast(const Model& m, const FaOne& o, Fa
       oprev = d.ord;
     }
     rk[k] = v ? d.lk - b32 : 0u;
-    const uint32_t dd = d.a ? r[0] : (d.b ? r[1] : r[2]);
+    const uint32_t dd = d.a ? r.r0 : (d.b ? r.r1 : r.r2);  // selects (an array here went to scratch)
     const uint32_t x = rk[k] + dd;  // dd = 0xFFFFFFFF (cold) wraps below dd: the max keeps it
     sk[k] = v ? (x > dd ? x : dd) : 0u;
     lmax = sk[k] > lmax ? sk[k] : lmax;
@@ -944,7 +953,7 @@ __device__ __forceinline__ void fa_local_fast(const Model& m, const FaOne& o, Fa
         a1 += sh.red[w][1];
         ac += sh.red[w][2];
       }
-      const bool cold2 = r[2] == 0xFFFFFFFFu;
+      const bool cold2 = r.r2 == 0xFFFFFFFFu;
       x = f == 0 ? (cold2 ? ac : 0ull) : f == 2 ? a0 : f == 3 ? a1 : (cold2 ? 0ull : T.mt - a0 - a1);
     }
     sh.out[f] = x;
@@ -964,6 +973,9 @@ __device__ __forceinline__ const void* fa_src_of(const FaRefs& a, uint32_t r) {
   }
 }
 
+template <int SRC, uint32_t R>
+__device__ __forceinline__ FaOne fa_one_ref(const FaRefs& a, const FaTile& T);
+
 // One tile by the fast path: its elements staged to LDS (memory sources),
 // the first and last keys in 64 bits, then the scan if the tile qualifies.
 // Returns whether the fast path took the tile (tile-uniform).
@@ -977,12 +989,18 @@ __device__ __forceinline__ bool fa_fast_tile(const Model& m, const FaRefs& a, co
   fa_rt(m, o.pv, sh);
   const bool full = T.mt == TILE;
   if constexpr (SRC != SRC_GEN) {
+    // all TI loads issued before the first is waited for: no branch around
+    // them (a partial tile's lanes past its end re-read its last element)
     const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(o.src) + T.base;
+    fa_raw_t<SRC> v[TI];
+    const uint32_t last = T.mt - 1;
 #pragma unroll
     for (int k = 0; k < TI; ++k) {
       const uint32_t e = (uint32_t)k * TB + threadIdx.x;
-      if (full || e < T.mt) sh.raw[fa_slot_n<TI>(e)] = src[e];
+      v[k] = __builtin_nontemporal_load(src + (e < last ? e : last));
     }
+#pragma unroll
+    for (int k = 0; k < TI; ++k) sh.raw[fa_slot_n<TI>((uint32_t)k * TB + threadIdx.x)] = v[k];
   }
   if (threadIdx.x < 2) {  // the first and the last key, in 64 bits
     const uint32_t e = threadIdx.x ? T.mt - 1 : 0;
@@ -994,15 +1012,15 @@ __device__ __forceinline__ bool fa_fast_tile(const Model& m, const FaRefs& a, co
   }
   __syncthreads();
   const unsigned long long base = sh.kb[0], kl = sh.kb[1];
-  uint32_t r[3];
   unsigned long long rmax = 0;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const unsigned long long x = sh.rt[c];
-    r[c] = x == KEY_EMPTY ? 0xFFFFFFFFu : (uint32_t)x;
     rmax = x != KEY_EMPTY && x > rmax ? x : rmax;
   }
-  if (!(kl >= base && kl - base < 0xFFFFFFFFull - rmax && r[0] != 0xFFFFFFFFu && r[1] != 0xFFFFFFFFu &&
+  auto r32 = [](unsigned long long x) { return x == KEY_EMPTY ? 0xFFFFFFFFu : (uint32_t)x; };
+  const FaRi r{r32(sh.rt[0]), r32(sh.rt[1]), r32(sh.rt[2])};
+  if (!(kl >= base && kl - base < 0xFFFFFFFFull - rmax && r.r0 != 0xFFFFFFFFu && r.r1 != 0xFFFFFFFFu &&
         (SRC != SRC_GEN || keyrun_fast_ok(kg, T.gbase, T.mt))))
     return false;
   unsigned long long* kl_out = klist + T.gt * (uint64_t)(2 * KL);

@@ -41,6 +41,7 @@
 #include <rocprim/iterator/transform_iterator.hpp>
 
 #include "pluss_faithful.h"
+#include "pluss_sort.h"
 
 namespace pluss {
 // Packed word (rank << 2 | case) of sample x of reference `ref`; ~0 (and the
@@ -542,15 +543,15 @@ static int faith_reserve(pluss_ctx* ctx, FaithfulBufs& b, uint64_t n, hipStream_
 }
 
 static int faith_tmp(pluss_ctx* ctx, FaithfulBufs& b, uint64_t n, hipStream_t s) {
+  // rocPRIM temporary storage: the pair sort and scans of the (key, sink) path
+  // (shapes with N % (cls/ds) != 0) and the prefix scans of the key-range shard
+  // protocol; packed words are sorted by pluss_sort.h (no temporary storage)
   size_t t1 = 0, t2 = 0, t3 = 0;
   const int fm = faith_fm(ctx->m);
-  if (fm == FM_PK32) {  // packed words: keys-only sort, pmax over the recomputed sinks
-    uint32_t *k = (uint32_t*)b.keys, *ks = (uint32_t*)b.keys_s;
-    PLUSS_HIP_CHECK(rocprim::radix_sort_keys(nullptr, t1, k, ks, n, 0, pk_bits(ctx->m), s));
-    auto it = rocprim::make_transform_iterator(ks, PkSinkOp<uint32_t>{make_pkview(ctx->m, 0)});
+  if (fm == FM_PK32) {
+    auto it = rocprim::make_transform_iterator((const uint32_t*)b.keys_s, PkSinkOp<uint32_t>{make_pkview(ctx->m, 0)});
     PLUSS_HIP_CHECK(rocprim::inclusive_scan(nullptr, t2, it, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
   } else if (fm == FM_PK64) {
-    PLUSS_HIP_CHECK(rocprim::radix_sort_keys(nullptr, t1, b.keys, b.keys_s, n, 0, pk_bits(ctx->m), s));
     auto it = rocprim::make_transform_iterator(b.keys_s, PkSinkOp<unsigned long long>{make_pkview(ctx->m, 0)});
     PLUSS_HIP_CHECK(rocprim::inclusive_scan(nullptr, t2, it, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
   } else {
@@ -579,6 +580,146 @@ static int faith_tmp(pluss_ctx* ctx, FaithfulBufs& b, uint64_t n, hipStream_t s)
   return PLUSS_OK;
 }
 
+// ---- the bucket sort of packed words (pluss_sort.h): the references' words,
+// made from their samples (SMP: in[r] = the samples) or already made (in[r] =
+// words), sorted into out (the references concatenated in order).  x1: 8 B x
+// total scratch words; y: another 8 B x total when payloads are 8 bytes.
+static int srt_reserve(FaithfulBufs& b, uint64_t bytes, hipStream_t s) {
+  if (bytes > b.sbcap) {
+    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+    if (int rc = grow(&b.sbuf, bytes)) return rc;
+    b.sbcap = bytes;
+  }
+  return PLUSS_OK;
+}
+
+struct SrtPlan {
+  SrtRefs a;
+  uint64_t ntot, h1, g2max, h2max, nbs;
+  bool p32;  // 4-byte payloads
+  size_t o_h1, o_h2, o_bs, o_par, o_cmap, o_tot, o_deep, bytes;
+};
+
+static SrtPlan srt_plan(const Model& m, const void* const in[6], const uint64_t cnt[6]) {
+  SrtPlan P;
+  std::memset((void*)&P, 0, sizeof P);
+  const uint32_t wb = pk_bits(m);
+  P.p32 = wb <= 32 + (uint32_t)SDIG;
+  uint64_t e = 0, c = 0, h = 0, np = 0;
+  for (int r = 0; r < 6; ++r) {
+    uint32_t d1 = srt_d1(cnt[r], wb);
+    if (cnt[r] && P.p32 && wb > 32 && d1 < wb - 32) d1 = wb - 32;  // every payload below 2^32
+    const uint64_t nch = (cnt[r] + SC - 1) / SC;
+    P.a.n[r] = cnt[r];
+    P.a.eoff[r] = e;
+    P.a.coff[r] = c;
+    P.a.hoff[r] = h;
+    P.a.d1[r] = d1;
+    P.a.in[r] = in[r];
+    e += cnt[r];
+    c += nch;
+    h += ((uint64_t)1 << d1) * nch;
+    np += (uint64_t)1 << d1;
+  }
+  P.a.eoff[6] = e;
+  P.a.coff[6] = c;
+  P.a.hoff[6] = h;
+  P.a.wb = wb;
+  P.a.np = (uint32_t)np;
+  P.ntot = e;
+  P.h1 = h;
+  P.g2max = e / SC + np + 1;
+  P.h2max = P.g2max * SB;
+  P.nbs = ((h > P.h2max ? h : P.h2max) + SBATCH - 1) / SBATCH;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t o = 0;
+  P.o_h1 = o;
+  o = al(o + 4 * P.h1);
+  P.o_h2 = o;
+  o = al(o + 4 * P.h2max);
+  P.o_bs = o;
+  o = al(o + 4 * P.nbs);
+  P.o_par = o;
+  o = al(o + sizeof(SrtParent) * np);
+  P.o_cmap = o;
+  o = al(o + 4 * P.g2max);
+  P.o_tot = o;  // [0] level-2 chunks, [1] hist2 entries, [2] deep items
+  o = al(o + 16);
+  P.o_deep = o;
+  o = al(o + sizeof(SrtItem) * np * SB);
+  P.bytes = o;
+  return P;
+}
+
+// exclusive scan of v[0, len) in place (dlen: the entries in use, on the device)
+static void srt_scan(uint32_t* v, uint64_t len, const uint32_t* dlen, uint32_t* bsum, hipStream_t s) {
+  const uint32_t nb = (uint32_t)((len + SBATCH - 1) / SBATCH);
+  if (!nb) return;
+  hipLaunchKernelGGL(k_scan_sums, dim3(nb), dim3(SB), 0, s, (const uint32_t*)v, len, dlen, bsum);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SB), 0, s, bsum, nb);
+  hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(SB), 0, s, v, len, dlen, (const uint32_t*)bsum);
+}
+
+template <typename KT, typename PT, bool SMP>
+static int srt_launch(pluss_ctx* ctx, FaithfulBufs& b, const SrtPlan& P, PT* X1, PT* Y, KT* out, hipStream_t s) {
+  const Model& m = ctx->m;
+  unsigned char* B = b.sbuf;
+  uint32_t* h1 = (uint32_t*)(B + P.o_h1);
+  uint32_t* h2 = (uint32_t*)(B + P.o_h2);
+  uint32_t* bs = (uint32_t*)(B + P.o_bs);
+  SrtParent* par = (SrtParent*)(B + P.o_par);
+  uint32_t* cmap = (uint32_t*)(B + P.o_cmap);
+  uint32_t* tot = (uint32_t*)(B + P.o_tot);
+  const SrtDeep dp{(SrtItem*)(B + P.o_deep), tot + 2, P.a.np * (uint32_t)SB};
+  PLUSS_HIP_CHECK(hipMemsetAsync(tot, 0, 16, s));
+  const unsigned g1 = (unsigned)P.a.coff[6];
+  hipLaunchKernelGGL((k_srt_count1<KT, SMP>), dim3(g1), dim3(SB), 0, s, m, P.a, h1, ctx->g);
+  srt_scan(h1, P.h1, nullptr, bs, s);
+  hipLaunchKernelGGL((k_srt_scatter1<KT, PT, SMP>), dim3(g1), dim3(SB), 0, s, m, P.a, (const uint32_t*)h1, X1, ctx->g);
+  hipLaunchKernelGGL(k_srt_plan, dim3(1), dim3(SB), 0, s, P.a, (const uint32_t*)h1, par, cmap, tot);
+  hipLaunchKernelGGL(k_srt_count2<PT>, dim3((unsigned)P.g2max), dim3(SB), 0, s, P.a, (const SrtParent*)par,
+                     (const uint32_t*)cmap, (const uint32_t*)tot, (const PT*)X1, h2);
+  srt_scan(h2, P.h2max, tot + 1, bs, s);
+  hipLaunchKernelGGL(k_srt_scatter2<PT>, dim3((unsigned)P.g2max), dim3(SB), 0, s, P.a, (const SrtParent*)par,
+                     (const uint32_t*)cmap, (const uint32_t*)tot, (const uint32_t*)h2, (const PT*)X1, Y);
+  hipLaunchKernelGGL((k_srt_final<PT, KT>), dim3(FG, P.a.np), dim3(SB), 0, s, P.a, (const SrtParent*)par,
+                     (const uint32_t*)h2, (const PT*)X1, (const PT*)Y, out, dp);
+  hipLaunchKernelGGL((k_srt_deep<PT, KT>), dim3(64), dim3(SB), 0, s, P.a, (const SrtParent*)par, X1, Y, out, dp);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  return PLUSS_OK;
+}
+
+// The sort of one or more references (cnt[r] = 0: none).  x1 (and y, for
+// 8-byte payloads) hold 8 B x total each; neither may alias in[] or out.
+template <typename KT, bool SMP>
+static int srt_sort(pluss_ctx* ctx, FaithfulBufs& b, const void* const in[6], const uint64_t cnt[6],
+                    unsigned long long* x1, unsigned long long* y, KT* out, hipStream_t s) {
+  const SrtPlan P = srt_plan(ctx->m, in, cnt);
+  if (P.ntot == 0) return PLUSS_OK;
+  if (P.ntot > 0xFFFFFFFFull) {
+    set_error("faithful mode: the radix source sorts at most 2^32-1 samples per call");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (int rc = srt_reserve(b, P.bytes, s)) return rc;
+  if (P.p32) {
+    uint32_t* X1 = reinterpret_cast<uint32_t*>(x1);
+    return srt_launch<KT, uint32_t, SMP>(ctx, b, P, X1, X1 + P.ntot, out, s);
+  }
+  return srt_launch<KT, unsigned long long, SMP>(ctx, b, P, x1, y, out, s);
+}
+
+// one reference's words, from its samples (SMP: d_in) or from the words in b.keys
+template <typename KT, bool SMP>
+static int srt_run(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, const void* d_in, uint64_t n, hipStream_t s) {
+  const void* in[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  uint64_t cnt[6] = {0, 0, 0, 0, 0, 0};
+  in[ref] = d_in;
+  cnt[ref] = n;
+  // scratch: the sample path writes b.keys / b.sinks; the word path reads b.keys, so its scratch is b.sinks_s / b.pmax
+  return srt_sort<KT, SMP>(ctx, b, in, cnt, SMP ? b.keys : b.sinks_s, SMP ? b.sinks : b.pmax,
+                           reinterpret_cast<KT*>(b.keys_s), s);
+}
+
 static int faith_keys(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, const uint64_t* d_samples, uint64_t n, uint64_t lo, uint64_t hi,
                       unsigned long long* cnt, hipStream_t s) {
   const Model& m = ctx->m;
@@ -602,18 +743,16 @@ static int faith_sort(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, uint64_t n, 
   size_t sz = b.tmp_bytes;
   const int fm = faith_fm(ctx->m);
   if (fm == FM_PK32) {
-    uint32_t *k = (uint32_t*)b.keys, *ks = (uint32_t*)b.keys_s;
-    PLUSS_HIP_CHECK(rocprim::radix_sort_keys(b.tmp, sz, k, ks, n, 0, pk_bits(ctx->m), s));
+    if (int rc = srt_run<uint32_t, false>(ctx, b, ref, b.keys, n, s)) return rc;
     if (!with_pmax) return PLUSS_OK;
-    sz = b.tmp_bytes;
-    auto it = rocprim::make_transform_iterator(ks, PkSinkOp<uint32_t>{make_pkview(ctx->m, (uint32_t)ref)});
+    auto it = rocprim::make_transform_iterator((const uint32_t*)b.keys_s,
+                                               PkSinkOp<uint32_t>{make_pkview(ctx->m, (uint32_t)ref)});
     PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, it, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
     return PLUSS_OK;
   }
   if (fm == FM_PK64) {
-    PLUSS_HIP_CHECK(rocprim::radix_sort_keys(b.tmp, sz, b.keys, b.keys_s, n, 0, pk_bits(ctx->m), s));
+    if (int rc = srt_run<unsigned long long, false>(ctx, b, ref, b.keys, n, s)) return rc;
     if (!with_pmax) return PLUSS_OK;
-    sz = b.tmp_bytes;
     auto it = rocprim::make_transform_iterator(b.keys_s,
                                                PkSinkOp<unsigned long long>{make_pkview(ctx->m, (uint32_t)ref)});
     PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, it, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
@@ -815,8 +954,11 @@ static FaRefs fa_none() {
 // (or (key, sink) pairs) of its list, sorted into b.keys_s, on stream s
 static int faith_keys_sorted(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, const uint64_t* d_samples, uint64_t n,
                              hipStream_t s) {
+  const int fm = faith_fm(ctx->m);
+  if (fm == FM_PK32) return srt_run<uint32_t, true>(ctx, b, ref, d_samples, n, s);
+  if (fm == FM_PK64) return srt_run<unsigned long long, true>(ctx, b, ref, d_samples, n, s);
   if (int rc = faith_keys(ctx, b, ref, d_samples, n, 0, 0, nullptr, s)) return rc;
-  return faith_sort(ctx, b, ref, n, s, faith_fm(ctx->m) == FM_PAIRS);
+  return faith_sort(ctx, b, ref, n, s, true);
 }
 
 // (key, sink) pairs (shapes with N % W != 0): the rocPRIM scans and the record pass
@@ -878,34 +1020,52 @@ int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64
     set_error("pluss_dev_faithful_hist_refs: null sample list");
     return PLUSS_ERR_CONFIG;
   }
-  for (int r = 0; r < 6; ++r) {  // every allocation before the fork
-    if (!counts[r]) continue;
-    if (int rc = faith_reserve(ctx, ctx->fbr[r], counts[r], s)) return rc;
-    if (int rc = faith_tmp(ctx, ctx->fbr[r], counts[r], s)) return rc;
-  }
   const int fm = faith_fm(ctx->m);
-  if (fm == FM_PAIRS) {  // the pair path scans per reference on its stream
+  if (fm == FM_PAIRS) {  // (key, sink) pairs: per reference on a stream of its own
+    for (int r = 0; r < 6; ++r) {  // every allocation before the fork
+      if (!counts[r]) continue;
+      if (int rc = faith_reserve(ctx, ctx->fbr[r], counts[r], s)) return rc;
+      if (int rc = faith_tmp(ctx, ctx->fbr[r], counts[r], s)) return rc;
+    }
     return fork_refs(ctx, counts, s, [&](int r, FaithfulBufs& b, hipStream_t rs) {
       if (int rc = faith_keys_sorted(ctx, b, r, d_samples + off[r], counts[r], rs)) return rc;
       return faith_pairs_scan(ctx, b, r, counts[r], rs);
     });
   }
-  uint64_t tiles = 0, chunks = 0;
-  for (int r = 0; r < 6; ++r) {
-    tiles += fa_tiles(counts[r]);
-    chunks += fa_chunks(fa_tiles(counts[r]));
-  }
-  if (int rc = fa_reserve(ctx->fb, tiles, chunks, s)) return rc;
-  if (int rc = fork_refs(ctx, counts, s, [&](int r, FaithfulBufs& b, hipStream_t rs) {
-        return faith_keys_sorted(ctx, b, r, d_samples + off[r], counts[r], rs);
-      }))
-    return rc;
+  // packed words: one bucket sort of the six references (full-chip grids),
+  // then one scan pipeline over the six sorted arrays
+  FaithfulBufs& b = ctx->fb;
+  if (int rc = faith_reserve(ctx, b, total, s)) return rc;
+  const void* in[6];
+  for (int r = 0; r < 6; ++r) in[r] = d_samples + off[r];
   FaRefs a = fa_none();
-  for (int r = 0; r < 6; ++r) {
-    a.n[r] = counts[r];
-    a.src[r] = ctx->fbr[r].keys_s;
+  if (fm == FM_PK32) {
+    if (int rc = srt_sort<uint32_t, true>(ctx, b, in, counts, b.keys, b.sinks, (uint32_t*)b.keys_s, s)) return rc;
+    for (int r = 0; r < 6; ++r) a.src[r] = (const uint32_t*)b.keys_s + off[r];
+  } else {
+    if (int rc = srt_sort<unsigned long long, true>(ctx, b, in, counts, b.keys, b.sinks, b.keys_s, s)) return rc;
+    for (int r = 0; r < 6; ++r) a.src[r] = b.keys_s + off[r];
   }
+  for (int r = 0; r < 6; ++r) a.n[r] = counts[r];
   return fa_run(ctx, a, fm == FM_PK32 ? SRC_W32 : SRC_W64, false, s);
+}
+
+// diagnostics: the bucket sort alone (include/pluss_diag.h)
+int diag_sort_words(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, void* d_words,
+                    int32_t* word_bytes, hipStream_t s) {
+  if (int rc = faith_direct_shape(ctx, "pluss_diag_sort_words")) return rc;
+  FaithfulBufs& b = ctx->fb;
+  if (int rc = faith_reserve(ctx, b, n, s)) return rc;
+  const int fm = faith_fm(ctx->m);
+  *word_bytes = fm == FM_PK32 ? 4 : 8;
+  if (n == 0) return PLUSS_OK;
+  if (fm == FM_PK32) {
+    if (int rc = srt_run<uint32_t, true>(ctx, b, ref, d_samples, n, s)) return rc;
+  } else if (int rc = srt_run<unsigned long long, true>(ctx, b, ref, d_samples, n, s)) {
+    return rc;
+  }
+  PLUSS_HIP_CHECK(hipMemcpyAsync(d_words, b.keys_s, n * (size_t)*word_bytes, hipMemcpyDeviceToDevice, s));
+  return PLUSS_OK;
 }
 
 // All six over a key-ordered list (each reference's block in key order).

@@ -74,6 +74,9 @@ struct FaithfulBufs {
   uint32_t epoch = 0;             // passes run on these buffers
   unsigned long long* shrec = nullptr;  // key-range shards: per reference the pass-3 record; staging words
   unsigned long long* fslot = nullptr;  // per reference: the main-table slot of its -1 (cold) key
+  // the radix source's bucket sort (pluss_sort.h): its histograms, parents, chunk map, deep items
+  uint64_t sbcap = 0;
+  unsigned char* sbuf = nullptr;
 };
 
 // state of a key-range shard between the phases of pluss_dev_faithful_shard_*
@@ -152,6 +155,8 @@ int launch_diag_dense(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t n, uns
                       int variant, int max_grid, hipStream_t s);
 int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s);
 int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t* counts, hipStream_t s);
+int diag_sort_words(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, void* d_words,
+                    int32_t* word_bytes, hipStream_t s);
 // faithful mode over key-ordered lists (no sort) and generated key-order lists (no input)
 int launch_faithful_sorted(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s);
 int launch_faithful_sorted_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t* counts, hipStream_t s);

@@ -1,0 +1,775 @@
+// pluss_sort.h — the radix source's sort, hand-written for CDNA: the six
+// references' samples in any order (r10 draws them with rand() into a
+// priority_queue, r10:151-185) -> their packed sort words (rank << 2 | case,
+// pluss_faithful.h) in ascending order per reference, i.e. r10's pop order,
+// all references in one launch sequence (full-chip grids; no per-reference
+// streams).  Replaces a library LSD radix sort (five 8-bit scatter passes over
+// 8-byte keys at N = 4096) by a two-level MSD bucket sort:
+//
+//   k_srt_count1    per chunk of SC samples: each sample's word and a
+//                   histogram of its top digit (d1 bits, <= 256 buckets) in
+//                   LDS; one column per chunk: hist1[ref block][digit][chunk];
+//   scan            exclusive scan of hist1 over all references = the
+//                   absolute start of each (digit, chunk) run;
+//   k_srt_scatter1  per chunk: batches of SBATCH words counting-sorted by digit
+//                   in LDS, written as runs (coalesced) to X1 -- as PAYLOADS:
+//                   the word without its top digit (4 bytes whenever that
+//                   fits: N <= 2^11 + ...; 8 otherwise);
+//   k_srt_plan      one workgroup: per top-level bucket (parent) its range and
+//                   the split of parents past SCAP by d2 more bits into
+//                   level-2 chunks (their count and histogram offsets);
+//   k_srt_count2,   the same count / scan / batched scatter for the parents'
+//   scan,           level-2 chunks, X1 -> Y (payloads stay within their
+//   k_srt_scatter2  parent's range);
+//   k_srt_final     one workgroup per item (a parent left whole, or a child of
+//                   a split one): payloads to LDS, counting-sorted by their
+//                   leading undecided bits, ties insertion-sorted, written as
+//                   words (the parent's digit put back) to OUT;
+//   k_srt_deep      items past SCAP (skewed or duplicated input only): split
+//                   again 8 bits at a time, depth first, inside one workgroup.
+//
+// Every payload moves between HBM arrays three times (X1, Y, OUT), with 4-byte
+// payloads when they fit.  A malformed sample raises the input flag (its word
+// is 0; a flagged pass is never read).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "pluss_device.h"
+
+namespace pluss {
+
+constexpr int SB = 256;                   // threads per sort workgroup
+constexpr int SE = 16;                    // words per thread per batch
+constexpr uint32_t SBATCH = SB * SE;      // words per LDS batch
+constexpr uint32_t SC = 4 * SBATCH;       // words per count/scatter chunk (both levels)
+constexpr uint32_t SCAP = 4096;           // largest item sorted in LDS (k_srt_final)
+constexpr int SDIG = 8;                   // largest digit of a split (256 children)
+constexpr int SDEPTH = 10;                // k_srt_deep's levels (64-bit words, 8-bit digits, + the item)
+static_assert(SCAP == SBATCH, "an item is one batch");
+
+// the references of one sort (a kernel argument)
+struct SrtRefs {
+  uint64_t n[6];
+  uint64_t eoff[7];   // first element of each reference in the concatenated arrays
+  uint64_t coff[7];   // first level-1 chunk of each reference; coff[6] = all chunks
+  uint64_t hoff[7];   // first hist1 entry of each reference; hoff[6] = all entries
+  uint32_t d1[6];     // top digit bits per reference (0: one bucket)
+  const void* in[6];  // samples (SMP) or words (!SMP) of each reference
+  uint32_t wb;        // word bits
+  uint32_t np;        // parents = sum of 2^d1
+};
+
+// a top-level bucket: range [start, start + count) of the concatenated arrays;
+// split past SCAP into 2^d2 children through nc2 level-2 chunks
+struct SrtParent {
+  uint32_t start, count, ref, b1;
+  uint32_t d2, nc2, cbase, h2off;
+};
+
+// an item past SCAP for k_srt_deep: payloads [start, start + count) of X1
+// (buf 0) or Y (buf 1) of parent p, equal on every bit >= hi
+struct SrtItem {
+  uint32_t start, count, hi, bufp;  // bufp = p << 1 | buf
+};
+struct SrtDeep {
+  SrtItem* items;
+  unsigned int* head;
+  uint32_t cap;
+};
+
+__host__ __device__ inline uint32_t srt_log2_ceil(uint64_t x) {
+  uint32_t b = 0;
+  while (b < 63 && (1ull << b) < x) ++b;
+  return b;
+}
+// top-level digit bits of a reference of n words (buckets of about 2K words, at most 256)
+__host__ __device__ inline uint32_t srt_d1(uint64_t n, uint32_t wb) {
+  const uint32_t l = srt_log2_ceil(n);
+  uint32_t d = l > 11 ? l - 11 : 0;
+  d = d > (uint32_t)SDIG ? (uint32_t)SDIG : d;
+  return d > wb ? wb : d;
+}
+// children of a parent past SCAP: a digit of d2 bits (children of about SCAP / 2)
+__host__ __device__ inline uint32_t srt_split_bits(uint32_t cnt, uint32_t hi) {
+  uint32_t D = srt_log2_ceil((cnt + SCAP / 2 - 1) / (SCAP / 2));
+  D = D < 1 ? 1 : (D > (uint32_t)SDIG ? (uint32_t)SDIG : D);
+  return D > hi ? hi : D;
+}
+template <typename T>
+__device__ __forceinline__ T srt_lowmask(uint32_t bits) {
+  return bits >= 8 * sizeof(T) ? (T) ~(T)0 : (T)(((T)1 << bits) - 1);
+}
+
+// the reference a level-1 chunk belongs to (uniform)
+__device__ __forceinline__ uint32_t srt_ref_of_chunk(const SrtRefs& a, uint64_t c) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int x = 1; x < 6; ++x) r += c >= a.coff[x] ? 1u : 0u;
+  return __builtin_amdgcn_readfirstlane(r);
+}
+// per-reference fields copied out by a switch (the kernel argument is never indexed dynamically)
+struct SrtOne {
+  uint64_t n, eoff, c0, h0;
+  uint32_t d1, nch;
+  const void* in;
+};
+__device__ __forceinline__ SrtOne srt_one(const SrtRefs& a, uint32_t r) {
+  SrtOne o;
+#define PLUSS_SRT_ONE(R)                                                                           \
+  case R:                                                                                          \
+    o = SrtOne{a.n[R], a.eoff[R], a.coff[R], a.hoff[R], a.d1[R], (uint32_t)(a.coff[R + 1] - a.coff[R]), a.in[R]}; \
+    break;
+  switch (r) {
+    PLUSS_SRT_ONE(0)
+    PLUSS_SRT_ONE(1)
+    PLUSS_SRT_ONE(2)
+    PLUSS_SRT_ONE(3)
+    PLUSS_SRT_ONE(4)
+    default: o = SrtOne{a.n[5], a.eoff[5], a.coff[5], a.hoff[5], a.d1[5], (uint32_t)(a.coff[6] - a.coff[5]), a.in[5]};
+  }
+#undef PLUSS_SRT_ONE
+  return o;
+}
+
+// the raw input element: a caller's sample (SMP) or a word already made (!SMP)
+template <typename KT, bool SMP>
+using srt_raw_t = typename std::conditional<SMP, uint64_t, KT>::type;
+
+// its word for reference REF (a malformed sample raises the input flag and becomes 0)
+template <typename KT, bool SMP, uint32_t REF>
+__device__ __forceinline__ KT srt_word(const Model& m, srt_raw_t<KT, SMP> x, GTable g) {
+  if constexpr (SMP) {
+    const Sample s = unpack(x);
+    if (s.ref != REF || s.c0 >= m.N || s.c1 >= m.N || s.c2 >= m.N) {
+      atomicOr(&g.flags[1], 1u);
+      return (KT)0;
+    }
+    const uint32_t c2 = (REF == C0 || REF == C1) ? 0u : s.c2;
+    const uint32_t k = fdiv(s.c0, m.dCS), p = s.c0 - k * m.CS;
+    const uint32_t kt = fdiv(k, m.dT), t = k - kt * m.T;
+    const uint64_t q = (uint64_t)kt * m.CS + p;
+    const uint64_t rank = ((q * m.N + s.c1) * m.N + c2) * m.T + t;
+    return (KT)((rank << 2) | case_fast<false>(m, REF, s.c0, s.c1, c2));
+  } else {
+    return x == (KT) ~(KT)0 ? (KT)0 : x;  // the key pass's malformed marker (already flagged)
+  }
+}
+// one batch of SE words per thread: every load issued before the first word is made
+template <typename KT, bool SMP, uint32_t REF>
+__device__ __forceinline__ void srt_load_words(const Model& m, const void* in, uint64_t b, uint64_t e1, KT (&w)[SE],
+                                               GTable g) {
+  const srt_raw_t<KT, SMP>* src = static_cast<const srt_raw_t<KT, SMP>*>(in);
+  srt_raw_t<KT, SMP> x[SE];
+  const uint64_t last = e1 - 1;
+#pragma unroll
+  for (int k = 0; k < SE; ++k) {
+    const uint64_t i = b + (uint64_t)k * SB + threadIdx.x;
+    x[k] = __builtin_nontemporal_load(src + (i < last ? i : last));
+  }
+#pragma unroll
+  for (int k = 0; k < SE; ++k) w[k] = srt_word<KT, SMP, REF>(m, x[k], g);
+}
+#define PLUSS_SRT_REFS(BODY)       \
+  switch (r) {                     \
+    case C0: { BODY(C0); } break;  \
+    case C1: { BODY(C1); } break;  \
+    case A0: { BODY(A0); } break;  \
+    case B0: { BODY(B0); } break;  \
+    case C2: { BODY(C2); } break;  \
+    default: { BODY(C3); } break;  \
+  }
+
+template <typename T>
+__device__ __forceinline__ uint32_t srt_dig(T w, uint32_t lo, uint32_t mask) {
+  return lo >= 8 * sizeof(T) ? 0u : (uint32_t)(w >> lo) & mask;
+}
+
+// exclusive scan of v[0, len) in LDS (len <= SB * 16), all SB threads; returns the total
+__device__ __forceinline__ uint32_t srt_block_scan(uint32_t* v, uint32_t len, uint32_t* wsum) {
+  const uint32_t per = (len + SB - 1) / SB;  // <= 16
+  const uint32_t b = threadIdx.x * per;
+  uint32_t loc[16], s = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k) {
+    loc[k] = (k < per && b + k < len) ? v[b + k] : 0u;
+    s += loc[k];
+  }
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  uint32_t inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += y;
+  }
+  if (lane == 63) wsum[wid] = inc;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int x = 0; x < SB / 64; ++x) {
+    pre += x < (int)wid ? wsum[x] : 0u;
+    tot += wsum[x];
+  }
+  uint32_t run = pre + inc - s;
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k) {
+    if (k < per && b + k < len) v[b + k] = run;
+    run += loc[k];
+  }
+  __syncthreads();
+  return tot;
+}
+
+// ---- exclusive scan of a u32 array in place (three launches): block sums of
+// SBATCH entries, their scan (one workgroup), the blocks rescanned with their
+// prefix.  len: the host's bound; *dlen (if given): the entries in use.
+__global__ __launch_bounds__(SB) void k_scan_sums(const uint32_t* __restrict__ v, uint64_t len,
+                                                 const uint32_t* dlen, uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t wsum[SB / 64];
+  const uint64_t L = dlen ? (*dlen < len ? *dlen : len) : len;
+  const uint64_t b = (uint64_t)blockIdx.x * SBATCH;
+  uint32_t s = 0;
+  if (b < L)
+    for (uint32_t i = threadIdx.x; i < SBATCH && b + i < L; i += SB) s += v[b + i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (__lane_id() == 0) wsum[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) bsum[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+__global__ __launch_bounds__(SB) void k_scan_top(uint32_t* __restrict__ bsum, uint32_t nb) {
+  __shared__ uint32_t v[SBATCH], wsum[SB / 64];
+  uint32_t carry = 0;
+  for (uint32_t b = 0; b < nb; b += SBATCH) {
+    const uint32_t m = nb - b < SBATCH ? nb - b : SBATCH;
+    for (uint32_t i = threadIdx.x; i < m; i += SB) v[i] = bsum[b + i];
+    __syncthreads();
+    const uint32_t tot = srt_block_scan(v, m, wsum);
+    for (uint32_t i = threadIdx.x; i < m; i += SB) bsum[b + i] = v[i] + carry;
+    carry += tot;
+    __syncthreads();
+  }
+}
+__global__ __launch_bounds__(SB) void k_scan_apply(uint32_t* __restrict__ v, uint64_t len, const uint32_t* dlen,
+                                                  const uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t t[SBATCH], wsum[SB / 64];
+  const uint64_t L = dlen ? (*dlen < len ? *dlen : len) : len;
+  const uint64_t b = (uint64_t)blockIdx.x * SBATCH;
+  if (b >= L) return;
+  const uint32_t m = L - b < SBATCH ? (uint32_t)(L - b) : SBATCH;
+  for (uint32_t i = threadIdx.x; i < m; i += SB) t[i] = v[b + i];
+  __syncthreads();
+  srt_block_scan(t, m, wsum);
+  const uint32_t c = bsum[blockIdx.x];
+  for (uint32_t i = threadIdx.x; i < m; i += SB) v[b + i] = t[i] + c;
+}
+
+// One batch of up to SBATCH values (w[k] valid iff vmask bit k) counting-sorted
+// by digit in LDS and written as runs: a value of digit d -> dst[cur[d] + its
+// rank among the batch's values of digit d]; cur[d] advanced.  put(x): the
+// value stored for x (the payload).
+template <typename T, typename OT, class PUT>
+__device__ __forceinline__ void srt_batch(const T (&w)[SE], uint32_t vmask, uint32_t lo, uint32_t mask, T* stage,
+                                          uint32_t* bcnt, uint32_t* bst, uint32_t* cur, uint32_t* wsum,
+                                          OT* __restrict__ dst, PUT&& put) {
+  bcnt[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t r[SE];
+#pragma unroll
+  for (int k = 0; k < SE; ++k) r[k] = (vmask >> k) & 1u ? atomicAdd(&bcnt[srt_dig(w[k], lo, mask)], 1u) : 0u;
+  __syncthreads();
+  bst[threadIdx.x] = bcnt[threadIdx.x];
+  __syncthreads();
+  const uint32_t m = srt_block_scan(bst, SB, wsum);
+#pragma unroll
+  for (int k = 0; k < SE; ++k)
+    if ((vmask >> k) & 1u) stage[bst[srt_dig(w[k], lo, mask)] + r[k]] = w[k];
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < m; i += SB) {
+    const T x = stage[i];
+    const uint32_t d = srt_dig(x, lo, mask);
+    dst[cur[d] + (i - bst[d])] = put(x);
+  }
+  __syncthreads();
+  cur[threadIdx.x] += bcnt[threadIdx.x];
+  __syncthreads();
+}
+
+// ---- level 1 ---------------------------------------------------------------
+template <typename KT, bool SMP>
+__global__ __launch_bounds__(SB) void k_srt_count1(Model m, SrtRefs a, uint32_t* __restrict__ hist, GTable g) {
+  __shared__ uint32_t cnt[SB];
+  cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t r = srt_ref_of_chunk(a, blockIdx.x);
+  const SrtOne o = srt_one(a, r);
+  const uint64_t c = blockIdx.x - o.c0;
+  const uint64_t e0 = c * SC, e1 = o.n - e0 < SC ? o.n : e0 + SC;
+  const uint32_t lo = a.wb - o.d1, mask = (1u << o.d1) - 1;
+#define PLUSS_SRT_COUNT1(R)                                                                  \
+  for (uint64_t b = e0; b < e1; b += SBATCH) {                                               \
+    KT w[SE];                                                                                \
+    srt_load_words<KT, SMP, R>(m, o.in, b, e1, w, g);                                        \
+    _Pragma("unroll") for (int k = 0; k < SE; ++k) if (b + (uint64_t)k * SB + threadIdx.x < e1) \
+        atomicAdd(&cnt[srt_dig(w[k], lo, mask)], 1u);                                        \
+  }
+  PLUSS_SRT_REFS(PLUSS_SRT_COUNT1)
+#undef PLUSS_SRT_COUNT1
+  __syncthreads();
+  if (threadIdx.x <= mask) hist[o.h0 + (uint64_t)threadIdx.x * o.nch + c] = cnt[threadIdx.x];
+}
+
+template <typename KT, typename PT, bool SMP>
+__global__ __launch_bounds__(SB) void k_srt_scatter1(Model m, SrtRefs a, const uint32_t* __restrict__ hist,
+                                                    PT* __restrict__ X1, GTable g) {
+  __shared__ KT stage[SBATCH];
+  __shared__ uint32_t bcnt[SB], bst[SB], cur[SB], wsum[SB / 64];
+  const uint32_t r = srt_ref_of_chunk(a, blockIdx.x);
+  const SrtOne o = srt_one(a, r);
+  const uint64_t c = blockIdx.x - o.c0;
+  const uint64_t e0 = c * SC, e1 = o.n - e0 < SC ? o.n : e0 + SC;
+  const uint32_t lo = a.wb - o.d1, mask = (1u << o.d1) - 1;
+  cur[threadIdx.x] = threadIdx.x <= mask ? hist[o.h0 + (uint64_t)threadIdx.x * o.nch + c] : 0u;
+  const KT pm = srt_lowmask<KT>(lo);
+  auto put = [&](KT x) { return (PT)(x & pm); };
+#define PLUSS_SRT_SCATTER1(R)                                                \
+  for (uint64_t b = e0; b < e1; b += SBATCH) {                               \
+    KT w[SE];                                                                \
+    uint32_t vm = 0;                                                         \
+    srt_load_words<KT, SMP, R>(m, o.in, b, e1, w, g);                        \
+    _Pragma("unroll") for (int k = 0; k < SE; ++k)                           \
+      vm |= (b + (uint64_t)k * SB + threadIdx.x < e1 ? 1u : 0u) << k;        \
+    srt_batch<KT, PT>(w, vm, lo, mask, stage, bcnt, bst, cur, wsum, X1, put); \
+  }
+  PLUSS_SRT_REFS(PLUSS_SRT_SCATTER1)
+#undef PLUSS_SRT_SCATTER1
+}
+
+// ---- the plan: parents, their splits and level-2 chunks (one workgroup).
+// tot[0] = level-2 chunks, tot[1] = hist2 entries.
+__global__ __launch_bounds__(SB) void k_srt_plan(SrtRefs a, const uint32_t* __restrict__ hist,
+                                                SrtParent* __restrict__ par, uint32_t* __restrict__ cmap,
+                                                uint32_t* __restrict__ tot) {
+  __shared__ uint32_t v1[SBATCH], v2[SBATCH], wsum[SB / 64];
+  const uint32_t np = a.np;  // <= 6 * 256
+  // parent p -> (reference, digit): references in order, 2^d1 parents each
+  auto locate = [&](uint32_t p, uint32_t& r, uint32_t& b1) {
+    r = 0;
+    uint32_t base = 0;
+    while (r < 5 && p >= base + (1u << a.d1[r])) {
+      base += 1u << a.d1[r];
+      ++r;
+    }
+    b1 = p - base;
+  };
+  // start of bucket b of reference r (a reference without chunks: every bucket empty at its offset)
+  auto bstart = [&](uint32_t r, uint32_t b) -> uint32_t {
+    const uint32_t nch = (uint32_t)(a.coff[r + 1] - a.coff[r]);
+    return nch ? hist[a.hoff[r] + (uint64_t)b * nch] : (uint32_t)a.eoff[r];
+  };
+  for (uint32_t p = threadIdx.x; p < np; p += SB) {
+    uint32_t r, b1;
+    locate(p, r, b1);
+    const uint32_t s = bstart(r, b1);
+    const uint32_t e = b1 + 1 < (1u << a.d1[r]) ? bstart(r, b1 + 1) : (uint32_t)a.eoff[r + 1];
+    const uint32_t cnt = e - s, hi = a.wb - a.d1[r];
+    const uint32_t d2 = (cnt > SCAP && hi > 0) ? srt_split_bits(cnt, hi) : 0u;
+    const uint32_t nc2 = d2 ? (cnt + SC - 1) / SC : 0u;
+    par[p] = SrtParent{s, cnt, r, b1, d2, nc2, 0, 0};
+    v1[p] = nc2;
+    v2[p] = nc2 << d2;
+  }
+  __syncthreads();
+  const uint32_t g2 = srt_block_scan(v1, np, wsum);
+  const uint32_t h2 = srt_block_scan(v2, np, wsum);
+  for (uint32_t p = threadIdx.x; p < np; p += SB) {
+    par[p].cbase = v1[p];
+    par[p].h2off = v2[p];
+    const uint32_t nc2 = par[p].nc2;
+    for (uint32_t k = 0; k < nc2; ++k) cmap[v1[p] + k] = p;
+  }
+  if (threadIdx.x == 0) {
+    tot[0] = g2;
+    tot[1] = h2;
+  }
+}
+
+// ---- level 2 (grid: the host's bound on level-2 chunks; tot[0] in use)
+template <typename PT>
+__global__ __launch_bounds__(SB) void k_srt_count2(const SrtRefs a, const SrtParent* __restrict__ par,
+                                                  const uint32_t* __restrict__ cmap, const uint32_t* __restrict__ tot,
+                                                  const PT* __restrict__ X1, uint32_t* __restrict__ hist2) {
+  __shared__ uint32_t cnt[SB];
+  if (blockIdx.x >= tot[0]) return;
+  const SrtParent P = par[cmap[blockIdx.x]];
+  const uint32_t k = blockIdx.x - P.cbase;
+  const uint32_t e0 = P.start + k * SC, e1 = P.count - k * SC < SC ? P.start + P.count : e0 + SC;
+  const uint32_t lo = a.wb - a.d1[P.ref] - P.d2, mask = (1u << P.d2) - 1;
+  cnt[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t b = e0; b < e1; b += SBATCH) {
+    PT w[SE];
+    const uint32_t last = e1 - 1;
+#pragma unroll
+    for (int j = 0; j < SE; ++j) {
+      const uint32_t i = b + (uint32_t)j * SB + threadIdx.x;
+      w[j] = X1[i < last ? i : last];
+    }
+#pragma unroll
+    for (int j = 0; j < SE; ++j)
+      if (b + (uint32_t)j * SB + threadIdx.x < e1) atomicAdd(&cnt[srt_dig(w[j], lo, mask)], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x <= mask) hist2[P.h2off + threadIdx.x * P.nc2 + k] = cnt[threadIdx.x];
+}
+
+template <typename PT>
+__global__ __launch_bounds__(SB) void k_srt_scatter2(const SrtRefs a, const SrtParent* __restrict__ par,
+                                                    const uint32_t* __restrict__ cmap,
+                                                    const uint32_t* __restrict__ tot, const uint32_t* __restrict__ hist2,
+                                                    const PT* __restrict__ X1, PT* __restrict__ Y) {
+  __shared__ PT stage[SBATCH];
+  __shared__ uint32_t bcnt[SB], bst[SB], cur[SB], wsum[SB / 64];
+  if (blockIdx.x >= tot[0]) return;
+  const SrtParent P = par[cmap[blockIdx.x]];
+  const uint32_t k = blockIdx.x - P.cbase;
+  const uint32_t e0 = P.start + k * SC, e1 = P.count - k * SC < SC ? P.start + P.count : e0 + SC;
+  const uint32_t lo = a.wb - a.d1[P.ref] - P.d2, mask = (1u << P.d2) - 1;
+  const uint32_t base = hist2[P.h2off];
+  cur[threadIdx.x] = threadIdx.x <= mask ? P.start + hist2[P.h2off + threadIdx.x * P.nc2 + k] - base : 0u;
+  auto put = [](PT x) { return x; };
+  for (uint32_t b = e0; b < e1; b += SBATCH) {
+    PT w[SE];
+    uint32_t vm = 0;
+    const uint32_t last = e1 - 1;
+#pragma unroll
+    for (int j = 0; j < SE; ++j) {
+      const uint32_t i = b + (uint32_t)j * SB + threadIdx.x;
+      w[j] = X1[i < last ? i : last];
+      vm |= (i < e1 ? 1u : 0u) << j;
+    }
+    srt_batch<PT, PT>(w, vm, lo, mask, stage, bcnt, bst, cur, wsum, Y, put);
+  }
+}
+
+// Sort one item (count <= SCAP payloads of src[s, s + count), equal on every bit
+// >= hi) in LDS and write it as words to OUT: counting sort by the leading D
+// undecided bits, then an insertion sort of each run of equal leading bits
+// (runs average below one payload).  bb: SCAP payloads; c: SCAP + 1 words.
+template <typename PT, typename KT>
+__device__ __forceinline__ void srt_sort_item(const PT* __restrict__ src, uint32_t s, uint32_t cnt, uint32_t hi,
+                                              KT prefix, KT* __restrict__ OUT, PT* bb, uint32_t* c,
+                                              uint32_t* wsum) {
+  PT w[SE];
+  const uint32_t last = cnt - 1;
+#pragma unroll
+  for (int k = 0; k < SE; ++k) {  // nt: past L1 (the deep pass reads back what this workgroup wrote)
+    const uint32_t i = (uint32_t)k * SB + threadIdx.x;
+    w[k] = __builtin_nontemporal_load(src + s + (i < last ? i : last));
+  }
+  if (hi == 0) {  // every payload equal
+#pragma unroll
+    for (int k = 0; k < SE; ++k) {
+      const uint32_t i = (uint32_t)k * SB + threadIdx.x;
+      if (i < cnt) OUT[s + i] = prefix | (KT)w[k];
+    }
+    return;
+  }
+  uint32_t D = srt_log2_ceil(cnt);
+  D = D < 1 ? 1 : D;
+  D = D > hi ? hi : D;
+  const uint32_t nb = 1u << D, lo = hi - D, mask = nb - 1;
+  for (uint32_t i = threadIdx.x; i < nb; i += SB) c[i] = 0;
+  __syncthreads();
+  uint32_t r[SE];
+#pragma unroll
+  for (int k = 0; k < SE; ++k) {
+    const uint32_t i = (uint32_t)k * SB + threadIdx.x;
+    r[k] = i < cnt ? atomicAdd(&c[srt_dig(w[k], lo, mask)], 1u) : 0u;
+  }
+  __syncthreads();
+  srt_block_scan(c, nb, wsum);
+  if (threadIdx.x == 0) c[nb] = cnt;
+#pragma unroll
+  for (int k = 0; k < SE; ++k) {
+    const uint32_t i = (uint32_t)k * SB + threadIdx.x;
+    if (i < cnt) bb[c[srt_dig(w[k], lo, mask)] + r[k]] = w[k];
+  }
+  __syncthreads();
+  if (lo > 0) {  // runs of equal leading bits: insertion sort (one thread per run)
+    for (uint32_t d = threadIdx.x; d < nb; d += SB) {
+      const uint32_t b0 = c[d], e = c[d + 1];
+      for (uint32_t i = b0 + 1; i < e; ++i) {
+        const PT x = bb[i];
+        uint32_t j = i;
+        while (j > b0 && bb[j - 1] > x) {
+          bb[j] = bb[j - 1];
+          --j;
+        }
+        bb[j] = x;
+      }
+    }
+    __syncthreads();
+  }
+  for (uint32_t i = threadIdx.x; i < cnt; i += SB) OUT[s + i] = prefix | (KT)bb[i];
+}
+
+template <typename KT>
+__device__ __forceinline__ KT srt_prefix(const SrtRefs& a, const SrtParent& P) {
+  const uint32_t hi = a.wb - a.d1[P.ref];
+  return hi >= 8 * sizeof(KT) ? (KT)0 : (KT)((KT)P.b1 << hi);
+}
+
+// A workgroup barrier that waits for LDS operations only: vector-memory loads
+// issued before it (the next item's payloads) stay in flight across it.
+__device__ __forceinline__ void srt_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// srt_block_scan with LDS-only barriers
+__device__ __forceinline__ void srt_block_scan_lds(uint32_t* v, uint32_t len, uint32_t* wsum) {
+  const uint32_t per = (len + SB - 1) / SB;  // <= 16
+  const uint32_t b = threadIdx.x * per;
+  uint32_t loc[16], sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k) {
+    loc[k] = (k < per && b + k < len) ? v[b + k] : 0u;
+    sum += loc[k];
+  }
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  uint32_t inc = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += y;
+  }
+  if (lane == 63) wsum[wid] = inc;
+  srt_lds_sync();
+  uint32_t pre = 0;
+#pragma unroll
+  for (int x = 0; x < SB / 64; ++x) pre += x < (int)wid ? wsum[x] : 0u;
+  uint32_t run = pre + inc - sum;
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k) {
+    if (k < per && b + k < len) v[b + k] = run;
+    run += loc[k];
+  }
+  srt_lds_sync();
+}
+
+template <typename PT>
+__device__ __forceinline__ void srt_item_load(const PT* __restrict__ src, uint32_t s, uint32_t cnt, PT (&w)[SE]) {
+  const uint32_t last = cnt - 1;
+#pragma unroll
+  for (int k = 0; k < SE; ++k) {
+    const uint32_t i = (uint32_t)k * SB + threadIdx.x;
+    w[k] = __builtin_nontemporal_load(src + s + (i < last ? i : last));
+  }
+}
+
+// srt_sort_item on payloads already in registers, LDS-only barriers; bb, c
+// free on entry and on return
+template <typename PT, typename KT>
+__device__ __forceinline__ void srt_item_sort(const PT (&w)[SE], uint32_t s, uint32_t cnt, uint32_t hi, KT prefix,
+                                              KT* __restrict__ OUT, PT* bb, uint32_t* c, uint32_t* wsum) {
+  if (hi == 0) {  // every payload equal
+#pragma unroll
+    for (int k = 0; k < SE; ++k) {
+      const uint32_t i = (uint32_t)k * SB + threadIdx.x;
+      if (i < cnt) OUT[s + i] = prefix | (KT)w[k];
+    }
+    return;
+  }
+  uint32_t D = srt_log2_ceil(cnt);
+  D = D < 1 ? 1 : D;
+  D = D > hi ? hi : D;
+  const uint32_t nb = 1u << D, lo = hi - D, mask = nb - 1;
+  for (uint32_t i = threadIdx.x; i < nb; i += SB) c[i] = 0;
+  srt_lds_sync();
+  uint32_t r[SE];
+#pragma unroll
+  for (int k = 0; k < SE; ++k) {
+    const uint32_t i = (uint32_t)k * SB + threadIdx.x;
+    r[k] = i < cnt ? atomicAdd(&c[srt_dig(w[k], lo, mask)], 1u) : 0u;
+  }
+  srt_lds_sync();
+  srt_block_scan_lds(c, nb, wsum);
+  if (threadIdx.x == 0) c[nb] = cnt;
+#pragma unroll
+  for (int k = 0; k < SE; ++k) {
+    const uint32_t i = (uint32_t)k * SB + threadIdx.x;
+    if (i < cnt) bb[c[srt_dig(w[k], lo, mask)] + r[k]] = w[k];
+  }
+  srt_lds_sync();
+  if (lo > 0) {  // runs of equal leading bits: insertion sort (one thread per run)
+    for (uint32_t d = threadIdx.x; d < nb; d += SB) {
+      const uint32_t b0 = c[d], e = c[d + 1];
+      for (uint32_t i = b0 + 1; i < e; ++i) {
+        const PT x = bb[i];
+        uint32_t j = i;
+        while (j > b0 && bb[j - 1] > x) {
+          bb[j] = bb[j - 1];
+          --j;
+        }
+        bb[j] = x;
+      }
+    }
+    srt_lds_sync();
+  }
+  for (uint32_t i = threadIdx.x; i < cnt; i += SB) OUT[s + i] = prefix | (KT)bb[i];
+  srt_lds_sync();
+}
+
+// ---- k_srt_final: grid (FG, parents).  A parent left whole is one item
+// (workgroup 0); a split parent's children d = x, x + FG, ... go to workgroup
+// x, each child's payloads loaded while the previous one is sorted.  Items
+// past SCAP go to the deep list.
+constexpr uint32_t FG = 4;
+template <typename PT, typename KT>
+__global__ __launch_bounds__(SB) void k_srt_final(const SrtRefs a, const SrtParent* __restrict__ par,
+                                                 const uint32_t* __restrict__ hist2, const PT* __restrict__ X1,
+                                                 const PT* __restrict__ Y, KT* __restrict__ OUT, SrtDeep dp) {
+  __shared__ PT bb[SCAP];
+  __shared__ uint32_t c[SCAP + 1], bnd[SB + 1], wsum[SB / 64];
+  const uint32_t p = blockIdx.y;
+  const SrtParent P = par[p];
+  const uint32_t hi1 = a.wb - a.d1[P.ref];
+  const KT prefix = srt_prefix<KT>(a, P);
+  auto deep = [&](uint32_t s, uint32_t cnt, uint32_t hi, uint32_t buf) {
+    if (threadIdx.x == 0) {
+      const unsigned int q = atomicAdd(dp.head, 1u);
+      if (q < dp.cap) dp.items[q] = SrtItem{s, cnt, hi, p << 1 | buf};
+    }
+  };
+  if (P.d2 == 0) {
+    if (blockIdx.x != 0 || P.count == 0) return;
+    if (P.count > SCAP) {
+      deep(P.start, P.count, hi1, 0);
+      return;
+    }
+    PT w[SE];
+    srt_item_load(X1, P.start, P.count, w);
+    srt_item_sort<PT, KT>(w, P.start, P.count, hi1, prefix, OUT, bb, c, wsum);
+    return;
+  }
+  const uint32_t nc = 1u << P.d2, hi = hi1 - P.d2;
+  const uint32_t base = hist2[P.h2off];
+  for (uint32_t i = threadIdx.x; i <= nc; i += SB)
+    bnd[i] = i < nc ? P.start + hist2[P.h2off + i * P.nc2] - base : P.start + P.count;
+  __syncthreads();
+  auto next = [&](uint32_t d) {  // the next child of this workgroup to sort here (pushing deep ones)
+    for (; d < nc; d += FG) {
+      const uint32_t cnt = bnd[d + 1] - bnd[d];
+      if (cnt == 0) continue;
+      if (cnt <= SCAP) break;
+      deep(bnd[d], cnt, hi, 1);
+    }
+    return d;
+  };
+  uint32_t d = next(blockIdx.x);
+  PT w[SE];
+  if (d < nc) srt_item_load(Y, bnd[d], bnd[d + 1] - bnd[d], w);
+  while (d < nc) {
+    const uint32_t dn = next(d + FG);
+    const uint32_t dl = dn < nc ? dn : d;  // no next child: a harmless reload (the loads stay unconditional)
+    PT wn[SE];
+    srt_item_load(Y, bnd[dl], bnd[dl + 1] - bnd[dl], wn);
+    srt_item_sort<PT, KT>(w, bnd[d], bnd[d + 1] - bnd[d], hi, prefix, OUT, bb, c, wsum);
+#pragma unroll
+    for (int k = 0; k < SE; ++k) w[k] = wn[k];
+    d = dn;
+  }
+}
+
+// ---- k_srt_deep: items past SCAP (skewed or duplicated words), split by
+// 8-bit digits depth first inside one workgroup; a level's children alternate
+// between Y and X1 at the same offsets; every item ends in OUT as words.
+template <typename PT, typename KT>
+__global__ __launch_bounds__(SB) void k_srt_deep(const SrtRefs a, const SrtParent* __restrict__ par,
+                                                PT* __restrict__ X1, PT* __restrict__ Y, KT* __restrict__ OUT,
+                                                SrtDeep dp) {
+  __shared__ PT stage[SBATCH];  // also the final sort's payload buffer (SBATCH == SCAP)
+  __shared__ uint32_t off[SDEPTH][SB + 1], c[SCAP + 1], bcnt[SB], bst[SB], cur[SB], wsum[SB / 64];
+  __shared__ SrtItem lv[SDEPTH];
+  __shared__ uint32_t nxt[SDEPTH], nchild[SDEPTH];
+  const uint32_t nd = *dp.head < dp.cap ? *dp.head : dp.cap;
+  auto put = [](PT x) { return x; };
+  for (uint32_t q = blockIdx.x; q < nd; q += gridDim.x) {
+    int top = 0;
+    const SrtItem root = dp.items[q];
+    const KT prefix = srt_prefix<KT>(a, par[root.bufp >> 1]);
+    if (threadIdx.x == 0) {
+      lv[0] = root;
+      nxt[0] = 0xFFFFFFFFu;  // not split yet
+    }
+    __syncthreads();
+    while (top >= 0) {
+      const SrtItem it = lv[top];
+      const uint32_t buf = it.bufp & 1u;
+      const uint32_t D = it.hi < (uint32_t)SDIG ? it.hi : (uint32_t)SDIG;
+      if (nxt[top] == 0xFFFFFFFFu) {  // first visit
+        if (it.count <= SCAP || it.hi == 0) {
+          if (it.count <= SCAP) {
+            srt_sort_item<PT, KT>(buf ? Y : X1, it.start, it.count, it.hi, prefix, OUT, stage, c, wsum);
+          } else {  // all equal
+            const PT* src = buf ? Y : X1;
+            for (uint32_t i = threadIdx.x; i < it.count; i += SB)
+              OUT[it.start + i] = prefix | (KT)__builtin_nontemporal_load(src + it.start + i);
+          }
+          __syncthreads();
+          --top;
+          continue;
+        }
+        const uint32_t lo = it.hi - D, mask = (1u << D) - 1;
+        const PT* src = buf ? Y : X1;
+        PT* dst = buf ? X1 : Y;
+        bcnt[threadIdx.x] = 0;
+        __syncthreads();
+        for (uint32_t b = 0; b < it.count; b += SBATCH) {  // histogram
+#pragma unroll
+          for (int k = 0; k < SE; ++k) {
+            const uint32_t i = b + (uint32_t)k * SB + threadIdx.x;
+            if (i < it.count) atomicAdd(&bcnt[srt_dig(__builtin_nontemporal_load(src + it.start + i), lo, mask)], 1u);
+          }
+        }
+        __syncthreads();
+        off[top][threadIdx.x] = bcnt[threadIdx.x];
+        __syncthreads();
+        srt_block_scan(off[top], SB, wsum);
+        if (threadIdx.x == 0) {
+          off[top][SB] = it.count;
+          nxt[top] = 0;
+          nchild[top] = mask + 1;
+        }
+        cur[threadIdx.x] = it.start + off[top][threadIdx.x];
+        __syncthreads();
+        for (uint32_t b = 0; b < it.count; b += SBATCH) {
+          PT w[SE];
+          uint32_t vm = 0;
+#pragma unroll
+          for (int k = 0; k < SE; ++k) {
+            const uint32_t i = b + (uint32_t)k * SB + threadIdx.x;
+            w[k] = __builtin_nontemporal_load(src + it.start + (i < it.count ? i : it.count - 1));
+            vm |= (i < it.count ? 1u : 0u) << k;
+          }
+          srt_batch<PT, PT>(w, vm, lo, mask, stage, bcnt, bst, cur, wsum, dst, put);
+        }
+      }
+      uint32_t d = nxt[top];  // the next non-empty child, if any
+      const uint32_t nc = nchild[top];
+      while (d < nc && off[top][d + 1] == off[top][d]) ++d;
+      __syncthreads();
+      if (d >= nc) {
+        --top;
+        continue;
+      }
+      if (threadIdx.x == 0) {
+        nxt[top] = d + 1;
+        lv[top + 1] = SrtItem{it.start + off[top][d], off[top][d + 1] - off[top][d], it.hi - D, it.bufp ^ 1u};
+        nxt[top + 1] = 0xFFFFFFFFu;
+      }
+      __syncthreads();
+      ++top;
+    }
+  }
+}
+
+}  // namespace pluss
