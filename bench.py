@@ -250,8 +250,9 @@ def faithful_bench(P, torch, device, stream):
     """FAITHFUL mode (r10 queue semantics) at config 2 (N=1024, T=8, 2^24
     samples), the six sampler_<REF> at once (one stream per reference, as r10
     runs one thread per reference):
-      radix:     the Feistel list (arbitrary order): keys -> rocPRIM radix sort ->
-                 the single-read scan pipeline (pluss_dev_faithful_hist_refs);
+      radix:     the Feistel list (arbitrary order): the hand-written bucket sort
+                 of the six references (csrc/pluss_sort.h) -> the single-read
+                 scan pipeline (pluss_dev_faithful_hist_refs);
       sorted:    the key-order list (pluss_dev_expand_sorted) read once, no sort
                  (pluss_dev_faithful_hist_sorted_refs): 8 B per sample;
       generated: the same key-order lists generated inside the pass, no input
@@ -337,7 +338,7 @@ def faithful_config3_bench(P, torch, device, stream, reps=5):
             off += c
         runs = {"sorted": (lambda: ctx.faithful_hist_sorted_refs(buf.data_ptr(), counts, sp), reps),
                 "generated": (lambda: ctx.gen_faithful_refs(SEED, counts, sp), reps),
-                "radix": (lambda: ctx.faithful_hist_refs(fe.data_ptr(), counts, sp), 2)}
+                "radix": (lambda: ctx.faithful_hist_refs(fe.data_ptr(), counts, sp), reps)}
         hs = {}
         for name, (run, k) in runs.items():
             ctx.reset(sp)

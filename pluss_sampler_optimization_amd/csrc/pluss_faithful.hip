@@ -626,6 +626,8 @@ static SrtPlan srt_plan(const Model& m, const void* const in[6], const uint64_t 
   P.a.hoff[6] = h;
   P.a.wb = wb;
   P.a.np = (uint32_t)np;
+  P.a.tsh = 0;
+  while ((1u << P.a.tsh) < m.T) ++P.a.tsh;
   P.ntot = e;
   P.h1 = h;
   P.g2max = e / SC + np + 1;
@@ -673,9 +675,18 @@ static int srt_launch(pluss_ctx* ctx, FaithfulBufs& b, const SrtPlan& P, PT* X1,
   const SrtDeep dp{(SrtItem*)(B + P.o_deep), tot + 2, P.a.np * (uint32_t)SB};
   PLUSS_HIP_CHECK(hipMemsetAsync(tot, 0, 16, s));
   const unsigned g1 = (unsigned)P.a.coff[6];
-  hipLaunchKernelGGL((k_srt_count1<KT, SMP>), dim3(g1), dim3(SB), 0, s, m, P.a, h1, ctx->g);
+  const bool p2 = m.p2 && (1u << P.a.tsh) == m.T;  // shift decodes of c0
+  if (p2)
+    hipLaunchKernelGGL((k_srt_count1<KT, SMP, true>), dim3(g1), dim3(SB), 0, s, m, P.a, h1, ctx->g);
+  else
+    hipLaunchKernelGGL((k_srt_count1<KT, SMP, false>), dim3(g1), dim3(SB), 0, s, m, P.a, h1, ctx->g);
   srt_scan(h1, P.h1, nullptr, bs, s);
-  hipLaunchKernelGGL((k_srt_scatter1<KT, PT, SMP>), dim3(g1), dim3(SB), 0, s, m, P.a, (const uint32_t*)h1, X1, ctx->g);
+  if (p2)
+    hipLaunchKernelGGL((k_srt_scatter1<KT, PT, SMP, true>), dim3(g1), dim3(SB), 0, s, m, P.a, (const uint32_t*)h1, X1,
+                       ctx->g);
+  else
+    hipLaunchKernelGGL((k_srt_scatter1<KT, PT, SMP, false>), dim3(g1), dim3(SB), 0, s, m, P.a, (const uint32_t*)h1,
+                       X1, ctx->g);
   hipLaunchKernelGGL(k_srt_plan, dim3(1), dim3(SB), 0, s, P.a, (const uint32_t*)h1, par, cmap, tot);
   hipLaunchKernelGGL(k_srt_count2<PT>, dim3((unsigned)P.g2max), dim3(SB), 0, s, P.a, (const SrtParent*)par,
                      (const uint32_t*)cmap, (const uint32_t*)tot, (const PT*)X1, h2);

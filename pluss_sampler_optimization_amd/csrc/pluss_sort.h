@@ -59,6 +59,7 @@ struct SrtRefs {
   const void* in[6];  // samples (SMP) or words (!SMP) of each reference
   uint32_t wb;        // word bits
   uint32_t np;        // parents = sum of 2^d1
+  uint32_t tsh;       // log2(T) (P2 decodes)
 };
 
 // a top-level bucket: range [start, start + count) of the concatenated arrays;
@@ -137,9 +138,10 @@ __device__ __forceinline__ SrtOne srt_one(const SrtRefs& a, uint32_t r) {
 template <typename KT, bool SMP>
 using srt_raw_t = typename std::conditional<SMP, uint64_t, KT>::type;
 
-// its word for reference REF (a malformed sample raises the input flag and becomes 0)
-template <typename KT, bool SMP, uint32_t REF>
-__device__ __forceinline__ KT srt_word(const Model& m, srt_raw_t<KT, SMP> x, GTable g) {
+// its word for reference REF (a malformed sample raises the input flag and
+// becomes 0).  P2: CS, T and CLS/DS powers of two -- c0 -> (q, tid) by shifts.
+template <typename KT, bool SMP, bool P2, uint32_t REF>
+__device__ __forceinline__ KT srt_word(const Model& m, uint32_t tsh, srt_raw_t<KT, SMP> x, GTable g) {
   if constexpr (SMP) {
     const Sample s = unpack(x);
     if (s.ref != REF || s.c0 >= m.N || s.c1 >= m.N || s.c2 >= m.N) {
@@ -147,19 +149,28 @@ __device__ __forceinline__ KT srt_word(const Model& m, srt_raw_t<KT, SMP> x, GTa
       return (KT)0;
     }
     const uint32_t c2 = (REF == C0 || REF == C1) ? 0u : s.c2;
-    const uint32_t k = fdiv(s.c0, m.dCS), p = s.c0 - k * m.CS;
-    const uint32_t kt = fdiv(k, m.dT), t = k - kt * m.T;
-    const uint64_t q = (uint64_t)kt * m.CS + p;
+    uint32_t t;
+    uint64_t q;
+    if constexpr (P2) {
+      const uint32_t k = s.c0 >> m.csshift;
+      t = k & (m.T - 1);
+      q = ((uint64_t)(k >> tsh) << m.csshift) | (s.c0 & m.csmask);
+    } else {
+      const uint32_t k = fdiv(s.c0, m.dCS), p = s.c0 - k * m.CS;
+      const uint32_t kt = fdiv(k, m.dT);
+      t = k - kt * m.T;
+      q = (uint64_t)kt * m.CS + p;
+    }
     const uint64_t rank = ((q * m.N + s.c1) * m.N + c2) * m.T + t;
-    return (KT)((rank << 2) | case_fast<false>(m, REF, s.c0, s.c1, c2));
+    return (KT)((rank << 2) | case_fast<P2>(m, REF, s.c0, s.c1, c2));
   } else {
     return x == (KT) ~(KT)0 ? (KT)0 : x;  // the key pass's malformed marker (already flagged)
   }
 }
 // one batch of SE words per thread: every load issued before the first word is made
-template <typename KT, bool SMP, uint32_t REF>
-__device__ __forceinline__ void srt_load_words(const Model& m, const void* in, uint64_t b, uint64_t e1, KT (&w)[SE],
-                                               GTable g) {
+template <typename KT, bool SMP, bool P2, uint32_t REF>
+__device__ __forceinline__ void srt_load_words(const Model& m, uint32_t tsh, const void* in, uint64_t b, uint64_t e1,
+                                               KT (&w)[SE], GTable g) {
   const srt_raw_t<KT, SMP>* src = static_cast<const srt_raw_t<KT, SMP>*>(in);
   srt_raw_t<KT, SMP> x[SE];
   const uint64_t last = e1 - 1;
@@ -169,7 +180,7 @@ __device__ __forceinline__ void srt_load_words(const Model& m, const void* in, u
     x[k] = __builtin_nontemporal_load(src + (i < last ? i : last));
   }
 #pragma unroll
-  for (int k = 0; k < SE; ++k) w[k] = srt_word<KT, SMP, REF>(m, x[k], g);
+  for (int k = 0; k < SE; ++k) w[k] = srt_word<KT, SMP, P2, REF>(m, tsh, x[k], g);
 }
 #define PLUSS_SRT_REFS(BODY)       \
   switch (r) {                     \
@@ -296,7 +307,7 @@ __device__ __forceinline__ void srt_batch(const T (&w)[SE], uint32_t vmask, uint
 }
 
 // ---- level 1 ---------------------------------------------------------------
-template <typename KT, bool SMP>
+template <typename KT, bool SMP, bool P2>
 __global__ __launch_bounds__(SB) void k_srt_count1(Model m, SrtRefs a, uint32_t* __restrict__ hist, GTable g) {
   __shared__ uint32_t cnt[SB];
   cnt[threadIdx.x] = 0;
@@ -309,7 +320,7 @@ __global__ __launch_bounds__(SB) void k_srt_count1(Model m, SrtRefs a, uint32_t*
 #define PLUSS_SRT_COUNT1(R)                                                                  \
   for (uint64_t b = e0; b < e1; b += SBATCH) {                                               \
     KT w[SE];                                                                                \
-    srt_load_words<KT, SMP, R>(m, o.in, b, e1, w, g);                                        \
+    srt_load_words<KT, SMP, P2, R>(m, a.tsh, o.in, b, e1, w, g);                                        \
     _Pragma("unroll") for (int k = 0; k < SE; ++k) if (b + (uint64_t)k * SB + threadIdx.x < e1) \
         atomicAdd(&cnt[srt_dig(w[k], lo, mask)], 1u);                                        \
   }
@@ -319,7 +330,7 @@ __global__ __launch_bounds__(SB) void k_srt_count1(Model m, SrtRefs a, uint32_t*
   if (threadIdx.x <= mask) hist[o.h0 + (uint64_t)threadIdx.x * o.nch + c] = cnt[threadIdx.x];
 }
 
-template <typename KT, typename PT, bool SMP>
+template <typename KT, typename PT, bool SMP, bool P2>
 __global__ __launch_bounds__(SB) void k_srt_scatter1(Model m, SrtRefs a, const uint32_t* __restrict__ hist,
                                                     PT* __restrict__ X1, GTable g) {
   __shared__ KT stage[SBATCH];
@@ -336,7 +347,7 @@ __global__ __launch_bounds__(SB) void k_srt_scatter1(Model m, SrtRefs a, const u
   for (uint64_t b = e0; b < e1; b += SBATCH) {                               \
     KT w[SE];                                                                \
     uint32_t vm = 0;                                                         \
-    srt_load_words<KT, SMP, R>(m, o.in, b, e1, w, g);                        \
+    srt_load_words<KT, SMP, P2, R>(m, a.tsh, o.in, b, e1, w, g);                        \
     _Pragma("unroll") for (int k = 0; k < SE; ++k)                           \
       vm |= (b + (uint64_t)k * SB + threadIdx.x < e1 ? 1u : 0u) << k;        \
     srt_batch<KT, PT>(w, vm, lo, mask, stage, bcnt, bst, cur, wsum, X1, put); \
@@ -520,20 +531,32 @@ __device__ __forceinline__ KT srt_prefix(const SrtRefs& a, const SrtParent& P) {
   return hi >= 8 * sizeof(KT) ? (KT)0 : (KT)((KT)P.b1 << hi);
 }
 
-// A workgroup barrier that waits for LDS operations only: vector-memory loads
-// issued before it (the next item's payloads) stay in flight across it.
-__device__ __forceinline__ void srt_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// The final pass's workgroup barrier.  (An LDS-only barrier -- s_waitcnt
+// lgkmcnt(0); s_barrier in inline asm, which would keep the next item's
+// prefetched loads in flight -- misplaced a few words per 10^5 on gfx950 in
+// tests/test_gpu_sort.py, intermittently; the full barrier never did.)
+__device__ __forceinline__ void srt_lds_sync() { __syncthreads(); }
 
-// srt_block_scan with LDS-only barriers
+// srt_block_scan with the final pass's barrier and 16-byte reads
 __device__ __forceinline__ void srt_block_scan_lds(uint32_t* v, uint32_t len, uint32_t* wsum) {
   const uint32_t per = (len + SB - 1) / SB;  // <= 16
   const uint32_t b = threadIdx.x * per;
   uint32_t loc[16], sum = 0;
+  if ((len & (4 * SB - 1)) == 0) {  // len a multiple of 1024: 16-byte LDS reads (no bank conflicts)
 #pragma unroll
-  for (uint32_t k = 0; k < 16; ++k) {
-    loc[k] = (k < per && b + k < len) ? v[b + k] : 0u;
-    sum += loc[k];
+    for (uint32_t k = 0; k < 16; k += 4) {
+      const uint4 q = k < per ? *reinterpret_cast<const uint4*>(v + b + k) : make_uint4(0, 0, 0, 0);
+      loc[k] = q.x;
+      loc[k + 1] = q.y;
+      loc[k + 2] = q.z;
+      loc[k + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) loc[k] = (k < per && b + k < len) ? v[b + k] : 0u;
   }
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k) sum += loc[k];
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
   uint32_t inc = sum;
 #pragma unroll
@@ -565,11 +588,16 @@ __device__ __forceinline__ void srt_item_load(const PT* __restrict__ src, uint32
   }
 }
 
-// srt_sort_item on payloads already in registers, LDS-only barriers; bb, c
-// free on entry and on return
+// srt_sort_item on payloads already in registers, LDS-only barriers: a
+// counting sort by the leading D undecided bits groups the payloads in bb;
+// each payload's final place is its group's start plus the number of the
+// group's payloads below it (ties: below it in bb), written to ob; then ob
+// goes out in order.  Groups average at most one payload (D = log2(cnt)), so
+// the count is a short loop in every lane (no per-thread insertion sort, which
+// diverged).  bb, ob: SCAP payloads; c: SCAP + 1 words; all free on return.
 template <typename PT, typename KT>
 __device__ __forceinline__ void srt_item_sort(const PT (&w)[SE], uint32_t s, uint32_t cnt, uint32_t hi, KT prefix,
-                                              KT* __restrict__ OUT, PT* bb, uint32_t* c, uint32_t* wsum) {
+                                              KT* __restrict__ OUT, PT* bb, PT* ob, uint32_t* c, uint32_t* wsum) {
   if (hi == 0) {  // every payload equal
 #pragma unroll
     for (int k = 0; k < SE; ++k) {
@@ -579,7 +607,7 @@ __device__ __forceinline__ void srt_item_sort(const PT (&w)[SE], uint32_t s, uin
     return;
   }
   uint32_t D = srt_log2_ceil(cnt);
-  D = D < 1 ? 1 : D;
+  D = D < 10 ? 10 : D;  // (nb a multiple of 1024: the scan's 16-byte reads)
   D = D > hi ? hi : D;
   const uint32_t nb = 1u << D, lo = hi - D, mask = nb - 1;
   for (uint32_t i = threadIdx.x; i < nb; i += SB) c[i] = 0;
@@ -590,31 +618,39 @@ __device__ __forceinline__ void srt_item_sort(const PT (&w)[SE], uint32_t s, uin
     const uint32_t i = (uint32_t)k * SB + threadIdx.x;
     r[k] = i < cnt ? atomicAdd(&c[srt_dig(w[k], lo, mask)], 1u) : 0u;
   }
+  if (threadIdx.x == 0) c[nb] = cnt;  // (the group end of the last digit; visible after the scan's barrier)
   srt_lds_sync();
   srt_block_scan_lds(c, nb, wsum);
-  if (threadIdx.x == 0) c[nb] = cnt;
+  uint32_t g0[SE], g1[SE];
 #pragma unroll
   for (int k = 0; k < SE; ++k) {
     const uint32_t i = (uint32_t)k * SB + threadIdx.x;
-    if (i < cnt) bb[c[srt_dig(w[k], lo, mask)] + r[k]] = w[k];
+    const uint32_t d = srt_dig(w[k], lo, mask);
+    g0[k] = c[d];
+    g1[k] = c[d + 1];
+    if (i < cnt) bb[g0[k] + r[k]] = w[k];
   }
   srt_lds_sync();
-  if (lo > 0) {  // runs of equal leading bits: insertion sort (one thread per run)
-    for (uint32_t d = threadIdx.x; d < nb; d += SB) {
-      const uint32_t b0 = c[d], e = c[d + 1];
-      for (uint32_t i = b0 + 1; i < e; ++i) {
-        const PT x = bb[i];
-        uint32_t j = i;
-        while (j > b0 && bb[j - 1] > x) {
-          bb[j] = bb[j - 1];
-          --j;
-        }
-        bb[j] = x;
-      }
-    }
+  if (lo == 0) {  // equal digits are equal payloads: bb is sorted
+    for (uint32_t i = threadIdx.x; i < cnt; i += SB) OUT[s + i] = prefix | (KT)bb[i];
     srt_lds_sync();
+    return;
   }
-  for (uint32_t i = threadIdx.x; i < cnt; i += SB) OUT[s + i] = prefix | (KT)bb[i];
+#pragma unroll
+  for (int k = 0; k < SE; ++k) {
+    const uint32_t i = (uint32_t)k * SB + threadIdx.x;
+    if (i < cnt) {
+      const uint32_t p = g0[k] + r[k];
+      uint32_t at = g0[k];
+      for (uint32_t j = g0[k]; j < g1[k]; ++j) {
+        const PT y = bb[j];
+        at += (y < w[k] || (y == w[k] && j < p)) ? 1u : 0u;
+      }
+      ob[at] = w[k];
+    }
+  }
+  srt_lds_sync();
+  for (uint32_t i = threadIdx.x; i < cnt; i += SB) OUT[s + i] = prefix | (KT)ob[i];
   srt_lds_sync();
 }
 
@@ -627,7 +663,7 @@ template <typename PT, typename KT>
 __global__ __launch_bounds__(SB) void k_srt_final(const SrtRefs a, const SrtParent* __restrict__ par,
                                                  const uint32_t* __restrict__ hist2, const PT* __restrict__ X1,
                                                  const PT* __restrict__ Y, KT* __restrict__ OUT, SrtDeep dp) {
-  __shared__ PT bb[SCAP];
+  __shared__ PT bb[SCAP], ob[SCAP];
   __shared__ uint32_t c[SCAP + 1], bnd[SB + 1], wsum[SB / 64];
   const uint32_t p = blockIdx.y;
   const SrtParent P = par[p];
@@ -647,7 +683,7 @@ __global__ __launch_bounds__(SB) void k_srt_final(const SrtRefs a, const SrtPare
     }
     PT w[SE];
     srt_item_load(X1, P.start, P.count, w);
-    srt_item_sort<PT, KT>(w, P.start, P.count, hi1, prefix, OUT, bb, c, wsum);
+    srt_item_sort<PT, KT>(w, P.start, P.count, hi1, prefix, OUT, bb, ob, c, wsum);
     return;
   }
   const uint32_t nc = 1u << P.d2, hi = hi1 - P.d2;
@@ -672,7 +708,7 @@ __global__ __launch_bounds__(SB) void k_srt_final(const SrtRefs a, const SrtPare
     const uint32_t dl = dn < nc ? dn : d;  // no next child: a harmless reload (the loads stay unconditional)
     PT wn[SE];
     srt_item_load(Y, bnd[dl], bnd[dl + 1] - bnd[dl], wn);
-    srt_item_sort<PT, KT>(w, bnd[d], bnd[d + 1] - bnd[d], hi, prefix, OUT, bb, c, wsum);
+    srt_item_sort<PT, KT>(w, bnd[d], bnd[d + 1] - bnd[d], hi, prefix, OUT, bb, ob, c, wsum);
 #pragma unroll
     for (int k = 0; k < SE; ++k) w[k] = wn[k];
     d = dn;
