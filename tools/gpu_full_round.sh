@@ -12,7 +12,7 @@ echo "== smoke" && timeout -k 10 300 python -c "import __graft_entry__ as g; g.s
 && echo "== bench" && timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" && python -c "
 import json; d=json.loads(open('$OUT/bench.json').read().strip().splitlines()[-1]); print(d['value'], d['roofline']['frac'], d['roofline']['traffic']); print(json.dumps(d['faithful_config3'])); print(json.dumps(d['cpu_baseline']))" \
 && echo "== trace" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 > "$OUT/prof.log" 2>&1 \
-&& python tools/stats_summary.py "$OUT/prof/run_kernel_stats.csv" | head -30
+&& python tools/stats_summary.py "$OUT/prof/run_kernel_stats.csv" > "$OUT/stats.txt" && sed -n 1,30p "$OUT/stats.txt"
 [ $? -eq 0 ] && echo "== config2/config4 bench lines" \
 && timeout -k 10 300 python bench.py --config config2 --no-extras --no-cpu-baseline > "$OUT/bench_config2.json" 2>> "$OUT/bench.err" \
 && timeout -k 10 300 python bench.py --config config4 --no-extras --no-cpu-baseline > "$OUT/bench_config4.json" 2>> "$OUT/bench.err" \
