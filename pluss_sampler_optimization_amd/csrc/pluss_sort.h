@@ -570,10 +570,23 @@ __device__ __forceinline__ void srt_block_scan_lds(uint32_t* v, uint32_t len, ui
 #pragma unroll
   for (int x = 0; x < SB / 64; ++x) pre += x < (int)wid ? wsum[x] : 0u;
   uint32_t run = pre + inc - sum;
+  if ((len & (4 * SB - 1)) == 0) {  // 16-byte writes too
 #pragma unroll
-  for (uint32_t k = 0; k < 16; ++k) {
-    if (k < per && b + k < len) v[b + k] = run;
-    run += loc[k];
+    for (uint32_t k = 0; k < 16; k += 4) {
+      uint4 q;
+      q.x = run;
+      q.y = q.x + loc[k];
+      q.z = q.y + loc[k + 1];
+      q.w = q.z + loc[k + 2];
+      run = q.w + loc[k + 3];
+      if (k < per) *reinterpret_cast<uint4*>(v + b + k) = q;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) {
+      if (k < per && b + k < len) v[b + k] = run;
+      run += loc[k];
+    }
   }
   srt_lds_sync();
 }
@@ -663,8 +676,12 @@ template <typename PT, typename KT>
 __global__ __launch_bounds__(SB) void k_srt_final(const SrtRefs a, const SrtParent* __restrict__ par,
                                                  const uint32_t* __restrict__ hist2, const PT* __restrict__ X1,
                                                  const PT* __restrict__ Y, KT* __restrict__ OUT, SrtDeep dp) {
-  __shared__ PT bb[SCAP], ob[SCAP];
+  // ob, the ranked payloads, reuses the counters once each payload holds its
+  // group bounds in registers (4-byte payloads; 8-byte ones get their own)
+  constexpr bool OB_IN_C = sizeof(PT) == sizeof(uint32_t);
+  __shared__ PT bb[SCAP], obx[OB_IN_C ? 1 : SCAP];
   __shared__ uint32_t c[SCAP + 1], bnd[SB + 1], wsum[SB / 64];
+  PT* ob = OB_IN_C ? reinterpret_cast<PT*>(c) : obx;
   const uint32_t p = blockIdx.y;
   const SrtParent P = par[p];
   const uint32_t hi1 = a.wb - a.d1[P.ref];
@@ -691,27 +708,16 @@ __global__ __launch_bounds__(SB) void k_srt_final(const SrtRefs a, const SrtPare
   for (uint32_t i = threadIdx.x; i <= nc; i += SB)
     bnd[i] = i < nc ? P.start + hist2[P.h2off + i * P.nc2] - base : P.start + P.count;
   __syncthreads();
-  auto next = [&](uint32_t d) {  // the next child of this workgroup to sort here (pushing deep ones)
-    for (; d < nc; d += FG) {
-      const uint32_t cnt = bnd[d + 1] - bnd[d];
-      if (cnt == 0) continue;
-      if (cnt <= SCAP) break;
-      deep(bnd[d], cnt, hi, 1);
+  for (uint32_t d = blockIdx.x; d < nc; d += FG) {  // this workgroup's children
+    const uint32_t s = bnd[d], cnt = bnd[d + 1] - s;
+    if (cnt == 0) continue;
+    if (cnt > SCAP) {
+      deep(s, cnt, hi, 1);
+      continue;
     }
-    return d;
-  };
-  uint32_t d = next(blockIdx.x);
-  PT w[SE];
-  if (d < nc) srt_item_load(Y, bnd[d], bnd[d + 1] - bnd[d], w);
-  while (d < nc) {
-    const uint32_t dn = next(d + FG);
-    const uint32_t dl = dn < nc ? dn : d;  // no next child: a harmless reload (the loads stay unconditional)
-    PT wn[SE];
-    srt_item_load(Y, bnd[dl], bnd[dl + 1] - bnd[dl], wn);
-    srt_item_sort<PT, KT>(w, bnd[d], bnd[d + 1] - bnd[d], hi, prefix, OUT, bb, ob, c, wsum);
-#pragma unroll
-    for (int k = 0; k < SE; ++k) w[k] = wn[k];
-    d = dn;
+    PT w[SE];
+    srt_item_load(Y, s, cnt, w);
+    srt_item_sort<PT, KT>(w, s, cnt, hi, prefix, OUT, bb, ob, c, wsum);
   }
 }
 
