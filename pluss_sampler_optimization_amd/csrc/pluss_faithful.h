@@ -1138,7 +1138,7 @@ __global__ __launch_bounds__(TB) void k_fa_local(Model m, FaRefs a, unsigned lon
 // The fast path over every tile (shapes with FaRefs::fast); the tiles it
 // cannot take are queued in slowq for k_fa_local.
 template <int SRC, bool CHECK>
-__global__ __launch_bounds__(TB) void k_fa_local_fast(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4))) void k_fa_local_fast(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
                                                       unsigned long long* __restrict__ part,
                                                       unsigned long long* __restrict__ klist,
                                                       unsigned long long* slots, unsigned int* slowq, GTable g) {
