@@ -484,6 +484,47 @@ def faithful_sharded_bench(P, torch, dist, device, stream, world, reps=3):
                     f"{reps}, max over ranks"}
 
 
+def capi_group_bench(P, torch, dist, cfg, counts, total, world, rank, backend, steps, warmup):
+    """The same dense step through the C ABI's multi-GPU group (pluss_group_*,
+    csrc/pluss_group.hip): the library holds the shards' resident lists, runs
+    the count and the RCCL all-reduce of the 19-word vector itself (one local
+    device: replayed from HIP graphs of 16 steps) -- what a C++ or Rust caller
+    of the reference gets without torch.  N>1: one rank per process, the RCCL
+    id made by rank 0 and handed over by torch.distributed.  N=1 also runs 8
+    logical shards on the one GPU (SURVEY §4.4's exchange rehearsal: not a
+    scaling point)."""
+    def run(g, label):
+        g.expand(SEED, counts)
+        g.dense(warmup)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        v = g.dense(steps)
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=torch.device("cuda", cfg.device))
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        ok = sum(v[:P.DENSE_BINS]) == total and v[P.DENSE_BINS] == 0
+        return {"shards": g.shards()[1], "ms_per_step": el / steps * 1e3, "value": total * steps / el,
+                "unit": "sampled accesses/s", "merged_vector_accounts_for_every_sample": bool(ok), "label": label}
+    if world > 1:
+        if backend != "nccl":
+            return {"skipped": "the group's RCCL communicator needs one GPU per rank (gloo rehearsal)"}
+        obj = [P.group_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        with P.Group.rank(cfg, world, rank, obj[0]) as g:
+            out = run(g, f"{world} ranks x 1 shard")
+    else:
+        with P.Group(cfg, [cfg.device], 1) as g:
+            out = run(g, "1 device x 1 shard")
+        with P.Group(cfg, [cfg.device], 8) as g:
+            out["logical_shards_8"] = run(g, "1 device x 8 logical shards (rehearsal)")
+    out["note"] = ("host clock around pluss_group_dense(K) (K passes, each a count launch per shard, the per-device "
+                   "sum and one RCCL all-reduce, until the merged vector is back on the host)")
+    return out
+
+
 def pmc_traffic(samples_per_launch):
     """Per-launch HBM bytes of the hot kernel from the committed rocprofv3 --pmc
     summary, if it was taken at this launch size (tools/prof_round.sh)."""
@@ -657,6 +698,13 @@ def main():
     collective_info = None
     if collective:
         collective_info = collective_costs(args, torch, dist, ctx, samples, n_local, dense, stream)
+    capi_group = None
+    if not args.no_extras:
+        try:  # a side line: its failure must not cost the headline line
+            capi_group = capi_group_bench(P, torch, dist, cfg, counts, total, world, rank, args.backend,
+                                          args.steps, args.warmup)
+        except Exception as e:  # noqa: BLE001
+            capi_group = {"error": repr(e)}
     faithful_shards = None
     if world > 1 and not args.no_extras:
         try:  # a side line: its failure must not cost the headline line
@@ -707,6 +755,8 @@ def main():
         result["collective"] = collective_info
     if faithful_shards is not None:
         result["faithful_sharded"] = faithful_shards
+    if capi_group is not None:
+        result["capi_group"] = capi_group
     if not args.no_extras:
         result["end_to_end"] = end_to_end_bench(P, torch, cfg, counts, parts, stream)
     if rank == 0 and not args.no_extras:

@@ -50,6 +50,7 @@ enum { PLUSS_THR_R10 = 0, PLUSS_THR_V1 = 1 };
 #define PLUSS_ERR_ALLOC (-3)    /* device/host allocation failed */
 #define PLUSS_ERR_CAPACITY (-4) /* output or histogram table too small */
 #define PLUSS_ERR_INPUT (-5)    /* malformed sample (ref > 5 or index >= N, wrong ref) */
+#define PLUSS_ERR_PEER (-6)     /* another shard or rank of a multi-GPU pass failed */
 
 typedef struct pluss_cfg {
   int64_t n;           /* loop bound N of the GEMM nest (reference: literal 128) */
@@ -185,75 +186,110 @@ int pluss_dev_gen_count_dense(pluss_ctx *ctx, uint64_t seed, const uint64_t tota
                               const uint64_t n[6], uint64_t *d_counts, void *stream);
 
 /* --- faithful mode over key-range shards (multi-GPU) ----------------------
-   One r10 sampler_<REF> (r10:135-696 and its five twins) split over ranks by
-   contiguous ranges of its sort key a*T+tid (pluss_utils.h:175-267 order).
-   Every rank passes the WHOLE per-reference sample list; each keeps the
-   samples whose key lies in its [key_lo, key_hi) and sorts only those.  The
-   library holds no communicator: between phases the caller exchanges the
-   small pluss_faith_shard summaries of all ranks (one all-gather each):
+   r10's sampler_<REF> is one sequential pass over the whole key-ordered list
+   (r10:187-695); the six references split over shards by contiguous ranges of
+   the sort key a*T+tid (IterationComp order, pluss_utils.h:175-267), one shard
+   per GPU (or several logical shards per GPU).  Each phase writes this shard's
+   summary row (PLUSS_SHARD_ROW u64 words, device memory) and the next phase
+   reads the rows of ALL shards, gathered by the caller in shard order (one
+   all-gather between phases, e.g. ncclAllGather in place; the group API below
+   does it itself).  No phase returns anything to the host, so with device
+   all-gathers the pass runs without a host round trip (the selected source
+   makes one, in local_selected).  The phases, on one handle per shard:
 
-     1 keys    -> n, first_key, max_sink
-                  j_off   = sum of n over earlier ranks, n_total = sum of all n,
-                  pmax_in = max of max_sink over earlier ranks with n > 0 (0 if none)
-     2 starts  -> n_starts;  s_off = sum of n_starts over earlier ranks
-     3 cut     -> cut;       cut = min over ranks
-     4 hist    (next_first_key = first_key of the next rank with n > 0, ~0 if
-                none; is_last = no later rank has n > 0) accumulates this
-                shard's part into the handle's histogram; then export and merge
-                the tables like clean mode.  The merged histogram and the sum of
-                `traversed` equal one pluss_dev_faithful_hist over the list.
-   Needs N % (chunk*threads) == 0 like pluss_dev_faithful_hist.             */
-typedef struct pluss_faith_shard {
-  uint64_t n;         /* phase 1: samples whose key is in [key_lo, key_hi) */
-  uint64_t first_key; /* phase 1: smallest key (~0 if n == 0) */
-  uint64_t max_sink;  /* phase 1: largest sink key (~0 if one is cold, 0 if n == 0) */
-  uint64_t n_starts;  /* phase 2: replay starts in this shard */
-  uint64_t cut;       /* phase 3: first Q1 cut candidate (global index), n_total if none */
-} pluss_faith_shard;
+     1. pluss_dev_faithful_shards_local: this shard's slices -- n[r] samples of
+        reference r from index first[r] of its key-ordered list of totals[r]
+        samples: d_samples (the slices back to back) or, d_samples == NULL,
+        generated (pluss_expand_sorted's lists, seed);
+        or, for lists in ANY order, pluss_dev_faithful_shards_select (every
+        shard passes the whole lists and keeps its key range [key_lo, key_hi)),
+        then, after an all-gather, pluss_dev_faithful_shards_local_selected;
+     2. pluss_dev_faithful_shards_carry   (the replay state entering the shard)
+     3. pluss_dev_faithful_shards_cut     (r10's Q1 exit over all shards)
+     4. pluss_dev_faithful_shards_hist    adds this shard's part of the
+        histograms and traversed to the handle; the shards' tables are then
+        summed (e.g. all-gather the exports) -- equal to one GPU's pass.
+   A shard that fails a phase still takes part in every all-gather with
+   row[PLUSS_SHARD_ROW_ERR] != 0; every shard then reports "a key-range shard
+   failed" (PLUSS_ERR_PEER) at its next fetch instead of waiting forever.
+   The row words (u64): [0,6) samples per reference, [6,12) largest sink,
+   [12,18) replay starts, [18,24) first Q1 cut candidate, [31] error.
+   Needs N % (chunk*threads) == 0 and N % (cls/ds) == 0. */
+#define PLUSS_SHARD_ROW 32
+#define PLUSS_SHARD_ROW_ERR 31
 
 /* keys of this shape lie in [0, *key_end) (= accesses per thread * threads) */
 int pluss_faithful_key_space(const pluss_cfg *cfg, uint64_t *key_end);
 
-/* Faithful mode over key-range shards, all six references at once, on the
-   single-read scan pipeline (multi-GPU: one shard per rank; the shards of a
-   reference partition its list in key order).  r10's sampler_<REF> is one
-   sequential pass over the whole list (r10:187-695); the caller exchanges
-   three per-reference summaries between the four phases:
-     1. local: this shard's slices -- n[r] samples of reference r from index
-        first[r] of its list of totals[r] samples: d_samples (key-ordered,
-        reference blocks back to back) or, d_samples == NULL, generated
-        (pluss_expand_sorted's lists, seed); out: the largest sink per
-        reference (0: none);
-     2. carry: carry_in[r] = the largest sink of the earlier shards (max of
-        their phase-1 outputs); out: this shard's replay-start counts;
-     3. cut: starts_before[r] = the earlier shards' start counts summed; out:
-        this shard's first Q1 cut candidate (global index; totals[r]: none);
-     4. hist: cut[r] = the smallest candidate over all shards; is_last[r] =
-        this is the last shard with samples of reference r: this shard's part
-        of the histograms and traversed is added to the handle (the tables of
-        the shards are then summed, e.g. by all-gathering the exports).
-   Needs N % (chunk*threads) == 0 and N % (cls/ds) == 0. */
 int pluss_dev_faithful_shards_local(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t seed, const uint64_t *totals,
-                                    const uint64_t *first, const uint64_t *n, uint64_t *max_sink, void *stream);
-int pluss_dev_faithful_shards_carry(pluss_ctx *ctx, const uint64_t *carry_in, uint64_t *starts, void *stream);
-int pluss_dev_faithful_shards_cut(pluss_ctx *ctx, const uint64_t *starts_before, uint64_t *cut, void *stream);
-int pluss_dev_faithful_shards_hist(pluss_ctx *ctx, const uint64_t *cut, const int32_t *is_last, void *stream);
+                                    const uint64_t *first, const uint64_t *n, uint64_t *d_row, void *stream);
+int pluss_dev_faithful_shards_select(pluss_ctx *ctx, const uint64_t *d_lists, const uint64_t *totals, uint64_t key_lo,
+                                     uint64_t key_hi, uint64_t *d_row, void *stream);
+int pluss_dev_faithful_shards_local_selected(pluss_ctx *ctx, const uint64_t *d_rows, int32_t shard, int32_t nshards,
+                                             uint64_t *d_row, void *stream);
+int pluss_dev_faithful_shards_carry(pluss_ctx *ctx, const uint64_t *d_rows, int32_t shard, int32_t nshards,
+                                    uint64_t *d_row, void *stream);
+int pluss_dev_faithful_shards_cut(pluss_ctx *ctx, const uint64_t *d_rows, int32_t shard, int32_t nshards,
+                                  uint64_t *d_row, void *stream);
+int pluss_dev_faithful_shards_hist(pluss_ctx *ctx, const uint64_t *d_rows, int32_t shard, int32_t nshards,
+                                   void *stream);
 
 /* Host only (no device): [*i_lo, *i_hi) = the indices of the samples of the
    key-order list of `total` samples of reference `ref` (pluss_expand_sorted's
    list) whose faithful keys lie in [key_lo, key_hi) -- the list is in key
    order, so two binary searches of the host generator.  A key-range shard of
-   faithful mode generates exactly that slice (dist.sharded_faithful_gen_hist). */
+   faithful mode generates exactly that slice. */
 int pluss_keyorder_index_range(const pluss_cfg *cfg, uint64_t seed, int32_t ref, uint64_t total, uint64_t key_lo,
                                uint64_t key_hi, uint64_t *i_lo, uint64_t *i_hi);
-int pluss_dev_faithful_shard_keys(pluss_ctx *ctx, int32_t ref, const uint64_t *d_samples, uint64_t n,
-                                  uint64_t key_lo, uint64_t key_hi, pluss_faith_shard *out, void *stream);
-int pluss_dev_faithful_shard_starts(pluss_ctx *ctx, uint64_t j_off, uint64_t pmax_in, pluss_faith_shard *out,
-                                    void *stream);
-int pluss_dev_faithful_shard_cut(pluss_ctx *ctx, uint64_t s_off, uint64_t n_total, pluss_faith_shard *out,
-                                 void *stream);
-int pluss_dev_faithful_shard_hist(pluss_ctx *ctx, uint64_t cut, uint64_t next_first_key, int32_t is_last,
-                                  void *stream);
+
+/* --- multi-GPU groups ------------------------------------------------------
+   The reference's callers run the six sampler_<REF> of r10 on host threads
+   and merge (r10:3191-3278; Rust src/main.rs:17-44); a group runs one pass
+   over every GPU of a node instead, and returns the merged histogram.  A
+   group is a set of shards: shards_per_device >= 1 logical shards on each
+   device (e.g. 8 on one device reproduce an 8-GPU job's partition and
+   exchanges).  The exchanges are RCCL collectives over the
+   devices (loaded on first use): one all-reduce of the dense vector per
+   clean pass, one all-gather of the shards' summary rows between the phases
+   of a faithful pass (no host round trip), one all-gather of the canonical
+   tables at the end.  Clean mode shards every reference's sample index range
+   (or a host list) into contiguous slices; faithful mode shards the sort key
+   a*T+tid into contiguous ranges.  Results equal one device's and are the
+   same on every rank.
+     pluss_group_create       one process, `ndev` distinct devices (ranks 0..ndev-1)
+     pluss_group_create_rank  one process of a multi-process job (one device,
+                              cfg->device; rank `rank` of `nranks`): rank 0
+                              makes the id with pluss_group_unique_id and the
+                              caller hands it to every rank (MPI, a file, ...)
+     pluss_group_sampled_hist a host list (every rank passes the same list):
+                              clean: slices counted and merged; faithful: the
+                              six samplers over the list's per-reference
+                              samples (any order), key-range sharded
+     pluss_group_gen_faithful the six samplers over generated key-order lists
+                              (pluss_expand_sorted's), each shard generating
+                              only its key range
+     pluss_group_expand       resident Feistel lists, each shard its slices of
+                              counts[r] samples per reference (pluss_expand_samples)
+     pluss_group_dense        `passes` dense passes over them (the bench step;
+                              one local device: replayed from HIP graphs); out:
+                              the last pass's merged dense vector (as
+                              pluss_dev_sampled_hist_dense)
+     pluss_group_gen_count_dense  generated key-order slices counted and merged */
+typedef struct pluss_group pluss_group;
+#define PLUSS_GROUP_ID_BYTES 128
+int pluss_group_unique_id(uint8_t id[PLUSS_GROUP_ID_BYTES]);
+int pluss_group_create(const pluss_cfg *cfg, const int32_t *devices, int32_t ndev, int32_t shards_per_device,
+                       pluss_group **out);
+int pluss_group_create_rank(const pluss_cfg *cfg, int32_t nranks, int32_t rank, const uint8_t id[PLUSS_GROUP_ID_BYTES],
+                            int32_t shards_per_device, pluss_group **out);
+int pluss_group_destroy(pluss_group *group);
+int pluss_group_shards(const pluss_group *group, int32_t *local_shards, int32_t *total_shards);
+int pluss_group_sampled_hist(pluss_group *group, const uint64_t *samples, uint64_t n, pluss_hist *out);
+int pluss_group_gen_faithful(pluss_group *group, uint64_t seed, const uint64_t totals[6], pluss_hist *out);
+int pluss_group_expand(pluss_group *group, uint64_t seed, const uint64_t counts[6]);
+int pluss_group_dense(pluss_group *group, uint32_t passes, uint64_t counts[PLUSS_DENSE_BINS + 1]);
+int pluss_group_gen_count_dense(pluss_group *group, uint64_t seed, const uint64_t totals[6],
+                                uint64_t counts[PLUSS_DENSE_BINS + 1]);
 
 /* synchronise and copy the handle's histogram into a host pluss_hist */
 int pluss_hist_fetch(pluss_ctx *ctx, pluss_hist *out);

@@ -13,7 +13,10 @@ LIB_PATH = os.path.join(HERE, "lib", "libpluss_gpu.so")
 PLUSS_OK = 0
 DENSE_BINS = 18  # PLUSS_DENSE_BINS; a dense count vector holds DENSE_BINS + 1 words (the last: malformed samples)
 ERRORS = {-1: "PLUSS_ERR_CONFIG", -2: "PLUSS_ERR_HIP", -3: "PLUSS_ERR_ALLOC", -4: "PLUSS_ERR_CAPACITY",
-          -5: "PLUSS_ERR_INPUT"}
+          -5: "PLUSS_ERR_INPUT", -6: "PLUSS_ERR_PEER"}
+SHARD_ROW = 32      # PLUSS_SHARD_ROW: u64 words of a key-range shard's summary row
+SHARD_ROW_ERR = 31  # PLUSS_SHARD_ROW_ERR
+GROUP_ID_BYTES = 128
 
 # every symbol declared in include/pluss_gpu.h
 EXPORTS = [
@@ -25,11 +28,13 @@ EXPORTS = [
     "pluss_dev_faithful_hist_sorted", "pluss_dev_faithful_hist_sorted_refs", "pluss_dev_gen_faithful_refs",
     "pluss_dev_fulltrace_hist", "pluss_dev_sampled_ri",
     "pluss_dev_hist_export", "pluss_dev_hist_export_reset", "pluss_dev_sampled_hist_export", "pluss_hist_fetch",
-    "pluss_hist_from_tables", "pluss_faithful_key_space", "pluss_keyorder_index_range", "pluss_dev_faithful_shard_keys",
-    "pluss_dev_faithful_shard_starts", "pluss_dev_faithful_shard_cut", "pluss_dev_faithful_shard_hist",
+    "pluss_hist_from_tables", "pluss_faithful_key_space", "pluss_keyorder_index_range",
     "pluss_dense_keys", "pluss_dev_sampled_hist_dense", "pluss_dev_gen_count_dense",
-    "pluss_dev_faithful_shards_local", "pluss_dev_faithful_shards_carry", "pluss_dev_faithful_shards_cut",
-    "pluss_dev_faithful_shards_hist",
+    "pluss_dev_faithful_shards_local", "pluss_dev_faithful_shards_select", "pluss_dev_faithful_shards_local_selected",
+    "pluss_dev_faithful_shards_carry", "pluss_dev_faithful_shards_cut", "pluss_dev_faithful_shards_hist",
+    "pluss_group_unique_id", "pluss_group_create", "pluss_group_create_rank", "pluss_group_destroy",
+    "pluss_group_shards", "pluss_group_sampled_hist", "pluss_group_gen_faithful", "pluss_group_expand",
+    "pluss_group_dense", "pluss_group_gen_count_dense",
 ]
 # include/pluss_diag.h (diagnostics, not the drop-in boundary)
 DIAG_EXPORTS = ["pluss_diag_dense", "pluss_diag_sort_words"]
@@ -49,11 +54,6 @@ class PlussHistEntry(ctypes.Structure):
 class PlussHist(ctypes.Structure):
     _fields_ = [("entries", ctypes.POINTER(PlussHistEntry)), ("capacity", ctypes.c_uint64),
                 ("n_entries", ctypes.c_uint64), ("traversed", ctypes.c_uint64 * 6)]
-
-
-class PlussFaithShard(ctypes.Structure):
-    _fields_ = [("n", ctypes.c_uint64), ("first_key", ctypes.c_uint64), ("max_sink", ctypes.c_uint64),
-                ("n_starts", ctypes.c_uint64), ("cut", ctypes.c_uint64)]
 
 
 class PlussError(RuntimeError):
@@ -116,19 +116,27 @@ def lib():
         "pluss_hist_from_tables": (ctypes.c_int, [vp, vp, u64, histp]),
         "pluss_faithful_key_space": (ctypes.c_int, [cfgp, P(u64)]),
         "pluss_keyorder_index_range": (ctypes.c_int, [cfgp, u64, i32, u64, u64, u64, P(u64), P(u64)]),
-        "pluss_dev_faithful_shard_keys": (ctypes.c_int, [vp, i32, vp, u64, u64, u64, P(PlussFaithShard), vp]),
-        "pluss_dev_faithful_shard_starts": (ctypes.c_int, [vp, u64, u64, P(PlussFaithShard), vp]),
-        "pluss_dev_faithful_shard_cut": (ctypes.c_int, [vp, u64, u64, P(PlussFaithShard), vp]),
-        "pluss_dev_faithful_shard_hist": (ctypes.c_int, [vp, u64, u64, i32, vp]),
         "pluss_dense_keys": (ctypes.c_int, [cfgp, P(u64)]),
         "pluss_dev_sampled_hist_dense": (ctypes.c_int, [vp, vp, u64, vp, vp]),
         "pluss_dev_gen_count_dense": (ctypes.c_int, [vp, u64, P(u64), P(u64), P(u64), vp, vp]),
         "pluss_diag_dense": (ctypes.c_int, [vp, vp, u64, vp, i32, i32, vp]),
         "pluss_diag_sort_words": (ctypes.c_int, [vp, i32, vp, u64, vp, ctypes.POINTER(i32), vp]),
-        "pluss_dev_faithful_shards_local": (ctypes.c_int, [vp, vp, u64, P(u64), P(u64), P(u64), P(u64), vp]),
-        "pluss_dev_faithful_shards_carry": (ctypes.c_int, [vp, P(u64), P(u64), vp]),
-        "pluss_dev_faithful_shards_cut": (ctypes.c_int, [vp, P(u64), P(u64), vp]),
-        "pluss_dev_faithful_shards_hist": (ctypes.c_int, [vp, P(u64), P(i32), vp]),
+        "pluss_dev_faithful_shards_local": (ctypes.c_int, [vp, vp, u64, P(u64), P(u64), P(u64), vp, vp]),
+        "pluss_dev_faithful_shards_select": (ctypes.c_int, [vp, vp, P(u64), u64, u64, vp, vp]),
+        "pluss_dev_faithful_shards_local_selected": (ctypes.c_int, [vp, vp, i32, i32, vp, vp]),
+        "pluss_dev_faithful_shards_carry": (ctypes.c_int, [vp, vp, i32, i32, vp, vp]),
+        "pluss_dev_faithful_shards_cut": (ctypes.c_int, [vp, vp, i32, i32, vp, vp]),
+        "pluss_dev_faithful_shards_hist": (ctypes.c_int, [vp, vp, i32, i32, vp]),
+        "pluss_group_unique_id": (ctypes.c_int, [vp]),
+        "pluss_group_create": (ctypes.c_int, [cfgp, P(i32), i32, i32, P(vp)]),
+        "pluss_group_create_rank": (ctypes.c_int, [cfgp, i32, i32, vp, i32, P(vp)]),
+        "pluss_group_destroy": (ctypes.c_int, [vp]),
+        "pluss_group_shards": (ctypes.c_int, [vp, P(i32), P(i32)]),
+        "pluss_group_sampled_hist": (ctypes.c_int, [vp, vp, u64, histp]),
+        "pluss_group_gen_faithful": (ctypes.c_int, [vp, u64, P(u64), histp]),
+        "pluss_group_expand": (ctypes.c_int, [vp, u64, P(u64)]),
+        "pluss_group_dense": (ctypes.c_int, [vp, ctypes.c_uint32, P(u64)]),
+        "pluss_group_gen_count_dense": (ctypes.c_int, [vp, u64, P(u64), P(u64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

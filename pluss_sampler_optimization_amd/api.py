@@ -16,7 +16,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import DENSE_BINS, PlussCfg, PlussFaithShard, PlussHist, PlussHistEntry, check, lib
+from ._lib import DENSE_BINS, GROUP_ID_BYTES, PlussCfg, PlussHist, PlussHistEntry, check, lib
 
 REFS = ["C0", "C1", "A0", "B0", "C2", "C3"]
 REF_ID = {r: i for i, r in enumerate(REFS)}
@@ -364,69 +364,127 @@ class Context:
               "pluss_diag_sort_words")
         return int(wb.value)
 
-    # faithful mode over key-range shards: the four phases of
-    # pluss_dev_faithful_shard_* (the caller exchanges the summaries; see dist.py)
-    def faithful_shard_keys(self, ref, d_samples, n, key_lo, key_hi, stream=None):
-        """Phase 1 -> (n, first_key, max_sink) of the samples with key in [key_lo, key_hi)."""
-        rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
-        o = PlussFaithShard()
-        check(lib().pluss_dev_faithful_shard_keys(self._h, rid, d_samples, n, key_lo, key_hi, ctypes.byref(o), stream),
-              "pluss_dev_faithful_shard_keys")
-        return int(o.n), int(o.first_key), int(o.max_sink)
-
-    def faithful_shard_starts(self, j_off, pmax_in, stream=None):
-        """Phase 2 -> number of replay starts in this shard."""
-        o = PlussFaithShard()
-        check(lib().pluss_dev_faithful_shard_starts(self._h, j_off, pmax_in, ctypes.byref(o), stream),
-              "pluss_dev_faithful_shard_starts")
-        return int(o.n_starts)
-
-    def faithful_shard_cut(self, s_off, n_total, stream=None):
-        """Phase 3 -> this shard's first Q1 cut candidate (global index; n_total if none)."""
-        o = PlussFaithShard()
-        check(lib().pluss_dev_faithful_shard_cut(self._h, s_off, n_total, ctypes.byref(o), stream),
-              "pluss_dev_faithful_shard_cut")
-        return int(o.cut)
-
-    def faithful_shard_hist(self, cut, next_first_key, is_last, stream=None):
-        """Phase 4: accumulate this shard's part of the sampler's histogram."""
-        check(lib().pluss_dev_faithful_shard_hist(self._h, cut, next_first_key, 1 if is_last else 0, stream),
-              "pluss_dev_faithful_shard_hist")
-
     # faithful mode over key-range shards of the single-read pipeline, all six
-    # references at once (pluss_dev_faithful_shards_*; dist.sharded_faithful_gen_hist)
-    def faithful_shards_local(self, d_samples, seed, totals, first, n, stream=None):
-        """Phase 1 -> the largest sink of this shard per reference.  d_samples None: generated slices."""
+    # references at once (pluss_dev_faithful_shards_*; dist.py): every phase
+    # writes this shard's summary row (SHARD_ROW u64 at d_row, device memory)
+    # and the next reads the rows of all shards gathered at d_rows
+    def faithful_shards_local(self, d_samples, seed, totals, first, n, d_row, stream=None):
+        """Phase 1 over key-ordered slices (d_samples None: generated slices)."""
         u6 = ctypes.c_uint64 * 6
-        out = u6()
         check(lib().pluss_dev_faithful_shards_local(self._h, d_samples, seed, u6(*map(int, totals)),
-                                                    u6(*map(int, first)), u6(*map(int, n)), out, stream),
+                                                    u6(*map(int, first)), u6(*map(int, n)), d_row, stream),
               "pluss_dev_faithful_shards_local")
-        return [int(x) for x in out]
 
-    def faithful_shards_carry(self, carry_in, stream=None):
-        """Phase 2 -> this shard's replay-start counts per reference."""
+    def faithful_shards_select(self, d_lists, totals, key_lo, key_hi, d_row, stream=None):
+        """Arbitrary-order lists (the six references' whole lists back to back):
+        keep the samples whose keys lie in [key_lo, key_hi)."""
         u6 = ctypes.c_uint64 * 6
-        out = u6()
-        check(lib().pluss_dev_faithful_shards_carry(self._h, u6(*map(int, carry_in)), out, stream),
+        check(lib().pluss_dev_faithful_shards_select(self._h, d_lists, u6(*map(int, totals)), key_lo, key_hi, d_row,
+                                                     stream), "pluss_dev_faithful_shards_select")
+
+    def faithful_shards_local_selected(self, d_rows, shard, nshards, d_row, stream=None):
+        """Phase 1 over the selected samples (reads the gathered rows on the host once)."""
+        check(lib().pluss_dev_faithful_shards_local_selected(self._h, d_rows, shard, nshards, d_row, stream),
+              "pluss_dev_faithful_shards_local_selected")
+
+    def faithful_shards_carry(self, d_rows, shard, nshards, d_row, stream=None):
+        """Phase 2: the replay state entering this shard -> its replay-start counts."""
+        check(lib().pluss_dev_faithful_shards_carry(self._h, d_rows, shard, nshards, d_row, stream),
               "pluss_dev_faithful_shards_carry")
-        return [int(x) for x in out]
 
-    def faithful_shards_cut(self, starts_before, stream=None):
-        """Phase 3 -> this shard's first Q1 cut candidate per reference (global index; the list length: none)."""
-        u6 = ctypes.c_uint64 * 6
-        out = u6()
-        check(lib().pluss_dev_faithful_shards_cut(self._h, u6(*map(int, starts_before)), out, stream),
+    def faithful_shards_cut(self, d_rows, shard, nshards, d_row, stream=None):
+        """Phase 3: the starts before this shard -> its first Q1 cut candidates."""
+        check(lib().pluss_dev_faithful_shards_cut(self._h, d_rows, shard, nshards, d_row, stream),
               "pluss_dev_faithful_shards_cut")
-        return [int(x) for x in out]
 
-    def faithful_shards_hist(self, cut, is_last, stream=None):
-        """Phase 4: add this shard's part of the histograms (global cut per reference)."""
-        check(lib().pluss_dev_faithful_shards_hist(self._h, (ctypes.c_uint64 * 6)(*map(int, cut)),
-                                                   (ctypes.c_int32 * 6)(*[1 if x else 0 for x in is_last]), stream),
+    def faithful_shards_hist(self, d_rows, shard, nshards, stream=None):
+        """Phase 4: add this shard's part of the histograms (the global cut from the rows)."""
+        check(lib().pluss_dev_faithful_shards_hist(self._h, d_rows, shard, nshards, stream),
               "pluss_dev_faithful_shards_hist")
 
     def fetch(self):
         h, keep = _hist_buf()
         check(lib().pluss_hist_fetch(self._h, ctypes.byref(h)), "pluss_hist_fetch")
         return Histogram._from_c(h)
+
+
+def group_unique_id():
+    """A fresh RCCL id (bytes) for Group.rank(): made on one rank, handed to all."""
+    buf = (ctypes.c_uint8 * GROUP_ID_BYTES)()
+    check(lib().pluss_group_unique_id(buf), "pluss_group_unique_id")
+    return bytes(buf)
+
+
+class Group:
+    """pluss_group_*: one pass over several GPUs (or several logical shards of
+    one GPU) behind the C ABI, merged over RCCL; results equal one GPU's."""
+
+    def __init__(self, cfg, devices=(0,), shards_per_device=1, _h=None):
+        self.cfg = cfg
+        self._c = cfg.to_c()
+        self._h = ctypes.c_void_p()
+        if _h is not None:
+            self._h = _h
+            return
+        devs = (ctypes.c_int32 * len(devices))(*devices)
+        check(lib().pluss_group_create(ctypes.byref(self._c), devs, len(devices), shards_per_device,
+                                       ctypes.byref(self._h)), "pluss_group_create")
+
+    @classmethod
+    def rank(cls, cfg, nranks, rank, uid, shards_per_device=1):
+        """One process of a multi-process job (cfg.device: this rank's GPU)."""
+        h = ctypes.c_void_p()
+        c = cfg.to_c()
+        buf = (ctypes.c_uint8 * GROUP_ID_BYTES).from_buffer_copy(uid)
+        check(lib().pluss_group_create_rank(ctypes.byref(c), nranks, rank, buf, shards_per_device, ctypes.byref(h)),
+              "pluss_group_create_rank")
+        return cls(cfg, _h=h)
+
+    def close(self):
+        if self._h:
+            lib().pluss_group_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def shards(self):
+        a, b = ctypes.c_int32(), ctypes.c_int32()
+        check(lib().pluss_group_shards(self._h, ctypes.byref(a), ctypes.byref(b)), "pluss_group_shards")
+        return int(a.value), int(b.value)
+
+    def sampled_hist(self, samples):
+        s, p = _u64(samples)
+        h, keep = _hist_buf()
+        check(lib().pluss_group_sampled_hist(self._h, p, len(s), ctypes.byref(h)), "pluss_group_sampled_hist")
+        return Histogram._from_c(h)
+
+    def gen_faithful(self, seed, totals):
+        h, keep = _hist_buf()
+        check(lib().pluss_group_gen_faithful(self._h, seed, (ctypes.c_uint64 * 6)(*map(int, totals)), ctypes.byref(h)),
+              "pluss_group_gen_faithful")
+        return Histogram._from_c(h)
+
+    def expand(self, seed, counts):
+        check(lib().pluss_group_expand(self._h, seed, (ctypes.c_uint64 * 6)(*map(int, counts))), "pluss_group_expand")
+
+    def dense(self, passes=1):
+        """`passes` dense passes over the resident lists; the last pass's merged vector."""
+        out = (ctypes.c_uint64 * (DENSE_BINS + 1))()
+        check(lib().pluss_group_dense(self._h, passes, out), "pluss_group_dense")
+        return [int(x) for x in out]
+
+    def gen_count_dense(self, seed, totals):
+        out = (ctypes.c_uint64 * (DENSE_BINS + 1))()
+        check(lib().pluss_group_gen_count_dense(self._h, seed, (ctypes.c_uint64 * 6)(*map(int, totals)), out),
+              "pluss_group_gen_count_dense")
+        return [int(x) for x in out]

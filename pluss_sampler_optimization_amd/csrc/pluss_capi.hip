@@ -56,6 +56,19 @@ static int check_flags(pluss_ctx* ctx) {
     set_error("malformed sample: ref > 5, an index >= N, or a reference other than the one requested");
     return PLUSS_ERR_INPUT;
   }
+  if (f[0] & FLAG_SHARD) {
+    set_error("a key-range shard of this faithful pass failed (its summary row carried an error word)");
+    return PLUSS_ERR_PEER;
+  }
+  if (f[0] & FLAG_SORT) {
+    set_error("the bucket sort's plan exceeded its capacity (faithful radix source)");
+    return PLUSS_ERR_CAPACITY;
+  }
+  if (f[0] & FLAG_LOOKBACK) {
+    set_error("faithful pass stalled: a chunk's predecessor never published its running max (another kernel "
+              "holding the GPU?)");
+    return PLUSS_ERR_HIP;
+  }
   if (f[0]) {
     set_error("histogram table overflow (more distinct (ref,kind,RI) keys than the table holds)");
     return PLUSS_ERR_CAPACITY;
@@ -175,13 +188,13 @@ int pluss_ctx_destroy(pluss_ctx* c) {
                   c->fb.keys_s, c->fb.sinks_s, c->fb.pmax,      c->fb.nstart, c->fb.tmp,
                   c->fb.scal, c->fb.st, c->fb.dpart, c->fb.tmax, c->fb.pmin, c->fb.fslot,
                   c->fb.klist, c->fb.slowq, c->fb.cval, c->fb.crec, c->fb.cflag, c->fb.shrec,
-                  c->fb.sbuf};
+                  c->fb.xin,   c->fb.sbuf};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (const auto& f : c->fbr) {
     void* fr[] = {f.keys,  f.sinks, f.keys_s, f.sinks_s, f.pmax,  f.nstart, f.tmp,   f.scal,  f.st,
                   f.dpart, f.tmax,  f.pmin,   f.fslot,   f.klist, f.slowq,  f.cval,  f.crec,  f.cflag,
-                  f.shrec, f.sbuf};
+                  f.shrec, f.xin,  f.sbuf};
     for (void* p : fr)
       if (p) (void)hipFree(p);
   }
@@ -322,24 +335,39 @@ int pluss_faithful_key_space(const pluss_cfg* cfg, uint64_t* key_end) {
 }
 
 int pluss_dev_faithful_shards_local(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t seed, const uint64_t* totals,
-                                    const uint64_t* first, const uint64_t* n, uint64_t* max_sink, void* stream) {
-  if (!ctx || !totals || !first || !n || !max_sink) return PLUSS_ERR_CONFIG;
-  return faith_shards_local(ctx, d_samples, seed, totals, first, n, max_sink, pick(ctx, stream));
+                                    const uint64_t* first, const uint64_t* n, uint64_t* d_row, void* stream) {
+  if (!ctx || !totals || !first || !n || !d_row) return PLUSS_ERR_CONFIG;
+  return faith_shards_local(ctx, d_samples, seed, totals, first, n, d_row, pick(ctx, stream));
 }
 
-int pluss_dev_faithful_shards_carry(pluss_ctx* ctx, const uint64_t* carry_in, uint64_t* starts, void* stream) {
-  if (!ctx || !carry_in || !starts) return PLUSS_ERR_CONFIG;
-  return faith_shards_carry(ctx, carry_in, starts, pick(ctx, stream));
+int pluss_dev_faithful_shards_select(pluss_ctx* ctx, const uint64_t* d_lists, const uint64_t* totals, uint64_t key_lo,
+                                     uint64_t key_hi, uint64_t* d_row, void* stream) {
+  if (!ctx || !totals || !d_row || key_lo > key_hi) return PLUSS_ERR_CONFIG;
+  return faith_shards_select(ctx, d_lists, totals, key_lo, key_hi, d_row, pick(ctx, stream));
 }
 
-int pluss_dev_faithful_shards_cut(pluss_ctx* ctx, const uint64_t* starts_before, uint64_t* cut, void* stream) {
-  if (!ctx || !starts_before || !cut) return PLUSS_ERR_CONFIG;
-  return faith_shards_cut(ctx, starts_before, cut, pick(ctx, stream));
+int pluss_dev_faithful_shards_local_selected(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards,
+                                             uint64_t* d_row, void* stream) {
+  if (!ctx || !d_row) return PLUSS_ERR_CONFIG;
+  return faith_shards_local_selected(ctx, d_rows, shard, nshards, d_row, pick(ctx, stream));
 }
 
-int pluss_dev_faithful_shards_hist(pluss_ctx* ctx, const uint64_t* cut, const int32_t* is_last, void* stream) {
-  if (!ctx || !cut || !is_last) return PLUSS_ERR_CONFIG;
-  return faith_shards_hist(ctx, cut, is_last, pick(ctx, stream));
+int pluss_dev_faithful_shards_carry(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards,
+                                    uint64_t* d_row, void* stream) {
+  if (!ctx || !d_row) return PLUSS_ERR_CONFIG;
+  return faith_shards_carry(ctx, d_rows, shard, nshards, d_row, pick(ctx, stream));
+}
+
+int pluss_dev_faithful_shards_cut(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards,
+                                  uint64_t* d_row, void* stream) {
+  if (!ctx || !d_row) return PLUSS_ERR_CONFIG;
+  return faith_shards_cut(ctx, d_rows, shard, nshards, d_row, pick(ctx, stream));
+}
+
+int pluss_dev_faithful_shards_hist(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards,
+                                   void* stream) {
+  if (!ctx) return PLUSS_ERR_CONFIG;
+  return faith_shards_hist(ctx, d_rows, shard, nshards, pick(ctx, stream));
 }
 
 int pluss_keyorder_index_range(const pluss_cfg* cfg, uint64_t seed, int32_t ref, uint64_t total, uint64_t key_lo,
@@ -365,30 +393,6 @@ int pluss_keyorder_index_range(const pluss_cfg* cfg, uint64_t seed, int32_t ref,
   *i_lo = first_at_least(key_lo);
   *i_hi = first_at_least(key_hi);
   return PLUSS_OK;
-}
-
-int pluss_dev_faithful_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, uint64_t key_lo,
-                                  uint64_t key_hi, pluss_faith_shard* out, void* stream) {
-  if (!ctx || !out || (!d_samples && n) || ref < 0 || ref > 5 || key_lo > key_hi) return PLUSS_ERR_CONFIG;
-  return faith_shard_keys(ctx, ref, d_samples, n, key_lo, key_hi, out, pick(ctx, stream));
-}
-
-int pluss_dev_faithful_shard_starts(pluss_ctx* ctx, uint64_t j_off, uint64_t pmax_in, pluss_faith_shard* out,
-                                    void* stream) {
-  if (!ctx || !out) return PLUSS_ERR_CONFIG;
-  return faith_shard_starts(ctx, j_off, pmax_in, out, pick(ctx, stream));
-}
-
-int pluss_dev_faithful_shard_cut(pluss_ctx* ctx, uint64_t s_off, uint64_t n_total, pluss_faith_shard* out,
-                                 void* stream) {
-  if (!ctx || !out) return PLUSS_ERR_CONFIG;
-  return faith_shard_cut(ctx, s_off, n_total, out, pick(ctx, stream));
-}
-
-int pluss_dev_faithful_shard_hist(pluss_ctx* ctx, uint64_t cut, uint64_t next_first_key, int32_t is_last,
-                                  void* stream) {
-  if (!ctx) return PLUSS_ERR_CONFIG;
-  return faith_shard_hist(ctx, cut, next_first_key, is_last, pick(ctx, stream));
 }
 
 int pluss_hist_fetch(pluss_ctx* ctx, pluss_hist* out) {

@@ -72,13 +72,13 @@ __device__ __noinline__ unsigned long long g_slot(GTable g, uint64_t key) {
     }
     s = (s + 1) & (GCAP - 1);
   }
-  atomicOr(&g.flags[0], 1u);
+  atomicOr(&g.flags[0], FLAG_OVERFLOW);
   return ~0ull;
 }
 
 __device__ __forceinline__ void g_add(GTable g, uint64_t key, uint64_t cnt) {
   atomicOr(&g.flags[3], 1u);  // main table in use: k_export must scan it
-  if (!g_add_cap(g.keys, g.counts, GCAP, key, cnt)) atomicOr(&g.flags[0], 1u);
+  if (!g_add_cap(g.keys, g.counts, GCAP, key, cnt)) atomicOr(&g.flags[0], FLAG_OVERFLOW);
 }
 
 __device__ __forceinline__ void g_add_rep(GTable g, uint32_t rep, uint64_t key, uint64_t cnt) {

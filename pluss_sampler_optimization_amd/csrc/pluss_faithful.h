@@ -144,15 +144,38 @@ __host__ __device__ inline uint64_t fa_tiles(uint64_t n) { return (n + TILE - 1)
 enum : int { SRC_W32 = 0, SRC_W64 = 1, SRC_SAMPLES = 2, SRC_GEN = 3 };
 enum : int { FA_LOCAL = 0, FA_FULL = 1, FA_CUT = 2 };
 
+// A key-range shard's exchange (include/pluss_gpu.h, PLUSS_SHARD_ROW): every
+// phase writes words of this shard's summary row; the next phase reads the
+// rows of all shards (gathered by the caller) and k_fa_xchg derives this
+// shard's inputs into xin.
+enum : int {
+  ROW_N = 0,       // [6] samples of each reference in the shard (phase 1)
+  ROW_MAX = 6,     // [6] the shard's largest sink per reference (phase 1; 0: none)
+  ROW_STARTS = 12, // [6] replay starts in the shard (phase 2)
+  ROW_CUT = 18,    // [6] the shard's first Q1 cut candidate, global index (phase 3; the list length: none)
+  ROW_ERR = 31,    // nonzero: the shard failed a phase (set by the caller)
+  ROW_W = 32
+};
+enum : int {
+  XIN_CIN = 0,     // [6] the largest sink of the earlier shards with samples (0: none)
+  XIN_SOFF = 6,    // [6] the replay starts of the earlier shards
+  XIN_CUT = 12,    // [6] the global cut (the smallest candidate over the shards)
+  XIN_LAST = 18,   // [6] no later shard has samples of the reference
+  XIN_FAIL = 24,   // some shard's row carries an error word
+  XIN_W = 32
+};
+
 struct FaRefs {
   uint64_t n[6];
   uint64_t toff[7];    // first (global) tile of each reference; toff[6] = all tiles
   uint64_t coff[7];    // first chunk (CH tiles) of each reference; coff[6] = all chunks
-  // key-range shards (multi-GPU; one GPU: joff 0, ntot = n, cin 0, soff 0): the global
-  // index of this shard's element 0 in the reference's list, the list's length, the
-  // running max of sinks entering the shard, the starts before it
-  uint64_t joff[6], ntot[6], soff[6];
-  unsigned long long cin[6];
+  // key-range shards (multi-GPU; one GPU: joff 0, ntot = n, xin null): the global
+  // index of this shard's element 0 in the reference's list, the list's length;
+  // xin (device memory, k_fa_xchg from the gathered summary rows): the running
+  // max of sinks entering the shard, the starts before it, the global cut, the
+  // last-shard flags, a failed-shard flag (XIN_* below)
+  uint64_t joff[6], ntot[6];
+  const unsigned long long* xin;
   const void* src[6];  // SRC_W*: sorted packed words; SRC_SAMPLES: the key-ordered samples
   PkView pv[6];
   KeyGen kg[6];        // SRC_GEN
@@ -1234,14 +1257,14 @@ __global__ __launch_bounds__(CH) void k_fa_chunk(Model m, FaRefs a, const unsign
     __hip_atomic_store(&cflag[c], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (wid == 0) {
-    unsigned long long p = a.cin[r];  // what entered this shard (earlier shards' sinks)
+    unsigned long long p = a.xin ? a.xin[XIN_CIN + r] : 0ull;  // what entered this shard (earlier shards' sinks)
     for (int64_t hi = (int64_t)lc - 1; hi >= 0; hi -= 64) {
       const int64_t j = hi - (int64_t)lane;
       uint32_t spins = 0;
       while (__ballot(j >= 0 && __hip_atomic_load(&cflag[c0 + j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch)) {
         __builtin_amdgcn_s_sleep(2);
         if (++spins > (1u << 24)) {  // a predecessor never published: flag it and stop waiting
-          if (lane == 0) atomicOr(&g.flags[0], 2u);
+          if (lane == 0) atomicOr(&g.flags[0], FLAG_LOOKBACK);
           break;
         }
       }
@@ -1377,7 +1400,8 @@ __global__ __launch_bounds__(CH) void k_fa_finish(Model m, FaRefs a, const unsig
                                                   const unsigned long long* __restrict__ part,
                                                   const unsigned long long* __restrict__ crec,
                                                   const unsigned long long* __restrict__ slots,
-                                                  unsigned long long* __restrict__ shrec, GTable g) {
+                                                  unsigned long long* __restrict__ shrec,
+                                                  unsigned long long* __restrict__ row, GTable g) {
   constexpr int NW = CH / 64;
   __shared__ FaLds<SRC, TB, TI> sh;
   __shared__ unsigned long long sw[NW], s_best, s_cin, s_red[NW][FPART];
@@ -1391,7 +1415,7 @@ __global__ __launch_bounds__(CH) void k_fa_finish(Model m, FaRefs a, const unsig
   const unsigned long long gl = tmax[t0 + nt - 1] > pmin[t0 + nt - 1] ? tmax[t0 + nt - 1] : pmin[t0 + nt - 1];
   unsigned long long v[FPART] = {0, 0, 0, 0, 0};  // this thread's sums: cold, traversed, case 0/1/2
   // 1. the cut chunk (blocks of CH chunks); run: starts before (earlier shards' included)
-  uint64_t run = a.soff[r], cc = nc, ccin = 0;
+  uint64_t run = a.xin ? a.xin[XIN_SOFF + r] : 0ull, cc = nc, ccin = 0;
   for (uint64_t b0 = 0; b0 < nc && cc == nc; b0 += CH) {
     const uint64_t i = b0 + threadIdx.x;
     const bool ok = i < nc;
@@ -1490,7 +1514,9 @@ __global__ __launch_bounds__(CH) void k_fa_finish(Model m, FaRefs a, const unsig
       if (ct < nt) x += sh.out[f];
       shrec[r * SRW + f] = x;
     } else if (threadIdx.x == FPART) {
-      shrec[r * SRW + FPART] = ct < nt ? sh.out[FPART] : n;
+      const unsigned long long cand = ct < nt ? sh.out[FPART] : n;
+      shrec[r * SRW + FPART] = cand;
+      row[ROW_CUT + r] = cand;  // phase 3's summary word
     } else if (threadIdx.x == FPART + 1) {
       shrec[r * SRW + FPART + 1] = gl;
     }
@@ -1518,24 +1544,26 @@ __global__ __launch_bounds__(CH) void k_fa_finish(Model m, FaRefs a, const unsig
   }
 }
 // pass 4 of a key-range shard: with the global cut of each reference (the
-// smallest candidate over the shards), record this shard's part: nothing if
-// the cut lies before it; its sums below the cut if it holds the cut; all of
-// it otherwise, and, on the list's last shard with nothing cut, Q3 and the end
-// of the last replay (as k_fa_finish does on one GPU).
-struct FaShardCut {
-  uint64_t cut[6];  // the global cut of each reference (its list's length: none)
-  int32_t last[6];  // this shard is the reference's last with samples
-};
+// smallest candidate over the shards, xin), record this shard's part: nothing
+// if the cut lies before it; its sums below the cut if it holds the cut; all
+// of it otherwise, and, on the list's last shard with nothing cut, Q3 and the
+// end of the last replay (as k_fa_finish does on one GPU).  Nothing is
+// recorded when a shard failed (the pass reports the failure at the fetch).
 template <int X = 0>  // (a template: instantiated only where launched)
-__global__ void k_fa_shard_apply(Model m, FaRefs a, const unsigned long long* __restrict__ shrec, FaShardCut c,
+__global__ void k_fa_shard_apply(Model m, FaRefs a, const unsigned long long* __restrict__ shrec,
+                                 const unsigned long long* __restrict__ xin,
                                  const unsigned long long* __restrict__ slots, GTable g) {
   const uint32_t r = threadIdx.x;
-  if (r >= 6 || a.n[r] == 0) return;
+  if (r >= 6 || a.n[r] == 0 || xin[XIN_FAIL]) return;
   const unsigned long long* sr = shrec + r * SRW;
-  const uint64_t G = c.cut[r], start = a.joff[r], n = a.ntot[r];
+  const uint64_t G = xin[XIN_CUT + r], start = a.joff[r], n = a.ntot[r];
+  if (G > n) {  // the gathered rows disagree with this shard's list length
+    atomicOr(&g.flags[0], FLAG_SHARD);
+    return;
+  }
   if (G < start) return;  // dropped by Q1 in an earlier shard
   unsigned long long cold = sr[0], trav = sr[1];
-  if (G == n && c.last[r]) {
+  if (G == n && xin[XIN_LAST + r]) {
     const unsigned long long gl = sr[FPART + 1];
     if (gl != KEY_EMPTY && gl % m.T == 0) cold += 1;
     trav += gl == KEY_EMPTY ? m.A * m.T : gl;
@@ -1546,23 +1574,76 @@ __global__ void k_fa_shard_apply(Model m, FaRefs a, const unsigned long long* __
     if (sr[2 + c]) atomicAdd(&g.bins[r * 3 + c], sr[2 + c]);
 }
 
-// per reference: the largest of its tiles' sinks (max_out[r]) and the sum of
-// its chunks' start counts (starts_out[r]); either pointer may be null
+// phase 1's summary row: every word's default (no starts, no cut candidate:
+// the list's length), then per reference its sample count and the largest of
+// its tiles' sinks (0: none).  what == 1 (phase 2): the sum of its chunks'
+// start counts.  what == 2 (phase 3, before the finish): the cut candidates'
+// default.  One workgroup of 64 per reference.
 template <int X = 0>  // (a template: instantiated only where launched)
 __global__ void k_fa_shard_sums(FaRefs a, const unsigned long long* __restrict__ tmax,
-                                const unsigned long long* __restrict__ crec, unsigned long long* max_out,
-                                unsigned long long* starts_out) {
+                                const unsigned long long* __restrict__ crec, unsigned long long* row, int what) {
   const uint32_t r = blockIdx.x, lane = __lane_id();
   unsigned long long mx = 0, st = 0;
-  if (max_out)
+  if (what == 2) {
+    if (lane == 0) row[ROW_CUT + r] = a.ntot[r];
+    return;
+  }
+  if (what == 0)
     for (uint64_t t = a.toff[r] + lane; t < a.toff[r + 1]; t += 64) mx = tmax[t] > mx ? tmax[t] : mx;
-  if (starts_out)
+  else
     for (uint64_t c = a.coff[r] + lane; c < a.coff[r + 1]; c += 64) st += crec[c * CW];
   mx = sc_wave_red<true>(mx);
   st = sc_wave_red<false>(st);
   if (lane == 0) {
-    if (max_out) max_out[r] = mx;
-    if (starts_out) starts_out[r] = st;
+    if (what == 0) {
+      row[ROW_N + r] = a.n[r];
+      row[ROW_MAX + r] = mx;
+      row[ROW_STARTS + r] = 0;
+      row[ROW_CUT + r] = a.ntot[r];
+      if (r == 0)
+        for (int w = 24; w < ROW_W; ++w) row[w] = 0;
+    } else {
+      row[ROW_STARTS + r] = st;
+    }
+  }
+}
+
+// This shard's inputs from the gathered rows of all `ns` shards (rows[s *
+// ROW_W ...], shard `me`), for the phase about to run: 2 carry (the largest
+// sink of the earlier shards with samples), 3 cut (the starts of the earlier
+// shards), 4 hist (the global cut and whether a later shard has samples).
+// Any row's error word marks the pass failed (FLAG_SHARD at the next fetch).
+template <int X = 0>  // (a template: instantiated only where launched)
+__global__ void k_fa_xchg(const unsigned long long* __restrict__ rows, uint32_t ns, uint32_t me, int phase,
+                          unsigned long long* __restrict__ xin, GTable g) {
+  const uint32_t r = threadIdx.x;
+  if (r == 6) {
+    unsigned long long f = 0;
+    for (uint32_t s = 0; s < ns; ++s) f |= rows[(uint64_t)s * ROW_W + ROW_ERR];
+    xin[XIN_FAIL] = f ? 1ull : 0ull;
+    if (f) atomicOr(&g.flags[0], FLAG_SHARD);
+  }
+  if (r >= 6) return;
+  if (phase == 2) {
+    unsigned long long c = 0;
+    for (uint32_t s = 0; s < me; ++s) {
+      const unsigned long long* w = rows + (uint64_t)s * ROW_W;
+      if (w[ROW_N + r] && w[ROW_MAX + r] > c) c = w[ROW_MAX + r];
+    }
+    xin[XIN_CIN + r] = c;
+  } else if (phase == 3) {
+    unsigned long long b = 0;
+    for (uint32_t s = 0; s < me; ++s) b += rows[(uint64_t)s * ROW_W + ROW_STARTS + r];
+    xin[XIN_SOFF + r] = b;
+  } else {
+    unsigned long long c = KEY_EMPTY, later = 0;
+    for (uint32_t s = 0; s < ns; ++s) {
+      const unsigned long long* w = rows + (uint64_t)s * ROW_W;
+      c = w[ROW_CUT + r] < c ? w[ROW_CUT + r] : c;
+      if (s > me) later |= w[ROW_N + r];
+    }
+    xin[XIN_CUT + r] = c;
+    xin[XIN_LAST + r] = later ? 0ull : 1ull;
   }
 }
 
@@ -1580,6 +1661,7 @@ struct FaLaunch {
   uint32_t epoch; // this pass's chunk-publication epoch
   int phase;      // FA_PH_*
   hipStream_t s;
+  unsigned long long* row;  // a key-range shard's summary row (FA_PH_CUT writes its cut candidates)
 };
 
 // phases of the pipeline: 1 local pass, 2 chunks (carry, fix-up), 3 finish
@@ -1596,6 +1678,8 @@ inline void fa_launch_t(const FaLaunch& L) {
     bool fast = false;
     if constexpr (P2) {  // fast tiles, then the queued rest (an empty queue: the workgroups return at once)
       if (L.a.fast) {
+        // the queue starts empty whatever an earlier, abandoned pass left in it
+        (void)hipMemsetAsync(b.slowq, 0, sizeof(unsigned int), L.s);
         hipLaunchKernelGGL((k_fa_local_fast<SRC, CHK>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
                            b.fslot, b.slowq, L.g);
         hipLaunchKernelGGL((k_fa_local<SRC, P2, CHK, true>), dim3(nres), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart,
@@ -1613,18 +1697,20 @@ inline void fa_launch_t(const FaLaunch& L) {
                        b.pmin, b.dpart, b.klist, b.cval, b.cflag, b.crec, L.epoch, b.slowq, L.g);
   if (ph == FA_PH_ALL)
     hipLaunchKernelGGL((k_fa_finish<SRC, P2, false>), dim3(6), dim3(CH), 0, L.s, L.m, L.a, b.tmax, b.pmin, b.dpart,
-                       b.crec, b.fslot, b.shrec, L.g);
+                       b.crec, b.fslot, b.shrec, (unsigned long long*)nullptr, L.g);
   if (ph == FA_PH_CUT)
     hipLaunchKernelGGL((k_fa_finish<SRC, P2, true>), dim3(6), dim3(CH), 0, L.s, L.m, L.a, b.tmax, b.pmin, b.dpart,
-                       b.crec, b.fslot, b.shrec, L.g);
+                       b.crec, b.fslot, b.shrec, L.row, L.g);
 }
 
 // a key-range shard's pass between its phases (pluss_dev_faithful_shards_*)
 struct FaShards {
   FaLaunch L;
   int src = SRC_GEN;
-  int phase = 0;  // last completed phase (1 local, 2 carry, 3 cut)
+  int phase = 0;  // last completed phase (SH_*)
+  uint64_t tot[6] = {0, 0, 0, 0, 0, 0};  // SH_SELECTED: every reference's whole-list length
 };
+enum : int { SH_NONE = 0, SH_LOCAL = 1, SH_CARRY = 2, SH_CUT = 3, SH_SELECTED = 10 };
 
 // the four sources (pluss_fa_w32.hip, pluss_fa_w64.hip, pluss_fa_smp.hip, pluss_fa_gen.hip)
 void fa_launch_w32(const FaLaunch& L);

@@ -34,11 +34,10 @@
 
 #include <algorithm>
 #include <cstring>
+#include <string>
 #include <type_traits>
+#include <vector>
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "pluss_faithful.h"
 #include "pluss_sort.h"
@@ -119,13 +118,6 @@ __global__ __launch_bounds__(BLOCK) void k_faith_keys(Model m, uint32_t ref, con
   }
 }
 
-// scal: [0] cut, [1] cold (tid 0), [2] traversed (mod 2^64), [3] shard size
-__global__ void k_faith_init(unsigned long long* scal, uint64_t cut) {
-  scal[0] = cut;
-  scal[1] = 0;
-  scal[2] = 0;
-}
-
 // Global prefix max at local i of a shard = max(pmax_in, local pmax_i);
 // pmax_in = largest sink of every earlier shard (0 if none).
 __device__ __forceinline__ unsigned long long gmax(const unsigned long long* pmax, uint64_t i,
@@ -145,39 +137,6 @@ struct FlagArgs {
   unsigned long long pmax_in;
   PkView pv;
 };
-template <int FM>
-__device__ __forceinline__ bool flag_at(const FlagArgs& a, uint64_t i) {
-  const unsigned long long before = i == 0 ? a.pmax_in : gmax(a.pmax, i - 1, a.pmax_in);
-  return a.j_off + i == 0 || key_at<FM>(a.keys, i, a.pv) > before;
-}
-template <int FM>
-struct FlagOp {  // rocprim transform: element index -> start flag
-  FlagArgs a;
-  __device__ unsigned int operator()(uint64_t i) const { return flag_at<FM>(a, i) ? 1u : 0u; }
-};
-
-// Q1: the first START j > 0 (global index) whose met-sample count
-// j - starts_before_j reaches the number of samples left, n_total - j.
-template <int FM>
-__global__ __launch_bounds__(BLOCK) void k_faith_cut(FlagArgs fa, const unsigned int* __restrict__ nstart, uint64_t n,
-                                                     uint64_t s_off, uint64_t n_total, unsigned long long* scal) {
-  const uint64_t j_off = fa.j_off;
-  unsigned long long best = KEY_EMPTY;
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
-    const uint64_t j = j_off + i;
-    if (j > 0 && flag_at<FM>(fa, i)) {
-      const uint64_t met = j - (s_off + (uint64_t)nstart[i] - 1);  // samples met before this START
-      if (met >= n_total - j && j < best) best = j;
-    }
-  }
-  // one atomic per wave instead of one per qualifying sample
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long x = __shfl_xor(best, o, 64);
-    best = x < best ? x : best;
-  }
-  if (__lane_id() == 0 && best != KEY_EMPTY) atomicMin(&scal[0], best);
-}
-
 // ---- one-GPU scan: prefix max of sinks, start flags, start counts and the Q1
 // cut in one pass over the sorted words (the shard path runs them as the
 // separate rocPRIM scans and k_faith_cut above, because its start offset and
@@ -543,30 +502,11 @@ static int faith_reserve(pluss_ctx* ctx, FaithfulBufs& b, uint64_t n, hipStream_
 }
 
 static int faith_tmp(pluss_ctx* ctx, FaithfulBufs& b, uint64_t n, hipStream_t s) {
-  // rocPRIM temporary storage: the pair sort and scans of the (key, sink) path
-  // (shapes with N % (cls/ds) != 0) and the prefix scans of the key-range shard
-  // protocol; packed words are sorted by pluss_sort.h (no temporary storage)
-  size_t t1 = 0, t2 = 0, t3 = 0;
-  const int fm = faith_fm(ctx->m);
-  if (fm == FM_PK32) {
-    auto it = rocprim::make_transform_iterator((const uint32_t*)b.keys_s, PkSinkOp<uint32_t>{make_pkview(ctx->m, 0)});
-    PLUSS_HIP_CHECK(rocprim::inclusive_scan(nullptr, t2, it, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
-  } else if (fm == FM_PK64) {
-    auto it = rocprim::make_transform_iterator(b.keys_s, PkSinkOp<unsigned long long>{make_pkview(ctx->m, 0)});
-    PLUSS_HIP_CHECK(rocprim::inclusive_scan(nullptr, t2, it, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
-  } else {
-    PLUSS_HIP_CHECK(
-        rocprim::radix_sort_pairs(nullptr, t1, b.keys, b.keys_s, b.sinks, b.sinks_s, n, 0, key_bits(ctx->m), s));
-    PLUSS_HIP_CHECK(
-        rocprim::inclusive_scan(nullptr, t2, b.sinks_s, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
-  }
-  {
-    const FlagArgs fa{b.keys_s, b.pmax, 0, 0, make_pkview(ctx->m, 0)};
-    auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint64_t>(0), FlagOp<FM_PAIRS>{fa});
-    PLUSS_HIP_CHECK(rocprim::inclusive_scan(nullptr, t3, it, b.nstart, n, rocprim::plus<unsigned int>(), s));
-  }
-  size_t need = t1 > t2 ? t1 : t2;
-  need = need > t3 ? need : t3;
+  // rocPRIM temporary storage of the (key, sink) pair sort (shapes with
+  // N % (cls/ds) != 0); packed words are sorted by pluss_sort.h (none needed)
+  size_t need = 0;
+  PLUSS_HIP_CHECK(
+      rocprim::radix_sort_pairs(nullptr, need, b.keys, b.keys_s, b.sinks, b.sinks_s, n, 0, key_bits(ctx->m), s));
   if (need > b.tmp_bytes) {
     PLUSS_HIP_CHECK(hipStreamSynchronize(s));
     if (b.tmp) (void)hipFree(b.tmp);
@@ -748,69 +688,12 @@ static int faith_keys(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, const uint64
   return PLUSS_OK;
 }
 
-// sort the shard's n (key, sink) pairs by key and take the prefix max of sinks
-static int faith_sort(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, uint64_t n, hipStream_t s, bool with_pmax = true) {
+// sort n (key, sink) pairs by key (k_faith_scan takes the prefix max of sinks)
+static int faith_sort(pluss_ctx* ctx, FaithfulBufs& b, uint64_t n, hipStream_t s) {
   if (int rc = faith_tmp(ctx, b, n, s)) return rc;
   size_t sz = b.tmp_bytes;
-  const int fm = faith_fm(ctx->m);
-  if (fm == FM_PK32) {
-    if (int rc = srt_run<uint32_t, false>(ctx, b, ref, b.keys, n, s)) return rc;
-    if (!with_pmax) return PLUSS_OK;
-    auto it = rocprim::make_transform_iterator((const uint32_t*)b.keys_s,
-                                               PkSinkOp<uint32_t>{make_pkview(ctx->m, (uint32_t)ref)});
-    PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, it, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
-    return PLUSS_OK;
-  }
-  if (fm == FM_PK64) {
-    if (int rc = srt_run<unsigned long long, false>(ctx, b, ref, b.keys, n, s)) return rc;
-    if (!with_pmax) return PLUSS_OK;
-    auto it = rocprim::make_transform_iterator(b.keys_s,
-                                               PkSinkOp<unsigned long long>{make_pkview(ctx->m, (uint32_t)ref)});
-    PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, it, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
-    return PLUSS_OK;
-  }
   PLUSS_HIP_CHECK(
       rocprim::radix_sort_pairs(b.tmp, sz, b.keys, b.keys_s, b.sinks, b.sinks_s, n, 0, key_bits(ctx->m), s));
-  if (!with_pmax) return PLUSS_OK;
-  sz = b.tmp_bytes;
-  PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, b.sinks_s, b.pmax, n, rocprim::maximum<unsigned long long>(), s));
-  return PLUSS_OK;
-}
-
-static int faith_starts(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, uint64_t n, uint64_t j_off, unsigned long long pmax_in,
-                        hipStream_t s) {
-  const FlagArgs fa{b.keys_s, b.pmax, j_off, pmax_in, make_pkview(ctx->m, (uint32_t)ref)};
-  size_t sz = b.tmp_bytes;
-  rocprim::counting_iterator<uint64_t> idx(0);
-  const int fm = faith_fm(ctx->m);
-  // nstart = inclusive scan of the start flags, evaluated inside the scan
-  if (fm == FM_PK32)
-    PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, rocprim::make_transform_iterator(idx, FlagOp<FM_PK32>{fa}),
-                                            b.nstart, n, rocprim::plus<unsigned int>(), s));
-  else if (fm == FM_PK64)
-    PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, rocprim::make_transform_iterator(idx, FlagOp<FM_PK64>{fa}),
-                                            b.nstart, n, rocprim::plus<unsigned int>(), s));
-  else
-    PLUSS_HIP_CHECK(rocprim::inclusive_scan(b.tmp, sz, rocprim::make_transform_iterator(idx, FlagOp<FM_PAIRS>{fa}),
-                                            b.nstart, n, rocprim::plus<unsigned int>(), s));
-  return PLUSS_OK;
-}
-
-// Q1 cut of this shard's elements into scal[0] (already holding the default)
-static int faith_cut(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, uint64_t n, uint64_t j_off, unsigned long long pmax_in,
-                     uint64_t s_off, uint64_t n_total, hipStream_t s) {
-  const FlagArgs fa{b.keys_s, b.pmax, j_off, pmax_in, make_pkview(ctx->m, (uint32_t)ref)};
-  const int fm = faith_fm(ctx->m);
-  if (fm == FM_PK32)
-    hipLaunchKernelGGL(k_faith_cut<FM_PK32>, dim3(grid_of(n)), dim3(BLOCK), 0, s, fa, b.nstart, n, s_off, n_total,
-                       b.scal);
-  else if (fm == FM_PK64)
-    hipLaunchKernelGGL(k_faith_cut<FM_PK64>, dim3(grid_of(n)), dim3(BLOCK), 0, s, fa, b.nstart, n, s_off, n_total,
-                       b.scal);
-  else
-    hipLaunchKernelGGL(k_faith_cut<FM_PAIRS>, dim3(grid_of(n)), dim3(BLOCK), 0, s, fa, b.nstart, n, s_off, n_total,
-                       b.scal);
-  PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }
 
@@ -898,8 +781,6 @@ static int fa_prepare(pluss_ctx* ctx, FaRefs& a, int src, bool check, bool shard
     if (!shard) {
       a.ntot[r] = a.n[r];
       a.joff[r] = 0;
-      a.soff[r] = 0;
-      a.cin[r] = 0;
     }
     a.toff[r] = t;
     t += fa_tiles(a.n[r]);
@@ -917,13 +798,17 @@ static int fa_prepare(pluss_ctx* ctx, FaRefs& a, int src, bool check, bool shard
     return PLUSS_ERR_CONFIG;
   }
   FaithfulBufs& b = ctx->fb;
+  if (shard && !b.xin) {
+    if (int rc = grow(&b.xin, XIN_W + 8)) return rc;
+  }
+  a.xin = shard ? b.xin : nullptr;
   // N, T, CS, CLS/DS powers of two: shift decoding (the word decode also
   // keeps q*N + c1 < N*N/T in 32 bits)
   const bool p2 = m.p2 && a.pv[0].p2 && (uint64_t)m.N * m.N / m.T < (1ull << 32);
   // the local pass's fast path: 24-bit multiplies (q*N + c1 < N*N/T and S
   // below 2^24) and the range check by bit masks (N a power of two)
   a.fast = (p2 && m.np2 && (uint64_t)m.N * m.N / m.T < (1ull << 24) && m.S < (1u << 24)) ? 1u : 0u;
-  *out = FaLaunch{m, a, ctx->g, &b, p2, t, 0, FA_PH_ALL, s};
+  *out = FaLaunch{m, a, ctx->g, &b, p2, t, 0, FA_PH_ALL, s, nullptr};
   if (t == 0) return PLUSS_OK;
   if (int rc = fa_reserve(b, t, c, s)) return rc;
   if (!b.shrec) {
@@ -969,7 +854,7 @@ static int faith_keys_sorted(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, const
   if (fm == FM_PK32) return srt_run<uint32_t, true>(ctx, b, ref, d_samples, n, s);
   if (fm == FM_PK64) return srt_run<unsigned long long, true>(ctx, b, ref, d_samples, n, s);
   if (int rc = faith_keys(ctx, b, ref, d_samples, n, 0, 0, nullptr, s)) return rc;
-  return faith_sort(ctx, b, ref, n, s, true);
+  return faith_sort(ctx, b, n, s);
 }
 
 // (key, sink) pairs (shapes with N % W != 0): the rocPRIM scans and the record pass
@@ -986,6 +871,7 @@ static int faith_pairs_scan(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, uint64
 
 // One sampler_<REF> over a list in any order: keys, radix sort, scan.
 int launch_faithful(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s) {
+  faith_shards_abandon(ctx);  // these share the handle's faithful buffers
   if (int rc = faith_check_shape(ctx)) return rc;
   if (n == 0) return PLUSS_OK;
   FaithfulBufs& b = ctx->fb;
@@ -1009,6 +895,7 @@ static int faith_direct_shape(const pluss_ctx* ctx, const char* api) {
 }
 
 int launch_faithful_sorted(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s) {
+  faith_shards_abandon(ctx);  // these share the handle's faithful buffers
   if (int rc = faith_direct_shape(ctx, "pluss_dev_faithful_hist_sorted")) return rc;
   FaRefs a = fa_none();
   a.n[ref] = n;
@@ -1021,6 +908,7 @@ int launch_faithful_sorted(pluss_ctx* ctx, int32_t ref, const uint64_t* d_sample
 // (r10's main runs one thread per reference, r10:3203-3257); then one scan
 // pipeline for the six sorted arrays.
 int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t* counts, hipStream_t s) {
+  faith_shards_abandon(ctx);  // these share the handle's faithful buffers
   if (int rc = faith_check_shape(ctx)) return rc;
   uint64_t off[6], total = 0;
   for (int r = 0; r < 6; ++r) {
@@ -1064,6 +952,7 @@ int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64
 // diagnostics: the bucket sort alone (include/pluss_diag.h)
 int diag_sort_words(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, void* d_words,
                     int32_t* word_bytes, hipStream_t s) {
+  faith_shards_abandon(ctx);  // these share the handle's faithful buffers
   if (int rc = faith_direct_shape(ctx, "pluss_diag_sort_words")) return rc;
   FaithfulBufs& b = ctx->fb;
   if (int rc = faith_reserve(ctx, b, n, s)) return rc;
@@ -1081,6 +970,7 @@ int diag_sort_words(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint
 
 // All six over a key-ordered list (each reference's block in key order).
 int launch_faithful_sorted_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t* counts, hipStream_t s) {
+  faith_shards_abandon(ctx);  // these share the handle's faithful buffers
   if (int rc = faith_direct_shape(ctx, "pluss_dev_faithful_hist_sorted_refs")) return rc;
   FaRefs a = fa_none();
   uint64_t off = 0;
@@ -1099,6 +989,7 @@ int launch_faithful_sorted_refs(pluss_ctx* ctx, const uint64_t* d_samples, const
 // All six over generated key-order lists (pluss_expand_sorted's lists of
 // totals[r] samples, never written to memory).
 int launch_gen_faithful_refs(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t s) {
+  faith_shards_abandon(ctx);  // these share the handle's faithful buffers
   if (int rc = faith_direct_shape(ctx, "pluss_dev_gen_faithful_refs")) return rc;
   FaRefs a = fa_none();
   for (int r = 0; r < 6; ++r) {
@@ -1110,110 +1001,55 @@ int launch_gen_faithful_refs(pluss_ctx* ctx, uint64_t seed, const uint64_t* tota
   return fa_run(ctx, a, SRC_GEN, false, s);
 }
 
-// ---- key-range shards (multi-GPU faithful mode; the caller exchanges the
-// ---- per-shard summaries between phases)
-int faith_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, uint64_t lo, uint64_t hi,
-                     pluss_faith_shard* out, hipStream_t s) {
-  FaithfulBufs& b = ctx->fb;
-  if (int rc = faith_check_shape(ctx)) return rc;
-  if (int rc = faith_reserve(ctx, b, n, s)) return rc;
-  FaithShard& f = ctx->fsh;
-  f = FaithShard{};
-  f.ref = ref;
-  PLUSS_HIP_CHECK(hipMemsetAsync(b.scal + 3, 0, 8, s));
-  if (n)
-    if (int rc = faith_keys(ctx, b, ref, d_samples, n, lo, hi, b.scal + 3, s)) return rc;
-  unsigned long long m = 0;
-  PLUSS_HIP_CHECK(hipMemcpyAsync(&m, b.scal + 3, 8, hipMemcpyDeviceToHost, s));
-  PLUSS_HIP_CHECK(hipStreamSynchronize(s));
-  f.n = m;
-  out->n = m;
-  out->first_key = KEY_EMPTY;
-  out->max_sink = 0;
-  if (m) {
-    if (int rc = faith_sort(ctx, b, ref, m, s)) return rc;
-    const int fm = faith_fm(ctx->m);
-    unsigned long long w64 = 0;
-    uint32_t w32 = 0;
-    if (fm == FM_PK32) PLUSS_HIP_CHECK(hipMemcpyAsync(&w32, b.keys_s, 4, hipMemcpyDeviceToHost, s));
-    else PLUSS_HIP_CHECK(hipMemcpyAsync(&w64, b.keys_s, 8, hipMemcpyDeviceToHost, s));
-    PLUSS_HIP_CHECK(hipMemcpyAsync(&out->max_sink, b.pmax + (m - 1), 8, hipMemcpyDeviceToHost, s));
-    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
-    const PkView pv = make_pkview(ctx->m, (uint32_t)ref);  // the smallest key of the shard
-    out->first_key = fm == FM_PK32 ? pk_key(w32, pv) : (fm == FM_PK64 ? pk_key(w64, pv) : w64);
-  }
-  f.max_sink = out->max_sink;
-  f.phase = 1;
-  return PLUSS_OK;
-}
-
-int faith_shard_starts(pluss_ctx* ctx, uint64_t j_off, uint64_t pmax_in, pluss_faith_shard* out, hipStream_t s) {
-  FaithfulBufs& b = ctx->fb;
-  FaithShard& f = ctx->fsh;
-  if (f.phase != 1) {
-    set_error("pluss_dev_faithful_shard_starts: call pluss_dev_faithful_shard_keys first");
-    return PLUSS_ERR_CONFIG;
-  }
-  f.j_off = j_off;
-  f.pmax_in = pmax_in;
-  out->n_starts = 0;
-  if (f.n) {
-    if (int rc = faith_starts(ctx, b, f.ref, f.n, j_off, pmax_in, s)) return rc;
-    unsigned int c = 0;
-    PLUSS_HIP_CHECK(hipMemcpyAsync(&c, b.nstart + (f.n - 1), 4, hipMemcpyDeviceToHost, s));
-    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
-    out->n_starts = c;
-  }
-  f.phase = 2;
-  return PLUSS_OK;
-}
-
-int faith_shard_cut(pluss_ctx* ctx, uint64_t s_off, uint64_t n_total, pluss_faith_shard* out, hipStream_t s) {
-  FaithfulBufs& b = ctx->fb;
-  FaithShard& f = ctx->fsh;
-  if (f.phase != 2) {
-    set_error("pluss_dev_faithful_shard_cut: call pluss_dev_faithful_shard_starts first");
-    return PLUSS_ERR_CONFIG;
-  }
-  if (f.j_off + f.n > n_total) {
-    set_error("pluss_dev_faithful_shard_cut: n_total is smaller than this shard's end");
-    return PLUSS_ERR_CONFIG;
-  }
-  f.n_total = n_total;
-  out->cut = n_total;
-  if (f.n) {
-    hipLaunchKernelGGL(k_faith_init, dim3(1), dim3(1), 0, s, b.scal, n_total);
-    if (int rc = faith_cut(ctx, b, f.ref, f.n, f.j_off, f.pmax_in, s_off, n_total, s)) return rc;
-    PLUSS_HIP_CHECK(hipMemcpyAsync(&out->cut, b.scal, 8, hipMemcpyDeviceToHost, s));
-    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
-  }
-  f.phase = 3;
-  return PLUSS_OK;
-}
-
-int faith_shard_hist(pluss_ctx* ctx, uint64_t cut, uint64_t next_first_key, int is_last, hipStream_t s) {
-  FaithfulBufs& b = ctx->fb;
-  FaithShard& f = ctx->fsh;
-  if (f.phase != 3) {
-    set_error("pluss_dev_faithful_shard_hist: call pluss_dev_faithful_shard_cut first");
-    return PLUSS_ERR_CONFIG;
-  }
-  if (cut > f.n_total) {
-    set_error("pluss_dev_faithful_shard_hist: cut > n_total");
-    return PLUSS_ERR_CONFIG;
-  }
-  const unsigned long long last = f.max_sink > f.pmax_in ? f.max_sink : f.pmax_in;  // global pmax at the shard end
-  const int next_start = next_first_key != KEY_EMPTY && next_first_key > last;
-  hipLaunchKernelGGL(k_faith_init, dim3(1), dim3(1), 0, s, b.scal, cut);
-  f.phase = 0;
-  return faith_record(ctx, b, f.ref, f.n, f.j_off, f.pmax_in, next_start, f.n_total, is_last, s);
-}
-
 // ---- key-range shards of the single-read pipeline (multi-GPU faithful mode;
 // dist.sharded_faithful_gen_hist): the caller exchanges the per-reference
 // summaries between the four phases
+// ---- key-range shards of the single-read pipeline (multi-GPU faithful mode):
+// every phase writes this shard's summary row in device memory and the next
+// reads the rows of all shards, gathered by the caller (an RCCL all-gather in
+// the group driver, pluss_group.hip, or dist.py); k_fa_xchg derives the
+// shard's inputs on the device, so no phase waits for the host
+__global__ void k_fa_sel_row(const unsigned long long* __restrict__ cnt, unsigned long long* __restrict__ row) {
+  const uint32_t w = threadIdx.x;
+  if (w < ROW_W) row[w] = w < 6 ? cnt[w] : 0ull;
+}
+
+static FaShards& shards_of(pluss_ctx* ctx) {
+  if (!ctx->fsh2) ctx->fsh2 = new FaShards();
+  return *ctx->fsh2;
+}
+
+static int shards_expect(pluss_ctx* ctx, int phase, const char* api, const uint64_t* d_rows, int32_t shard,
+                         int32_t nshards) {
+  if (!ctx->fsh2 || ctx->fsh2->phase != phase) {
+    set_error(std::string(api) + ": out of order (the phases run local, carry, cut, hist on one handle, with no "
+                                 "other faithful call in between)");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (!d_rows || nshards < 1 || shard < 0 || shard >= nshards) {
+    set_error(std::string(api) + ": needs the gathered rows of all shards and 0 <= shard < nshards");
+    return PLUSS_ERR_CONFIG;
+  }
+  return PLUSS_OK;
+}
+
+// phase 1's launches and summary row, whatever the source
+static int shards_phase1(pluss_ctx* ctx, FaShards& f, uint64_t* d_row, hipStream_t s) {
+  f.L.s = s;
+  if (f.L.t)
+    if (int rc = fa_launch(ctx, f.L, f.src, FA_PH_LOCAL)) return rc;
+  FaithfulBufs& b = ctx->fb;
+  hipLaunchKernelGGL(k_fa_shard_sums<0>, dim3(6), dim3(64), 0, s, f.L.a, b.tmax, b.crec, (unsigned long long*)d_row,
+                     0);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  f.phase = SH_LOCAL;
+  return PLUSS_OK;
+}
+
 int faith_shards_local(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t seed, const uint64_t* totals,
-                       const uint64_t* first, const uint64_t* n, uint64_t* max_sink, hipStream_t s) {
+                       const uint64_t* first, const uint64_t* n, uint64_t* d_row, hipStream_t s) {
+  FaShards& f = shards_of(ctx);
+  f = FaShards{};  // whatever an earlier pass left half finished
   if (int rc = faith_direct_shape(ctx, "pluss_dev_faithful_shards_local")) return rc;
   FaRefs a = fa_none();
   uint64_t off = 0;
@@ -1233,96 +1069,154 @@ int faith_shards_local(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t seed,
       a.kg[r] = keygen_of(ctx, seed, r, totals[r]);
     }
   }
-  if (off && !d_samples) {
-    set_error("pluss_dev_faithful_shards_local: null sample list");
-    return PLUSS_ERR_CONFIG;
-  }
-  if (!ctx->fsh2) ctx->fsh2 = new FaShards();
-  FaShards& f = *ctx->fsh2;
-  f = FaShards{};
   f.src = d_samples ? SRC_SAMPLES : SRC_GEN;
   if (int rc = fa_prepare(ctx, a, f.src, true, true, s, &f.L)) return rc;
-  for (int r = 0; r < 6; ++r) max_sink[r] = 0;
-  if (f.L.t) {
-    if (int rc = fa_launch(ctx, f.L, f.src, FA_PH_LOCAL)) return rc;
-    FaithfulBufs& b = ctx->fb;
-    hipLaunchKernelGGL(k_fa_shard_sums<0>, dim3(6), dim3(64), 0, s, f.L.a, b.tmax, b.crec, b.shrec + 6 * SRW,
-                       (unsigned long long*)nullptr);
-    PLUSS_HIP_CHECK(hipGetLastError());
-    PLUSS_HIP_CHECK(hipMemcpyAsync(max_sink, b.shrec + 6 * SRW, 6 * 8, hipMemcpyDeviceToHost, s));
-    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
-  }
-  f.phase = 1;
-  return PLUSS_OK;
+  return shards_phase1(ctx, f, d_row, s);
 }
 
-int faith_shards_carry(pluss_ctx* ctx, const uint64_t* carry_in, uint64_t* starts, hipStream_t s) {
-  if (!ctx->fsh2) ctx->fsh2 = new FaShards();
-  FaShards& f = *ctx->fsh2;
-  if (f.phase != 1) {
-    set_error("pluss_dev_faithful_shards_carry: call pluss_dev_faithful_shards_local first");
+// arbitrary-order lists (what r10 hands over): every shard reads the whole
+// lists and keeps its key range as packed sort words
+int faith_shards_select(pluss_ctx* ctx, const uint64_t* d_lists, const uint64_t* totals, uint64_t key_lo,
+                        uint64_t key_hi, uint64_t* d_row, hipStream_t s) {
+  FaShards& f = shards_of(ctx);
+  f = FaShards{};
+  if (int rc = faith_direct_shape(ctx, "pluss_dev_faithful_shards_select")) return rc;
+  uint64_t total = 0;
+  for (int r = 0; r < 6; ++r) total += totals[r];
+  if (total && !d_lists) {
+    set_error("pluss_dev_faithful_shards_select: null sample lists");
     return PLUSS_ERR_CONFIG;
-  }
-  for (int r = 0; r < 6; ++r) {
-    f.L.a.cin[r] = carry_in[r];
-    starts[r] = 0;
-  }
-  if (f.L.t) {
-    if (int rc = fa_launch(ctx, f.L, f.src, FA_PH_CHUNK)) return rc;
-    FaithfulBufs& b = ctx->fb;
-    hipLaunchKernelGGL(k_fa_shard_sums<0>, dim3(6), dim3(64), 0, s, f.L.a, b.tmax, b.crec, (unsigned long long*)nullptr,
-                       b.shrec + 6 * SRW + 8);
-    PLUSS_HIP_CHECK(hipGetLastError());
-    PLUSS_HIP_CHECK(hipMemcpyAsync(starts, b.shrec + 6 * SRW + 8, 6 * 8, hipMemcpyDeviceToHost, s));
-    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
-  }
-  f.phase = 2;
-  return PLUSS_OK;
-}
-
-int faith_shards_cut(pluss_ctx* ctx, const uint64_t* starts_before, uint64_t* cut, hipStream_t s) {
-  if (!ctx->fsh2) ctx->fsh2 = new FaShards();
-  FaShards& f = *ctx->fsh2;
-  if (f.phase != 2) {
-    set_error("pluss_dev_faithful_shards_cut: call pluss_dev_faithful_shards_carry first");
-    return PLUSS_ERR_CONFIG;
-  }
-  for (int r = 0; r < 6; ++r) {
-    f.L.a.soff[r] = starts_before[r];
-    cut[r] = f.L.a.ntot[r];
-  }
-  if (f.L.t) {
-    if (int rc = fa_launch(ctx, f.L, f.src, FA_PH_CUT)) return rc;
-    FaithfulBufs& b = ctx->fb;
-    unsigned long long rec[6 * SRW];
-    PLUSS_HIP_CHECK(hipMemcpyAsync(rec, b.shrec, sizeof rec, hipMemcpyDeviceToHost, s));
-    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
-    for (int r = 0; r < 6; ++r)
-      if (f.L.a.n[r]) cut[r] = rec[r * SRW + FPART];
-  }
-  f.phase = 3;
-  return PLUSS_OK;
-}
-
-int faith_shards_hist(pluss_ctx* ctx, const uint64_t* cut, const int32_t* is_last, hipStream_t s) {
-  if (!ctx->fsh2) ctx->fsh2 = new FaShards();
-  FaShards& f = *ctx->fsh2;
-  if (f.phase != 3) {
-    set_error("pluss_dev_faithful_shards_hist: call pluss_dev_faithful_shards_cut first");
-    return PLUSS_ERR_CONFIG;
-  }
-  f.phase = 0;
-  if (!f.L.t) return PLUSS_OK;
-  FaShardCut c;
-  for (int r = 0; r < 6; ++r) {
-    c.cut[r] = cut[r];
-    c.last[r] = is_last[r];
   }
   FaithfulBufs& b = ctx->fb;
-  hipLaunchKernelGGL(k_fa_shard_apply<0>, dim3(1), dim3(64), 0, s, f.L.m, f.L.a, b.shrec, c, b.fslot, f.L.g);
+  if (int rc = faith_reserve(ctx, b, total, s)) return rc;
+  if (!b.xin)
+    if (int rc = grow(&b.xin, XIN_W + 8)) return rc;
+  unsigned long long* cnt = b.xin + XIN_W;
+  PLUSS_HIP_CHECK(hipMemsetAsync(cnt, 0, 8 * sizeof(unsigned long long), s));
+  const int fm = faith_fm(ctx->m);
+  uint64_t off = 0;
+  for (int r = 0; r < 6; ++r) {
+    f.tot[r] = totals[r];
+    if (totals[r]) {
+      // reference r's words go to its own region of b.keys (room for its whole list)
+      void* out = fm == FM_PK32 ? (void*)((uint32_t*)b.keys + off) : (void*)(b.keys + off);
+      if (fm == FM_PK32)
+        hipLaunchKernelGGL((k_faith_keys<true, FM_PK32>), dim3(grid_of(totals[r])), dim3(BLOCK), 0, s, ctx->m,
+                           (uint32_t)r, d_lists + off, totals[r], key_lo, key_hi, out, (unsigned long long*)nullptr,
+                           cnt + r, ctx->g);
+      else
+        hipLaunchKernelGGL((k_faith_keys<true, FM_PK64>), dim3(grid_of(totals[r])), dim3(BLOCK), 0, s, ctx->m,
+                           (uint32_t)r, d_lists + off, totals[r], key_lo, key_hi, out, (unsigned long long*)nullptr,
+                           cnt + r, ctx->g);
+    }
+    off += totals[r];
+  }
+  hipLaunchKernelGGL(k_fa_sel_row, dim3(1), dim3(ROW_W), 0, s, (const unsigned long long*)cnt,
+                     (unsigned long long*)d_row);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  ctx->tables_dirty = true;
+  f.phase = SH_SELECTED;
+  return PLUSS_OK;
+}
+
+// phase 1 of the selected words: the one host round trip of an arbitrary-order
+// pass (the launch grids need this shard's counts), then the sort and the local pass
+int faith_shards_local_selected(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards,
+                                uint64_t* d_row, hipStream_t s) {
+  if (int rc = shards_expect(ctx, SH_SELECTED, "pluss_dev_faithful_shards_local_selected", d_rows, shard, nshards))
+    return rc;
+  FaShards& f = *ctx->fsh2;
+  std::vector<unsigned long long> rows((size_t)nshards * ROW_W);
+  PLUSS_HIP_CHECK(hipMemcpyAsync(rows.data(), d_rows, rows.size() * 8, hipMemcpyDeviceToHost, s));
+  PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+  FaRefs a = fa_none();
+  const void* in[6];
+  uint64_t cnt[6], woff = 0, soff = 0;
+  const int fm = faith_fm(ctx->m);
+  FaithfulBufs& b = ctx->fb;
+  for (int r = 0; r < 6; ++r) {
+    uint64_t before = 0, all = 0;
+    for (int32_t x = 0; x < nshards; ++x) {
+      const unsigned long long v = rows[(size_t)x * ROW_W + ROW_N + r];
+      all += v;
+      if (x < shard) before += v;
+    }
+    cnt[r] = rows[(size_t)shard * ROW_W + ROW_N + r];
+    if (cnt[r] > f.tot[r] || all > f.tot[r]) {  // (a failed shard's row: the pass is reported at the fetch)
+      cnt[r] = 0;
+      all = before = 0;
+    }
+    a.n[r] = cnt[r];
+    a.ntot[r] = all;
+    a.joff[r] = before;
+    in[r] = fm == FM_PK32 ? (const void*)((const uint32_t*)b.keys + woff) : (const void*)(b.keys + woff);
+    a.src[r] = fm == FM_PK32 ? (const void*)((const uint32_t*)b.keys_s + soff) : (const void*)(b.keys_s + soff);
+    woff += f.tot[r];
+    soff += cnt[r];
+  }
+  if (fm == FM_PK32) {
+    if (int rc = srt_sort<uint32_t, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, (uint32_t*)b.keys_s, s)) return rc;
+  } else if (int rc = srt_sort<unsigned long long, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, b.keys_s, s)) {
+    return rc;
+  }
+  f.src = fm == FM_PK32 ? SRC_W32 : SRC_W64;
+  if (int rc = fa_prepare(ctx, a, f.src, false, true, s, &f.L)) return rc;
+  return shards_phase1(ctx, f, d_row, s);
+}
+
+int faith_shards_carry(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards, uint64_t* d_row,
+                       hipStream_t s) {
+  if (int rc = shards_expect(ctx, SH_LOCAL, "pluss_dev_faithful_shards_carry", d_rows, shard, nshards)) return rc;
+  FaShards& f = *ctx->fsh2;
+  FaithfulBufs& b = ctx->fb;
+  f.L.s = s;
+  hipLaunchKernelGGL(k_fa_xchg<0>, dim3(1), dim3(64), 0, s, (const unsigned long long*)d_rows, (uint32_t)nshards,
+                     (uint32_t)shard, 2, b.xin, ctx->g);
+  if (f.L.t)
+    if (int rc = fa_launch(ctx, f.L, f.src, FA_PH_CHUNK)) return rc;
+  hipLaunchKernelGGL(k_fa_shard_sums<0>, dim3(6), dim3(64), 0, s, f.L.a, b.tmax, b.crec, (unsigned long long*)d_row,
+                     1);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  f.phase = SH_CARRY;
+  return PLUSS_OK;
+}
+
+int faith_shards_cut(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards, uint64_t* d_row,
+                     hipStream_t s) {
+  if (int rc = shards_expect(ctx, SH_CARRY, "pluss_dev_faithful_shards_cut", d_rows, shard, nshards)) return rc;
+  FaShards& f = *ctx->fsh2;
+  FaithfulBufs& b = ctx->fb;
+  f.L.s = s;
+  hipLaunchKernelGGL(k_fa_xchg<0>, dim3(1), dim3(64), 0, s, (const unsigned long long*)d_rows, (uint32_t)nshards,
+                     (uint32_t)shard, 3, b.xin, ctx->g);
+  hipLaunchKernelGGL(k_fa_shard_sums<0>, dim3(6), dim3(64), 0, s, f.L.a, b.tmax, b.crec, (unsigned long long*)d_row,
+                     2);
+  if (f.L.t) {
+    f.L.row = (unsigned long long*)d_row;
+    if (int rc = fa_launch(ctx, f.L, f.src, FA_PH_CUT)) return rc;
+  }
+  PLUSS_HIP_CHECK(hipGetLastError());
+  f.phase = SH_CUT;
+  return PLUSS_OK;
+}
+
+int faith_shards_hist(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards, hipStream_t s) {
+  if (int rc = shards_expect(ctx, SH_CUT, "pluss_dev_faithful_shards_hist", d_rows, shard, nshards)) return rc;
+  FaShards& f = *ctx->fsh2;
+  FaithfulBufs& b = ctx->fb;
+  f.phase = SH_NONE;
+  hipLaunchKernelGGL(k_fa_xchg<0>, dim3(1), dim3(64), 0, s, (const unsigned long long*)d_rows, (uint32_t)nshards,
+                     (uint32_t)shard, 4, b.xin, ctx->g);
+  if (f.L.t)
+    hipLaunchKernelGGL(k_fa_shard_apply<0>, dim3(1), dim3(64), 0, s, f.L.m, f.L.a, b.shrec,
+                       (const unsigned long long*)b.xin, b.fslot, f.L.g);
   PLUSS_HIP_CHECK(hipGetLastError());
   ctx->tables_dirty = true;
   return PLUSS_OK;
+}
+
+void faith_shards_abandon(pluss_ctx* ctx) {
+  if (ctx->fsh2) ctx->fsh2->phase = SH_NONE;
 }
 
 void faith_shards_free(pluss_ctx* ctx) {

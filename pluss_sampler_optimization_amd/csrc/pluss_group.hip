@@ -1,0 +1,767 @@
+// pluss_group.hip — multi-GPU behind the C ABI (include/pluss_gpu.h,
+// pluss_group_*): one process drives a set of shards over one or more HIP
+// devices (one pluss_ctx per shard, several logical shards per device if
+// asked), or one rank of a multi-process job.  The exchanges run on the
+// devices over RCCL (xGMI): one all-reduce of the 19-word dense vector per
+// clean pass, one all-gather of the shards' summary rows between the phases
+// of a faithful pass, one all-gather of the canonical tables at the end.
+//
+// Replaces what the reference's callers would otherwise have to write around
+// the one-GPU entry points: r10's main (six sampler_<REF> threads, then the
+// merge, r10:3191-3278) and the Rust main (src/main.rs:17-44) reach every GPU
+// of a node through these calls.  RCCL is loaded on first use (dlopen of
+// librccl.so.1: the copy a PyTorch process already mapped, else ROCm's), so
+// one-GPU users of libpluss_gpu.so never load it.
+//
+// Shards are numbered device-major: global shard g = rank * spd + j lives on
+// the device of RCCL rank `rank` (one per device; a process's local devices
+// are ranks 0..ndev-1 of its own communicator, or its one device is rank
+// `rank` of a multi-process communicator) as its j-th logical shard.
+// Clean mode: shard g takes the slice [c*g/S, c*(g+1)/S) of every reference's
+// index range (or of a host list).  Faithful mode: shard g takes the sort-key
+// range [K*g/S, K*(g+1)/S) (K = pluss_faithful_key_space).
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "pluss_faithful.h"
+
+namespace pluss {
+
+// ---- RCCL, loaded on first use ------------------------------------------------
+struct Rccl {
+  bool tried = false, ok = false;
+  std::string why;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+static Rccl g_rccl;
+
+static Rccl* rccl() {
+  Rccl& R = g_rccl;
+  if (R.tried) return R.ok ? &R : nullptr;
+  R.tried = true;
+  void* h = nullptr;
+  for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"})
+    if ((h = dlopen(name, RTLD_NOW | RTLD_GLOBAL))) break;
+  if (!h) {
+    R.why = std::string("cannot load librccl.so.1: ") + dlerror();
+    return nullptr;
+  }
+  auto sym = [&](const char* s) {
+    void* p = dlsym(h, s);
+    if (!p && R.why.empty()) R.why = std::string("librccl.so.1 lacks ") + s;
+    return p;
+  };
+  R.GetUniqueId = (decltype(R.GetUniqueId))sym("ncclGetUniqueId");
+  R.CommInitRank = (decltype(R.CommInitRank))sym("ncclCommInitRank");
+  R.CommInitAll = (decltype(R.CommInitAll))sym("ncclCommInitAll");
+  R.CommDestroy = (decltype(R.CommDestroy))sym("ncclCommDestroy");
+  R.AllReduce = (decltype(R.AllReduce))sym("ncclAllReduce");
+  R.AllGather = (decltype(R.AllGather))sym("ncclAllGather");
+  R.GroupStart = (decltype(R.GroupStart))sym("ncclGroupStart");
+  R.GroupEnd = (decltype(R.GroupEnd))sym("ncclGroupEnd");
+  R.GetErrorString = (decltype(R.GetErrorString))sym("ncclGetErrorString");
+  R.ok = R.why.empty();
+  return R.ok ? &R : nullptr;
+}
+
+#define PLUSS_NCCL_CHECK(expr)                                                                       \
+  do {                                                                                               \
+    ncclResult_t r_ = (expr);                                                                        \
+    if (r_ != ncclSuccess) {                                                                         \
+      ::pluss::set_error(std::string(#expr) + ": " + g_rccl.GetErrorString(r_));                     \
+      return PLUSS_ERR_HIP;                                                                          \
+    }                                                                                                \
+  } while (0)
+
+// per shard, the block all-gathered at the end of a one-shot pass: its
+// canonical table (GCAP keys, GCAP counts), traversed[8], flags[8]
+constexpr size_t GBLOCK = 2 * (size_t)GCAP + 16;
+constexpr int DVEC = 32;  // words per dense vector slot (DBINS used)
+
+__global__ void k_group_sum(const unsigned long long* __restrict__ vecs, int n, unsigned long long* __restrict__ out) {
+  const int i = threadIdx.x;
+  if (i >= (int)DBINS) return;
+  unsigned long long s = 0;
+  for (int j = 0; j < n; ++j) s += vecs[j * DVEC + i];
+  out[i] = s;
+}
+
+// a shard's traversed and flags words into its gathered block
+__global__ void k_group_block_tail(GTable g, unsigned long long* __restrict__ blk) {
+  const int i = threadIdx.x;
+  if (i < 8) blk[2 * GCAP + i] = g.trav[i];
+  else if (i < 16) blk[2 * GCAP + i] = g.flags[i - 8];
+}
+
+__global__ void k_group_row_fail(unsigned long long* row) { row[ROW_ERR] = 1; }
+
+}  // namespace pluss
+
+using namespace pluss;
+
+struct pluss_group {
+  pluss_cfg cfg;
+  Model m;
+  int ndev = 0, spd = 1;          // local devices, logical shards per device
+  int nranks = 1, rank0 = 0;      // RCCL ranks; the rank of local device 0
+  int nshards = 1;                // all shards of the job (nranks * spd)
+  std::vector<int> dev;           // local device ordinals
+  std::vector<pluss_ctx*> ctx;    // local shards, device-major
+  std::vector<ncclComm_t> comm;   // per local device
+  std::vector<hipStream_t> xs;    // per local device: the exchange stream
+  std::vector<hipEvent_t> ev;     // per local shard / device: join events
+  std::vector<unsigned long long*> rows;  // per device: nshards * ROW_W
+  std::vector<unsigned long long*> vec;   // per device: spd dense vectors, then the merged one
+  std::vector<unsigned long long*> blk;   // per device: nshards * GBLOCK
+  std::vector<unsigned long long*> list;  // per local shard: resident samples (pluss_group_expand)
+  std::vector<uint64_t> list_n;
+  std::vector<unsigned long long*> whole; // per device: uploaded whole lists (faithful, arbitrary order)
+  std::vector<uint64_t> whole_cap;
+  std::map<uint32_t, hipGraphExec_t> graphs;  // dense passes captured per batch size (one local device)
+};
+
+namespace pluss {
+
+static int gshard(const pluss_group* G, int d, int j) { return (G->rank0 + d) * G->spd + j; }
+static pluss_ctx* shard(pluss_group* G, int d, int j) { return G->ctx[(size_t)d * G->spd + j]; }
+
+static void group_free(pluss_group* G) {
+  for (int d = 0; d < G->ndev; ++d) {
+    (void)hipSetDevice(G->dev[d]);
+    if (d < (int)G->xs.size() && G->xs[d]) (void)hipStreamSynchronize(G->xs[d]);
+  }
+  for (auto& kv : G->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (size_t i = 0; i < G->ctx.size(); ++i) {
+    if (i < G->list.size() && G->list[i]) (void)hipFree(G->list[i]);
+    if (G->ctx[i]) pluss_ctx_destroy(G->ctx[i]);
+  }
+  for (int d = 0; d < G->ndev; ++d) {
+    (void)hipSetDevice(G->dev[d]);
+    for (auto* v : {&G->rows, &G->vec, &G->blk, &G->whole})
+      if (d < (int)v->size() && (*v)[d]) (void)hipFree((*v)[d]);
+    if (d < (int)G->comm.size() && G->comm[d] && g_rccl.ok) (void)g_rccl.CommDestroy(G->comm[d]);
+    if (d < (int)G->xs.size() && G->xs[d]) (void)hipStreamDestroy(G->xs[d]);
+  }
+  for (auto e : G->ev)
+    if (e) (void)hipEventDestroy(e);
+  delete G;
+}
+
+// contexts, streams, events and exchange buffers once the ranks are known
+static int group_setup(pluss_group* G) {
+  const int S = G->spd;
+  G->ctx.assign((size_t)G->ndev * S, nullptr);
+  G->list.assign(G->ctx.size(), nullptr);
+  G->list_n.assign(G->ctx.size(), 0);
+  G->xs.assign(G->ndev, nullptr);
+  G->ev.assign(G->ctx.size() + G->ndev, nullptr);
+  G->rows.assign(G->ndev, nullptr);
+  G->vec.assign(G->ndev, nullptr);
+  G->blk.assign(G->ndev, nullptr);
+  G->whole.assign(G->ndev, nullptr);
+  G->whole_cap.assign(G->ndev, 0);
+  for (int d = 0; d < G->ndev; ++d) {
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    for (int j = 0; j < S; ++j) {
+      pluss_cfg c = G->cfg;
+      c.device = G->dev[d];
+      if (int rc = pluss_ctx_create(&c, &G->ctx[(size_t)d * S + j])) return rc;
+    }
+    PLUSS_HIP_CHECK(hipStreamCreateWithFlags(&G->xs[d], hipStreamNonBlocking));
+    PLUSS_HIP_CHECK(hipMalloc((void**)&G->rows[d], (size_t)G->nshards * ROW_W * 8));
+    PLUSS_HIP_CHECK(hipMemset(G->rows[d], 0, (size_t)G->nshards * ROW_W * 8));
+    PLUSS_HIP_CHECK(hipMalloc((void**)&G->vec[d], (size_t)(S + 1) * DVEC * 8));
+    PLUSS_HIP_CHECK(hipMemset(G->vec[d], 0, (size_t)(S + 1) * DVEC * 8));
+    PLUSS_HIP_CHECK(hipMalloc((void**)&G->blk[d], (size_t)G->nshards * GBLOCK * 8));
+  }
+  for (auto& e : G->ev) PLUSS_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return PLUSS_OK;
+}
+
+static int group_check_cfg(const pluss_cfg* cfg, int32_t spd, Model* m) {
+  if (int rc = validate_cfg(cfg, m)) return rc;
+  if (spd < 1 || spd > 64) {
+    set_error("pluss_group: shards_per_device must be in [1, 64]");
+    return PLUSS_ERR_CONFIG;
+  }
+  return PLUSS_OK;
+}
+
+// every local shard's stream joins its device's exchange stream
+static int join_shards(pluss_group* G) {
+  for (int d = 0; d < G->ndev; ++d)
+    for (int j = 0; j < G->spd; ++j) {
+      const size_t i = (size_t)d * G->spd + j;
+      PLUSS_HIP_CHECK(hipEventRecord(G->ev[i], G->ctx[i]->stream));
+      PLUSS_HIP_CHECK(hipStreamWaitEvent(G->xs[d], G->ev[i], 0));
+    }
+  return PLUSS_OK;
+}
+// ... and forks back: every shard stream waits for its device's exchange
+static int fork_shards(pluss_group* G) {
+  for (int d = 0; d < G->ndev; ++d) {
+    hipEvent_t e = G->ev[G->ctx.size() + d];
+    PLUSS_HIP_CHECK(hipEventRecord(e, G->xs[d]));
+    for (int j = 0; j < G->spd; ++j) PLUSS_HIP_CHECK(hipStreamWaitEvent(G->ctx[(size_t)d * G->spd + j]->stream, e, 0));
+  }
+  return PLUSS_OK;
+}
+
+// in-place all-gather of per-shard blocks of `w` u64 words over the ranks
+// (each device holds every shard's slot; its own shards' slots are written)
+static int gather_blocks(pluss_group* G, std::vector<unsigned long long*>& buf, size_t w) {
+  if (int rc = join_shards(G)) return rc;
+  PLUSS_NCCL_CHECK(g_rccl.GroupStart());
+  for (int d = 0; d < G->ndev; ++d) {
+    unsigned long long* own = buf[d] + (size_t)(G->rank0 + d) * G->spd * w;
+    PLUSS_NCCL_CHECK(g_rccl.AllGather(own, buf[d], (size_t)G->spd * w, ncclUint64, G->comm[d], G->xs[d]));
+  }
+  PLUSS_NCCL_CHECK(g_rccl.GroupEnd());
+  return fork_shards(G);
+}
+
+static void shard_ranges(uint64_t c, int g, int S, uint64_t* first, uint64_t* n) {
+  const uint64_t lo = (uint64_t)((unsigned __int128)c * g / S), hi = (uint64_t)((unsigned __int128)c * (g + 1) / S);
+  *first = lo;
+  *n = hi - lo;
+}
+
+// The end of a one-shot pass: every shard's canonical table, traversed and
+// flags all-gathered, summed on the host (the same on every rank).  The first
+// error of a local shard wins; a flagged shard anywhere fails the pass.
+static int group_collect(pluss_group* G, int first_rc, const std::string& first_err, pluss_hist* out) {
+  for (int d = 0; d < G->ndev; ++d) {
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    for (int j = 0; j < G->spd; ++j) {
+      pluss_ctx* c = shard(G, d, j);
+      unsigned long long* b = G->blk[d] + (size_t)gshard(G, d, j) * GBLOCK;
+      if (int rc = pluss_dev_hist_export(c, (uint64_t*)b, (uint64_t*)(b + GCAP), GCAP, c->stream)) return rc;
+      hipLaunchKernelGGL(k_group_block_tail, dim3(1), dim3(64), 0, c->stream, c->g, b);
+      PLUSS_HIP_CHECK(hipGetLastError());
+    }
+  }
+  if (int rc = gather_blocks(G, G->blk, GBLOCK)) return rc;
+  std::vector<unsigned long long> h((size_t)G->nshards * GBLOCK);
+  PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
+  PLUSS_HIP_CHECK(hipMemcpyAsync(h.data(), G->blk[0], h.size() * 8, hipMemcpyDeviceToHost, G->xs[0]));
+  for (int d = 0; d < G->ndev; ++d) PLUSS_HIP_CHECK(hipStreamSynchronize(G->xs[d]));
+  if (first_rc) {
+    set_error(first_err);
+    return first_rc;
+  }
+  std::vector<uint64_t> keys, cnts;
+  keys.reserve((size_t)G->nshards * GCAP);
+  cnts.reserve((size_t)G->nshards * GCAP);
+  uint64_t trav[6] = {0, 0, 0, 0, 0, 0};
+  for (int g = 0; g < G->nshards; ++g) {
+    const unsigned long long* b = h.data() + (size_t)g * GBLOCK;
+    const unsigned long long* fl = b + 2 * GCAP + 8;
+    if (fl[1]) {
+      set_error("shard " + std::to_string(g) + ": malformed sample (ref > 5, an index >= N, or a wrong reference)");
+      return PLUSS_ERR_INPUT;
+    }
+    if (fl[0] & FLAG_SHARD) {
+      set_error("a key-range shard of this faithful pass failed (shard " + std::to_string(g) + " saw its error word)");
+      return PLUSS_ERR_PEER;
+    }
+    if (fl[0]) {
+      set_error("shard " + std::to_string(g) + ": histogram table overflow or stalled pass (flags " +
+                std::to_string(fl[0]) + ")");
+      return PLUSS_ERR_CAPACITY;
+    }
+    for (uint32_t i = 0; i < GCAP; ++i) {
+      if (b[i] == KEY_EMPTY || b[i] == KEY_NONE) break;  // sorted, empties last
+      keys.push_back(b[i]);
+      cnts.push_back(b[GCAP + i]);
+    }
+    for (int r = 0; r < 6; ++r) trav[r] += b[2 * GCAP + r];
+  }
+  if (int rc = pluss_hist_from_tables(keys.data(), cnts.data(), keys.size(), out)) return rc;
+  for (int r = 0; r < 6; ++r) out->traversed[r] = trav[r];
+  return PLUSS_OK;
+}
+
+static int group_reset(pluss_group* G) {
+  for (int d = 0; d < G->ndev; ++d) {
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    for (int j = 0; j < G->spd; ++j) {
+      pluss_ctx* c = shard(G, d, j);
+      if (int rc = pluss_dev_hist_reset(c, c->stream)) return rc;
+    }
+  }
+  return PLUSS_OK;
+}
+
+// one faithful key-range pass over the local shards, the rows exchanged
+// between the phases; `phase1(d, j, g, row)` runs a shard's first phase
+template <class F>
+static int group_faithful(pluss_group* G, bool selected, F&& phase1, int* frc, std::string* ferr) {
+  auto note = [&](int rc, int d, unsigned long long* row, pluss_ctx* c) {
+    if (!rc) return;
+    if (!*frc) {
+      *frc = rc;
+      *ferr = pluss_last_error();
+    }
+    hipLaunchKernelGGL(k_group_row_fail, dim3(1), dim3(1), 0, c->stream, row);  // every shard learns of it
+  };
+  auto each = [&](auto&& fn) {
+    for (int d = 0; d < G->ndev; ++d) {
+      (void)hipSetDevice(G->dev[d]);
+      for (int j = 0; j < G->spd; ++j) {
+        const int g = gshard(G, d, j);
+        pluss_ctx* c = shard(G, d, j);
+        unsigned long long* row = G->rows[d] + (size_t)g * ROW_W;
+        note(fn(c, d, j, g, (uint64_t*)row), d, row, c);
+      }
+    }
+  };
+  each([&](pluss_ctx* c, int d, int j, int g, uint64_t* row) { return phase1(c, d, j, g, row); });
+  if (int rc = gather_blocks(G, G->rows, ROW_W)) return rc;
+  if (selected) {
+    each([&](pluss_ctx* c, int d, int, int g, uint64_t* row) {
+      return pluss_dev_faithful_shards_local_selected(c, (const uint64_t*)G->rows[d], g, G->nshards, row, c->stream);
+    });
+    if (int rc = gather_blocks(G, G->rows, ROW_W)) return rc;
+  }
+  each([&](pluss_ctx* c, int d, int, int g, uint64_t* row) {
+    return pluss_dev_faithful_shards_carry(c, (const uint64_t*)G->rows[d], g, G->nshards, row, c->stream);
+  });
+  if (int rc = gather_blocks(G, G->rows, ROW_W)) return rc;
+  each([&](pluss_ctx* c, int d, int, int g, uint64_t* row) {
+    return pluss_dev_faithful_shards_cut(c, (const uint64_t*)G->rows[d], g, G->nshards, row, c->stream);
+  });
+  if (int rc = gather_blocks(G, G->rows, ROW_W)) return rc;
+  each([&](pluss_ctx* c, int d, int, int g, uint64_t*) {
+    return pluss_dev_faithful_shards_hist(c, (const uint64_t*)G->rows[d], g, G->nshards, c->stream);
+  });
+  return PLUSS_OK;
+}
+
+// dense vectors of the local shards summed per device, all-reduced over the ranks, on the exchange streams
+static int dense_merge(pluss_group* G) {
+  if (int rc = join_shards(G)) return rc;
+  for (int d = 0; d < G->ndev; ++d) {
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    hipLaunchKernelGGL(k_group_sum, dim3(1), dim3(64), 0, G->xs[d], (const unsigned long long*)G->vec[d], G->spd,
+                       G->vec[d] + (size_t)G->spd * DVEC);
+  }
+  PLUSS_HIP_CHECK(hipGetLastError());
+  PLUSS_NCCL_CHECK(g_rccl.GroupStart());
+  for (int d = 0; d < G->ndev; ++d) {
+    unsigned long long* v = G->vec[d] + (size_t)G->spd * DVEC;
+    PLUSS_NCCL_CHECK(g_rccl.AllReduce(v, v, DBINS, ncclUint64, ncclSum, G->comm[d], G->xs[d]));
+  }
+  PLUSS_NCCL_CHECK(g_rccl.GroupEnd());
+  return fork_shards(G);
+}
+
+// one dense pass over the resident lists, everything on the exchange streams (capturable)
+static int dense_pass_on_xs(pluss_group* G) {
+  for (int d = 0; d < G->ndev; ++d) {
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    for (int j = 0; j < G->spd; ++j) {
+      const size_t i = (size_t)d * G->spd + j;
+      if (int rc = pluss_dev_sampled_hist_dense(G->ctx[i], (const uint64_t*)G->list[i], G->list_n[i],
+                                                (uint64_t*)(G->vec[d] + (size_t)j * DVEC), G->xs[d]))
+        return rc;
+    }
+    hipLaunchKernelGGL(k_group_sum, dim3(1), dim3(64), 0, G->xs[d], (const unsigned long long*)G->vec[d], G->spd,
+                       G->vec[d] + (size_t)G->spd * DVEC);
+  }
+  PLUSS_HIP_CHECK(hipGetLastError());
+  PLUSS_NCCL_CHECK(g_rccl.GroupStart());
+  for (int d = 0; d < G->ndev; ++d) {
+    unsigned long long* v = G->vec[d] + (size_t)G->spd * DVEC;
+    PLUSS_NCCL_CHECK(g_rccl.AllReduce(v, v, DBINS, ncclUint64, ncclSum, G->comm[d], G->xs[d]));
+  }
+  PLUSS_NCCL_CHECK(g_rccl.GroupEnd());
+  return PLUSS_OK;
+}
+
+static int dense_result(pluss_group* G, uint64_t* counts) {
+  for (int d = 0; d < G->ndev; ++d) {
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    PLUSS_HIP_CHECK(hipStreamSynchronize(G->xs[d]));
+  }
+  PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
+  if (counts)
+    PLUSS_HIP_CHECK(hipMemcpy(counts, G->vec[0] + (size_t)G->spd * DVEC, DBINS * 8,
+                              hipMemcpyDeviceToHost));
+  return PLUSS_OK;
+}
+
+}  // namespace pluss
+
+extern "C" {
+
+int pluss_group_unique_id(uint8_t id[PLUSS_GROUP_ID_BYTES]) {
+  if (!id) return PLUSS_ERR_CONFIG;
+  Rccl* R = rccl();
+  if (!R) {
+    set_error(g_rccl.why);
+    return PLUSS_ERR_HIP;
+  }
+  ncclUniqueId u;
+  PLUSS_NCCL_CHECK(R->GetUniqueId(&u));
+  std::memcpy(id, u.internal, PLUSS_GROUP_ID_BYTES);
+  return PLUSS_OK;
+}
+
+int pluss_group_create(const pluss_cfg* cfg, const int32_t* devices, int32_t ndev, int32_t shards_per_device,
+                       pluss_group** out) {
+  if (!out) return PLUSS_ERR_CONFIG;
+  *out = nullptr;
+  Model m;
+  if (int rc = group_check_cfg(cfg, shards_per_device, &m)) return rc;
+  int nd = 0;
+  PLUSS_HIP_CHECK(hipGetDeviceCount(&nd));
+  if (!devices || ndev < 1 || ndev > nd) {
+    set_error("pluss_group_create: need 1 <= ndev <= " + std::to_string(nd) + " device ordinals");
+    return PLUSS_ERR_CONFIG;
+  }
+  for (int i = 0; i < ndev; ++i)
+    for (int k = 0; k < i; ++k)
+      if (devices[i] < 0 || devices[i] >= nd || devices[i] == devices[k]) {
+        set_error("pluss_group_create: device ordinals must be distinct and in range (several shards of one "
+                  "device: shards_per_device)");
+        return PLUSS_ERR_CONFIG;
+      }
+  if (devices[0] < 0 || devices[0] >= nd) {
+    set_error("pluss_group_create: device ordinal out of range");
+    return PLUSS_ERR_CONFIG;
+  }
+  Rccl* R = rccl();
+  if (!R) {
+    set_error(g_rccl.why);
+    return PLUSS_ERR_HIP;
+  }
+  pluss_group* G = new pluss_group();
+  G->cfg = *cfg;
+  G->m = m;
+  G->ndev = ndev;
+  G->spd = shards_per_device;
+  G->nranks = ndev;
+  G->rank0 = 0;
+  G->nshards = ndev * shards_per_device;
+  G->dev.assign(devices, devices + ndev);
+  G->comm.assign(ndev, nullptr);
+  if (int rc = group_setup(G)) {
+    const std::string e = pluss_last_error();
+    group_free(G);
+    set_error(e);
+    return rc;
+  }
+  ncclResult_t r = R->CommInitAll(G->comm.data(), ndev, G->dev.data());
+  if (r != ncclSuccess) {
+    const std::string e = std::string("ncclCommInitAll: ") + R->GetErrorString(r);
+    G->comm.assign(ndev, nullptr);
+    group_free(G);
+    set_error(e);
+    return PLUSS_ERR_HIP;
+  }
+  *out = G;
+  return PLUSS_OK;
+}
+
+int pluss_group_create_rank(const pluss_cfg* cfg, int32_t nranks, int32_t rank, const uint8_t id[PLUSS_GROUP_ID_BYTES],
+                            int32_t shards_per_device, pluss_group** out) {
+  if (!out || !id) return PLUSS_ERR_CONFIG;
+  *out = nullptr;
+  Model m;
+  if (int rc = group_check_cfg(cfg, shards_per_device, &m)) return rc;
+  if (nranks < 1 || rank < 0 || rank >= nranks) {
+    set_error("pluss_group_create_rank: need 0 <= rank < nranks");
+    return PLUSS_ERR_CONFIG;
+  }
+  int nd = 0;
+  PLUSS_HIP_CHECK(hipGetDeviceCount(&nd));
+  if (cfg->device < 0 || cfg->device >= nd) {
+    set_error("pluss_group_create_rank: cfg.device out of range");
+    return PLUSS_ERR_CONFIG;
+  }
+  Rccl* R = rccl();
+  if (!R) {
+    set_error(g_rccl.why);
+    return PLUSS_ERR_HIP;
+  }
+  pluss_group* G = new pluss_group();
+  G->cfg = *cfg;
+  G->m = m;
+  G->ndev = 1;
+  G->spd = shards_per_device;
+  G->nranks = nranks;
+  G->rank0 = rank;
+  G->nshards = nranks * shards_per_device;
+  G->dev.assign(1, cfg->device);
+  G->comm.assign(1, nullptr);
+  if (int rc = group_setup(G)) {
+    const std::string e = pluss_last_error();
+    group_free(G);
+    set_error(e);
+    return rc;
+  }
+  ncclUniqueId u;
+  std::memcpy(u.internal, id, PLUSS_GROUP_ID_BYTES);
+  (void)hipSetDevice(cfg->device);
+  ncclResult_t r = R->CommInitRank(&G->comm[0], nranks, u, rank);
+  if (r != ncclSuccess) {
+    const std::string e = std::string("ncclCommInitRank: ") + R->GetErrorString(r);
+    G->comm[0] = nullptr;
+    group_free(G);
+    set_error(e);
+    return PLUSS_ERR_HIP;
+  }
+  *out = G;
+  return PLUSS_OK;
+}
+
+int pluss_group_destroy(pluss_group* G) {
+  if (G) group_free(G);
+  return PLUSS_OK;
+}
+
+int pluss_group_shards(const pluss_group* G, int32_t* local, int32_t* total) {
+  if (!G) return PLUSS_ERR_CONFIG;
+  if (local) *local = G->ndev * G->spd;
+  if (total) *total = G->nshards;
+  return PLUSS_OK;
+}
+
+int pluss_group_expand(pluss_group* G, uint64_t seed, const uint64_t counts[6]) {
+  if (!G || !counts) return PLUSS_ERR_CONFIG;
+  for (int d = 0; d < G->ndev; ++d) {
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    for (int j = 0; j < G->spd; ++j) {
+      const size_t i = (size_t)d * G->spd + j;
+      const int g = gshard(G, d, j);
+      uint64_t f[6], n[6], tot = 0;
+      for (int r = 0; r < 6; ++r) {
+        shard_ranges(counts[r], g, G->nshards, &f[r], &n[r]);
+        tot += n[r];
+      }
+      PLUSS_HIP_CHECK(hipStreamSynchronize(G->ctx[i]->stream));
+      if (G->list[i]) (void)hipFree(G->list[i]);
+      G->list[i] = nullptr;
+      G->list_n[i] = 0;
+      PLUSS_HIP_CHECK(hipMalloc((void**)&G->list[i], (tot ? tot : 1) * 8));
+      uint64_t off = 0;
+      for (int r = 0; r < 6; ++r) {
+        if (int rc = pluss_dev_expand(G->ctx[i], seed, r, f[r], n[r], (uint64_t*)G->list[i] + off, nullptr)) return rc;
+        off += n[r];
+      }
+      G->list_n[i] = tot;
+    }
+  }
+  for (int d = 0; d < G->ndev; ++d)
+    for (int j = 0; j < G->spd; ++j) PLUSS_HIP_CHECK(hipStreamSynchronize(shard(G, d, j)->stream));
+  return PLUSS_OK;
+}
+
+int pluss_group_dense(pluss_group* G, uint32_t passes, uint64_t counts[PLUSS_DENSE_BINS + 1]) {
+  if (!G) return PLUSS_ERR_CONFIG;
+  if (!G->m.fast) {
+    set_error("pluss_group_dense: needs N % (cls/ds) == 0");
+    return PLUSS_ERR_CONFIG;
+  }
+  for (size_t i = 0; i < G->ctx.size(); ++i)
+    if (!G->list[i]) {
+      set_error("pluss_group_dense: no resident lists (pluss_group_expand first)");
+      return PLUSS_ERR_CONFIG;
+    }
+  constexpr uint32_t BATCH = 16;  // passes per captured graph
+  uint32_t left = passes;
+  if (G->ndev == 1 && passes >= BATCH) {
+    // one local device: BATCH passes (kernels and RCCL all-reduces) replayed from one HIP graph
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
+    hipGraphExec_t ex = nullptr;
+    auto it = G->graphs.find(BATCH);
+    if (it != G->graphs.end()) {
+      ex = it->second;
+    } else {
+      PLUSS_HIP_CHECK(hipStreamBeginCapture(G->xs[0], hipStreamCaptureModeThreadLocal));
+      int rc = PLUSS_OK;
+      for (uint32_t k = 0; k < BATCH && !rc; ++k) rc = dense_pass_on_xs(G);
+      hipGraph_t gr = nullptr;
+      const hipError_t e = hipStreamEndCapture(G->xs[0], &gr);
+      if (rc) return rc;
+      if (e != hipSuccess) {
+        set_error(std::string("pluss_group_dense: graph capture: ") + hipGetErrorString(e));
+        return PLUSS_ERR_HIP;
+      }
+      const hipError_t e2 = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(gr);
+      if (e2 != hipSuccess) {
+        set_error(std::string("pluss_group_dense: graph instantiate: ") + hipGetErrorString(e2));
+        return PLUSS_ERR_HIP;
+      }
+      G->graphs[BATCH] = ex;
+    }
+    for (; left >= BATCH; left -= BATCH) PLUSS_HIP_CHECK(hipGraphLaunch(ex, G->xs[0]));
+  }
+  for (; left; --left)
+    if (int rc = dense_pass_on_xs(G)) return rc;
+  if (int rc = dense_result(G, counts)) return rc;
+  for (size_t i = 0; i < G->ctx.size(); ++i) {  // malformed samples also raise at the handle's flags
+    unsigned int f[2] = {0, 0};
+    PLUSS_HIP_CHECK(hipMemcpy(f, G->ctx[i]->g.flags, sizeof f, hipMemcpyDeviceToHost));
+    if (f[1]) {
+      set_error("pluss_group_dense: malformed sample in shard " + std::to_string(i));
+      return PLUSS_ERR_INPUT;
+    }
+  }
+  return PLUSS_OK;
+}
+
+int pluss_group_gen_count_dense(pluss_group* G, uint64_t seed, const uint64_t totals[6],
+                                uint64_t counts[PLUSS_DENSE_BINS + 1]) {
+  if (!G || !totals) return PLUSS_ERR_CONFIG;
+  for (int d = 0; d < G->ndev; ++d) {
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    for (int j = 0; j < G->spd; ++j) {
+      const int g = gshard(G, d, j);
+      uint64_t f[6], n[6];
+      for (int r = 0; r < 6; ++r) shard_ranges(totals[r], g, G->nshards, &f[r], &n[r]);
+      pluss_ctx* c = shard(G, d, j);
+      if (int rc = pluss_dev_gen_count_dense(c, seed, totals, f, n, (uint64_t*)(G->vec[d] + (size_t)j * DVEC),
+                                             c->stream))
+        return rc;
+    }
+  }
+  if (int rc = dense_merge(G)) return rc;
+  return dense_result(G, counts);
+}
+
+int pluss_group_sampled_hist(pluss_group* G, const uint64_t* samples, uint64_t n, pluss_hist* out) {
+  if (!G || !out || (n && !samples)) return PLUSS_ERR_CONFIG;
+  if (int rc = group_reset(G)) return rc;
+  int frc = PLUSS_OK;
+  std::string ferr;
+  const int S = G->nshards;
+  if (G->cfg.mode == PLUSS_MODE_CLEAN) {
+    // shard g: the slice [n*g/S, n*(g+1)/S) of the list, any shape
+    for (int d = 0; d < G->ndev; ++d) {
+      PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+      for (int j = 0; j < G->spd; ++j) {
+        const size_t i = (size_t)d * G->spd + j;
+        uint64_t f, m;
+        shard_ranges(n, gshard(G, d, j), S, &f, &m);
+        PLUSS_HIP_CHECK(hipStreamSynchronize(G->ctx[i]->stream));
+        if (G->list[i]) (void)hipFree(G->list[i]);
+        G->list[i] = nullptr;
+        G->list_n[i] = 0;
+        PLUSS_HIP_CHECK(hipMalloc((void**)&G->list[i], (m ? m : 1) * 8));
+        PLUSS_HIP_CHECK(hipMemcpyAsync(G->list[i], samples + f, m * 8, hipMemcpyHostToDevice, G->ctx[i]->stream));
+        G->list_n[i] = m;
+        const int rc = pluss_dev_sampled_hist(G->ctx[i], (const uint64_t*)G->list[i], m, G->ctx[i]->stream);
+        if (rc && !frc) {
+          frc = rc;
+          ferr = pluss_last_error();
+        }
+      }
+    }
+    return group_collect(G, frc, ferr, out);
+  }
+  // faithful: r10's six samplers, each over its reference's samples in list order
+  std::vector<uint64_t> per[6];
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint32_t r = (uint32_t)(samples[i] >> 60);
+    if (r > 5) {
+      set_error("malformed sample: ref > 5");
+      return PLUSS_ERR_INPUT;
+    }
+    per[r].push_back(samples[i]);
+  }
+  uint64_t totals[6], all = 0;
+  for (int r = 0; r < 6; ++r) all += (totals[r] = per[r].size());
+  if ((uint64_t)G->cfg.n % ((uint64_t)G->cfg.chunk * (uint64_t)G->cfg.threads) != 0) {
+    set_error("faithful mode needs N % (chunk*threads) == 0 (lockstep interleaving order)");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (!G->m.fast) {
+    // (key, sink) pairs (N % (cls/ds) != 0) are not key-range sharded: the job's first shard runs every sampler
+    if (G->rank0 == 0) {
+      PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
+      pluss_ctx* c = G->ctx[0];
+      for (int r = 0; r < 6 && !frc; ++r) {
+        if (per[r].empty()) continue;
+        uint64_t* dl = nullptr;
+        PLUSS_HIP_CHECK(hipMalloc((void**)&dl, per[r].size() * 8));
+        PLUSS_HIP_CHECK(hipMemcpy(dl, per[r].data(), per[r].size() * 8, hipMemcpyHostToDevice));
+        frc = pluss_dev_faithful_hist(c, r, dl, per[r].size(), c->stream);
+        if (frc) ferr = pluss_last_error();
+        PLUSS_HIP_CHECK(hipStreamSynchronize(c->stream));
+        (void)hipFree(dl);
+      }
+    }
+    return group_collect(G, frc, ferr, out);
+  }
+  // every device holds the whole lists once; each shard keeps its key range
+  uint64_t key_end = 0;
+  if (int rc = pluss_faithful_key_space(&G->cfg, &key_end)) return rc;
+  for (int d = 0; d < G->ndev; ++d) {
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    if (G->whole_cap[d] < all) {
+      for (int j = 0; j < G->spd; ++j) PLUSS_HIP_CHECK(hipStreamSynchronize(shard(G, d, j)->stream));
+      if (G->whole[d]) (void)hipFree(G->whole[d]);
+      G->whole[d] = nullptr;
+      G->whole_cap[d] = 0;
+      PLUSS_HIP_CHECK(hipMalloc((void**)&G->whole[d], (all ? all : 1) * 8));
+      G->whole_cap[d] = all;
+    }
+    uint64_t off = 0;
+    for (int r = 0; r < 6; ++r) {
+      PLUSS_HIP_CHECK(hipMemcpyAsync(G->whole[d] + off, per[r].data(), per[r].size() * 8, hipMemcpyHostToDevice, G->xs[d]));
+      off += per[r].size();
+    }
+    PLUSS_HIP_CHECK(hipStreamSynchronize(G->xs[d]));
+  }
+  auto sel = [&](pluss_ctx* c, int d, int, int g, uint64_t* row) {
+    const uint64_t lo = (uint64_t)((unsigned __int128)key_end * g / S);
+    const uint64_t hi = (uint64_t)((unsigned __int128)key_end * (g + 1) / S);
+    return pluss_dev_faithful_shards_select(c, (const uint64_t*)G->whole[d], totals, lo, hi, row, c->stream);
+  };
+  if (int rc = group_faithful(G, true, sel, &frc, &ferr)) return rc;
+  return group_collect(G, frc, ferr, out);
+}
+
+int pluss_group_gen_faithful(pluss_group* G, uint64_t seed, const uint64_t totals[6], pluss_hist* out) {
+  if (!G || !totals || !out) return PLUSS_ERR_CONFIG;
+  uint64_t key_end = 0;
+  if (int rc = pluss_faithful_key_space(&G->cfg, &key_end)) return rc;
+  if (int rc = group_reset(G)) return rc;
+  int frc = PLUSS_OK;
+  std::string ferr;
+  const int S = G->nshards;
+  auto gen = [&](pluss_ctx* c, int, int, int g, uint64_t* row) {
+    const uint64_t lo = (uint64_t)((unsigned __int128)key_end * g / S);
+    const uint64_t hi = (uint64_t)((unsigned __int128)key_end * (g + 1) / S);
+    uint64_t f[6] = {0, 0, 0, 0, 0, 0}, m[6] = {0, 0, 0, 0, 0, 0};
+    for (int r = 0; r < 6; ++r) {
+      if (!totals[r]) continue;
+      uint64_t a = 0, b = 0;
+      if (int rc = pluss_keyorder_index_range(&G->cfg, seed, r, totals[r], lo, hi, &a, &b)) return rc;
+      f[r] = a;
+      m[r] = b - a;
+    }
+    return pluss_dev_faithful_shards_local(c, nullptr, seed, totals, f, m, row, c->stream);
+  };
+  if (int rc = group_faithful(G, false, gen, &frc, &ferr)) return rc;
+  return group_collect(G, frc, ferr, out);
+}
+
+}  // extern "C"

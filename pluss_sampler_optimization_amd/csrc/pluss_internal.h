@@ -51,6 +51,11 @@ struct GTable {
   unsigned long long* dbins;    // NBROW * BSTRIDE: dense pass, per-row words (zero between passes)
   unsigned long long* dtot;     // BSTRIDE: dense pass, per-bin words over the rows (zero between passes)
 };
+// bits of flags[0] (each reported by its own message at the next fetch)
+constexpr unsigned int FLAG_OVERFLOW = 1u;  // more distinct histogram keys than the tables hold
+constexpr unsigned int FLAG_LOOKBACK = 2u;  // a faithful chunk's predecessor never published (stalled pass)
+constexpr unsigned int FLAG_SHARD = 4u;     // a key-range shard of this pass failed (its row's error word)
+constexpr unsigned int FLAG_SORT = 8u;      // the bucket sort's plan exceeded its capacity (input left unsorted)
 constexpr size_t DB_OFF = (2 * (size_t)(GCAP + NREP * RCAP) + NBROW * BSTRIDE + 4 + 8 + BSTRIDE - 1) / BSTRIDE * BSTRIDE;
 constexpr size_t TABLE_WORDS = DB_OFF + (size_t)(NBROW + 1) * BSTRIDE;
 constexpr size_t TABLE_BYTES = TABLE_WORDS * 8;
@@ -73,18 +78,11 @@ struct FaithfulBufs {
   unsigned int* cflag = nullptr;  // per chunk: the epoch of the pass that published cval (zeroed once)
   uint32_t epoch = 0;             // passes run on these buffers
   unsigned long long* shrec = nullptr;  // key-range shards: per reference the pass-3 record; staging words
+  unsigned long long* xin = nullptr;    // key-range shards: this shard's exchange inputs (XIN_*), then 8 counters
   unsigned long long* fslot = nullptr;  // per reference: the main-table slot of its -1 (cold) key
   // the radix source's bucket sort (pluss_sort.h): its histograms, parents, chunk map, deep items
   uint64_t sbcap = 0;
   unsigned char* sbuf = nullptr;
-};
-
-// state of a key-range shard between the phases of pluss_dev_faithful_shard_*
-struct FaithShard {
-  int phase = 0;  // last completed phase (1 keys, 2 starts, 3 cut)
-  int32_t ref = 0;
-  uint64_t n = 0, j_off = 0, n_total = 0;
-  unsigned long long pmax_in = 0, max_sink = 0;
 };
 
 struct FaShards;  // a key-range shard's state between the phases of pluss_dev_faithful_shards_* (pluss_faithful.h)
@@ -101,7 +99,6 @@ struct pluss_ctx {
   unsigned long long *d_exp_keys, *d_exp_counts;  // GCAP each, canonical export
   unsigned int* d_exp_n;
   pluss::FaithfulBufs fb;
-  pluss::FaithShard fsh;
   pluss::FaShards* fsh2;  // created on first use (faith_shards_local), freed by faith_shards_free
   pluss::FaithfulBufs fbr[6];  // per-reference buffers of pluss_dev_faithful_hist_refs
   hipStream_t fst[6];          // ... and its streams (created on first use)
@@ -161,17 +158,20 @@ int diag_sort_words(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint
 int launch_faithful_sorted(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, hipStream_t s);
 int launch_faithful_sorted_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64_t* counts, hipStream_t s);
 int launch_gen_faithful_refs(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t s);
-int faith_shard_keys(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples, uint64_t n, uint64_t lo, uint64_t hi,
-                     pluss_faith_shard* out, hipStream_t s);
-int faith_shard_starts(pluss_ctx* ctx, uint64_t j_off, uint64_t pmax_in, pluss_faith_shard* out, hipStream_t s);
-int faith_shard_cut(pluss_ctx* ctx, uint64_t s_off, uint64_t n_total, pluss_faith_shard* out, hipStream_t s);
-int faith_shard_hist(pluss_ctx* ctx, uint64_t cut, uint64_t next_first_key, int is_last, hipStream_t s);
-// key-range shards of the single-read pipeline (all six references at once)
+// key-range shards of the single-read pipeline (all six references at once;
+// summary rows in device memory, include/pluss_gpu.h PLUSS_SHARD_ROW)
 int faith_shards_local(pluss_ctx* ctx, const uint64_t* d_samples, uint64_t seed, const uint64_t* totals,
-                       const uint64_t* first, const uint64_t* n, uint64_t* max_sink, hipStream_t s);
-int faith_shards_carry(pluss_ctx* ctx, const uint64_t* carry_in, uint64_t* starts, hipStream_t s);
-int faith_shards_cut(pluss_ctx* ctx, const uint64_t* starts_before, uint64_t* cut, hipStream_t s);
-int faith_shards_hist(pluss_ctx* ctx, const uint64_t* cut, const int32_t* is_last, hipStream_t s);
+                       const uint64_t* first, const uint64_t* n, uint64_t* d_row, hipStream_t s);
+int faith_shards_select(pluss_ctx* ctx, const uint64_t* d_lists, const uint64_t* totals, uint64_t key_lo,
+                        uint64_t key_hi, uint64_t* d_row, hipStream_t s);
+int faith_shards_local_selected(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards,
+                                uint64_t* d_row, hipStream_t s);
+int faith_shards_carry(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards, uint64_t* d_row,
+                       hipStream_t s);
+int faith_shards_cut(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards, uint64_t* d_row,
+                     hipStream_t s);
+int faith_shards_hist(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards, hipStream_t s);
+void faith_shards_abandon(pluss_ctx* ctx);  // a one-GPU faithful call ends any half-finished shard pass
 void faith_shards_free(pluss_ctx* ctx);
 
 }  // namespace pluss

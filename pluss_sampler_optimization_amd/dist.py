@@ -16,16 +16,18 @@ of a pass is a dense vector of PLUSS_DENSE_BINS (ref, case) counts
 merge is one element-wise all-reduce of DENSE_BINS + 1 int64 words
 (sharded_clean_dense) -- the bench's multi-GPU step.
 
-Faithful mode (one r10 sampler_<REF> with its cross-sample queue semantics)
-needs one global key order, so it is sharded by contiguous ranges of the sort
-key a*T+tid instead: every rank reads the whole per-reference
-list, keeps and sorts its key range, and four small all-gathers of per-shard
-summaries (count / first key / max sink, start count, cut candidate) carry
-the scan state across shards (include/pluss_gpu.h, pluss_dev_faithful_shard_*).
+Faithful mode (r10's six sampler_<REF> with their cross-sample queue
+semantics) needs one global key order, so it is sharded by contiguous ranges
+of the sort key a*T+tid instead.  Each phase of
+pluss_dev_faithful_shards_* writes this rank's summary row in device memory;
+the rows are all-gathered between phases (over RCCL the whole pass runs
+without a host round trip) and the next phase derives its inputs from them on
+the device.  The same protocol runs inside libpluss_gpu.so for one-process
+multi-GPU callers (pluss_group_*, csrc/pluss_group.hip).
 """
 import numpy as np
 
-from ._lib import DENSE_BINS, PlussError
+from ._lib import DENSE_BINS, SHARD_ROW, SHARD_ROW_ERR, PlussError
 from .api import (REFS, Context, Histogram, faithful_key_space, hist_from_dense, hist_from_tables,
                   keyorder_index_range)
 
@@ -172,133 +174,156 @@ def torch_allgather(group=None, device=None):
     return allgather
 
 
-def faithful_shard_protocol(shard, ref, d_samples, n, key_lo, key_hi, rank, allgather, stream=None, err=None):
-    """The four phases of a key-range-sharded faithful sampler on `shard` (a
-    Context, or any object with the same faithful_shard_* methods), exchanging
-    the per-shard summaries with `allgather`.  Returns (n_total, cut).
+class DeviceRows:
+    """The summary rows of a key-range-sharded faithful pass on this rank's
+    GPU: `row` (this shard's SHARD_ROW words) and `rows` (all shards', in rank
+    order) as device pointers for the pluss_dev_faithful_shards_* phases.
+    exchange() all-gathers them: over RCCL on the device, ordered with the
+    library's launches on the current stream (no host round trip); over gloo
+    (several ranks sharing one GPU in tests) through host copies."""
 
-    Every exchange carries an error word: a rank whose phase raised (or that
-    enters with `err`, e.g. from generating its slice) still takes part in the
-    exchange, and then every rank raises at that same exchange -- no rank is
-    left waiting in a later collective."""
-    def exchange(vals):
+    def __init__(self, world, dev, group=None):
+        import torch
+        import torch.distributed as dist
+        self.group, self.world = group, world
+        self.nccl = dist.get_backend(group) == "nccl"
+        self._row = torch.zeros(SHARD_ROW, dtype=torch.int64, device=dev)
+        self._rows = torch.zeros(world * SHARD_ROW, dtype=torch.int64, device=dev)
+        self.row, self.rows = self._row.data_ptr(), self._rows.data_ptr()
+
+    def fail(self):
+        self._row[SHARD_ROW_ERR] = 1
+
+    def exchange(self):
+        import torch
+        import torch.distributed as dist
+        if self.nccl:
+            dist.all_gather_into_tensor(self._rows, self._row, group=self.group)
+            return
+        torch.cuda.current_stream(self._row.device).synchronize()
+        out = torch.empty(self.world * SHARD_ROW, dtype=torch.int64)
+        dist.all_gather_into_tensor(out, self._row.cpu(), group=self.group)
+        self._rows.copy_(out)
+
+
+def faithful_shards_protocol(shard, phase1, rank, world, rx, stream=None, err=None, selected=False):
+    """The phases of a key-range-sharded faithful pass on `shard` (a Context,
+    or any object with the same faithful_shards_* methods), the rows exchanged
+    by `rx` (DeviceRows, or a host stand-in with row / rows / fail / exchange)
+    between phases:
+      phase1(row)  this shard's first phase (faithful_shards_local over
+                   key-ordered or generated slices, or faithful_shards_select
+                   over arbitrary-order lists, then -- selected=True --
+                   faithful_shards_local_selected after the first exchange);
+      carry, cut, hist, with the gathered rows of all shards.
+    A rank whose phase raises (or that enters with `err`) marks its row failed
+    and still takes part in every exchange; the other ranks' device phases see
+    the error word and their fetch raises (PLUSS_ERR_PEER), so no rank waits
+    forever.  Returns this rank's error (None if it ran every phase)."""
+    def run(fn, *args):
         nonlocal err
-        g = allgather([1 if err is not None else 0] + list(vals))
+        if err is None:
+            try:
+                fn(*args)
+            except Exception as e:  # noqa: BLE001 -- reported after the pass, on every rank
+                err = e
         if err is not None:
-            raise err
-        if any(x[0] for x in g):
-            raise PlussError("another rank's faithful shard pass failed")
-        return [x[1:] for x in g]
-
-    def phase(fn, *args, default):
-        nonlocal err
-        if err is not None:
-            return default
-        try:
-            return fn(*args)
-        except Exception as e:  # noqa: BLE001 -- re-raised at the next exchange, on every rank
-            err = e
-            return default
-    m, first, mx = phase(shard.faithful_shard_keys, ref, d_samples, n, key_lo, key_hi, stream,
-                         default=(0, KEY_EMPTY, 0))
-    g = exchange([m, first, mx])
-    j_off = sum(x[0] for x in g[:rank])
-    n_total = sum(x[0] for x in g)
-    pmax_in = max([x[2] for x in g[:rank] if x[0] > 0], default=0)
-    later = [x for x in g[rank + 1:] if x[0] > 0]
-    next_first = later[0][1] if later else KEY_EMPTY
-    ns = phase(shard.faithful_shard_starts, j_off, pmax_in, stream, default=0)
-    s_off = sum(x[0] for x in exchange([ns])[:rank])
-    c = phase(shard.faithful_shard_cut, s_off, n_total, stream, default=n_total)
-    cut = min(x[0] for x in exchange([c]))
-    phase(shard.faithful_shard_hist, cut, next_first, not later, stream, default=None)
-    exchange([])  # the last phase's error, before the caller's merge collectives
-    return n_total, cut
+            rx.fail()
+    run(phase1, rx.row)
+    rx.exchange()
+    if selected:
+        run(shard.faithful_shards_local_selected, rx.rows, rank, world, rx.row, stream)
+        rx.exchange()
+    run(shard.faithful_shards_carry, rx.rows, rank, world, rx.row, stream)
+    rx.exchange()
+    run(shard.faithful_shards_cut, rx.rows, rank, world, rx.row, stream)
+    rx.exchange()
+    run(shard.faithful_shards_hist, rx.rows, rank, world, stream)
+    return err
 
 
-def _export_fetch(ctx, keys, cnts, sp, dev):
-    """Export the handle's canonical table and read its flags: (traversed, error or None)."""
-    import torch
-    try:
-        ctx.export(keys.data_ptr(), cnts.data_ptr(), TABLE_CAP, sp)
-        torch.cuda.synchronize(dev)
-        return ctx.fetch().traversed, None
-    except Exception as e:  # noqa: BLE001 -- raised on every rank by raise_together
-        return [0] * 6, e
-
-
-def sharded_faithful_hist(cfg, samples_by_ref, group=None, stream=None):
-    """Faithful mode over key-range shards, one GPU per rank.
-
-    samples_by_ref: {ref: device int64 tensor holding that reference's whole
-    sample list} (identical on every rank).  Returns the merged Histogram,
-    with `traversed` summed over ranks (identical on all ranks)."""
+def merge_results(ctx, err, dev, group=None):
+    """The end of a sharded faithful pass: this rank's canonical table,
+    traversed and error word, all-gathered in ONE collective and summed on
+    the host (the same Histogram on every rank).  Raises on every rank if any
+    rank failed."""
     import torch
     import torch.distributed as dist
-    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    world = dist.get_world_size(group)
     nccl = dist.get_backend(group) == "nccl"
-    dev = torch.device("cuda", cfg.device)
-    ag = torch_allgather(group, dev if nccl else "cpu")
-    lo, hi = key_range(faithful_key_space(cfg), rank, world)
-    sp = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-    keys = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
-    cnts = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
-    with Context(cfg) as ctx:
-        ctx.reset(sp)
-        for ref, t in samples_by_ref.items():
-            faithful_shard_protocol(ctx, ref, t.data_ptr(), t.numel(), lo, hi, rank, ag, sp)
-        trav, err = _export_fetch(ctx, keys, cnts, sp, dev)
-    raise_together(err, group, dev if nccl else None)
-    tsum = [sum(col) % (1 << 64) for col in zip(*ag(trav))]
+    W = 2 * TABLE_CAP + 8
+    blk = torch.zeros(W, dtype=torch.int64, device=dev)
+    trav = [0] * 6
+    if err is None:
+        try:
+            sp = torch.cuda.current_stream(dev).cuda_stream
+            ctx.export(blk.data_ptr(), blk.data_ptr() + 8 * TABLE_CAP, TABLE_CAP, sp)
+            trav = ctx.fetch().traversed  # the pass's one host wait; raises on this rank's flags
+        except Exception as e:  # noqa: BLE001
+            err = e
+    tail = np.array(trav + [1 if err is not None else 0, 0], dtype=np.uint64).view(np.int64)
+    blk[2 * TABLE_CAP:] = torch.from_numpy(tail).to(dev)
     if not nccl:
-        keys, cnts = keys.cpu(), cnts.cpu()
-    h = allgather_tables(keys, cnts, group)
+        blk = blk.cpu()
+    out = torch.empty(world * W, dtype=torch.int64, device=blk.device)
+    dist.all_gather_into_tensor(out, blk, group=group)
+    g = out.cpu().numpy().view(np.uint64).reshape(world, W)
+    if err is not None:
+        raise err
+    if g[:, 2 * TABLE_CAP + 6].any():
+        raise PlussError("another rank's faithful shard pass failed")
+    h = merge_tables(g[:, :TABLE_CAP], g[:, TABLE_CAP:2 * TABLE_CAP])
+    tsum = [int(x) for x in g[:, 2 * TABLE_CAP:2 * TABLE_CAP + 6].sum(axis=0, dtype=np.uint64)]
     return Histogram(h.bins, tsum)
 
 
-def faithful_shards_protocol(shard, d_samples, seed, totals, first, n, rank, allgather, stream=None, err=None):
-    """Faithful mode over key-range shards of the single-read pipeline, all six
-    references at once (pluss_dev_faithful_shards_*): `shard` (a Context, or
-    any object with the same faithful_shards_* methods) holds this rank's
-    slices [first[r], first[r] + n[r]) of the six key-ordered lists of
-    totals[r] samples (d_samples; None: generated), and three exchanges of
-    six-word summaries carry the scan across the ranks:
-      1. (n, largest sink) -> the largest sink of the earlier ranks = the carry;
-      2. the start counts -> the starts before this rank;
-      3. the first Q1 cut candidates -> the global cut (their minimum).
-    Every exchange carries an error word, as in faithful_shard_protocol.
-    Returns the global cuts."""
-    def exchange(vals):
-        nonlocal err
-        g = allgather([1 if err is not None else 0] + [int(v) for v in vals])
-        if err is not None:
-            raise err
-        if any(x[0] for x in g):
-            raise PlussError("another rank's faithful shard pass failed")
-        return [x[1:] for x in g]
+def _open(cfg, sp):
+    """(Context, None), or (None, the error): a rank that cannot even open its
+    handle (e.g. out of memory) still takes part in every exchange of the pass
+    with its row marked failed, so the other ranks do not wait forever."""
+    try:
+        ctx = Context(cfg)
+    except Exception as e:  # noqa: BLE001 -- reported after the pass, on every rank
+        return None, e
+    try:
+        ctx.reset(sp)
+    except Exception as e:  # noqa: BLE001
+        ctx.close()
+        return None, e
+    return ctx, None
 
-    def phase(fn, *args, default):
-        nonlocal err
-        if err is not None:
-            return default
-        try:
-            return fn(*args)
-        except Exception as e:  # noqa: BLE001 -- re-raised at the next exchange, on every rank
-            err = e
-            return default
-    mx = phase(shard.faithful_shards_local, d_samples, seed, totals, first, n, stream, default=[0] * 6)
-    g = exchange(list(n) + list(mx))
-    carry = [max([x[6 + r] for x in g[:rank] if x[r] > 0], default=0) for r in range(6)]
-    last = [not any(x[r] > 0 for x in g[rank + 1:]) for r in range(6)]
-    st = phase(shard.faithful_shards_carry, carry, stream, default=[0] * 6)
-    g = exchange(st)
-    before = [sum(x[r] for x in g[:rank]) for r in range(6)]
-    cand = phase(shard.faithful_shards_cut, before, stream, default=list(totals))
-    g = exchange(cand)
-    cut = [min(x[r] for x in g) for r in range(6)]
-    phase(shard.faithful_shards_hist, cut, last, stream, default=None)
-    exchange([])  # the last phase's error, before the caller's merge collectives
-    return cut
+
+def sharded_faithful_hist(cfg, samples_by_ref, group=None, stream=None):
+    """Faithful mode over key-range shards, one GPU per rank, over lists in
+    any order (what r10 hands over).
+
+    samples_by_ref: {ref: device int64 tensor holding that reference's whole
+    sample list} (identical on every rank).  Every rank keeps its key range
+    (faithful_shards_select), sorts it and runs the single-read pipeline's
+    phases.  Returns the merged Histogram, with `traversed` summed over ranks
+    (identical on all ranks)."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    dev = torch.device("cuda", cfg.device)
+    lo, hi = key_range(faithful_key_space(cfg), rank, world)
+    sp = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    totals = [0] * 6
+    for r, t in samples_by_ref.items():
+        totals[REFS.index(r) if isinstance(r, str) else int(r)] = t.numel()
+    lists = torch.cat([samples_by_ref[r].reshape(-1) for r in sorted(samples_by_ref,
+                       key=lambda x: REFS.index(x) if isinstance(x, str) else int(x))]) if samples_by_ref else \
+        torch.zeros(1, dtype=torch.int64, device=dev)
+    rx = DeviceRows(world, dev, group)
+    ctx, err = _open(cfg, sp)
+    try:
+        err = faithful_shards_protocol(
+            ctx, lambda row: ctx.faithful_shards_select(lists.data_ptr(), totals, lo, hi, row, sp), rank, world, rx,
+            sp, err=err, selected=True)
+        return merge_results(ctx, err, dev, group)
+    finally:
+        if ctx is not None:
+            ctx.close()
 
 
 def sharded_faithful_gen_hist(cfg, seed, totals, group=None, stream=None):
@@ -307,19 +332,14 @@ def sharded_faithful_gen_hist(cfg, seed, totals, group=None, stream=None):
     samples whose keys fall in its range -- an index slice, found by the host
     search pluss_keyorder_index_range, since the lists are in key order and
     random access -- and generates them inside its single-read pass; no rank
-    reads or holds a whole list.  Then the three-exchange protocol of
-    faithful_shards_protocol.  Returns the merged Histogram (identical on
+    reads or holds a whole list.  Returns the merged Histogram (identical on
     every rank)."""
     import torch
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    nccl = dist.get_backend(group) == "nccl"
     dev = torch.device("cuda", cfg.device)
-    ag = torch_allgather(group, dev if nccl else "cpu")
     lo, hi = key_range(faithful_key_space(cfg), rank, world)
     sp = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-    keys = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
-    cnts = torch.empty(TABLE_CAP, dtype=torch.int64, device=dev)
     err = None
     first, n = [0] * 6, [0] * 6
     try:
@@ -327,15 +347,16 @@ def sharded_faithful_gen_hist(cfg, seed, totals, group=None, stream=None):
             if t:
                 a, b = keyorder_index_range(cfg, seed, r, int(t), lo, hi)
                 first[r], n[r] = a, b - a
-    except Exception as e:  # noqa: BLE001 -- raised on every rank by the protocol's first exchange
+    except Exception as e:  # noqa: BLE001 -- reported after the pass, on every rank
         err = e
-    with Context(cfg) as ctx:
-        ctx.reset(sp)
-        faithful_shards_protocol(ctx, None, seed, [int(t) for t in totals], first, n, rank, ag, sp, err=err)
-        trav, err = _export_fetch(ctx, keys, cnts, sp, dev)
-    raise_together(err, group, dev if nccl else None)
-    tsum = [sum(col) % (1 << 64) for col in zip(*ag(trav))]
-    if not nccl:
-        keys, cnts = keys.cpu(), cnts.cpu()
-    h = allgather_tables(keys, cnts, group)
-    return Histogram(h.bins, tsum)
+    rx = DeviceRows(world, dev, group)
+    tot = [int(t) for t in totals]
+    ctx, err2 = _open(cfg, sp)
+    try:
+        err = faithful_shards_protocol(
+            ctx, lambda row: ctx.faithful_shards_local(None, seed, tot, first, n, row, sp), rank, world, rx, sp,
+            err=err or err2)
+        return merge_results(ctx, err, dev, group)
+    finally:
+        if ctx is not None:
+            ctx.close()

@@ -252,3 +252,33 @@ def _torch_stream(request):
     with torch.cuda.stream(s):
         yield
     torch.cuda.synchronize()
+
+
+def gpu_lockstep(ctxs, phase1s, stream, selected=False):
+    """The pluss_dev_faithful_shards_* phases over several handles on one GPU,
+    one handle per shard: the summary rows live in a device tensor and are
+    "all-gathered" by a device copy on the current stream between phases (what
+    an RCCL all-gather does across GPUs).  phase1s[i](ctx, d_row) runs shard
+    i's first phase."""
+    import torch
+    from pluss_sampler_optimization_amd import SHARD_ROW
+    ns = len(ctxs)
+    rows = torch.zeros(ns, SHARD_ROW, dtype=torch.int64, device="cuda")
+    g = torch.zeros(ns * SHARD_ROW, dtype=torch.int64, device="cuda")
+
+    def gather():
+        g.copy_(rows.reshape(-1))
+    for i, (ctx, p1) in enumerate(zip(ctxs, phase1s)):
+        p1(ctx, rows[i].data_ptr())
+    gather()
+    if selected:
+        for i, ctx in enumerate(ctxs):
+            ctx.faithful_shards_local_selected(g.data_ptr(), i, ns, rows[i].data_ptr(), stream)
+        gather()
+    for name in ("carry", "cut"):
+        for i, ctx in enumerate(ctxs):
+            getattr(ctx, "faithful_shards_" + name)(g.data_ptr(), i, ns, rows[i].data_ptr(), stream)
+        gather()
+    for i, ctx in enumerate(ctxs):
+        ctx.faithful_shards_hist(g.data_ptr(), i, ns, stream)
+    return rows

@@ -481,23 +481,15 @@ def test_sharded_two_ranks_on_one_gpu_equals_single_rank():
 KEY_EMPTY = (1 << 64) - 1
 
 
-def _lockstep_shards(ctxs, bounds, ref, d_ptr, n, stream):
-    """Run the four pluss_dev_faithful_shard_* phases over several handles in
-    one process, exchanging the summaries by hand (what dist.py does with
-    all-gathers)."""
-    g = [ctx.faithful_shard_keys(ref, d_ptr, n, bounds[i], bounds[i + 1], stream) for i, ctx in enumerate(ctxs)]
-    starts = []
-    for i, ctx in enumerate(ctxs):
-        j_off = sum(x[0] for x in g[:i])
-        pmax_in = max([x[2] for x in g[:i] if x[0] > 0], default=0)
-        starts.append(ctx.faithful_shard_starts(j_off, pmax_in, stream))
-    n_total = sum(x[0] for x in g)
-    assert n_total == n
-    cut = min(ctx.faithful_shard_cut(sum(starts[:i]), n_total, stream) for i, ctx in enumerate(ctxs))
-    for i, ctx in enumerate(ctxs):
-        later = [x for x in g[i + 1:] if x[0] > 0]
-        ctx.faithful_shard_hist(cut, later[0][1] if later else KEY_EMPTY, not later, stream)
-    return g
+def _select_shards(ctxs, bounds, t, totals, stream):
+    """The pluss_dev_faithful_shards_* phases over several handles in one
+    process, each keeping its key range [bounds[i], bounds[i+1]) of the whole
+    arbitrary-order lists (the six references back to back in t); the rows are
+    gathered by device copies (conftest.gpu_lockstep)."""
+    from conftest import gpu_lockstep
+    return gpu_lockstep(ctxs, [lambda ctx, row, i=i: ctx.faithful_shards_select(t.data_ptr(), totals, bounds[i],
+                                                                                 bounds[i + 1], row, stream)
+                               for i in range(len(ctxs))], stream, selected=True)
 
 
 def _merged(ctxs):
@@ -520,14 +512,15 @@ def test_faithful_key_range_shards_equal_reference_dumps(orc, name, d, smp):
     ks = P.faithful_key_space(c)
     bounds = [0, ks // 3, ks // 3, ks]  # shard 1 is empty
     stream = torch.cuda.current_stream().cuda_stream
+    lists = [orc.pack_array(ref, smp[ref]) for ref in orc.REFS]
+    totals = [len(x) for x in lists]
+    t = torch.from_numpy(np.concatenate(lists).astype(np.uint64).view(np.int64)).cuda()
     ctxs = [P.Context(c) for _ in range(3)]
     try:
         for x in ctxs:
             x.reset(stream)
-        for ref in orc.REFS:
-            t = torch.from_numpy(orc.pack_array(ref, smp[ref]).view(np.int64)).cuda()
-            g = _lockstep_shards(ctxs, bounds, ref, t.data_ptr(), t.numel(), stream)
-            assert g[1][0] == 0
+        rows = _select_shards(ctxs, bounds, t, totals, stream).cpu().numpy()
+        assert not rows[1, :6].any()  # the empty shard kept nothing
         bins, trav = _merged(ctxs)
     finally:
         for x in ctxs:
@@ -542,25 +535,24 @@ def test_faithful_key_range_shards_equal_reference_dumps(orc, name, d, smp):
                                              (1024, 8, 5000000, 2)])
 def test_faithful_key_range_shards_equal_one_gpu(N, T, per, nshards):
     """Longer lists (many replays, Q1 drops, cold samples): the sharded phases
-    equal one-handle faithful mode exactly, traversed included.  The last case
-    gives the 3-D references 1221 tiles each (the finish kernel's many-tile
-    path), checked against the independent shard kernels."""
+    over arbitrary-order lists equal one-handle faithful mode exactly,
+    traversed included.  The last case gives the 3-D references 1221 tiles
+    each (the finish kernel's many-tile path)."""
     torch = pytest.importorskip("torch")
     c = cfg(N, T, mode="faithful")
     ks = P.faithful_key_space(c)
     bounds = [ks * i // nshards for i in range(nshards + 1)]
     stream = torch.cuda.current_stream().cuda_stream
+    lists = [P.expand_samples(c, 0x5EED0000 + N, r, 0, per if r >= 2 else min(per, (N - 1) ** 2)) for r in range(6)]
+    totals = [len(x) for x in lists]
+    t = torch.from_numpy(np.concatenate(lists).view(np.int64)).cuda()
     ctxs = [P.Context(c) for _ in range(nshards)]
     one = P.Context(c)
     try:
         for x in ctxs + [one]:
             x.reset(stream)
-        for r in range(6):
-            n = per if r >= 2 else min(per, (N - 1) ** 2)
-            s = P.expand_samples(c, 0x5EED0000 + N, r, 0, n)
-            t = torch.from_numpy(s.view(np.int64)).cuda()
-            _lockstep_shards(ctxs, bounds, r, t.data_ptr(), n, stream)
-            one.faithful_hist(r, t.data_ptr(), n, stream)
+        _select_shards(ctxs, bounds, t, totals, stream)
+        one.faithful_hist_refs(t.data_ptr(), totals, stream)
         bins, trav = _merged(ctxs)
         h = one.fetch()
     finally:
@@ -571,14 +563,60 @@ def test_faithful_key_range_shards_equal_one_gpu(N, T, per, nshards):
 
 
 def test_faithful_shard_phase_order_is_enforced():
+    """Phases out of order, a one-GPU faithful call between phases, or rows
+    that do not cover the shard are configuration errors (a
+    half-finished shard pass can never leak into a later pass)."""
+    torch = pytest.importorskip("torch")
     c = cfg(64, 4, mode="faithful")
+    stream = torch.cuda.current_stream().cuda_stream
+    rows = torch.zeros(2 * P.SHARD_ROW, dtype=torch.int64, device="cuda")
+    row = rows.data_ptr()
     with P.Context(c) as ctx:
         with pytest.raises(P.PlussError, match="PLUSS_ERR_CONFIG"):
-            ctx.faithful_shard_starts(0, 0)
+            ctx.faithful_shards_carry(row, 0, 2, row, stream)
         with pytest.raises(P.PlussError, match="PLUSS_ERR_CONFIG"):
-            ctx.faithful_shard_hist(0, KEY_EMPTY, True)
+            ctx.faithful_shards_hist(row, 0, 2, stream)
+        totals = [0, 0, 0, 0, 100, 0]
+        ctx.faithful_shards_local(None, 1, totals, [0] * 6, totals, row, stream)
+        with pytest.raises(P.PlussError, match="PLUSS_ERR_CONFIG"):
+            ctx.faithful_shards_carry(row, 2, 2, row, stream)  # shard out of range
+        ctx.gen_faithful_refs(1, totals, stream)  # a one-GPU pass ends the shard pass
+        with pytest.raises(P.PlussError, match="PLUSS_ERR_CONFIG"):
+            ctx.faithful_shards_carry(row, 0, 2, row, stream)
+        # a re-issued local phase restarts cleanly: twice, then the whole pass == one GPU
+        ctx.reset(stream)
+        for _ in range(2):
+            ctx.faithful_shards_local(None, 1, totals, [0] * 6, totals, rows[0:P.SHARD_ROW].data_ptr(), stream)
+        rows[P.SHARD_ROW:] = 0
+        rows[P.SHARD_ROW + 18:P.SHARD_ROW + 24] = torch.tensor(totals, dtype=torch.int64, device="cuda")
+        for name in ("carry", "cut"):
+            getattr(ctx, "faithful_shards_" + name)(rows.data_ptr(), 0, 2, rows.data_ptr(), stream)
+        ctx.faithful_shards_hist(rows.data_ptr(), 0, 2, stream)
+        got = ctx.fetch()
+        ctx.reset(stream)
+        ctx.gen_faithful_refs(1, totals, stream)
+        assert got.bins == ctx.fetch().bins
     with pytest.raises(P.PlussError, match="PLUSS_ERR_CONFIG"):
         P.faithful_key_space(cfg(60, 4, mode="faithful"))
+
+
+def test_failed_shard_row_fails_every_shard():
+    """A row carrying the error word makes the other shards' passes record
+    nothing and fail at their fetch with PLUSS_ERR_PEER (no shard waits)."""
+    torch = pytest.importorskip("torch")
+    c = cfg(64, 4, mode="faithful")
+    stream = torch.cuda.current_stream().cuda_stream
+    totals = [50, 50, 300, 300, 300, 300]
+    rows = torch.zeros(2 * P.SHARD_ROW, dtype=torch.int64, device="cuda")
+    with P.Context(c) as ctx:
+        ctx.reset(stream)
+        ctx.faithful_shards_local(None, 3, totals, [0] * 6, totals, rows.data_ptr(), stream)
+        rows[P.SHARD_ROW + P.SHARD_ROW_ERR] = 1  # shard 1 failed
+        for name in ("carry", "cut"):
+            getattr(ctx, "faithful_shards_" + name)(rows.data_ptr(), 0, 2, rows.data_ptr(), stream)
+        ctx.faithful_shards_hist(rows.data_ptr(), 0, 2, stream)
+        with pytest.raises(P.PlussError, match="PLUSS_ERR_PEER"):
+            ctx.fetch()
 
 
 def _faith_dist_worker(rank, world, port, q):

@@ -17,7 +17,7 @@ Run on an MI355X:  python -m pytest tests -m gpu -x -q
 import numpy as np
 import pytest
 
-from conftest import all_tids_list, window_list
+from conftest import all_tids_list, gpu_lockstep, window_list
 
 pytestmark = pytest.mark.gpu
 
@@ -122,11 +122,12 @@ def test_words64_over_1024_tiles(orc, kind):
 
 
 def shards_by_hand(c, splits, totals, lists=None, seed=None):
-    """The four phases of pluss_dev_faithful_shards_* on one GPU, one handle
-    per shard, the summaries exchanged here: splits[r] = the index boundaries
-    of reference r's list over the shards (uneven, empty shards allowed).
-    lists: key-ordered sample lists (each shard gets its slices); None: the
-    generated key-order lists of `seed`.  Returns the merged Histogram."""
+    """The phases of pluss_dev_faithful_shards_* on one GPU, one handle per
+    shard, the summary rows gathered by device copies (conftest.gpu_lockstep):
+    splits[r] = the index boundaries of reference r's list over the shards
+    (uneven, empty shards allowed).  lists: key-ordered sample lists (each
+    shard gets its slices); None: the generated key-order lists of `seed`.
+    Returns the merged Histogram."""
     S = len(splits[0]) - 1
     first = [[splits[r][k] for r in range(6)] for k in range(S)]
     n = [[splits[r][k + 1] - splits[r][k] for r in range(6)] for k in range(S)]
@@ -140,16 +141,10 @@ def shards_by_hand(c, splits, totals, lists=None, seed=None):
         else:
             bufs.append(None)
     ptr = [b.data_ptr() if b is not None else None for b in bufs]
-    mx = [ctx.faithful_shards_local(ptr[k], seed or 0, totals, first[k], n[k], stream()) for k, ctx in enumerate(ctxs)]
-    carry = [[max([mx[j][r] for j in range(k) if n[j][r] > 0], default=0) for r in range(6)] for k in range(S)]
-    st = [ctx.faithful_shards_carry(carry[k], stream()) for k, ctx in enumerate(ctxs)]
-    before = [[sum(st[j][r] for j in range(k)) for r in range(6)] for k in range(S)]
-    cand = [ctx.faithful_shards_cut(before[k], stream()) for k, ctx in enumerate(ctxs)]
-    cut = [min(cand[k][r] for k in range(S)) for r in range(6)]
+    gpu_lockstep(ctxs, [lambda ctx, row, k=k: ctx.faithful_shards_local(ptr[k], seed or 0, totals, first[k], n[k], row,
+                                                                         stream()) for k in range(S)], stream())
     bins, trav = {}, [0] * 6
-    for k, ctx in enumerate(ctxs):
-        last = [not any(n[j][r] > 0 for j in range(k + 1, S)) for r in range(6)]
-        ctx.faithful_shards_hist(cut, last, stream())
+    for ctx in ctxs:
         h = ctx.fetch()
         for key, v in h.bins.items():
             bins[key] = bins.get(key, 0) + v
@@ -183,3 +178,36 @@ def test_key_range_shards_equal_one_gpu(orc, kind):
     assert got.bins == want.bins and list(got.traversed) == list(want.traversed)
     if kind == "windows":
         check_vs_oracle(orc, c, {"shards": got}, lists, [r for r in P.REFS if r != "B0"])
+
+
+def test_selected_key_range_shards_equal_one_gpu(orc):
+    """Arbitrary-order lists (what r10 hands over) through the shard protocol's
+    select + local_selected phases: every shard reads the whole shuffled lists,
+    keeps its key range (5 uneven ranges, one empty), sorts it with the bucket
+    sort and runs the single-read pipeline; merged == one GPU's radix source ==
+    the stepping oracle."""
+    N, T = 4096, 8
+    c = P.SamplerConfig(n=N, threads=T, mode="faithful")
+    lists = [window_list(N, T, 4, ref, 10000, [0, N // T - 1], 16, 17 + r) for r, ref in enumerate(P.REFS)]
+    totals = [len(x) for x in lists]
+    want = three_sources(c, lists)["radix"]
+    rng = np.random.default_rng(5)
+    shuf = np.concatenate([x[rng.permutation(len(x))] for x in lists]).astype(np.uint64)
+    t = torch.from_numpy(shuf.view(np.int64)).cuda()
+    ks = P.faithful_key_space(c)
+    b = [0, ks // 9, ks // 9, ks // 2, (3 * ks) // 4, ks]  # shard 1 is empty
+    ctxs = [P.Context(c) for _ in range(5)]
+    for ctx in ctxs:
+        ctx.reset(stream())
+    gpu_lockstep(ctxs, [lambda ctx, row, k=k: ctx.faithful_shards_select(t.data_ptr(), totals, b[k], b[k + 1], row,
+                                                                          stream()) for k in range(5)],
+                 stream(), selected=True)
+    bins, trav = {}, [0] * 6
+    for ctx in ctxs:
+        h = ctx.fetch()
+        for key, v in h.bins.items():
+            bins[key] = bins.get(key, 0) + v
+        trav = [(x + y) % (1 << 64) for x, y in zip(trav, h.traversed)]
+        ctx.close()
+    assert bins == want.bins and trav == list(want.traversed)
+    check_vs_oracle(orc, c, {"selected": P.Histogram(bins, trav)}, lists, [r for r in P.REFS if r != "B0"])

@@ -1,0 +1,103 @@
+"""Multi-GPU behind the C ABI (include/pluss_gpu.h, pluss_group_*;
+csrc/pluss_group.hip): a plain-C caller (tests/helpers/group_main.c, the
+shape of the reference's own main()s, r10:3191-3278 / src/main.rs:17-44)
+drives a group of shards over RCCL and checks every merged result against
+the same pass on one device.  On the one-GPU box: one device with one shard
+(a one-rank RCCL communicator) and one device with 8 logical shards (SURVEY
+§4.4: an 8-GPU job's partition and exchanges on one card).  The Python Group
+wrapper is also checked against the reference's own r10 dumps."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import expected_raw, golden_configs
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIBDIR = os.path.join(ROOT, "pluss_sampler_optimization_amd", "lib")
+SRC = os.path.join(ROOT, "tests", "helpers", "group_main.c")
+
+
+def build(out_dir):
+    if not os.path.exists(os.path.join(LIBDIR, "libpluss_gpu.so")):
+        pytest.skip("libraries not built")
+    exe = os.path.join(out_dir, "group_main")
+    cc = shutil.which("gcc") or pytest.skip("no gcc")
+    r = subprocess.run([cc, "-O2", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-o", exe,
+                        SRC, "-L", LIBDIR, "-lpluss_gpu", f"-Wl,-rpath,{LIBDIR}", "-Wl,-rpath,/opt/rocm/lib"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return exe
+
+
+def test_c_caller_compiles_and_links(tmp_path):
+    exe = build(str(tmp_path))
+    out = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
+    assert "libpluss_gpu.so" in out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,T,total,spd", [(128, 4, 200000, 1), (128, 4, 200000, 8), (256, 8, 1 << 20, 8),
+                                           (1024, 8, 1 << 22, 3)])
+def test_c_group_equals_one_device(tmp_path, N, T, total, spd):
+    exe = build(str(tmp_path))
+    r = subprocess.run([exe, str(N), str(T), str(total), str(spd), "0"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    lines = r.stdout.strip().splitlines()
+    assert lines[0] == f"shards {spd} of {spd}"
+    assert lines[1:] == ["ok clean sampled_hist", "ok clean dense x20 (resident lists)", "ok clean gen_count_dense",
+                         "ok faithful sampled_hist (any order)", "ok faithful gen_faithful (key-order lists)"]
+
+
+P = None
+
+
+def _P():
+    global P
+    if P is None:
+        P = pytest.importorskip("pluss_sampler_optimization_amd")
+    return P
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spd", [1, 8])
+@pytest.mark.parametrize("name,d,smp", golden_configs()[:4], ids=[g[0] for g in golden_configs()[:4]])
+def test_group_reproduces_reference_dumps(orc, name, d, smp, spd):
+    """The reference's r10 sample lists through a group (key-range shards,
+    rows all-gathered over RCCL, tables merged): its raw histograms."""
+    P = _P()
+    N, T = d["N"], d["T"]
+    c = P.SamplerConfig(n=N, threads=T, mode="faithful")
+    lst = np.concatenate([orc.pack_array(ref, smp[ref]) for ref in orc.REFS])
+    with P.Group(c, [0], spd) as g:
+        h = g.sampled_hist(np.random.default_rng(3).permutation(lst))
+    for r, ref in enumerate(orc.REFS):
+        exp, etrav = expected_raw(d, ref)
+        assert {k: v for k, v in h.bins.items() if k[0] == ref} == exp, (name, ref)
+        assert h.traversed[r] == etrav, (name, ref)
+
+
+@pytest.mark.gpu
+def test_group_pairs_shape_and_errors(orc):
+    """A shape with N % (cls/ds) != 0 ((key, sink) pairs, not key-range
+    sharded: the job's first shard runs the samplers) equals one device; a
+    malformed sample fails the group pass."""
+    P = _P()
+    c = P.SamplerConfig(n=100, threads=1, mode="faithful")
+    lst = np.concatenate([P.expand_samples(c, 9, r, 0, n) for r, n in enumerate(P.default_counts(100, 20000))])
+    with P.Group(c, [0], 4) as g:
+        assert g.sampled_hist(lst) == P.sampled_hist(c, lst)
+        bad = lst.copy()
+        bad[7] = (7 << 60) | 1
+        with pytest.raises(P.PlussError, match="PLUSS_ERR_INPUT"):
+            g.sampled_hist(bad)
+    cc = P.SamplerConfig(n=128, threads=4)
+    with P.Group(cc, [0], 2) as g:
+        bad = np.concatenate([P.expand_samples(cc, 9, r, 0, 1000) for r in range(6)])
+        bad[5] = (2 << 60) | (200 << 40)  # index >= N
+        with pytest.raises(P.PlussError, match="PLUSS_ERR_INPUT"):
+            g.sampled_hist(bad)
+        with pytest.raises(P.PlussError, match="PLUSS_ERR_CONFIG"):
+            g.dense(1)  # no resident lists yet
