@@ -375,6 +375,64 @@ def faithful_config3_bench(P, torch, device, stream, reps=5):
     return out
 
 
+def faithful_pipeline_bench(P, torch, device, stream, reps=3):
+    """r10's whole timed unit (r10:3199-3278) at BASELINE shapes, end to end:
+    the six references' sample lists generated, the six sampler_<REF>
+    (faithful mode, r10's queue semantics), the raw histograms fetched, then on
+    the host r10's per-reference CRI (no_share_distribute + share_distribute,
+    pluss_cri_r10), the floor-log2 merge into the reuse histogram, pluss_AET
+    and the MRC printout.  Sources of the lists:
+      feistel_radix: uniform lists in arbitrary order (r10's rand() draw,
+                     r10:156-185), generated on the device and sorted inside the
+                     pass (the radix source);
+      generated:     key-order lists generated inside the pass (no sort).
+    Host clock around everything, median of `reps`; `host_share` = the CRI ->
+    MRC text part's fraction."""
+    from pluss_sampler_optimization_amd import host as H
+    out = {}
+    sp = stream.cuda_stream
+    dev = torch.device("cuda", device)
+    for name, N, total in (("config2", 1024, 1 << 24), ("config3", 4096, 1 << 28)):
+        counts = P.default_counts(N, total)
+        fcfg = P.SamplerConfig(n=N, threads=8, mode="faithful", device=device)
+        buf = torch.empty(total, dtype=torch.int64, device=dev)
+        res = {"workload": f"GEMM N={N}, T=8, {total} samples (BASELINE {name} budget on one GPU), faithful"}
+        with P.Context(fcfg) as ctx:
+            def feistel_radix():
+                off = 0
+                for r, c in enumerate(counts):
+                    ctx.expand(SEED, r, 0, c, buf.data_ptr() + 8 * off, sp)
+                    off += c
+                ctx.faithful_hist_refs(buf.data_ptr(), counts, sp)
+
+            def generated():
+                ctx.gen_faithful_refs(SEED, counts, sp)
+            for src, dev_part in (("feistel_radix", feistel_radix), ("generated", generated)):
+                runs = []
+                for k in range(reps + 1):  # the first run warms (code load, buffers)
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    ctx.reset(sp)
+                    dev_part()
+                    h = ctx.fetch()  # waits for the device; the raw histograms on the host
+                    t1 = time.perf_counter()
+                    _, reuse, mrc = H.mrc_from_r10(8, h)
+                    text = H.format_mrc(mrc)
+                    t2 = time.perf_counter()
+                    if k:
+                        runs.append((t2 - t0, t2 - t1))
+                runs.sort()
+                tot_s, host_s = runs[len(runs) // 2]
+                res[src] = {"ms": tot_s * 1e3, "host_ms": host_s * 1e3, "host_share": host_s / tot_s,
+                            "samples_per_s": total / tot_s, "mrc_rows": len(text.splitlines()) - 1,
+                            "recorded": h.total() - sum(h.cold(r) for r in P.REFS)}
+        del buf
+        out[name] = res
+    out["note"] = ("one pass of r10's timer: lists -> six faithful samplers -> fetch -> pluss_cri_r10 per reference "
+                   "-> log2 merge -> pluss_aet -> MRC text; host clock, median of %d" % reps)
+    return out
+
+
 def end_to_end_bench(P, torch, cfg, counts, parts, stream, steps=20):
     """Sample generation inside the timed unit, as in r10 (r10:156-185 within the
     timer r10:3199): this rank's slices of the six key-order lists generated and
@@ -768,6 +826,10 @@ def main():
             result["faithful_config3"] = faithful_config3_bench(P, torch, local, stream)
         except Exception as e:  # noqa: BLE001
             result["faithful_config3"] = {"error": repr(e)}
+        try:
+            result["faithful_pipeline"] = faithful_pipeline_bench(P, torch, local, stream)
+        except Exception as e:  # noqa: BLE001
+            result["faithful_pipeline"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         host = samples.cpu().numpy().view(np.uint64)
 

@@ -105,6 +105,18 @@ int pluss_default_counts(int64_t n, uint64_t total, uint64_t counts[6]);
 int pluss_expand_sorted(const pluss_cfg *cfg, uint64_t seed, int32_t ref, uint64_t total, uint64_t first, uint64_t n,
                         uint64_t *out);
 
+/* r10's own draw in r10's pop order: samples [first, first+n)
+   of the list of `total` distinct samples of reference `ref` drawn UNIFORMLY
+   without replacement from its span^d iteration points -- the distribution of
+   r10's rand() draw with duplicate rejection (r10:156-185) -- generated
+   directly in key order (IterationComp, pluss_utils.h:175-267): Bernoulli
+   candidates per leaf of the key-ordered space, then a uniform subset of
+   them removed down to `total` (csrc/pluss_uniform.h).  Distinct, strictly
+   increasing in key.  Needs N % (chunk*threads) == 0 and total + 10
+   sqrt(total) + 32 < 2^32. */
+int pluss_expand_uniform_sorted(const pluss_cfg *cfg, uint64_t seed, int32_t ref, uint64_t total, uint64_t first,
+                                uint64_t n, uint64_t *out);
+
 /* --- handle API: device-resident inputs, explicit streams ----------------
    `stream` is a hipStream_t (NULL = the handle's own stream).  Device
    pointers are plain addresses of device memory on cfg->device.           */
@@ -140,6 +152,12 @@ int pluss_dev_faithful_hist_sorted_refs(pluss_ctx *ctx, const uint64_t *d_sample
    being written to memory (r10 generates its samples inside its timer,
    r10:156-185). */
 int pluss_dev_gen_faithful_refs(pluss_ctx *ctx, uint64_t seed, const uint64_t totals[6], void *stream);
+/* the same over r10's own distribution: pluss_dev_expand_uniform_sorted's
+   lists, generated inside the pass (never written to memory) -- r10's whole
+   sampler pass, its uniform draw included, without a sort */
+int pluss_dev_gen_uniform_faithful_refs(pluss_ctx *ctx, uint64_t seed, const uint64_t totals[6], void *stream);
+int pluss_dev_expand_uniform_sorted(pluss_ctx *ctx, uint64_t seed, int32_t ref, uint64_t total, uint64_t first,
+                                    uint64_t n, uint64_t *d_out, void *stream);
 /* full trace: every access of the nest (sampling rate 1.0); accumulates like
    the other passes, and adds the N*N*(4N+2) accesses to traversed[0] */
 int pluss_dev_fulltrace_hist(pluss_ctx *ctx, void *stream);

@@ -51,6 +51,8 @@ def lib():
         L.orc_expand_sorted.argtypes = [P(OrcCfg), ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
                                         ctypes.c_uint64, P(ctypes.c_uint64)]
         L.orc_expand_sorted.restype = ctypes.c_int
+        L.orc_expand_uniform.argtypes = L.orc_expand_sorted.argtypes
+        L.orc_expand_uniform.restype = ctypes.c_int
         for f in (L.orc_fulltrace, L.orc_fulltrace_mt, L.orc_clean, L.orc_faithful, L.orc_expand):
             f.restype = ctypes.c_int
         _lib = L
@@ -144,6 +146,19 @@ def expand_sorted(c, seed, ref, total, first, n):
                                  out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
     if rc:
         raise RuntimeError(f"orc_expand_sorted rc={rc}")
+    return out
+
+
+def expand_uniform(c, seed, ref, total, first, n):
+    """Samples [first, first+n) of the list of `total` samples of reference
+    `ref` drawn uniformly without replacement, in key order (DESIGN.md §4,
+    orc_expand_uniform)."""
+    out = np.empty(n, dtype=np.uint64)
+    rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
+    rc = lib().orc_expand_uniform(ctypes.byref(c), seed, rid, total, first, n,
+                                  out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+    if rc:
+        raise RuntimeError(f"orc_expand_uniform rc={rc}")
     return out
 
 

@@ -40,6 +40,7 @@
  * Histogram keys are exact (raw) RI values; -1 = cold.  kind 0 = noshare,
  * kind 1 = share (share_ratio THREAD_NUM-1 in the reference).
  */
+#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -611,4 +612,154 @@ int orc_expand_sorted(const orc_cfg *c, uint64_t seed, int ref, uint64_t S, uint
         out[x] = ((uint64_t)ref << 60) | (c0 << 40) | (c1 << 20) | c2;
     }
     return 0;
+}
+
+/* ------------------------------------------------ r10's draw, key order -- */
+/* r10 draws S distinct uniform points of a reference (rand() % (N-1) per
+   index, duplicates rejected, r10:156-185) and pops them in key order.  Spec
+   (the product's statement is csrc/pluss_uniform.h): every point
+   is a candidate with probability p = min(1, (S + 10 sqrt(S) + 32) / D);
+   leaves = key rows ((q, c1) for 3-D, q for 2-D references) cut into blocks of
+   K w-values times the threads, K = clamp(floor(16 / (T p)), 1, span) and K*T < 2^32; a
+   leaf's candidate count is Binomial(G, p) by inversion of one hash draw
+   (or one Bernoulli draw per point in leaves of <= 64 points, more than 64
+   expected candidates or p > 1/64), its candidates independent uniform offsets sorted and
+   redrawn on a duplicate; of the T' candidates the ranks F(0..T'-S-1) of a
+   keyed Feistel permutation of [0, T') are removed.  Samples [first, first+n)
+   of the survivors in key order.  Returns -3 if T' < S (probability ~1e-23),
+   -4 if a leaf draws more than 1024 candidates or 4096 colliding offset draws. */
+static uint64_t u_hash(uint64_t lk, uint64_t i) { return mix64(lk + i * 0x8CB92BA72F3D8DD7ULL); }
+static double u_u01(uint64_t h) { return (double)(h >> 11) * 0x1.0p-53; }
+static uint64_t u_leafkey(uint64_t base, uint64_t l, uint32_t a) {
+    return mix64(base + l * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)a * 0xD1B54A32D192ED03ULL);
+}
+static int u_cmp64(const void *a, const void *b) {
+    uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+    return x < y ? -1 : x > y;
+}
+
+int orc_expand_uniform(const orc_cfg *c, uint64_t seed, int ref, uint64_t S, uint64_t first, uint64_t n,
+                       uint64_t *out) {
+    if (!cfg_ok(c) || ref < 0 || ref > 5 || c->N % (c->CS * c->T)) return -1;
+    const int dim3 = !(ref == R_C0 || ref == R_C1);
+    const uint64_t T = (uint64_t)c->T, CS = (uint64_t)c->CS, Q = (uint64_t)(c->N / c->T);
+    const uint64_t span = c->range_full ? (uint64_t)c->N : (uint64_t)c->N - 1;
+    const uint64_t QA = c->range_full ? Q : Q - 1, W = span;
+    const uint64_t RA = dim3 ? QA * span : QA, RB = c->range_full ? 0 : (dim3 ? span : 1);
+    const uint64_t D = (RA * T + RB * (T - 1)) * W;
+    if (S < 1 || S > D || first + n > S) return -2;
+    const double E = (double)S + 10.0 * sqrt((double)S) + 32.0;
+    if (E >= 4294967296.0) return -2;
+    const double p = E >= (double)D ? 1.0 : E / (double)D;
+    const double r = p < 1.0 ? p / (1.0 - p) : 0.0;
+    const double kk = 16.0 / ((double)T * p);
+    uint64_t K = kk < 1.0 ? 1 : (kk >= (double)W ? W : (uint64_t)kk);
+    if (K > 0xFFFFFFFFULL / T) K = 0xFFFFFFFFULL / T; /* a leaf's points fit 32 bits */
+    const uint64_t nb = (W + K - 1) / K, LA = RA * nb, L = LA + RB * nb;
+    const uint64_t base = mix64(seed ^ ((uint64_t)(ref + 1) * 0x9E3779B97F4A7C15ULL) ^ 0xC2B2AE3D27D4EB4FULL);
+    /* leaf geometry */
+#define LEAF(l, blk, row, wb, kw, tb, G)                          \
+    do {                                                          \
+        blk = (l) >= LA;                                          \
+        uint64_t lb_ = blk ? (l) - LA : (l);                      \
+        row = lb_ / nb; wb = lb_ % nb;                            \
+        kw = W - wb * K < K ? W - wb * K : K;                     \
+        tb = blk ? T - 1 : T; G = kw * tb;                        \
+    } while (0)
+    uint32_t *cnt = (uint32_t *)malloc((L ? L : 1) * sizeof(uint32_t));
+    uint64_t *off = (uint64_t *)malloc(1025 * sizeof(uint64_t));
+    if (!cnt || !off) { free(cnt); free(off); return -5; }
+    uint64_t Tp = 0;
+    int rc = 0;
+    for (uint64_t l = 0; l < L && !rc; l++) {
+        int blk; uint64_t row, wb, kw, tb, G, x = 0;
+        LEAF(l, blk, row, wb, kw, tb, G);
+        (void)row; (void)blk;
+        if (p >= 1.0) {
+            x = G;
+        } else if (G <= 64 || (double)G * p > 64.0 || p > 0.015625) {
+            const uint64_t lk = u_leafkey(base, l, 0xFFFFFFFFu);
+            for (uint64_t j = 0; j < G; j++) x += u_u01(u_hash(lk, j)) < p;
+        } else {
+            double pm = 1.0, b = 1.0 - p;
+            for (uint64_t e = G; e; e >>= 1) { if (e & 1) pm = pm * b; b = b * b; }
+            double xu = u_u01(u_hash(u_leafkey(base, l, 0xFFFFFFFEu), 0));
+            while (xu >= pm && x < G) {
+                xu = xu - pm;
+                pm = pm * (double)(G - x); pm = pm / (double)(x + 1); pm = pm * r;
+                x++;
+            }
+        }
+        if (x > 1024) rc = -4;
+        cnt[l] = (uint32_t)x;
+        Tp += x;
+    }
+    if (!rc && Tp < S) rc = -3;
+    uint64_t *rem = NULL, m = 0;
+    if (!rc) {
+        m = Tp - S;
+        rem = (uint64_t *)malloc((m ? m : 1) * sizeof(uint64_t));
+        if (!rem) rc = -5;
+    }
+    if (!rc) { /* the removed candidate ranks: F(0..m-1), F a Feistel permutation of [0, Tp) */
+        int h = 1; while ((1ULL << (2 * h)) < Tp) h++;
+        const uint32_t M = (uint32_t)((1ULL << h) - 1);
+        uint32_t key[4];
+        for (int q = 0; q < 4; q++)
+            key[q] = (uint32_t)mix64(base ^ ((uint64_t)(q + 1) * 0xD1B54A32D192ED03ULL) ^ 0x6A09E667F3BCC909ULL);
+        for (uint64_t i = 0; i < m; i++) {
+            uint64_t y = i;
+            do {
+                uint32_t Lh = (uint32_t)(y >> h), R = (uint32_t)y & M;
+                for (int q = 0; q < 4; q++) { uint32_t t = R; R = Lh ^ (lowbias32(R ^ key[q]) & M); Lh = t; }
+                y = ((uint64_t)Lh << h) | R;
+            } while (y >= Tp);
+            rem[i] = y;
+        }
+        qsort(rem, m, sizeof(uint64_t), u_cmp64);
+    }
+    /* the survivors in key order */
+    uint64_t rank = 0, ri = 0, idx = 0;
+    for (uint64_t l = 0; l < L && !rc && idx < first + n; l++) {
+        const uint64_t cl = cnt[l];
+        if (!cl) continue;
+        int blk; uint64_t row, wb, kw, tb, G;
+        LEAF(l, blk, row, wb, kw, tb, G);
+        if (p >= 1.0) {
+            for (uint64_t j = 0; j < G; j++) off[j] = j;
+        } else if (G <= 64 || (double)G * p > 64.0 || p > 0.015625) {
+            const uint64_t lk = u_leafkey(base, l, 0xFFFFFFFFu);
+            uint64_t k = 0;
+            for (uint64_t j = 0; j < G; j++)
+                if (u_u01(u_hash(lk, j)) < p) off[k++] = j;
+        } else {
+            for (uint32_t a = 0;; a++) {
+                if (a == 4096) { rc = -4; break; }
+                const uint64_t lk = u_leafkey(base, l, a);
+                for (uint64_t i = 0; i < cl; i++)
+                    off[i] = (uint64_t)(((unsigned __int128)u_hash(lk, i) * G) >> 64);
+                qsort(off, cl, sizeof(uint64_t), u_cmp64);
+                int dup = 0;
+                for (uint64_t i = 1; i < cl; i++) dup |= off[i] == off[i - 1];
+                if (!dup) break;
+            }
+        }
+        for (uint64_t i = 0; i < cl; i++, rank++) {
+            while (ri < m && rem[ri] < rank) ri++;
+            if (ri < m && rem[ri] == rank) continue;  /* removed */
+            if (idx >= first && idx < first + n) {
+                const uint64_t o = off[i], w = wb * K + o / tb, t = o % tb;
+                uint64_t q, c1, c2 = dim3 ? w : 0;
+                if (blk) { q = Q - 1; c1 = dim3 ? row : w; }
+                else if (dim3) { q = row / span; c1 = row % span; }
+                else { q = row; c1 = w; }
+                const uint64_t c0 = ((q / CS) * T + t) * CS + q % CS;
+                out[idx - first] = ((uint64_t)ref << 60) | (c0 << 40) | (c1 << 20) | c2;
+            }
+            idx++;
+        }
+    }
+#undef LEAF
+    free(cnt); free(off); free(rem);
+    return rc;
 }

@@ -22,7 +22,8 @@ GROUP_ID_BYTES = 128
 EXPORTS = [
     "pluss_last_error", "pluss_device_count", "pluss_version",
     "pluss_gemm_sampled_hist", "pluss_gemm_fulltrace_hist", "pluss_gemm_sampled_ri", "pluss_expand_samples",
-    "pluss_default_counts", "pluss_expand_sorted", "pluss_dev_expand_sorted",
+    "pluss_default_counts", "pluss_expand_sorted", "pluss_dev_expand_sorted", "pluss_expand_uniform_sorted",
+    "pluss_dev_expand_uniform_sorted", "pluss_dev_gen_uniform_faithful_refs",
     "pluss_ctx_create", "pluss_ctx_destroy", "pluss_ctx_stream", "pluss_dev_expand", "pluss_dev_hist_reset",
     "pluss_dev_sampled_hist", "pluss_dev_faithful_hist", "pluss_dev_faithful_hist_refs",
     "pluss_dev_faithful_hist_sorted", "pluss_dev_faithful_hist_sorted_refs", "pluss_dev_gen_faithful_refs",
@@ -96,6 +97,9 @@ def lib():
         "pluss_default_counts": (ctypes.c_int, [i64, u64, P(u64)]),
         "pluss_expand_sorted": (ctypes.c_int, [cfgp, u64, i32, u64, u64, u64, vp]),
         "pluss_dev_expand_sorted": (ctypes.c_int, [vp, u64, i32, u64, u64, u64, vp, vp]),
+        "pluss_expand_uniform_sorted": (ctypes.c_int, [cfgp, u64, i32, u64, u64, u64, vp]),
+        "pluss_dev_expand_uniform_sorted": (ctypes.c_int, [vp, u64, i32, u64, u64, u64, vp, vp]),
+        "pluss_dev_gen_uniform_faithful_refs": (ctypes.c_int, [vp, u64, P(u64), vp]),
         "pluss_ctx_create": (ctypes.c_int, [cfgp, P(vp)]),
         "pluss_ctx_destroy": (ctypes.c_int, [vp]),
         "pluss_ctx_stream": (vp, [vp]),

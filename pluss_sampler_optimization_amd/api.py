@@ -170,6 +170,18 @@ def expand_sorted(cfg, seed, ref, total, first, n):
     return out
 
 
+def expand_uniform_sorted(cfg, seed, ref, total, first, n):
+    """Samples [first, first+n) of reference `ref`'s list of `total` samples
+    drawn uniformly without replacement (r10's rand() draw with duplicate
+    rejection, r10:156-185), generated directly in r10's pop order."""
+    out = np.empty(n, dtype=np.uint64)
+    c = cfg.to_c()
+    rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
+    check(lib().pluss_expand_uniform_sorted(ctypes.byref(c), seed, rid, total, first, n,
+                                            out.ctypes.data_as(ctypes.c_void_p)), "pluss_expand_uniform_sorted")
+    return out
+
+
 def default_counts(n, total):
     counts = (ctypes.c_uint64 * 6)()
     check(lib().pluss_default_counts(n, total, counts), "pluss_default_counts")
@@ -289,6 +301,16 @@ class Context:
         rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
         check(lib().pluss_dev_expand_sorted(self._h, seed, rid, total, first, n, d_out, stream),
               "pluss_dev_expand_sorted")
+
+    def expand_uniform_sorted(self, seed, ref, total, first, n, d_out, stream=None):
+        rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
+        check(lib().pluss_dev_expand_uniform_sorted(self._h, seed, rid, total, first, n, d_out, stream),
+              "pluss_dev_expand_uniform_sorted")
+
+    def gen_uniform_faithful_refs(self, seed, totals, stream=None):
+        """The six samplers over r10's uniform draw generated in key order inside the pass."""
+        c = (ctypes.c_uint64 * 6)(*[int(x) for x in totals])
+        check(lib().pluss_dev_gen_uniform_faithful_refs(self._h, seed, c, stream), "pluss_dev_gen_uniform_faithful_refs")
 
     def sampled_hist(self, d_samples, n, stream=None):
         check(lib().pluss_dev_sampled_hist(self._h, d_samples, n, stream), "pluss_dev_sampled_hist")

@@ -20,8 +20,9 @@ HOST_SOURCES = ["host/pluss_host.cpp"]
 CLI = os.path.join(LIBDIR, "pluss_cli")
 ARCH = os.environ.get("PLUSS_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["pluss_kernels.hip", "pluss_faithful.hip", "pluss_fa_w32.hip", "pluss_fa_w64.hip", "pluss_fa_smp.hip",
-           "pluss_fa_gen.hip", "pluss_group.hip", "pluss_capi.hip"]
-HEADERS = ["pluss_model.h", "pluss_internal.h", "pluss_device.h", "pluss_faithful.h", "pluss_sort.h"]
+           "pluss_fa_gen.hip", "pluss_fa_uni.hip", "pluss_uniform.hip", "pluss_group.hip",
+           "pluss_capi.hip"]
+HEADERS = ["pluss_model.h", "pluss_internal.h", "pluss_device.h", "pluss_faithful.h", "pluss_sort.h", "pluss_uniform.h"]
 
 
 def _hipcc():

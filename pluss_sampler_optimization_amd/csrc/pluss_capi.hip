@@ -64,6 +64,11 @@ static int check_flags(pluss_ctx* ctx) {
     set_error("the bucket sort's plan exceeded its capacity (faithful radix source)");
     return PLUSS_ERR_CAPACITY;
   }
+  if (f[0] & FLAG_UNI) {
+    set_error("uniform key-order generator: fewer candidates than samples, or a candidate window past its "
+              "capacity (probability below 1e-20; another seed draws afresh)");
+    return PLUSS_ERR_CAPACITY;
+  }
   if (f[0] & FLAG_LOOKBACK) {
     set_error("faithful pass stalled: a chunk's predecessor never published its running max (another kernel "
               "holding the GPU?)");
@@ -198,6 +203,11 @@ int pluss_ctx_destroy(pluss_ctx* c) {
     for (void* p : fr)
       if (p) (void)hipFree(p);
   }
+  {
+    void* ub[] = {c->ub.set, c->ub.cnt, c->ub.bits, c->ub.tmap, c->ub.pre, c->ub.rb, c->ub.bsum};
+    for (void* p : ub)
+      if (p) (void)hipFree(p);
+  }
   for (int r = 0; r < 6; ++r)
     if (c->fst[r]) (void)hipStreamDestroy(c->fst[r]);
   for (int e = 0; e < 7; ++e)
@@ -244,6 +254,17 @@ int pluss_dev_faithful_hist_sorted_refs(pluss_ctx* ctx, const uint64_t* d_sample
 int pluss_dev_gen_faithful_refs(pluss_ctx* ctx, uint64_t seed, const uint64_t totals[6], void* stream) {
   if (!ctx || !totals) return PLUSS_ERR_CONFIG;
   return launch_gen_faithful_refs(ctx, seed, totals, pick(ctx, stream));
+}
+
+int pluss_dev_gen_uniform_faithful_refs(pluss_ctx* ctx, uint64_t seed, const uint64_t totals[6], void* stream) {
+  if (!ctx || !totals) return PLUSS_ERR_CONFIG;
+  return launch_gen_uniform_faithful_refs(ctx, seed, totals, pick(ctx, stream));
+}
+
+int pluss_dev_expand_uniform_sorted(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t total, uint64_t first,
+                                    uint64_t n, uint64_t* d_out, void* stream) {
+  if (!ctx || ref < 0 || ref > 5 || (n && !d_out)) return PLUSS_ERR_CONFIG;
+  return launch_expand_uniform_sorted(ctx, seed, ref, total, first, n, d_out, pick(ctx, stream));
 }
 
 int pluss_dev_fulltrace_hist(pluss_ctx* ctx, void* stream) {
@@ -540,6 +561,23 @@ int pluss_expand_sorted(const pluss_cfg* cfg, uint64_t seed, int32_t ref, uint64
   sc.bufs.push_back(d);
   if (int rc = launch_expand_sorted(sc.ctx, seed, ref, total, first, n, d, sc.ctx->stream)) return rc;
   PLUSS_HIP_CHECK(hipStreamSynchronize(sc.ctx->stream));
+  PLUSS_HIP_CHECK(hipMemcpy(out, d, n * 8, hipMemcpyDeviceToHost));
+  return PLUSS_OK;
+}
+
+int pluss_expand_uniform_sorted(const pluss_cfg* cfg, uint64_t seed, int32_t ref, uint64_t total, uint64_t first,
+                                uint64_t n, uint64_t* out) {
+  if ((n && !out) || ref < 0 || ref > 5) return PLUSS_ERR_CONFIG;
+  Scoped sc;
+  if (int rc = pluss_ctx_create(cfg, &sc.ctx)) return rc;
+  if (int rc = uni_check(sc.ctx, ref, total, "pluss_expand_uniform_sorted")) return rc;
+  if (!n) return PLUSS_OK;
+  uint64_t* d = nullptr;
+  PLUSS_HIP_CHECK(hipMalloc((void**)&d, n * 8));
+  sc.bufs.push_back(d);
+  if (int rc = launch_expand_uniform_sorted(sc.ctx, seed, ref, total, first, n, d, sc.ctx->stream)) return rc;
+  PLUSS_HIP_CHECK(hipStreamSynchronize(sc.ctx->stream));
+  if (int rc = check_flags(sc.ctx)) return rc;
   PLUSS_HIP_CHECK(hipMemcpy(out, d, n * 8, hipMemcpyDeviceToHost));
   return PLUSS_OK;
 }

@@ -9,6 +9,7 @@
 #include <type_traits>
 
 #include "pluss_device.h"
+#include "pluss_uniform.h"
 
 namespace pluss {
 
@@ -141,7 +142,11 @@ constexpr int FPW = FPART + 2;              // ... + the start count and the Q1 
 constexpr int KL = 64;                      // local starts kept per tile (one wave lane each)
 __host__ __device__ inline uint64_t fa_tiles(uint64_t n) { return (n + TILE - 1) / TILE; }
 
-enum : int { SRC_W32 = 0, SRC_W64 = 1, SRC_SAMPLES = 2, SRC_GEN = 3 };
+enum : int { SRC_W32 = 0, SRC_W64 = 1, SRC_SAMPLES = 2, SRC_GEN = 3, SRC_UNI = 4 };
+static_assert(TILE == UG_TILE, "the uniform generator stages the pipeline's tiles");
+// sources whose elements are packed samples (SRC_UNI: generated into LDS from the plan)
+template <int SRC>
+constexpr bool fa_smp() { return SRC == SRC_SAMPLES || SRC == SRC_UNI; }
 enum : int { FA_LOCAL = 0, FA_FULL = 1, FA_CUT = 2 };
 
 // A key-range shard's exchange (include/pluss_gpu.h, PLUSS_SHARD_ROW): every
@@ -179,6 +184,7 @@ struct FaRefs {
   const void* src[6];  // SRC_W*: sorted packed words; SRC_SAMPLES: the key-ordered samples
   PkView pv[6];
   KeyGen kg[6];        // SRC_GEN
+  const UniSet* us;    // SRC_UNI: the plan of the uniform key-order lists (device memory)
   uint32_t fast;       // the local pass's fast path applies to the shape (fa_run)
 };
 
@@ -292,7 +298,7 @@ __device__ __forceinline__ Elem elem_of_sample_ref(const Model& m, const PkView&
 
 template <int SRC, bool P2, uint32_t REF>
 __device__ __forceinline__ Elem fa_decode_ref(const Model& m, const PkView& v, fa_raw_t<SRC> w, bool& bad) {
-  if constexpr (SRC == SRC_SAMPLES) return elem_of_sample_ref<REF, P2>(m, v, (uint64_t)w, bad);
+  if constexpr (fa_smp<SRC>()) return elem_of_sample_ref<REF, P2>(m, v, (uint64_t)w, bad);
   else return elem_of_word<P2>(m, v, REF, w);
 }
 
@@ -319,6 +325,7 @@ struct FaLds {
   unsigned long long klast[NT / 64];
   unsigned long long kb[2];     // the tile's first and last keys (FA_LOCAL)
   fa_raw_t<SRC> raw[SRC == SRC_GEN ? 1 : TILE + TILE / EPT];
+  uint32_t cand[SRC == SRC_UNI ? UG_CAP : 1];  // the uniform generator's candidate offsets
 };
 // LDS slot of tile element e for runs of EPT elements per thread (one pad per run)
 template <int EPT>
@@ -331,6 +338,7 @@ struct FaOne {
   uint64_t n;
   const void* src;
   PkView pv;
+  const UniSet* us;
 };
 
 // This thread's run of the tile: keys (KEY_EMPTY past the end), cases (2 bits
@@ -348,17 +356,22 @@ __device__ __forceinline__ void fa_load_run(const Model& m, const FaOne& o, cons
   cases = 0;
   t0s = 0;
   if constexpr (SRC != SRC_GEN) {
-    const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(o.src) + T.base;
-    fa_raw_t<SRC> v[EPT];  // every load issued before the first wait (partial tiles: clamped, no branch)
-    const uint32_t last = T.mt - 1;
+    if constexpr (SRC == SRC_UNI) {
+      uni_stage<NT>(o.us, T.r, T.lt, T.mt, sh.raw, sh.cand, o.us->flags,
+                    [](uint32_t e) { return fa_slot_n<EPT>(e); });
+    } else {
+      const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(o.src) + T.base;
+      fa_raw_t<SRC> v[EPT];  // every load issued before the first wait (partial tiles: clamped, no branch)
+      const uint32_t last = T.mt - 1;
 #pragma unroll
-    for (int k = 0; k < EPT; ++k) {
-      const uint32_t e = (uint32_t)k * NT + threadIdx.x;
-      v[k] = src[FULLT ? e : (e < last ? e : last)];
+      for (int k = 0; k < EPT; ++k) {
+        const uint32_t e = (uint32_t)k * NT + threadIdx.x;
+        v[k] = src[FULLT ? e : (e < last ? e : last)];
+      }
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) sh.raw[fa_slot_n<EPT>((uint32_t)k * NT + threadIdx.x)] = v[k];
+      __syncthreads();
     }
-#pragma unroll
-    for (int k = 0; k < EPT; ++k) sh.raw[fa_slot_n<EPT>((uint32_t)k * NT + threadIdx.x)] = v[k];
-    __syncthreads();
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
       key[k] = KEY_EMPTY;
@@ -1011,7 +1024,9 @@ __device__ __forceinline__ bool fa_fast_tile(const Model& m, const FaRefs& a, co
   if constexpr (SRC == SRC_GEN) kg = a.kg[REF];
   fa_rt(m, o.pv, sh);
   const bool full = T.mt == TILE;
-  if constexpr (SRC != SRC_GEN) {
+  if constexpr (SRC == SRC_UNI) {
+    uni_stage<TB>(o.us, T.r, T.lt, T.mt, sh.raw, sh.cand, o.us->flags, [](uint32_t e) { return fa_slot_n<TI>(e); });
+  } else if constexpr (SRC != SRC_GEN) {
     // all TI loads issued before the first is waited for: no branch around
     // them (a partial tile's lanes past its end re-read its last element)
     const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(o.src) + T.base;
@@ -1030,6 +1045,8 @@ __device__ __forceinline__ bool fa_fast_tile(const Model& m, const FaRefs& a, co
     bool b2 = false;
     if constexpr (SRC == SRC_GEN)
       sh.kb[threadIdx.x] = elem_of_digits<true>(m, o.pv, REF, keygen_digits_at(kg, T.gbase + e)).key;
+    else if constexpr (SRC == SRC_UNI)
+      sh.kb[threadIdx.x] = fa_decode_ref<SRC, true, REF>(m, o.pv, sh.raw[fa_slot_n<TI>(e)], b2).key;
     else
       sh.kb[threadIdx.x] = fa_decode_ref<SRC, true, REF>(m, o.pv, src_at<SRC>(o, e), b2).key;
   }
@@ -1061,7 +1078,7 @@ __device__ __forceinline__ bool fa_fast_tile(const Model& m, const FaRefs& a, co
   } else {
     auto el = [&](int k, uint32_t& odd) -> FaDec {
       const fa_raw_t<SRC> w = sh.raw[fa_slot_n<TI>(e0 + k)];
-      if constexpr (SRC == SRC_SAMPLES) return fa_dec_sample<REF>(m, o.pv, (uint64_t)w, odd);
+      if constexpr (fa_smp<SRC>()) return fa_dec_sample<REF>(m, o.pv, (uint64_t)w, odd);
       else return fa_dec_word<REF>(m, o.pv, w);
     };
     if (full) fa_local_fast<SRC, CHECK, REF, true>(m, o, sh, base, r, el, kl_out, g);
@@ -1130,6 +1147,7 @@ __device__ __forceinline__ FaOne fa_one_ref(const FaRefs& a, const FaTile& T) {
   o.n = a.ntot[R];  // the reference's whole list (all shards)
   o.src = a.src[R];
   o.pv = a.pv[R];
+  o.us = a.us;
   return o;
 }
 
@@ -1717,5 +1735,6 @@ void fa_launch_w32(const FaLaunch& L);
 void fa_launch_w64(const FaLaunch& L);
 void fa_launch_smp(const FaLaunch& L);
 void fa_launch_gen(const FaLaunch& L);
+void fa_launch_uni(const FaLaunch& L);
 
 }  // namespace pluss

@@ -612,7 +612,7 @@ static int srt_launch(pluss_ctx* ctx, FaithfulBufs& b, const SrtPlan& P, PT* X1,
   SrtParent* par = (SrtParent*)(B + P.o_par);
   uint32_t* cmap = (uint32_t*)(B + P.o_cmap);
   uint32_t* tot = (uint32_t*)(B + P.o_tot);
-  const SrtDeep dp{(SrtItem*)(B + P.o_deep), tot + 2, P.a.np * (uint32_t)SB};
+  const SrtDeep dp{(SrtItem*)(B + P.o_deep), tot + 2, P.a.np * (uint32_t)SB, ctx->g.flags};
   PLUSS_HIP_CHECK(hipMemsetAsync(tot, 0, 16, s));
   const unsigned g1 = (unsigned)P.a.coff[6];
   const bool p2 = m.p2 && (1u << P.a.tsh) == m.T;  // shift decodes of c0
@@ -826,6 +826,7 @@ static int fa_launch(pluss_ctx* ctx, const FaLaunch& L, int src, int phase) {
     case SRC_W32: fa_launch_w32(l); break;
     case SRC_W64: fa_launch_w64(l); break;
     case SRC_SAMPLES: fa_launch_smp(l); break;
+    case SRC_UNI: fa_launch_uni(l); break;
     default: fa_launch_gen(l); break;
   }
   PLUSS_HIP_CHECK(hipGetLastError());
@@ -1004,6 +1005,25 @@ int launch_gen_faithful_refs(pluss_ctx* ctx, uint64_t seed, const uint64_t* tota
 // ---- key-range shards of the single-read pipeline (multi-GPU faithful mode;
 // dist.sharded_faithful_gen_hist): the caller exchanges the per-reference
 // summaries between the four phases
+// All six over r10's own distribution (uniform draws without replacement,
+// r10:156-185) generated in key order inside the pass (pluss_uniform.h): the
+// plan, then the pipeline staging each tile from it.
+int launch_gen_uniform_faithful_refs(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t s) {
+  faith_shards_abandon(ctx);  // these share the handle's faithful buffers
+  if (int rc = faith_direct_shape(ctx, "pluss_dev_gen_uniform_faithful_refs")) return rc;
+  FaRefs a = fa_none();
+  uint64_t any = 0;
+  for (int r = 0; r < 6; ++r) {
+    a.n[r] = totals[r];
+    any += totals[r];
+  }
+  if (!any) return PLUSS_OK;
+  const UniSet* us = nullptr;
+  if (int rc = uni_plan(ctx, seed, totals, s, &us)) return rc;
+  a.us = us;
+  return fa_run(ctx, a, SRC_UNI, false, s);
+}
+
 // ---- key-range shards of the single-read pipeline (multi-GPU faithful mode):
 // every phase writes this shard's summary row in device memory and the next
 // reads the rows of all shards, gathered by the caller (an RCCL all-gather in

@@ -130,6 +130,8 @@ struct pluss_group {
   std::vector<unsigned long long*> blk;   // per device: nshards * GBLOCK
   std::vector<unsigned long long*> list;  // per local shard: resident samples (pluss_group_expand)
   std::vector<uint64_t> list_n;
+  std::vector<unsigned long long*> hl;    // per local shard: its slice of a host list (clean sampled_hist)
+  std::vector<uint64_t> hl_cap;
   std::vector<unsigned long long*> whole; // per device: uploaded whole lists (faithful, arbitrary order)
   std::vector<uint64_t> whole_cap;
   std::map<uint32_t, hipGraphExec_t> graphs;  // dense passes captured per batch size (one local device)
@@ -148,6 +150,7 @@ static void group_free(pluss_group* G) {
   for (auto& kv : G->graphs) (void)hipGraphExecDestroy(kv.second);
   for (size_t i = 0; i < G->ctx.size(); ++i) {
     if (i < G->list.size() && G->list[i]) (void)hipFree(G->list[i]);
+    if (i < G->hl.size() && G->hl[i]) (void)hipFree(G->hl[i]);
     if (G->ctx[i]) pluss_ctx_destroy(G->ctx[i]);
   }
   for (int d = 0; d < G->ndev; ++d) {
@@ -168,6 +171,8 @@ static int group_setup(pluss_group* G) {
   G->ctx.assign((size_t)G->ndev * S, nullptr);
   G->list.assign(G->ctx.size(), nullptr);
   G->list_n.assign(G->ctx.size(), 0);
+  G->hl.assign(G->ctx.size(), nullptr);
+  G->hl_cap.assign(G->ctx.size(), 0);
   G->xs.assign(G->ndev, nullptr);
   G->ev.assign(G->ctx.size() + G->ndev, nullptr);
   G->rows.assign(G->ndev, nullptr);
@@ -660,14 +665,16 @@ int pluss_group_sampled_hist(pluss_group* G, const uint64_t* samples, uint64_t n
         const size_t i = (size_t)d * G->spd + j;
         uint64_t f, m;
         shard_ranges(n, gshard(G, d, j), S, &f, &m);
-        PLUSS_HIP_CHECK(hipStreamSynchronize(G->ctx[i]->stream));
-        if (G->list[i]) (void)hipFree(G->list[i]);
-        G->list[i] = nullptr;
-        G->list_n[i] = 0;
-        PLUSS_HIP_CHECK(hipMalloc((void**)&G->list[i], (m ? m : 1) * 8));
-        PLUSS_HIP_CHECK(hipMemcpyAsync(G->list[i], samples + f, m * 8, hipMemcpyHostToDevice, G->ctx[i]->stream));
-        G->list_n[i] = m;
-        const int rc = pluss_dev_sampled_hist(G->ctx[i], (const uint64_t*)G->list[i], m, G->ctx[i]->stream);
+        if (G->hl_cap[i] < m || !G->hl[i]) {
+          PLUSS_HIP_CHECK(hipStreamSynchronize(G->ctx[i]->stream));
+          if (G->hl[i]) (void)hipFree(G->hl[i]);
+          G->hl[i] = nullptr;
+          G->hl_cap[i] = 0;
+          PLUSS_HIP_CHECK(hipMalloc((void**)&G->hl[i], (m ? m : 1) * 8));
+          G->hl_cap[i] = m ? m : 1;
+        }
+        PLUSS_HIP_CHECK(hipMemcpyAsync(G->hl[i], samples + f, m * 8, hipMemcpyHostToDevice, G->ctx[i]->stream));
+        const int rc = pluss_dev_sampled_hist(G->ctx[i], (const uint64_t*)G->hl[i], m, G->ctx[i]->stream);
         if (rc && !frc) {
           frc = rc;
           ferr = pluss_last_error();

@@ -56,6 +56,7 @@ constexpr unsigned int FLAG_OVERFLOW = 1u;  // more distinct histogram keys than
 constexpr unsigned int FLAG_LOOKBACK = 2u;  // a faithful chunk's predecessor never published (stalled pass)
 constexpr unsigned int FLAG_SHARD = 4u;     // a key-range shard of this pass failed (its row's error word)
 constexpr unsigned int FLAG_SORT = 8u;      // the bucket sort's plan exceeded its capacity (input left unsorted)
+constexpr unsigned int FLAG_UNI = 16u;      // the uniform key-order generator drew too few candidates (P ~ 1e-23)
 constexpr size_t DB_OFF = (2 * (size_t)(GCAP + NREP * RCAP) + NBROW * BSTRIDE + 4 + 8 + BSTRIDE - 1) / BSTRIDE * BSTRIDE;
 constexpr size_t TABLE_WORDS = DB_OFF + (size_t)(NBROW + 1) * BSTRIDE;
 constexpr size_t TABLE_BYTES = TABLE_WORDS * 8;
@@ -85,6 +86,14 @@ struct FaithfulBufs {
   unsigned char* sbuf = nullptr;
 };
 
+struct UniSet;  // the uniform key-order generator's plan (pluss_uniform.h)
+struct UniBufs {  // its device buffers (grown on demand, per handle)
+  UniSet* set = nullptr;
+  uint32_t *cnt = nullptr, *bits = nullptr, *tmap = nullptr;
+  uint64_t *pre = nullptr, *rb = nullptr, *bsum = nullptr;
+  size_t set_cap = 0, cnt_cap = 0, bits_cap = 0, tmap_cap = 0, pre_cap = 0, rb_cap = 0, bsum_cap = 0;
+};
+
 struct FaShards;  // a key-range shard's state between the phases of pluss_dev_faithful_shards_* (pluss_faithful.h)
 
 }  // namespace pluss
@@ -101,6 +110,7 @@ struct pluss_ctx {
   pluss::FaithfulBufs fb;
   pluss::FaShards* fsh2;  // created on first use (faith_shards_local), freed by faith_shards_free
   pluss::FaithfulBufs fbr[6];  // per-reference buffers of pluss_dev_faithful_hist_refs
+  pluss::UniBufs ub;           // the uniform key-order generator's plan
   hipStream_t fst[6];          // ... and its streams (created on first use)
   hipEvent_t fev[7];           // fork / join events
   hipStream_t last;   // stream of the most recent launch (fetch orders after it)
@@ -171,7 +181,13 @@ int faith_shards_carry(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, in
 int faith_shards_cut(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards, uint64_t* d_row,
                      hipStream_t s);
 int faith_shards_hist(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards, hipStream_t s);
-void faith_shards_abandon(pluss_ctx* ctx);  // a one-GPU faithful call ends any half-finished shard pass
+void faith_shards_abandon(pluss_ctx* ctx);
+// r10's uniform draw in key order (pluss_uniform.h / .hip)
+int uni_check(const pluss_ctx* ctx, int32_t ref, uint64_t total, const char* api);
+int uni_plan(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t s, const UniSet** out);
+int launch_expand_uniform_sorted(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t total, uint64_t first,
+                                 uint64_t n, uint64_t* d_out, hipStream_t s);
+int launch_gen_uniform_faithful_refs(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t s);  // a one-GPU faithful call ends any half-finished shard pass
 void faith_shards_free(pluss_ctx* ctx);
 
 }  // namespace pluss

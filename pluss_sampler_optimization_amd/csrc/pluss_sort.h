@@ -78,6 +78,7 @@ struct SrtDeep {
   SrtItem* items;
   unsigned int* head;
   uint32_t cap;
+  unsigned int* flags;  // the handle's flags: FLAG_SORT when an item finds the list full
 };
 
 __host__ __device__ inline uint32_t srt_log2_ceil(uint64_t x) {
@@ -690,6 +691,7 @@ __global__ __launch_bounds__(SB) void k_srt_final(const SrtRefs a, const SrtPare
     if (threadIdx.x == 0) {
       const unsigned int q = atomicAdd(dp.head, 1u);
       if (q < dp.cap) dp.items[q] = SrtItem{s, cnt, hi, p << 1 | buf};
+      else atomicOr(&dp.flags[0], FLAG_SORT);  // never written past the list: the pass reports it instead
     }
   };
   if (P.d2 == 0) {

@@ -1,0 +1,345 @@
+// pluss_uniform.h — r10's own sample distribution generated directly in r10's
+// pop order.
+//
+// r10 draws each reference's samples with rand() % (N-1) per index and
+// rejects duplicates (r10:156-185): a uniform S-subset of the reference's
+// span^d iteration points (the Feistel lists' distribution).
+// Its priority queue then pops them in key order a*T+tid (IterationComp,
+// pluss_utils.h:175-267).  This generator produces that same distribution
+// already in key order, without a sort:
+//
+//   1. candidates: every point is a candidate independently with probability
+//      p = min(1, (S + 10 sqrt(S) + 32) / D) (D points).  The points are cut
+//      into leaves of consecutive points in key order -- a leaf is one key
+//      "row" (q, c1) of 3-D references, or q of 2-D ones, cut into blocks of K
+//      w-values (w = c2, or c1) times the simulated threads -- so a leaf's
+//      candidate count is Binomial(G_l, p), drawn per leaf by inversion from a
+//      counter-based hash (about UG_MEAN per leaf); the candidates themselves
+//      are a uniform subset of the leaf of that size (independent uniform
+//      offsets, sorted, redrawn on a duplicate), i.e. Bernoulli(p) sampling
+//      of the whole space;
+//   2. conditioned on T' >= S candidates, removing a uniform (T'-S)-subset of
+//      them (the first T'-S outputs of a keyed Feistel permutation of the
+//      candidate ranks [0, T')) leaves a uniform S-subset of the points
+//      (exchangeability: Bernoulli sampling conditioned on its size is
+//      uniform over subsets of that size, and so is a uniform sub-subset).
+//      T' < S (probability about Phi(-10) = 7.6e-24) is reported as an error.
+//
+// Sample i of the list is the i-th surviving candidate in key order.  The
+// per-leaf counts, their prefix, the removal bitmap and its prefix form the
+// plan (pluss_uniform.hip); any tile of TILE consecutive samples is then
+// generated independently from it (k_fa_* SRC_UNI, k_ug_expand).  Every
+// floating-point step is an IEEE add, multiply or divide in a fixed order
+// (no FMA contraction, no library call), so the host oracle
+// (oracle/pluss_oracle.c orc_expand_uniform) reproduces the lists bit for bit.
+#pragma once
+#include <math.h>
+#include <stdint.h>
+
+#include "pluss_model.h"
+
+#if defined(__HIPCC__)
+#include "pluss_internal.h"
+#endif
+
+namespace pluss {
+
+constexpr uint32_t UG_MEAN = 16;     // expected candidates per leaf
+constexpr uint32_t UG_DIRECT = 64;   // leaves of at most this many points: one Bernoulli draw per point
+constexpr uint32_t UG_LEAFMAX = 1024;  // more candidates in one leaf: PLUSS_ERR_CAPACITY (P < 1e-300)
+constexpr uint32_t UG_CAP = 6144;      // candidates of one tile's leaves (LDS words)
+constexpr uint32_t UG_TRIES = 4096;    // redraws of a leaf's offsets before FLAG_UNI (P(dup) <= 1/2 per draw)
+constexpr uint32_t UG_TILE = 4096;     // samples per tile (== the faithful pipeline's TILE)
+
+struct UniGen {
+  uint32_t ref, dim3, T, span, Q, CS;
+  uint32_t tsh, tp2, cssh, csp2;  // T = 2^tsh, CS = 2^cssh (shift decodes)
+  uint64_t S, D;                  // samples, points
+  uint64_t W, K, nb;              // w-values per row, w-values per leaf, leaves per row
+  uint64_t RA, RB, LA, L;         // rows of block A / B, leaves of block A, all leaves
+  double p, r;                    // candidate probability per point; p / (1 - p)
+  uint64_t base;                  // hash key of (seed, ref)
+  Div64 dnb, dspan, dtA, dtB;     // division by nb, span, T, T-1
+};
+
+// Host: the generator of S samples of reference `ref` (validated by the
+// caller: N % (CS*T) == 0, 1 <= S <= span^d, S + 10 sqrt(S) + 32 < 2^32).
+inline UniGen make_unigen(uint64_t N, uint64_t T, uint64_t CS, bool range_full, uint64_t seed, uint32_t ref,
+                          uint64_t S) {
+  UniGen u;
+  u.ref = ref;
+  u.dim3 = (ref == C0 || ref == C1) ? 0u : 1u;
+  u.T = (uint32_t)T;
+  u.CS = (uint32_t)CS;
+  u.span = (uint32_t)(range_full ? N : N - 1);
+  u.Q = (uint32_t)(N / T);
+  const uint64_t QA = range_full ? u.Q : u.Q - 1;
+  u.W = u.span;
+  u.RA = u.dim3 ? QA * u.span : QA;
+  u.RB = range_full ? 0 : (u.dim3 ? u.span : 1);
+  u.D = (u.RA * T + u.RB * (T - 1)) * u.W;
+  u.S = S;
+  const double E = (double)S + 10.0 * sqrt((double)S) + 32.0;
+  u.p = E >= (double)u.D ? 1.0 : E / (double)u.D;
+  u.r = u.p < 1.0 ? u.p / (1.0 - u.p) : 0.0;
+  const double kk = (double)UG_MEAN / ((double)T * u.p);
+  u.K = kk < 1.0 ? 1 : (kk >= (double)u.W ? u.W : (uint64_t)kk);
+  if (u.K > 0xFFFFFFFFull / T) u.K = 0xFFFFFFFFull / T;  // a leaf's points fit 32 bits
+  u.nb = (u.W + u.K - 1) / u.K;
+  u.LA = u.RA * u.nb;
+  u.L = u.LA + u.RB * u.nb;
+  u.base = mix64(seed ^ ((uint64_t)(ref + 1) * 0x9E3779B97F4A7C15ull) ^ 0xC2B2AE3D27D4EB4Full);
+  u.tsh = 0;
+  while ((1ull << u.tsh) < T) ++u.tsh;
+  u.tp2 = (1ull << u.tsh) == T ? 1u : 0u;
+  u.cssh = 0;
+  while ((1ull << u.cssh) < CS) ++u.cssh;
+  u.csp2 = (1ull << u.cssh) == CS ? 1u : 0u;
+  u.dnb = make_div64(u.nb);
+  u.dspan = make_div64(u.span ? u.span : 1);
+  u.dtA = make_div64(T);
+  u.dtB = make_div64(T > 1 ? T - 1 : 1);
+  return u;
+}
+
+// a leaf: its block (0: A, 1: B), row, w-block, w-values and points
+struct UniLeaf {
+  uint32_t blk;
+  uint64_t row, wb, kw, tb, G;
+};
+PM_HD UniLeaf uni_leaf(const UniGen& u, uint64_t l) {
+  UniLeaf f;
+  f.blk = l >= u.LA ? 1u : 0u;
+  const uint64_t lb = f.blk ? l - u.LA : l;
+  f.row = div64(lb, u.dnb);
+  f.wb = lb - f.row * u.nb;
+  const uint64_t w0 = f.wb * u.K;
+  f.kw = u.W - w0 < u.K ? u.W - w0 : u.K;
+  f.tb = f.blk ? u.T - 1 : u.T;
+  f.G = f.kw * f.tb;
+  return f;
+}
+
+// the leaf's hash key for attempt a (a = ~0: per-point draws, ~1: the count)
+PM_HD uint64_t uni_leafkey(const UniGen& u, uint64_t l, uint32_t a) {
+  return mix64(u.base + l * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)a * 0xD1B54A32D192ED03ull);
+}
+PM_HD uint64_t uni_hash(uint64_t lk, uint64_t i) { return mix64(lk + i * 0x8CB92BA72F3D8DD7ull); }
+PM_HD double uni_u01(uint64_t h) { return (double)(h >> 11) * 0x1.0p-53; }
+
+// per-point Bernoulli draws (small or dense leaves: with p <= 1/64 and at most
+// 4*UG_MEAN expected candidates, independent offsets collide rarely)
+PM_HD bool uni_direct(const UniGen& u, const UniLeaf& f) {
+  return f.G <= UG_DIRECT || (double)f.G * u.p > 4.0 * (double)UG_MEAN || u.p > 0.015625;
+}
+
+// The leaf's candidate count: Binomial(G, p).  Inversion with the pmf
+// recurrence f(x+1) = f(x) (G-x)/(x+1) * p/(1-p) from f(0) = (1-p)^G (square
+// and multiply), one uniform draw.
+PM_HD uint64_t uni_count(const UniGen& u, uint64_t l) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+  const UniLeaf f = uni_leaf(u, l);
+  if (u.p >= 1.0) return f.G;
+  if (uni_direct(u, f)) {
+    const uint64_t lk = uni_leafkey(u, l, 0xFFFFFFFFu);
+    uint64_t c = 0;
+    for (uint64_t j = 0; j < f.G; ++j) c += uni_u01(uni_hash(lk, j)) < u.p ? 1u : 0u;
+    return c;
+  }
+  double pm = 1.0, b = 1.0 - u.p;
+  for (uint64_t e = f.G; e; e >>= 1) {
+    if (e & 1) pm = pm * b;
+    b = b * b;
+  }
+  double x_u = uni_u01(uni_hash(uni_leafkey(u, l, 0xFFFFFFFEu), 0));
+  uint64_t x = 0;
+  while (x_u >= pm && x < f.G) {
+    x_u = x_u - pm;
+    pm = pm * (double)(f.G - x);
+    pm = pm / (double)(x + 1);
+    pm = pm * u.r;
+    ++x;
+  }
+  return x;
+}
+
+// candidate offset i (attempt a) of a counted leaf: uniform in [0, G)
+PM_HD uint64_t uni_offset(uint64_t lk, uint64_t i, uint64_t G) { return mulhi64(uni_hash(lk, i), G); }
+
+// ---- the removal permutation: a keyed cycle-walking Feistel permutation of
+// the candidate ranks [0, Tp); its first Tp - S outputs are removed
+struct UniPerm {
+  uint32_t key[4], h;
+  uint64_t D, mask;
+};
+PM_HD UniPerm uni_perm_make(const UniGen& u, uint64_t Tp) {
+  UniPerm p;
+  p.D = Tp;
+  p.h = 1;
+  while ((1ull << (2 * p.h)) < Tp) ++p.h;
+  p.mask = (1ull << p.h) - 1;
+  for (int r = 0; r < 4; ++r)
+    p.key[r] = (uint32_t)mix64(u.base ^ ((uint64_t)(r + 1) * 0xD1B54A32D192ED03ull) ^ 0x6A09E667F3BCC909ull);
+  return p;
+}
+PM_HD uint64_t uni_perm(const UniPerm& p, uint64_t y) {
+  const uint32_t mask = (uint32_t)p.mask;
+  do {
+    uint32_t L = (uint32_t)(y >> p.h), R = (uint32_t)y & mask;
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t t = R;
+      R = L ^ (lowbias32(R ^ p.key[r]) & mask);
+      L = t;
+    }
+    y = ((uint64_t)L << p.h) | R;
+  } while (y >= p.D);
+  return y;
+}
+
+// digits of the point at offset o of leaf f (o < f.G: w = wb*K + o / tb, t = o % tb)
+PM_HD KeyDigits uni_digits(const UniGen& u, const UniLeaf& f, uint64_t o) {
+  KeyDigits d;
+  uint64_t wq;
+  if (!f.blk && u.tp2) {
+    wq = o >> u.tsh;
+    d.t = (uint32_t)(o & (u.T - 1));
+  } else {
+    const Div64& dt = f.blk ? u.dtB : u.dtA;
+    wq = div64(o, dt);
+    d.t = (uint32_t)(o - wq * f.tb);
+  }
+  const uint32_t w = (uint32_t)(f.wb * u.K + wq);
+  if (f.blk) {
+    d.q = u.Q - 1;
+    d.c1 = u.dim3 ? (uint32_t)f.row : w;
+  } else if (u.dim3) {
+    const uint64_t q = div64(f.row, u.dspan);
+    d.q = (uint32_t)q;
+    d.c1 = (uint32_t)(f.row - q * u.span);
+  } else {
+    d.q = (uint32_t)f.row;
+    d.c1 = w;
+  }
+  d.c2 = u.dim3 ? w : 0u;
+  return d;
+}
+
+// packed sample ref|c0|c1|c2 of digits (c0 = ((q / CS) * T + t) * CS + q % CS)
+PM_HD uint64_t uni_pack(const UniGen& u, const KeyDigits& d) {
+  const uint32_t c0 = (u.csp2 && u.tp2) ? (((((d.q >> u.cssh) << u.tsh) | d.t) << u.cssh) | (d.q & (u.CS - 1)))
+                                        : ((d.q / u.CS) * u.T + d.t) * u.CS + d.q % u.CS;
+  return pack(u.ref, c0, d.c1, d.c2);
+}
+
+// ---- the plan of up to six references' lists (device memory) ----------------
+struct UniSet {
+  UniGen u[6];
+  uint64_t loff[7];     // first leaf of each reference in cnt / pre; loff[6] = all leaves
+  uint64_t woff[7];     // first removal-bitmap word of each reference
+  uint64_t tmoff[7];    // first tile-map entry of each reference (tiles of UG_TILE samples)
+  const uint32_t* cnt;  // candidates per leaf
+  const uint64_t* pre;  // exclusive prefix of cnt over all leaves (loff[6] + 1 words)
+  const uint32_t* bits; // removed candidate ranks, per reference
+  const uint64_t* rb;   // exclusive prefix of the bitmap words' popcounts (woff[6] + 1 words)
+  const uint32_t* tmap; // per tile: the leaf holding its first sample
+  unsigned int* flags;  // the handle's flags (FLAG_UNI)
+};
+
+#if defined(__HIPCC__)
+// candidates of reference r before leaf l / removed candidates of rank < x
+__device__ __forceinline__ uint64_t uni_pre(const UniSet* __restrict__ us, uint32_t r, uint64_t l) {
+  return us->pre[us->loff[r] + l] - us->pre[us->loff[r]];
+}
+__device__ __forceinline__ uint64_t uni_word(const UniSet* __restrict__ us, uint32_t r, uint64_t x) {
+  const uint64_t w = us->woff[r] + (x >> 5), e = us->woff[r + 1] - 1;  // (clamped: a flagged plan stays in bounds)
+  return w < e ? w : e;
+}
+__device__ __forceinline__ uint64_t uni_removed_before(const UniSet* __restrict__ us, uint32_t r, uint64_t x) {
+  const uint64_t w = uni_word(us, r, x);
+  const uint32_t below = us->bits[w] & ((1u << (x & 31)) - 1u);
+  return us->rb[w] - us->rb[us->woff[r]] + (uint64_t)__popc(below);
+}
+
+// Generate samples [lt*UG_TILE, lt*UG_TILE + mt) of reference r's list into
+// raw[slot(e)] (e = sample - lt*UG_TILE), all NT threads of the workgroup; cand:
+// LDS scratch of UG_CAP words.  The leaves from the one holding the tile's
+// first sample to the one holding the next tile's first are regenerated:
+// each thread draws one leaf's candidates (sorted offsets) into cand at the
+// leaf's candidate rank, then every surviving candidate of the tile is packed
+// at its sample index.  A window past UG_CAP candidates or a leaf past
+// UG_LEAFMAX (neither happens with probability above 1e-20) sets FLAG_UNI.
+template <int NT, class SLOT>
+__device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_t r, uint64_t lt, uint32_t mt,
+                                          unsigned long long* raw, uint32_t* cand, unsigned int* flags,
+                                          SLOT&& slot) {
+  const UniGen& u = us->u[r];
+  const uint64_t tm0 = us->tmoff[r], nt = us->tmoff[r + 1] - tm0, lg0 = us->loff[r];
+  const uint64_t la = us->tmap[tm0 + lt], lb = lt + 1 < nt ? us->tmap[tm0 + lt + 1] : u.L - 1;
+  const uint64_t pbase = us->pre[lg0];
+  const bool leaves_ok = la <= lb && lb < u.L;
+  const uint64_t r0 = leaves_ok ? us->pre[lg0 + la] - pbase : 0, rend = leaves_ok ? us->pre[lg0 + lb + 1] - pbase : 0;
+  if (!leaves_ok || rend - r0 > UG_CAP) {
+    if (threadIdx.x == 0) atomicOr(flags, FLAG_UNI);
+    __syncthreads();
+    return;
+  }
+  const uint64_t f0 = lt * UG_TILE;
+  for (uint64_t l = la + threadIdx.x; l <= lb; l += NT) {
+    const uint32_t c = us->cnt[lg0 + l];
+    if (!c) continue;
+    if (c > UG_LEAFMAX) {
+      atomicOr(flags, FLAG_UNI);
+      continue;
+    }
+    uint32_t* seg = cand + (us->pre[lg0 + l] - pbase - r0);
+    const UniLeaf f = uni_leaf(u, l);
+    if (u.p >= 1.0) {
+      for (uint32_t j = 0; j < c; ++j) seg[j] = j;
+    } else if (uni_direct(u, f)) {
+      const uint64_t lk = uni_leafkey(u, l, 0xFFFFFFFFu);
+      uint32_t k = 0;
+      for (uint32_t j = 0; j < (uint32_t)f.G; ++j)
+        if (uni_u01(uni_hash(lk, j)) < u.p) seg[k++] = j;
+    } else {
+      for (uint32_t a = 0;; ++a) {  // independent uniform offsets, sorted; redrawn on a duplicate
+        if (a == UG_TRIES) {
+          atomicOr(flags, FLAG_UNI);
+          break;
+        }
+        const uint64_t lk = uni_leafkey(u, l, a);
+        for (uint32_t i = 0; i < c; ++i) {
+          const uint32_t x = (uint32_t)uni_offset(lk, i, f.G);
+          uint32_t j = i;
+          while (j > 0 && seg[j - 1] > x) {
+            seg[j] = seg[j - 1];
+            --j;
+          }
+          seg[j] = x;
+        }
+        bool dup = false;
+        for (uint32_t i = 1; i < c; ++i) dup |= seg[i] == seg[i - 1];
+        if (!dup) break;
+      }
+    }
+  }
+  __syncthreads();
+  for (uint64_t l = la + threadIdx.x; l <= lb; l += NT) {
+    const uint32_t c = us->cnt[lg0 + l];
+    if (!c || c > UG_LEAFMAX) continue;
+    const uint64_t x0 = us->pre[lg0 + l] - pbase;
+    const uint32_t* seg = cand + (x0 - r0);
+    const UniLeaf f = uni_leaf(u, l);
+    for (uint32_t i = 0; i < c; ++i) {
+      const uint64_t x = x0 + i;
+      if ((us->bits[uni_word(us, r, x)] >> (x & 31)) & 1u) continue;  // removed
+      const uint64_t e = x - uni_removed_before(us, r, x) - f0;
+      if (e < mt) raw[slot((uint32_t)e)] = uni_pack(u, uni_digits(u, f, seg[i]));
+    }
+  }
+  __syncthreads();
+}
+#endif
+
+}  // namespace pluss

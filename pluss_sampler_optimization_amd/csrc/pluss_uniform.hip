@@ -1,0 +1,288 @@
+// pluss_uniform.hip — r10's uniform draw in key order (pluss_uniform.h): the
+// plan kernels, the materialised lists (pluss_dev_expand_uniform_sorted) and
+// the faithful pass over lists generated inside it
+// (pluss_dev_gen_uniform_faithful_refs).
+//
+// Plan, all references at once (a few small launches, no host round trip):
+//   k_ug_count   every leaf's candidate count (Binomial by inversion);
+//   scan         their exclusive prefix over all leaves (candidate ranks);
+//   k_ug_remove  per reference T' = its candidates, the ranks F(0..T'-S-1) of
+//                the removal permutation set in its bitmap (T' < S: FLAG_UNI);
+//   scan         the prefix of the bitmap words' popcounts;
+//   k_ug_tiles   per leaf its surviving candidates' sample indices; the leaf
+//                holding each tile's first sample.
+// A tile of samples is then generated from the plan alone (uni_stage).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+
+#include "pluss_faithful.h"
+#include "pluss_uniform.h"
+
+namespace pluss {
+
+constexpr uint32_t UB = 256, UE = 16, UBATCH = UB * UE;  // scan: threads, values per thread, per block
+
+template <int MODE>
+__device__ __forceinline__ uint64_t ug_val(const uint32_t* in, uint64_t i) {
+  return MODE ? (uint64_t)__popc(in[i]) : (uint64_t)in[i];
+}
+
+// per block of UBATCH values: their sum
+template <int MODE>
+__global__ __launch_bounds__(UB) void k_ug_bsum(const uint32_t* __restrict__ in, uint64_t n,
+                                               uint64_t* __restrict__ bsum) {
+  __shared__ uint64_t w[UB / 64];
+  const uint64_t b0 = (uint64_t)blockIdx.x * UBATCH;
+  uint64_t s = 0;
+  for (uint32_t k = 0; k < UE; ++k) {
+    const uint64_t i = b0 + (uint64_t)k * UB + threadIdx.x;
+    if (i < n) s += ug_val<MODE>(in, i);
+  }
+  s = sc_wave_red<false>(s);
+  if (__lane_id() == 0) w[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) bsum[blockIdx.x] = w[0] + w[1] + w[2] + w[3];
+}
+
+// exclusive scan of the nb block sums in place (one workgroup); bsum[nb] = the total
+__global__ __launch_bounds__(UB) void k_ug_btop(uint64_t* __restrict__ bsum, uint32_t nb) {
+  __shared__ uint64_t w[UB / 64];
+  uint64_t carry = 0;
+  for (uint32_t b = 0; b < nb; b += UB) {
+    const uint32_t i = b + threadIdx.x;
+    const uint64_t v = i < nb ? bsum[i] : 0ull;
+    const uint64_t inc = sc_wave_scan<false>(v, __lane_id());
+    if (__lane_id() == 63) w[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+    for (uint32_t x = 0; x < UB / 64; ++x) {
+      if (x < (threadIdx.x >> 6)) pre += w[x];
+      tot += w[x];
+    }
+    if (i < nb) bsum[i] = carry + pre + inc - v;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bsum[nb] = carry;
+}
+
+// out[i] = exclusive prefix of the values (out[n] = the total)
+template <int MODE>
+__global__ __launch_bounds__(UB) void k_ug_bapply(const uint32_t* __restrict__ in, uint64_t n,
+                                                 const uint64_t* __restrict__ bsum, uint64_t* __restrict__ out) {
+  __shared__ uint64_t w[UB / 64];
+  const uint64_t b0 = (uint64_t)blockIdx.x * UBATCH + (uint64_t)threadIdx.x * UE;  // a run of UE values per thread
+  uint64_t v[UE], s = 0;
+  for (uint32_t k = 0; k < UE; ++k) {
+    v[k] = b0 + k < n ? ug_val<MODE>(in, b0 + k) : 0ull;
+    s += v[k];
+  }
+  const uint64_t inc = sc_wave_scan<false>(s, __lane_id());
+  if (__lane_id() == 63) w[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  uint64_t pre = bsum[blockIdx.x];
+  for (uint32_t x = 0; x < (threadIdx.x >> 6); ++x) pre += w[x];
+  uint64_t run = pre + inc - s;
+  for (uint32_t k = 0; k < UE; ++k) {
+    if (b0 + k < n) out[b0 + k] = run;
+    run += v[k];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = bsum[gridDim.x];
+}
+
+static int ug_scan(const uint32_t* in, uint64_t n, uint64_t* bsum, uint64_t* out, int mode, hipStream_t s) {
+  const uint32_t nb = (uint32_t)((n + UBATCH - 1) / UBATCH);
+  if (nb == 0) {
+    PLUSS_HIP_CHECK(hipMemsetAsync(out, 0, 8, s));
+    return PLUSS_OK;
+  }
+  if (mode) hipLaunchKernelGGL(k_ug_bsum<1>, dim3(nb), dim3(UB), 0, s, in, n, bsum);
+  else hipLaunchKernelGGL(k_ug_bsum<0>, dim3(nb), dim3(UB), 0, s, in, n, bsum);
+  hipLaunchKernelGGL(k_ug_btop, dim3(1), dim3(UB), 0, s, bsum, nb);
+  if (mode) hipLaunchKernelGGL(k_ug_bapply<1>, dim3(nb), dim3(UB), 0, s, in, n, (const uint64_t*)bsum, out);
+  else hipLaunchKernelGGL(k_ug_bapply<0>, dim3(nb), dim3(UB), 0, s, in, n, (const uint64_t*)bsum, out);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  return PLUSS_OK;
+}
+
+__device__ __forceinline__ uint32_t ug_ref_of(const uint64_t* off, uint64_t g) {
+  uint32_t r = 0;
+  for (int x = 1; x < 6; ++x) r += g >= off[x] ? 1u : 0u;
+  return r;
+}
+
+__global__ __launch_bounds__(UB) void k_ug_count(const UniSet* __restrict__ us, uint32_t* __restrict__ cnt,
+                                                unsigned int* flags) {
+  const uint64_t n = us->loff[6];
+  for (uint64_t g = (uint64_t)blockIdx.x * UB + threadIdx.x; g < n; g += (uint64_t)gridDim.x * UB) {
+    const uint32_t r = ug_ref_of(us->loff, g);
+    const uint64_t c = uni_count(us->u[r], g - us->loff[r]);
+    if (c > UG_LEAFMAX) atomicOr(flags, FLAG_UNI);
+    cnt[g] = c > UG_LEAFMAX ? UG_LEAFMAX + 1 : (uint32_t)c;
+  }
+}
+
+// the removal bitmaps (zeroed); T' < S or a bitmap too small for T' sets FLAG_UNI
+__global__ __launch_bounds__(UB) void k_ug_remove(const UniSet* __restrict__ us, uint32_t* __restrict__ bits,
+                                                 unsigned int* flags) {
+  const uint64_t stride = (uint64_t)gridDim.x * UB;
+  for (uint32_t r = 0; r < 6; ++r) {
+    const UniGen& u = us->u[r];
+    if (us->loff[r + 1] == us->loff[r]) continue;
+    const uint64_t Tp = us->pre[us->loff[r + 1]] - us->pre[us->loff[r]];
+    if (Tp < u.S || (Tp >> 5) >= us->woff[r + 1] - us->woff[r]) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(flags, FLAG_UNI);
+      continue;
+    }
+    const UniPerm P = uni_perm_make(u, Tp);
+    const uint64_t m = Tp - u.S;
+    for (uint64_t i = (uint64_t)blockIdx.x * UB + threadIdx.x; i < m; i += stride) {
+      const uint64_t y = uni_perm(P, i);
+      atomicOr(&bits[us->woff[r] + (y >> 5)], 1u << (y & 31));
+    }
+  }
+}
+
+// per leaf: the sample index of its first surviving candidate and their
+// number; the leaf holding each tile's first sample
+__global__ __launch_bounds__(UB) void k_ug_tiles(const UniSet* __restrict__ us, uint32_t* __restrict__ tmap) {
+  const uint64_t n = us->loff[6];
+  for (uint64_t g = (uint64_t)blockIdx.x * UB + threadIdx.x; g < n; g += (uint64_t)gridDim.x * UB) {
+    const uint32_t c = us->cnt[g];
+    if (!c || c > UG_LEAFMAX) continue;
+    const uint32_t r = ug_ref_of(us->loff, g);
+    const uint64_t l = g - us->loff[r];
+    const uint64_t x0 = uni_pre(us, r, l);
+    const uint64_t b0 = uni_removed_before(us, r, x0), b1 = uni_removed_before(us, r, x0 + c);
+    const uint64_t f = x0 - b0, kept = c - (b1 - b0);
+    const uint64_t nt = us->tmoff[r + 1] - us->tmoff[r];
+    for (uint64_t t = (f + UG_TILE - 1) / UG_TILE; t * UG_TILE < f + kept && t < nt; ++t)
+      tmap[us->tmoff[r] + t] = (uint32_t)l;
+  }
+}
+
+// materialised list: samples [first, first + n) of reference r, one tile per workgroup
+__global__ __launch_bounds__(UB) void k_ug_expand(const UniSet* __restrict__ us, uint32_t r, uint64_t first,
+                                                 uint64_t n, uint64_t S, uint64_t* __restrict__ out,
+                                                 unsigned int* flags) {
+  __shared__ unsigned long long raw[UG_TILE];
+  __shared__ uint32_t cand[UG_CAP];
+  const uint64_t lt = first / UG_TILE + blockIdx.x;
+  const uint64_t t0 = lt * UG_TILE;
+  const uint32_t mt = (uint32_t)(S - t0 < UG_TILE ? S - t0 : UG_TILE);
+  uni_stage<UB>(us, r, lt, mt, raw, cand, flags, [](uint32_t e) { return e; });
+  for (uint32_t e = threadIdx.x; e < mt; e += UB) {
+    const uint64_t i = t0 + e;
+    if (i >= first && i < first + n) out[i - first] = raw[e];
+  }
+}
+
+__global__ void k_ug_setup(const UniSet h, UniSet* d) { *d = h; }
+
+static int ug_grow(void** p, size_t* cap, size_t bytes) {
+  if (bytes <= *cap) return PLUSS_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  if (hipMalloc(p, bytes) != hipSuccess) {
+    set_error("hipMalloc failed for the uniform generator's plan");
+    return PLUSS_ERR_ALLOC;
+  }
+  *cap = bytes;
+  return PLUSS_OK;
+}
+
+int uni_check(const pluss_ctx* ctx, int32_t ref, uint64_t total, const char* api) {
+  const pluss_cfg& c = ctx->cfg;
+  if ((uint64_t)c.n % ((uint64_t)c.chunk * (uint64_t)c.threads) != 0) {
+    set_error(std::string(api) + ": needs N % (chunk*threads) == 0 (key order)");
+    return PLUSS_ERR_CONFIG;
+  }
+  const uint64_t span = c.range_full ? (uint64_t)c.n : (uint64_t)c.n - 1;
+  const uint64_t D = (ref == PLUSS_C0 || ref == PLUSS_C1) ? span * span : span * span * span;
+  const double E = (double)total + 10.0 * std::sqrt((double)total) + 32.0;
+  if (total < 1 || total > D || E >= 4294967296.0) {
+    set_error(std::string(api) + ": needs 1 <= total <= span^d and total + 10 sqrt(total) + 32 < 2^32");
+    return PLUSS_ERR_CONFIG;
+  }
+  return PLUSS_OK;
+}
+
+// The plan of the references with totals[r] > 0 on stream s; *out = its
+// device UniSet (valid until the next plan on this handle).
+int uni_plan(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t s, const UniSet** out) {
+  UniBufs& b = ctx->ub;
+  UniSet h;
+  std::memset((void*)&h, 0, sizeof h);
+  uint64_t L = 0, Wd = 0, Tt = 0;
+  for (int r = 0; r < 6; ++r) {
+    h.loff[r] = L;
+    h.woff[r] = Wd;
+    h.tmoff[r] = Tt;
+    if (!totals[r]) continue;
+    if (int rc = uni_check(ctx, r, totals[r], "uniform key-order lists")) return rc;
+    h.u[r] = make_unigen((uint64_t)ctx->cfg.n, (uint64_t)ctx->cfg.threads, (uint64_t)ctx->cfg.chunk,
+                         ctx->cfg.range_full != 0, seed, (uint32_t)r, totals[r]);
+    L += h.u[r].L;
+    // room for T' candidates: its mean plus 20 standard deviations (or all points when p = 1)
+    const double E = h.u[r].p * (double)h.u[r].D;
+    const uint64_t tmax = (uint64_t)(E + 20.0 * std::sqrt(E) + 1024.0);
+    Wd += tmax / 32 + 2;
+    Tt += fa_tiles(totals[r]);
+  }
+  h.loff[6] = L;
+  h.woff[6] = Wd;
+  h.tmoff[6] = Tt;
+  const uint64_t nbL = (L + UBATCH - 1) / UBATCH + 1, nbW = (Wd + UBATCH - 1) / UBATCH + 1;
+  int rc = PLUSS_OK;
+  if (!b.set) rc = ug_grow((void**)&b.set, &b.set_cap, sizeof(UniSet));
+  if (!rc) rc = ug_grow((void**)&b.cnt, &b.cnt_cap, (L + 1) * 4);
+  if (!rc) rc = ug_grow((void**)&b.pre, &b.pre_cap, (L + 1) * 8);
+  if (!rc) rc = ug_grow((void**)&b.bits, &b.bits_cap, (Wd + 1) * 4);
+  if (!rc) rc = ug_grow((void**)&b.rb, &b.rb_cap, (Wd + 1) * 8);
+  if (!rc) rc = ug_grow((void**)&b.tmap, &b.tmap_cap, (Tt + 1) * 4);
+  if (!rc) rc = ug_grow((void**)&b.bsum, &b.bsum_cap, (nbL > nbW ? nbL : nbW) * 8 + 8);
+  if (rc) return rc;
+  h.cnt = b.cnt;
+  h.pre = b.pre;
+  h.bits = b.bits;
+  h.rb = b.rb;
+  h.tmap = b.tmap;
+  h.flags = ctx->g.flags;
+  // the plan's parameters travel as a kernel argument (ordered on the stream, no host buffer to keep)
+  hipLaunchKernelGGL(k_ug_setup, dim3(1), dim3(1), 0, s, h, b.set);
+  const int grid = (int)std::min<uint64_t>((L + UB - 1) / UB + 1, 4096);
+  hipLaunchKernelGGL(k_ug_count, dim3(grid), dim3(UB), 0, s, (const UniSet*)b.set, b.cnt, ctx->g.flags);
+  if (int e = ug_scan(b.cnt, L, b.bsum, b.pre, 0, s)) return e;
+  PLUSS_HIP_CHECK(hipMemsetAsync(b.bits, 0, (Wd + 1) * 4, s));
+  PLUSS_HIP_CHECK(hipMemsetAsync(b.tmap, 0, (Tt + 1) * 4, s));
+  hipLaunchKernelGGL(k_ug_remove, dim3(1024), dim3(UB), 0, s, (const UniSet*)b.set, b.bits, ctx->g.flags);
+  if (int e = ug_scan(b.bits, Wd, b.bsum, b.rb, 1, s)) return e;
+  hipLaunchKernelGGL(k_ug_tiles, dim3(grid), dim3(UB), 0, s, (const UniSet*)b.set, b.tmap);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  *out = b.set;
+  return PLUSS_OK;
+}
+
+int launch_expand_uniform_sorted(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t total, uint64_t first,
+                                 uint64_t n, uint64_t* d_out, hipStream_t s) {
+  if (int rc = uni_check(ctx, ref, total, "pluss_dev_expand_uniform_sorted")) return rc;
+  if (first > total || n > total - first) {
+    set_error("pluss_dev_expand_uniform_sorted: [first, first + n) exceeds the list");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (!n) return PLUSS_OK;
+  uint64_t t[6] = {0, 0, 0, 0, 0, 0};
+  t[ref] = total;
+  const UniSet* us = nullptr;
+  if (int rc = uni_plan(ctx, seed, t, s, &us)) return rc;
+  const uint64_t tiles = (first + n - 1) / UG_TILE - first / UG_TILE + 1;
+  hipLaunchKernelGGL(k_ug_expand, dim3((unsigned)tiles), dim3(UB), 0, s, us, (uint32_t)ref, first, n, total,
+                     d_out, ctx->g.flags);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  return PLUSS_OK;
+}
+
+}  // namespace pluss

@@ -95,16 +95,20 @@ int main(int argc, char** argv) {
     CHECK(pluss_group_expand(g, seed, counts));
     CHECK(pluss_group_dense(g, 20, gv));
     CHECK(pluss_dense_keys(&clean, keys));
+    /* (bins of one key -- a reference's unused cases -- summed) vs the whole list's histogram */
     int ok = gv[PLUSS_DENSE_BINS] == 0;
-    for (int k = 0; k < PLUSS_DENSE_BINS; ++k) {
-      uint64_t want = 0;
-      for (uint64_t i = 0; i < b.n_entries; ++i) {
-        const pluss_hist_entry* e = &b.entries[i];
-        const uint64_t key = ((uint64_t)e->ref << 60) | ((uint64_t)e->kind << 56) | (uint64_t)(e->ri + 2);
-        if (key == keys[k]) want = e->count;
-      }
-      ok &= gv[k] == want;
+    uint64_t total_dense = 0;
+    for (int k = 0; k < PLUSS_DENSE_BINS; ++k) total_dense += gv[k];
+    for (uint64_t i = 0; i < b.n_entries; ++i) {
+      const pluss_hist_entry* e = &b.entries[i];
+      const uint64_t key = ((uint64_t)e->ref << 60) | ((uint64_t)e->kind << 56) | (uint64_t)(e->ri + 2);
+      uint64_t got = 0;
+      for (int k = 0; k < PLUSS_DENSE_BINS; ++k)
+        if (keys[k] == key) got += gv[k];
+      ok &= got == e->count;
+      total_dense -= got;
     }
+    ok &= total_dense == 0;  /* no count outside the list's keys */
     report("clean dense x20 (resident lists)", ok);
 
     /* generated key-order slices counted, vs one shard on one device */

@@ -115,3 +115,15 @@ def test_widest_words():
     """N = 2^20 - 32 (T=8): ranks up to N^3, 62-bit words."""
     N = (1 << 20) - 32
     check(N, 8, "C3", feistel(N, 8, "C3", 300_000), 8)
+
+
+@pytest.mark.parametrize("ref", ["C0", "C1"])
+def test_skewed_sparse_ranks(ref):
+    """The 2-D references' sparse ranks (c2 = 0: the low rank bits always
+    zero) concentrated in two thread-local rows of every thread (60,000 of the
+    65,520 points): a few top-level buckets far past SCAP, split and split
+    again on digits whose low part never varies -- the shape of round 3's
+    C0 failures (tests above at N=4096), skewed."""
+    w = window_list(4096, 8, 4, ref, 60_000, [0, 1], 0, 9)
+    rng = np.random.default_rng(4)
+    check(4096, 8, ref, w[rng.permutation(len(w))], 8)

@@ -45,7 +45,7 @@ def test_c_group_equals_one_device(tmp_path, N, T, total, spd):
     exe = build(str(tmp_path))
     r = subprocess.run([exe, str(N), str(T), str(total), str(spd), "0"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
-    lines = r.stdout.strip().splitlines()
+    lines = [x for x in r.stdout.strip().splitlines() if x.split(" ")[0] in ("shards", "ok", "MISMATCH")]  # (RCCL's banner)
     assert lines[0] == f"shards {spd} of {spd}"
     assert lines[1:] == ["ok clean sampled_hist", "ok clean dense x20 (resident lists)", "ok clean gen_count_dense",
                          "ok faithful sampled_hist (any order)", "ok faithful gen_faithful (key-order lists)"]
