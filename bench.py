@@ -320,7 +320,8 @@ def faithful_config3_bench(P, torch, device, stream, reps=5):
     key-order list resident in HBM, read once per pass (8 B per sample);
     generated = the same lists generated inside the pass; radix = r10's real
     input, a list in arbitrary order (the keyed Feistel lists, as rand() draws
-    them, r10:156-185), sorted inside the pass."""
+    them, r10:156-185), sorted inside the pass; uniform = r10's distribution
+    generated in key order inside the pass (pluss_dev_gen_uniform_faithful_refs)."""
     N, T, total = 4096, 8, 1 << 28
     counts = P.default_counts(N, total)
     fcfg = P.SamplerConfig(n=N, threads=T, mode="faithful", device=device)
@@ -338,7 +339,8 @@ def faithful_config3_bench(P, torch, device, stream, reps=5):
             off += c
         runs = {"sorted": (lambda: ctx.faithful_hist_sorted_refs(buf.data_ptr(), counts, sp), reps),
                 "generated": (lambda: ctx.gen_faithful_refs(SEED, counts, sp), reps),
-                "radix": (lambda: ctx.faithful_hist_refs(fe.data_ptr(), counts, sp), reps)}
+                "radix": (lambda: ctx.faithful_hist_refs(fe.data_ptr(), counts, sp), reps),
+                "uniform": (lambda: ctx.gen_uniform_faithful_refs(SEED, counts, sp), reps)}
         hs = {}
         for name, (run, k) in runs.items():
             ctx.reset(sp)
@@ -355,6 +357,9 @@ def faithful_config3_bench(P, torch, device, stream, reps=5):
             out[name] = {"ms": ms, "samples_per_s": total / (ms * 1e-3)}
     out["radix"]["recorded"] = hs["radix"].total() - sum(hs["radix"].cold(r) for r in P.REFS)
     out["radix"]["over_sorted"] = out["radix"]["ms"] / out["sorted"]["ms"]
+    out["uniform"]["recorded"] = hs["uniform"].total() - sum(hs["uniform"].cold(r) for r in P.REFS)
+    out["uniform"]["note"] = ("r10's own distribution (uniform draw without replacement, r10:156-185) generated in "
+                              "key order inside the pass: plan + tile staging, no list in memory, no sort")
     del buf, fe
     assert hs["sorted"].bins == hs["generated"].bins and list(hs["sorted"].traversed) == list(hs["generated"].traversed)
     ach = 8 * total / (out["sorted"]["ms"] * 1e-3) / 1e9
@@ -385,7 +390,9 @@ def faithful_pipeline_bench(P, torch, device, stream, reps=3):
       feistel_radix: uniform lists in arbitrary order (r10's rand() draw,
                      r10:156-185), generated on the device and sorted inside the
                      pass (the radix source);
-      generated:     key-order lists generated inside the pass (no sort).
+      uniform:       r10's distribution generated in key order inside the pass
+                     (pluss_dev_gen_uniform_faithful_refs: no list, no sort);
+      generated:     key-order stratified lists generated inside the pass.
     Host clock around everything, median of `reps`; `host_share` = the CRI ->
     MRC text part's fraction."""
     from pluss_sampler_optimization_amd import host as H
@@ -407,7 +414,10 @@ def faithful_pipeline_bench(P, torch, device, stream, reps=3):
 
             def generated():
                 ctx.gen_faithful_refs(SEED, counts, sp)
-            for src, dev_part in (("feistel_radix", feistel_radix), ("generated", generated)):
+
+            def uniform():
+                ctx.gen_uniform_faithful_refs(SEED, counts, sp)
+            for src, dev_part in (("feistel_radix", feistel_radix), ("uniform", uniform), ("generated", generated)):
                 runs = []
                 for k in range(reps + 1):  # the first run warms (code load, buffers)
                     torch.cuda.synchronize()

@@ -1,5 +1,5 @@
-"""Faithful-mode pass time of the three sources (key-ordered list, generated
-lists, radix sort of a Feistel list) on the bench's faithful workload
+"""Faithful-mode pass time of the four sources (key-ordered list, generated
+lists, radix sort of a Feistel list, r10's uniform draw generated in key order) on the bench's faithful workload
 (N=1024, T=8, 2^24 samples) or other shapes.
 usage: python tools/fa_time.py [N T log2(samples)]..."""
 import json
@@ -43,7 +43,8 @@ for N, T, lg in shapes:
             off += c
         runs = {"sorted": lambda: ctx.faithful_hist_sorted_refs(buf.data_ptr(), counts, sp),
                 "generated": lambda: ctx.gen_faithful_refs(SEED, counts, sp),
-                "radix": lambda: ctx.faithful_hist_refs(fe.data_ptr(), counts, sp)}
+                "radix": lambda: ctx.faithful_hist_refs(fe.data_ptr(), counts, sp),
+                "uniform": lambda: ctx.gen_uniform_faithful_refs(SEED, counts, sp)}
         res = {"N": N, "T": T, "samples": total}
         hs = {}
         for name, run in runs.items():
