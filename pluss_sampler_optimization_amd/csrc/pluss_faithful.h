@@ -324,8 +324,9 @@ struct FaLds {
   unsigned long long rt[4];     // ri*T per case (KEY_EMPTY: cold; case 3: malformed)
   unsigned long long klast[NT / 64];
   unsigned long long kb[2];     // the tile's first and last keys (FA_LOCAL)
+  fa_raw_t<SRC> prevw;          // the element before the tile (the fast path's order check)
   fa_raw_t<SRC> raw[SRC == SRC_GEN ? 1 : TILE + TILE / EPT];
-  uint32_t cand[SRC == SRC_UNI ? UG_CAP : 1];  // the uniform generator's candidate offsets
+  uint32_t cand[SRC == SRC_UNI ? UG_CAND : 1];  // the uniform generator's scratch (uni_stage)
 };
 // LDS slot of tile element e for runs of EPT elements per thread (one pad per run)
 template <int EPT>
@@ -900,10 +901,9 @@ __device__ __forceinline__ void fa_local_fast(const Model& m, const FaOne& o, Fa
   __syncthreads();
   if (CHECK) {
     if (lane == 0 && wid > 0 && nv) unordered |= !(ofirst > sh.klast[wid - 1]);
-    if (threadIdx.x == 0 && T.base > 0) {
+    if (threadIdx.x == 0 && T.base > 0) {  // (staged with the tile)
       uint32_t o2 = 0;
-      const fa_raw_t<SRC> w = static_cast<const fa_raw_t<SRC>*>(o.src)[T.base - 1];
-      unordered |= !(ofirst > fa_dec_sample<REF>(m, o.pv, (uint64_t)w, o2).ord);
+      unordered |= !(ofirst > fa_dec_sample<REF>(m, o.pv, (uint64_t)sh.prevw, o2).ord);
     }
     if (__ballot(odd != 0 || unordered) && lane == 0) atomicOr(&g.flags[1], 1u);
   }
@@ -999,22 +999,51 @@ __device__ __forceinline__ void fa_local_fast(const Model& m, const FaOne& o, Fa
 
 template <int SRC>
 __device__ __forceinline__ const void* fa_src_of(const FaRefs& a, uint32_t r) {
-  switch (r) {
-    case 0: return a.src[0];
-    case 1: return a.src[1];
-    case 2: return a.src[2];
-    case 3: return a.src[3];
-    case 4: return a.src[4];
-    default: return a.src[5];
-  }
+  // selects, not a switch (which can become an indexed load of the kernel
+  // argument, and an indexed argument is copied to scratch)
+  const void* p = a.src[0];
+#pragma unroll
+  for (uint32_t x = 1; x < 6; ++x) p = r == x ? a.src[x] : p;
+  return p;
 }
 
 template <int SRC, uint32_t R>
 __device__ __forceinline__ FaOne fa_one_ref(const FaRefs& a, const FaTile& T);
 
-// One tile by the fast path: its elements staged to LDS (memory sources),
-// the first and last keys in 64 bits, then the scan if the tile qualifies.
-// Returns whether the fast path took the tile (tile-uniform).
+// A memory source's tile (k_fa_local_fast): thread x's TI coalesced elements
+// (round k: element k*TB + x; a partial tile's lanes past its end re-read its
+// last element) and the element before the tile (the order check), loaded
+// into registers, then written to LDS.
+template <int SRC>
+struct FaPre {
+  fa_raw_t<SRC> v[TI];
+  fa_raw_t<SRC> prev;
+};
+template <int SRC>
+__device__ __forceinline__ const void* fa_src_of(const FaRefs& a, uint32_t r);
+template <int SRC>
+__device__ __forceinline__ void fa_prefetch(const FaRefs& a, const FaTile& T, FaPre<SRC>& p) {
+  // every load issued before the first is waited for, none behind a branch
+  const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(fa_src_of<SRC>(a, T.r)) + T.base;
+  const uint32_t last = T.mt - 1;
+#pragma unroll
+  for (int k = 0; k < TI; ++k) {
+    const uint32_t e = (uint32_t)k * TB + threadIdx.x;
+    p.v[k] = __builtin_nontemporal_load(src + (e < last ? e : last));
+  }
+  p.prev = src[T.base > 0 ? -1 : 0];  // (one wave-uniform address)
+}
+template <int SRC>
+__device__ __forceinline__ void fa_stage(const FaPre<SRC>& p, FaLds<SRC, TB, TI>& sh) {
+#pragma unroll
+  for (int k = 0; k < TI; ++k) sh.raw[fa_slot_n<TI>((uint32_t)k * TB + threadIdx.x)] = p.v[k];
+  if (threadIdx.x == 0) sh.prevw = p.prev;
+}
+
+// One tile by the fast path: the first and last keys in 64 bits (memory
+// sources: the tile already staged in LDS; generated sources: generated
+// here), then the scan if the tile qualifies.  Returns whether the fast path
+// took the tile (tile-uniform).
 template <int SRC, bool CHECK, uint32_t REF>
 __device__ __forceinline__ bool fa_fast_tile(const Model& m, const FaRefs& a, const FaTile& T,
                                              FaLds<SRC, TB, TI>& sh, unsigned long long* __restrict__ klist,
@@ -1024,31 +1053,15 @@ __device__ __forceinline__ bool fa_fast_tile(const Model& m, const FaRefs& a, co
   if constexpr (SRC == SRC_GEN) kg = a.kg[REF];
   fa_rt(m, o.pv, sh);
   const bool full = T.mt == TILE;
-  if constexpr (SRC == SRC_UNI) {
+  if constexpr (SRC == SRC_UNI)
     uni_stage<TB>(o.us, T.r, T.lt, T.mt, sh.raw, sh.cand, o.us->flags, [](uint32_t e) { return fa_slot_n<TI>(e); });
-  } else if constexpr (SRC != SRC_GEN) {
-    // all TI loads issued before the first is waited for: no branch around
-    // them (a partial tile's lanes past its end re-read its last element)
-    const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(o.src) + T.base;
-    fa_raw_t<SRC> v[TI];
-    const uint32_t last = T.mt - 1;
-#pragma unroll
-    for (int k = 0; k < TI; ++k) {
-      const uint32_t e = (uint32_t)k * TB + threadIdx.x;
-      v[k] = __builtin_nontemporal_load(src + (e < last ? e : last));
-    }
-#pragma unroll
-    for (int k = 0; k < TI; ++k) sh.raw[fa_slot_n<TI>((uint32_t)k * TB + threadIdx.x)] = v[k];
-  }
   if (threadIdx.x < 2) {  // the first and the last key, in 64 bits
     const uint32_t e = threadIdx.x ? T.mt - 1 : 0;
     bool b2 = false;
     if constexpr (SRC == SRC_GEN)
       sh.kb[threadIdx.x] = elem_of_digits<true>(m, o.pv, REF, keygen_digits_at(kg, T.gbase + e)).key;
-    else if constexpr (SRC == SRC_UNI)
-      sh.kb[threadIdx.x] = fa_decode_ref<SRC, true, REF>(m, o.pv, sh.raw[fa_slot_n<TI>(e)], b2).key;
     else
-      sh.kb[threadIdx.x] = fa_decode_ref<SRC, true, REF>(m, o.pv, src_at<SRC>(o, e), b2).key;
+      sh.kb[threadIdx.x] = fa_decode_ref<SRC, true, REF>(m, o.pv, sh.raw[fa_slot_n<TI>(e)], b2).key;
   }
   __syncthreads();
   const unsigned long long base = sh.kb[0], kl = sh.kb[1];
@@ -1084,6 +1097,203 @@ __device__ __forceinline__ bool fa_fast_tile(const Model& m, const FaRefs& a, co
     if (full) fa_local_fast<SRC, CHECK, REF, true>(m, o, sh, base, r, el, kl_out, g);
     else fa_local_fast<SRC, CHECK, REF, false>(m, o, sh, base, r, el, kl_out, g);
   }
+  return true;
+}
+
+// ---- the fast path of memory sources, lane-major (k_fa_local_lm): wave w
+// scans elements [1024w, 1024w + 1024) of the tile in 16 steps, lane L of
+// step k holding element 1024w + 64k + L, loaded straight into registers
+// (coalesced, all 16 loads issued before the first is used) -- no LDS staging
+// of the tile, so occupancy is set by registers alone.  Per step: the decode,
+// the sink, and a DPP max-scan of the sinks over the lanes (the running max
+// before each lane within the step); the waves' largest sinks are exchanged
+// once, and a second sweep over the kept offsets finds the starts.  The
+// tile's first and last keys are decoded by every wave (two uniform loads):
+// no barrier before the scan.  Results as fa_local_fast's.
+struct FaLm {
+  unsigned long long out[FPW + 1];
+  unsigned long long ordl[TB / 64];       // each wave's last element's order word (CHECK)
+  unsigned long long red[TB / 64][6];     // per wave: starts, case 0, case 1, case 2 of tid 0, sum(key - run), last start + 1
+  uint32_t wmax[TB / 64];                 // each wave's largest sink (offset)
+  uint32_t kl[TB / 64][KL][2];            // each wave's first KL starts: key offset, running max before it
+};
+
+template <int SRC, bool CHECK, uint32_t REF, bool FULLT>
+__device__ __forceinline__ bool fa_lane_tile(const Model& m, const FaRefs& a, const FaTile& T, FaLm& sh,
+                                             unsigned long long* __restrict__ klist, GTable g) {
+  constexpr int NW = TB / 64, ST = TI;  // waves, steps per wave
+  const FaOne o = fa_one_ref<SRC, REF>(a, T);
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(o.src) + T.base;
+  const uint32_t last = T.mt - 1, e0 = wid * (64 * ST) + lane;
+  fa_raw_t<SRC> v[ST];
+#pragma unroll
+  for (int k = 0; k < ST; ++k) {
+    const uint32_t e = e0 + 64u * k;
+    v[k] = __builtin_nontemporal_load(src + (e < last ? e : last));
+  }
+  // ri*T per case (0xFFFFFFFF: cold) and the tile's first and last keys, in every wave
+  auto rt = [&](int c) -> unsigned long long {
+    const int64_t ri = c == 0 ? o.pv.ri[0] : (c == 1 ? o.pv.ri[1] : o.pv.ri[2]);
+    return ri < 0 ? KEY_EMPTY : (unsigned long long)ri * m.T;
+  };
+  const unsigned long long t0 = rt(0), t1 = rt(1), t2 = rt(2);
+  unsigned long long rmax = 0;
+  rmax = t0 != KEY_EMPTY && t0 > rmax ? t0 : rmax;
+  rmax = t1 != KEY_EMPTY && t1 > rmax ? t1 : rmax;
+  rmax = t2 != KEY_EMPTY && t2 > rmax ? t2 : rmax;
+  bool b2 = false;
+  const unsigned long long base = fa_decode_ref<SRC, true, REF>(m, o.pv, src[0], b2).key;
+  const unsigned long long kl = fa_decode_ref<SRC, true, REF>(m, o.pv, src[last], b2).key;
+  auto r32 = [](unsigned long long x) { return x == KEY_EMPTY ? 0xFFFFFFFFu : (uint32_t)x; };
+  const FaRi r{r32(t0), r32(t1), r32(t2)};
+  if (!(kl >= base && kl - base < 0xFFFFFFFFull - rmax && r.r0 != 0xFFFFFFFFu && r.r1 != 0xFFFFFFFFu))
+    return false;  // (the same decision in every wave)
+  const uint32_t b32 = (uint32_t)base;
+  // sweep 1: offsets, sinks, the running max of sinks before each lane within the wave
+  uint32_t rk[ST], ex[ST], wm = 0, odd = 0;
+  uint32_t w01 = 0, wc = 0, unord = 0;  // w01: case 0 | case 1 << 16; wc: case 2 of tid 0
+  unsigned long long oprev = 0, ofirst = 0;
+#pragma unroll
+  for (int k = 0; k < ST; ++k) {
+    const bool val = FULLT || e0 + 64u * k <= last;
+    uint32_t oddk = 0;
+    FaDec d;
+    if constexpr (fa_smp<SRC>()) d = fa_dec_sample<REF>(m, o.pv, (uint64_t)v[k], oddk);
+    else d = fa_dec_word<REF>(m, o.pv, v[k]);
+    odd |= val ? oddk : 0u;
+    if (CHECK) {  // against the previous lane (the step before: its lane 63); integer
+                  // arithmetic, not compare masks (which the unrolled steps kept in SGPRs)
+      const uint32_t plo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)d.ord, 0x138, 0xf, 0xf, false);
+      const uint32_t phi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(d.ord >> 32), 0x138, 0xf, 0xf, false);
+      unsigned long long up = ((unsigned long long)phi << 32) | plo;
+      if (lane == 0) up = k > 0 ? oprev : d.ord - 1;  // (the wave's first element: checked after the barrier)
+      if (k == 0) ofirst = d.ord;
+      const uint32_t bad = (uint32_t)((d.ord - up - 1) >> 63);  // ord <= up (orders stay below 2^56)
+      unord |= val ? bad : 0u;
+      oprev = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(d.ord >> 32), 63) << 32) |
+              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)d.ord, 63);
+    }
+    rk[k] = val ? d.lk - b32 : 0u;
+    const uint32_t dd = d.a ? r.r0 : (d.b ? r.r1 : r.r2);
+    const uint32_t x = rk[k] + dd;  // cold: dd = 0xFFFFFFFF, the max keeps it
+    const uint32_t s = val ? (x > dd ? x : dd) : 0u;
+    const uint32_t inc = wave_scan_dpp<true>(s), xk = wave_shr1(inc);
+    ex[k] = xk > wm ? xk : wm;  // (the steps before: wm)
+    const uint32_t sm = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    wm = sm > wm ? sm : wm;
+    // per-lane counts (not ballots: every step's compare masks held in SGPRs spilled them)
+    w01 += val ? (d.a ? 1u : (d.b ? 0x10000u : 0u)) : 0u;
+    wc += (val && !d.a && !d.b && d.t0) ? 1u : 0u;
+    // the checks are reduced step by step: left to their use after the
+    // barrier, the compiler kept every step's raw element and order word live
+    __asm__ volatile("" : "+v"(odd), "+v"(unord), "+v"(w01), "+v"(wc));
+    __builtin_amdgcn_sched_barrier(0);  // one step at a time: hoisted decodes held every step's case masks in SGPRs
+  }
+  if (lane == 0) {
+    sh.wmax[wid] = wm;
+    sh.ordl[wid] = oprev;
+  }
+  __syncthreads();
+  uint32_t pm = 0, tm = 0;  // the running max entering this wave; the tile's largest sink
+#pragma unroll
+  for (int x = 0; x < NW; ++x) {
+    const uint32_t w = sh.wmax[x];
+    if (x < (int)wid) pm = w > pm ? w : pm;
+    tm = w > tm ? w : tm;
+  }
+  if (CHECK) {  // the wave's first element against the element before it (the previous wave's last, or the tile's)
+    bool unordered = unord != 0;
+    if (lane == 0 && e0 <= last) {
+      if (wid > 0) {
+        unordered |= !(ofirst > sh.ordl[wid - 1]);
+      } else if (T.base > 0) {
+        uint32_t o2 = 0;
+        unordered |= !(ofirst > fa_dec_sample<REF>(m, o.pv, (uint64_t)src[-1], o2).ord);
+      }
+    }
+    if (__ballot(odd != 0 || unordered) && lane == 0) atomicOr(&g.flags[1], 1u);
+  }
+  // sweep 2: the starts (the tile's first element is one), their sum(key - run), the wave's first KL
+  uint32_t dsum = 0, cnt = 0, kc = 0;
+  unsigned long long jl = 0;
+#pragma unroll
+  for (int k = 0; k < ST; ++k) {
+    const uint32_t rn = ex[k] > pm ? ex[k] : pm;  // (pm: the earlier waves)
+    const bool st = rk[k] > rn || (k == 0 && e0 == 0);
+    dsum += __builtin_elementwise_sub_sat(rk[k], rn);
+    const unsigned long long bal = __ballot(st);
+    if (bal) {
+      const uint32_t nb = (uint32_t)__popcll(bal);
+      jl = T.gbase + (uint64_t)(wid * (64 * ST) + 64 * k + (63 - __builtin_clzll(bal))) + 1;
+      if (kc < (uint32_t)KL) {
+        const uint32_t rank = kc + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        if (st && rank < (uint32_t)KL) {
+          sh.kl[wid][rank][0] = rk[k];
+          sh.kl[wid][rank][1] = rn;
+        }
+        kc += nb;
+      }
+      cnt += nb;
+    }
+  }
+  const uint32_t sd = wave_sum_dpp(dsum), s01 = wave_sum_dpp(w01), sc = wave_sum_dpp(wc);
+  if (lane == 0) {
+    sh.red[wid][0] = cnt;
+    sh.red[wid][1] = s01 & 0xFFFFu;
+    sh.red[wid][2] = s01 >> 16;
+    sh.red[wid][3] = sc;
+    sh.red[wid][4] = sd;
+    sh.red[wid][5] = jl;
+  }
+  __syncthreads();
+  uint64_t cagg = 0;
+#pragma unroll
+  for (int x = 0; x < NW; ++x) cagg += sh.red[x][0];
+  if (threadIdx.x < (uint32_t)KL) {  // the tile's first KL starts: the waves' lists in order
+    const uint32_t i = threadIdx.x;
+    uint64_t s0 = 0;
+#pragma unroll
+    for (int x = 0; x < NW; ++x) {
+      const uint64_t c = sh.red[x][0];
+      if (i >= s0 && i < s0 + c) {
+        klist[2 * i] = base + sh.kl[x][i - s0][0];
+        klist[2 * i + 1] = i == 0 ? 0ull : base + sh.kl[x][i - s0][1];
+      }
+      s0 += c;
+    }
+  }
+  if (threadIdx.x < FPW + 1) {
+    const uint32_t f = threadIdx.x;
+    unsigned long long x = 0;
+    if (f == FPART) {
+      x = cagg;
+    } else if (f == FPART + 1) {  // hmax = 2j - (starts before j) at the last start j > 0
+      unsigned long long j = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) j = sh.red[w][5] > j ? sh.red[w][5] : j;
+      x = j > 1 ? 2 * (j - 1) - (cagg - 1) : 0ull;
+    } else if (f == FPW) {
+      x = tm == 0xFFFFFFFFu ? KEY_EMPTY : base + tm;
+    } else if (f == 1) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) x += sh.red[w][4];
+      x = 0ull - base - x;
+    } else {
+      unsigned long long a0 = 0, a1 = 0, ac = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        a0 += sh.red[w][1];
+        a1 += sh.red[w][2];
+        ac += sh.red[w][3];
+      }
+      const bool cold2 = r.r2 == 0xFFFFFFFFu;
+      x = f == 0 ? (cold2 ? ac : 0ull) : f == 2 ? a0 : f == 3 ? a1 : (cold2 ? 0ull : T.mt - a0 - a1);
+    }
+    sh.out[f] = x;
+  }
+  __syncthreads();
   return true;
 }
 
@@ -1176,8 +1386,14 @@ __global__ __launch_bounds__(TB) void k_fa_local(Model m, FaRefs a, unsigned lon
   }
 }
 
-// The fast path over every tile (shapes with FaRefs::fast); the tiles it
-// cannot take are queued in slowq for k_fa_local.
+// The fast path over every tile (shapes with FaRefs::fast), one tile per
+// workgroup; the tiles it cannot take are queued in slowq for k_fa_local.
+// (A resident grid that loads the next tile into registers while scanning the
+// current one ran at 2 waves per SIMD and was 1.4x slower at config 3: the
+// scan's dependent chains need the 4 waves per SIMD of this form to issue.)
+template <int SRC>
+constexpr bool fa_mem() { return SRC == SRC_W32 || SRC == SRC_W64 || SRC == SRC_SAMPLES; }
+
 template <int SRC, bool CHECK>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4))) void k_fa_local_fast(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
                                                       unsigned long long* __restrict__ part,
@@ -1186,10 +1402,44 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4))) void k_
   __shared__ FaLds<SRC, TB, TI> sh;
   const FaTile T = fa_tile(a, blockIdx.x);
   fa_cold_slot(T, g, slots);
+  if constexpr (fa_mem<SRC>()) {
+    FaPre<SRC> p;
+    fa_prefetch<SRC>(a, T, p);
+    fa_stage<SRC>(p, sh);
+    __syncthreads();
+  }
   bool done = false;
 #define PLUSS_FA_FAST(R) done = fa_fast_tile<SRC, CHECK, R>(m, a, T, sh, klist, g);
   PLUSS_FA_REFS(PLUSS_FA_FAST)
 #undef PLUSS_FA_FAST
+  if (done) {
+    if (threadIdx.x < FPW) part[blockIdx.x * (uint64_t)FPW + threadIdx.x] = sh.out[threadIdx.x];
+    if (threadIdx.x == FPW) tmax[blockIdx.x] = sh.out[FPW];
+  } else if (threadIdx.x == 0) {
+    slowq[1 + atomicAdd(&slowq[0], 1u)] = (unsigned int)blockIdx.x;
+  }
+}
+
+// The lane-major fast path over every tile of a memory source (fa_lane_tile);
+// the tiles it cannot take are queued in slowq for k_fa_local.
+template <int SRC, bool CHECK>
+__global__ __launch_bounds__(TB) void k_fa_local_lm(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
+                                                    unsigned long long* __restrict__ part,
+                                                    unsigned long long* __restrict__ klist, unsigned long long* slots,
+                                                    unsigned int* slowq, GTable g) {
+  static_assert(fa_mem<SRC>(), "generated sources: k_fa_local_fast");
+  __shared__ FaLm sh;
+  const FaTile T = fa_tile(a, blockIdx.x);
+  fa_cold_slot(T, g, slots);
+  unsigned long long* kl_out = klist + T.gt * (uint64_t)(2 * KL);
+  bool done = false;
+  // full tiles only: the few partial ones (a reference's last tile) go to the slow pass,
+  // which keeps the kernel's registers at the full tile's (8 waves per SIMD)
+#define PLUSS_FA_LM(R) done = fa_lane_tile<SRC, CHECK, R, true>(m, a, T, sh, kl_out, g);
+  if (T.mt == TILE) {
+    PLUSS_FA_REFS(PLUSS_FA_LM)
+  }
+#undef PLUSS_FA_LM
   if (done) {
     if (threadIdx.x < FPW) part[blockIdx.x * (uint64_t)FPW + threadIdx.x] = sh.out[threadIdx.x];
     if (threadIdx.x == FPW) tmax[blockIdx.x] = sh.out[FPW];
@@ -1698,8 +1948,12 @@ inline void fa_launch_t(const FaLaunch& L) {
       if (L.a.fast) {
         // the queue starts empty whatever an earlier, abandoned pass left in it
         (void)hipMemsetAsync(b.slowq, 0, sizeof(unsigned int), L.s);
-        hipLaunchKernelGGL((k_fa_local_fast<SRC, CHK>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
-                           b.fslot, b.slowq, L.g);
+        if constexpr (fa_mem<SRC>())
+          hipLaunchKernelGGL((k_fa_local_lm<SRC, CHK>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
+                             b.fslot, b.slowq, L.g);
+        else
+          hipLaunchKernelGGL((k_fa_local_fast<SRC, CHK>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart,
+                             b.klist, b.fslot, b.slowq, L.g);
         hipLaunchKernelGGL((k_fa_local<SRC, P2, CHK, true>), dim3(nres), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart,
                            b.klist, b.fslot, b.slowq, L.g);
         fast = true;

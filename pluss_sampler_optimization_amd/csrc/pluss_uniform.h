@@ -84,6 +84,10 @@ inline UniGen make_unigen(uint64_t N, uint64_t T, uint64_t CS, bool range_full, 
   u.r = u.p < 1.0 ? u.p / (1.0 - u.p) : 0.0;
   const double kk = (double)UG_MEAN / ((double)T * u.p);
   u.K = kk < 1.0 ? 1 : (kk >= (double)u.W ? u.W : (uint64_t)kk);
+  // balanced leaves: a row cut into nb = floor(W / K) blocks of ceil(W / nb)
+  // w-values (not K, K, ..., and a sliver of a few points)
+  const uint64_t nb0 = u.W / u.K ? u.W / u.K : 1;
+  u.K = (u.W + nb0 - 1) / nb0;
   if (u.K > 0xFFFFFFFFull / T) u.K = 0xFFFFFFFFull / T;  // a leaf's points fit 32 bits
   u.nb = (u.W + u.K - 1) / u.K;
   u.LA = u.RA * u.nb;
@@ -263,38 +267,161 @@ __device__ __forceinline__ uint64_t uni_removed_before(const UniSet* __restrict_
 }
 
 // Generate samples [lt*UG_TILE, lt*UG_TILE + mt) of reference r's list into
-// raw[slot(e)] (e = sample - lt*UG_TILE), all NT threads of the workgroup; cand:
-// LDS scratch of UG_CAP words.  The leaves from the one holding the tile's
-// first sample to the one holding the next tile's first are regenerated:
-// each thread draws one leaf's candidates (sorted offsets) into cand at the
-// leaf's candidate rank, then every surviving candidate of the tile is packed
-// at its sample index.  A window past UG_CAP candidates or a leaf past
+// raw[slot(e)] (e = sample - lt*UG_TILE), all NT threads of the workgroup;
+// cand: LDS scratch of UG_CAND words.  The leaves from the one holding the
+// tile's first sample to the one holding the next tile's first are
+// regenerated: the removal bitmap's words over their candidate ranks and the
+// words' removed-before counts are staged in LDS first (a few hundred words,
+// coalesced), then each thread draws one leaf's candidates (sorted offsets,
+// in cand at the leaf's candidate rank) and packs every surviving one at its
+// sample index -- per candidate only LDS reads and integer work, the leaf's
+// row decoded once.  A window past UG_CAP candidates or a leaf past
 // UG_LEAFMAX (neither happens with probability above 1e-20) sets FLAG_UNI.
+constexpr uint32_t UG_WCAP = UG_CAP / 32 + 2;      // bitmap words over a window of UG_CAP ranks
+constexpr uint32_t UG_CAND = UG_CAP + 2 * UG_WCAP;  // cand: offsets, then the window's words and counts
+
+// a leaf's row decoded once: the digits of its offset o are then shifts (block A, T a power of two)
+struct UniRowD {
+  uint32_t q, c1, w0;
+};
+__device__ __forceinline__ UniRowD uni_row(const UniGen& u, const UniLeaf& f) {
+  UniRowD d;
+  d.w0 = (uint32_t)(f.wb * u.K);
+  if (f.blk) {
+    d.q = u.Q - 1;
+    d.c1 = u.dim3 ? (uint32_t)f.row : 0u;
+  } else if (u.dim3) {
+    const uint64_t q = div64(f.row, u.dspan);
+    d.q = (uint32_t)q;
+    d.c1 = (uint32_t)(f.row - q * u.span);
+  } else {
+    d.q = (uint32_t)f.row;
+    d.c1 = 0;
+  }
+  return d;
+}
+// = uni_pack(u, uni_digits(u, f, o))
+__device__ __forceinline__ uint64_t uni_pack_row(const UniGen& u, const UniLeaf& f, const UniRowD& rd, uint32_t o) {
+  uint32_t wq, t;
+  if (!f.blk && u.tp2) {
+    wq = o >> u.tsh;
+    t = o & (u.T - 1);
+  } else {
+    wq = (uint32_t)div64(o, f.blk ? u.dtB : u.dtA);
+    t = o - wq * (uint32_t)f.tb;
+  }
+  KeyDigits d;
+  const uint32_t w = rd.w0 + wq;
+  d.t = t;
+  d.q = rd.q;
+  d.c1 = u.dim3 ? rd.c1 : w;
+  d.c2 = u.dim3 ? w : 0u;
+  return uni_pack(u, d);
+}
+
+// uni_offset for G < 2^32, in 32-bit pieces: floor(h * G / 2^64)
+__device__ __forceinline__ uint32_t uni_offset32(uint64_t lk, uint32_t i, uint32_t G) {
+  const uint64_t h = uni_hash(lk, i);
+  const uint64_t t = (uint64_t)(uint32_t)(h >> 32) * G + __umulhi((uint32_t)h, G);
+  return (uint32_t)(t >> 32);
+}
+// ascending bitonic sort of NC (a power of two) values in registers
+template <int NC>
+__device__ __forceinline__ void uni_sort_net(uint32_t (&v)[NC]) {
+#pragma unroll
+  for (int k = 2; k <= NC; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+      for (int i = 0; i < NC; ++i) {
+        const int l = i ^ j;
+        if (l > i) {
+          const uint32_t a = v[i], b = v[l], lo = a < b ? a : b, hi = a < b ? b : a;
+          const bool up = (i & k) == 0;
+          v[i] = up ? lo : hi;
+          v[l] = up ? hi : lo;
+        }
+      }
+}
+constexpr uint32_t UG_NET = 32;  // leaves of at most this many candidates: sorted in registers
+
 template <int NT, class SLOT>
 __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_t r, uint64_t lt, uint32_t mt,
                                           unsigned long long* raw, uint32_t* cand, unsigned int* flags,
                                           SLOT&& slot) {
-  const UniGen& u = us->u[r];
+  // the generator and the plan's arrays copied out once: read through the
+  // plan pointer after every LDS store (generic stores may alias it), they
+  // were reloaded from memory per candidate
+  const UniGen u = us->u[r];
+  const uint32_t* __restrict__ cnt = us->cnt;
+  const uint64_t* __restrict__ pre = us->pre;
   const uint64_t tm0 = us->tmoff[r], nt = us->tmoff[r + 1] - tm0, lg0 = us->loff[r];
   const uint64_t la = us->tmap[tm0 + lt], lb = lt + 1 < nt ? us->tmap[tm0 + lt + 1] : u.L - 1;
-  const uint64_t pbase = us->pre[lg0];
+  const uint64_t pbase = pre[lg0];
   const bool leaves_ok = la <= lb && lb < u.L;
-  const uint64_t r0 = leaves_ok ? us->pre[lg0 + la] - pbase : 0, rend = leaves_ok ? us->pre[lg0 + lb + 1] - pbase : 0;
+  const uint64_t r0 = leaves_ok ? pre[lg0 + la] - pbase : 0, rend = leaves_ok ? pre[lg0 + lb + 1] - pbase : 0;
   if (!leaves_ok || rend - r0 > UG_CAP) {
     if (threadIdx.x == 0) atomicOr(flags, FLAG_UNI);
     __syncthreads();
     return;
   }
+  // the window's bitmap words [wlo, wlo + nw) (reference-relative) and their removed-before counts
+  const uint64_t wo = us->woff[r], wend = us->woff[r + 1] - wo;  // (a flagged plan's indices are clamped)
+  const uint64_t wlo = r0 >> 5;
+  const uint32_t nw = rend > r0 ? (uint32_t)(((rend - 1) >> 5) - wlo + 1) : 0u;
+  uint32_t* bw = cand + UG_CAP;
+  uint32_t* rbw = bw + UG_WCAP;
+  const uint64_t wl = wlo < wend ? wlo : wend - 1;
+  const uint64_t rem0 = us->rb[wo + wl] - us->rb[wo];
+  for (uint32_t i = threadIdx.x; i < nw; i += NT) {
+    const uint64_t w = wlo + i < wend ? wlo + i : wend - 1;
+    bw[i] = us->bits[wo + w];
+    rbw[i] = (uint32_t)(us->rb[wo + w] - us->rb[wo] - rem0);
+  }
+  __syncthreads();
   const uint64_t f0 = lt * UG_TILE;
   for (uint64_t l = la + threadIdx.x; l <= lb; l += NT) {
-    const uint32_t c = us->cnt[lg0 + l];
+    const uint32_t c = cnt[lg0 + l];
     if (!c) continue;
     if (c > UG_LEAFMAX) {
       atomicOr(flags, FLAG_UNI);
       continue;
     }
-    uint32_t* seg = cand + (us->pre[lg0 + l] - pbase - r0);
+    const uint64_t x0 = pre[lg0 + l] - pbase;
+    uint32_t* seg = cand + (x0 - r0);
     const UniLeaf f = uni_leaf(u, l);
+    auto emit = [&](uint32_t i, uint32_t o, const UniRowD& rd) {
+      const uint64_t x = x0 + i;
+      const uint32_t wi = (uint32_t)((x >> 5) - wlo), word = bw[wi];
+      if ((word >> (x & 31)) & 1u) return;  // removed
+      const uint64_t e = x - (rem0 + rbw[wi] + (uint64_t)__popc(word & ((1u << (x & 31)) - 1u))) - f0;
+      if (e < mt) raw[slot((uint32_t)e)] = uni_pack_row(u, f, rd, o);
+    };
+    if (u.p < 1.0 && c <= UG_NET && !uni_direct(u, f)) {
+      // the common leaf: its offsets drawn and sorted in registers (an insertion
+      // sort through LDS was a chain of dependent LDS round trips, divergent per lane)
+      const uint32_t G = (uint32_t)f.G;  // (K*T < 2^32)
+      uint32_t v[UG_NET];
+      for (uint32_t a = 0;; ++a) {
+        if (a == UG_TRIES) {
+          atomicOr(flags, FLAG_UNI);
+          break;
+        }
+        const uint64_t lk = uni_leafkey(u, l, a);
+#pragma unroll
+        for (uint32_t q = 0; q < UG_NET; ++q) v[q] = q < c ? uni_offset32(lk, q, G) : 0xFFFFFFFFu;
+        uni_sort_net<UG_NET>(v);
+        bool dup = false;  // (offsets < G <= 2^32 - 1: the padding sorts last and never matches)
+#pragma unroll
+        for (uint32_t q = 0; q + 1 < UG_NET; ++q) dup |= v[q] == v[q + 1] && q + 1 < c;
+        if (!dup) break;
+      }
+      const UniRowD rd = uni_row(u, f);
+#pragma unroll
+      for (uint32_t q = 0; q < UG_NET; ++q)
+        if (q < c) emit(q, v[q], rd);
+      continue;
+    }
     if (u.p >= 1.0) {
       for (uint32_t j = 0; j < c; ++j) seg[j] = j;
     } else if (uni_direct(u, f)) {
@@ -309,34 +436,22 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
           break;
         }
         const uint64_t lk = uni_leafkey(u, l, a);
+        bool dup = false;
         for (uint32_t i = 0; i < c; ++i) {
           const uint32_t x = (uint32_t)uni_offset(lk, i, f.G);
-          uint32_t j = i;
-          while (j > 0 && seg[j - 1] > x) {
-            seg[j] = seg[j - 1];
+          uint32_t j = i, y = 0;
+          while (j > 0 && (y = seg[j - 1]) > x) {
+            seg[j] = y;
             --j;
           }
+          dup |= j > 0 && y == x;
           seg[j] = x;
         }
-        bool dup = false;
-        for (uint32_t i = 1; i < c; ++i) dup |= seg[i] == seg[i - 1];
         if (!dup) break;
       }
     }
-  }
-  __syncthreads();
-  for (uint64_t l = la + threadIdx.x; l <= lb; l += NT) {
-    const uint32_t c = us->cnt[lg0 + l];
-    if (!c || c > UG_LEAFMAX) continue;
-    const uint64_t x0 = us->pre[lg0 + l] - pbase;
-    const uint32_t* seg = cand + (x0 - r0);
-    const UniLeaf f = uni_leaf(u, l);
-    for (uint32_t i = 0; i < c; ++i) {
-      const uint64_t x = x0 + i;
-      if ((us->bits[uni_word(us, r, x)] >> (x & 31)) & 1u) continue;  // removed
-      const uint64_t e = x - uni_removed_before(us, r, x) - f0;
-      if (e < mt) raw[slot((uint32_t)e)] = uni_pack(u, uni_digits(u, f, seg[i]));
-    }
+    const UniRowD rd = uni_row(u, f);
+    for (uint32_t i = 0; i < c; ++i) emit(i, seg[i], rd);
   }
   __syncthreads();
 }

@@ -113,14 +113,19 @@ __device__ __forceinline__ uint32_t ug_ref_of(const uint64_t* off, uint64_t g) {
   return r;
 }
 
+// (references outermost: the generator's fields are wave-uniform, scalar loads)
 __global__ __launch_bounds__(UB) void k_ug_count(const UniSet* __restrict__ us, uint32_t* __restrict__ cnt,
                                                 unsigned int* flags) {
-  const uint64_t n = us->loff[6];
-  for (uint64_t g = (uint64_t)blockIdx.x * UB + threadIdx.x; g < n; g += (uint64_t)gridDim.x * UB) {
-    const uint32_t r = ug_ref_of(us->loff, g);
-    const uint64_t c = uni_count(us->u[r], g - us->loff[r]);
-    if (c > UG_LEAFMAX) atomicOr(flags, FLAG_UNI);
-    cnt[g] = c > UG_LEAFMAX ? UG_LEAFMAX + 1 : (uint32_t)c;
+  const uint64_t stride = (uint64_t)gridDim.x * UB;
+  for (uint32_t r = 0; r < 6; ++r) {
+    const uint64_t g0 = us->loff[r], n = us->loff[r + 1] - g0;
+    if (!n) continue;
+    const UniGen u = us->u[r];
+    for (uint64_t l = (uint64_t)blockIdx.x * UB + threadIdx.x; l < n; l += stride) {
+      const uint64_t c = uni_count(u, l);
+      if (c > UG_LEAFMAX) atomicOr(flags, FLAG_UNI);
+      cnt[g0 + l] = c > UG_LEAFMAX ? UG_LEAFMAX + 1 : (uint32_t)c;
+    }
   }
 }
 
@@ -148,18 +153,18 @@ __global__ __launch_bounds__(UB) void k_ug_remove(const UniSet* __restrict__ us,
 // per leaf: the sample index of its first surviving candidate and their
 // number; the leaf holding each tile's first sample
 __global__ __launch_bounds__(UB) void k_ug_tiles(const UniSet* __restrict__ us, uint32_t* __restrict__ tmap) {
-  const uint64_t n = us->loff[6];
-  for (uint64_t g = (uint64_t)blockIdx.x * UB + threadIdx.x; g < n; g += (uint64_t)gridDim.x * UB) {
-    const uint32_t c = us->cnt[g];
-    if (!c || c > UG_LEAFMAX) continue;
-    const uint32_t r = ug_ref_of(us->loff, g);
-    const uint64_t l = g - us->loff[r];
-    const uint64_t x0 = uni_pre(us, r, l);
-    const uint64_t b0 = uni_removed_before(us, r, x0), b1 = uni_removed_before(us, r, x0 + c);
-    const uint64_t f = x0 - b0, kept = c - (b1 - b0);
-    const uint64_t nt = us->tmoff[r + 1] - us->tmoff[r];
-    for (uint64_t t = (f + UG_TILE - 1) / UG_TILE; t * UG_TILE < f + kept && t < nt; ++t)
-      tmap[us->tmoff[r] + t] = (uint32_t)l;
+  const uint64_t stride = (uint64_t)gridDim.x * UB;
+  for (uint32_t r = 0; r < 6; ++r) {
+    const uint64_t g0 = us->loff[r], n = us->loff[r + 1] - g0;
+    const uint64_t tm0 = us->tmoff[r], nt = us->tmoff[r + 1] - tm0;
+    for (uint64_t l = (uint64_t)blockIdx.x * UB + threadIdx.x; l < n; l += stride) {
+      const uint32_t c = us->cnt[g0 + l];
+      if (!c || c > UG_LEAFMAX) continue;
+      const uint64_t x0 = uni_pre(us, r, l);
+      const uint64_t b0 = uni_removed_before(us, r, x0), b1 = uni_removed_before(us, r, x0 + c);
+      const uint64_t f = x0 - b0, kept = c - (b1 - b0);
+      for (uint64_t t = (f + UG_TILE - 1) / UG_TILE; t * UG_TILE < f + kept && t < nt; ++t) tmap[tm0 + t] = (uint32_t)l;
+    }
   }
 }
 
@@ -168,7 +173,7 @@ __global__ __launch_bounds__(UB) void k_ug_expand(const UniSet* __restrict__ us,
                                                  uint64_t n, uint64_t S, uint64_t* __restrict__ out,
                                                  unsigned int* flags) {
   __shared__ unsigned long long raw[UG_TILE];
-  __shared__ uint32_t cand[UG_CAP];
+  __shared__ uint32_t cand[UG_CAND];
   const uint64_t lt = first / UG_TILE + blockIdx.x;
   const uint64_t t0 = lt * UG_TILE;
   const uint32_t mt = (uint32_t)(S - t0 < UG_TILE ? S - t0 : UG_TILE);

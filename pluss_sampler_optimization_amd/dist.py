@@ -277,6 +277,16 @@ def merge_results(ctx, err, dev, group=None):
     return Histogram(h.bins, tsum)
 
 
+def _pass_stream(dev, stream):
+    """The torch stream a sharded faithful pass runs on: the library's phases,
+    the row exchanges (DeviceRows) and the merge all on it, so they are
+    ordered.  The legacy null stream is never used: the library would take
+    its own stream for it (stream == NULL), unordered with torch's copies."""
+    import torch
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    return torch.cuda.Stream(dev) if st.cuda_stream == 0 else st
+
+
 def _open(cfg, sp):
     """(Context, None), or (None, the error): a rank that cannot even open its
     handle (e.g. out of memory) still takes part in every exchange of the pass
@@ -307,23 +317,27 @@ def sharded_faithful_hist(cfg, samples_by_ref, group=None, stream=None):
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     dev = torch.device("cuda", cfg.device)
     lo, hi = key_range(faithful_key_space(cfg), rank, world)
-    sp = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    st = _pass_stream(dev, stream)
+    sp = st.cuda_stream
     totals = [0] * 6
     for r, t in samples_by_ref.items():
         totals[REFS.index(r) if isinstance(r, str) else int(r)] = t.numel()
     lists = torch.cat([samples_by_ref[r].reshape(-1) for r in sorted(samples_by_ref,
                        key=lambda x: REFS.index(x) if isinstance(x, str) else int(x))]) if samples_by_ref else \
         torch.zeros(1, dtype=torch.int64, device=dev)
-    rx = DeviceRows(world, dev, group)
-    ctx, err = _open(cfg, sp)
-    try:
-        err = faithful_shards_protocol(
-            ctx, lambda row: ctx.faithful_shards_select(lists.data_ptr(), totals, lo, hi, row, sp), rank, world, rx,
-            sp, err=err, selected=True)
-        return merge_results(ctx, err, dev, group)
-    finally:
-        if ctx is not None:
-            ctx.close()
+    if st != torch.cuda.current_stream(dev):
+        st.wait_stream(torch.cuda.current_stream(dev))  # (the caller's lists)
+    with torch.cuda.stream(st):
+        rx = DeviceRows(world, dev, group)
+        ctx, err = _open(cfg, sp)
+        try:
+            err = faithful_shards_protocol(
+                ctx, lambda row: ctx.faithful_shards_select(lists.data_ptr(), totals, lo, hi, row, sp), rank, world,
+                rx, sp, err=err, selected=True)
+            return merge_results(ctx, err, dev, group)
+        finally:
+            if ctx is not None:
+                ctx.close()
 
 
 def sharded_faithful_gen_hist(cfg, seed, totals, group=None, stream=None):
@@ -339,7 +353,8 @@ def sharded_faithful_gen_hist(cfg, seed, totals, group=None, stream=None):
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     dev = torch.device("cuda", cfg.device)
     lo, hi = key_range(faithful_key_space(cfg), rank, world)
-    sp = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    st = _pass_stream(dev, stream)
+    sp = st.cuda_stream
     err = None
     first, n = [0] * 6, [0] * 6
     try:
@@ -349,14 +364,17 @@ def sharded_faithful_gen_hist(cfg, seed, totals, group=None, stream=None):
                 first[r], n[r] = a, b - a
     except Exception as e:  # noqa: BLE001 -- reported after the pass, on every rank
         err = e
-    rx = DeviceRows(world, dev, group)
     tot = [int(t) for t in totals]
-    ctx, err2 = _open(cfg, sp)
-    try:
-        err = faithful_shards_protocol(
-            ctx, lambda row: ctx.faithful_shards_local(None, seed, tot, first, n, row, sp), rank, world, rx, sp,
-            err=err or err2)
-        return merge_results(ctx, err, dev, group)
-    finally:
-        if ctx is not None:
-            ctx.close()
+    if st != torch.cuda.current_stream(dev):
+        st.wait_stream(torch.cuda.current_stream(dev))  # (the caller's lists)
+    with torch.cuda.stream(st):
+        rx = DeviceRows(world, dev, group)
+        ctx, err2 = _open(cfg, sp)
+        try:
+            err = faithful_shards_protocol(
+                ctx, lambda row: ctx.faithful_shards_local(None, seed, tot, first, n, row, sp), rank, world, rx, sp,
+                err=err or err2)
+            return merge_results(ctx, err, dev, group)
+        finally:
+            if ctx is not None:
+                ctx.close()

@@ -13,6 +13,11 @@ import pluss_sampler_optimization_amd as P  # noqa: E402
 
 SEED = 0x5EED0001
 args = sys.argv[1:]
+only = None  # --only radix,uniform: time those sources alone (e.g. under a kernel trace)
+if "--only" in args:
+    i = args.index("--only")
+    only = set(args[i + 1].split(","))
+    del args[i:i + 2]
 shapes = [tuple(int(x) for x in args[i:i + 3]) for i in range(0, len(args), 3)] or [(1024, 8, 24)]
 st = torch.cuda.Stream()
 sp = st.cuda_stream
@@ -47,12 +52,14 @@ for N, T, lg in shapes:
                 "uniform": lambda: ctx.gen_uniform_faithful_refs(SEED, counts, sp)}
         res = {"N": N, "T": T, "samples": total}
         hs = {}
+        runs = {k: v for k, v in runs.items() if only is None or k in only or k == "sorted"}
         for name, run in runs.items():
             ctx.reset(sp)
             run()
             torch.cuda.synchronize()
             hs[name] = ctx.fetch()
             res[name + "_ms"] = timed(run)
-        assert hs["sorted"].bins == hs["generated"].bins
+        if "generated" in hs:
+            assert hs["sorted"].bins == hs["generated"].bins
         res["recorded"] = hs["sorted"].total()
         print(json.dumps(res), flush=True)
