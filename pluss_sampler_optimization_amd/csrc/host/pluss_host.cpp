@@ -121,6 +121,64 @@ int emit_text(const std::string& s, char* buf, uint64_t cap, uint64_t* len) {
   return PLUSS_OK;
 }
 
+
+// pluss_AET (pluss_utils.h:758-804), the reference's walk of t with its
+// additions in its order; the points go straight to the output array (one per
+// cache size c = 0..min(max RI, 327680), in c order: no map of 327,681 points).
+int aet_impl(const pluss_kv* hist, uint64_t n, pluss_kv* mrc, uint64_t cap, uint64_t* n_out) {
+  if (n && !hist) return PLUSS_ERR_CONFIG;
+  Hist h;
+  double total = 0;
+  long max_rt = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    total += hist[i].value;
+    h[(long)hist[i].key] += hist[i].value;
+    if (max_rt < hist[i].key) max_rt = (long)hist[i].key;
+  }
+  std::map<uint64_t, double> P;
+  double acc = 0.;
+  auto m1 = h.find(-1);
+  if (m1 != h.end()) acc = m1->second;
+  for (auto it = h.rbegin(); it != h.rend(); ++it) {
+    if (it->first == -1) break;
+    P[(uint64_t)it->first] = acc / total;
+    acc += it->second;
+  }
+  P[0] = 1.0;
+  // walk t = 0..max_rt like the reference (same additions, same order)
+  std::vector<std::pair<uint64_t, double>> pv(P.begin(), P.end());
+  size_t pi = 0;
+  double sum_p = 0, pred = -1.0, cur = pv[0].second;
+  uint64_t t = 0;
+  const uint64_t cs = 2560 * 1024 / sizeof(double);
+  const uint64_t top = (uint64_t)max_rt < cs ? (uint64_t)max_rt : cs;  // c = 0..top
+  const uint64_t nout = max_rt >= 0 ? top + 1 : 0;
+  if (n_out) *n_out = nout;
+  if (nout > cap) return PLUSS_ERR_CAPACITY;
+  uint64_t k = 0;
+  for (uint64_t c = 0; c <= (uint64_t)max_rt && c <= cs; c++) {
+    while (sum_p < (double)c && t <= (uint64_t)max_rt) {
+      while (pi < pv.size() && pv[pi].first < t) ++pi;
+      if (pi < pv.size() && pv[pi].first == t) {
+        sum_p += pv[pi].second;
+        cur = pv[pi].second;
+        t++;
+      } else {
+        sum_p += cur;
+        t++;
+      }
+    }
+    if (pred != -1.0 || pred - cur < 0.0001) {  // (the reference's test: every c is written)
+      if (pred == -1.0) pred = cur;
+      mrc[k].key = (int64_t)c;
+      mrc[k].value = cur;
+      ++k;
+    }
+  }
+  if (n_out) *n_out = k;
+  return PLUSS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -207,52 +265,7 @@ int pluss_log2_merge(const pluss_kv* in, uint64_t n, pluss_kv* out, uint64_t cap
 }
 
 int pluss_aet(const pluss_kv* hist, uint64_t n, pluss_kv* mrc, uint64_t cap, uint64_t* n_out) {
-  // pluss_AET (pluss_utils.h:758-804)
-  if (n && !hist) return PLUSS_ERR_CONFIG;
-  Hist h;
-  double total = 0;
-  long max_rt = 0;
-  for (uint64_t i = 0; i < n; ++i) {
-    total += hist[i].value;
-    h[(long)hist[i].key] += hist[i].value;
-    if (max_rt < hist[i].key) max_rt = (long)hist[i].key;
-  }
-  std::map<uint64_t, double> P;
-  double acc = 0.;
-  auto m1 = h.find(-1);
-  if (m1 != h.end()) acc = m1->second;
-  for (auto it = h.rbegin(); it != h.rend(); ++it) {
-    if (it->first == -1) break;
-    P[(uint64_t)it->first] = acc / total;
-    acc += it->second;
-  }
-  P[0] = 1.0;
-  // walk t = 0..max_rt exactly like the reference (same additions, same order)
-  std::vector<std::pair<uint64_t, double>> pv(P.begin(), P.end());
-  size_t pi = 0;
-  double sum_p = 0, pred = -1.0, cur = pv[0].second;
-  uint64_t t = 0;
-  const uint64_t cs = 2560 * 1024 / sizeof(double);
-  Hist out;
-  for (uint64_t c = 0; c <= (uint64_t)max_rt && c <= cs; c++) {
-    while (sum_p < c && t <= (uint64_t)max_rt) {
-      while (pi < pv.size() && pv[pi].first < t) ++pi;
-      if (pi < pv.size() && pv[pi].first == t) {
-        sum_p += pv[pi].second;
-        cur = pv[pi].second;
-      } else {
-        sum_p += cur;
-      }
-      t++;
-    }
-    if (pred != -1.0) {
-      out[(long)c] = cur;
-    } else if (pred - cur < 0.0001) {
-      out[(long)c] = cur;
-      pred = cur;
-    }
-  }
-  return emit(out, mrc, cap, n_out);
+  return aet_impl(hist, n, mrc, cap, n_out);
 }
 
 int pluss_format_hist(const char* title, const pluss_kv* hist, uint64_t n, char* buf, uint64_t cap, uint64_t* len) {
@@ -270,24 +283,28 @@ int pluss_format_hist(const char* title, const pluss_kv* hist, uint64_t n, char*
 }
 
 int pluss_format_mrc(const pluss_kv* mrc, uint64_t n, char* buf, uint64_t cap, uint64_t* len) {
-  // pluss_print_mrc (pluss_utils.h:851-883): plateaus printed as first/last point
-  std::map<uint64_t, double> m;
-  for (uint64_t i = 0; i < n; ++i) m[(uint64_t)mrc[i].key] = mrc[i].value;
+  // pluss_print_mrc (pluss_utils.h:851-883): plateaus printed as first/last point.
+  // The points in key order (pluss_aet's output already is: no map needed).
+  std::vector<std::pair<uint64_t, double>> m;
+  m.reserve(n);
+  bool sorted = true;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (i && (uint64_t)mrc[i].key <= (uint64_t)mrc[i - 1].key) sorted = false;
+    m.emplace_back((uint64_t)mrc[i].key, mrc[i].value);
+  }
+  if (!sorted) {
+    std::map<uint64_t, double> mm;
+    for (uint64_t i = 0; i < n; ++i) mm[(uint64_t)mrc[i].key] = mrc[i].value;
+    m.assign(mm.begin(), mm.end());
+  }
   std::ostringstream os;
   os << "miss ratio\n";
-  auto it1 = m.begin(), it2 = m.begin();
-  while (it1 != m.end()) {
-    while (true) {
-      auto it3 = it2;
-      ++it3;
-      if (it3 == m.end()) break;
-      if (it1->second - it3->second < 0.00001) ++it2;
-      else break;
-    }
-    os << it1->first << ", " << it1->second << "\n";
-    if (it1 != it2) os << it2->first << ", " << it2->second << "\n";
-    it1 = ++it2;
-    it2 = it1;
+  size_t i1 = 0, i2 = 0;
+  while (i1 < m.size()) {
+    while (i2 + 1 < m.size() && m[i1].second - m[i2 + 1].second < 0.00001) ++i2;
+    os << m[i1].first << ", " << m[i1].second << "\n";
+    if (i1 != i2) os << m[i2].first << ", " << m[i2].second << "\n";
+    i1 = ++i2;
   }
   return emit_text(os.str(), buf, cap, len);
 }

@@ -12,6 +12,8 @@ reference's host code after the sampler:
 import ctypes
 import os
 
+import numpy as np
+
 from ._lib import PlussError, PlussHistEntry
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -41,8 +43,8 @@ def host_lib():
         L.pluss_format_hist.argtypes = [ctypes.c_char_p, P(PlussKV), ctypes.c_uint64, ctypes.c_char_p,
                                         ctypes.c_uint64, u64p]
         L.pluss_format_mrc.argtypes = [P(PlussKV), ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64, u64p]
-        for f in (L.pluss_cri_r10, L.pluss_cri_v1, L.pluss_log2_merge, L.pluss_aet, L.pluss_format_hist,
-                  L.pluss_format_mrc):
+        for f in (L.pluss_cri_r10, L.pluss_cri_v1, L.pluss_log2_merge, L.pluss_aet,
+                  L.pluss_format_hist, L.pluss_format_mrc):
             f.restype = ctypes.c_int
         _hl = L
     return _hl
@@ -61,24 +63,38 @@ def _entries(bins):
     return arr, len(items)
 
 
+_KV = np.dtype([("key", np.int64), ("value", np.float64)])  # == pluss_kv
+
+
 def _kv(d):
-    items = sorted(d.items())
-    arr = (PlussKV * max(1, len(items)))()
-    for i, (k, v) in enumerate(items):
-        arr[i].key = int(k)
-        arr[i].value = float(v)
-    return arr, len(items)
+    """{key: value} (or a _KV array) -> a pluss_kv array sorted by key, built
+    with numpy (an MRC has 327,681 points)."""
+    if isinstance(d, np.ndarray):
+        a = np.ascontiguousarray(d[np.argsort(d["key"], kind="stable")]) if len(d) else np.zeros(1, _KV)
+        return (PlussKV * len(a)).from_buffer(a), len(d)
+    n = len(d)
+    a = np.zeros(max(1, n), _KV)
+    if n:
+        keys = np.fromiter(d.keys(), dtype=np.int64, count=n)
+        vals = np.fromiter(d.values(), dtype=np.float64, count=n)
+        o = np.argsort(keys, kind="stable")
+        a["key"][:n] = keys[o]
+        a["value"][:n] = vals[o]
+    return (PlussKV * len(a)).from_buffer(a), n
 
 
-def _call_kv(fn, *args, cap=1 << 20):
-    out = (PlussKV * cap)()
+def _call_kv(fn, *args, cap=1 << 12, as_array=False):
+    out = np.empty(cap, _KV)
     n = ctypes.c_uint64()
-    rc = fn(*args, out, cap, ctypes.byref(n))
+    rc = fn(*args, out.ctypes.data_as(ctypes.POINTER(PlussKV)), cap, ctypes.byref(n))
     if rc == -4:
-        return _call_kv(fn, *args, cap=int(n.value) + 1)
+        return _call_kv(fn, *args, cap=int(n.value) + 1, as_array=as_array)
     if rc:
         raise PlussError(f"{fn.__name__}: rc={rc}")
-    return {out[i].key: out[i].value for i in range(n.value)}
+    m = int(n.value)
+    if as_array:
+        return out[:m]
+    return dict(zip(out["key"][:m].tolist(), out["value"][:m].tolist()))
 
 
 def r10_sampler_output(threads, bins):
@@ -103,9 +119,16 @@ def log2_merge(*hists):
     return _call_kv(host_lib().pluss_log2_merge, arr, n)
 
 
-def aet(hist):
+def aet_array(hist):
+    """pluss_aet as a structured array (key = cache size, value = miss ratio),
+    in key order: the 327,681 points stay out of Python objects."""
     arr, n = _kv(hist)
-    return _call_kv(host_lib().pluss_aet, arr, n)
+    return _call_kv(host_lib().pluss_aet, arr, n, as_array=True)
+
+
+def aet(hist):
+    a = aet_array(hist)
+    return dict(zip(a["key"].tolist(), a["value"].tolist()))
 
 
 def _text(fn, *args):
@@ -168,3 +191,12 @@ def mrc_from_r10(threads, hist):
             per_ref[ref] = r10_sampler_output(threads, bins)
     reuse = log2_merge(*per_ref.values())
     return per_ref, reuse, aet(reuse)
+
+
+def mrc_text_from_r10(threads, hist):
+    """mrc_from_r10 down to the reference's MRC printout (pluss_print_mrc),
+    the curve kept in an array: r10's whole host part after the samplers.
+    Returns (reuse_histogram, mrc_text)."""
+    reuse = log2_merge(*[r10_sampler_output(threads, b) for b in
+                         ({k: v for k, v in hist.bins.items() if k[0] == ref} for ref in REFS) if b])
+    return reuse, format_mrc(aet_array(reuse))

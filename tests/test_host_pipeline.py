@@ -68,6 +68,24 @@ def test_v1_fulltrace_pipeline_matches_seq_acc_output(orc):
     assert str(trav) == _section(txt, titles[4], titles)[0]
 
 
+@pytest.mark.parametrize("name,d,smp", GOLD[:3], ids=[g[0] for g in GOLD[:3]])
+def test_array_path_equals_dict_path(name, d, smp):
+    """host.mrc_text_from_r10 (the curve kept in an array: the bench's
+    pipeline leg) prints the same text as the dict path, and aet_array holds
+    aet's points in key order."""
+    import numpy as np
+
+    class Hh:
+        bins = {k: v for ref in ORDER for k, v in _raw_bins(d, ref).items()}
+    per = {ref: H.r10_sampler_output(d["T"], _raw_bins(d, ref)) for ref in ORDER}
+    reuse = H.log2_merge(*[per[r] for r in H.REFS])
+    r2, text = H.mrc_text_from_r10(d["T"], Hh)
+    assert r2 == reuse
+    assert text == H.format_mrc(H.aet(reuse))
+    a = H.aet_array(reuse)
+    assert list(a["key"]) == sorted(H.aet(reuse)) and (np.diff(a["key"]) > 0).all()
+
+
 def test_aet_edge_cases():
     assert H.aet({}) == {0: 1.0}  # pluss_AET: P[0] = 1 and c = 0 is always emitted
     m = H.aet({-1: 10.0})
