@@ -620,7 +620,7 @@ int orc_expand_sorted(const orc_cfg *c, uint64_t seed, int ref, uint64_t S, uint
    (the product's statement is csrc/pluss_uniform.h): every point
    is a candidate with probability p = min(1, (S + 10 sqrt(S) + 32) / D);
    leaves = key rows ((q, c1) for 3-D, q for 2-D references) cut into blocks of
-   w-values times the threads: K0 = clamp(floor(16 / (T p)), 1, span), nb = max(1, floor(span / K0))
+   w-values times the threads: K0 = clamp(floor(16 / (T p)), 1, span), nb = max(1, round(span / K0))
    blocks per row of K = ceil(span / nb) w-values (K*T < 2^32); a
    leaf's candidate count is Binomial(G, p) by inversion of one hash draw
    (or one Bernoulli draw per point in leaves of <= 64 points, more than 64
@@ -655,7 +655,7 @@ int orc_expand_uniform(const orc_cfg *c, uint64_t seed, int ref, uint64_t S, uin
     const double r = p < 1.0 ? p / (1.0 - p) : 0.0;
     const double kk = 16.0 / ((double)T * p);
     uint64_t K = kk < 1.0 ? 1 : (kk >= (double)W ? W : (uint64_t)kk);
-    const uint64_t nb0 = W / K ? W / K : 1; /* balanced: nb0 = floor(W / K) blocks of ceil(W / nb0) */
+    const uint64_t nb0 = (2 * W + K) / (2 * K) ? (2 * W + K) / (2 * K) : 1; /* balanced: round(W / K) blocks of ceil(W / nb0) */
     K = (W + nb0 - 1) / nb0;
     if (K > 0xFFFFFFFFULL / T) K = 0xFFFFFFFFULL / T; /* a leaf's points fit 32 bits */
     const uint64_t nb = (W + K - 1) / K, LA = RA * nb, L = LA + RB * nb;

@@ -1110,27 +1110,31 @@ __device__ __forceinline__ bool fa_fast_tile(const Model& m, const FaRefs& a, co
 // once, and a second sweep over the kept offsets finds the starts.  The
 // tile's first and last keys are decoded by every wave (two uniform loads):
 // no barrier before the scan.  Results as fa_local_fast's.
+template <int NT>  // threads of the workgroup (NT / 64 waves, TILE / NT steps each)
 struct FaLm {
   unsigned long long out[FPW + 1];
-  unsigned long long ordl[TB / 64];       // each wave's last element's order word (CHECK)
-  unsigned long long red[TB / 64][6];     // per wave: starts, case 0, case 1, case 2 of tid 0, sum(key - run), last start + 1
-  uint32_t wmax[TB / 64];                 // each wave's largest sink (offset)
-  uint32_t kl[TB / 64][KL][2];            // each wave's first KL starts: key offset, running max before it
+  unsigned long long ordl[NT / 64];       // each wave's last element's order word (CHECK)
+  unsigned long long red[NT / 64][6];     // per wave: starts, case 0, case 1, case 2 of tid 0, sum(key - run), last start + 1
+  uint32_t wmax[NT / 64];                 // each wave's largest sink (offset)
+  uint32_t kl[NT / 64][KL][2];            // each wave's first KL starts: key offset, running max before it
 };
 
-template <int SRC, bool CHECK, uint32_t REF, bool FULLT>
-__device__ __forceinline__ bool fa_lane_tile(const Model& m, const FaRefs& a, const FaTile& T, FaLm& sh,
-                                             unsigned long long* __restrict__ klist, GTable g) {
-  constexpr int NW = TB / 64, ST = TI;  // waves, steps per wave
+// (SRC_UNI: the tile generated into LDS first, `tile`, element e at tile[e])
+template <int SRC, bool CHECK, uint32_t REF, bool FULLT, int NT>
+__device__ __forceinline__ bool fa_lane_tile(const Model& m, const FaRefs& a, const FaTile& T, FaLm<NT>& sh,
+                                             unsigned long long* __restrict__ klist, GTable g,
+                                             const fa_raw_t<SRC>* tile = nullptr) {
+  constexpr int NW = NT / 64, ST = TILE / NT;  // waves, steps per wave
   const FaOne o = fa_one_ref<SRC, REF>(a, T);
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
-  const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(o.src) + T.base;
+  const fa_raw_t<SRC>* src = SRC == SRC_UNI ? tile : static_cast<const fa_raw_t<SRC>*>(o.src) + T.base;
   const uint32_t last = T.mt - 1, e0 = wid * (64 * ST) + lane;
   fa_raw_t<SRC> v[ST];
 #pragma unroll
   for (int k = 0; k < ST; ++k) {
     const uint32_t e = e0 + 64u * k;
-    v[k] = __builtin_nontemporal_load(src + (e < last ? e : last));
+    if constexpr (SRC == SRC_UNI) v[k] = src[e < last ? e : last];
+    else v[k] = __builtin_nontemporal_load(src + (e < last ? e : last));
   }
   // ri*T per case (0xFFFFFFFF: cold) and the tile's first and last keys, in every wave
   auto rt = [&](int c) -> unsigned long long {
@@ -1422,21 +1426,39 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4))) void k_
 
 // The lane-major fast path over every tile of a memory source (fa_lane_tile);
 // the tiles it cannot take are queued in slowq for k_fa_local.
+// SRC_UNI: the tile is first generated into LDS (uni_stage, in key order), then
+// scanned lane-major.  (512 threads per tile, so that each of a tile's ~258
+// leaves had its own thread, ran 1.5x slower at config 3: 2 workgroups per CU.)
+template <int SRC>
+constexpr int fa_lm_nt() { return TB; }
+template <int SRC>
+struct FaLmLds {
+  FaLm<fa_lm_nt<SRC>()> s;
+  fa_raw_t<SRC> raw[SRC == SRC_UNI ? TILE : 1];
+  uint32_t cand[SRC == SRC_UNI ? UG_CAND : 1];
+};
+template <int SRC>
+constexpr bool fa_lm() { return fa_mem<SRC>() || SRC == SRC_UNI; }
+
 template <int SRC, bool CHECK>
-__global__ __launch_bounds__(TB) void k_fa_local_lm(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
+__global__ __launch_bounds__(fa_lm_nt<SRC>()) __attribute__((amdgpu_waves_per_eu(4))) void k_fa_local_lm(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
                                                     unsigned long long* __restrict__ part,
                                                     unsigned long long* __restrict__ klist, unsigned long long* slots,
                                                     unsigned int* slowq, GTable g) {
-  static_assert(fa_mem<SRC>(), "generated sources: k_fa_local_fast");
-  __shared__ FaLm sh;
+  static_assert(fa_lm<SRC>(), "the stratified generated source: k_fa_local_fast");
+  constexpr int NT = fa_lm_nt<SRC>();
+  __shared__ FaLmLds<SRC> L;
+  FaLm<NT>& sh = L.s;
   const FaTile T = fa_tile(a, blockIdx.x);
   fa_cold_slot(T, g, slots);
   unsigned long long* kl_out = klist + T.gt * (uint64_t)(2 * KL);
   bool done = false;
   // full tiles only: the few partial ones (a reference's last tile) go to the slow pass,
   // which keeps the kernel's registers at the full tile's (8 waves per SIMD)
-#define PLUSS_FA_LM(R) done = fa_lane_tile<SRC, CHECK, R, true>(m, a, T, sh, kl_out, g);
+#define PLUSS_FA_LM(R) done = fa_lane_tile<SRC, CHECK, R, true, NT>(m, a, T, sh, kl_out, g, L.raw);
   if (T.mt == TILE) {
+    if constexpr (SRC == SRC_UNI)
+      uni_stage<NT>(a.us, T.r, T.lt, T.mt, L.raw, L.cand, a.us->flags, [](uint32_t e) { return e; });
     PLUSS_FA_REFS(PLUSS_FA_LM)
   }
 #undef PLUSS_FA_LM
@@ -1948,8 +1970,8 @@ inline void fa_launch_t(const FaLaunch& L) {
       if (L.a.fast) {
         // the queue starts empty whatever an earlier, abandoned pass left in it
         (void)hipMemsetAsync(b.slowq, 0, sizeof(unsigned int), L.s);
-        if constexpr (fa_mem<SRC>())
-          hipLaunchKernelGGL((k_fa_local_lm<SRC, CHK>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
+        if constexpr (fa_lm<SRC>())
+          hipLaunchKernelGGL((k_fa_local_lm<SRC, CHK>), dim3(t), dim3(fa_lm_nt<SRC>()), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
                              b.fslot, b.slowq, L.g);
         else
           hipLaunchKernelGGL((k_fa_local_fast<SRC, CHK>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart,

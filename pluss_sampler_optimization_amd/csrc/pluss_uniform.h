@@ -44,7 +44,7 @@
 
 namespace pluss {
 
-constexpr uint32_t UG_MEAN = 16;     // expected candidates per leaf
+constexpr uint32_t UG_MEAN = 16;     // expected candidates per leaf (K0)
 constexpr uint32_t UG_DIRECT = 64;   // leaves of at most this many points: one Bernoulli draw per point
 constexpr uint32_t UG_LEAFMAX = 1024;  // more candidates in one leaf: PLUSS_ERR_CAPACITY (P < 1e-300)
 constexpr uint32_t UG_CAP = 6144;      // candidates of one tile's leaves (LDS words)
@@ -58,9 +58,21 @@ struct UniGen {
   uint64_t W, K, nb;              // w-values per row, w-values per leaf, leaves per row
   uint64_t RA, RB, LA, L;         // rows of block A / B, leaves of block A, all leaves
   double p, r;                    // candidate probability per point; p / (1 - p)
+  double pm[4];                   // (1 - p)^G of the four leaf sizes: block A / B x full / last block of a row
   uint64_t base;                  // hash key of (seed, ref)
   Div64 dnb, dspan, dtA, dtB;     // division by nb, span, T, T-1
 };
+
+// (1 - p)^G by square and multiply, a fixed sequence of IEEE multiplies (host
+// and device agree bit for bit)
+PM_HD double uni_pow1p(double b, uint64_t e) {
+  double pm = 1.0;
+  for (; e; e >>= 1) {
+    if (e & 1) pm = pm * b;
+    b = b * b;
+  }
+  return pm;
+}
 
 // Host: the generator of S samples of reference `ref` (validated by the
 // caller: N % (CS*T) == 0, 1 <= S <= span^d, S + 10 sqrt(S) + 32 < 2^32).
@@ -84,9 +96,10 @@ inline UniGen make_unigen(uint64_t N, uint64_t T, uint64_t CS, bool range_full, 
   u.r = u.p < 1.0 ? u.p / (1.0 - u.p) : 0.0;
   const double kk = (double)UG_MEAN / ((double)T * u.p);
   u.K = kk < 1.0 ? 1 : (kk >= (double)u.W ? u.W : (uint64_t)kk);
-  // balanced leaves: a row cut into nb = floor(W / K) blocks of ceil(W / nb)
-  // w-values (not K, K, ..., and a sliver of a few points)
-  const uint64_t nb0 = u.W / u.K ? u.W / u.K : 1;
+  // balanced leaves: a row cut into nb = round(W / K) blocks of ceil(W / nb)
+  // w-values (not K, K, ..., and a sliver of a few points); about 11-24
+  // candidates per leaf
+  const uint64_t nb0 = (2 * u.W + u.K) / (2 * u.K) ? (2 * u.W + u.K) / (2 * u.K) : 1;
   u.K = (u.W + nb0 - 1) / nb0;
   if (u.K > 0xFFFFFFFFull / T) u.K = 0xFFFFFFFFull / T;  // a leaf's points fit 32 bits
   u.nb = (u.W + u.K - 1) / u.K;
@@ -99,6 +112,12 @@ inline UniGen make_unigen(uint64_t N, uint64_t T, uint64_t CS, bool range_full, 
   u.cssh = 0;
   while ((1ull << u.cssh) < CS) ++u.cssh;
   u.csp2 = (1ull << u.cssh) == CS ? 1u : 0u;
+  // a leaf has K w-values (the row's last block: W - (nb-1) K) times T threads (block B: T - 1)
+  const uint64_t kl = u.W - (u.nb - 1) * u.K;
+  u.pm[0] = uni_pow1p(1.0 - u.p, u.K * T);
+  u.pm[1] = uni_pow1p(1.0 - u.p, kl * T);
+  u.pm[2] = uni_pow1p(1.0 - u.p, u.K * (T > 1 ? T - 1 : 1));
+  u.pm[3] = uni_pow1p(1.0 - u.p, kl * (T > 1 ? T - 1 : 1));
   u.dnb = make_div64(u.nb);
   u.dspan = make_div64(u.span ? u.span : 1);
   u.dtA = make_div64(T);
@@ -134,7 +153,7 @@ PM_HD double uni_u01(uint64_t h) { return (double)(h >> 11) * 0x1.0p-53; }
 // per-point Bernoulli draws (small or dense leaves: with p <= 1/64 and at most
 // 4*UG_MEAN expected candidates, independent offsets collide rarely)
 PM_HD bool uni_direct(const UniGen& u, const UniLeaf& f) {
-  return f.G <= UG_DIRECT || (double)f.G * u.p > 4.0 * (double)UG_MEAN || u.p > 0.015625;
+  return f.G <= UG_DIRECT || (double)f.G * u.p > 64.0 || u.p > 0.015625;
 }
 
 // The leaf's candidate count: Binomial(G, p).  Inversion with the pmf
@@ -152,11 +171,9 @@ PM_HD uint64_t uni_count(const UniGen& u, uint64_t l) {
     for (uint64_t j = 0; j < f.G; ++j) c += uni_u01(uni_hash(lk, j)) < u.p ? 1u : 0u;
     return c;
   }
-  double pm = 1.0, b = 1.0 - u.p;
-  for (uint64_t e = f.G; e; e >>= 1) {
-    if (e & 1) pm = pm * b;
-    b = b * b;
-  }
+  // (1 - p)^G: one of the four leaf sizes' values, computed once (make_unigen)
+  // (selects, not an index: an indexed copy of the generator went to scratch)
+  double pm = f.blk ? (f.kw == u.K ? u.pm[2] : u.pm[3]) : (f.kw == u.K ? u.pm[0] : u.pm[1]);
   double x_u = uni_u01(uni_hash(uni_leafkey(u, l, 0xFFFFFFFEu), 0));
   uint64_t x = 0;
   while (x_u >= pm && x < f.G) {
@@ -272,15 +289,21 @@ __device__ __forceinline__ uint64_t uni_removed_before(const UniSet* __restrict_
 // tile's first sample to the one holding the next tile's first are
 // regenerated: the removal bitmap's words over their candidate ranks and the
 // words' removed-before counts are staged in LDS first (a few hundred words,
-// coalesced), then each thread draws one leaf's candidates (sorted offsets,
-// in cand at the leaf's candidate rank) and packs every surviving one at its
-// sample index -- per candidate only LDS reads and integer work, the leaf's
-// row decoded once.  A window past UG_CAP candidates or a leaf past
-// UG_LEAFMAX (neither happens with probability above 1e-20) sets FLAG_UNI.
-constexpr uint32_t UG_WCAP = UG_CAP / 32 + 2;      // bitmap words over a window of UG_CAP ranks
-constexpr uint32_t UG_CAND = UG_CAP + 2 * UG_WCAP;  // cand: offsets, then the window's words and counts
+// coalesced), then each thread draws one leaf's candidates in key order and
+// packs every surviving one at its sample index:
+//   per-point draws (small or dense leaves) come out in order;
+//   up to UG_NET offsets are sorted in registers (a bitonic network);
+//   larger leaves (rare) are insertion-sorted in a shared LDS scratch of
+//   UG_SCR words, or, when the tile's large leaves overflow it, emitted by
+//   repeated minimum search over their offsets (no scratch; O(c^2)).
+// A window past UG_CAP candidates or a leaf past UG_LEAFMAX (neither happens
+// with probability above 1e-20) sets FLAG_UNI.
+constexpr uint32_t UG_WCAP = UG_CAP / 32 + 2;  // bitmap words over a window of UG_CAP ranks
+constexpr uint32_t UG_SCR = 768;               // the large leaves' scratch (words; 4 workgroups of the scan per CU)
+constexpr uint32_t UG_CAND = UG_SCR + 2 * UG_WCAP + 1;  // cand: scratch, the window's words and counts, an allocator
 
-// a leaf's row decoded once: the digits of its offset o are then shifts (block A, T a power of two)
+// a leaf's row decoded once, and its packed samples' fixed bits: the digits
+// of offset o are then shifts (block A, T a power of two)
 struct UniRowD {
   uint32_t q, c1, w0;
 };
@@ -369,8 +392,10 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
   const uint64_t wo = us->woff[r], wend = us->woff[r + 1] - wo;  // (a flagged plan's indices are clamped)
   const uint64_t wlo = r0 >> 5;
   const uint32_t nw = rend > r0 ? (uint32_t)(((rend - 1) >> 5) - wlo + 1) : 0u;
-  uint32_t* bw = cand + UG_CAP;
+  uint32_t* scr = cand;
+  uint32_t* bw = cand + UG_SCR;
   uint32_t* rbw = bw + UG_WCAP;
+  uint32_t* alloc = rbw + UG_WCAP;
   const uint64_t wl = wlo < wend ? wlo : wend - 1;
   const uint64_t rem0 = us->rb[wo + wl] - us->rb[wo];
   for (uint32_t i = threadIdx.x; i < nw; i += NT) {
@@ -378,6 +403,7 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
     bw[i] = us->bits[wo + w];
     rbw[i] = (uint32_t)(us->rb[wo + w] - us->rb[wo] - rem0);
   }
+  if (threadIdx.x == 0) *alloc = 0;
   __syncthreads();
   const uint64_t f0 = lt * UG_TILE;
   for (uint64_t l = la + threadIdx.x; l <= lb; l += NT) {
@@ -388,16 +414,28 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
       continue;
     }
     const uint64_t x0 = pre[lg0 + l] - pbase;
-    uint32_t* seg = cand + (x0 - r0);
     const UniLeaf f = uni_leaf(u, l);
-    auto emit = [&](uint32_t i, uint32_t o, const UniRowD& rd) {
+    const UniRowD rd = uni_row(u, f);
+    // candidate i of the leaf (in key order) has rank x0 + i; the removed ones are skipped
+    const uint32_t w0i = (uint32_t)((x0 >> 5) - wlo);
+    uint64_t rem = rem0 + rbw[w0i] + (uint64_t)__popc(bw[w0i] & ((1u << (x0 & 31)) - 1u));  // removed before x0
+    auto emit = [&](uint32_t i, uint32_t o) {
       const uint64_t x = x0 + i;
-      const uint32_t wi = (uint32_t)((x >> 5) - wlo), word = bw[wi];
-      if ((word >> (x & 31)) & 1u) return;  // removed
-      const uint64_t e = x - (rem0 + rbw[wi] + (uint64_t)__popc(word & ((1u << (x & 31)) - 1u))) - f0;
+      if ((bw[(uint32_t)((x >> 5) - wlo)] >> (x & 31)) & 1u) {
+        ++rem;
+        return;
+      }
+      const uint64_t e = x - rem - f0;
       if (e < mt) raw[slot((uint32_t)e)] = uni_pack_row(u, f, rd, o);
     };
-    if (u.p < 1.0 && c <= UG_NET && !uni_direct(u, f)) {
+    if (u.p >= 1.0) {
+      for (uint32_t j = 0; j < c; ++j) emit(j, j);
+    } else if (uni_direct(u, f)) {  // per-point draws: already in order
+      const uint64_t lk = uni_leafkey(u, l, 0xFFFFFFFFu);
+      uint32_t k = 0;
+      for (uint32_t j = 0; j < (uint32_t)f.G && k < c; ++j)
+        if (uni_u01(uni_hash(lk, j)) < u.p) emit(k++, j);
+    } else if (c <= UG_NET) {
       // the common leaf: its offsets drawn and sorted in registers (an insertion
       // sort through LDS was a chain of dependent LDS round trips, divergent per lane)
       const uint32_t G = (uint32_t)f.G;  // (K*T < 2^32)
@@ -416,42 +454,55 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
         for (uint32_t q = 0; q + 1 < UG_NET; ++q) dup |= v[q] == v[q + 1] && q + 1 < c;
         if (!dup) break;
       }
-      const UniRowD rd = uni_row(u, f);
 #pragma unroll
       for (uint32_t q = 0; q < UG_NET; ++q)
-        if (q < c) emit(q, v[q], rd);
-      continue;
-    }
-    if (u.p >= 1.0) {
-      for (uint32_t j = 0; j < c; ++j) seg[j] = j;
-    } else if (uni_direct(u, f)) {
-      const uint64_t lk = uni_leafkey(u, l, 0xFFFFFFFFu);
-      uint32_t k = 0;
-      for (uint32_t j = 0; j < (uint32_t)f.G; ++j)
-        if (uni_u01(uni_hash(lk, j)) < u.p) seg[k++] = j;
-    } else {
+        if (q < c) emit(q, v[q]);
+    } else {  // a large leaf (rare)
+      const uint32_t G = (uint32_t)f.G;
+      const uint32_t off = atomicAdd(alloc, c);
+      uint64_t lk = 0;
       for (uint32_t a = 0;; ++a) {  // independent uniform offsets, sorted; redrawn on a duplicate
         if (a == UG_TRIES) {
           atomicOr(flags, FLAG_UNI);
           break;
         }
-        const uint64_t lk = uni_leafkey(u, l, a);
+        lk = uni_leafkey(u, l, a);
         bool dup = false;
-        for (uint32_t i = 0; i < c; ++i) {
-          const uint32_t x = (uint32_t)uni_offset(lk, i, f.G);
-          uint32_t j = i, y = 0;
-          while (j > 0 && (y = seg[j - 1]) > x) {
-            seg[j] = y;
-            --j;
+        if (off + c <= UG_SCR) {
+          uint32_t* seg = scr + off;
+          for (uint32_t i = 0; i < c; ++i) {
+            const uint32_t x = uni_offset32(lk, i, G);
+            uint32_t j = i, y = 0;
+            while (j > 0 && (y = seg[j - 1]) > x) {
+              seg[j] = y;
+              --j;
+            }
+            dup |= j > 0 && y == x;
+            seg[j] = x;
           }
-          dup |= j > 0 && y == x;
-          seg[j] = x;
+        } else {
+          for (uint32_t i = 1; i < c && !dup; ++i) {
+            const uint32_t x = uni_offset32(lk, i, G);
+            for (uint32_t j = 0; j < i; ++j) dup |= uni_offset32(lk, j, G) == x;
+          }
         }
         if (!dup) break;
       }
+      if (off + c <= UG_SCR) {
+        for (uint32_t i = 0; i < c; ++i) emit(i, scr[off + i]);
+      } else {  // no scratch left: the offsets in order by repeated minimum search
+        int64_t last = -1;
+        for (uint32_t i = 0; i < c; ++i) {
+          uint32_t m = 0xFFFFFFFFu;
+          for (uint32_t j = 0; j < c; ++j) {
+            const uint32_t x = uni_offset32(lk, j, G);
+            if ((int64_t)x > last && x < m) m = x;
+          }
+          emit(i, m);
+          last = m;
+        }
+      }
     }
-    const UniRowD rd = uni_row(u, f);
-    for (uint32_t i = 0; i < c; ++i) emit(i, seg[i], rd);
   }
   __syncthreads();
 }

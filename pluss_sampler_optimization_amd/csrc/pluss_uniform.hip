@@ -120,7 +120,7 @@ __global__ __launch_bounds__(UB) void k_ug_count(const UniSet* __restrict__ us, 
   for (uint32_t r = 0; r < 6; ++r) {
     const uint64_t g0 = us->loff[r], n = us->loff[r + 1] - g0;
     if (!n) continue;
-    const UniGen u = us->u[r];
+    const UniGen& u = us->u[r];  // (wave-uniform: scalar loads; a by-value copy went to scratch)
     for (uint64_t l = (uint64_t)blockIdx.x * UB + threadIdx.x; l < n; l += stride) {
       const uint64_t c = uni_count(u, l);
       if (c > UG_LEAFMAX) atomicOr(flags, FLAG_UNI);
