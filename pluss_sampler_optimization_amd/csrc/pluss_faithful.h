@@ -324,7 +324,6 @@ struct FaLds {
   unsigned long long rt[4];     // ri*T per case (KEY_EMPTY: cold; case 3: malformed)
   unsigned long long klast[NT / 64];
   unsigned long long kb[2];     // the tile's first and last keys (FA_LOCAL)
-  fa_raw_t<SRC> prevw;          // the element before the tile (the fast path's order check)
   fa_raw_t<SRC> raw[SRC == SRC_GEN ? 1 : TILE + TILE / EPT];
   uint32_t cand[SRC == SRC_UNI ? UG_CAND : 1];  // the uniform generator's scratch (uni_stage)
 };
@@ -865,22 +864,15 @@ __device__ __forceinline__ void fa_local_fast(const Model& m, const FaOne& o, Fa
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
   const uint32_t e0 = threadIdx.x * TI;
   const uint32_t nv = FULLT ? TI : (e0 < T.mt ? (T.mt - e0 < TI ? T.mt - e0 : TI) : 0u);
+  static_assert(!CHECK, "generated lists are in key order by construction (the order check is fa_lane_tile's)");
   const uint32_t b32 = (uint32_t)base;
-  uint32_t rk[TI], sk[TI], lmax = 0, odd = 0;
+  uint32_t rk[TI], sk[TI], lmax = 0;
   uint32_t w0 = 0, w1 = 0, wc = 0;  // wave counts (ballots): case 0, case 1, case 2 of tid 0
-  bool unordered = false;
-  unsigned long long ofirst = 0, oprev = 0;
 #pragma unroll
   for (int k = 0; k < TI; ++k) {
     const bool v = FULLT || (uint32_t)k < nv;
-    uint32_t oddk = 0;  // a partial tile's LDS slots past its end hold stale words: not checked
+    uint32_t oddk = 0;
     const FaDec d = el(k, oddk);
-    odd |= v ? oddk : 0u;
-    if (CHECK && v) {
-      if (k == 0) ofirst = d.ord;
-      else unordered |= !(d.ord > oprev);
-      oprev = d.ord;
-    }
     rk[k] = v ? d.lk - b32 : 0u;
     const uint32_t dd = d.a ? r.r0 : (d.b ? r.r1 : r.r2);  // selects (an array here went to scratch)
     const uint32_t x = rk[k] + dd;  // dd = 0xFFFFFFFF (cold) wraps below dd: the max keeps it
@@ -890,23 +882,10 @@ __device__ __forceinline__ void fa_local_fast(const Model& m, const FaOne& o, Fa
     w1 += (uint32_t)__popcll(__ballot(v && !d.a && d.b));
     wc += (uint32_t)__popcll(__ballot(v && !d.a && !d.b && d.t0));
   }
-  if (CHECK) {  // across lanes, waves and the tile's start (the element before it)
-    const unsigned long long up = __shfl_up(oprev, 1, 64);
-    if (lane > 0 && nv) unordered |= !(ofirst > up);
-    if (lane == 63) sh.klast[wid] = oprev;
-  }
   // running max of sinks entering this lane
   const uint32_t linc = wave_scan_dpp<true>(lmax);
   if (lane == 63) sh.w[wid] = linc;
   __syncthreads();
-  if (CHECK) {
-    if (lane == 0 && wid > 0 && nv) unordered |= !(ofirst > sh.klast[wid - 1]);
-    if (threadIdx.x == 0 && T.base > 0) {  // (staged with the tile)
-      uint32_t o2 = 0;
-      unordered |= !(ofirst > fa_dec_sample<REF>(m, o.pv, (uint64_t)sh.prevw, o2).ord);
-    }
-    if (__ballot(odd != 0 || unordered) && lane == 0) atomicOr(&g.flags[1], 1u);
-  }
   uint32_t carry = wave_shr1(linc), tm = 0;
 #pragma unroll
   for (int x = 0; x < NW; ++x) {
@@ -1010,58 +989,22 @@ __device__ __forceinline__ const void* fa_src_of(const FaRefs& a, uint32_t r) {
 template <int SRC, uint32_t R>
 __device__ __forceinline__ FaOne fa_one_ref(const FaRefs& a, const FaTile& T);
 
-// A memory source's tile (k_fa_local_fast): thread x's TI coalesced elements
-// (round k: element k*TB + x; a partial tile's lanes past its end re-read its
-// last element) and the element before the tile (the order check), loaded
-// into registers, then written to LDS.
-template <int SRC>
-struct FaPre {
-  fa_raw_t<SRC> v[TI];
-  fa_raw_t<SRC> prev;
-};
-template <int SRC>
-__device__ __forceinline__ const void* fa_src_of(const FaRefs& a, uint32_t r);
-template <int SRC>
-__device__ __forceinline__ void fa_prefetch(const FaRefs& a, const FaTile& T, FaPre<SRC>& p) {
-  // every load issued before the first is waited for, none behind a branch
-  const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(fa_src_of<SRC>(a, T.r)) + T.base;
-  const uint32_t last = T.mt - 1;
-#pragma unroll
-  for (int k = 0; k < TI; ++k) {
-    const uint32_t e = (uint32_t)k * TB + threadIdx.x;
-    p.v[k] = __builtin_nontemporal_load(src + (e < last ? e : last));
-  }
-  p.prev = src[T.base > 0 ? -1 : 0];  // (one wave-uniform address)
-}
-template <int SRC>
-__device__ __forceinline__ void fa_stage(const FaPre<SRC>& p, FaLds<SRC, TB, TI>& sh) {
-#pragma unroll
-  for (int k = 0; k < TI; ++k) sh.raw[fa_slot_n<TI>((uint32_t)k * TB + threadIdx.x)] = p.v[k];
-  if (threadIdx.x == 0) sh.prevw = p.prev;
-}
-
-// One tile by the fast path: the first and last keys in 64 bits (memory
-// sources: the tile already staged in LDS; generated sources: generated
-// here), then the scan if the tile qualifies.  Returns whether the fast path
-// took the tile (tile-uniform).
+// One tile of the stratified generated lists by the thread-major fast path:
+// the first and last keys in 64 bits, then the scan if the tile qualifies.
+// Returns whether the fast path took the tile (tile-uniform).  (Lists in
+// memory and the uniform lists take the lane-major path, fa_lane_tile.)
 template <int SRC, bool CHECK, uint32_t REF>
 __device__ __forceinline__ bool fa_fast_tile(const Model& m, const FaRefs& a, const FaTile& T,
                                              FaLds<SRC, TB, TI>& sh, unsigned long long* __restrict__ klist,
                                              GTable g) {
+  static_assert(SRC == SRC_GEN, "the thread-major fast path serves the stratified generated lists");
   const FaOne o = fa_one_ref<SRC, REF>(a, T);
-  KeyGen kg;
-  if constexpr (SRC == SRC_GEN) kg = a.kg[REF];
+  const KeyGen kg = a.kg[REF];
   fa_rt(m, o.pv, sh);
   const bool full = T.mt == TILE;
-  if constexpr (SRC == SRC_UNI)
-    uni_stage<TB>(o.us, T.r, T.lt, T.mt, sh.raw, sh.cand, o.us->flags, [](uint32_t e) { return fa_slot_n<TI>(e); });
   if (threadIdx.x < 2) {  // the first and the last key, in 64 bits
     const uint32_t e = threadIdx.x ? T.mt - 1 : 0;
-    bool b2 = false;
-    if constexpr (SRC == SRC_GEN)
-      sh.kb[threadIdx.x] = elem_of_digits<true>(m, o.pv, REF, keygen_digits_at(kg, T.gbase + e)).key;
-    else
-      sh.kb[threadIdx.x] = fa_decode_ref<SRC, true, REF>(m, o.pv, sh.raw[fa_slot_n<TI>(e)], b2).key;
+    sh.kb[threadIdx.x] = elem_of_digits<true>(m, o.pv, REF, keygen_digits_at(kg, T.gbase + e)).key;
   }
   __syncthreads();
   const unsigned long long base = sh.kb[0], kl = sh.kb[1];
@@ -1074,29 +1017,19 @@ __device__ __forceinline__ bool fa_fast_tile(const Model& m, const FaRefs& a, co
   auto r32 = [](unsigned long long x) { return x == KEY_EMPTY ? 0xFFFFFFFFu : (uint32_t)x; };
   const FaRi r{r32(sh.rt[0]), r32(sh.rt[1]), r32(sh.rt[2])};
   if (!(kl >= base && kl - base < 0xFFFFFFFFull - rmax && r.r0 != 0xFFFFFFFFu && r.r1 != 0xFFFFFFFFu &&
-        (SRC != SRC_GEN || keyrun_fast_ok(kg, T.gbase, T.mt))))
+        keyrun_fast_ok(kg, T.gbase, T.mt)))
     return false;
   unsigned long long* kl_out = klist + T.gt * (uint64_t)(2 * KL);
   const uint32_t e0 = threadIdx.x * TI;
-  if constexpr (SRC == SRC_GEN) {
-    KeyRunF run;
-    keyrunf_start(kg, run, T.gbase + (e0 < T.mt ? e0 : 0u));
-    auto el = [&](int, uint32_t&) -> FaDec {
-      const KeyDigits dg = keyrunf_digits(kg, run);
-      keyrunf_next(kg, run);
-      return fa_dec_digits<REF>(m, o.pv, dg.q, dg.c1, dg.c2, dg.t);
-    };
-    if (full) fa_local_fast<SRC, CHECK, REF, true>(m, o, sh, base, r, el, kl_out, g);
-    else fa_local_fast<SRC, CHECK, REF, false>(m, o, sh, base, r, el, kl_out, g);
-  } else {
-    auto el = [&](int k, uint32_t& odd) -> FaDec {
-      const fa_raw_t<SRC> w = sh.raw[fa_slot_n<TI>(e0 + k)];
-      if constexpr (fa_smp<SRC>()) return fa_dec_sample<REF>(m, o.pv, (uint64_t)w, odd);
-      else return fa_dec_word<REF>(m, o.pv, w);
-    };
-    if (full) fa_local_fast<SRC, CHECK, REF, true>(m, o, sh, base, r, el, kl_out, g);
-    else fa_local_fast<SRC, CHECK, REF, false>(m, o, sh, base, r, el, kl_out, g);
-  }
+  KeyRunF run;
+  keyrunf_start(kg, run, T.gbase + (e0 < T.mt ? e0 : 0u));
+  auto el = [&](int, uint32_t&) -> FaDec {
+    const KeyDigits dg = keyrunf_digits(kg, run);
+    keyrunf_next(kg, run);
+    return fa_dec_digits<REF>(m, o.pv, dg.q, dg.c1, dg.c2, dg.t);
+  };
+  if (full) fa_local_fast<SRC, CHECK, REF, true>(m, o, sh, base, r, el, kl_out, g);
+  else fa_local_fast<SRC, CHECK, REF, false>(m, o, sh, base, r, el, kl_out, g);
   return true;
 }
 
@@ -1403,15 +1336,10 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4))) void k_
                                                       unsigned long long* __restrict__ part,
                                                       unsigned long long* __restrict__ klist,
                                                       unsigned long long* slots, unsigned int* slowq, GTable g) {
+  static_assert(SRC == SRC_GEN, "lists in memory and uniform lists: k_fa_local_lm");
   __shared__ FaLds<SRC, TB, TI> sh;
   const FaTile T = fa_tile(a, blockIdx.x);
   fa_cold_slot(T, g, slots);
-  if constexpr (fa_mem<SRC>()) {
-    FaPre<SRC> p;
-    fa_prefetch<SRC>(a, T, p);
-    fa_stage<SRC>(p, sh);
-    __syncthreads();
-  }
   bool done = false;
 #define PLUSS_FA_FAST(R) done = fa_fast_tile<SRC, CHECK, R>(m, a, T, sh, klist, g);
   PLUSS_FA_REFS(PLUSS_FA_FAST)

@@ -28,7 +28,7 @@ fetch = sum(v.get("FETCH_SIZE", 0.0) for v in kern.values())
 write = sum(v.get("WRITE_SIZE", 0.0) for v in kern.values())
 c3 = os.environ.get("PROF_SHAPE") == "config3"
 out = {
-    "pipeline": "faithful pass, six references (k_fa_local_fast, k_fa_local, k_fa_chunk, k_fa_finish)",
+    "pipeline": "faithful pass, six references (k_fa_local_lm or k_fa_local_fast, k_fa_local, k_fa_chunk, k_fa_finish)",
     "workload": ("GEMM N=4096, T=8, 2^28 samples (config 3 on one GPU)" if c3 else
                  "GEMM N=1024, T=8, 2^24 samples (config 2 budget)"),
     "samples_per_pass": 1 << 28 if c3 else 1 << 24,
