@@ -204,7 +204,7 @@ int pluss_ctx_destroy(pluss_ctx* c) {
       if (p) (void)hipFree(p);
   }
   {
-    void* ub[] = {c->ub.set, c->ub.cnt, c->ub.bits, c->ub.tmap, c->ub.pre, c->ub.rb, c->ub.bsum};
+    void* ub[] = {c->ub.set, c->ub.cnt, c->ub.bits, c->ub.tmap, c->ub.pre, c->ub.rb, c->ub.bsum, c->ub.pmt};
     for (void* p : ub)
       if (p) (void)hipFree(p);
   }

@@ -91,7 +91,8 @@ struct UniBufs {  // its device buffers (grown on demand, per handle)
   UniSet* set = nullptr;
   uint32_t *cnt = nullptr, *bits = nullptr, *tmap = nullptr;
   uint64_t *pre = nullptr, *rb = nullptr, *bsum = nullptr;
-  size_t set_cap = 0, cnt_cap = 0, bits_cap = 0, tmap_cap = 0, pre_cap = 0, rb_cap = 0, bsum_cap = 0;
+  double* pmt = nullptr;  // the binomial pmf per leaf size (uni_count_tab)
+  size_t set_cap = 0, cnt_cap = 0, bits_cap = 0, tmap_cap = 0, pre_cap = 0, rb_cap = 0, bsum_cap = 0, pmt_cap = 0;
 };
 
 struct FaShards;  // a key-range shard's state between the phases of pluss_dev_faithful_shards_* (pluss_faithful.h)

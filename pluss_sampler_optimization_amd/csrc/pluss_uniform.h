@@ -266,7 +266,34 @@ struct UniSet {
   const uint64_t* rb;   // exclusive prefix of the bitmap words' popcounts (woff[6] + 1 words)
   const uint32_t* tmap; // per tile: the leaf holding its first sample
   unsigned int* flags;  // the handle's flags (FLAG_UNI)
+  const double* pmt;    // per reference and leaf size class: pmf(0..UG_LEAFMAX + 1) of uni_count's recurrence
 };
+constexpr uint32_t UG_PMT = UG_LEAFMAX + 2;  // table entries per leaf size class (4 classes per reference)
+
+#if defined(__HIPCC__)
+// uni_count with the pmf recurrence read from the reference's table for the
+// leaf's size (the same doubles: the table is that recurrence, run once per
+// class by k_ug_pmt) -- the loop left is compare and subtract, no division
+__device__ __forceinline__ uint64_t uni_count_tab(const UniGen& u, uint64_t l, const double* __restrict__ pmt) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+  const UniLeaf f = uni_leaf(u, l);
+  if (u.p >= 1.0 || uni_direct(u, f)) return uni_count(u, l);
+  const double* t = pmt + ((f.blk ? 2 : 0) + (f.kw == u.K ? 0 : 1)) * UG_PMT;
+  double x_u = uni_u01(uni_hash(uni_leafkey(u, l, 0xFFFFFFFEu), 0));
+  uint64_t x = 0;
+  double pm = t[0];
+  while (x_u >= pm && x < f.G) {
+    x_u = x_u - pm;
+    ++x;
+    if (x > UG_LEAFMAX) return x;  // (flagged by the caller)
+    pm = t[x];
+    if (pm == 0.0) return UG_LEAFMAX + 1;  // past the table's reach (P < 1e-300): flagged
+  }
+  return x;
+}
+#endif
 
 #if defined(__HIPCC__)
 // candidates of reference r before leaf l / removed candidates of rank < x

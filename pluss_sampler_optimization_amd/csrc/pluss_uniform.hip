@@ -113,6 +113,42 @@ __device__ __forceinline__ uint32_t ug_ref_of(const uint64_t* off, uint64_t g) {
   return r;
 }
 
+// the pmf table of every reference's four leaf sizes: uni_count's recurrence
+// f(x+1) = f(x) (G-x)/(x+1) * p/(1-p) from f(0) = (1-p)^G, the same operations
+// in the same order (no contraction).  One wave per (reference, size class):
+// lane 0 runs the recurrence (sequential, a division per step) only as far as
+// the mean + 40 standard deviations + 64; the other entries are zeros, filled
+// by the whole wave (a leaf that reaches them, P < 1e-300, is flagged like any
+// leaf past UG_LEAFMAX).
+__global__ __launch_bounds__(64) void k_ug_pmt(const UniSet* __restrict__ us, double* __restrict__ pmt) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+  const uint32_t r = blockIdx.x >> 2, cls = blockIdx.x & 3u;
+  if (us->loff[r + 1] == us->loff[r]) return;
+  const UniGen& u = us->u[r];
+  if (u.p >= 1.0) return;
+  const uint64_t kl = u.W - (u.nb - 1) * u.K, tb = cls >= 2 ? (u.T > 1 ? u.T - 1 : 1) : u.T;
+  const uint64_t G = ((cls & 1u) ? kl : u.K) * tb;
+  const double mean = (double)G * u.p;
+  const double xmd = mean + 40.0 * sqrt(mean) + 64.0;
+  const uint64_t xm = xmd < (double)(UG_PMT - 1) ? (uint64_t)xmd : UG_PMT - 1;
+  double* t = pmt + (r * 4 + cls) * UG_PMT;
+  for (uint64_t x = xm + 1 + threadIdx.x; x < UG_PMT; x += 64) t[x] = 0.0;
+  if (threadIdx.x == 0) {
+    double pm = cls == 0 ? u.pm[0] : cls == 1 ? u.pm[1] : cls == 2 ? u.pm[2] : u.pm[3];
+    t[0] = pm;
+    for (uint64_t x = 0; x < xm; ++x) {
+      if (x < G) {
+        pm = pm * (double)(G - x);
+        pm = pm / (double)(x + 1);
+        pm = pm * u.r;
+      }
+      t[x + 1] = pm;
+    }
+  }
+}
+
 // (references outermost: the generator's fields are wave-uniform, scalar loads)
 __global__ __launch_bounds__(UB) void k_ug_count(const UniSet* __restrict__ us, uint32_t* __restrict__ cnt,
                                                 unsigned int* flags) {
@@ -121,8 +157,9 @@ __global__ __launch_bounds__(UB) void k_ug_count(const UniSet* __restrict__ us, 
     const uint64_t g0 = us->loff[r], n = us->loff[r + 1] - g0;
     if (!n) continue;
     const UniGen& u = us->u[r];  // (wave-uniform: scalar loads; a by-value copy went to scratch)
+    const double* pmt = us->pmt + r * 4 * UG_PMT;
     for (uint64_t l = (uint64_t)blockIdx.x * UB + threadIdx.x; l < n; l += stride) {
-      const uint64_t c = uni_count(u, l);
+      const uint64_t c = uni_count_tab(u, l, pmt);
       if (c > UG_LEAFMAX) atomicOr(flags, FLAG_UNI);
       cnt[g0 + l] = c > UG_LEAFMAX ? UG_LEAFMAX + 1 : (uint32_t)c;
     }
@@ -248,6 +285,7 @@ int uni_plan(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t 
   if (!rc) rc = ug_grow((void**)&b.bits, &b.bits_cap, (Wd + 1) * 4);
   if (!rc) rc = ug_grow((void**)&b.rb, &b.rb_cap, (Wd + 1) * 8);
   if (!rc) rc = ug_grow((void**)&b.tmap, &b.tmap_cap, (Tt + 1) * 4);
+  if (!rc) rc = ug_grow((void**)&b.pmt, &b.pmt_cap, 6 * 4 * UG_PMT * sizeof(double));
   if (!rc) rc = ug_grow((void**)&b.bsum, &b.bsum_cap, (nbL > nbW ? nbL : nbW) * 8 + 8);
   if (rc) return rc;
   h.cnt = b.cnt;
@@ -255,10 +293,12 @@ int uni_plan(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t 
   h.bits = b.bits;
   h.rb = b.rb;
   h.tmap = b.tmap;
+  h.pmt = b.pmt;
   h.flags = ctx->g.flags;
   // the plan's parameters travel as a kernel argument (ordered on the stream, no host buffer to keep)
   hipLaunchKernelGGL(k_ug_setup, dim3(1), dim3(1), 0, s, h, b.set);
   const int grid = (int)std::min<uint64_t>((L + UB - 1) / UB + 1, 4096);
+  hipLaunchKernelGGL(k_ug_pmt, dim3(24), dim3(64), 0, s, (const UniSet*)b.set, b.pmt);
   hipLaunchKernelGGL(k_ug_count, dim3(grid), dim3(UB), 0, s, (const UniSet*)b.set, b.cnt, ctx->g.flags);
   if (int e = ug_scan(b.cnt, L, b.bsum, b.pre, 0, s)) return e;
   PLUSS_HIP_CHECK(hipMemsetAsync(b.bits, 0, (Wd + 1) * 4, s));
