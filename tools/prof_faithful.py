@@ -1,7 +1,9 @@
 """Minimal driver for rocprofv3 passes over the faithful (r10 queue semantics)
 pipeline: config 2's budget (N=1024, T=8, 2^24 samples, six references in one
-pass).  PROF_FAITH=sorted (key-order list in HBM, read once) or generated (the
-same lists generated inside the pass); PROF_REPS passes."""
+pass).  PROF_FAITH=sorted (key-order list in HBM, read once), generated (the
+same lists generated inside the pass), radix (Feistel lists in any order,
+sorted inside the pass) or uniform (r10's draw generated in key order inside
+the pass); PROF_REPS passes."""
 import os
 import sys
 
@@ -24,12 +26,19 @@ buf = torch.empty(total, dtype=torch.int64, device=dev)
 ctx = P.Context(cfg)
 off = 0
 for r, c in enumerate(counts):
-    ctx.expand_sorted(SEED, r, c, 0, c, buf.data_ptr() + 8 * off, sp)
+    if mode == "radix":  # the Feistel lists (any order), sorted inside the pass
+        ctx.expand(SEED, r, 0, c, buf.data_ptr() + 8 * off, sp)
+    else:
+        ctx.expand_sorted(SEED, r, c, 0, c, buf.data_ptr() + 8 * off, sp)
     off += c
 for _ in range(int(os.environ.get("PROF_REPS", 5))):
     ctx.reset(sp)
     if mode == "sorted":
         ctx.faithful_hist_sorted_refs(buf.data_ptr(), counts, sp)
+    elif mode == "radix":
+        ctx.faithful_hist_refs(buf.data_ptr(), counts, sp)
+    elif mode == "uniform":
+        ctx.gen_uniform_faithful_refs(SEED, counts, sp)
     else:
         ctx.gen_faithful_refs(SEED, counts, sp)
 torch.cuda.synchronize()
