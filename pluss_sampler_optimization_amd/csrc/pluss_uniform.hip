@@ -68,15 +68,28 @@ __global__ __launch_bounds__(UB) void k_ug_btop(uint64_t* __restrict__ bsum, uin
   if (threadIdx.x == 0) bsum[nb] = carry;
 }
 
-// out[i] = exclusive prefix of the values (out[n] = the total)
+// out[i] = exclusive prefix of the values (out[n] = the total).  The block's
+// values go through LDS both ways: read and written coalesced (a thread's own
+// run of UE consecutive values read straight from memory was a 64-byte
+// stride per lane, ~2 TB/s), scanned as runs of UE per thread.
+__device__ __forceinline__ uint32_t ug_pad(uint32_t i) { return i + (i >> 4); }  // (runs of 16: conflict-free)
 template <int MODE>
 __global__ __launch_bounds__(UB) void k_ug_bapply(const uint32_t* __restrict__ in, uint64_t n,
                                                  const uint64_t* __restrict__ bsum, uint64_t* __restrict__ out) {
   __shared__ uint64_t w[UB / 64];
-  const uint64_t b0 = (uint64_t)blockIdx.x * UBATCH + (uint64_t)threadIdx.x * UE;  // a run of UE values per thread
-  uint64_t v[UE], s = 0;
+  __shared__ uint64_t sv[UBATCH + UBATCH / 16];
+  const uint64_t b0 = (uint64_t)blockIdx.x * UBATCH;
+#pragma unroll
   for (uint32_t k = 0; k < UE; ++k) {
-    v[k] = b0 + k < n ? ug_val<MODE>(in, b0 + k) : 0ull;
+    const uint32_t i = k * UB + threadIdx.x;
+    sv[ug_pad(i)] = b0 + i < n ? ug_val<MODE>(in, b0 + i) : 0ull;
+  }
+  __syncthreads();
+  const uint32_t j0 = threadIdx.x * UE;
+  uint64_t v[UE], s = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < UE; ++k) {
+    v[k] = sv[ug_pad(j0 + k)];
     s += v[k];
   }
   const uint64_t inc = sc_wave_scan<false>(s, __lane_id());
@@ -85,9 +98,16 @@ __global__ __launch_bounds__(UB) void k_ug_bapply(const uint32_t* __restrict__ i
   uint64_t pre = bsum[blockIdx.x];
   for (uint32_t x = 0; x < (threadIdx.x >> 6); ++x) pre += w[x];
   uint64_t run = pre + inc - s;
+#pragma unroll
   for (uint32_t k = 0; k < UE; ++k) {
-    if (b0 + k < n) out[b0 + k] = run;
+    sv[ug_pad(j0 + k)] = run;
     run += v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < UE; ++k) {
+    const uint32_t i = k * UB + threadIdx.x;
+    if (b0 + i < n) out[b0 + i] = sv[ug_pad(i)];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = bsum[gridDim.x];
 }
