@@ -446,6 +446,12 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
     // candidate i of the leaf (in key order) has rank x0 + i; the removed ones are skipped
     const uint32_t w0i = (uint32_t)((x0 >> 5) - wlo);
     uint64_t rem = rem0 + rbw[w0i] + (uint64_t)__popc(bw[w0i] & ((1u << (x0 & 31)) - 1u));  // removed before x0
+    // the packed sample's fixed bits for this leaf (block A, T and CS powers of
+    // two: every BASELINE shape): offset o adds t = o % T to c0 and w = o / T
+    // to c2 (3-D) or c1 (2-D); other leaves take uni_pack_row
+    const bool fastp = !f.blk && u.tp2 && u.csp2;
+    const uint32_t c0b = ((rd.q >> u.cssh) << (u.tsh + u.cssh)) | (rd.q & (u.CS - 1));
+    const uint64_t pkb = pack(u.ref, c0b, u.dim3 ? rd.c1 : 0u, u.dim3 ? rd.w0 : 0u);
     auto emit = [&](uint32_t i, uint32_t o) {
       const uint64_t x = x0 + i;
       if ((bw[(uint32_t)((x >> 5) - wlo)] >> (x & 31)) & 1u) {
@@ -453,7 +459,17 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
         return;
       }
       const uint64_t e = x - rem - f0;
-      if (e < mt) raw[slot((uint32_t)e)] = uni_pack_row(u, f, rd, o);
+      if (e < mt) {
+        uint64_t pk;
+        if (fastp) {
+          const uint32_t wq = o >> u.tsh, t = o & (u.T - 1);
+          pk = pkb | ((uint64_t)t << (40 + u.cssh));
+          pk = u.dim3 ? pk + wq : pk | ((uint64_t)(rd.w0 + wq) << 20);  // (c2 = w0 + wq < 2^20)
+        } else {
+          pk = uni_pack_row(u, f, rd, o);
+        }
+        raw[slot((uint32_t)e)] = pk;
+      }
     };
     if (u.p >= 1.0) {
       for (uint32_t j = 0; j < c; ++j) emit(j, j);
