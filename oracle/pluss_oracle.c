@@ -624,7 +624,7 @@ int orc_expand_sorted(const orc_cfg *c, uint64_t seed, int ref, uint64_t S, uint
    blocks per row of K = ceil(span / nb) w-values (K*T < 2^32); a
    leaf's candidate count is Binomial(G, p) by inversion of one hash draw
    (or one Bernoulli draw per point in leaves of <= 64 points, more than 64
-   expected candidates or p > 1/64), its candidates independent uniform offsets sorted and
+   expected candidates or p > 1/64), its candidates independent uniform offsets (two 32-bit ones per 64-bit hash in leaves of <= 2^16 points) sorted and
    redrawn on a duplicate; of the T' candidates the ranks F(0..T'-S-1) of a
    keyed Feistel permutation of [0, T') are removed.  Samples [first, first+n)
    of the survivors in key order.  Returns -3 if T' < S (probability ~1e-23),
@@ -739,8 +739,14 @@ int orc_expand_uniform(const orc_cfg *c, uint64_t seed, int ref, uint64_t S, uin
             for (uint32_t a = 0;; a++) {
                 if (a == 4096) { rc = -4; break; }
                 const uint64_t lk = u_leafkey(base, l, a);
-                for (uint64_t i = 0; i < cl; i++)
-                    off[i] = (uint64_t)(((unsigned __int128)u_hash(lk, i) * G) >> 64);
+                for (uint64_t i = 0; i < cl; i++) {
+                    if (G <= 65536) { /* two 32-bit offsets per hash */
+                        const uint64_t h = u_hash(lk, i >> 1);
+                        off[i] = ((uint64_t)(uint32_t)((i & 1) ? h >> 32 : h) * G) >> 32;
+                    } else {
+                        off[i] = (uint64_t)(((unsigned __int128)u_hash(lk, i) * G) >> 64);
+                    }
+                }
                 qsort(off, cl, sizeof(uint64_t), u_cmp64);
                 int dup = 0;
                 for (uint64_t i = 1; i < cl; i++) dup |= off[i] == off[i - 1];

@@ -186,8 +186,18 @@ PM_HD uint64_t uni_count(const UniGen& u, uint64_t l) {
   return x;
 }
 
-// candidate offset i (attempt a) of a counted leaf: uniform in [0, G)
-PM_HD uint64_t uni_offset(uint64_t lk, uint64_t i, uint64_t G) { return mulhi64(uni_hash(lk, i), G); }
+// candidate offset i (attempt a) of a counted leaf: uniform in [0, G).  Leaves
+// of at most UG_PAIRG points take two offsets from one 64-bit hash, 32 bits
+// each (a relative bias below G / 2^32 <= 1.6e-5); larger ones one per hash.
+constexpr uint64_t UG_PAIRG = 1ull << 16;
+PM_HD uint64_t uni_offset(uint64_t lk, uint64_t i, uint64_t G) {
+  if (G <= UG_PAIRG) {
+    const uint64_t h = uni_hash(lk, i >> 1);
+    const uint32_t half = (i & 1) ? (uint32_t)(h >> 32) : (uint32_t)h;
+    return ((uint64_t)half * G) >> 32;
+  }
+  return mulhi64(uni_hash(lk, i), G);
+}
 
 // ---- the removal permutation: a keyed cycle-walking Feistel permutation of
 // the candidate ranks [0, Tp); its first Tp - S outputs are removed
@@ -369,8 +379,12 @@ __device__ __forceinline__ uint64_t uni_pack_row(const UniGen& u, const UniLeaf&
   return uni_pack(u, d);
 }
 
-// uni_offset for G < 2^32, in 32-bit pieces: floor(h * G / 2^64)
+// uni_offset for G < 2^32, in 32-bit pieces (floor(h * G / 2^64) for the large leaves)
 __device__ __forceinline__ uint32_t uni_offset32(uint64_t lk, uint32_t i, uint32_t G) {
+  if (G <= UG_PAIRG) {
+    const uint64_t h = uni_hash(lk, i >> 1);
+    return __umulhi((i & 1) ? (uint32_t)(h >> 32) : (uint32_t)h, G);
+  }
   const uint64_t h = uni_hash(lk, i);
   const uint64_t t = (uint64_t)(uint32_t)(h >> 32) * G + __umulhi((uint32_t)h, G);
   return (uint32_t)(t >> 32);
@@ -489,8 +503,20 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
           break;
         }
         const uint64_t lk = uni_leafkey(u, l, a);
+        if (G <= UG_PAIRG) {  // two offsets per hash; slots past every lane's count skipped
 #pragma unroll
-        for (uint32_t q = 0; q < UG_NET; ++q) v[q] = q < c ? uni_offset32(lk, q, G) : 0xFFFFFFFFu;
+          for (uint32_t q = 0; q < UG_NET; q += 2) {
+            v[q] = v[q + 1] = 0xFFFFFFFFu;
+            if (__any(q < c)) {
+              const uint64_t h = uni_hash(lk, q >> 1);
+              if (q < c) v[q] = __umulhi((uint32_t)h, G);
+              if (q + 1 < c) v[q + 1] = __umulhi((uint32_t)(h >> 32), G);
+            }
+          }
+        } else {
+#pragma unroll
+          for (uint32_t q = 0; q < UG_NET; ++q) v[q] = q < c ? uni_offset32(lk, q, G) : 0xFFFFFFFFu;
+        }
         uni_sort_net<UG_NET>(v);
         bool dup = false;  // (offsets < G <= 2^32 - 1: the padding sorts last and never matches)
 #pragma unroll
