@@ -389,23 +389,23 @@ __device__ __forceinline__ uint32_t uni_offset32(uint64_t lk, uint32_t i, uint32
   const uint64_t t = (uint64_t)(uint32_t)(h >> 32) * G + __umulhi((uint32_t)h, G);
   return (uint32_t)(t >> 32);
 }
-// ascending bitonic sort of NC (a power of two) values in registers
+// ascending sort of NC (a power of two) values in registers: Batcher's
+// odd-even merge sort (191 compare-exchanges for 32, a bitonic network 240)
 template <int NC>
 __device__ __forceinline__ void uni_sort_net(uint32_t (&v)[NC]) {
 #pragma unroll
-  for (int k = 2; k <= NC; k <<= 1)
+  for (int p = 1; p < NC; p <<= 1)
 #pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1)
+    for (int k = p; k >= 1; k >>= 1)
 #pragma unroll
-      for (int i = 0; i < NC; ++i) {
-        const int l = i ^ j;
-        if (l > i) {
-          const uint32_t a = v[i], b = v[l], lo = a < b ? a : b, hi = a < b ? b : a;
-          const bool up = (i & k) == 0;
-          v[i] = up ? lo : hi;
-          v[l] = up ? hi : lo;
-        }
-      }
+      for (int j = k % p; j + k < NC; j += 2 * k)
+#pragma unroll
+        for (int i = 0; i < k && i + j + k < NC; ++i)
+          if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+            const uint32_t a = v[i + j], b = v[i + j + k];
+            v[i + j] = a < b ? a : b;
+            v[i + j + k] = a < b ? b : a;
+          }
 }
 constexpr uint32_t UG_NET = 32;  // leaves of at most this many candidates: sorted in registers
 
