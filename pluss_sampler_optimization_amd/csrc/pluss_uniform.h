@@ -329,7 +329,7 @@ __device__ __forceinline__ uint64_t uni_removed_before(const UniSet* __restrict_
 // coalesced), then each thread draws one leaf's candidates in key order and
 // packs every surviving one at its sample index:
 //   per-point draws (small or dense leaves) come out in order;
-//   up to UG_NET offsets are sorted in registers (a bitonic network);
+//   up to UG_NET offsets are sorted in registers (an odd-even merge network);
 //   larger leaves (rare) are insertion-sorted in a shared LDS scratch of
 //   UG_SCR words, or, when the tile's large leaves overflow it, emitted by
 //   repeated minimum search over their offsets (no scratch; O(c^2)).
