@@ -86,6 +86,21 @@ def test_array_path_equals_dict_path(name, d, smp):
     assert list(a["key"]) == sorted(H.aet(reuse)) and (np.diff(a["key"]) > 0).all()
 
 
+def test_format_mrc_any_key_order():
+    """pluss_format_mrc takes the points in key order without a map (pluss_aet's
+    output); points out of order or repeated go through the ordered map, last
+    value winning, as before."""
+    import numpy as np
+    pts = {c: max(0.0, 1.0 - c / 50.0) for c in range(0, 120)}
+    want = H.format_mrc(pts)
+    a = np.zeros(len(pts), H._KV)
+    a["key"] = list(pts.keys())[::-1]
+    a["value"] = list(pts.values())[::-1]
+    arr = (H.PlussKV * len(a)).from_buffer(a)  # reversed: the map path
+    assert H._text(H.host_lib().pluss_format_mrc, arr, len(a)) == want
+    assert H.format_mrc(H.aet({1: 5.0, 4: 3.0, -1: 2.0})) == H.format_mrc(dict(H.aet({1: 5.0, 4: 3.0, -1: 2.0})))
+
+
 def test_aet_edge_cases():
     assert H.aet({}) == {0: 1.0}  # pluss_AET: P[0] = 1 and c = 0 is always emitted
     m = H.aet({-1: 10.0})
