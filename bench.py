@@ -588,7 +588,7 @@ def capi_group_bench(P, torch, dist, cfg, counts, total, world, rank, backend, s
             out = run(g, "1 device x 1 shard")
         with P.Group(cfg, [cfg.device], 8) as g:
             out["logical_shards_8"] = run(g, "1 device x 8 logical shards (rehearsal)")
-        out["faithful"] = capi_group_faithful(P, cfg)
+        out["faithful"], out["faithful_uniform"] = capi_group_faithful(P, cfg)
     out["note"] = ("host clock around pluss_group_dense(K) (K passes, each a count launch per shard, the per-device "
                    "sum and one RCCL all-reduce, until the merged vector is back on the host)")
     return out
@@ -603,20 +603,28 @@ def capi_group_faithful(P, cfg, reps=3):
     median of `reps`; every shard count's histogram equals the one-shard one."""
     fcfg = P.SamplerConfig(n=4096, threads=cfg.threads, chunk=cfg.chunk, mode="faithful", device=cfg.device)
     totals = P.default_counts(4096, 1 << 28)
-    out, ref = {}, None
-    for spd in (1, 2, 8):
-        with P.Group(fcfg, [cfg.device], spd) as g:
-            h = g.gen_faithful(SEED, totals)
-            ts = []
-            for _ in range(reps):
-                t0 = time.perf_counter()
-                h = g.gen_faithful(SEED, totals)
-                ts.append(time.perf_counter() - t0)
-        ts.sort()
-        ref = ref or h
-        out[f"shards_{spd}"] = {"ms": ts[len(ts) // 2] * 1e3, "equals_one_shard": h == ref}
+
+    def leg(call):
+        out, ref = {}, None
+        for spd in (1, 2, 8):
+            with P.Group(fcfg, [cfg.device], spd) as g:
+                h = call(g)
+                ts = []
+                for _ in range(reps):
+                    t0 = time.perf_counter()
+                    h = call(g)
+                    ts.append(time.perf_counter() - t0)
+            ts.sort()
+            ref = ref or h
+            out[f"shards_{spd}"] = {"ms": ts[len(ts) // 2] * 1e3, "equals_one_shard": h == ref and
+                                    h.traversed == ref.traversed}
+        return out
+    out = leg(lambda g: g.gen_faithful(SEED, totals))
     out["workload"] = "GEMM N=4096, T=8, 2^28 samples (config 3), faithful, generated key-order lists, one device"
-    return out
+    uni = leg(lambda g: g.gen_uniform_faithful(SEED, totals))
+    uni["workload"] = ("the same over r10's own law (pluss_group_gen_uniform_faithful: uniform draws without "
+                       "replacement in key order, each shard generating only its stretch of every list)")
+    return out, uni
 
 
 def pmc_traffic(samples_per_launch):

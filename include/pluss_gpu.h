@@ -118,8 +118,13 @@ int pluss_expand_uniform_sorted(const pluss_cfg *cfg, uint64_t seed, int32_t ref
                                 uint64_t n, uint64_t *out);
 
 /* --- handle API: device-resident inputs, explicit streams ----------------
-   `stream` is a hipStream_t (NULL = the handle's own stream).  Device
-   pointers are plain addresses of device memory on cfg->device.           */
+   `stream` is a hipStream_t, taken as every HIP API takes it: NULL is HIP's
+   null stream, ordered with the caller's own null-stream work (copies,
+   memsets, kernels).  The handle also owns a non-blocking stream,
+   pluss_ctx_stream(), which a caller passes explicitly to run unordered with
+   the null stream.  pluss_hist_fetch orders after the stream of the last
+   call.  Device pointers are plain addresses of device memory on
+   cfg->device.                                                             */
 int pluss_ctx_create(const pluss_cfg *cfg, pluss_ctx **out);
 int pluss_ctx_destroy(pluss_ctx *ctx);
 void *pluss_ctx_stream(pluss_ctx *ctx);
@@ -252,6 +257,29 @@ int pluss_dev_faithful_shards_cut(pluss_ctx *ctx, const uint64_t *d_rows, int32_
 int pluss_dev_faithful_shards_hist(pluss_ctx *ctx, const uint64_t *d_rows, int32_t shard, int32_t nshards,
                                    void *stream);
 
+/* r10's own law over key-range shards: the lists of pluss_expand_uniform_sorted
+   (uniform draws without replacement, r10:156-185, in key order), each shard
+   generating only its stretch of every list.  Shard g of G holds, per
+   reference, the leaves [L*g/G, L*(g+1)/G) of the key-ordered space (a leaf:
+   one key row's block of points), so its samples are contiguous
+   in key order.  Its first phase is split in two around one extra all-gather:
+     0. pluss_dev_faithful_shards_uniform_count: this shard's candidates per
+        reference (row[ROW_N + r], the words [0,6)); all-gather the rows;
+     1. pluss_dev_faithful_shards_uniform_local: from the gathered rows, the
+        candidates before this shard and in all, the removal of its window, so
+        its slice [first, first + n) of each list (read back once: the launch
+        grids need n), then the local pass over that slice, generated tile by
+        tile (its row as phase 1 of the other sources);
+   then carry, cut and hist as above.  The result equals
+   pluss_dev_gen_uniform_faithful_refs on one device. */
+int pluss_dev_faithful_shards_uniform_count(pluss_ctx *ctx, uint64_t seed, const uint64_t *totals, int32_t shard,
+                                            int32_t nshards, uint64_t *d_row, void *stream);
+int pluss_dev_faithful_shards_uniform_local(pluss_ctx *ctx, const uint64_t *d_rows, int32_t shard, int32_t nshards,
+                                            uint64_t *d_row, void *stream);
+/* the slice of each reference's list this handle's last key-range pass ran
+   over (after its local phase): indices [first[r], first[r] + n[r]) */
+int pluss_dev_faithful_shards_slice(pluss_ctx *ctx, uint64_t first[6], uint64_t n[6]);
+
 /* Host only (no device): [*i_lo, *i_hi) = the indices of the samples of the
    key-order list of `total` samples of reference `ref` (pluss_expand_sorted's
    list) whose faithful keys lie in [key_lo, key_hi) -- the list is in key
@@ -267,10 +295,13 @@ int pluss_keyorder_index_range(const pluss_cfg *cfg, uint64_t seed, int32_t ref,
    group is a set of shards: shards_per_device >= 1 logical shards on each
    device (e.g. 8 on one device reproduce an 8-GPU job's partition and
    exchanges).  The exchanges are RCCL collectives over the
-   devices (loaded on first use): one all-reduce of the dense vector per
-   clean pass, one all-gather of the shards' summary rows between the phases
-   of a faithful pass (no host round trip), one all-gather of the canonical
-   tables at the end.  Clean mode shards every reference's sample index range
+   devices (loaded on first use): one all-gather of the shards' summary rows
+   between the phases of a faithful pass (no host round trip), and at the end
+   of every pass one all-reduce of the shards' dense result vectors (bins,
+   cold and traversed counts, one word per failure condition; shapes with
+   N % (cls/ds) != 0: one all-gather of the shards' canonical tables).  A
+   shard that fails on its host still takes part in every collective with its
+   error word set, and every rank returns PLUSS_ERR_PEER (or its own error).  Clean mode shards every reference's sample index range
    (or a host list) into contiguous slices; faithful mode shards the sort key
    a*T+tid into contiguous ranges.  Results equal one device's and are the
    same on every rank.
@@ -286,6 +317,9 @@ int pluss_keyorder_index_range(const pluss_cfg *cfg, uint64_t seed, int32_t ref,
      pluss_group_gen_faithful the six samplers over generated key-order lists
                               (pluss_expand_sorted's), each shard generating
                               only its key range
+     pluss_group_gen_uniform_faithful  the same over r10's own law
+                              (pluss_expand_uniform_sorted's lists; equal to
+                              pluss_dev_gen_uniform_faithful_refs on one device)
      pluss_group_expand       resident Feistel lists, each shard its slices of
                               counts[r] samples per reference (pluss_expand_samples)
      pluss_group_dense        `passes` dense passes over them (the bench step;
@@ -304,6 +338,7 @@ int pluss_group_destroy(pluss_group *group);
 int pluss_group_shards(const pluss_group *group, int32_t *local_shards, int32_t *total_shards);
 int pluss_group_sampled_hist(pluss_group *group, const uint64_t *samples, uint64_t n, pluss_hist *out);
 int pluss_group_gen_faithful(pluss_group *group, uint64_t seed, const uint64_t totals[6], pluss_hist *out);
+int pluss_group_gen_uniform_faithful(pluss_group *group, uint64_t seed, const uint64_t totals[6], pluss_hist *out);
 int pluss_group_expand(pluss_group *group, uint64_t seed, const uint64_t counts[6]);
 int pluss_group_dense(pluss_group *group, uint32_t passes, uint64_t counts[PLUSS_DENSE_BINS + 1]);
 int pluss_group_gen_count_dense(pluss_group *group, uint64_t seed, const uint64_t totals[6],

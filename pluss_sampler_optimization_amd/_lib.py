@@ -33,8 +33,11 @@ EXPORTS = [
     "pluss_dense_keys", "pluss_dev_sampled_hist_dense", "pluss_dev_gen_count_dense",
     "pluss_dev_faithful_shards_local", "pluss_dev_faithful_shards_select", "pluss_dev_faithful_shards_local_selected",
     "pluss_dev_faithful_shards_carry", "pluss_dev_faithful_shards_cut", "pluss_dev_faithful_shards_hist",
+    "pluss_dev_faithful_shards_uniform_count", "pluss_dev_faithful_shards_uniform_local",
+    "pluss_dev_faithful_shards_slice",
     "pluss_group_unique_id", "pluss_group_create", "pluss_group_create_rank", "pluss_group_destroy",
-    "pluss_group_shards", "pluss_group_sampled_hist", "pluss_group_gen_faithful", "pluss_group_expand",
+    "pluss_group_shards", "pluss_group_sampled_hist", "pluss_group_gen_faithful",
+    "pluss_group_gen_uniform_faithful", "pluss_group_expand",
     "pluss_group_dense", "pluss_group_gen_count_dense",
 ]
 # include/pluss_diag.h (diagnostics, not the drop-in boundary)
@@ -131,6 +134,9 @@ def lib():
         "pluss_dev_faithful_shards_carry": (ctypes.c_int, [vp, vp, i32, i32, vp, vp]),
         "pluss_dev_faithful_shards_cut": (ctypes.c_int, [vp, vp, i32, i32, vp, vp]),
         "pluss_dev_faithful_shards_hist": (ctypes.c_int, [vp, vp, i32, i32, vp]),
+        "pluss_dev_faithful_shards_uniform_count": (ctypes.c_int, [vp, u64, P(u64), i32, i32, vp, vp]),
+        "pluss_dev_faithful_shards_uniform_local": (ctypes.c_int, [vp, vp, i32, i32, vp, vp]),
+        "pluss_dev_faithful_shards_slice": (ctypes.c_int, [vp, P(u64), P(u64)]),
         "pluss_group_unique_id": (ctypes.c_int, [vp]),
         "pluss_group_create": (ctypes.c_int, [cfgp, P(i32), i32, i32, P(vp)]),
         "pluss_group_create_rank": (ctypes.c_int, [cfgp, i32, i32, vp, i32, P(vp)]),
@@ -138,6 +144,7 @@ def lib():
         "pluss_group_shards": (ctypes.c_int, [vp, P(i32), P(i32)]),
         "pluss_group_sampled_hist": (ctypes.c_int, [vp, vp, u64, histp]),
         "pluss_group_gen_faithful": (ctypes.c_int, [vp, u64, P(u64), histp]),
+        "pluss_group_gen_uniform_faithful": (ctypes.c_int, [vp, u64, P(u64), histp]),
         "pluss_group_expand": (ctypes.c_int, [vp, u64, P(u64)]),
         "pluss_group_dense": (ctypes.c_int, [vp, ctypes.c_uint32, P(u64)]),
         "pluss_group_gen_count_dense": (ctypes.c_int, [vp, u64, P(u64), P(u64)]),

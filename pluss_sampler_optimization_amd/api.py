@@ -273,6 +273,11 @@ class Context:
     def stream(self):
         return lib().pluss_ctx_stream(self._h)
 
+    def _s(self, stream):
+        """stream=None: the handle's own stream (the C ABI takes NULL as HIP's
+        null stream, include/pluss_gpu.h)."""
+        return self.stream if stream is None else stream
+
     def close(self):
         if self._h:
             lib().pluss_ctx_destroy(self._h)
@@ -291,90 +296,90 @@ class Context:
             pass
 
     def reset(self, stream=None):
-        check(lib().pluss_dev_hist_reset(self._h, stream), "pluss_dev_hist_reset")
+        check(lib().pluss_dev_hist_reset(self._h, self._s(stream)), "pluss_dev_hist_reset")
 
     def expand(self, seed, ref, first, n, d_out, stream=None):
         rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
-        check(lib().pluss_dev_expand(self._h, seed, rid, first, n, d_out, stream), "pluss_dev_expand")
+        check(lib().pluss_dev_expand(self._h, seed, rid, first, n, d_out, self._s(stream)), "pluss_dev_expand")
 
     def expand_sorted(self, seed, ref, total, first, n, d_out, stream=None):
         rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
-        check(lib().pluss_dev_expand_sorted(self._h, seed, rid, total, first, n, d_out, stream),
+        check(lib().pluss_dev_expand_sorted(self._h, seed, rid, total, first, n, d_out, self._s(stream)),
               "pluss_dev_expand_sorted")
 
     def expand_uniform_sorted(self, seed, ref, total, first, n, d_out, stream=None):
         rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
-        check(lib().pluss_dev_expand_uniform_sorted(self._h, seed, rid, total, first, n, d_out, stream),
+        check(lib().pluss_dev_expand_uniform_sorted(self._h, seed, rid, total, first, n, d_out, self._s(stream)),
               "pluss_dev_expand_uniform_sorted")
 
     def gen_uniform_faithful_refs(self, seed, totals, stream=None):
         """The six samplers over r10's uniform draw generated in key order inside the pass."""
         c = (ctypes.c_uint64 * 6)(*[int(x) for x in totals])
-        check(lib().pluss_dev_gen_uniform_faithful_refs(self._h, seed, c, stream), "pluss_dev_gen_uniform_faithful_refs")
+        check(lib().pluss_dev_gen_uniform_faithful_refs(self._h, seed, c, self._s(stream)), "pluss_dev_gen_uniform_faithful_refs")
 
     def sampled_hist(self, d_samples, n, stream=None):
-        check(lib().pluss_dev_sampled_hist(self._h, d_samples, n, stream), "pluss_dev_sampled_hist")
+        check(lib().pluss_dev_sampled_hist(self._h, d_samples, n, self._s(stream)), "pluss_dev_sampled_hist")
 
     def faithful_hist(self, ref, d_samples, n, stream=None):
         rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
-        check(lib().pluss_dev_faithful_hist(self._h, rid, d_samples, n, stream), "pluss_dev_faithful_hist")
+        check(lib().pluss_dev_faithful_hist(self._h, rid, d_samples, n, self._s(stream)), "pluss_dev_faithful_hist")
 
     def faithful_hist_refs(self, d_samples, counts, stream=None):
         """All six sampler_<REF> at once (r10's main: one thread per reference):
         d_samples holds counts[0] samples of reference 0, then counts[1] of
         reference 1, ...  Same result as six faithful_hist calls."""
         c = (ctypes.c_uint64 * 6)(*[int(x) for x in counts])
-        check(lib().pluss_dev_faithful_hist_refs(self._h, d_samples, c, stream), "pluss_dev_faithful_hist_refs")
+        check(lib().pluss_dev_faithful_hist_refs(self._h, d_samples, c, self._s(stream)), "pluss_dev_faithful_hist_refs")
 
     def faithful_hist_sorted(self, ref, d_samples, n, stream=None):
         """faithful_hist over a list already in key order (no sort; checked)."""
         rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
-        check(lib().pluss_dev_faithful_hist_sorted(self._h, rid, d_samples, n, stream), "pluss_dev_faithful_hist_sorted")
+        check(lib().pluss_dev_faithful_hist_sorted(self._h, rid, d_samples, n, self._s(stream)), "pluss_dev_faithful_hist_sorted")
 
     def faithful_hist_sorted_refs(self, d_samples, counts, stream=None):
         c = (ctypes.c_uint64 * 6)(*[int(x) for x in counts])
-        check(lib().pluss_dev_faithful_hist_sorted_refs(self._h, d_samples, c, stream),
+        check(lib().pluss_dev_faithful_hist_sorted_refs(self._h, d_samples, c, self._s(stream)),
               "pluss_dev_faithful_hist_sorted_refs")
 
     def gen_faithful_refs(self, seed, totals, stream=None):
         """The six samplers over generated key-order lists (never materialised)."""
         c = (ctypes.c_uint64 * 6)(*[int(x) for x in totals])
-        check(lib().pluss_dev_gen_faithful_refs(self._h, seed, c, stream), "pluss_dev_gen_faithful_refs")
+        check(lib().pluss_dev_gen_faithful_refs(self._h, seed, c, self._s(stream)), "pluss_dev_gen_faithful_refs")
 
     def fulltrace(self, stream=None):
-        check(lib().pluss_dev_fulltrace_hist(self._h, stream), "pluss_dev_fulltrace_hist")
+        check(lib().pluss_dev_fulltrace_hist(self._h, self._s(stream)), "pluss_dev_fulltrace_hist")
 
     def sampled_ri(self, d_samples, n, d_ri, d_sink, stream=None):
-        check(lib().pluss_dev_sampled_ri(self._h, d_samples, n, d_ri, d_sink, stream), "pluss_dev_sampled_ri")
+        check(lib().pluss_dev_sampled_ri(self._h, d_samples, n, d_ri, d_sink, self._s(stream)), "pluss_dev_sampled_ri")
 
     def export(self, d_keys, d_counts, cap, stream=None):
-        check(lib().pluss_dev_hist_export(self._h, d_keys, d_counts, cap, stream), "pluss_dev_hist_export")
+        check(lib().pluss_dev_hist_export(self._h, d_keys, d_counts, cap, self._s(stream)), "pluss_dev_hist_export")
 
     def export_reset(self, d_keys, d_counts, cap, stream=None):
         """export(), then leave the histogram empty for the next pass (one launch)."""
-        check(lib().pluss_dev_hist_export_reset(self._h, d_keys, d_counts, cap, stream), "pluss_dev_hist_export_reset")
+        check(lib().pluss_dev_hist_export_reset(self._h, d_keys, d_counts, cap, self._s(stream)), "pluss_dev_hist_export_reset")
 
     def sampled_hist_export(self, d_samples, n, d_keys, d_counts, cap, stream=None):
         """sampled_hist() then export_reset() -- one launch for N % (CLS/DS) == 0 shapes."""
-        check(lib().pluss_dev_sampled_hist_export(self._h, d_samples, n, d_keys, d_counts, cap, stream),
+        check(lib().pluss_dev_sampled_hist_export(self._h, d_samples, n, d_keys, d_counts, cap, self._s(stream)),
               "pluss_dev_sampled_hist_export")
 
     def sampled_hist_dense(self, d_samples, n, d_counts, stream=None):
         """One launch: this pass's dense counts (DENSE_BINS + 1 u64 at d_counts; see dense_keys)."""
-        check(lib().pluss_dev_sampled_hist_dense(self._h, d_samples, n, d_counts, stream),
+        check(lib().pluss_dev_sampled_hist_dense(self._h, d_samples, n, d_counts, self._s(stream)),
               "pluss_dev_sampled_hist_dense")
 
     def gen_count_dense(self, seed, totals, first, n, d_counts, stream=None):
         """Generate slices [first[r], first[r]+n[r]) of the six key-order lists and
         count them (dense vector) in one launch; the lists never touch memory."""
         a = [(ctypes.c_uint64 * 6)(*[int(x) for x in v]) for v in (totals, first, n)]
-        check(lib().pluss_dev_gen_count_dense(self._h, seed, a[0], a[1], a[2], d_counts, stream),
+        check(lib().pluss_dev_gen_count_dense(self._h, seed, a[0], a[1], a[2], d_counts, self._s(stream)),
               "pluss_dev_gen_count_dense")
 
     def diag_dense(self, d_samples, n, d_counts, variant=0, max_grid=0, stream=None):
         """Diagnostics (include/pluss_diag.h): a dense pass with an ablation variant
         (0 product, 1 loads only, 2 no tail) and/or a workgroup cap."""
-        check(lib().pluss_diag_dense(self._h, d_samples, n, d_counts, variant, max_grid, stream), "pluss_diag_dense")
+        check(lib().pluss_diag_dense(self._h, d_samples, n, d_counts, variant, max_grid, self._s(stream)), "pluss_diag_dense")
 
     def diag_sort_words(self, ref, d_samples, n, d_words, stream=None):
         """Diagnostics (include/pluss_diag.h): the faithful radix source's bucket
@@ -382,7 +387,7 @@ class Context:
         words, ascending, into d_words.  Returns the word size in bytes (4 or 8)."""
         rid = REF_ID[ref] if isinstance(ref, str) else int(ref)
         wb = ctypes.c_int32(0)
-        check(lib().pluss_diag_sort_words(self._h, rid, d_samples, n, d_words, ctypes.byref(wb), stream),
+        check(lib().pluss_diag_sort_words(self._h, rid, d_samples, n, d_words, ctypes.byref(wb), self._s(stream)),
               "pluss_diag_sort_words")
         return int(wb.value)
 
@@ -394,7 +399,7 @@ class Context:
         """Phase 1 over key-ordered slices (d_samples None: generated slices)."""
         u6 = ctypes.c_uint64 * 6
         check(lib().pluss_dev_faithful_shards_local(self._h, d_samples, seed, u6(*map(int, totals)),
-                                                    u6(*map(int, first)), u6(*map(int, n)), d_row, stream),
+                                                    u6(*map(int, first)), u6(*map(int, n)), d_row, self._s(stream)),
               "pluss_dev_faithful_shards_local")
 
     def faithful_shards_select(self, d_lists, totals, key_lo, key_hi, d_row, stream=None):
@@ -402,27 +407,48 @@ class Context:
         keep the samples whose keys lie in [key_lo, key_hi)."""
         u6 = ctypes.c_uint64 * 6
         check(lib().pluss_dev_faithful_shards_select(self._h, d_lists, u6(*map(int, totals)), key_lo, key_hi, d_row,
-                                                     stream), "pluss_dev_faithful_shards_select")
+                                                     self._s(stream)), "pluss_dev_faithful_shards_select")
 
     def faithful_shards_local_selected(self, d_rows, shard, nshards, d_row, stream=None):
         """Phase 1 over the selected samples (reads the gathered rows on the host once)."""
-        check(lib().pluss_dev_faithful_shards_local_selected(self._h, d_rows, shard, nshards, d_row, stream),
+        check(lib().pluss_dev_faithful_shards_local_selected(self._h, d_rows, shard, nshards, d_row, self._s(stream)),
               "pluss_dev_faithful_shards_local_selected")
 
     def faithful_shards_carry(self, d_rows, shard, nshards, d_row, stream=None):
         """Phase 2: the replay state entering this shard -> its replay-start counts."""
-        check(lib().pluss_dev_faithful_shards_carry(self._h, d_rows, shard, nshards, d_row, stream),
+        check(lib().pluss_dev_faithful_shards_carry(self._h, d_rows, shard, nshards, d_row, self._s(stream)),
               "pluss_dev_faithful_shards_carry")
 
     def faithful_shards_cut(self, d_rows, shard, nshards, d_row, stream=None):
         """Phase 3: the starts before this shard -> its first Q1 cut candidates."""
-        check(lib().pluss_dev_faithful_shards_cut(self._h, d_rows, shard, nshards, d_row, stream),
+        check(lib().pluss_dev_faithful_shards_cut(self._h, d_rows, shard, nshards, d_row, self._s(stream)),
               "pluss_dev_faithful_shards_cut")
 
     def faithful_shards_hist(self, d_rows, shard, nshards, stream=None):
         """Phase 4: add this shard's part of the histograms (the global cut from the rows)."""
-        check(lib().pluss_dev_faithful_shards_hist(self._h, d_rows, shard, nshards, stream),
+        check(lib().pluss_dev_faithful_shards_hist(self._h, d_rows, shard, nshards, self._s(stream)),
               "pluss_dev_faithful_shards_hist")
+
+    def faithful_shards_uniform_count(self, seed, totals, shard, nshards, d_row, stream=None):
+        """r10's own law over key-range shards, phase 0: this shard's leaves'
+        candidates per reference into its row (then all-gather the rows)."""
+        u6 = ctypes.c_uint64 * 6
+        check(lib().pluss_dev_faithful_shards_uniform_count(self._h, seed, u6(*map(int, totals)), shard, nshards,
+                                                            d_row, self._s(stream)),
+              "pluss_dev_faithful_shards_uniform_count")
+
+    def faithful_shards_uniform_local(self, d_rows, shard, nshards, d_row, stream=None):
+        """Phase 1 of the uniform source: this shard's slice from the gathered
+        candidate counts (one host round trip), then its local pass."""
+        check(lib().pluss_dev_faithful_shards_uniform_local(self._h, d_rows, shard, nshards, d_row,
+                                                            self._s(stream)),
+              "pluss_dev_faithful_shards_uniform_local")
+
+    def faithful_shards_slice(self):
+        """[(first, n)] per reference: the slices the last key-range pass ran over."""
+        f, n = (ctypes.c_uint64 * 6)(), (ctypes.c_uint64 * 6)()
+        check(lib().pluss_dev_faithful_shards_slice(self._h, f, n), "pluss_dev_faithful_shards_slice")
+        return [(int(a), int(b)) for a, b in zip(f, n)]
 
     def fetch(self):
         h, keep = _hist_buf()
@@ -494,6 +520,13 @@ class Group:
         h, keep = _hist_buf()
         check(lib().pluss_group_gen_faithful(self._h, seed, (ctypes.c_uint64 * 6)(*map(int, totals)), ctypes.byref(h)),
               "pluss_group_gen_faithful")
+        return Histogram._from_c(h)
+
+    def gen_uniform_faithful(self, seed, totals):
+        """r10's own law (expand_uniform_sorted's lists) over the group's key-range shards."""
+        h, keep = _hist_buf()
+        check(lib().pluss_group_gen_uniform_faithful(self._h, seed, (ctypes.c_uint64 * 6)(*map(int, totals)),
+                                                     ctypes.byref(h)), "pluss_group_gen_uniform_faithful")
         return Histogram._from_c(h)
 
     def expand(self, seed, counts):

@@ -71,8 +71,8 @@ def build(verbose=False, force=False):
     # host half of the pipeline (CRI / AET / formats): plain C++, no HIP
     hsrc = [os.path.join(CSRC, h) for h in HOST_SOURCES]
     if force or _stale(HOST_LIB, hsrc + [os.path.join(inc, "pluss_host.h"), os.path.join(inc, "pluss_gpu.h")]):
-        run([os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-I", inc, "-o",
-             HOST_LIB, *hsrc])
+        run([os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall", "-I", inc,
+             "-o", HOST_LIB, *hsrc])
     # the reference's drivers (acc / speed / sample / replay) over both libraries
     csrc_cli = os.path.join(CSRC, "host", "pluss_cli.cpp")
     if force or _stale(CLI, [csrc_cli, LIB, HOST_LIB]):

@@ -249,22 +249,29 @@ int run_samplers(const Opts& o, const std::vector<uint64_t>* given) {
   pluss_hist h{buf.data(), buf.size(), 0, {0}};
   if (int rc = pluss_gemm_sampled_hist(&cfg, samples.data(), samples.size(), &h)) die("pluss_gemm_sampled_hist", rc);
   auto raw = fetch(h, buf);
-  std::vector<std::vector<pluss_kv>> per(6);
-  std::vector<pluss_kv> all;
+  // r10's host half in one call: the six CRI steps on host threads, the merge, AET, the MRC text
+  uint64_t nr = 0, nm = 0, nt = 0;
+  if (int rc = pluss_r10_host_pipeline(cfg.threads, &h, 0, nullptr, 0, &nr, nullptr, 0, &nm, nullptr, 0, &nt))
+    die("pluss_r10_host_pipeline", rc);
+  std::vector<pluss_kv> rih(nr ? nr : 1), mrc(nm ? nm : 1);
+  std::string mrc_txt(nt + 1, '\0');
+  if (int rc = pluss_r10_host_pipeline(cfg.threads, &h, 0, rih.data(), rih.size(), &nr, mrc.data(), mrc.size(), &nm,
+                                       &mrc_txt[0], nt + 1, &nt))
+    die("pluss_r10_host_pipeline", rc);
+  rih.resize(nr);
+  mrc.resize(nm);
+  mrc_txt.resize(nt);
+  std::cout << (now() - t0) << "\n";
+  std::vector<std::vector<pluss_kv>> per(6);  // each sampler_<REF>'s output, for its printout
   for (int r = 0; r < 6; ++r) {
     std::vector<pluss_hist_entry> mine;
     for (auto& e : raw)
       if (e.ref == r) mine.push_back(e);
-    if (mine.empty()) continue;
-    per[r] = call_kv(pluss_cri_r10, (int64_t)cfg.threads, mine.data(), (uint64_t)mine.size());
-    all.insert(all.end(), per[r].begin(), per[r].end());
+    if (!mine.empty()) per[r] = call_kv(pluss_cri_r10, (int64_t)cfg.threads, mine.data(), (uint64_t)mine.size());
   }
-  auto rih = call_kv(pluss_log2_merge, all.data(), (uint64_t)all.size());
-  auto mrc = call_kv(pluss_aet, rih.data(), (uint64_t)rih.size());
-  std::cout << (now() - t0) << "\n";
   for (int r : PRINT_ORDER) std::cout << text_hist(REFNAME[r], per[r]);
   std::cout << text_hist("Start to dump reuse time", rih);
-  std::cout << text_mrc(mrc);
+  std::cout << mrc_txt;
   uint64_t mx = 0;
   for (int r = 0; r < 6; ++r) mx = h.traversed[r] > mx ? h.traversed[r] : mx;
   std::cout << "max iteration traversed\n" << mx << "\n";

@@ -49,40 +49,50 @@ int validate_cfg(const pluss_cfg* c, Model* m) {
   return PLUSS_OK;
 }
 
-static int check_flags(pluss_ctx* ctx) {
-  unsigned int f[4] = {0, 0, 0, 0};
-  PLUSS_HIP_CHECK(hipMemcpy(f, ctx->g.flags, sizeof f, hipMemcpyDeviceToHost));
-  if (f[1]) {
-    set_error("malformed sample: ref > 5, an index >= N, or a reference other than the one requested");
+// The error a pass's flags report: flags[1] (malformed input) and the bits of
+// flags[0], each with its own message and code; shared by the one-GPU fetch
+// and the group's merge (`who`: the shard prefix of the message, or "").
+int flags_error(unsigned int f0, unsigned int bad, const std::string& who) {
+  if (bad) {
+    set_error(who + "malformed sample: ref > 5, an index >= N, or a reference other than the one requested");
     return PLUSS_ERR_INPUT;
   }
-  if (f[0] & FLAG_SHARD) {
-    set_error("a key-range shard of this faithful pass failed (its summary row carried an error word)");
+  if (f0 & FLAG_SHARD) {
+    set_error(who + "a key-range shard of this faithful pass failed (its summary row carried an error word)");
     return PLUSS_ERR_PEER;
   }
-  if (f[0] & FLAG_SORT) {
-    set_error("the bucket sort's plan exceeded its capacity (faithful radix source)");
+  if (f0 & FLAG_SORT) {
+    set_error(who + "the bucket sort's plan exceeded its capacity (faithful radix source)");
     return PLUSS_ERR_CAPACITY;
   }
-  if (f[0] & FLAG_UNI) {
-    set_error("uniform key-order generator: fewer candidates than samples, or a candidate window past its "
+  if (f0 & FLAG_UNI) {
+    set_error(who + "uniform key-order generator: fewer candidates than samples, or a candidate window past its "
               "capacity (probability below 1e-20; another seed draws afresh)");
     return PLUSS_ERR_CAPACITY;
   }
-  if (f[0] & FLAG_LOOKBACK) {
-    set_error("faithful pass stalled: a chunk's predecessor never published its running max (another kernel "
+  if (f0 & FLAG_LOOKBACK) {
+    set_error(who + "faithful pass stalled: a chunk's predecessor never published its running max (another kernel "
               "holding the GPU?)");
     return PLUSS_ERR_HIP;
   }
-  if (f[0]) {
-    set_error("histogram table overflow (more distinct (ref,kind,RI) keys than the table holds)");
+  if (f0) {
+    set_error(who + "histogram table overflow (more distinct (ref,kind,RI) keys than the table holds)");
     return PLUSS_ERR_CAPACITY;
   }
   return PLUSS_OK;
 }
 
+static int check_flags(pluss_ctx* ctx) {
+  unsigned int f[4] = {0, 0, 0, 0};
+  PLUSS_HIP_CHECK(hipMemcpy(f, ctx->g.flags, sizeof f, hipMemcpyDeviceToHost));
+  return flags_error(f[0], f[1], "");
+}
+
+// stream == NULL is HIP's null stream (ordered with the caller's null-stream
+// work, as every HIP API takes it); the handle's own stream is pluss_ctx_stream()
 static hipStream_t pick(pluss_ctx* ctx, void* stream) {
-  ctx->last = stream ? (hipStream_t)stream : ctx->stream;
+  ctx->last = (hipStream_t)stream;
+  ctx->has_last = true;
   return ctx->last;
 }
 
@@ -203,11 +213,7 @@ int pluss_ctx_destroy(pluss_ctx* c) {
     for (void* p : fr)
       if (p) (void)hipFree(p);
   }
-  {
-    void* ub[] = {c->ub.set, c->ub.cnt, c->ub.bits, c->ub.tmap, c->ub.pre, c->ub.rb, c->ub.bsum, c->ub.pmt};
-    for (void* p : ub)
-      if (p) (void)hipFree(p);
-  }
+  uni_free(c);
   for (int r = 0; r < 6; ++r)
     if (c->fst[r]) (void)hipStreamDestroy(c->fst[r]);
   for (int e = 0; e < 7; ++e)
@@ -373,6 +379,25 @@ int pluss_dev_faithful_shards_local_selected(pluss_ctx* ctx, const uint64_t* d_r
   return faith_shards_local_selected(ctx, d_rows, shard, nshards, d_row, pick(ctx, stream));
 }
 
+int pluss_dev_faithful_shards_uniform_count(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, int32_t shard,
+                                            int32_t nshards, uint64_t* d_row, void* stream) {
+  if (!ctx || !totals || !d_row) return PLUSS_ERR_CONFIG;
+  return faith_shards_uniform_count(ctx, seed, totals, shard, nshards, d_row, pick(ctx, stream));
+}
+
+int pluss_dev_faithful_shards_uniform_local(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards,
+                                            uint64_t* d_row, void* stream) {
+  if (!ctx || !d_row) return PLUSS_ERR_CONFIG;
+  hipStream_t s = pick(ctx, stream);
+  if (int rc = faith_shards_uniform_window(ctx, d_rows, shard, nshards, s)) return rc;
+  return faith_shards_uniform_finish(ctx, d_row, s);
+}
+
+int pluss_dev_faithful_shards_slice(pluss_ctx* ctx, uint64_t first[6], uint64_t n[6]) {
+  if (!ctx || !first || !n) return PLUSS_ERR_CONFIG;
+  return faith_shards_slice(ctx, first, n);
+}
+
 int pluss_dev_faithful_shards_carry(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards,
                                     uint64_t* d_row, void* stream) {
   if (!ctx || !d_row) return PLUSS_ERR_CONFIG;
@@ -418,7 +443,7 @@ int pluss_keyorder_index_range(const pluss_cfg* cfg, uint64_t seed, int32_t ref,
 
 int pluss_hist_fetch(pluss_ctx* ctx, pluss_hist* out) {
   if (!ctx || !out) return PLUSS_ERR_CONFIG;
-  hipStream_t s = ctx->last ? ctx->last : ctx->stream;
+  hipStream_t s = ctx->has_last ? ctx->last : ctx->stream;
   if (int rc = launch_export(ctx, ctx->d_exp_keys, ctx->d_exp_counts, GCAP, s)) return rc;
   PLUSS_HIP_CHECK(hipStreamSynchronize(s));
   if (int rc = check_flags(ctx)) return rc;
@@ -508,7 +533,7 @@ int pluss_gemm_fulltrace_hist(const pluss_cfg* cfg, pluss_hist* out) {
   if (!out) return PLUSS_ERR_CONFIG;
   Scoped sc;
   if (int rc = pluss_ctx_create(cfg, &sc.ctx)) return rc;
-  if (int rc = pluss_dev_fulltrace_hist(sc.ctx, nullptr)) return rc;
+  if (int rc = pluss_dev_fulltrace_hist(sc.ctx, sc.ctx->stream)) return rc;
   return pluss_hist_fetch(sc.ctx, out);
 }
 

@@ -1930,9 +1930,11 @@ struct FaShards {
   FaLaunch L;
   int src = SRC_GEN;
   int phase = 0;  // last completed phase (SH_*)
-  uint64_t tot[6] = {0, 0, 0, 0, 0, 0};  // SH_SELECTED: every reference's whole-list length
+  uint64_t tot[6] = {0, 0, 0, 0, 0, 0};  // SH_SELECTED, SH_UCOUNT: every reference's whole-list length
+  int32_t shard = 0, nshards = 1;         // SH_UCOUNT: this shard's leaves
+  bool has_slice = false;                 // the local phase ran: L.a holds this shard's slices
 };
-enum : int { SH_NONE = 0, SH_LOCAL = 1, SH_CARRY = 2, SH_CUT = 3, SH_SELECTED = 10 };
+enum : int { SH_NONE = 0, SH_LOCAL = 1, SH_CARRY = 2, SH_CUT = 3, SH_SELECTED = 10, SH_UCOUNT = 11, SH_UWINDOW = 12 };
 
 // the four sources (pluss_fa_w32.hip, pluss_fa_w64.hip, pluss_fa_smp.hip, pluss_fa_gen.hip)
 void fa_launch_w32(const FaLaunch& L);

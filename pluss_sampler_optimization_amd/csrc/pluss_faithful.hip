@@ -1063,6 +1063,7 @@ static int shards_phase1(pluss_ctx* ctx, FaShards& f, uint64_t* d_row, hipStream
                      0);
   PLUSS_HIP_CHECK(hipGetLastError());
   f.phase = SH_LOCAL;
+  f.has_slice = true;
   return PLUSS_OK;
 }
 
@@ -1182,6 +1183,101 @@ int faith_shards_local_selected(pluss_ctx* ctx, const uint64_t* d_rows, int32_t 
   f.src = fm == FM_PK32 ? SRC_W32 : SRC_W64;
   if (int rc = fa_prepare(ctx, a, f.src, false, true, s, &f.L)) return rc;
   return shards_phase1(ctx, f, d_row, s);
+}
+
+// r10's own law (pluss_uniform.h) over key-range shards: shard g of G holds,
+// per reference, the leaves [L*g/G, L*(g+1)/G) of the key-ordered space (L
+// leaves), so its samples are a contiguous stretch of the list in key order.
+// Phase 0 counts this shard's candidates (row[ROW_N + r]); after the gather
+// every shard knows the candidates before it and in all (X0, T'), removes the
+// ranks of its window, and so its slice of the list: [first, first + n) --
+// read back once (the launch grids need n), then the local pass over the tiles
+// of that slice, each generated from the shard's plan.
+__global__ void k_ug_row(const UniSet* __restrict__ us, unsigned long long* __restrict__ row) {
+  const uint32_t w = threadIdx.x;
+  if (w >= ROW_W) return;
+  unsigned long long v = 0;
+  if (w >= ROW_N && w < ROW_N + 6) {
+    const uint32_t r = w - ROW_N;
+    v = us->pre[us->loff[r + 1]] - us->pre[us->loff[r]];
+  }
+  row[w] = v;
+}
+
+int faith_shards_uniform_count(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, int32_t shard, int32_t nshards,
+                               uint64_t* d_row, hipStream_t s) {
+  FaShards& f = shards_of(ctx);
+  f = FaShards{};
+  if (int rc = faith_direct_shape(ctx, "pluss_dev_faithful_shards_uniform_count")) return rc;
+  if (nshards < 1 || shard < 0 || shard >= nshards) {
+    set_error("pluss_dev_faithful_shards_uniform_count: needs 0 <= shard < nshards");
+    return PLUSS_ERR_CONFIG;
+  }
+  for (int r = 0; r < 6; ++r) f.tot[r] = totals[r];
+  if (int rc = uni_plan_count(ctx, seed, totals, (uint32_t)shard, (uint32_t)nshards, s)) return rc;
+  hipLaunchKernelGGL(k_ug_row, dim3(1), dim3(ROW_W), 0, s, (const UniSet*)ctx->ub.set, (unsigned long long*)d_row);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  ctx->tables_dirty = true;
+  f.shard = shard;
+  f.nshards = nshards;
+  f.phase = SH_UCOUNT;
+  return PLUSS_OK;
+}
+
+// the removal over this shard's candidate window, and this shard's slice copied
+// to the host (asynchronously: a caller driving several shards issues every
+// shard's window before waiting on any)
+int faith_shards_uniform_window(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards,
+                                hipStream_t s) {
+  if (int rc = shards_expect(ctx, SH_UCOUNT, "pluss_dev_faithful_shards_uniform_local", d_rows, shard, nshards))
+    return rc;
+  FaShards& f = *ctx->fsh2;
+  if (shard != f.shard || nshards != f.nshards) {
+    set_error("pluss_dev_faithful_shards_uniform_local: shard / nshards differ from the count phase's");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (int rc = uni_plan_remove(ctx, (const unsigned long long*)d_rows, (uint32_t)shard, (uint32_t)nshards, s))
+    return rc;
+  PLUSS_HIP_CHECK(hipMemcpyAsync(ctx->ub.hinfo, ctx->ub.info, UI_W * 8, hipMemcpyDeviceToHost, s));
+  f.phase = SH_UWINDOW;
+  return PLUSS_OK;
+}
+
+// ... then the shard's slice, its tile map and the local pass (phase 1)
+int faith_shards_uniform_finish(pluss_ctx* ctx, uint64_t* d_row, hipStream_t s) {
+  if (!ctx->fsh2 || ctx->fsh2->phase != SH_UWINDOW) {
+    set_error("pluss_dev_faithful_shards_uniform_local: out of order");
+    return PLUSS_ERR_CONFIG;
+  }
+  FaShards& f = *ctx->fsh2;
+  PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+  FaRefs a = fa_none();
+  uint64_t n[6];
+  for (int r = 0; r < 6; ++r) {
+    const uint64_t first = ctx->ub.hinfo[6 + r], m = ctx->ub.hinfo[12 + r];
+    n[r] = f.tot[r] && first <= f.tot[r] && m <= f.tot[r] - first ? m : 0;  // (a flagged plan: reported at the fetch)
+    a.n[r] = n[r];
+    a.ntot[r] = f.tot[r];
+    a.joff[r] = n[r] ? first : 0;
+  }
+  const UniSet* us = nullptr;
+  if (int rc = uni_plan_tiles(ctx, n, s, &us)) return rc;
+  a.us = us;
+  f.src = SRC_UNI;
+  if (int rc = fa_prepare(ctx, a, f.src, false, true, s, &f.L)) return rc;
+  return shards_phase1(ctx, f, d_row, s);
+}
+
+int faith_shards_slice(pluss_ctx* ctx, uint64_t* first, uint64_t* n) {
+  if (!ctx->fsh2 || !ctx->fsh2->has_slice) {
+    set_error("pluss_dev_faithful_shards_slice: no key-range pass past its local phase on this handle");
+    return PLUSS_ERR_CONFIG;
+  }
+  for (int r = 0; r < 6; ++r) {
+    first[r] = ctx->fsh2->L.a.joff[r];
+    n[r] = ctx->fsh2->L.a.n[r];
+  }
+  return PLUSS_OK;
 }
 
 int faith_shards_carry(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards, uint64_t* d_row,

@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <string>
 #include <vector>
@@ -88,27 +89,94 @@ static Rccl* rccl() {
     }                                                                                                \
   } while (0)
 
-// per shard, the block all-gathered at the end of a one-shot pass: its
-// canonical table (GCAP keys, GCAP counts), traversed[8], flags[8]
+// a HIP call's result as a PLUSS_* code (the error message set), without returning
+static int hip_rc(hipError_t e, const char* what) {
+  if (e == hipSuccess) return PLUSS_OK;
+  set_error(std::string(what) + ": " + hipGetErrorString(e));
+  return PLUSS_ERR_HIP;
+}
+
+// per shard, the block all-gathered at the end of a one-shot pass over a shape
+// with arbitrary keys (N % (cls/ds) != 0): its canonical table (GCAP keys, GCAP
+// counts), traversed[8], flags[7] and a local-failure word
 constexpr size_t GBLOCK = 2 * (size_t)GCAP + 16;
-constexpr int DVEC = 32;  // words per dense vector slot (DBINS used)
+constexpr int GB_FAIL = 15;  // (tail word: nonzero when the shard failed on the host)
+
+// The dense result vector of a shard (one slot of DVEC words; every shape with
+// N % (cls/ds) == 0): a pass's whole histogram is then a fixed set of words,
+// merged over the shards by a sum (one RCCL all-reduce) -- the 18 (ref, case)
+// bins, the malformed count, per reference the -1 (cold) key's count and
+// whether some shard materialised it (faithful mode, r10:196,671),
+// traversed, and one word per failure condition (the number of shards that
+// met it).  A shard that fails on the host still sends its slot, with the
+// local-failure word set, so no rank waits in the all-reduce.
+constexpr int DVEC = 48;
+enum : int { GV_BAD = 18, GV_COLD = 19, GV_PRES = 25, GV_TRAV = 31, GV_COND = 37, GV_W = 45 };
+enum : int { GC_LOCAL = 0, GC_BAD = 1, GC_OVERFLOW = 2, GC_LOOKBACK = 3, GC_SHARD = 4, GC_SORT = 5, GC_UNI = 6,
+             GC_NONDENSE = 7 };
 
 __global__ void k_group_sum(const unsigned long long* __restrict__ vecs, int n, unsigned long long* __restrict__ out) {
   const int i = threadIdx.x;
-  if (i >= (int)DBINS) return;
+  if (i >= GV_W) return;
   unsigned long long s = 0;
   for (int j = 0; j < n; ++j) s += vecs[j * DVEC + i];
   out[i] = s;
 }
 
+// a shard's slot from its handle's histogram state: the direct bins folded over
+// their rows, the tables' -1 keys (any other key: GC_NONDENSE, the merge falls
+// back to the tables), traversed and the flags
+__global__ __launch_bounds__(256) void k_group_vec(Model m, GTable g, unsigned long long* __restrict__ slot, int fail) {
+  __shared__ unsigned long long v[GV_W];
+  const uint32_t t = threadIdx.x;
+  if (t < GV_W) v[t] = 0;
+  __syncthreads();
+  if (t < 18) {
+    unsigned long long x = 0;
+    for (uint32_t row = 0; row < NBROW; ++row) x += g.bins[row * BSTRIDE + t];
+    v[t] = x;
+  } else if (t >= 32 && t < 38) {
+    v[GV_TRAV + (t - 32)] = g.trav[t - 32];
+  } else if (t == 64) {
+    const unsigned int f0 = g.flags[0];
+    v[GV_COND + GC_LOCAL] = fail ? 1u : 0u;
+    v[GV_COND + GC_BAD] = g.flags[1] ? 1u : 0u;
+    v[GV_COND + GC_OVERFLOW] = (f0 & FLAG_OVERFLOW) ? 1u : 0u;
+    v[GV_COND + GC_LOOKBACK] = (f0 & FLAG_LOOKBACK) ? 1u : 0u;
+    v[GV_COND + GC_SHARD] = (f0 & FLAG_SHARD) ? 1u : 0u;
+    v[GV_COND + GC_SORT] = (f0 & FLAG_SORT) ? 1u : 0u;
+    v[GV_COND + GC_UNI] = (f0 & FLAG_UNI) ? 1u : 0u;
+  }
+  __syncthreads();
+  for (uint32_t i = t; i < GCAP + NREP * RCAP; i += 256) {
+    const unsigned long long k = i < GCAP ? g.keys[i] : g.rkeys[i - GCAP];
+    if (k == KEY_NONE) continue;
+    const unsigned long long c = i < GCAP ? g.counts[i] : g.rcounts[i - GCAP];
+    const uint32_t r = key_ref(k);
+    if (r < 6 && key_kind(k) == 0 && key_ri(k) == -1) {
+      atomicAdd(&v[GV_COLD + r], c);
+      v[GV_PRES + r] = 1;
+      continue;
+    }
+    int b = -1;
+#pragma unroll
+    for (int x = 0; x < 18; ++x) b = m.keytab[x] == k ? x : b;
+    if (b >= 0) atomicAdd(&v[b], c);
+    else v[GV_COND + GC_NONDENSE] = 1;
+  }
+  __syncthreads();
+  if (t < GV_W) slot[t] = v[t];
+}
+
+// a slot (or a gathered row / block) of a shard that failed on the host
+__global__ void k_group_word(unsigned long long* w, unsigned long long v) { *w = v; }
+
 // a shard's traversed and flags words into its gathered block
 __global__ void k_group_block_tail(GTable g, unsigned long long* __restrict__ blk) {
   const int i = threadIdx.x;
   if (i < 8) blk[2 * GCAP + i] = g.trav[i];
-  else if (i < 16) blk[2 * GCAP + i] = g.flags[i - 8];
+  else if (i < 15) blk[2 * GCAP + i] = g.flags[i - 8];
 }
-
-__global__ void k_group_row_fail(unsigned long long* row) { row[ROW_ERR] = 1; }
 
 }  // namespace pluss
 
@@ -246,18 +314,40 @@ static void shard_ranges(uint64_t c, int g, int S, uint64_t* first, uint64_t* n)
   *n = hi - lo;
 }
 
-// The end of a one-shot pass: every shard's canonical table, traversed and
-// flags all-gathered, summed on the host (the same on every rank).  The first
-// error of a local shard wins; a flagged shard anywhere fails the pass.
-static int group_collect(pluss_group* G, int first_rc, const std::string& first_err, pluss_hist* out) {
+// The first error of a group call on this rank (the local shards' own),
+// kept while the call still runs every collective.
+struct GErr {
+  int rc = PLUSS_OK;
+  std::string msg;
+  void note(int r) {
+    if (r && !rc) {
+      rc = r;
+      msg = pluss_last_error();
+    }
+  }
+  void note(int r, const std::string& m) {
+    if (r && !rc) {
+      rc = r;
+      msg = m;
+    }
+  }
+};
+
+// The end of a one-shot pass over a shape with arbitrary keys: every shard's
+// canonical table, traversed, flags and failure word all-gathered, summed on
+// the host (the same on every rank).  This rank's first error wins; a shard
+// that failed anywhere fails the pass on every rank (PLUSS_ERR_PEER).
+static int collect_tables(pluss_group* G, GErr& E, pluss_hist* out) {
   for (int d = 0; d < G->ndev; ++d) {
-    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    E.note(hip_rc(hipSetDevice(G->dev[d]), "hipSetDevice"));
     for (int j = 0; j < G->spd; ++j) {
       pluss_ctx* c = shard(G, d, j);
       unsigned long long* b = G->blk[d] + (size_t)gshard(G, d, j) * GBLOCK;
-      if (int rc = pluss_dev_hist_export(c, (uint64_t*)b, (uint64_t*)(b + GCAP), GCAP, c->stream)) return rc;
+      const int rc = pluss_dev_hist_export(c, (uint64_t*)b, (uint64_t*)(b + GCAP), GCAP, c->stream);
+      E.note(rc);
       hipLaunchKernelGGL(k_group_block_tail, dim3(1), dim3(64), 0, c->stream, c->g, b);
-      PLUSS_HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(k_group_word, dim3(1), dim3(1), 0, c->stream, b + 2 * GCAP + GB_FAIL, E.rc ? 1ull : 0ull);
+      E.note(hip_rc(hipGetLastError(), "group block"));
     }
   }
   if (int rc = gather_blocks(G, G->blk, GBLOCK)) return rc;
@@ -265,9 +355,9 @@ static int group_collect(pluss_group* G, int first_rc, const std::string& first_
   PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
   PLUSS_HIP_CHECK(hipMemcpyAsync(h.data(), G->blk[0], h.size() * 8, hipMemcpyDeviceToHost, G->xs[0]));
   for (int d = 0; d < G->ndev; ++d) PLUSS_HIP_CHECK(hipStreamSynchronize(G->xs[d]));
-  if (first_rc) {
-    set_error(first_err);
-    return first_rc;
+  if (E.rc) {
+    set_error(E.msg);
+    return E.rc;
   }
   std::vector<uint64_t> keys, cnts;
   keys.reserve((size_t)G->nshards * GCAP);
@@ -275,20 +365,16 @@ static int group_collect(pluss_group* G, int first_rc, const std::string& first_
   uint64_t trav[6] = {0, 0, 0, 0, 0, 0};
   for (int g = 0; g < G->nshards; ++g) {
     const unsigned long long* b = h.data() + (size_t)g * GBLOCK;
-    const unsigned long long* fl = b + 2 * GCAP + 8;
-    if (fl[1]) {
-      set_error("shard " + std::to_string(g) + ": malformed sample (ref > 5, an index >= N, or a wrong reference)");
-      return PLUSS_ERR_INPUT;
-    }
-    if (fl[0] & FLAG_SHARD) {
-      set_error("a key-range shard of this faithful pass failed (shard " + std::to_string(g) + " saw its error word)");
+    if (b[2 * GCAP + GB_FAIL]) {
+      set_error("shard " + std::to_string(g) + " of this group pass failed on its host");
       return PLUSS_ERR_PEER;
     }
-    if (fl[0]) {
-      set_error("shard " + std::to_string(g) + ": histogram table overflow or stalled pass (flags " +
-                std::to_string(fl[0]) + ")");
-      return PLUSS_ERR_CAPACITY;
-    }
+  }
+  for (int g = 0; g < G->nshards; ++g) {
+    const unsigned long long* b = h.data() + (size_t)g * GBLOCK;
+    const unsigned long long* fl = b + 2 * GCAP + 8;
+    if (int rc = flags_error((unsigned int)fl[0], (unsigned int)fl[1], "shard " + std::to_string(g) + ": "))
+      return rc;
     for (uint32_t i = 0; i < GCAP; ++i) {
       if (b[i] == KEY_EMPTY || b[i] == KEY_NONE) break;  // sorted, empties last
       keys.push_back(b[i]);
@@ -301,46 +387,49 @@ static int group_collect(pluss_group* G, int first_rc, const std::string& first_
   return PLUSS_OK;
 }
 
-static int group_reset(pluss_group* G) {
+static int group_reset(pluss_group* G, GErr& E) {
   for (int d = 0; d < G->ndev; ++d) {
-    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    E.note(hip_rc(hipSetDevice(G->dev[d]), "hipSetDevice"));
     for (int j = 0; j < G->spd; ++j) {
       pluss_ctx* c = shard(G, d, j);
-      if (int rc = pluss_dev_hist_reset(c, c->stream)) return rc;
+      E.note(pluss_dev_hist_reset(c, c->stream));
     }
-  }
-  return PLUSS_OK;
+  }  // (the dense slots need no reset: k_group_vec and k_group_sum write every word)
+  return E.rc;
 }
 
-// one faithful key-range pass over the local shards, the rows exchanged
-// between the phases; `phase1(d, j, g, row)` runs a shard's first phase
-template <class F>
-static int group_faithful(pluss_group* G, bool selected, F&& phase1, int* frc, std::string* ferr) {
-  auto note = [&](int rc, int d, unsigned long long* row, pluss_ctx* c) {
-    if (!rc) return;
-    if (!*frc) {
-      *frc = rc;
-      *ferr = pluss_last_error();
-    }
-    hipLaunchKernelGGL(k_group_row_fail, dim3(1), dim3(1), 0, c->stream, row);  // every shard learns of it
-  };
-  auto each = [&](auto&& fn) {
+// a shard's step: its error noted (first one wins) and its summary row marked
+// failed, so every shard learns of it at the next gather
+using ShardFn = std::function<int(pluss_ctx*, int d, int j, int g, uint64_t* row)>;
+
+// One faithful key-range pass over the local shards, the rows exchanged
+// between the phases: phase1 (each shard's first phase), then, after the
+// first gather, the optional mid steps (mid1 on every shard, then mid2 on
+// every shard: a source whose local phase needs the gathered rows, e.g. the
+// uniform source's window, enqueued on all shards before any waits), then
+// carry, cut and hist.  Returns only errors of the collectives themselves;
+// shard failures are in E and in the rows.
+static int group_faithful(pluss_group* G, const ShardFn& phase1, const ShardFn& mid1, const ShardFn& mid2,
+                          GErr& E) {
+  auto each = [&](const ShardFn& fn) {
     for (int d = 0; d < G->ndev; ++d) {
       (void)hipSetDevice(G->dev[d]);
       for (int j = 0; j < G->spd; ++j) {
         const int g = gshard(G, d, j);
         pluss_ctx* c = shard(G, d, j);
         unsigned long long* row = G->rows[d] + (size_t)g * ROW_W;
-        note(fn(c, d, j, g, (uint64_t*)row), d, row, c);
+        if (const int rc = fn(c, d, j, g, (uint64_t*)row)) {
+          E.note(rc);
+          hipLaunchKernelGGL(k_group_word, dim3(1), dim3(1), 0, c->stream, row + ROW_ERR, 1ull);
+        }
       }
     }
   };
-  each([&](pluss_ctx* c, int d, int j, int g, uint64_t* row) { return phase1(c, d, j, g, row); });
+  each(phase1);
   if (int rc = gather_blocks(G, G->rows, ROW_W)) return rc;
-  if (selected) {
-    each([&](pluss_ctx* c, int d, int, int g, uint64_t* row) {
-      return pluss_dev_faithful_shards_local_selected(c, (const uint64_t*)G->rows[d], g, G->nshards, row, c->stream);
-    });
+  if (mid1) {
+    each(mid1);
+    if (mid2) each(mid2);
     if (int rc = gather_blocks(G, G->rows, ROW_W)) return rc;
   }
   each([&](pluss_ctx* c, int d, int, int g, uint64_t* row) {
@@ -357,7 +446,7 @@ static int group_faithful(pluss_group* G, bool selected, F&& phase1, int* frc, s
   return PLUSS_OK;
 }
 
-// dense vectors of the local shards summed per device, all-reduced over the ranks, on the exchange streams
+// the slots of the local shards summed per device, all-reduced over the ranks, on the exchange streams
 static int dense_merge(pluss_group* G) {
   if (int rc = join_shards(G)) return rc;
   for (int d = 0; d < G->ndev; ++d) {
@@ -369,21 +458,32 @@ static int dense_merge(pluss_group* G) {
   PLUSS_NCCL_CHECK(g_rccl.GroupStart());
   for (int d = 0; d < G->ndev; ++d) {
     unsigned long long* v = G->vec[d] + (size_t)G->spd * DVEC;
-    PLUSS_NCCL_CHECK(g_rccl.AllReduce(v, v, DBINS, ncclUint64, ncclSum, G->comm[d], G->xs[d]));
+    PLUSS_NCCL_CHECK(g_rccl.AllReduce(v, v, GV_W, ncclUint64, ncclSum, G->comm[d], G->xs[d]));
   }
   PLUSS_NCCL_CHECK(g_rccl.GroupEnd());
   return fork_shards(G);
 }
 
-// one dense pass over the resident lists, everything on the exchange streams (capturable)
-static int dense_pass_on_xs(pluss_group* G) {
+// one dense pass over the resident lists, everything on the exchange streams
+// (capturable); a shard without a list sends a failed slot
+static int dense_pass_on_xs(pluss_group* G, GErr& E) {
   for (int d = 0; d < G->ndev; ++d) {
     PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
     for (int j = 0; j < G->spd; ++j) {
       const size_t i = (size_t)d * G->spd + j;
-      if (int rc = pluss_dev_sampled_hist_dense(G->ctx[i], (const uint64_t*)G->list[i], G->list_n[i],
-                                                (uint64_t*)(G->vec[d] + (size_t)j * DVEC), G->xs[d]))
-        return rc;
+      unsigned long long* slot = G->vec[d] + (size_t)j * DVEC;
+      int rc = PLUSS_OK;
+      if (!G->list[i]) {
+        set_error("pluss_group_dense: no resident lists (pluss_group_expand first)");
+        rc = PLUSS_ERR_CONFIG;
+      } else {
+        rc = pluss_dev_sampled_hist_dense(G->ctx[i], (const uint64_t*)G->list[i], G->list_n[i], (uint64_t*)slot,
+                                          G->xs[d]);
+      }
+      if (rc) {
+        E.note(rc);
+        hipLaunchKernelGGL(k_group_word, dim3(1), dim3(1), 0, G->xs[d], slot + GV_COND + GC_LOCAL, 1ull);
+      }
     }
     hipLaunchKernelGGL(k_group_sum, dim3(1), dim3(64), 0, G->xs[d], (const unsigned long long*)G->vec[d], G->spd,
                        G->vec[d] + (size_t)G->spd * DVEC);
@@ -392,21 +492,69 @@ static int dense_pass_on_xs(pluss_group* G) {
   PLUSS_NCCL_CHECK(g_rccl.GroupStart());
   for (int d = 0; d < G->ndev; ++d) {
     unsigned long long* v = G->vec[d] + (size_t)G->spd * DVEC;
-    PLUSS_NCCL_CHECK(g_rccl.AllReduce(v, v, DBINS, ncclUint64, ncclSum, G->comm[d], G->xs[d]));
+    PLUSS_NCCL_CHECK(g_rccl.AllReduce(v, v, GV_W, ncclUint64, ncclSum, G->comm[d], G->xs[d]));
   }
   PLUSS_NCCL_CHECK(g_rccl.GroupEnd());
   return PLUSS_OK;
 }
 
-static int dense_result(pluss_group* G, uint64_t* counts) {
+// the merged vector on the host once every exchange stream has drained; the
+// first error: this rank's own, then a shard that failed anywhere, then the
+// merged flags (each condition reported as one GPU's fetch reports it)
+static int vec_fetch(pluss_group* G, const GErr& E, unsigned long long* v) {
   for (int d = 0; d < G->ndev; ++d) {
     PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
     PLUSS_HIP_CHECK(hipStreamSynchronize(G->xs[d]));
   }
   PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
-  if (counts)
-    PLUSS_HIP_CHECK(hipMemcpy(counts, G->vec[0] + (size_t)G->spd * DVEC, DBINS * 8,
-                              hipMemcpyDeviceToHost));
+  PLUSS_HIP_CHECK(hipMemcpy(v, G->vec[0] + (size_t)G->spd * DVEC, GV_W * 8, hipMemcpyDeviceToHost));
+  if (E.rc) {
+    set_error(E.msg);
+    return E.rc;
+  }
+  const unsigned long long* c = v + GV_COND;
+  if (c[GC_LOCAL]) {
+    set_error(std::to_string(c[GC_LOCAL]) + " shard(s) of this group pass failed on their host");
+    return PLUSS_ERR_PEER;
+  }
+  const unsigned int f0 = (c[GC_OVERFLOW] ? FLAG_OVERFLOW : 0u) | (c[GC_LOOKBACK] ? FLAG_LOOKBACK : 0u) |
+                          (c[GC_SHARD] ? FLAG_SHARD : 0u) | (c[GC_SORT] ? FLAG_SORT : 0u) | (c[GC_UNI] ? FLAG_UNI : 0u);
+  return flags_error(f0, (v[GV_BAD] || c[GC_BAD]) ? 1u : 0u, "group pass: ");
+}
+
+// The end of a one-shot pass over a shape with N % (cls/ds) == 0: every
+// shard's slot (k_group_vec), one all-reduce, the merged histogram built from
+// the vector on the host.  A key outside the dense set (none expected) falls
+// back to the tables, on every rank alike.
+static int collect(pluss_group* G, GErr& E, pluss_hist* out) {
+  if (!G->m.fast) return collect_tables(G, E, out);
+  for (int d = 0; d < G->ndev; ++d) {
+    E.note(hip_rc(hipSetDevice(G->dev[d]), "hipSetDevice"));
+    for (int j = 0; j < G->spd; ++j) {
+      pluss_ctx* c = shard(G, d, j);
+      hipLaunchKernelGGL(k_group_vec, dim3(1), dim3(256), 0, c->stream, G->m, c->g, G->vec[d] + (size_t)j * DVEC,
+                         E.rc ? 1 : 0);
+    }
+    E.note(hip_rc(hipGetLastError(), "k_group_vec"));
+  }
+  if (int rc = dense_merge(G)) return rc;
+  unsigned long long v[GV_W];
+  const int rc = vec_fetch(G, E, v);
+  if (rc) return rc;
+  if (v[GV_COND + GC_NONDENSE]) return collect_tables(G, E, out);
+  std::vector<uint64_t> keys, cnts;
+  for (int b = 0; b < PLUSS_DENSE_BINS; ++b)
+    if (v[b]) {
+      keys.push_back(G->m.keytab[b]);
+      cnts.push_back(v[b]);
+    }
+  for (int r = 0; r < 6; ++r)
+    if (v[GV_PRES + r]) {  // the -1 key, materialised (r10:196,671), merged with a dense cold bin of the same key
+      keys.push_back(make_key((uint32_t)r, 0, -1));
+      cnts.push_back(v[GV_COLD + r]);
+    }
+  if (int rc2 = pluss_hist_from_tables(keys.data(), cnts.data(), keys.size(), out)) return rc2;
+  for (int r = 0; r < 6; ++r) out->traversed[r] = v[GV_TRAV + r];
   return PLUSS_OK;
 }
 
@@ -547,8 +695,21 @@ int pluss_group_shards(const pluss_group* G, int32_t* local, int32_t* total) {
   return PLUSS_OK;
 }
 
+// the captured dense passes point at the resident lists and their sizes:
+// dropped whenever the lists change (a replay would read freed lists)
+static int drop_graphs(pluss_group* G) {
+  for (int d = 0; d < G->ndev; ++d) {
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    PLUSS_HIP_CHECK(hipStreamSynchronize(G->xs[d]));
+  }
+  for (auto& kv : G->graphs) (void)hipGraphExecDestroy(kv.second);
+  G->graphs.clear();
+  return PLUSS_OK;
+}
+
 int pluss_group_expand(pluss_group* G, uint64_t seed, const uint64_t counts[6]) {
   if (!G || !counts) return PLUSS_ERR_CONFIG;
+  if (int rc = drop_graphs(G)) return rc;
   for (int d = 0; d < G->ndev; ++d) {
     PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
     for (int j = 0; j < G->spd; ++j) {
@@ -566,7 +727,8 @@ int pluss_group_expand(pluss_group* G, uint64_t seed, const uint64_t counts[6]) 
       PLUSS_HIP_CHECK(hipMalloc((void**)&G->list[i], (tot ? tot : 1) * 8));
       uint64_t off = 0;
       for (int r = 0; r < 6; ++r) {
-        if (int rc = pluss_dev_expand(G->ctx[i], seed, r, f[r], n[r], (uint64_t*)G->list[i] + off, nullptr)) return rc;
+        if (int rc = pluss_dev_expand(G->ctx[i], seed, r, f[r], n[r], (uint64_t*)G->list[i] + off, G->ctx[i]->stream))
+          return rc;
         off += n[r];
       }
       G->list_n[i] = tot;
@@ -583,14 +745,16 @@ int pluss_group_dense(pluss_group* G, uint32_t passes, uint64_t counts[PLUSS_DEN
     set_error("pluss_group_dense: needs N % (cls/ds) == 0");
     return PLUSS_ERR_CONFIG;
   }
-  for (size_t i = 0; i < G->ctx.size(); ++i)
-    if (!G->list[i]) {
-      set_error("pluss_group_dense: no resident lists (pluss_group_expand first)");
-      return PLUSS_ERR_CONFIG;
-    }
+  GErr E;
+  bool lists = true;
+  for (size_t i = 0; i < G->ctx.size(); ++i) lists &= G->list[i] != nullptr;
+  for (int d = 0; d < G->ndev; ++d) {
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    PLUSS_HIP_CHECK(hipMemsetAsync(G->vec[d], 0, (size_t)(G->spd + 1) * DVEC * 8, G->xs[d]));
+  }
   constexpr uint32_t BATCH = 16;  // passes per captured graph
-  uint32_t left = passes;
-  if (G->ndev == 1 && passes >= BATCH) {
+  uint32_t left = passes ? passes : 1;
+  if (G->ndev == 1 && lists && left >= BATCH) {
     // one local device: BATCH passes (kernels and RCCL all-reduces) replayed from one HIP graph
     PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
     hipGraphExec_t ex = nullptr;
@@ -600,10 +764,13 @@ int pluss_group_dense(pluss_group* G, uint32_t passes, uint64_t counts[PLUSS_DEN
     } else {
       PLUSS_HIP_CHECK(hipStreamBeginCapture(G->xs[0], hipStreamCaptureModeThreadLocal));
       int rc = PLUSS_OK;
-      for (uint32_t k = 0; k < BATCH && !rc; ++k) rc = dense_pass_on_xs(G);
+      for (uint32_t k = 0; k < BATCH && !rc; ++k) rc = dense_pass_on_xs(G, E);
       hipGraph_t gr = nullptr;
       const hipError_t e = hipStreamEndCapture(G->xs[0], &gr);
-      if (rc) return rc;
+      if (rc || E.rc) {
+        if (gr) (void)hipGraphDestroy(gr);
+        return rc ? rc : E.rc;  // (host-side failures while capturing: nothing was launched)
+      }
       if (e != hipSuccess) {
         set_error(std::string("pluss_group_dense: graph capture: ") + hipGetErrorString(e));
         return PLUSS_ERR_HIP;
@@ -619,142 +786,161 @@ int pluss_group_dense(pluss_group* G, uint32_t passes, uint64_t counts[PLUSS_DEN
     for (; left >= BATCH; left -= BATCH) PLUSS_HIP_CHECK(hipGraphLaunch(ex, G->xs[0]));
   }
   for (; left; --left)
-    if (int rc = dense_pass_on_xs(G)) return rc;
-  if (int rc = dense_result(G, counts)) return rc;
-  for (size_t i = 0; i < G->ctx.size(); ++i) {  // malformed samples also raise at the handle's flags
-    unsigned int f[2] = {0, 0};
-    PLUSS_HIP_CHECK(hipMemcpy(f, G->ctx[i]->g.flags, sizeof f, hipMemcpyDeviceToHost));
-    if (f[1]) {
-      set_error("pluss_group_dense: malformed sample in shard " + std::to_string(i));
-      return PLUSS_ERR_INPUT;
-    }
-  }
-  return PLUSS_OK;
+    if (int rc = dense_pass_on_xs(G, E)) return rc;
+  unsigned long long v[GV_W];
+  const int rc = vec_fetch(G, E, v);
+  if (counts)
+    for (int b = 0; b <= PLUSS_DENSE_BINS; ++b) counts[b] = v[b];  // (malformed samples: the count, and an error)
+  return rc;
 }
 
 int pluss_group_gen_count_dense(pluss_group* G, uint64_t seed, const uint64_t totals[6],
                                 uint64_t counts[PLUSS_DENSE_BINS + 1]) {
   if (!G || !totals) return PLUSS_ERR_CONFIG;
+  GErr E;
   for (int d = 0; d < G->ndev; ++d) {
     PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    PLUSS_HIP_CHECK(hipMemsetAsync(G->vec[d], 0, (size_t)(G->spd + 1) * DVEC * 8, G->xs[d]));
+  }
+  if (int rc = fork_shards(G)) return rc;  // (the slots are cleared before the shards write them)
+  for (int d = 0; d < G->ndev; ++d) {
+    E.note(hip_rc(hipSetDevice(G->dev[d]), "hipSetDevice"));
     for (int j = 0; j < G->spd; ++j) {
       const int g = gshard(G, d, j);
       uint64_t f[6], n[6];
       for (int r = 0; r < 6; ++r) shard_ranges(totals[r], g, G->nshards, &f[r], &n[r]);
       pluss_ctx* c = shard(G, d, j);
-      if (int rc = pluss_dev_gen_count_dense(c, seed, totals, f, n, (uint64_t*)(G->vec[d] + (size_t)j * DVEC),
-                                             c->stream))
-        return rc;
+      unsigned long long* slot = G->vec[d] + (size_t)j * DVEC;
+      if (const int rc = pluss_dev_gen_count_dense(c, seed, totals, f, n, (uint64_t*)slot, c->stream)) {
+        E.note(rc);
+        hipLaunchKernelGGL(k_group_word, dim3(1), dim3(1), 0, c->stream, slot + GV_COND + GC_LOCAL, 1ull);
+      }
     }
   }
   if (int rc = dense_merge(G)) return rc;
-  return dense_result(G, counts);
+  unsigned long long v[GV_W];
+  const int rc = vec_fetch(G, E, v);
+  if (counts)
+    for (int b = 0; b <= PLUSS_DENSE_BINS; ++b) counts[b] = v[b];
+  return rc;
 }
 
 int pluss_group_sampled_hist(pluss_group* G, const uint64_t* samples, uint64_t n, pluss_hist* out) {
   if (!G || !out || (n && !samples)) return PLUSS_ERR_CONFIG;
-  if (int rc = group_reset(G)) return rc;
-  int frc = PLUSS_OK;
-  std::string ferr;
+  GErr E;
+  group_reset(G, E);
   const int S = G->nshards;
   if (G->cfg.mode == PLUSS_MODE_CLEAN) {
     // shard g: the slice [n*g/S, n*(g+1)/S) of the list, any shape
     for (int d = 0; d < G->ndev; ++d) {
-      PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+      E.note(hip_rc(hipSetDevice(G->dev[d]), "hipSetDevice"));
       for (int j = 0; j < G->spd; ++j) {
         const size_t i = (size_t)d * G->spd + j;
         uint64_t f, m;
         shard_ranges(n, gshard(G, d, j), S, &f, &m);
         if (G->hl_cap[i] < m || !G->hl[i]) {
-          PLUSS_HIP_CHECK(hipStreamSynchronize(G->ctx[i]->stream));
+          E.note(hip_rc(hipStreamSynchronize(G->ctx[i]->stream), "hipStreamSynchronize"));
           if (G->hl[i]) (void)hipFree(G->hl[i]);
           G->hl[i] = nullptr;
           G->hl_cap[i] = 0;
-          PLUSS_HIP_CHECK(hipMalloc((void**)&G->hl[i], (m ? m : 1) * 8));
+          if (const int rc = hip_rc(hipMalloc((void**)&G->hl[i], (m ? m : 1) * 8), "hipMalloc (group slice)")) {
+            G->hl[i] = nullptr;
+            E.note(rc);
+            continue;  // (this shard sends a failed slot)
+          }
           G->hl_cap[i] = m ? m : 1;
         }
-        PLUSS_HIP_CHECK(hipMemcpyAsync(G->hl[i], samples + f, m * 8, hipMemcpyHostToDevice, G->ctx[i]->stream));
-        const int rc = pluss_dev_sampled_hist(G->ctx[i], (const uint64_t*)G->hl[i], m, G->ctx[i]->stream);
-        if (rc && !frc) {
-          frc = rc;
-          ferr = pluss_last_error();
-        }
+        int rc = hip_rc(hipMemcpyAsync(G->hl[i], samples + f, m * 8, hipMemcpyHostToDevice, G->ctx[i]->stream),
+                        "hipMemcpyAsync (group slice)");
+        if (!rc) rc = pluss_dev_sampled_hist(G->ctx[i], (const uint64_t*)G->hl[i], m, G->ctx[i]->stream);
+        E.note(rc);
       }
     }
-    return group_collect(G, frc, ferr, out);
+    return collect(G, E, out);
+  }
+  if ((uint64_t)G->cfg.n % ((uint64_t)G->cfg.chunk * (uint64_t)G->cfg.threads) != 0) {
+    set_error("faithful mode needs N % (chunk*threads) == 0 (lockstep interleaving order)");
+    return PLUSS_ERR_CONFIG;  // (the same on every rank)
   }
   // faithful: r10's six samplers, each over its reference's samples in list order
   std::vector<uint64_t> per[6];
   for (uint64_t i = 0; i < n; ++i) {
     const uint32_t r = (uint32_t)(samples[i] >> 60);
     if (r > 5) {
-      set_error("malformed sample: ref > 5");
-      return PLUSS_ERR_INPUT;
+      E.note(PLUSS_ERR_INPUT, "malformed sample: ref > 5");
+      break;
     }
     per[r].push_back(samples[i]);
   }
   uint64_t totals[6], all = 0;
   for (int r = 0; r < 6; ++r) all += (totals[r] = per[r].size());
-  if ((uint64_t)G->cfg.n % ((uint64_t)G->cfg.chunk * (uint64_t)G->cfg.threads) != 0) {
-    set_error("faithful mode needs N % (chunk*threads) == 0 (lockstep interleaving order)");
-    return PLUSS_ERR_CONFIG;
-  }
   if (!G->m.fast) {
     // (key, sink) pairs (N % (cls/ds) != 0) are not key-range sharded: the job's first shard runs every sampler
-    if (G->rank0 == 0) {
-      PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
+    if (G->rank0 == 0 && !E.rc) {
+      (void)hipSetDevice(G->dev[0]);
       pluss_ctx* c = G->ctx[0];
-      for (int r = 0; r < 6 && !frc; ++r) {
+      for (int r = 0; r < 6 && !E.rc; ++r) {
         if (per[r].empty()) continue;
         uint64_t* dl = nullptr;
-        PLUSS_HIP_CHECK(hipMalloc((void**)&dl, per[r].size() * 8));
-        PLUSS_HIP_CHECK(hipMemcpy(dl, per[r].data(), per[r].size() * 8, hipMemcpyHostToDevice));
-        frc = pluss_dev_faithful_hist(c, r, dl, per[r].size(), c->stream);
-        if (frc) ferr = pluss_last_error();
-        PLUSS_HIP_CHECK(hipStreamSynchronize(c->stream));
-        (void)hipFree(dl);
+        int rc = hip_rc(hipMalloc((void**)&dl, per[r].size() * 8), "hipMalloc (group list)");
+        if (!rc) rc = hip_rc(hipMemcpy(dl, per[r].data(), per[r].size() * 8, hipMemcpyHostToDevice), "hipMemcpy");
+        if (!rc) rc = pluss_dev_faithful_hist(c, r, dl, per[r].size(), c->stream);
+        if (!rc) rc = hip_rc(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+        if (dl) (void)hipFree(dl);
+        E.note(rc);
       }
     }
-    return group_collect(G, frc, ferr, out);
+    return collect_tables(G, E, out);
   }
   // every device holds the whole lists once; each shard keeps its key range
   uint64_t key_end = 0;
-  if (int rc = pluss_faithful_key_space(&G->cfg, &key_end)) return rc;
-  for (int d = 0; d < G->ndev; ++d) {
-    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
-    if (G->whole_cap[d] < all) {
-      for (int j = 0; j < G->spd; ++j) PLUSS_HIP_CHECK(hipStreamSynchronize(shard(G, d, j)->stream));
+  E.note(pluss_faithful_key_space(&G->cfg, &key_end));
+  std::vector<int> dev_ok(G->ndev, 0);
+  for (int d = 0; d < G->ndev && !E.rc; ++d) {
+    int rc = hip_rc(hipSetDevice(G->dev[d]), "hipSetDevice");
+    if (!rc && G->whole_cap[d] < all) {
+      for (int j = 0; j < G->spd; ++j) (void)hipStreamSynchronize(shard(G, d, j)->stream);
       if (G->whole[d]) (void)hipFree(G->whole[d]);
       G->whole[d] = nullptr;
       G->whole_cap[d] = 0;
-      PLUSS_HIP_CHECK(hipMalloc((void**)&G->whole[d], (all ? all : 1) * 8));
-      G->whole_cap[d] = all;
+      rc = hip_rc(hipMalloc((void**)&G->whole[d], (all ? all : 1) * 8), "hipMalloc (group lists)");
+      if (rc) G->whole[d] = nullptr;
+      else G->whole_cap[d] = all;
     }
     uint64_t off = 0;
-    for (int r = 0; r < 6; ++r) {
-      PLUSS_HIP_CHECK(hipMemcpyAsync(G->whole[d] + off, per[r].data(), per[r].size() * 8, hipMemcpyHostToDevice, G->xs[d]));
+    for (int r = 0; r < 6 && !rc; ++r) {
+      rc = hip_rc(hipMemcpyAsync(G->whole[d] + off, per[r].data(), per[r].size() * 8, hipMemcpyHostToDevice,
+                                 G->xs[d]), "hipMemcpyAsync (group lists)");
       off += per[r].size();
     }
-    PLUSS_HIP_CHECK(hipStreamSynchronize(G->xs[d]));
+    if (!rc) rc = hip_rc(hipStreamSynchronize(G->xs[d]), "hipStreamSynchronize");
+    E.note(rc);
+    dev_ok[d] = rc == PLUSS_OK;
   }
-  auto sel = [&](pluss_ctx* c, int d, int, int g, uint64_t* row) {
+  ShardFn sel = [&](pluss_ctx* c, int d, int, int g, uint64_t* row) -> int {
+    if (!dev_ok[d]) {
+      set_error("this device's copy of the lists failed");
+      return PLUSS_ERR_PEER;
+    }
     const uint64_t lo = (uint64_t)((unsigned __int128)key_end * g / S);
     const uint64_t hi = (uint64_t)((unsigned __int128)key_end * (g + 1) / S);
     return pluss_dev_faithful_shards_select(c, (const uint64_t*)G->whole[d], totals, lo, hi, row, c->stream);
   };
-  if (int rc = group_faithful(G, true, sel, &frc, &ferr)) return rc;
-  return group_collect(G, frc, ferr, out);
+  ShardFn loc = [&](pluss_ctx* c, int d, int, int g, uint64_t* row) {
+    return pluss_dev_faithful_shards_local_selected(c, (const uint64_t*)G->rows[d], g, S, row, c->stream);
+  };
+  if (int rc = group_faithful(G, sel, loc, nullptr, E)) return rc;
+  return collect(G, E, out);
 }
 
 int pluss_group_gen_faithful(pluss_group* G, uint64_t seed, const uint64_t totals[6], pluss_hist* out) {
   if (!G || !totals || !out) return PLUSS_ERR_CONFIG;
   uint64_t key_end = 0;
-  if (int rc = pluss_faithful_key_space(&G->cfg, &key_end)) return rc;
-  if (int rc = group_reset(G)) return rc;
-  int frc = PLUSS_OK;
-  std::string ferr;
+  if (int rc = pluss_faithful_key_space(&G->cfg, &key_end)) return rc;  // (the same on every rank)
+  GErr E;
+  group_reset(G, E);
   const int S = G->nshards;
-  auto gen = [&](pluss_ctx* c, int, int, int g, uint64_t* row) {
+  ShardFn gen = [&](pluss_ctx* c, int, int, int g, uint64_t* row) -> int {
     const uint64_t lo = (uint64_t)((unsigned __int128)key_end * g / S);
     const uint64_t hi = (uint64_t)((unsigned __int128)key_end * (g + 1) / S);
     uint64_t f[6] = {0, 0, 0, 0, 0, 0}, m[6] = {0, 0, 0, 0, 0, 0};
@@ -767,8 +953,30 @@ int pluss_group_gen_faithful(pluss_group* G, uint64_t seed, const uint64_t total
     }
     return pluss_dev_faithful_shards_local(c, nullptr, seed, totals, f, m, row, c->stream);
   };
-  if (int rc = group_faithful(G, false, gen, &frc, &ferr)) return rc;
-  return group_collect(G, frc, ferr, out);
+  if (int rc = group_faithful(G, gen, nullptr, nullptr, E)) return rc;
+  return collect(G, E, out);
+}
+
+int pluss_group_gen_uniform_faithful(pluss_group* G, uint64_t seed, const uint64_t totals[6], pluss_hist* out) {
+  if (!G || !totals || !out) return PLUSS_ERR_CONFIG;
+  uint64_t key_end = 0;
+  if (int rc = pluss_faithful_key_space(&G->cfg, &key_end)) return rc;  // (the same on every rank)
+  GErr E;
+  group_reset(G, E);
+  const int S = G->nshards;
+  // phase 0: each shard's candidates; then every shard's window (enqueued on
+  // all shards before any waits for its slice), then each local pass
+  ShardFn count = [&](pluss_ctx* c, int, int, int g, uint64_t* row) {
+    return faith_shards_uniform_count(c, seed, totals, g, S, row, c->stream);
+  };
+  ShardFn window = [&](pluss_ctx* c, int d, int, int g, uint64_t*) {
+    return faith_shards_uniform_window(c, (const uint64_t*)G->rows[d], g, S, c->stream);
+  };
+  ShardFn finish = [&](pluss_ctx* c, int, int, int, uint64_t* row) {
+    return faith_shards_uniform_finish(c, row, c->stream);
+  };
+  if (int rc = group_faithful(G, count, window, finish, E)) return rc;
+  return collect(G, E, out);
 }
 
 }  // extern "C"

@@ -89,10 +89,14 @@ struct FaithfulBufs {
 struct UniSet;  // the uniform key-order generator's plan (pluss_uniform.h)
 struct UniBufs {  // its device buffers (grown on demand, per handle)
   UniSet* set = nullptr;
+  UniSet* host = nullptr;  // the host copy of *set (built by uni_plan_count, completed by uni_plan_tiles)
   uint32_t *cnt = nullptr, *bits = nullptr, *tmap = nullptr;
   uint64_t *pre = nullptr, *rb = nullptr, *bsum = nullptr;
   double* pmt = nullptr;  // the binomial pmf per leaf size (uni_count_tab)
-  size_t set_cap = 0, cnt_cap = 0, bits_cap = 0, tmap_cap = 0, pre_cap = 0, rb_cap = 0, bsum_cap = 0, pmt_cap = 0;
+  unsigned long long* info = nullptr;   // per reference: removed ranks below the plan, its first survivor, survivors
+  unsigned long long* hinfo = nullptr;  // pinned host copy of info (a key-range shard's one round trip)
+  size_t set_cap = 0, cnt_cap = 0, bits_cap = 0, tmap_cap = 0, pre_cap = 0, rb_cap = 0, bsum_cap = 0, pmt_cap = 0,
+         info_cap = 0;
 };
 
 struct FaShards;  // a key-range shard's state between the phases of pluss_dev_faithful_shards_* (pluss_faithful.h)
@@ -114,7 +118,8 @@ struct pluss_ctx {
   pluss::UniBufs ub;           // the uniform key-order generator's plan
   hipStream_t fst[6];          // ... and its streams (created on first use)
   hipEvent_t fev[7];           // fork / join events
-  hipStream_t last;   // stream of the most recent launch (fetch orders after it)
+  hipStream_t last;   // stream of the most recent launch (fetch orders after it; NULL: HIP's null stream)
+  bool has_last;      // a launch has set `last` (before the first: the handle's own stream)
   bool tables_dirty;  // hash tables may hold counts (GENERIC / faithful launches since the last reset)
 };
 
@@ -132,6 +137,8 @@ void set_error(const std::string& msg);
   } while (0)
 
 int validate_cfg(const pluss_cfg* cfg, Model* m);
+// the error reported by a pass's flags (flags[0] bits, flags[1] malformed input), or PLUSS_OK
+int flags_error(unsigned int f0, unsigned int bad, const std::string& who);
 
 // launchers (return PLUSS_OK or PLUSS_ERR_*)
 int launch_table_reset(pluss_ctx* ctx, hipStream_t s);
@@ -182,10 +189,22 @@ int faith_shards_carry(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, in
 int faith_shards_cut(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards, uint64_t* d_row,
                      hipStream_t s);
 int faith_shards_hist(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards, hipStream_t s);
+// r10's uniform law over key-range shards: candidates counted (phase 0), then
+// the window (enqueued, slice read back asynchronously) and the local pass
+int faith_shards_uniform_count(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, int32_t shard, int32_t nshards,
+                               uint64_t* d_row, hipStream_t s);
+int faith_shards_uniform_window(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards,
+                                hipStream_t s);
+int faith_shards_uniform_finish(pluss_ctx* ctx, uint64_t* d_row, hipStream_t s);
+int faith_shards_slice(pluss_ctx* ctx, uint64_t* first, uint64_t* n);
 void faith_shards_abandon(pluss_ctx* ctx);
 // r10's uniform draw in key order (pluss_uniform.h / .hip)
 int uni_check(const pluss_ctx* ctx, int32_t ref, uint64_t total, const char* api);
 int uni_plan(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t s, const UniSet** out);
+int uni_plan_count(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, uint32_t shard, uint32_t ns, hipStream_t s);
+int uni_plan_remove(pluss_ctx* ctx, const unsigned long long* rows, uint32_t shard, uint32_t ns, hipStream_t s);
+int uni_plan_tiles(pluss_ctx* ctx, const uint64_t* n, hipStream_t s, const UniSet** out);
+void uni_free(pluss_ctx* ctx);
 int launch_expand_uniform_sorted(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t total, uint64_t first,
                                  uint64_t n, uint64_t* d_out, hipStream_t s);
 int launch_gen_uniform_faithful_refs(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t s);  // a one-GPU faithful call ends any half-finished shard pass

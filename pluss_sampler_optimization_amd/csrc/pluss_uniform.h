@@ -268,6 +268,9 @@ PM_HD uint64_t uni_pack(const UniGen& u, const KeyDigits& d) {
 struct UniSet {
   UniGen u[6];
   uint64_t loff[7];     // first leaf of each reference in cnt / pre; loff[6] = all leaves
+  uint64_t lbase[6];    // the reference's leaf (in UniGen's numbering) held at loff[r]: 0 on one GPU; a
+                        // key-range shard holds the leaves [lbase, lbase + loff[r+1] - loff[r]) and ranks
+                        // its candidates from its own first one (the plan's coordinates are the shard's)
   uint64_t woff[7];     // first removal-bitmap word of each reference
   uint64_t tmoff[7];    // first tile-map entry of each reference (tiles of UG_TILE samples)
   const uint32_t* cnt;  // candidates per leaf
@@ -278,6 +281,7 @@ struct UniSet {
   unsigned int* flags;  // the handle's flags (FLAG_UNI)
   const double* pmt;    // per reference and leaf size class: pmf(0..UG_LEAFMAX + 1) of uni_count's recurrence
 };
+constexpr int UI_W = 24;  // a plan's info words (UniBufs::info): [0,6) removed ranks below it, [6,12) first, [12,18) n
 constexpr uint32_t UG_PMT = UG_LEAFMAX + 2;  // table entries per leaf size class (4 classes per reference)
 
 #if defined(__HIPCC__)
@@ -420,9 +424,10 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
   const uint32_t* __restrict__ cnt = us->cnt;
   const uint64_t* __restrict__ pre = us->pre;
   const uint64_t tm0 = us->tmoff[r], nt = us->tmoff[r + 1] - tm0, lg0 = us->loff[r];
-  const uint64_t la = us->tmap[tm0 + lt], lb = lt + 1 < nt ? us->tmap[tm0 + lt + 1] : u.L - 1;
+  const uint64_t nl = us->loff[r + 1] - lg0, lbase = us->lbase[r];  // (leaves held; their first's number)
+  const uint64_t la = us->tmap[tm0 + lt], lb = lt + 1 < nt ? us->tmap[tm0 + lt + 1] : nl - 1;
   const uint64_t pbase = pre[lg0];
-  const bool leaves_ok = la <= lb && lb < u.L;
+  const bool leaves_ok = nl > 0 && la <= lb && lb < nl;
   const uint64_t r0 = leaves_ok ? pre[lg0 + la] - pbase : 0, rend = leaves_ok ? pre[lg0 + lb + 1] - pbase : 0;
   if (!leaves_ok || rend - r0 > UG_CAP) {
     if (threadIdx.x == 0) atomicOr(flags, FLAG_UNI);
@@ -455,7 +460,7 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
       continue;
     }
     const uint64_t x0 = pre[lg0 + l] - pbase;
-    const UniLeaf f = uni_leaf(u, l);
+    const UniLeaf f = uni_leaf(u, lbase + l);
     const UniRowD rd = uni_row(u, f);
     // candidate i of the leaf (in key order) has rank x0 + i; the removed ones are skipped
     const uint32_t w0i = (uint32_t)((x0 >> 5) - wlo);
@@ -488,7 +493,7 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
     if (u.p >= 1.0) {
       for (uint32_t j = 0; j < c; ++j) emit(j, j);
     } else if (uni_direct(u, f)) {  // per-point draws: already in order
-      const uint64_t lk = uni_leafkey(u, l, 0xFFFFFFFFu);
+      const uint64_t lk = uni_leafkey(u, lbase + l, 0xFFFFFFFFu);
       uint32_t k = 0;
       for (uint32_t j = 0; j < (uint32_t)f.G && k < c; ++j)
         if (uni_u01(uni_hash(lk, j)) < u.p) emit(k++, j);
@@ -502,7 +507,7 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
           atomicOr(flags, FLAG_UNI);
           break;
         }
-        const uint64_t lk = uni_leafkey(u, l, a);
+        const uint64_t lk = uni_leafkey(u, lbase + l, a);
         if (G <= UG_PAIRG) {  // two offsets per hash; slots past every lane's count skipped
 #pragma unroll
           for (uint32_t q = 0; q < UG_NET; q += 2) {
@@ -535,7 +540,7 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
           atomicOr(flags, FLAG_UNI);
           break;
         }
-        lk = uni_leafkey(u, l, a);
+        lk = uni_leafkey(u, lbase + l, a);
         bool dup = false;
         if (off + c <= UG_SCR) {
           uint32_t* seg = scr + off;

@@ -169,42 +169,104 @@ __global__ __launch_bounds__(64) void k_ug_pmt(const UniSet* __restrict__ us, do
   }
 }
 
-// (references outermost: the generator's fields are wave-uniform, scalar loads)
+// (references outermost: the generator's fields are wave-uniform, scalar
+// loads).  Leaf l of the plan is the generator's leaf lbase[r] + l.
 __global__ __launch_bounds__(UB) void k_ug_count(const UniSet* __restrict__ us, uint32_t* __restrict__ cnt,
                                                 unsigned int* flags) {
   const uint64_t stride = (uint64_t)gridDim.x * UB;
   for (uint32_t r = 0; r < 6; ++r) {
-    const uint64_t g0 = us->loff[r], n = us->loff[r + 1] - g0;
+    const uint64_t g0 = us->loff[r], n = us->loff[r + 1] - g0, lb = us->lbase[r];
     if (!n) continue;
     const UniGen& u = us->u[r];  // (wave-uniform: scalar loads; a by-value copy went to scratch)
     const double* pmt = us->pmt + r * 4 * UG_PMT;
     for (uint64_t l = (uint64_t)blockIdx.x * UB + threadIdx.x; l < n; l += stride) {
-      const uint64_t c = uni_count_tab(u, l, pmt);
+      const uint64_t c = uni_count_tab(u, lb + l, pmt);
       if (c > UG_LEAFMAX) atomicOr(flags, FLAG_UNI);
       cnt[g0 + l] = c > UG_LEAFMAX ? UG_LEAFMAX + 1 : (uint32_t)c;
     }
   }
 }
 
-// the removal bitmaps (zeroed); T' < S or a bitmap too small for T' sets FLAG_UNI
+// The candidates of the earlier shards (X0) and of all shards (T') of
+// reference r, from the gathered summary rows of a key-range pass (rows ==
+// nullptr, one GPU: 0 and this plan's own candidates C).
+__device__ __forceinline__ void ug_window(const unsigned long long* rows, uint32_t shard, uint32_t ns, uint32_t r,
+                                          uint64_t C, uint64_t& X0, uint64_t& Tp) {
+  if (!rows) {
+    X0 = 0;
+    Tp = C;
+    return;
+  }
+  X0 = Tp = 0;
+  for (uint32_t x = 0; x < ns; ++x) {
+    const unsigned long long v = rows[(uint64_t)x * ROW_W + ROW_N + r];
+    Tp += v;
+    if (x < shard) X0 += v;
+  }
+}
+
+// The removal bitmaps (zeroed) over this plan's candidate ranks: the ranks
+// F(0 .. T'-S-1) of the removal permutation of all T' candidates that fall in
+// [X0, X0 + C), at rank - X0; those below X0 are counted into rem0[r] (every
+// shard evaluates the whole removed set, ~10 sqrt(S) ranks).  T' < S, a bitmap
+// too small for C, or rows that disagree with this plan's C set FLAG_UNI.
 __global__ __launch_bounds__(UB) void k_ug_remove(const UniSet* __restrict__ us, uint32_t* __restrict__ bits,
+                                                 const unsigned long long* __restrict__ rows, uint32_t shard,
+                                                 uint32_t ns, unsigned long long* __restrict__ rem0,
                                                  unsigned int* flags) {
   const uint64_t stride = (uint64_t)gridDim.x * UB;
   for (uint32_t r = 0; r < 6; ++r) {
     const UniGen& u = us->u[r];
-    if (us->loff[r + 1] == us->loff[r]) continue;
-    const uint64_t Tp = us->pre[us->loff[r + 1]] - us->pre[us->loff[r]];
-    if (Tp < u.S || (Tp >> 5) >= us->woff[r + 1] - us->woff[r]) {
+    if (u.S == 0) continue;  // (a reference without samples)
+    const uint64_t C = us->pre[us->loff[r + 1]] - us->pre[us->loff[r]];
+    uint64_t X0, Tp;
+    ug_window(rows, shard, ns, r, C, X0, Tp);
+    const bool bad_rows = rows && rows[(uint64_t)shard * ROW_W + ROW_N + r] != C;
+    if (Tp < u.S || (C >> 5) >= us->woff[r + 1] - us->woff[r] || bad_rows) {
       if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(flags, FLAG_UNI);
       continue;
     }
     const UniPerm P = uni_perm_make(u, Tp);
     const uint64_t m = Tp - u.S;
+    uint32_t below = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * UB + threadIdx.x; i < m; i += stride) {
       const uint64_t y = uni_perm(P, i);
-      atomicOr(&bits[us->woff[r] + (y >> 5)], 1u << (y & 31));
+      if (y < X0) {
+        ++below;
+      } else if (y - X0 < C) {
+        const uint64_t z = y - X0;
+        atomicOr(&bits[us->woff[r] + (z >> 5)], 1u << (z & 31));
+      }
+    }
+    if (rows) {
+      const uint64_t b = sc_wave_red<false>((unsigned long long)below);
+      if (__lane_id() == 0 && b) atomicAdd(&rem0[r], (unsigned long long)b);
     }
   }
+}
+
+// per reference: the list index of this plan's first survivor (X0 minus the
+// removed ranks below X0; 0 on one GPU) and its survivors (C minus the ranks
+// removed in its window) -> info[6 + r], info[12 + r]
+__global__ void k_ug_info(const UniSet* __restrict__ us, const unsigned long long* __restrict__ rows, uint32_t shard,
+                          uint32_t ns, unsigned long long* __restrict__ info) {
+  const uint32_t r = threadIdx.x;
+  if (r >= 6) return;
+  const UniGen& u = us->u[r];
+  unsigned long long first = 0, n = 0;
+  if (u.S) {
+    const uint64_t C = us->pre[us->loff[r + 1]] - us->pre[us->loff[r]];
+    uint64_t X0, Tp;
+    ug_window(rows, shard, ns, r, C, X0, Tp);
+    const uint64_t removed = us->rb[us->woff[r + 1]] - us->rb[us->woff[r]];
+    const uint64_t below = rows ? info[r] : 0ull;
+    first = X0 >= below ? X0 - below : 0ull;
+    n = C >= removed ? C - removed : 0ull;
+    if (first > u.S) first = u.S;  // (a flagged plan: kept in range, reported at the fetch)
+    if (n > u.S - first) n = u.S - first;
+  }
+  info[6 + r] = first;
+  info[12 + r] = n;
 }
 
 // per leaf: the sample index of its first surviving candidate and their
@@ -272,42 +334,60 @@ int uni_check(const pluss_ctx* ctx, int32_t ref, uint64_t total, const char* api
   return PLUSS_OK;
 }
 
-// The plan of the references with totals[r] > 0 on stream s; *out = its
-// device UniSet (valid until the next plan on this handle).
-int uni_plan(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t s, const UniSet** out) {
+// The plan, in three parts on stream s (ctx->ub; valid until the next plan on
+// this handle):
+//   uni_plan_count   the generators, this plan's leaves of each reference
+//                    (one GPU: all of them; key-range shard `shard` of `ns`:
+//                    the leaves [L*shard/ns, L*(shard+1)/ns)), their candidate
+//                    counts and the counts' prefix;
+//   uni_plan_remove  the removal bitmap over this plan's candidates (rows: the
+//                    gathered summary rows of the shards' candidate counts,
+//                    nullptr on one GPU), its prefix, and per reference the
+//                    list index of the plan's first survivor and their number
+//                    (ub.info[6 + r], [12 + r]);
+//   uni_plan_tiles   the leaf holding each tile's first sample for n[r]
+//                    samples per reference; *out = the device UniSet.
+int uni_plan_count(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, uint32_t shard, uint32_t ns, hipStream_t s) {
   UniBufs& b = ctx->ub;
-  UniSet h;
+  if (!b.host) b.host = new UniSet();
+  UniSet& h = *b.host;
   std::memset((void*)&h, 0, sizeof h);
-  uint64_t L = 0, Wd = 0, Tt = 0;
+  uint64_t L = 0, Wd = 0;
   for (int r = 0; r < 6; ++r) {
     h.loff[r] = L;
     h.woff[r] = Wd;
-    h.tmoff[r] = Tt;
     if (!totals[r]) continue;
     if (int rc = uni_check(ctx, r, totals[r], "uniform key-order lists")) return rc;
     h.u[r] = make_unigen((uint64_t)ctx->cfg.n, (uint64_t)ctx->cfg.threads, (uint64_t)ctx->cfg.chunk,
                          ctx->cfg.range_full != 0, seed, (uint32_t)r, totals[r]);
-    L += h.u[r].L;
-    // room for T' candidates: its mean plus 20 standard deviations (or all points when p = 1)
-    const double E = h.u[r].p * (double)h.u[r].D;
+    const uint64_t Lr = h.u[r].L;
+    const uint64_t la = (uint64_t)((unsigned __int128)Lr * shard / ns), lb = (uint64_t)((unsigned __int128)Lr * (shard + 1) / ns);
+    h.lbase[r] = la;
+    L += lb - la;
+    // room for this plan's candidates: their mean plus 20 standard deviations (or every point when p = 1)
+    const double pts = std::min((double)h.u[r].D, (double)(lb - la) * (double)h.u[r].K * (double)h.u[r].T);
+    const double E = h.u[r].p * pts;
     const uint64_t tmax = (uint64_t)(E + 20.0 * std::sqrt(E) + 1024.0);
     Wd += tmax / 32 + 2;
-    Tt += fa_tiles(totals[r]);
   }
   h.loff[6] = L;
   h.woff[6] = Wd;
-  h.tmoff[6] = Tt;
   const uint64_t nbL = (L + UBATCH - 1) / UBATCH + 1, nbW = (Wd + UBATCH - 1) / UBATCH + 1;
   int rc = PLUSS_OK;
   if (!b.set) rc = ug_grow((void**)&b.set, &b.set_cap, sizeof(UniSet));
+  if (!rc && !b.info) rc = ug_grow((void**)&b.info, &b.info_cap, UI_W * 8);
   if (!rc) rc = ug_grow((void**)&b.cnt, &b.cnt_cap, (L + 1) * 4);
   if (!rc) rc = ug_grow((void**)&b.pre, &b.pre_cap, (L + 1) * 8);
   if (!rc) rc = ug_grow((void**)&b.bits, &b.bits_cap, (Wd + 1) * 4);
   if (!rc) rc = ug_grow((void**)&b.rb, &b.rb_cap, (Wd + 1) * 8);
-  if (!rc) rc = ug_grow((void**)&b.tmap, &b.tmap_cap, (Tt + 1) * 4);
   if (!rc) rc = ug_grow((void**)&b.pmt, &b.pmt_cap, 6 * 4 * UG_PMT * sizeof(double));
   if (!rc) rc = ug_grow((void**)&b.bsum, &b.bsum_cap, (nbL > nbW ? nbL : nbW) * 8 + 8);
   if (rc) return rc;
+  if (!b.hinfo && hipHostMalloc((void**)&b.hinfo, UI_W * 8) != hipSuccess) {
+    b.hinfo = nullptr;
+    set_error("hipHostMalloc failed for the uniform generator's plan");
+    return PLUSS_ERR_ALLOC;
+  }
   h.cnt = b.cnt;
   h.pre = b.pre;
   h.bits = b.bits;
@@ -321,14 +401,59 @@ int uni_plan(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t 
   hipLaunchKernelGGL(k_ug_pmt, dim3(24), dim3(64), 0, s, (const UniSet*)b.set, b.pmt);
   hipLaunchKernelGGL(k_ug_count, dim3(grid), dim3(UB), 0, s, (const UniSet*)b.set, b.cnt, ctx->g.flags);
   if (int e = ug_scan(b.cnt, L, b.bsum, b.pre, 0, s)) return e;
+  PLUSS_HIP_CHECK(hipGetLastError());
+  return PLUSS_OK;
+}
+
+int uni_plan_remove(pluss_ctx* ctx, const unsigned long long* rows, uint32_t shard, uint32_t ns, hipStream_t s) {
+  UniBufs& b = ctx->ub;
+  const uint64_t Wd = b.host->woff[6];
   PLUSS_HIP_CHECK(hipMemsetAsync(b.bits, 0, (Wd + 1) * 4, s));
-  PLUSS_HIP_CHECK(hipMemsetAsync(b.tmap, 0, (Tt + 1) * 4, s));
-  hipLaunchKernelGGL(k_ug_remove, dim3(1024), dim3(UB), 0, s, (const UniSet*)b.set, b.bits, ctx->g.flags);
+  PLUSS_HIP_CHECK(hipMemsetAsync(b.info, 0, UI_W * 8, s));
+  hipLaunchKernelGGL(k_ug_remove, dim3(1024), dim3(UB), 0, s, (const UniSet*)b.set, b.bits, rows, shard, ns, b.info,
+                     ctx->g.flags);
   if (int e = ug_scan(b.bits, Wd, b.bsum, b.rb, 1, s)) return e;
+  hipLaunchKernelGGL(k_ug_info, dim3(1), dim3(64), 0, s, (const UniSet*)b.set, rows, shard, ns, b.info);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  return PLUSS_OK;
+}
+
+int uni_plan_tiles(pluss_ctx* ctx, const uint64_t* n, hipStream_t s, const UniSet** out) {
+  UniBufs& b = ctx->ub;
+  UniSet& h = *b.host;
+  uint64_t Tt = 0;
+  for (int r = 0; r < 6; ++r) {
+    h.tmoff[r] = Tt;
+    Tt += fa_tiles(n[r]);
+  }
+  h.tmoff[6] = Tt;
+  if (int rc = ug_grow((void**)&b.tmap, &b.tmap_cap, (Tt + 1) * 4)) return rc;
+  h.tmap = b.tmap;
+  hipLaunchKernelGGL(k_ug_setup, dim3(1), dim3(1), 0, s, h, b.set);
+  PLUSS_HIP_CHECK(hipMemsetAsync(b.tmap, 0, (Tt + 1) * 4, s));
+  const uint64_t L = h.loff[6];
+  const int grid = (int)std::min<uint64_t>((L + UB - 1) / UB + 1, 4096);
   hipLaunchKernelGGL(k_ug_tiles, dim3(grid), dim3(UB), 0, s, (const UniSet*)b.set, b.tmap);
   PLUSS_HIP_CHECK(hipGetLastError());
   *out = b.set;
   return PLUSS_OK;
+}
+
+void uni_free(pluss_ctx* ctx) {
+  UniBufs& b = ctx->ub;
+  void* ub[] = {b.set, b.cnt, b.bits, b.tmap, b.pre, b.rb, b.bsum, b.pmt, b.info};
+  for (void* p : ub)
+    if (p) (void)hipFree(p);
+  if (b.hinfo) (void)hipHostFree(b.hinfo);
+  delete b.host;
+  b = UniBufs();
+}
+
+// The whole plan of the lists on one GPU (every leaf; n = totals)
+int uni_plan(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t s, const UniSet** out) {
+  if (int rc = uni_plan_count(ctx, seed, totals, 0, 1, s)) return rc;
+  if (int rc = uni_plan_remove(ctx, nullptr, 0, 1, s)) return rc;
+  return uni_plan_tiles(ctx, totals, s, out);
 }
 
 int launch_expand_uniform_sorted(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t total, uint64_t first,

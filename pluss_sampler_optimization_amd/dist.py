@@ -280,8 +280,9 @@ def merge_results(ctx, err, dev, group=None):
 def _pass_stream(dev, stream):
     """The torch stream a sharded faithful pass runs on: the library's phases,
     the row exchanges (DeviceRows) and the merge all on it, so they are
-    ordered.  The legacy null stream is never used: the library would take
-    its own stream for it (stream == NULL), unordered with torch's copies."""
+    ordered.  A caller on the null stream gets a stream of its own for the
+    pass (the library would take NULL as HIP's null stream, which is ordered
+    too but serialises against every other stream of the device)."""
     import torch
     st = stream if stream is not None else torch.cuda.current_stream(dev)
     return torch.cuda.Stream(dev) if st.cuda_stream == 0 else st

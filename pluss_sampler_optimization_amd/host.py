@@ -14,7 +14,7 @@ import os
 
 import numpy as np
 
-from ._lib import PlussError, PlussHistEntry
+from ._lib import PlussError, PlussHist, PlussHistEntry
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 HOST_LIB_PATH = os.path.join(HERE, "lib", "libpluss_host.so")
@@ -43,8 +43,11 @@ def host_lib():
         L.pluss_format_hist.argtypes = [ctypes.c_char_p, P(PlussKV), ctypes.c_uint64, ctypes.c_char_p,
                                         ctypes.c_uint64, u64p]
         L.pluss_format_mrc.argtypes = [P(PlussKV), ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64, u64p]
+        L.pluss_r10_host_pipeline.argtypes = [ctypes.c_int64, P(PlussHist), ctypes.c_int32, P(PlussKV),
+                                              ctypes.c_uint64, u64p, P(PlussKV), ctypes.c_uint64, u64p,
+                                              ctypes.c_char_p, ctypes.c_uint64, u64p]
         for f in (L.pluss_cri_r10, L.pluss_cri_v1, L.pluss_log2_merge, L.pluss_aet,
-                  L.pluss_format_hist, L.pluss_format_mrc):
+                  L.pluss_format_hist, L.pluss_format_mrc, L.pluss_r10_host_pipeline):
             f.restype = ctypes.c_int
         _hl = L
     return _hl
@@ -193,10 +196,46 @@ def mrc_from_r10(threads, hist):
     return per_ref, reuse, aet(reuse)
 
 
-def mrc_text_from_r10(threads, hist):
-    """mrc_from_r10 down to the reference's MRC printout (pluss_print_mrc),
-    the curve kept in an array: r10's whole host part after the samplers.
-    Returns (reuse_histogram, mrc_text)."""
-    reuse = log2_merge(*[r10_sampler_output(threads, b) for b in
-                         ({k: v for k, v in hist.bins.items() if k[0] == ref} for ref in REFS) if b])
-    return reuse, format_mrc(aet_array(reuse))
+def r10_pipeline(threads, hist, workers=0, want_mrc=False):
+    """r10's whole host half after the samplers in ONE native call
+    (pluss_r10_host_pipeline, r10:3203-3277): the six references' CRI on
+    `workers` host threads (0: one per reference, as r10's sampler threads
+    run them), the floor-log2 merge in r10's reference order, pluss_AET and
+    pluss_print_mrc.  `hist`: a Histogram of all six references' raw bins.
+    Returns (reuse_histogram {key: count}, mrc_text[, mrc array])."""
+    items = [(REFS.index(r), k, ri, c) for (r, k, ri), c in hist.bins.items()]
+    arr = (PlussHistEntry * max(1, len(items)))()
+    for i, (r, k, ri, c) in enumerate(items):
+        arr[i].ref, arr[i].kind, arr[i].ri, arr[i].count = r, k, ri, c
+    h = PlussHist()
+    h.entries = arr
+    h.capacity = len(arr)
+    h.n_entries = len(items)
+    L = host_lib()
+    nr, nm, nt = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    rc = L.pluss_r10_host_pipeline(threads, ctypes.byref(h), workers, None, 0, ctypes.byref(nr), None, 0,
+                                   ctypes.byref(nm), None, 0, ctypes.byref(nt))
+    if rc:
+        raise PlussError(f"pluss_r10_host_pipeline: rc={rc}")
+    reuse = np.empty(max(1, nr.value), _KV)
+    mrc = np.empty(max(1, nm.value), _KV) if want_mrc else None
+    buf = ctypes.create_string_buffer(nt.value + 1)
+    rc = L.pluss_r10_host_pipeline(threads, ctypes.byref(h), workers, reuse.ctypes.data_as(ctypes.POINTER(PlussKV)),
+                                   len(reuse), ctypes.byref(nr),
+                                   mrc.ctypes.data_as(ctypes.POINTER(PlussKV)) if want_mrc else None,
+                                   len(mrc) if want_mrc else 0, ctypes.byref(nm), buf, nt.value + 1,
+                                   ctypes.byref(nt))
+    if rc:
+        raise PlussError(f"pluss_r10_host_pipeline: rc={rc}")
+    m = int(nr.value)
+    rd = dict(zip(reuse["key"][:m].tolist(), reuse["value"][:m].tolist()))
+    if want_mrc:
+        return rd, buf.value.decode(), mrc[:int(nm.value)]
+    return rd, buf.value.decode()
+
+
+def mrc_text_from_r10(threads, hist, workers=0):
+    """r10's whole host part after the samplers, down to the reference's MRC
+    printout (pluss_print_mrc): one native call (r10_pipeline).  Returns
+    (reuse_histogram, mrc_text)."""
+    return r10_pipeline(threads, hist, workers)

@@ -254,12 +254,14 @@ def _torch_stream(request):
     torch.cuda.synchronize()
 
 
-def gpu_lockstep(ctxs, phase1s, stream, selected=False):
+def gpu_lockstep(ctxs, phase1s, stream, selected=False, mid=None):
     """The pluss_dev_faithful_shards_* phases over several handles on one GPU,
     one handle per shard: the summary rows live in a device tensor and are
     "all-gathered" by a device copy on the current stream between phases (what
     an RCCL all-gather does across GPUs).  phase1s[i](ctx, d_row) runs shard
-    i's first phase."""
+    i's first phase; a source whose local phase needs the gathered rows runs it
+    after the first gather: selected=True (local_selected) or mid(ctx, i, ns,
+    d_rows, d_row) (e.g. the uniform source's uniform_local)."""
     import torch
     from pluss_sampler_optimization_amd import SHARD_ROW
     ns = len(ctxs)
@@ -272,8 +274,10 @@ def gpu_lockstep(ctxs, phase1s, stream, selected=False):
         p1(ctx, rows[i].data_ptr())
     gather()
     if selected:
+        mid = lambda ctx, i, ns_, grows, row: ctx.faithful_shards_local_selected(grows, i, ns_, row, stream)  # noqa
+    if mid is not None:
         for i, ctx in enumerate(ctxs):
-            ctx.faithful_shards_local_selected(g.data_ptr(), i, ns, rows[i].data_ptr(), stream)
+            mid(ctx, i, ns, g.data_ptr(), rows[i].data_ptr())
         gather()
     for name in ("carry", "cut"):
         for i, ctx in enumerate(ctxs):

@@ -51,6 +51,26 @@ static pluss_hist new_hist(void) {
   return h;
 }
 
+/* a merged dense vector vs the whole list's histogram (bins of one key -- a
+   reference's unused cases -- summed; no count outside the list's keys) */
+static int dense_matches(const pluss_cfg* cfg, const uint64_t* gv, const pluss_hist* b) {
+  uint64_t keys[PLUSS_DENSE_BINS];
+  if (pluss_dense_keys(cfg, keys)) return 0;
+  int ok = gv[PLUSS_DENSE_BINS] == 0;
+  uint64_t total_dense = 0;
+  for (int k = 0; k < PLUSS_DENSE_BINS; ++k) total_dense += gv[k];
+  for (uint64_t i = 0; i < b->n_entries; ++i) {
+    const pluss_hist_entry* e = &b->entries[i];
+    const uint64_t key = ((uint64_t)e->ref << 60) | ((uint64_t)e->kind << 56) | (uint64_t)(e->ri + 2);
+    uint64_t got = 0;
+    for (int k = 0; k < PLUSS_DENSE_BINS; ++k)
+      if (keys[k] == key) got += gv[k];
+    ok &= got == e->count;
+    total_dense -= got;
+  }
+  return ok && total_dense == 0;
+}
+
 int main(int argc, char** argv) {
   if (argc < 6) {
     fprintf(stderr, "usage: %s N THREADS TOTAL SHARDS_PER_DEVICE DEVICE...\n", argv[0]);
@@ -91,25 +111,35 @@ int main(int argc, char** argv) {
 
     /* resident lists, dense passes (the bench step), RCCL all-reduce: the
        merged vector of the last of 20 passes vs the whole list's histogram */
-    uint64_t gv[PLUSS_DENSE_BINS + 1], ov[PLUSS_DENSE_BINS + 1], keys[PLUSS_DENSE_BINS];
+    uint64_t gv[PLUSS_DENSE_BINS + 1], ov[PLUSS_DENSE_BINS + 1];
     CHECK(pluss_group_expand(g, seed, counts));
     CHECK(pluss_group_dense(g, 20, gv));
-    CHECK(pluss_dense_keys(&clean, keys));
-    /* (bins of one key -- a reference's unused cases -- summed) vs the whole list's histogram */
-    int ok = gv[PLUSS_DENSE_BINS] == 0;
-    uint64_t total_dense = 0;
-    for (int k = 0; k < PLUSS_DENSE_BINS; ++k) total_dense += gv[k];
-    for (uint64_t i = 0; i < b.n_entries; ++i) {
-      const pluss_hist_entry* e = &b.entries[i];
-      const uint64_t key = ((uint64_t)e->ref << 60) | ((uint64_t)e->kind << 56) | (uint64_t)(e->ri + 2);
-      uint64_t got = 0;
-      for (int k = 0; k < PLUSS_DENSE_BINS; ++k)
-        if (keys[k] == key) got += gv[k];
-      ok &= got == e->count;
-      total_dense -= got;
+    report("clean dense x20 (resident lists)", dense_matches(&clean, gv, &b));
+
+    /* the lists changed under a captured pass: expand other counts, then 32
+       passes (replayed from a graph of 16) must count the new lists */
+    {
+      uint64_t counts2[6], total2 = total / 2 + 7;
+      CHECK(pluss_default_counts(N, total2, counts2));
+      uint64_t* list2 = (uint64_t*)malloc(total2 * sizeof(uint64_t));
+      uint64_t o2 = 0;
+      for (int r = 0; r < 6; ++r) {
+        CHECK(pluss_expand_samples(&clean, seed + 1, r, 0, counts2[r], list2 + o2));
+        o2 += counts2[r];
+      }
+      pluss_hist b2 = new_hist();
+      CHECK(pluss_gemm_sampled_hist(&clean, list2, total2, &b2));
+      CHECK(pluss_group_dense(g, 32, gv));
+      CHECK(pluss_group_expand(g, seed + 1, counts2));
+      CHECK(pluss_group_dense(g, 32, gv));
+      int ok2 = dense_matches(&clean, gv, &b2);
+      CHECK(pluss_group_expand(g, seed, counts));
+      CHECK(pluss_group_dense(g, 32, gv));
+      ok2 &= dense_matches(&clean, gv, &b);
+      report("clean dense x32 after re-expanding", ok2);
+      free(b2.entries);
+      free(list2);
     }
-    ok &= total_dense == 0;  /* no count outside the list's keys */
-    report("clean dense x20 (resident lists)", ok);
 
     /* generated key-order slices counted, vs one shard on one device */
     CHECK(pluss_group_gen_count_dense(g, seed, counts, gv));
@@ -141,6 +171,16 @@ int main(int argc, char** argv) {
     CHECK(pluss_dev_gen_faithful_refs(c, seed, counts, NULL));
     CHECK(pluss_hist_fetch(c, &c2));
     report("faithful gen_faithful (key-order lists)", same_hist(&c1, &c2));
+
+    /* r10's own law: each shard generates only its stretch of the uniform lists */
+    pluss_hist u1 = new_hist(), u2 = new_hist();
+    CHECK(pluss_group_gen_uniform_faithful(g, seed, counts, &u1));
+    CHECK(pluss_dev_hist_reset(c, NULL));
+    CHECK(pluss_dev_gen_uniform_faithful_refs(c, seed, counts, NULL));
+    CHECK(pluss_hist_fetch(c, &u2));
+    report("faithful gen_uniform_faithful (r10's law)", same_hist(&u1, &u2));
+    free(u1.entries);
+    free(u2.entries);
     pluss_ctx_destroy(c);
     pluss_group_destroy(g);
     free(a.entries);

@@ -9,6 +9,8 @@ Run on an MI355X:  python -m pytest tests/test_gpu_uniform.py -m gpu -x -q
 import numpy as np
 import pytest
 
+from conftest import gpu_lockstep
+
 pytestmark = pytest.mark.gpu
 
 P = pytest.importorskip("pluss_sampler_optimization_amd")
@@ -90,3 +92,89 @@ def test_config3_uniform_pass(orc):
     oc = orc.cfg(N, T)
     for a in (0, n2 // 2, n2 - 50_000):
         np.testing.assert_array_equal(c2[a:a + 50_000], orc.expand_uniform(oc, SEED, "C2", n2, a, 50_000))
+
+
+@pytest.mark.parametrize("spd", [1, 3, 8])
+@pytest.mark.parametrize("N,T,total", [(64, 4, 12_000), (128, 4, 8720 * 4), (256, 4, 200_000)])
+def test_group_over_uniform_lists(orc, N, T, total, spd):
+    """test_faithful_over_uniform_lists through the C-ABI group (key-range
+    shards, each generating only its stretch of the uniform lists): the
+    stepping r10 oracle on the same lists."""
+    c = P.SamplerConfig(n=N, threads=T, mode="faithful")
+    totals = P.default_counts(N, total)
+    with P.Group(c, [0], spd) as g:
+        h = g.gen_uniform_faithful(SEED, totals)
+    oc = orc.cfg(N, T)
+    for r, ref in enumerate(P.REFS):
+        want, wtrav = orc.faithful(oc, ref, orc.expand_uniform(oc, SEED, ref, totals[r], 0, totals[r]))
+        assert {k: v for k, v in h.bins.items() if k[0] == ref} == want, (ref, spd)
+        assert h.traversed[r] == wtrav, (ref, spd)
+
+
+# Uniform lists dense enough for Q1 to cut the 2-D references about half way
+# (57 % recorded), the 3-D ones sparse (replays chained across tiles); B0 only
+# where the oracle's share replays stay affordable (each is (N-7)(4N+2)
+# lockstep accesses per thread)
+DENSE = {1024: [500_000, 500_000, 20_000, 40, 300_000, 300_000],
+         4096: [8_000_000, 8_000_000, 3_000, 0, 1_000_000, 1_000_000]}
+
+
+@pytest.mark.parametrize("N", [1024, 4096])
+def test_uniform_source_vs_oracle_at_baseline_n(orc, N):
+    """The faithful pass over r10's law generated inside the pipeline, at the
+    BASELINE configs' N (2 and 3): equal to the stepping r10 oracle
+    (orc_faithful) replaying the oracle's own uniform lists, through one GPU
+    and through a group of 5 logical shards; Q1 cuts C0/C1 inside the list."""
+    T = 8
+    c = P.SamplerConfig(n=N, threads=T, mode="faithful")
+    totals = DENSE[N]
+    with P.Context(c) as ctx:
+        ctx.reset(stream())
+        ctx.gen_uniform_faithful_refs(SEED, totals, stream())
+        one = ctx.fetch()
+    with P.Group(c, [0], 5) as g:
+        grp = g.gen_uniform_faithful(SEED, totals)
+    assert grp.bins == one.bins and grp.traversed == one.traversed
+    oc = orc.cfg(N, T)
+    for r, ref in enumerate(P.REFS):
+        if not totals[r]:
+            continue
+        want, wtrav = orc.faithful(oc, ref, orc.expand_uniform(oc, SEED, ref, totals[r], 0, totals[r]))
+        assert {k: v for k, v in one.bins.items() if k[0] == ref} == want, (N, ref)
+        assert one.traversed[r] == wtrav, (N, ref)
+    for ref in ("C0", "C1"):  # Q1 cut inside the list
+        rec = sum(v for k, v in one.bins.items() if k[0] == ref and k[2] != -1)
+        assert 0.3 * totals[P.REF_ID[ref]] < rec < 0.8 * totals[P.REF_ID[ref]]
+
+
+def test_uniform_key_range_shards_by_hand(orc):
+    """The uniform source's shard phases (uniform_count, gather,
+    uniform_local, carry, cut, hist) run by hand over 6 handles on one GPU at
+    config 2's shape: the shards' slices tile every list in order, and the
+    merged histogram equals one GPU's pass."""
+    N, T = 1024, 8
+    c = P.SamplerConfig(n=N, threads=T, mode="faithful")
+    totals = P.default_counts(N, 1 << 22)
+    with P.Context(c) as ctx:
+        ctx.reset(stream())
+        ctx.gen_uniform_faithful_refs(SEED, totals, stream())
+        want = ctx.fetch()
+    ns = 6
+    ctxs = [P.Context(c) for _ in range(ns)]
+    for ctx in ctxs:
+        ctx.reset(stream())
+    gpu_lockstep(ctxs, [lambda ctx, row, k=k: ctx.faithful_shards_uniform_count(SEED, totals, k, ns, row, stream())
+                        for k in range(ns)], stream(),
+                 mid=lambda ctx, i, n_, grows, row: ctx.faithful_shards_uniform_local(grows, i, n_, row, stream()))
+    bins, trav, nxt = {}, [0] * 6, [0] * 6
+    for ctx in ctxs:
+        for r, (first, n) in enumerate(ctx.faithful_shards_slice()):
+            assert first == nxt[r] or n == 0, (r, first, nxt[r])
+            nxt[r] = first + n if n else nxt[r]
+        h = ctx.fetch()
+        for key, v in h.bins.items():
+            bins[key] = bins.get(key, 0) + v
+        trav = [(a + b) % (1 << 64) for a, b in zip(trav, h.traversed)]
+        ctx.close()
+    assert nxt == totals
+    assert bins == want.bins and trav == list(want.traversed)

@@ -47,8 +47,44 @@ def test_c_group_equals_one_device(tmp_path, N, T, total, spd):
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
     lines = [x for x in r.stdout.strip().splitlines() if x.split(" ")[0] in ("shards", "ok", "MISMATCH")]  # (RCCL's banner)
     assert lines[0] == f"shards {spd} of {spd}"
-    assert lines[1:] == ["ok clean sampled_hist", "ok clean dense x20 (resident lists)", "ok clean gen_count_dense",
-                         "ok faithful sampled_hist (any order)", "ok faithful gen_faithful (key-order lists)"]
+    assert lines[1:] == ["ok clean sampled_hist", "ok clean dense x20 (resident lists)",
+                         "ok clean dense x32 after re-expanding", "ok clean gen_count_dense",
+                         "ok faithful sampled_hist (any order)", "ok faithful gen_faithful (key-order lists)",
+                         "ok faithful gen_uniform_faithful (r10's law)"]
+
+
+STREAM_SRC = os.path.join(ROOT, "tests", "helpers", "stream_main.c")
+
+
+def build_stream(out_dir):
+    if not os.path.exists(os.path.join(LIBDIR, "libpluss_gpu.so")):
+        pytest.skip("libraries not built")
+    exe = os.path.join(out_dir, "stream_main")
+    cc = shutil.which("gcc") or pytest.skip("no gcc")
+    r = subprocess.run([cc, "-O2", "-std=c11", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__", "-I",
+                        os.path.join(ROOT, "include"), "-I", "/opt/rocm/include", "-o", exe, STREAM_SRC, "-L", LIBDIR,
+                        "-lpluss_gpu", "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{LIBDIR}",
+                        "-Wl,-rpath,/opt/rocm/lib"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return exe
+
+
+def test_stream_caller_compiles_and_links(tmp_path):
+    exe = build_stream(str(tmp_path))
+    assert "libpluss_gpu.so" in subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
+
+
+@pytest.mark.gpu
+def test_null_stream_orders_with_callers_work(tmp_path):
+    """stream == NULL is HIP's null stream (include/pluss_gpu.h): a C caller's
+    null-stream memsets and copies interleaved with library calls on NULL
+    need no synchronisation of their own (round 4's g2 race)."""
+    exe = build_stream(str(tmp_path))
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    lines = [x for x in r.stdout.strip().splitlines() if x.split(" ")[0] in ("ok", "MISMATCH")]
+    assert lines == ["ok caller memset -> pass on NULL"] * 3 + ["ok library expand on NULL -> caller copy",
+                                                                "ok pass on pluss_ctx_stream"]
 
 
 P = None
@@ -77,6 +113,28 @@ def test_group_reproduces_reference_dumps(orc, name, d, smp, spd):
         exp, etrav = expected_raw(d, ref)
         assert {k: v for k, v in h.bins.items() if k[0] == ref} == exp, (name, ref)
         assert h.traversed[r] == etrav, (name, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spd", [1, 8])
+@pytest.mark.parametrize("N,T,total", [(128, 4, 50000), (256, 8, 400000), (1024, 8, 1 << 20)])
+def test_group_uniform_faithful_equals_one_device(N, T, total, spd):
+    """r10's own law over key-range shards (each shard generating only its
+    stretch of the uniform lists): the one-device pass over the same lists,
+    and, at N=128, the stepping r10 oracle over the materialised lists."""
+    P = _P()
+    c = P.SamplerConfig(n=N, threads=T, mode="faithful")
+    counts = P.default_counts(N, total)
+    with P.Group(c, [0], spd) as g:
+        h = g.gen_uniform_faithful(77, counts)
+    import torch
+    st = torch.cuda.Stream()
+    with P.Context(c) as ctx:
+        ctx.reset(st.cuda_stream)
+        ctx.gen_uniform_faithful_refs(77, counts, st.cuda_stream)
+        st.synchronize()
+        one = ctx.fetch()
+    assert h.bins == one.bins and h.traversed == one.traversed
 
 
 @pytest.mark.gpu

@@ -68,11 +68,13 @@ def test_v1_fulltrace_pipeline_matches_seq_acc_output(orc):
     assert str(trav) == _section(txt, titles[4], titles)[0]
 
 
-@pytest.mark.parametrize("name,d,smp", GOLD[:3], ids=[g[0] for g in GOLD[:3]])
-def test_array_path_equals_dict_path(name, d, smp):
-    """host.mrc_text_from_r10 (the curve kept in an array: the bench's
-    pipeline leg) prints the same text as the dict path, and aet_array holds
-    aet's points in key order."""
+@pytest.mark.parametrize("name,d,smp", GOLD, ids=[g[0] for g in GOLD])
+def test_native_pipeline_matches_reference_printout(name, d, smp):
+    """pluss_r10_host_pipeline (host.mrc_text_from_r10: the six CRI steps on
+    host threads, the merge in r10's reference order, AET, the MRC text) in
+    one native call: the reference's printed reuse histogram and MRC, the
+    chained calls' results to the last few ulps, the same text with one
+    worker or six, and the points (want_mrc) those of pluss_aet."""
     import numpy as np
 
     class Hh:
@@ -80,10 +82,35 @@ def test_array_path_equals_dict_path(name, d, smp):
     per = {ref: H.r10_sampler_output(d["T"], _raw_bins(d, ref)) for ref in ORDER}
     reuse = H.log2_merge(*[per[r] for r in H.REFS])
     r2, text = H.mrc_text_from_r10(d["T"], Hh)
-    assert r2 == reuse
-    assert text == H.format_mrc(H.aet(reuse))
-    a = H.aet_array(reuse)
-    assert list(a["key"]) == sorted(H.aet(reuse)) and (np.diff(a["key"]) > 0).all()
+    assert set(r2) == set(reuse) and all(abs(r2[k] - reuse[k]) <= 1e-12 * abs(reuse[k]) for k in reuse)
+    assert _rows(H.format_hist("Start to dump reuse time", r2)) == d["printed"]["reuse"]
+    assert _rows(text) == d["printed"]["mrc"]
+    assert text == H.format_mrc(H.aet(r2))
+    r3, text1, pts = H.r10_pipeline(d["T"], Hh, workers=1, want_mrc=True)
+    assert r3 == r2 and text1 == text
+    a = H.aet_array(r2)
+    assert (pts["key"] == a["key"]).all() and (pts["value"] == a["value"]).all()
+    assert list(a["key"]) == sorted(H.aet(r2)) and (np.diff(a["key"]) > 0).all()
+
+
+def test_aet_jumps_equal_the_reference_walk(tmp_path):
+    """pluss_aet takes the walk's runs of equal additions in jumps (integer
+    arithmetic in ulps, ties and binade ends made one by one): on random
+    histograms (keys up to 2^29, fractional counts, cold keys) every point
+    equals the reference's one-addition-per-t walk bit for bit
+    (tests/helpers/aet_check.cpp restates pluss_AET, pluss_utils.h:758-804)."""
+    import shutil
+    import subprocess
+    root = os.path.dirname(GOLDEN.rstrip("/").rsplit("/", 1)[0])
+    lib = os.path.join(root, "pluss_sampler_optimization_amd", "lib")
+    exe = str(tmp_path / "aet_check")
+    cxx = shutil.which("g++") or pytest.skip("no g++")
+    r = subprocess.run([cxx, "-O2", "-std=c++17", "-I", os.path.join(root, "include"), "-o", exe,
+                        os.path.join(root, "tests", "helpers", "aet_check.cpp"), "-L", lib, "-lpluss_host",
+                        f"-Wl,-rpath,{lib}"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    r = subprocess.run([exe, "60", "11"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok 60 cases"), r.stdout[-2000:]
 
 
 def test_format_mrc_any_key_order():
