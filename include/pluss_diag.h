@@ -36,6 +36,15 @@ int pluss_diag_dense(pluss_ctx *ctx, const uint64_t *d_samples, uint64_t n, uint
 int pluss_diag_sort_words(pluss_ctx *ctx, int32_t ref, const uint64_t *d_samples, uint64_t n, void *d_words,
                           int32_t *word_bytes, void *stream);
 
+/* The uniform source's parts alone (r10's law, pluss_dev_gen_uniform_faithful_refs),
+   to see where its pass time goes: what = 0 the plan (counts, prefix, removal,
+   tile map); 1 the plan, then every full tile generated into LDS as the
+   lane-major local pass stages it (nothing scanned; one word per tile written
+   to d_out, which holds one u64 per tile of all references); 2 the same
+   staging as the slow and rescan paths do it (packed samples). */
+int pluss_diag_uniform_parts(pluss_ctx *ctx, uint64_t seed, const uint64_t totals[6], int32_t what, uint64_t *d_out,
+                             void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -622,7 +622,9 @@ int orc_expand_sorted(const orc_cfg *c, uint64_t seed, int ref, uint64_t S, uint
    leaves = key rows ((q, c1) for 3-D, q for 2-D references) cut into blocks of
    w-values times the threads: K0 = clamp(floor(16 / (T p)), 1, span), nb = max(1, round(span / K0))
    blocks per row of K = ceil(span / nb) w-values (K*T < 2^32); a
-   leaf's candidate count is Binomial(G, p) by inversion of one hash draw
+   leaf's candidate count is Binomial(G, p) by inversion of one hash draw u
+   against the CDF (the smallest x with u < cdf(x), pmf by the recurrence
+   pmf(x+1) = ((pmf(x) (G-x)) / (x+1)) p/(1-p), cdf by the running sum)
    (or one Bernoulli draw per point in leaves of <= 64 points, more than 64
    expected candidates or p > 1/64), its candidates independent uniform offsets (two 32-bit ones per 64-bit hash in leaves of <= 2^16 points) sorted and
    redrawn on a duplicate; of the T' candidates the ranks F(0..T'-S-1) of a
@@ -684,13 +686,15 @@ int orc_expand_uniform(const orc_cfg *c, uint64_t seed, int ref, uint64_t S, uin
             const uint64_t lk = u_leafkey(base, l, 0xFFFFFFFFu);
             for (uint64_t j = 0; j < G; j++) x += u_u01(u_hash(lk, j)) < p;
         } else {
+            /* inversion against the CDF: the smallest x with u < cdf(x), at most G */
             double pm = 1.0, b = 1.0 - p;
             for (uint64_t e = G; e; e >>= 1) { if (e & 1) pm = pm * b; b = b * b; }
-            double xu = u_u01(u_hash(u_leafkey(base, l, 0xFFFFFFFEu), 0));
-            while (xu >= pm && x < G) {
-                xu = xu - pm;
+            const double xu = u_u01(u_hash(u_leafkey(base, l, 0xFFFFFFFEu), 0));
+            double cdf = pm;
+            while (!(xu < cdf) && x < G) {
                 pm = pm * (double)(G - x); pm = pm / (double)(x + 1); pm = pm * r;
                 x++;
+                cdf = cdf + pm;
             }
         }
         if (x > 1024) rc = -4;

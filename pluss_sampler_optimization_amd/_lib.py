@@ -41,7 +41,7 @@ EXPORTS = [
     "pluss_group_dense", "pluss_group_gen_count_dense",
 ]
 # include/pluss_diag.h (diagnostics, not the drop-in boundary)
-DIAG_EXPORTS = ["pluss_diag_dense", "pluss_diag_sort_words"]
+DIAG_EXPORTS = ["pluss_diag_dense", "pluss_diag_sort_words", "pluss_diag_uniform_parts"]
 
 
 class PlussCfg(ctypes.Structure):
@@ -128,6 +128,7 @@ def lib():
         "pluss_dev_gen_count_dense": (ctypes.c_int, [vp, u64, P(u64), P(u64), P(u64), vp, vp]),
         "pluss_diag_dense": (ctypes.c_int, [vp, vp, u64, vp, i32, i32, vp]),
         "pluss_diag_sort_words": (ctypes.c_int, [vp, i32, vp, u64, vp, ctypes.POINTER(i32), vp]),
+        "pluss_diag_uniform_parts": (ctypes.c_int, [vp, u64, P(u64), i32, vp, vp]),
         "pluss_dev_faithful_shards_local": (ctypes.c_int, [vp, vp, u64, P(u64), P(u64), P(u64), vp, vp]),
         "pluss_dev_faithful_shards_select": (ctypes.c_int, [vp, vp, P(u64), u64, u64, vp, vp]),
         "pluss_dev_faithful_shards_local_selected": (ctypes.c_int, [vp, vp, i32, i32, vp, vp]),

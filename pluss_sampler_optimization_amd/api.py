@@ -391,6 +391,13 @@ class Context:
               "pluss_diag_sort_words")
         return int(wb.value)
 
+    def diag_uniform_parts(self, seed, totals, what, d_out, stream=None):
+        """Diagnostics (include/pluss_diag.h): the uniform source's plan (0), or
+        the plan and every full tile staged (1: as the lane-major pass, 2: packed)."""
+        c = (ctypes.c_uint64 * 6)(*[int(x) for x in totals])
+        check(lib().pluss_diag_uniform_parts(self._h, seed, c, what, d_out, self._s(stream)),
+              "pluss_diag_uniform_parts")
+
     # faithful mode over key-range shards of the single-read pipeline, all six
     # references at once (pluss_dev_faithful_shards_*; dist.py): every phase
     # writes this shard's summary row (SHARD_ROW u64 at d_row, device memory)

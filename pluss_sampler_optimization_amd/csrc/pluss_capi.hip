@@ -349,6 +349,12 @@ int pluss_diag_sort_words(pluss_ctx* ctx, int32_t ref, const uint64_t* d_samples
   return diag_sort_words(ctx, ref, d_samples, n, d_words, word_bytes, pick(ctx, stream));
 }
 
+int pluss_diag_uniform_parts(pluss_ctx* ctx, uint64_t seed, const uint64_t totals[6], int32_t what, uint64_t* d_out,
+                             void* stream) {
+  if (!ctx || !totals || what < 0 || what > 2 || (what && !d_out)) return PLUSS_ERR_CONFIG;
+  return diag_uniform_parts(ctx, seed, totals, what, d_out, pick(ctx, stream));
+}
+
 int pluss_faithful_key_space(const pluss_cfg* cfg, uint64_t* key_end) {
   Model m;
   if (!key_end) return PLUSS_ERR_CONFIG;

@@ -186,6 +186,7 @@ struct FaRefs {
   KeyGen kg[6];        // SRC_GEN
   const UniSet* us;    // SRC_UNI: the plan of the uniform key-order lists (device memory)
   uint32_t fast;       // the local pass's fast path applies to the shape (fa_run)
+  uint32_t unidec;     // SRC_UNI: keys below 2^61 and leaf key spans below 2^32 (uni_stage DEC)
 };
 
 // key, sink, case (3: malformed, flagged) and tid == 0 of one element.  P2:
@@ -357,8 +358,7 @@ __device__ __forceinline__ void fa_load_run(const Model& m, const FaOne& o, cons
   t0s = 0;
   if constexpr (SRC != SRC_GEN) {
     if constexpr (SRC == SRC_UNI) {
-      uni_stage<NT>(o.us, T.r, T.lt, T.mt, sh.raw, sh.cand, o.us->flags,
-                    [](uint32_t e) { return fa_slot_n<EPT>(e); });
+      // (generated into sh.raw by fa_uni_pre, once, before the per-reference dispatch)
     } else {
       const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(o.src) + T.base;
       fa_raw_t<SRC> v[EPT];  // every load issued before the first wait (partial tiles: clamped, no branch)
@@ -407,6 +407,16 @@ __device__ __forceinline__ void fa_load_run(const Model& m, const FaOne& o, cons
       }
     }
   }
+}
+
+// SRC_UNI: the tile generated into sh.raw (packed samples, runs of EPT per
+// thread), before the kernels' per-reference dispatch (one copy of the
+// generator per kernel, not one per reference)
+template <int SRC, int NT, int EPT>
+__device__ __forceinline__ void fa_uni_pre(const FaRefs& a, const FaTile& T, FaLds<SRC, NT, EPT>& sh) {
+  if constexpr (SRC == SRC_UNI)
+    uni_stage<NT, false>(a.us, T.r, T.lt, T.mt, sh.raw, sh.cand, a.us->flags,
+                         [](uint32_t e) { return fa_slot_n<EPT>(e); });
 }
 
 // The scan of a loaded run.  carry_in: the running max entering the tile
@@ -1053,6 +1063,18 @@ struct FaLm {
 };
 
 // (SRC_UNI: the tile generated into LDS first, `tile`, element e at tile[e])
+// a uniform tile's staged element (uni_stage DEC): the key's low 32 bits and the case flags, no decode
+__device__ __forceinline__ FaDec fa_dec_staged(unsigned long long w) {
+  FaDec d;
+  d.lk = (uint32_t)w;
+  const uint32_t h = (uint32_t)(w >> 32);
+  d.a = (h & 1u) != 0;
+  d.b = (h & 2u) != 0;
+  d.t0 = (h & 4u) != 0;
+  d.ord = 0;
+  return d;
+}
+
 template <int SRC, bool CHECK, uint32_t REF, bool FULLT, int NT>
 __device__ __forceinline__ bool fa_lane_tile(const Model& m, const FaRefs& a, const FaTile& T, FaLm<NT>& sh,
                                              unsigned long long* __restrict__ klist, GTable g,
@@ -1080,8 +1102,13 @@ __device__ __forceinline__ bool fa_lane_tile(const Model& m, const FaRefs& a, co
   rmax = t1 != KEY_EMPTY && t1 > rmax ? t1 : rmax;
   rmax = t2 != KEY_EMPTY && t2 > rmax ? t2 : rmax;
   bool b2 = false;
-  const unsigned long long base = fa_decode_ref<SRC, true, REF>(m, o.pv, src[0], b2).key;
-  const unsigned long long kl = fa_decode_ref<SRC, true, REF>(m, o.pv, src[last], b2).key;
+  // (SRC_UNI: a staged element holds its whole key, the high bits from bit 35)
+  auto key_of = [&](fa_raw_t<SRC> w) -> unsigned long long {
+    if constexpr (SRC == SRC_UNI) return ((unsigned long long)(w >> 35) << 32) | (uint32_t)w;
+    else return fa_decode_ref<SRC, true, REF>(m, o.pv, w, b2).key;
+  };
+  const unsigned long long base = key_of(src[0]);
+  const unsigned long long kl = key_of(src[last]);
   auto r32 = [](unsigned long long x) { return x == KEY_EMPTY ? 0xFFFFFFFFu : (uint32_t)x; };
   const FaRi r{r32(t0), r32(t1), r32(t2)};
   if (!(kl >= base && kl - base < 0xFFFFFFFFull - rmax && r.r0 != 0xFFFFFFFFu && r.r1 != 0xFFFFFFFFu))
@@ -1096,7 +1123,8 @@ __device__ __forceinline__ bool fa_lane_tile(const Model& m, const FaRefs& a, co
     const bool val = FULLT || e0 + 64u * k <= last;
     uint32_t oddk = 0;
     FaDec d;
-    if constexpr (fa_smp<SRC>()) d = fa_dec_sample<REF>(m, o.pv, (uint64_t)v[k], oddk);
+    if constexpr (SRC == SRC_UNI) d = fa_dec_staged(v[k]);
+    else if constexpr (fa_smp<SRC>()) d = fa_dec_sample<REF>(m, o.pv, (uint64_t)v[k], oddk);
     else d = fa_dec_word<REF>(m, o.pv, v[k]);
     odd |= val ? oddk : 0u;
     if (CHECK) {  // against the previous lane (the step before: its lane 63); integer
@@ -1317,6 +1345,7 @@ __global__ __launch_bounds__(TB) void k_fa_local(Model m, FaRefs a, unsigned lon
   if constexpr (SRC == SRC_GEN) kg = a.kg[R];                                                             \
   if (T.mt == TILE) fa_local_tile<SRC, P2, CHECK, R, true>(m, o, kg, gt, sh, tmax, part, klist, g);       \
   else fa_local_tile<SRC, P2, CHECK, R, false>(m, o, kg, gt, sh, tmax, part, klist, g);
+    fa_uni_pre<SRC>(a, T, sh);
     PLUSS_FA_REFS(PLUSS_FA_LOCAL)
 #undef PLUSS_FA_LOCAL
     __syncthreads();  // sh is reused by the next queued tile
@@ -1362,7 +1391,7 @@ constexpr int fa_lm_nt() { return TB; }
 template <int SRC>
 struct FaLmLds {
   FaLm<fa_lm_nt<SRC>()> s;
-  fa_raw_t<SRC> raw[SRC == SRC_UNI ? TILE : 1];
+  fa_raw_t<SRC> raw[SRC == SRC_UNI ? TILE : 1];  // (SRC_UNI: staged elements, uni_stage DEC)
   uint32_t cand[SRC == SRC_UNI ? UG_CAND : 1];
 };
 template <int SRC>
@@ -1382,11 +1411,15 @@ __global__ __launch_bounds__(fa_lm_nt<SRC>()) __attribute__((amdgpu_waves_per_eu
   unsigned long long* kl_out = klist + T.gt * (uint64_t)(2 * KL);
   bool done = false;
   // full tiles only: the few partial ones (a reference's last tile) go to the slow pass,
-  // which keeps the kernel's registers at the full tile's (8 waves per SIMD)
+  // which keeps the kernel's registers at the full tile's (8 waves per SIMD; with the
+  // partial-tile path in the same kernel: 85 VGPRs, 5 waves)
 #define PLUSS_FA_LM(R) done = fa_lane_tile<SRC, CHECK, R, true, NT>(m, a, T, sh, kl_out, g, L.raw);
   if (T.mt == TILE) {
-    if constexpr (SRC == SRC_UNI)
-      uni_stage<NT>(a.us, T.r, T.lt, T.mt, L.raw, L.cand, a.us->flags, [](uint32_t e) { return e; });
+    if constexpr (SRC == SRC_UNI) {
+      // (T, N and their shifts are the same in every reference's view)
+      const UniDec dz{(uint32_t)m.N, (uint32_t)m.W - 1u, a.pv[0].Q, (uint32_t)m.S, a.pv[0].nsh, a.pv[0].tsh};
+      uni_stage<NT, true>(a.us, T.r, T.lt, T.mt, L.raw, L.cand, a.us->flags, [](uint32_t e) { return e; }, dz);
+    }
     PLUSS_FA_REFS(PLUSS_FA_LM)
   }
 #undef PLUSS_FA_LM
@@ -1558,6 +1591,7 @@ __global__ __launch_bounds__(CH) void k_fa_chunk(Model m, FaRefs a, const unsign
   }
     __threadfence_block();  // pmin of the tile (written above) is read by every thread
     __syncthreads();
+    fa_uni_pre<SRC>(a, T, sh);
     PLUSS_FA_REFS(PLUSS_FA_RESCAN)
 #undef PLUSS_FA_RESCAN
     if (threadIdx.x == who) {
@@ -1719,6 +1753,7 @@ __global__ __launch_bounds__(CH) void k_fa_finish(Model m, FaRefs a, const unsig
     fa_load_run<SRC, P2, R, TB, TI, false>(m, o, kg, sh, key, cases, t0s, bad);                             \
     fa_scan<FA_CUT, SRC, TB, TI, false>(m, o, key, cases, t0s, carry, cin, sh, nullptr);                    \
   }
+    fa_uni_pre<SRC>(a, T, sh);
     PLUSS_FA_REFS(PLUSS_FA_CUT)
 #undef PLUSS_FA_CUT
   }
@@ -1895,9 +1930,11 @@ inline void fa_launch_t(const FaLaunch& L) {
   if (ph == FA_PH_ALL || ph == FA_PH_LOCAL) {
     bool fast = false;
     if constexpr (P2) {  // fast tiles, then the queued rest (an empty queue: the workgroups return at once)
-      if (L.a.fast) {
+      if (L.a.fast && (SRC != SRC_UNI || L.a.unidec)) {
         // the queue starts empty whatever an earlier, abandoned pass left in it
-        (void)hipMemsetAsync(b.slowq, 0, sizeof(unsigned int), L.s);
+        // (a pass whose chunk phase ran left it empty: no fill launch then)
+        if (!b.slowq_clean) (void)hipMemsetAsync(b.slowq, 0, sizeof(unsigned int), L.s);
+        b.slowq_clean = false;
         if constexpr (fa_lm<SRC>())
           hipLaunchKernelGGL((k_fa_local_lm<SRC, CHK>), dim3(t), dim3(fa_lm_nt<SRC>()), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
                              b.fslot, b.slowq, L.g);
@@ -1913,6 +1950,9 @@ inline void fa_launch_t(const FaLaunch& L) {
       hipLaunchKernelGGL((k_fa_local<SRC, P2, CHK, false>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart,
                          b.klist, b.fslot, (unsigned int*)nullptr, L.g);
     }
+  }
+  if (ph == FA_PH_ALL || ph == FA_PH_CHUNK) {
+    b.slowq_clean = true;  // (k_fa_chunk empties the queue)
   }
   if (ph == FA_PH_ALL || ph == FA_PH_CHUNK)
     hipLaunchKernelGGL((k_fa_chunk<SRC, P2>), dim3((unsigned)L.a.coff[6]), dim3(CH), 0, L.s, L.m, L.a, b.tmax,

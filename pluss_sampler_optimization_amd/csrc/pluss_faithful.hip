@@ -808,6 +808,10 @@ static int fa_prepare(pluss_ctx* ctx, FaRefs& a, int src, bool check, bool shard
   // the local pass's fast path: 24-bit multiplies (q*N + c1 < N*N/T and S
   // below 2^24) and the range check by bit masks (N a power of two)
   a.fast = (p2 && m.np2 && (uint64_t)m.N * m.N / m.T < (1ull << 24) && m.S < (1u << 24)) ? 1u : 0u;
+  // the uniform source's staged elements carry whole keys (below 2^61) and a
+  // leaf's keys as 32-bit increments (a row of a 2-D reference spans N*S*T keys)
+  a.unidec = ((unsigned __int128)m.A * m.T < ((unsigned __int128)1 << 61) &&
+              (uint64_t)m.N * m.S * m.T < (1ull << 32)) ? 1u : 0u;
   *out = FaLaunch{m, a, ctx->g, &b, p2, t, 0, FA_PH_ALL, s, nullptr};
   if (t == 0) return PLUSS_OK;
   if (int rc = fa_reserve(b, t, c, s)) return rc;

@@ -74,6 +74,7 @@ struct FaithfulBufs {
   uint64_t dcap = 0;
   unsigned long long *dpart = nullptr, *tmax = nullptr, *pmin = nullptr, *klist = nullptr;
   unsigned int* slowq = nullptr;  // tiles the local fast path left: [0] count (zero between passes), then indices
+  bool slowq_clean = false;       // slowq[0] is zero on the stream (k_fa_chunk emptied it): no reset launch needed
   uint64_t ccap = 0;              // chunks (of k_fa_chunk's CH tiles) the buffers below hold
   unsigned long long *cval = nullptr, *crec = nullptr;  // per chunk: its largest sink; its summary for the finish
   unsigned int* cflag = nullptr;  // per chunk: the epoch of the pass that published cval (zeroed once)
@@ -205,6 +206,8 @@ int uni_plan_count(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, uint32
 int uni_plan_remove(pluss_ctx* ctx, const unsigned long long* rows, uint32_t shard, uint32_t ns, hipStream_t s);
 int uni_plan_tiles(pluss_ctx* ctx, const uint64_t* n, hipStream_t s, const UniSet** out);
 void uni_free(pluss_ctx* ctx);
+int diag_uniform_parts(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, int32_t what, uint64_t* d_out,
+                       hipStream_t s);
 int launch_expand_uniform_sorted(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t total, uint64_t first,
                                  uint64_t n, uint64_t* d_out, hipStream_t s);
 int launch_gen_uniform_faithful_refs(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t s);  // a one-GPU faithful call ends any half-finished shard pass

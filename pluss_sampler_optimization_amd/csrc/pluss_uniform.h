@@ -36,6 +36,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "pluss_model.h"
 
 #if defined(__HIPCC__)
@@ -61,6 +63,7 @@ struct UniGen {
   double pm[4];                   // (1 - p)^G of the four leaf sizes: block A / B x full / last block of a row
   uint64_t base;                  // hash key of (seed, ref)
   Div64 dnb, dspan, dtA, dtB;     // division by nb, span, T, T-1
+  FastDiv fA, fB;                 // 32-bit division by T, T-1 (a leaf's offset -> w, t)
 };
 
 // (1 - p)^G by square and multiply, a fixed sequence of IEEE multiplies (host
@@ -122,6 +125,8 @@ inline UniGen make_unigen(uint64_t N, uint64_t T, uint64_t CS, bool range_full, 
   u.dspan = make_div64(u.span ? u.span : 1);
   u.dtA = make_div64(T);
   u.dtB = make_div64(T > 1 ? T - 1 : 1);
+  u.fA = make_fastdiv((uint32_t)T);
+  u.fB = make_fastdiv((uint32_t)(T > 1 ? T - 1 : 1));
   return u;
 }
 
@@ -156,9 +161,12 @@ PM_HD bool uni_direct(const UniGen& u, const UniLeaf& f) {
   return f.G <= UG_DIRECT || (double)f.G * u.p > 64.0 || u.p > 0.015625;
 }
 
-// The leaf's candidate count: Binomial(G, p).  Inversion with the pmf
-// recurrence f(x+1) = f(x) (G-x)/(x+1) * p/(1-p) from f(0) = (1-p)^G (square
-// and multiply), one uniform draw.
+// The leaf's candidate count: Binomial(G, p) by inversion of one uniform
+// draw u against the CDF: the smallest x with u < cdf(x), at most G, where
+// pmf(0) = (1-p)^G (square and multiply), pmf(x+1) = ((pmf(x) (G-x)) / (x+1))
+// p/(1-p) and cdf(x) = cdf(x-1) + pmf(x), each an IEEE operation in this
+// order.  (The device reads cdf from a table of the same values, k_ug_pmt, and
+// binary-searches it.)
 PM_HD uint64_t uni_count(const UniGen& u, uint64_t l) {
 #if defined(__clang__)
 #pragma clang fp contract(off)
@@ -174,14 +182,15 @@ PM_HD uint64_t uni_count(const UniGen& u, uint64_t l) {
   // (1 - p)^G: one of the four leaf sizes' values, computed once (make_unigen)
   // (selects, not an index: an indexed copy of the generator went to scratch)
   double pm = f.blk ? (f.kw == u.K ? u.pm[2] : u.pm[3]) : (f.kw == u.K ? u.pm[0] : u.pm[1]);
-  double x_u = uni_u01(uni_hash(uni_leafkey(u, l, 0xFFFFFFFEu), 0));
+  const double x_u = uni_u01(uni_hash(uni_leafkey(u, l, 0xFFFFFFFEu), 0));
+  double cdf = pm;
   uint64_t x = 0;
-  while (x_u >= pm && x < f.G) {
-    x_u = x_u - pm;
+  while (!(x_u < cdf) && x < f.G) {
     pm = pm * (double)(f.G - x);
     pm = pm / (double)(x + 1);
     pm = pm * u.r;
     ++x;
+    cdf = cdf + pm;
   }
   return x;
 }
@@ -279,33 +288,31 @@ struct UniSet {
   const uint64_t* rb;   // exclusive prefix of the bitmap words' popcounts (woff[6] + 1 words)
   const uint32_t* tmap; // per tile: the leaf holding its first sample
   unsigned int* flags;  // the handle's flags (FLAG_UNI)
-  const double* pmt;    // per reference and leaf size class: pmf(0..UG_LEAFMAX + 1) of uni_count's recurrence
+  const double* pmt;    // per reference and leaf size class: uni_count's cdf(0..xm), +inf past it, [UG_PMT-1] = xm
 };
 constexpr int UI_W = 24;  // a plan's info words (UniBufs::info): [0,6) removed ranks below it, [6,12) first, [12,18) n
 constexpr uint32_t UG_PMT = UG_LEAFMAX + 2;  // table entries per leaf size class (4 classes per reference)
 
 #if defined(__HIPCC__)
-// uni_count with the pmf recurrence read from the reference's table for the
-// leaf's size (the same doubles: the table is that recurrence, run once per
-// class by k_ug_pmt) -- the loop left is compare and subtract, no division
+// uni_count with the CDF read from the reference's table for the leaf's size
+// class (the same doubles: the table is that recurrence and sum, run once per
+// class by k_ug_pmt): a binary search of UG_CDF entries, no loop per lane.
+// Entries past the class's reach xm (mean + 40 sd + 64) are +inf and
+// cdf[UG_PMT - 1] holds xm: a draw past it (P < 1e-300) returns UG_LEAFMAX + 1
+// (flagged by the caller) unless G lies within the reach.
+constexpr uint32_t UG_CDF = 512;  // searched entries (xm < 448: the counted leaves expect at most 64 candidates)
 __device__ __forceinline__ uint64_t uni_count_tab(const UniGen& u, uint64_t l, const double* __restrict__ pmt) {
-#if defined(__clang__)
-#pragma clang fp contract(off)
-#endif
   const UniLeaf f = uni_leaf(u, l);
   if (u.p >= 1.0 || uni_direct(u, f)) return uni_count(u, l);
   const double* t = pmt + ((f.blk ? 2 : 0) + (f.kw == u.K ? 0 : 1)) * UG_PMT;
-  double x_u = uni_u01(uni_hash(uni_leafkey(u, l, 0xFFFFFFFEu), 0));
-  uint64_t x = 0;
-  double pm = t[0];
-  while (x_u >= pm && x < f.G) {
-    x_u = x_u - pm;
-    ++x;
-    if (x > UG_LEAFMAX) return x;  // (flagged by the caller)
-    pm = t[x];
-    if (pm == 0.0) return UG_LEAFMAX + 1;  // past the table's reach (P < 1e-300): flagged
-  }
-  return x;
+  const double x_u = uni_u01(uni_hash(uni_leafkey(u, l, 0xFFFFFFFEu), 0));
+  uint32_t lo = 0;  // entries below lo are <= x_u
+#pragma unroll
+  for (uint32_t step = UG_CDF / 2; step; step >>= 1)
+    if (t[lo + step - 1] <= x_u) lo += step;
+  const uint64_t xm = (uint64_t)t[UG_PMT - 1];
+  if (lo > xm && f.G > xm) return UG_LEAFMAX + 1;
+  return lo < f.G ? lo : f.G;
 }
 #endif
 
@@ -413,10 +420,24 @@ __device__ __forceinline__ void uni_sort_net(uint32_t (&v)[NC]) {
 }
 constexpr uint32_t UG_NET = 32;  // leaves of at most this many candidates: sorted in registers
 
-template <int NT, class SLOT>
+// What the faithful scan needs of a shape to take staged elements decoded
+// (uni_stage DEC): the key's low 32 bits and the case flags, per candidate,
+// from its leaf's constants (k_fa_local_lm)
+struct UniDec {
+  uint32_t N, Wm1, Q, S, nsh, tsh;
+};
+
+// Generate samples [lt*UG_TILE, lt*UG_TILE + mt) of reference r's list into
+// raw[slot(e)] (e = sample - lt*UG_TILE), all NT threads of the workgroup;
+// cand: LDS scratch of UG_CAND words.  DEC: instead of the packed sample,
+// raw[e] = its faithful key a*T + tid's low 32 bits | case 0 flag << 32 |
+// case 1 flag << 33 | tid == 0 << 34 | the key's high bits << 35
+// (fa_lane_tile's element, nothing left to decode; shapes whose keys stay
+// below 2^61 and whose leaves span less than 2^32 keys, FaRefs::unidec).
+template <int NT, bool DEC, class SLOT>
 __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_t r, uint64_t lt, uint32_t mt,
                                           unsigned long long* raw, uint32_t* cand, unsigned int* flags,
-                                          SLOT&& slot) {
+                                          SLOT&& slot, const UniDec dz = UniDec{}) {
   // the generator and the plan's arrays copied out once: read through the
   // plan pointer after every LDS store (generic stores may alias it), they
   // were reloaded from memory per candidate
@@ -434,7 +455,8 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
     __syncthreads();
     return;
   }
-  // the window's bitmap words [wlo, wlo + nw) (reference-relative) and their removed-before counts
+  // the window's bitmap words [wlo, wlo + nw] (reference-relative; one past
+  // its last, so any leaf can read two words) and their removed-before counts
   const uint64_t wo = us->woff[r], wend = us->woff[r + 1] - wo;  // (a flagged plan's indices are clamped)
   const uint64_t wlo = r0 >> 5;
   const uint32_t nw = rend > r0 ? (uint32_t)(((rend - 1) >> 5) - wlo + 1) : 0u;
@@ -444,9 +466,9 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
   uint32_t* alloc = rbw + UG_WCAP;
   const uint64_t wl = wlo < wend ? wlo : wend - 1;
   const uint64_t rem0 = us->rb[wo + wl] - us->rb[wo];
-  for (uint32_t i = threadIdx.x; i < nw; i += NT) {
+  for (uint32_t i = threadIdx.x; i <= nw; i += NT) {
     const uint64_t w = wlo + i < wend ? wlo + i : wend - 1;
-    bw[i] = us->bits[wo + w];
+    bw[i] = wlo + i < wend ? us->bits[wo + w] : 0u;
     rbw[i] = (uint32_t)(us->rb[wo + w] - us->rb[wo] - rem0);
   }
   if (threadIdx.x == 0) *alloc = 0;
@@ -463,14 +485,64 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
     const UniLeaf f = uni_leaf(u, lbase + l);
     const UniRowD rd = uni_row(u, f);
     // candidate i of the leaf (in key order) has rank x0 + i; the removed ones are skipped
-    const uint32_t w0i = (uint32_t)((x0 >> 5) - wlo);
-    uint64_t rem = rem0 + rbw[w0i] + (uint64_t)__popc(bw[w0i] & ((1u << (x0 & 31)) - 1u));  // removed before x0
+    const uint32_t w0i = (uint32_t)((x0 >> 5) - wlo), sh = (uint32_t)x0 & 31u;
+    const uint64_t remb = rem0 + rbw[w0i] + (uint64_t)__popc(bw[w0i] & ((1u << sh) - 1u));  // removed before x0
+    // tile-relative index of the leaf's first candidate if nothing of it were removed
+    const int32_t be = (int32_t)((int64_t)(x0 - remb) - (int64_t)f0);
     // the packed sample's fixed bits for this leaf (block A, T and CS powers of
     // two: every BASELINE shape): offset o adds t = o % T to c0 and w = o / T
-    // to c2 (3-D) or c1 (2-D); other leaves take uni_pack_row
+    // to c2 (3-D) or c1 (2-D); other leaves divide
     const bool fastp = !f.blk && u.tp2 && u.csp2;
     const uint32_t c0b = ((rd.q >> u.cssh) << (u.tsh + u.cssh)) | (rd.q & (u.CS - 1));
     const uint64_t pkb = pack(u.ref, c0b, u.dim3 ? rd.c1 : 0u, u.dim3 ? rd.w0 : 0u);
+    // DEC: the key lkb64 + (wq * dk + t) (the increment below 2^32, the
+    // shape's condition for this mode) and the case flags of the leaf's row
+    // (pluss_faithful.h fa_dec_digits): for 3-D references only c2 = w moves,
+    // so case 0 is ((w & am) != av) && w < alim and case 1 a leaf constant
+    uint32_t lkb = 0, khi = 0, dk = 0, am = 0, av = 1, alim = 0xFFFFFFFFu, bfl = 2u;
+    if constexpr (DEC) {
+      const uint32_t qc0 = (rd.q << dz.nsh) + (u.dim3 ? rd.c1 : rd.w0);
+      const uint64_t lk64 = ((uint64_t)qc0 * dz.S + (u.ref < 2 ? u.ref : u.ref + 4u * rd.w0)) << dz.tsh;
+      lkb = (uint32_t)lk64;
+      khi = (uint32_t)(lk64 >> 32);
+      dk = (u.dim3 ? 4u : dz.S) << dz.tsh;
+      if (u.ref == C3) {
+        alim = dz.N - 1;                          // c2 + 1 < N
+        bfl = (rd.c1 & dz.Wm1) != dz.Wm1 ? 2u : 0u;
+      } else if (u.ref == A0) {
+        am = av = dz.Wm1;                         // (c2 & Wm1) != Wm1
+        bfl = rd.c1 + 1 < dz.N ? 2u : 0u;
+      } else if (u.ref == B0) {
+        av = (rd.c1 & dz.Wm1) != dz.Wm1 ? 1u : 0u;  // a leaf constant
+        bfl = rd.q + 1 < dz.Q ? 2u : 0u;
+      }
+    }
+    const FastDiv fd = f.blk ? u.fB : u.fA;
+    const uint32_t tb = (uint32_t)f.tb;
+    auto put = [&](uint32_t e, uint32_t o, auto fastc) {  // candidate at offset o, kept as tile element e < mt
+      constexpr bool FP = decltype(fastc)::value;       // (block A, T and CS powers of two: shifts)
+      const uint32_t wq = FP ? o >> u.tsh : (uint32_t)(((uint64_t)umulhi32(o, fd.m) + o) >> fd.s);
+      const uint32_t t = FP ? o & (u.T - 1) : o - wq * tb;
+      if constexpr (!DEC) {
+        uint64_t pk;
+        if (FP) {
+          pk = pkb | ((uint64_t)t << (40 + u.cssh));
+          pk = u.dim3 ? pk + wq : pk | ((uint64_t)(rd.w0 + wq) << 20);  // (c2 = w0 + wq < 2^20)
+        } else {
+          pk = uni_pack_row(u, f, rd, o);
+        }
+        raw[slot(e)] = pk;
+      } else {
+        const uint32_t w = rd.w0 + wq;
+        const uint32_t ca = ((w & am) != av && w < alim) ? 1u : 0u;
+        const uint32_t lk = lkb + (wq * dk + t);
+        const uint32_t hi = khi + (lk < lkb ? 1u : 0u);
+        raw[e] = (unsigned long long)lk |
+                 ((unsigned long long)(ca | bfl | (t == 0 ? 4u : 0u) | (hi << 3)) << 32);
+      }
+    };
+    // one candidate at a time, the removed ones counted as they come (the rare paths)
+    uint64_t rem = remb;
     auto emit = [&](uint32_t i, uint32_t o) {
       const uint64_t x = x0 + i;
       if ((bw[(uint32_t)((x >> 5) - wlo)] >> (x & 31)) & 1u) {
@@ -478,17 +550,7 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
         return;
       }
       const uint64_t e = x - rem - f0;
-      if (e < mt) {
-        uint64_t pk;
-        if (fastp) {
-          const uint32_t wq = o >> u.tsh, t = o & (u.T - 1);
-          pk = pkb | ((uint64_t)t << (40 + u.cssh));
-          pk = u.dim3 ? pk + wq : pk | ((uint64_t)(rd.w0 + wq) << 20);  // (c2 = w0 + wq < 2^20)
-        } else {
-          pk = uni_pack_row(u, f, rd, o);
-        }
-        raw[slot((uint32_t)e)] = pk;
-      }
+      if (e < mt) put((uint32_t)e, o, std::false_type{});
     };
     if (u.p >= 1.0) {
       for (uint32_t j = 0; j < c; ++j) emit(j, j);
@@ -528,9 +590,19 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
         for (uint32_t q = 0; q + 1 < UG_NET; ++q) dup |= v[q] == v[q + 1] && q + 1 < c;
         if (!dup) break;
       }
+      // the leaf's removed candidates from its two bitmap words at once (c <= 32
+      // ranks from x0); candidate q is tile element be + q - (removed below q)
+      const uint64_t W = (uint64_t)bw[w0i] | ((uint64_t)bw[w0i + 1] << 32);
+      const uint32_t rm = (uint32_t)(W >> sh) & (c >= 32 ? 0xFFFFFFFFu : (1u << c) - 1u);
+      auto slots = [&](auto fastc) {
 #pragma unroll
-      for (uint32_t q = 0; q < UG_NET; ++q)
-        if (q < c) emit(q, v[q]);
+        for (uint32_t q = 0; q < UG_NET; ++q) {
+          const int32_t e = be + (int32_t)q - (int32_t)__popc(rm & ((1u << q) - 1u));
+          if (q < c && !((rm >> q) & 1u) && (uint32_t)e < mt) put((uint32_t)e, v[q], fastc);
+        }
+      };
+      if (fastp) slots(std::true_type{});
+      else slots(std::false_type{});
     } else {  // a large leaf (rare)
       const uint32_t G = (uint32_t)f.G;
       const uint32_t off = atomicAdd(alloc, c);

@@ -133,39 +133,44 @@ __device__ __forceinline__ uint32_t ug_ref_of(const uint64_t* off, uint64_t g) {
   return r;
 }
 
-// the pmf table of every reference's four leaf sizes: uni_count's recurrence
-// f(x+1) = f(x) (G-x)/(x+1) * p/(1-p) from f(0) = (1-p)^G, the same operations
-// in the same order (no contraction).  One wave per (reference, size class):
-// lane 0 runs the recurrence (sequential, a division per step) only as far as
-// the mean + 40 standard deviations + 64; the other entries are zeros, filled
-// by the whole wave (a leaf that reaches them, P < 1e-300, is flagged like any
-// leaf past UG_LEAFMAX).
+// the CDF table of every reference's four leaf sizes: uni_count's recurrence
+// and running sum, the same operations in the same order (no contraction).
+// One wave per (reference, size class): lane 0 runs them (sequential, a
+// division per step) only as far as the mean + 40 standard deviations + 64
+// (xm, kept in the last entry); the entries past it are +inf, filled by the
+// whole wave (a draw that reaches them, P < 1e-300, is flagged like any leaf
+// past UG_LEAFMAX).
 __global__ __launch_bounds__(64) void k_ug_pmt(const UniSet* __restrict__ us, double* __restrict__ pmt) {
 #if defined(__clang__)
 #pragma clang fp contract(off)
 #endif
   const uint32_t r = blockIdx.x >> 2, cls = blockIdx.x & 3u;
-  if (us->loff[r + 1] == us->loff[r]) return;
+  if (us->loff[r + 1] == us->loff[r] && us->u[r].S == 0) return;
   const UniGen& u = us->u[r];
   if (u.p >= 1.0) return;
   const uint64_t kl = u.W - (u.nb - 1) * u.K, tb = cls >= 2 ? (u.T > 1 ? u.T - 1 : 1) : u.T;
   const uint64_t G = ((cls & 1u) ? kl : u.K) * tb;
   const double mean = (double)G * u.p;
   const double xmd = mean + 40.0 * sqrt(mean) + 64.0;
-  const uint64_t xm = xmd < (double)(UG_PMT - 1) ? (uint64_t)xmd : UG_PMT - 1;
+  const uint64_t xm = xmd < (double)(UG_CDF - 2) ? (uint64_t)xmd : UG_CDF - 2;
   double* t = pmt + (r * 4 + cls) * UG_PMT;
-  for (uint64_t x = xm + 1 + threadIdx.x; x < UG_PMT; x += 64) t[x] = 0.0;
+  for (uint64_t x = xm + 1 + threadIdx.x; x < UG_PMT - 1; x += 64) t[x] = __builtin_inf();
   if (threadIdx.x == 0) {
     double pm = cls == 0 ? u.pm[0] : cls == 1 ? u.pm[1] : cls == 2 ? u.pm[2] : u.pm[3];
-    t[0] = pm;
+    double cdf = pm;
+    t[0] = cdf;
     for (uint64_t x = 0; x < xm; ++x) {
       if (x < G) {
         pm = pm * (double)(G - x);
         pm = pm / (double)(x + 1);
         pm = pm * u.r;
+      } else {
+        pm = 0.0;
       }
-      t[x + 1] = pm;
+      cdf = cdf + pm;
+      t[x + 1] = cdf;
     }
+    t[UG_PMT - 1] = (double)xm;
   }
 }
 
@@ -296,7 +301,7 @@ __global__ __launch_bounds__(UB) void k_ug_expand(const UniSet* __restrict__ us,
   const uint64_t lt = first / UG_TILE + blockIdx.x;
   const uint64_t t0 = lt * UG_TILE;
   const uint32_t mt = (uint32_t)(S - t0 < UG_TILE ? S - t0 : UG_TILE);
-  uni_stage<UB>(us, r, lt, mt, raw, cand, flags, [](uint32_t e) { return e; });
+  uni_stage<UB, false>(us, r, lt, mt, raw, cand, flags, [](uint32_t e) { return e; });
   for (uint32_t e = threadIdx.x; e < mt; e += UB) {
     const uint64_t i = t0 + e;
     if (i >= first && i < first + n) out[i - first] = raw[e];
@@ -304,6 +309,22 @@ __global__ __launch_bounds__(UB) void k_ug_expand(const UniSet* __restrict__ us,
 }
 
 __global__ void k_ug_setup(const UniSet h, UniSet* d) { *d = h; }
+
+// diagnostics (pluss_diag_uniform_parts): every full tile staged, nothing scanned
+template <bool DEC>
+__global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(4))) void k_ug_stage_only(
+    const UniSet* __restrict__ us, UniDec dz, uint64_t* __restrict__ out) {
+  __shared__ unsigned long long raw[UG_TILE];
+  __shared__ uint32_t cand[UG_CAND];
+  const uint64_t gt = blockIdx.x;
+  uint32_t r = 0;
+  for (uint32_t x = 1; x < 6; ++x) r += gt >= us->tmoff[x] ? 1u : 0u;
+  r = __builtin_amdgcn_readfirstlane(r);
+  const uint64_t lt = gt - us->tmoff[r], S = us->u[r].S;
+  if ((lt + 1) * UG_TILE > S) return;  // (full tiles only)
+  uni_stage<UB, DEC>(us, r, lt, UG_TILE, raw, cand, us->flags, [](uint32_t e) { return e; }, dz);
+  if (threadIdx.x == 0) out[gt] = raw[0] ^ raw[UG_TILE - 1];
+}
 
 static int ug_grow(void** p, size_t* cap, size_t bytes) {
   if (bytes <= *cap) return PLUSS_OK;
@@ -454,6 +475,24 @@ int uni_plan(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t 
   if (int rc = uni_plan_count(ctx, seed, totals, 0, 1, s)) return rc;
   if (int rc = uni_plan_remove(ctx, nullptr, 0, 1, s)) return rc;
   return uni_plan_tiles(ctx, totals, s, out);
+}
+
+int diag_uniform_parts(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, int32_t what, uint64_t* d_out,
+                       hipStream_t s) {
+  const UniSet* us = nullptr;
+  if (int rc = uni_plan(ctx, seed, totals, s, &us)) return rc;
+  if (what == 0) return PLUSS_OK;
+  const Model& m = ctx->m;
+  uint32_t nsh = 0, tsh = 0;
+  while ((1ull << nsh) < m.N) ++nsh;
+  while ((1ull << tsh) < m.T) ++tsh;
+  const UniDec dz{(uint32_t)m.N, (uint32_t)m.W - 1u, (uint32_t)(m.N / m.T), (uint32_t)m.S, nsh, tsh};
+  const unsigned tiles = (unsigned)ctx->ub.host->tmoff[6];
+  if (!tiles) return PLUSS_OK;
+  if (what == 1) hipLaunchKernelGGL(k_ug_stage_only<true>, dim3(tiles), dim3(UB), 0, s, us, dz, d_out);
+  else hipLaunchKernelGGL(k_ug_stage_only<false>, dim3(tiles), dim3(UB), 0, s, us, dz, d_out);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  return PLUSS_OK;
 }
 
 int launch_expand_uniform_sorted(pluss_ctx* ctx, uint64_t seed, int32_t ref, uint64_t total, uint64_t first,

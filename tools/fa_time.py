@@ -39,6 +39,7 @@ for N, T, lg in shapes:
     total = 1 << lg
     counts = P.default_counts(N, total)
     buf = torch.empty(total, dtype=torch.int64, device="cuda")
+    scratch = torch.empty(total // 4096 + 16, dtype=torch.int64, device="cuda")
     fe = torch.empty(total, dtype=torch.int64, device="cuda")
     with P.Context(P.SamplerConfig(n=N, threads=T, mode="faithful")) as ctx:
         off = 0
@@ -49,7 +50,11 @@ for N, T, lg in shapes:
         runs = {"sorted": lambda: ctx.faithful_hist_sorted_refs(buf.data_ptr(), counts, sp),
                 "generated": lambda: ctx.gen_faithful_refs(SEED, counts, sp),
                 "radix": lambda: ctx.faithful_hist_refs(fe.data_ptr(), counts, sp),
-                "uniform": lambda: ctx.gen_uniform_faithful_refs(SEED, counts, sp)}
+                "uniform": lambda: ctx.gen_uniform_faithful_refs(SEED, counts, sp),
+                # (diagnostics: the uniform source's plan alone, and plan + staging of every full tile)
+                "uni_plan": lambda: ctx.diag_uniform_parts(SEED, counts, 0, scratch.data_ptr(), sp),
+                "uni_stage_dec": lambda: ctx.diag_uniform_parts(SEED, counts, 1, scratch.data_ptr(), sp),
+                "uni_stage_packed": lambda: ctx.diag_uniform_parts(SEED, counts, 2, scratch.data_ptr(), sp)}
         res = {"N": N, "T": T, "samples": total}
         hs = {}
         runs = {k: v for k, v in runs.items() if only is None or k in only or k == "sorted"}
@@ -57,7 +62,8 @@ for N, T, lg in shapes:
             ctx.reset(sp)
             run()
             torch.cuda.synchronize()
-            hs[name] = ctx.fetch()
+            if not name.startswith("uni_"):
+                hs[name] = ctx.fetch()
             res[name + "_ms"] = timed(run)
         if "generated" in hs:
             assert hs["sorted"].bins == hs["generated"].bins
