@@ -1410,19 +1410,26 @@ __global__ __launch_bounds__(fa_lm_nt<SRC>()) __attribute__((amdgpu_waves_per_eu
   fa_cold_slot(T, g, slots);
   unsigned long long* kl_out = klist + T.gt * (uint64_t)(2 * KL);
   bool done = false;
-  // full tiles only: the few partial ones (a reference's last tile) go to the slow pass,
-  // which keeps the kernel's registers at the full tile's (8 waves per SIMD; with the
-  // partial-tile path in the same kernel: 85 VGPRs, 5 waves)
-#define PLUSS_FA_LM(R) done = fa_lane_tile<SRC, CHECK, R, true, NT>(m, a, T, sh, kl_out, g, L.raw);
-  if (T.mt == TILE) {
-    if constexpr (SRC == SRC_UNI) {
-      // (T, N and their shifts are the same in every reference's view)
-      const UniDec dz{(uint32_t)m.N, (uint32_t)m.W - 1u, a.pv[0].Q, (uint32_t)m.S, a.pv[0].nsh, a.pv[0].tsh};
-      uni_stage<NT, true>(a.us, T.r, T.lt, T.mt, L.raw, L.cand, a.us->flags, [](uint32_t e) { return e; }, dz);
-    }
+  // lists in memory: full tiles only, the few partial ones (a reference's last
+  // tile) go to the slow pass, which keeps the kernel's registers at the full
+  // tile's (8 waves per SIMD; with the partial-tile path in the same kernel: 85
+  // VGPRs, 5 waves).  The uniform source takes its partial tiles here too (its
+  // occupancy is set by the staging's registers and LDS either way; in the
+  // slow pass they cost ~60 us per pass)
+  if constexpr (SRC == SRC_UNI) {
+    // (T, N and their shifts are the same in every reference's view)
+    const UniDec dz{(uint32_t)m.N, (uint32_t)m.W - 1u, a.pv[0].Q, (uint32_t)m.S, a.pv[0].nsh, a.pv[0].tsh};
+    uni_stage<NT, true>(a.us, T.r, T.lt, T.mt, L.raw, L.cand, a.us->flags, [](uint32_t e) { return e; }, dz);
+#define PLUSS_FA_LM(R)                                                                              \
+  if (T.mt == TILE) done = fa_lane_tile<SRC, CHECK, R, true, NT>(m, a, T, sh, kl_out, g, L.raw);   \
+  else done = fa_lane_tile<SRC, CHECK, R, false, NT>(m, a, T, sh, kl_out, g, L.raw);
     PLUSS_FA_REFS(PLUSS_FA_LM)
-  }
 #undef PLUSS_FA_LM
+  } else if (T.mt == TILE) {
+#define PLUSS_FA_LM(R) done = fa_lane_tile<SRC, CHECK, R, true, NT>(m, a, T, sh, kl_out, g, L.raw);
+    PLUSS_FA_REFS(PLUSS_FA_LM)
+#undef PLUSS_FA_LM
+  }
   if (done) {
     if (threadIdx.x < FPW) part[blockIdx.x * (uint64_t)FPW + threadIdx.x] = sh.out[threadIdx.x];
     if (threadIdx.x == FPW) tmax[blockIdx.x] = sh.out[FPW];
@@ -1831,32 +1838,49 @@ __global__ void k_fa_shard_apply(Model m, FaRefs a, const unsigned long long* __
 // the list's length), then per reference its sample count and the largest of
 // its tiles' sinks (0: none).  what == 1 (phase 2): the sum of its chunks'
 // start counts.  what == 2 (phase 3, before the finish): the cut candidates'
-// default.  One workgroup of 64 per reference.
+// default.  One workgroup of SS_NT per reference, each thread's loads issued
+// in batches of 8 (a single wave walking 16K tiles took ~25 us per launch).
+constexpr int SS_NT = 1024;
 template <int X = 0>  // (a template: instantiated only where launched)
-__global__ void k_fa_shard_sums(FaRefs a, const unsigned long long* __restrict__ tmax,
-                                const unsigned long long* __restrict__ crec, unsigned long long* row, int what) {
-  const uint32_t r = blockIdx.x, lane = __lane_id();
-  unsigned long long mx = 0, st = 0;
+__global__ __launch_bounds__(SS_NT) void k_fa_shard_sums(FaRefs a, const unsigned long long* __restrict__ tmax,
+                                                        const unsigned long long* __restrict__ crec,
+                                                        unsigned long long* row, int what) {
+  const uint32_t r = blockIdx.x, lane = __lane_id(), wid = threadIdx.x >> 6;
+  __shared__ unsigned long long sw[SS_NT / 64];
   if (what == 2) {
-    if (lane == 0) row[ROW_CUT + r] = a.ntot[r];
+    if (threadIdx.x == 0) row[ROW_CUT + r] = a.ntot[r];
     return;
   }
-  if (what == 0)
-    for (uint64_t t = a.toff[r] + lane; t < a.toff[r + 1]; t += 64) mx = tmax[t] > mx ? tmax[t] : mx;
-  else
-    for (uint64_t c = a.coff[r] + lane; c < a.coff[r + 1]; c += 64) st += crec[c * CW];
-  mx = sc_wave_red<true>(mx);
-  st = sc_wave_red<false>(st);
-  if (lane == 0) {
+  unsigned long long acc = 0;
+  const uint64_t lo = what == 0 ? a.toff[r] : a.coff[r], hi = what == 0 ? a.toff[r + 1] : a.coff[r + 1];
+  const uint64_t stride = what == 0 ? 1 : CW;
+  const unsigned long long* src = what == 0 ? tmax : crec;
+  for (uint64_t i0 = lo + threadIdx.x; i0 < hi; i0 += 8 * SS_NT) {
+    unsigned long long v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint64_t i = i0 + (uint64_t)k * SS_NT;
+      v[k] = i < hi ? src[i * stride] : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc = what == 0 ? (v[k] > acc ? v[k] : acc) : acc + v[k];
+  }
+  acc = what == 0 ? sc_wave_red<true>(acc) : sc_wave_red<false>(acc);
+  if (lane == 0) sw[wid] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long x = 0;
+#pragma unroll
+    for (int w = 0; w < SS_NT / 64; ++w) x = what == 0 ? (sw[w] > x ? sw[w] : x) : x + sw[w];
     if (what == 0) {
       row[ROW_N + r] = a.n[r];
-      row[ROW_MAX + r] = mx;
+      row[ROW_MAX + r] = x;
       row[ROW_STARTS + r] = 0;
       row[ROW_CUT + r] = a.ntot[r];
       if (r == 0)
         for (int w = 24; w < ROW_W; ++w) row[w] = 0;
     } else {
-      row[ROW_STARTS + r] = st;
+      row[ROW_STARTS + r] = x;
     }
   }
 }
@@ -1953,6 +1977,9 @@ inline void fa_launch_t(const FaLaunch& L) {
   }
   if (ph == FA_PH_ALL || ph == FA_PH_CHUNK) {
     b.slowq_clean = true;  // (k_fa_chunk empties the queue)
+    // a replayed graph runs with the epoch it was captured with: the chunk
+    // flags start from zero in it, so no look-back reads an earlier replay's values
+    if (b.capture) (void)hipMemsetAsync(b.cflag, 0, L.a.coff[6] * sizeof(unsigned int), L.s);
   }
   if (ph == FA_PH_ALL || ph == FA_PH_CHUNK)
     hipLaunchKernelGGL((k_fa_chunk<SRC, P2>), dim3((unsigned)L.a.coff[6]), dim3(CH), 0, L.s, L.m, L.a, b.tmax,

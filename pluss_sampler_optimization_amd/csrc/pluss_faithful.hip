@@ -1063,7 +1063,7 @@ static int shards_phase1(pluss_ctx* ctx, FaShards& f, uint64_t* d_row, hipStream
   if (f.L.t)
     if (int rc = fa_launch(ctx, f.L, f.src, FA_PH_LOCAL)) return rc;
   FaithfulBufs& b = ctx->fb;
-  hipLaunchKernelGGL(k_fa_shard_sums<0>, dim3(6), dim3(64), 0, s, f.L.a, b.tmax, b.crec, (unsigned long long*)d_row,
+  hipLaunchKernelGGL(k_fa_shard_sums<0>, dim3(6), dim3(SS_NT), 0, s, f.L.a, b.tmax, b.crec, (unsigned long long*)d_row,
                      0);
   PLUSS_HIP_CHECK(hipGetLastError());
   f.phase = SH_LOCAL;
@@ -1294,7 +1294,7 @@ int faith_shards_carry(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, in
                      (uint32_t)shard, 2, b.xin, ctx->g);
   if (f.L.t)
     if (int rc = fa_launch(ctx, f.L, f.src, FA_PH_CHUNK)) return rc;
-  hipLaunchKernelGGL(k_fa_shard_sums<0>, dim3(6), dim3(64), 0, s, f.L.a, b.tmax, b.crec, (unsigned long long*)d_row,
+  hipLaunchKernelGGL(k_fa_shard_sums<0>, dim3(6), dim3(SS_NT), 0, s, f.L.a, b.tmax, b.crec, (unsigned long long*)d_row,
                      1);
   PLUSS_HIP_CHECK(hipGetLastError());
   f.phase = SH_CARRY;
@@ -1309,7 +1309,7 @@ int faith_shards_cut(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int3
   f.L.s = s;
   hipLaunchKernelGGL(k_fa_xchg<0>, dim3(1), dim3(64), 0, s, (const unsigned long long*)d_rows, (uint32_t)nshards,
                      (uint32_t)shard, 3, b.xin, ctx->g);
-  hipLaunchKernelGGL(k_fa_shard_sums<0>, dim3(6), dim3(64), 0, s, f.L.a, b.tmax, b.crec, (unsigned long long*)d_row,
+  hipLaunchKernelGGL(k_fa_shard_sums<0>, dim3(6), dim3(SS_NT), 0, s, f.L.a, b.tmax, b.crec, (unsigned long long*)d_row,
                      2);
   if (f.L.t) {
     f.L.row = (unsigned long long*)d_row;

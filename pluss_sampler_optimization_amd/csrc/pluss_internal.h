@@ -75,6 +75,7 @@ struct FaithfulBufs {
   unsigned long long *dpart = nullptr, *tmax = nullptr, *pmin = nullptr, *klist = nullptr;
   unsigned int* slowq = nullptr;  // tiles the local fast path left: [0] count (zero between passes), then indices
   bool slowq_clean = false;       // slowq[0] is zero on the stream (k_fa_chunk emptied it): no reset launch needed
+  bool capture = false;           // the pass is being captured into a graph: chunk flags reset inside it
   uint64_t ccap = 0;              // chunks (of k_fa_chunk's CH tiles) the buffers below hold
   unsigned long long *cval = nullptr, *crec = nullptr;  // per chunk: its largest sink; its summary for the finish
   unsigned int* cflag = nullptr;  // per chunk: the epoch of the pass that published cval (zeroed once)
@@ -95,6 +96,8 @@ struct UniBufs {  // its device buffers (grown on demand, per handle)
   uint64_t *pre = nullptr, *rb = nullptr, *bsum = nullptr;
   double* pmt = nullptr;  // the binomial pmf per leaf size (uni_count_tab)
   unsigned long long* info = nullptr;   // per reference: removed ranks below the plan, its first survivor, survivors
+  uint64_t pmt_key[6][10] = {};         // what the CDF tables in pmt were built for (k_ug_pmt runs when it changes)
+  bool pmt_valid = false;
   unsigned long long* hinfo = nullptr;  // pinned host copy of info (a key-range shard's one round trip)
   size_t set_cap = 0, cnt_cap = 0, bits_cap = 0, tmap_cap = 0, pre_cap = 0, rb_cap = 0, bsum_cap = 0, pmt_cap = 0,
          info_cap = 0;

@@ -401,7 +401,11 @@ int uni_plan_count(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, uint32
   if (!rc) rc = ug_grow((void**)&b.pre, &b.pre_cap, (L + 1) * 8);
   if (!rc) rc = ug_grow((void**)&b.bits, &b.bits_cap, (Wd + 1) * 4);
   if (!rc) rc = ug_grow((void**)&b.rb, &b.rb_cap, (Wd + 1) * 8);
-  if (!rc) rc = ug_grow((void**)&b.pmt, &b.pmt_cap, 6 * 4 * UG_PMT * sizeof(double));
+  if (!rc) {
+    void* before = b.pmt;
+    rc = ug_grow((void**)&b.pmt, &b.pmt_cap, 6 * 4 * UG_PMT * sizeof(double));
+    if (b.pmt != before) b.pmt_valid = false;
+  }
   if (!rc) rc = ug_grow((void**)&b.bsum, &b.bsum_cap, (nbL > nbW ? nbL : nbW) * 8 + 8);
   if (rc) return rc;
   if (!b.hinfo && hipHostMalloc((void**)&b.hinfo, UI_W * 8) != hipSuccess) {
@@ -419,7 +423,27 @@ int uni_plan_count(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, uint32
   // the plan's parameters travel as a kernel argument (ordered on the stream, no host buffer to keep)
   hipLaunchKernelGGL(k_ug_setup, dim3(1), dim3(1), 0, s, h, b.set);
   const int grid = (int)std::min<uint64_t>((L + UB - 1) / UB + 1, 4096);
-  hipLaunchKernelGGL(k_ug_pmt, dim3(24), dim3(64), 0, s, (const UniSet*)b.set, b.pmt);
+  // the CDF tables depend on the shape and the sample counts only (p and the
+  // four leaf sizes of each reference), not on the seed or the shard: kept
+  // while they stay the same
+  uint64_t key[6][10];
+  std::memset(key, 0, sizeof key);
+  for (int r = 0; r < 6; ++r) {
+    const UniGen& g = h.u[r];
+    if (!g.S) continue;
+    std::memcpy(&key[r][0], &g.p, 8);
+    std::memcpy(&key[r][1], &g.r, 8);
+    key[r][2] = g.K;
+    key[r][3] = g.W;
+    key[r][4] = g.nb;
+    key[r][5] = g.T;
+    std::memcpy(&key[r][6], g.pm, 32);
+  }
+  if (!b.pmt_valid || std::memcmp(key, b.pmt_key, sizeof key) != 0) {
+    hipLaunchKernelGGL(k_ug_pmt, dim3(24), dim3(64), 0, s, (const UniSet*)b.set, b.pmt);
+    std::memcpy(b.pmt_key, key, sizeof key);
+    b.pmt_valid = true;
+  }
   hipLaunchKernelGGL(k_ug_count, dim3(grid), dim3(UB), 0, s, (const UniSet*)b.set, b.cnt, ctx->g.flags);
   if (int e = ug_scan(b.cnt, L, b.bsum, b.pre, 0, s)) return e;
   PLUSS_HIP_CHECK(hipGetLastError());

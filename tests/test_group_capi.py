@@ -138,6 +138,38 @@ def test_group_uniform_faithful_equals_one_device(N, T, total, spd):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("spd", [1, 8])
+def test_group_faithful_replays_equal_one_device(spd):
+    """Repeated identical pluss_group_gen_faithful calls (the second captured
+    into a HIP graph, later ones replayed) give the one-device pass every
+    time; a different seed in between runs eagerly and drops the graph; the
+    group's other passes in between invalidate it too."""
+    P = _P()
+    import torch
+    N, T = 1024, 8
+    c = P.SamplerConfig(n=N, threads=T, mode="faithful")
+    totals = P.default_counts(N, 1 << 22)
+    st = torch.cuda.Stream()
+
+    def one(seed):
+        with P.Context(c) as ctx:
+            ctx.reset(st.cuda_stream)
+            ctx.gen_faithful_refs(seed, totals, st.cuda_stream)
+            st.synchronize()
+            return ctx.fetch()
+    a, b = one(11), one(12)
+    with P.Group(c, [0], spd) as g:
+        for seed in (11, 11, 11, 11, 12, 11, 11, 11):
+            h = g.gen_faithful(seed, totals)
+            w = a if seed == 11 else b
+            assert h.bins == w.bins and h.traversed == w.traversed, seed
+        g.gen_uniform_faithful(11, totals)  # another pass on the same handles
+        for _ in range(3):
+            h = g.gen_faithful(11, totals)
+            assert h.bins == a.bins and h.traversed == a.traversed
+
+
+@pytest.mark.gpu
 def test_group_pairs_shape_and_errors(orc):
     """A shape with N % (cls/ds) != 0 ((key, sink) pairs, not key-range
     sharded: the job's first shard runs the samplers) equals one device; a

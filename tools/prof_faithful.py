@@ -23,6 +23,7 @@ N, total = (4096, 1 << 28) if os.environ.get("PROF_SHAPE") == "config3" else (10
 cfg = P.SamplerConfig(n=N, threads=8, mode="faithful")
 counts = P.default_counts(N, total)
 buf = torch.empty(total, dtype=torch.int64, device=dev)
+scratch = torch.empty(total // 4096 + 16, dtype=torch.int64, device=dev)
 ctx = P.Context(cfg)
 off = 0
 for r, c in enumerate(counts):
@@ -39,9 +40,11 @@ for _ in range(int(os.environ.get("PROF_REPS", 5))):
         ctx.faithful_hist_refs(buf.data_ptr(), counts, sp)
     elif mode == "uniform":
         ctx.gen_uniform_faithful_refs(SEED, counts, sp)
+    elif mode == "uni_stage":  # diagnostics: the plan and every full tile staged, nothing scanned
+        ctx.diag_uniform_parts(SEED, counts, 1, scratch.data_ptr(), sp)
     else:
         ctx.gen_faithful_refs(SEED, counts, sp)
 torch.cuda.synchronize()
 h = ctx.fetch()
-assert h.total() > 0
+assert h.total() > 0 or mode == "uni_stage"
 print("ok", mode, h.total())
