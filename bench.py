@@ -588,7 +588,7 @@ def capi_group_bench(P, torch, dist, cfg, counts, total, world, rank, backend, s
             out = run(g, "1 device x 1 shard")
         with P.Group(cfg, [cfg.device], 8) as g:
             out["logical_shards_8"] = run(g, "1 device x 8 logical shards (rehearsal)")
-        out["faithful"], out["faithful_uniform"] = capi_group_faithful(P, cfg)
+        out["faithful"], out["faithful_uniform"], out["faithful_any_order"] = capi_group_faithful(P, cfg)
     out["note"] = ("host clock around pluss_group_dense(K) (K passes, each a count launch per shard, the per-device "
                    "sum and one RCCL all-reduce, until the merged vector is back on the host)")
     return out
@@ -604,9 +604,9 @@ def capi_group_faithful(P, cfg, reps=3):
     fcfg = P.SamplerConfig(n=4096, threads=cfg.threads, chunk=cfg.chunk, mode="faithful", device=cfg.device)
     totals = P.default_counts(4096, 1 << 28)
 
-    def leg(call):
+    def leg(call, spds=(1, 2, 8)):
         out, ref = {}, None
-        for spd in (1, 2, 8):
+        for spd in spds:
             with P.Group(fcfg, [cfg.device], spd) as g:
                 h = call(g)  # (the first call grows the buffers, a second identical one is captured)
                 h = call(g)
@@ -625,7 +625,39 @@ def capi_group_faithful(P, cfg, reps=3):
     uni = leg(lambda g: g.gen_uniform_faithful(SEED, totals))
     uni["workload"] = ("the same over r10's own law (pluss_group_gen_uniform_faithful: uniform draws without "
                        "replacement in key order, each shard generating only its stretch of every list)")
-    return out, uni
+    # r10's any-order input handed over in host memory (pinned): the keyed
+    # Feistel lists, as rand() draws them (r10:156-185)
+    import torch
+    dev = torch.device("cuda", cfg.device)
+    total = sum(totals)
+    host = torch.empty(total, dtype=torch.int64, pin_memory=True)
+    with P.Context(fcfg) as ctx:
+        d = torch.empty(total, dtype=torch.int64, device=dev)
+        st = torch.cuda.Stream(device=dev)
+        off = 0
+        for r, c in enumerate(totals):
+            ctx.expand(SEED, r, 0, c, d.data_ptr() + 8 * off, st.cuda_stream)
+            off += c
+        st.synchronize()
+        host.copy_(d)
+        ts = []
+        for _ in range(reps):  # the upload alone, for scale (the group's copy is the same bytes)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            d.copy_(host, non_blocking=True)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        del d
+    ts.sort()
+    lst = host.numpy().view("uint64")
+    anyo = leg(lambda g: g.sampled_hist(lst), spds=(1, 8))
+    anyo["h2d_ms"] = ts[len(ts) // 2] * 1e3
+    anyo["workload"] = ("the same shape over r10's any-order input (pluss_group_sampled_hist: a host list, the "
+                        "Feistel lists in pinned memory): each device uploads its slice, partitions it by key-range "
+                        "shard and reference on the device, (several devices: one grouped send/receive), each shard "
+                        "sorts its words; h2d_ms = the same bytes' upload alone")
+    del lst, host
+    return out, uni, anyo
 
 
 def pmc_traffic(samples_per_launch):

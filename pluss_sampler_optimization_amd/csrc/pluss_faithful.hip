@@ -1189,6 +1189,227 @@ int faith_shards_local_selected(pluss_ctx* ctx, const uint64_t* d_rows, int32_t 
   return shards_phase1(ctx, f, d_row, s);
 }
 
+// ---- arbitrary-order lists partitioned on the devices (pluss_group_sampled_hist)
+// A device reads its slice of the caller's list once to count, once to place:
+// each sample's reference r and key-range shard g (the largest g with
+// bounds[g] <= key, a binary search over the S+1 bounds staged in LDS) make
+// its bin g*6+r.  Workgroup b takes the contiguous block [n*b/B, n*(b+1)/B).
+//   k_fa_part<true>   per block and bin the count -> hist[bin*B + b]
+//   k_fa_part_scan    per bin: the total, and hist made the exclusive offsets
+//   k_fa_part<false>  each sample's packed word to out[rstart[bin] + hist[bin*B+b]
+//                     + its rank in the block] (ranks from wave-aggregated LDS
+//                     atomics: the order inside a bin is arbitrary, it is sorted next)
+// No global atomics; malformed samples raise the handle's bad-input flag.
+constexpr int PT_NT = 256;
+
+__host__ __device__ inline uint32_t part_bins(uint32_t S) { return 6 * S; }
+
+template <bool COUNT, typename KT>
+__global__ __launch_bounds__(PT_NT) void k_fa_part(Model m, const uint64_t* __restrict__ smp, uint64_t n,
+                                                   const unsigned long long* __restrict__ bounds, uint32_t S,
+                                                   uint32_t* __restrict__ hist, uint32_t B,
+                                                   const unsigned long long* __restrict__ rstart, KT* __restrict__ out,
+                                                   GTable g) {
+  extern __shared__ unsigned long long pt_lds[];
+  unsigned long long* lb = pt_lds;                       // S + 1 bounds
+  uint32_t* lc = (uint32_t*)(pt_lds + S + 1);            // per bin: the block's count so far
+  unsigned long long* lbase = pt_lds + S + 1 + (part_bins(S) + 1) / 2;  // scatter: per bin its base
+  const uint32_t nb = part_bins(S), b = blockIdx.x;
+  for (uint32_t i = threadIdx.x; i <= S; i += PT_NT) lb[i] = bounds[i];
+  for (uint32_t i = threadIdx.x; i < nb; i += PT_NT) {
+    lc[i] = 0;
+    if (!COUNT) lbase[i] = rstart[i] + hist[(size_t)i * B + b];
+  }
+  __syncthreads();
+  const uint64_t lo = n * b / B, hi = n * (b + 1) / B;  // (n < 2^40, B <= 4096)
+  const uint32_t lane = __lane_id();
+  for (uint64_t base = lo; base < hi; base += PT_NT) {
+    const uint64_t i = base + threadIdx.x;
+    uint32_t bin = ~0u;
+    KT word = 0;
+    if (i < hi) {
+      const uint64_t x = smp[i];
+      const Sample s = unpack(x);
+      if (s.ref > 5 || s.c0 >= m.N || s.c1 >= m.N || s.c2 >= m.N) {
+        atomicOr(&g.flags[1], 1u);
+      } else {
+        const uint32_t c2 = (s.ref == C0 || s.ref == C1) ? 0u : s.c2;
+        uint64_t P;
+        uint32_t t;
+        position(m, s.ref, s.c0, s.c1, c2, &P, &t);
+        const unsigned long long key = P * m.T + t;
+        uint32_t a = 0, z = S;  // lb[a] <= key < lb[z]
+        while (z - a > 1) {
+          const uint32_t mid = (a + z) >> 1;
+          if (lb[mid] <= key) a = mid;
+          else z = mid;
+        }
+        bin = a * 6 + s.ref;
+        if (!COUNT) word = pk_word_of<KT>(m, s.ref, x, g);
+      }
+    }
+    // one LDS atomic per distinct bin of the wave
+    unsigned long long pend = __ballot(bin != ~0u);
+    while (pend) {
+      const int lead = __ffsll((long long)pend) - 1;
+      const uint32_t bb = __shfl(bin, lead, 64);
+      const unsigned long long mk = __ballot(bin == bb);
+      uint32_t at = 0;
+      if ((int)lane == lead) at = atomicAdd(&lc[bb], (uint32_t)__popcll(mk));
+      if (!COUNT) {
+        at = __shfl(at, lead, 64);
+        if (bin == bb) out[lbase[bb] + at + __popcll(mk & ((1ull << lane) - 1))] = word;
+      }
+      pend &= ~mk;
+    }
+  }
+  if (COUNT) {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nb; i += PT_NT) hist[(size_t)i * B + b] = lc[i];
+  }
+}
+
+// one workgroup per bin: the exclusive scan of its B block counts, the total to tot[bin]
+__global__ __launch_bounds__(PT_NT) void k_fa_part_scan(uint32_t* __restrict__ hist, uint32_t B,
+                                                        unsigned long long* __restrict__ tot) {
+  __shared__ unsigned long long ws[PT_NT / 64];
+  uint32_t* h = hist + (size_t)blockIdx.x * B;
+  const uint32_t per = (B + PT_NT - 1) / PT_NT, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t i0 = t * per, i1 = min(B, i0 + per);
+  unsigned long long mine = 0;
+  for (uint32_t i = i0; i < i1; ++i) mine += h[i];
+  unsigned long long inc = mine;  // inclusive scan over the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long v = __shfl_up(inc, d, 64);
+    if ((int)lane >= d) inc += v;
+  }
+  if (lane == 63) ws[w] = inc;
+  __syncthreads();
+  unsigned long long before = 0, all = 0;
+  for (uint32_t x = 0; x < PT_NT / 64; ++x) {
+    if (x < w) before += ws[x];
+    all += ws[x];
+  }
+  unsigned long long run = before + inc - mine;
+  for (uint32_t i = i0; i < i1; ++i) {
+    const uint32_t v = h[i];
+    h[i] = (uint32_t)run;
+    run += v;
+  }
+  if (t == 0) tot[blockIdx.x] = all;
+}
+
+// copies of word segments {src offset, dst offset, count} (the exchange's
+// receive blocks into per-(shard, reference) order): blockIdx.y = segment
+template <typename KT>
+__global__ __launch_bounds__(PT_NT) void k_fa_seg_copy(const unsigned long long* __restrict__ seg,
+                                                       const KT* __restrict__ src, KT* __restrict__ dst) {
+  const unsigned long long* q = seg + 3 * (size_t)blockIdx.y;
+  const unsigned long long so = q[0], d = q[1], c = q[2];
+  for (unsigned long long i = (unsigned long long)blockIdx.x * PT_NT + threadIdx.x; i < c;
+       i += (unsigned long long)gridDim.x * PT_NT)
+    dst[d + i] = src[so + i];
+}
+
+uint32_t faith_part_blocks(uint64_t n, uint32_t S) {
+  uint64_t B = n / 16384;  // >= 16K samples per workgroup
+  const uint64_t cap = std::max<uint64_t>(1, ((uint64_t)1 << 22) / part_bins(S));  // hist <= 16 MB
+  B = std::min<uint64_t>(std::min<uint64_t>(B, 4096), cap);
+  return (uint32_t)std::max<uint64_t>(B, 1);
+}
+
+int faith_word_bytes(const pluss_ctx* ctx) {
+  const int fm = faith_fm(ctx->m);
+  return fm == FM_PK32 ? 4 : fm == FM_PK64 ? 8 : 0;
+}
+
+static size_t part_lds(uint32_t S) { return 8 * ((size_t)S + 1 + (part_bins(S) + 1) / 2 + part_bins(S)); }
+
+int faith_part_count(pluss_ctx* ctx, const uint64_t* d_smp, uint64_t n, const unsigned long long* d_bounds,
+                     uint32_t S, uint32_t* d_hist, uint32_t B, unsigned long long* d_tot, hipStream_t s) {
+  if (S < 1 || S > 1024 || part_lds(S) > 64 * 1024) {
+    set_error("faithful partition: at most 1024 shards");
+    return PLUSS_ERR_CONFIG;
+  }
+  if (faith_word_bytes(ctx) == 4)
+    hipLaunchKernelGGL((k_fa_part<true, uint32_t>), dim3(B), dim3(PT_NT), part_lds(S), s, ctx->m, d_smp, n, d_bounds, S,
+                       d_hist, B, (const unsigned long long*)nullptr, (uint32_t*)nullptr, ctx->g);
+  else
+    hipLaunchKernelGGL((k_fa_part<true, unsigned long long>), dim3(B), dim3(PT_NT), part_lds(S), s, ctx->m, d_smp, n,
+                       d_bounds, S, d_hist, B, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                       ctx->g);
+  hipLaunchKernelGGL(k_fa_part_scan, dim3(part_bins(S)), dim3(PT_NT), 0, s, d_hist, B, d_tot);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  ctx->tables_dirty = true;
+  return PLUSS_OK;
+}
+
+int faith_part_scatter(pluss_ctx* ctx, const uint64_t* d_smp, uint64_t n, const unsigned long long* d_bounds,
+                       uint32_t S, uint32_t* d_hist, uint32_t B, const unsigned long long* d_rstart, void* d_out,
+                       hipStream_t s) {
+  if (faith_word_bytes(ctx) == 4)
+    hipLaunchKernelGGL((k_fa_part<false, uint32_t>), dim3(B), dim3(PT_NT), part_lds(S), s, ctx->m, d_smp, n, d_bounds,
+                       S, d_hist, B, d_rstart, (uint32_t*)d_out, ctx->g);
+  else
+    hipLaunchKernelGGL((k_fa_part<false, unsigned long long>), dim3(B), dim3(PT_NT), part_lds(S), s, ctx->m, d_smp, n,
+                       d_bounds, S, d_hist, B, d_rstart, (unsigned long long*)d_out, ctx->g);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  return PLUSS_OK;
+}
+
+int faith_seg_copy(const unsigned long long* d_seg, uint32_t nseg, uint64_t maxn, const void* src, void* dst,
+                   int wbytes, hipStream_t s) {
+  if (!nseg || !maxn) return PLUSS_OK;
+  const uint32_t gx = (uint32_t)std::min<uint64_t>((maxn + PT_NT - 1) / PT_NT, 1024);
+  if (wbytes == 4)
+    hipLaunchKernelGGL(k_fa_seg_copy<uint32_t>, dim3(gx, nseg), dim3(PT_NT), 0, s, d_seg, (const uint32_t*)src,
+                       (uint32_t*)dst);
+  else
+    hipLaunchKernelGGL(k_fa_seg_copy<unsigned long long>, dim3(gx, nseg), dim3(PT_NT), 0, s, d_seg,
+                       (const unsigned long long*)src, (unsigned long long*)dst);
+  PLUSS_HIP_CHECK(hipGetLastError());
+  return PLUSS_OK;
+}
+
+// phase 1 over words already partitioned to this shard (in[r]: cnt[r] words of
+// reference r, any order; all[r] and before[r]: the reference's words over all
+// shards and over the shards before this one): the sort and the local pass
+int faith_shards_local_words(pluss_ctx* ctx, const void* const in[6], const uint64_t* cnt, const uint64_t* all,
+                             const uint64_t* before, uint64_t* d_row, hipStream_t s) {
+  FaShards& f = shards_of(ctx);
+  f = FaShards{};
+  if (int rc = faith_direct_shape(ctx, "pluss_group_sampled_hist")) return rc;
+  const int fm = faith_fm(ctx->m);
+  if (fm == FM_PAIRS) {
+    set_error("pluss_group_sampled_hist: packed words need N % (cls/ds) == 0");
+    return PLUSS_ERR_CONFIG;
+  }
+  FaithfulBufs& b = ctx->fb;
+  uint64_t tot = 0;
+  for (int r = 0; r < 6; ++r) tot += cnt[r];
+  if (int rc = faith_reserve(ctx, b, tot, s)) return rc;
+  FaRefs a = fa_none();
+  uint64_t soff = 0;
+  for (int r = 0; r < 6; ++r) {
+    f.tot[r] = all[r];
+    a.n[r] = cnt[r];
+    a.ntot[r] = all[r];
+    a.joff[r] = before[r];
+    a.src[r] = fm == FM_PK32 ? (const void*)((const uint32_t*)b.keys_s + soff) : (const void*)(b.keys_s + soff);
+    soff += cnt[r];
+  }
+  if (fm == FM_PK32) {
+    if (int rc = srt_sort<uint32_t, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, (uint32_t*)b.keys_s, s)) return rc;
+  } else if (int rc = srt_sort<unsigned long long, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, b.keys_s, s)) {
+    return rc;
+  }
+  ctx->tables_dirty = true;
+  f.src = fm == FM_PK32 ? SRC_W32 : SRC_W64;
+  if (int rc = fa_prepare(ctx, a, f.src, false, true, s, &f.L)) return rc;
+  return shards_phase1(ctx, f, d_row, s);
+}
+
 // r10's own law (pluss_uniform.h) over key-range shards: shard g of G holds,
 // per reference, the leaves [L*g/G, L*(g+1)/G) of the key-ordered space (L
 // leaves), so its samples are a contiguous stretch of the list in key order.

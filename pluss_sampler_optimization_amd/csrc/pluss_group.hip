@@ -45,6 +45,8 @@ struct Rccl {
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
   ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*GroupStart)() = nullptr;
   ncclResult_t (*GroupEnd)() = nullptr;
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
@@ -73,6 +75,8 @@ static Rccl* rccl() {
   R.CommDestroy = (decltype(R.CommDestroy))sym("ncclCommDestroy");
   R.AllReduce = (decltype(R.AllReduce))sym("ncclAllReduce");
   R.AllGather = (decltype(R.AllGather))sym("ncclAllGather");
+  R.Send = (decltype(R.Send))sym("ncclSend");
+  R.Recv = (decltype(R.Recv))sym("ncclRecv");
   R.GroupStart = (decltype(R.GroupStart))sym("ncclGroupStart");
   R.GroupEnd = (decltype(R.GroupEnd))sym("ncclGroupEnd");
   R.GetErrorString = (decltype(R.GetErrorString))sym("ncclGetErrorString");
@@ -192,6 +196,21 @@ struct FaGraph {
   hipGraphExec_t ex = nullptr;
 };
 
+// A device's buffers of the any-order faithful pass (grown on demand): its
+// slice of the caller's list, the range bounds, the per-block bin counts, the
+// all-gathered bin totals of every device, the bins' starts, the words placed
+// by (shard, reference), and, over several devices, the received words, the
+// words in per-shard order and the copy segments; host copies kept alive
+// until the call's streams drain.
+struct PartBufs {
+  struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+  };
+  Buf smp, bounds, hist, tot, rstart, words, recv, fin, seg;
+  std::vector<unsigned long long> h_bounds, h_rstart, h_seg;
+};
+
 }  // namespace pluss
 
 using namespace pluss;
@@ -214,8 +233,7 @@ struct pluss_group {
   std::vector<uint64_t> list_n;
   std::vector<unsigned long long*> hl;    // per local shard: its slice of a host list (clean sampled_hist)
   std::vector<uint64_t> hl_cap;
-  std::vector<unsigned long long*> whole; // per device: uploaded whole lists (faithful, arbitrary order)
-  std::vector<uint64_t> whole_cap;
+  std::vector<pluss::PartBufs> part;      // per device: the any-order faithful pass
   std::map<uint32_t, hipGraphExec_t> graphs;  // dense passes captured per batch size (one local device)
   pluss::FaGraph* fg = nullptr;               // the last faithful pass, captured (pluss_group_gen_faithful)
 };
@@ -242,8 +260,13 @@ static void group_free(pluss_group* G) {
   }
   for (int d = 0; d < G->ndev; ++d) {
     (void)hipSetDevice(G->dev[d]);
-    for (auto* v : {&G->rows, &G->vec, &G->blk, &G->whole})
+    for (auto* v : {&G->rows, &G->vec, &G->blk})
       if (d < (int)v->size() && (*v)[d]) (void)hipFree((*v)[d]);
+    if (d < (int)G->part.size()) {
+      PartBufs& P = G->part[d];
+      for (auto* b : {&P.smp, &P.bounds, &P.hist, &P.tot, &P.rstart, &P.words, &P.recv, &P.fin, &P.seg})
+        if (b->p) (void)hipFree(b->p);
+    }
     if (d < (int)G->comm.size() && G->comm[d] && g_rccl.ok) (void)g_rccl.CommDestroy(G->comm[d]);
     if (d < (int)G->xs.size() && G->xs[d]) (void)hipStreamDestroy(G->xs[d]);
   }
@@ -265,8 +288,7 @@ static int group_setup(pluss_group* G) {
   G->rows.assign(G->ndev, nullptr);
   G->vec.assign(G->ndev, nullptr);
   G->blk.assign(G->ndev, nullptr);
-  G->whole.assign(G->ndev, nullptr);
-  G->whole_cap.assign(G->ndev, 0);
+  G->part.assign(G->ndev, PartBufs{});
   for (int d = 0; d < G->ndev; ++d) {
     PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
     for (int j = 0; j < S; ++j) {
@@ -596,6 +618,226 @@ static void forget_faithful_graph(pluss_group* G) {
   if (G->fg) G->fg->seen = false;
 }
 
+// a device buffer of at least `bytes` (the device's streams drained before it is replaced)
+static int part_buf(pluss_group* G, int d, PartBufs::Buf& b, size_t bytes) {
+  if (b.cap >= bytes && b.p) return PLUSS_OK;
+  PLUSS_HIP_CHECK(hipStreamSynchronize(G->xs[d]));
+  for (int j = 0; j < G->spd; ++j) PLUSS_HIP_CHECK(hipStreamSynchronize(shard(G, d, j)->stream));
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  if (hipMalloc(&b.p, bytes ? bytes : 8) != hipSuccess) {
+    b.p = nullptr;
+    set_error("pluss_group_sampled_hist: hipMalloc of " + std::to_string(bytes) + " bytes failed");
+    return PLUSS_ERR_ALLOC;
+  }
+  b.cap = bytes ? bytes : 8;
+  return PLUSS_OK;
+}
+
+// Faithful mode over an any-order host list (every rank passes the same list),
+// shapes with N % (cls/ds) == 0, all of it on the devices:
+//  1. device gd (of R) uploads only its slice [n*gd/R, n*(gd+1)/R), reads it
+//     once to count its samples per bin (key-range shard g, reference r);
+//  2. one all-gather of the bin totals (R x 6S words) and one host round trip
+//     (the placements and the sorts' launch sizes need them);
+//  3. the device reads its slice again and places each sample's packed word
+//     in its bin's region (g-major: each destination's shards contiguous);
+//  4. over several devices, one grouped RCCL send/receive per device pair
+//     moves each destination's regions there, and a copy puts the received
+//     words in (shard, reference) order; on one device the regions already are;
+//  5. each shard sorts its words and runs the key-range phases (the rows
+//     all-gathered between them), and the pass ends in the dense all-reduce.
+// No sample goes through the host, no device holds more than its slice and
+// its shards' words, and no shard reads another's samples.  A device that
+// fails before the totals marks its block all ones: every rank sees it and
+// fails the pass (PLUSS_ERR_PEER) after taking part in every collective.
+static int group_any_order(pluss_group* G, const uint64_t* samples, uint64_t n, GErr& E, pluss_hist* out) {
+  const int S = G->nshards, R = G->nranks, spd = G->spd;
+  const uint32_t nb = 6u * (uint32_t)S;
+  uint64_t key_end = 0;
+  E.note(pluss_faithful_key_space(&G->cfg, &key_end));
+  if (n >= ((uint64_t)1 << 40)) E.note(PLUSS_ERR_CONFIG, "pluss_group_sampled_hist: at most 2^40 samples");
+  const int wb = faith_word_bytes(G->ctx[0]);
+  std::vector<uint64_t> sl0(G->ndev), sln(G->ndev);
+  std::vector<uint32_t> nblk(G->ndev);
+  if (int rc = join_shards(G)) return rc;  // (the shards' table resets come first)
+  for (int d = 0; d < G->ndev; ++d) {
+    E.note(hip_rc(hipSetDevice(G->dev[d]), "hipSetDevice"));
+    PartBufs& P = G->part[d];
+    const int gd = G->rank0 + d;
+    sl0[d] = (uint64_t)((unsigned __int128)n * gd / R);
+    sln[d] = (uint64_t)((unsigned __int128)n * (gd + 1) / R) - sl0[d];
+    nblk[d] = faith_part_blocks(sln[d], (uint32_t)S);
+    int rc = E.rc;
+    if (!rc) rc = part_buf(G, d, P.tot, (size_t)R * nb * 8);
+    if (!rc) rc = part_buf(G, d, P.smp, sln[d] * 8);
+    if (!rc) rc = part_buf(G, d, P.bounds, ((size_t)S + 1) * 8);
+    if (!rc) rc = part_buf(G, d, P.hist, (size_t)nb * nblk[d] * 4);
+    if (!rc) {
+      P.h_bounds.resize((size_t)S + 1);
+      for (int g = 0; g <= S; ++g) P.h_bounds[g] = (unsigned long long)((unsigned __int128)key_end * g / S);
+      rc = hip_rc(hipMemcpyAsync(P.bounds.p, P.h_bounds.data(), P.h_bounds.size() * 8, hipMemcpyHostToDevice,
+                                 G->xs[d]), "hipMemcpyAsync (bounds)");
+    }
+    if (!rc && sln[d])
+      rc = hip_rc(hipMemcpyAsync(P.smp.p, samples + sl0[d], sln[d] * 8, hipMemcpyHostToDevice, G->xs[d]),
+                  "hipMemcpyAsync (list slice)");
+    unsigned long long* own = P.tot.p ? (unsigned long long*)P.tot.p + (size_t)gd * nb : nullptr;
+    if (!rc)
+      rc = faith_part_count(shard(G, d, 0), (const uint64_t*)P.smp.p, sln[d], (const unsigned long long*)P.bounds.p,
+                            (uint32_t)S, (uint32_t*)P.hist.p, nblk[d], own, G->xs[d]);
+    if (rc) {
+      E.note(rc);
+      if (!own) return rc;  // (no buffer to take part in the gather with: nothing else to do)
+      E.note(hip_rc(hipMemsetAsync(own, 0xFF, (size_t)nb * 8, G->xs[d]), "hipMemsetAsync"));
+    }
+  }
+  std::vector<unsigned long long*> tots(G->ndev);
+  for (int d = 0; d < G->ndev; ++d) tots[d] = (unsigned long long*)G->part[d].tot.p;
+  if (int rc = gather_blocks(G, tots, (size_t)6 * R)) return rc;
+  // the one host round trip: every device's bin totals
+  std::vector<unsigned long long> T((size_t)R * nb);
+  PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
+  PLUSS_HIP_CHECK(hipMemcpyAsync(T.data(), tots[0], T.size() * 8, hipMemcpyDeviceToHost, G->xs[0]));
+  for (int d = 0; d < G->ndev; ++d) {
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    PLUSS_HIP_CHECK(hipStreamSynchronize(G->xs[d]));
+  }
+  bool failed = false;
+  for (int e = 0; e < R; ++e) failed |= T[(size_t)e * nb] == ~0ull;
+  // per (shard, reference): its words over every device
+  std::vector<uint64_t> bin_all(nb, 0);
+  if (!failed)
+    for (int e = 0; e < R; ++e)
+      for (uint32_t x = 0; x < nb; ++x) bin_all[x] += T[(size_t)e * nb + x];
+  for (uint32_t x = 0; x < nb && !failed; ++x)
+    if (bin_all[x] > 0xFFFFFFFFull) {
+      E.note(PLUSS_ERR_CONFIG, "faithful mode: at most 2^32-1 samples per reference and shard");
+      failed = true;  // (the same on every rank)
+    }
+  if (failed) E.note(PLUSS_ERR_PEER, "a device's partition of the list failed");
+  // each device's placement and, over several devices, the exchange
+  std::vector<const unsigned char*> fin(G->ndev, nullptr);
+  std::vector<std::vector<uint64_t>> foff(G->ndev);  // per local shard and reference: its words' start in fin
+  for (int d = 0; d < G->ndev && !failed; ++d) {
+    E.note(hip_rc(hipSetDevice(G->dev[d]), "hipSetDevice"));
+    PartBufs& P = G->part[d];
+    const int gd = G->rank0 + d;
+    const unsigned long long* mine = T.data() + (size_t)gd * nb;
+    P.h_rstart.assign(nb, 0);
+    for (uint32_t x = 1; x < nb; ++x) P.h_rstart[x] = P.h_rstart[x - 1] + mine[x - 1];
+    int rc = part_buf(G, d, P.rstart, (size_t)nb * 8);
+    if (!rc) rc = part_buf(G, d, P.words, sln[d] * wb);
+    if (!rc)
+      rc = hip_rc(hipMemcpyAsync(P.rstart.p, P.h_rstart.data(), (size_t)nb * 8, hipMemcpyHostToDevice, G->xs[d]),
+                  "hipMemcpyAsync (bin starts)");
+    if (!rc)
+      rc = faith_part_scatter(shard(G, d, 0), (const uint64_t*)P.smp.p, sln[d], (const unsigned long long*)P.bounds.p,
+                              (uint32_t)S, (uint32_t*)P.hist.p, nblk[d], (const unsigned long long*)P.rstart.p,
+                              P.words.p, G->xs[d]);
+    E.note(rc);
+    foff[d].assign((size_t)spd * 6, 0);
+    if (R == 1) {  // the regions are already per (shard, reference)
+      fin[d] = (const unsigned char*)P.words.p;
+      for (int x = 0; x < spd * 6; ++x) foff[d][x] = P.h_rstart[x];
+    }
+  }
+  if (R > 1 && !failed) {
+    // what each device receives: from source e, e's words of this device's shards
+    std::vector<uint64_t> rtot(G->ndev, 0);
+    for (int d = 0; d < G->ndev; ++d) {
+      const int gd = G->rank0 + d;
+      for (int e = 0; e < R; ++e)
+        for (int x = 0; x < spd * 6; ++x) rtot[d] += T[(size_t)e * nb + (size_t)gd * spd * 6 + x];
+      PartBufs& P = G->part[d];
+      E.note(hip_rc(hipSetDevice(G->dev[d]), "hipSetDevice"));
+      E.note(part_buf(G, d, P.recv, rtot[d] * wb));
+      E.note(part_buf(G, d, P.fin, rtot[d] * wb));
+      E.note(part_buf(G, d, P.seg, (size_t)R * spd * 6 * 3 * 8));
+    }
+    if (E.rc) return E.rc;  // (allocation failures here are on every rank alike only by chance: reported, not hung)
+    PLUSS_NCCL_CHECK(g_rccl.GroupStart());
+    for (int d = 0; d < G->ndev; ++d) {
+      PartBufs& P = G->part[d];
+      const int gd = G->rank0 + d;
+      uint64_t roff = 0;
+      for (int e = 0; e < R; ++e) {
+        uint64_t sc = 0, rc = 0;
+        for (int x = 0; x < spd * 6; ++x) {
+          sc += T[(size_t)gd * nb + (size_t)e * spd * 6 + x];
+          rc += T[(size_t)e * nb + (size_t)gd * spd * 6 + x];
+        }
+        const uint64_t soff = P.h_rstart[(size_t)e * spd * 6];
+        if (sc)
+          PLUSS_NCCL_CHECK(g_rccl.Send((const unsigned char*)P.words.p + soff * wb, sc * wb, ncclUint8, e, G->comm[d],
+                                       G->xs[d]));
+        if (rc)
+          PLUSS_NCCL_CHECK(g_rccl.Recv((unsigned char*)P.recv.p + roff * wb, rc * wb, ncclUint8, e, G->comm[d],
+                                       G->xs[d]));
+        roff += rc;
+      }
+    }
+    PLUSS_NCCL_CHECK(g_rccl.GroupEnd());
+    // the received blocks [source][shard][reference] into [shard][reference][source]
+    for (int d = 0; d < G->ndev; ++d) {
+      PartBufs& P = G->part[d];
+      const int gd = G->rank0 + d;
+      PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+      uint64_t o = 0;
+      for (int x = 0; x < spd * 6; ++x) {
+        foff[d][x] = o;
+        for (int e = 0; e < R; ++e) o += T[(size_t)e * nb + (size_t)gd * spd * 6 + x];
+      }
+      P.h_seg.clear();
+      uint64_t roff = 0, maxn = 0;
+      for (int e = 0; e < R; ++e) {
+        uint64_t before_e = 0;
+        for (int x = 0; x < spd * 6; ++x) {
+          const uint64_t c = T[(size_t)e * nb + (size_t)gd * spd * 6 + x];
+          uint64_t at = foff[d][x];
+          for (int e2 = 0; e2 < e; ++e2) at += T[(size_t)e2 * nb + (size_t)gd * spd * 6 + x];
+          if (c) {
+            P.h_seg.push_back(roff + before_e);
+            P.h_seg.push_back(at);
+            P.h_seg.push_back(c);
+            maxn = std::max(maxn, c);
+          }
+          before_e += c;
+        }
+        roff += before_e;
+      }
+      const uint32_t nseg = (uint32_t)(P.h_seg.size() / 3);
+      if (nseg)
+        PLUSS_HIP_CHECK(hipMemcpyAsync(P.seg.p, P.h_seg.data(), P.h_seg.size() * 8, hipMemcpyHostToDevice, G->xs[d]));
+      if (int rc = faith_seg_copy((const unsigned long long*)P.seg.p, nseg, maxn, P.recv.p, P.fin.p, wb, G->xs[d]))
+        return rc;
+      fin[d] = (const unsigned char*)P.fin.p;
+    }
+  }
+  if (int rc = fork_shards(G)) return rc;  // (every shard's sort after its device's words)
+  ShardFn loc = [&](pluss_ctx* c, int d, int j, int g, uint64_t* row) -> int {
+    if (failed || !fin[d]) {
+      set_error("a device's partition of the list failed");
+      return PLUSS_ERR_PEER;
+    }
+    const void* in[6];
+    uint64_t cnt[6], all[6], before[6];
+    for (int r = 0; r < 6; ++r) {
+      cnt[r] = bin_all[(size_t)g * 6 + r];
+      all[r] = before[r] = 0;
+      for (int g2 = 0; g2 < S; ++g2) {
+        all[r] += bin_all[(size_t)g2 * 6 + r];
+        if (g2 < g) before[r] += bin_all[(size_t)g2 * 6 + r];
+      }
+      in[r] = fin[d] + foff[d][(size_t)j * 6 + r] * wb;
+    }
+    return faith_shards_local_words(c, in, cnt, all, before, row, c->stream);
+  };
+  if (int rc = group_faithful(G, loc, nullptr, nullptr, E)) return rc;
+  return collect(G, E, out);
+}
+
 }  // namespace pluss
 
 extern "C" {
@@ -904,7 +1146,10 @@ int pluss_group_sampled_hist(pluss_group* G, const uint64_t* samples, uint64_t n
     set_error("faithful mode needs N % (chunk*threads) == 0 (lockstep interleaving order)");
     return PLUSS_ERR_CONFIG;  // (the same on every rank)
   }
-  // faithful: r10's six samplers, each over its reference's samples in list order
+  if (G->m.fast) return group_any_order(G, samples, n, E, out);
+  // faithful, (key, sink) pairs (N % (cls/ds) != 0; not key-range sharded):
+  // the job's first shard runs r10's six samplers, each over its reference's
+  // samples in list order
   std::vector<uint64_t> per[6];
   for (uint64_t i = 0; i < n; ++i) {
     const uint32_t r = (uint32_t)(samples[i] >> 60);
@@ -914,65 +1159,21 @@ int pluss_group_sampled_hist(pluss_group* G, const uint64_t* samples, uint64_t n
     }
     per[r].push_back(samples[i]);
   }
-  uint64_t totals[6], all = 0;
-  for (int r = 0; r < 6; ++r) all += (totals[r] = per[r].size());
-  if (!G->m.fast) {
-    // (key, sink) pairs (N % (cls/ds) != 0) are not key-range sharded: the job's first shard runs every sampler
-    if (G->rank0 == 0 && !E.rc) {
-      (void)hipSetDevice(G->dev[0]);
-      pluss_ctx* c = G->ctx[0];
-      for (int r = 0; r < 6 && !E.rc; ++r) {
-        if (per[r].empty()) continue;
-        uint64_t* dl = nullptr;
-        int rc = hip_rc(hipMalloc((void**)&dl, per[r].size() * 8), "hipMalloc (group list)");
-        if (!rc) rc = hip_rc(hipMemcpy(dl, per[r].data(), per[r].size() * 8, hipMemcpyHostToDevice), "hipMemcpy");
-        if (!rc) rc = pluss_dev_faithful_hist(c, r, dl, per[r].size(), c->stream);
-        if (!rc) rc = hip_rc(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
-        if (dl) (void)hipFree(dl);
-        E.note(rc);
-      }
+  if (G->rank0 == 0 && !E.rc) {
+    (void)hipSetDevice(G->dev[0]);
+    pluss_ctx* c = G->ctx[0];
+    for (int r = 0; r < 6 && !E.rc; ++r) {
+      if (per[r].empty()) continue;
+      uint64_t* dl = nullptr;
+      int rc = hip_rc(hipMalloc((void**)&dl, per[r].size() * 8), "hipMalloc (group list)");
+      if (!rc) rc = hip_rc(hipMemcpy(dl, per[r].data(), per[r].size() * 8, hipMemcpyHostToDevice), "hipMemcpy");
+      if (!rc) rc = pluss_dev_faithful_hist(c, r, dl, per[r].size(), c->stream);
+      if (!rc) rc = hip_rc(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+      if (dl) (void)hipFree(dl);
+      E.note(rc);
     }
-    return collect_tables(G, E, out);
   }
-  // every device holds the whole lists once; each shard keeps its key range
-  uint64_t key_end = 0;
-  E.note(pluss_faithful_key_space(&G->cfg, &key_end));
-  std::vector<int> dev_ok(G->ndev, 0);
-  for (int d = 0; d < G->ndev && !E.rc; ++d) {
-    int rc = hip_rc(hipSetDevice(G->dev[d]), "hipSetDevice");
-    if (!rc && G->whole_cap[d] < all) {
-      for (int j = 0; j < G->spd; ++j) (void)hipStreamSynchronize(shard(G, d, j)->stream);
-      if (G->whole[d]) (void)hipFree(G->whole[d]);
-      G->whole[d] = nullptr;
-      G->whole_cap[d] = 0;
-      rc = hip_rc(hipMalloc((void**)&G->whole[d], (all ? all : 1) * 8), "hipMalloc (group lists)");
-      if (rc) G->whole[d] = nullptr;
-      else G->whole_cap[d] = all;
-    }
-    uint64_t off = 0;
-    for (int r = 0; r < 6 && !rc; ++r) {
-      rc = hip_rc(hipMemcpyAsync(G->whole[d] + off, per[r].data(), per[r].size() * 8, hipMemcpyHostToDevice,
-                                 G->xs[d]), "hipMemcpyAsync (group lists)");
-      off += per[r].size();
-    }
-    if (!rc) rc = hip_rc(hipStreamSynchronize(G->xs[d]), "hipStreamSynchronize");
-    E.note(rc);
-    dev_ok[d] = rc == PLUSS_OK;
-  }
-  ShardFn sel = [&](pluss_ctx* c, int d, int, int g, uint64_t* row) -> int {
-    if (!dev_ok[d]) {
-      set_error("this device's copy of the lists failed");
-      return PLUSS_ERR_PEER;
-    }
-    const uint64_t lo = (uint64_t)((unsigned __int128)key_end * g / S);
-    const uint64_t hi = (uint64_t)((unsigned __int128)key_end * (g + 1) / S);
-    return pluss_dev_faithful_shards_select(c, (const uint64_t*)G->whole[d], totals, lo, hi, row, c->stream);
-  };
-  ShardFn loc = [&](pluss_ctx* c, int d, int, int g, uint64_t* row) {
-    return pluss_dev_faithful_shards_local_selected(c, (const uint64_t*)G->rows[d], g, S, row, c->stream);
-  };
-  if (int rc = group_faithful(G, sel, loc, nullptr, E)) return rc;
-  return collect(G, E, out);
+  return collect_tables(G, E, out);
 }
 
 int pluss_group_gen_faithful(pluss_group* G, uint64_t seed, const uint64_t totals[6], pluss_hist* out) {

@@ -188,6 +188,19 @@ int faith_shards_select(pluss_ctx* ctx, const uint64_t* d_lists, const uint64_t*
                         uint64_t key_hi, uint64_t* d_row, hipStream_t s);
 int faith_shards_local_selected(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards,
                                 uint64_t* d_row, hipStream_t s);
+// arbitrary-order lists partitioned by (key-range shard, reference) on the
+// device (the group's any-order faithful pass), and phase 1 over the words
+uint32_t faith_part_blocks(uint64_t n, uint32_t S);
+int faith_word_bytes(const pluss_ctx* ctx);
+int faith_part_count(pluss_ctx* ctx, const uint64_t* d_smp, uint64_t n, const unsigned long long* d_bounds,
+                     uint32_t S, uint32_t* d_hist, uint32_t B, unsigned long long* d_tot, hipStream_t s);
+int faith_part_scatter(pluss_ctx* ctx, const uint64_t* d_smp, uint64_t n, const unsigned long long* d_bounds,
+                       uint32_t S, uint32_t* d_hist, uint32_t B, const unsigned long long* d_rstart, void* d_out,
+                       hipStream_t s);
+int faith_seg_copy(const unsigned long long* d_seg, uint32_t nseg, uint64_t maxn, const void* src, void* dst,
+                   int wbytes, hipStream_t s);
+int faith_shards_local_words(pluss_ctx* ctx, const void* const in[6], const uint64_t* cnt, const uint64_t* all,
+                             const uint64_t* before, uint64_t* d_row, hipStream_t s);
 int faith_shards_carry(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards, uint64_t* d_row,
                        hipStream_t s);
 int faith_shards_cut(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards, uint64_t* d_row,

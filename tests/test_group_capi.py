@@ -170,6 +170,50 @@ def test_group_faithful_replays_equal_one_device(spd):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("spd", [1, 3, 8])
+@pytest.mark.parametrize("N,total", [(1024, 1 << 20), (2048, 1 << 20)])
+def test_group_any_order_equals_one_device(N, total, spd):
+    """r10's any-order input through the group, partitioned on the device by
+    (key-range shard, reference) (4-byte words at N=1024, 8-byte at 2048):
+    the one-device radix pass over the same lists; then a shorter shuffled
+    list on the same group (buffers reused), and a malformed sample
+    (PLUSS_ERR_INPUT)."""
+    P = _P()
+    import torch
+    c = P.SamplerConfig(n=N, threads=8, mode="faithful")
+    st = torch.cuda.Stream()
+
+    def lists(seed, tot):
+        counts = P.default_counts(N, tot)
+        lst = np.concatenate([P.expand_samples(c, seed, r, 0, n) for r, n in enumerate(counts)])
+        return counts, lst
+
+    def one(counts, lst):
+        d = torch.from_numpy(lst.view(np.int64)).to("cuda")
+        with P.Context(c) as ctx:
+            ctx.reset(st.cuda_stream)
+            ctx.faithful_hist_refs(d.data_ptr(), counts, st.cuda_stream)
+            st.synchronize()
+            return ctx.fetch()
+    counts, lst = lists(5, total)
+    counts2, lst2 = lists(6, total // 3)
+    w1, w2 = one(counts, lst), one(counts2, lst2)
+    with P.Group(c, [0], spd) as g:
+        h = g.sampled_hist(lst)
+        assert h.bins == w1.bins and list(h.traversed) == list(w1.traversed)
+        h = g.sampled_hist(np.random.default_rng(1).permutation(lst2))
+        assert h.bins == w2.bins and list(h.traversed) == list(w2.traversed)
+        h = g.sampled_hist(lst)  # (again, after the smaller one)
+        assert h.bins == w1.bins and list(h.traversed) == list(w1.traversed)
+        bad = lst2.copy()
+        bad[len(bad) // 2] = (3 << 60) | (np.uint64(N + 5) << np.uint64(40))
+        with pytest.raises(P.PlussError, match="PLUSS_ERR_INPUT"):
+            g.sampled_hist(bad)
+        h = g.sampled_hist(lst2)  # (a failed pass leaves the group usable)
+        assert h.bins == w2.bins
+
+
+@pytest.mark.gpu
 def test_group_pairs_shape_and_errors(orc):
     """A shape with N % (cls/ds) != 0 ((key, sink) pairs, not key-range
     sharded: the job's first shard runs the samplers) equals one device; a
