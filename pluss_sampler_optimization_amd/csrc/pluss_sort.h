@@ -47,6 +47,7 @@ constexpr uint32_t SC = 4 * SBATCH;       // words per count/scatter chunk (both
 constexpr uint32_t SCAP = 4096;           // largest item sorted in LDS (k_srt_final)
 constexpr int SDIG = 8;                   // largest digit of a split (256 children)
 constexpr int SDEPTH = 10;                // k_srt_deep's levels (64-bit words, 8-bit digits, + the item)
+constexpr uint32_t SSPLIT = 3072;         // a split parent's children average at most this many words
 static_assert(SCAP == SBATCH, "an item is one batch");
 
 // the references of one sort (a kernel argument)
@@ -93,9 +94,11 @@ __host__ __device__ inline uint32_t srt_d1(uint64_t n, uint32_t wb) {
   d = d > (uint32_t)SDIG ? (uint32_t)SDIG : d;
   return d > wb ? wb : d;
 }
-// children of a parent past SCAP: a digit of d2 bits (children of about SCAP / 2)
+// children of a parent past SCAP: a digit of d2 bits, children of SSPLIT / 2 to
+// SSPLIT words on average (uniform input: a few sd of ~50 around it, far below
+// SCAP; k_srt_final's batches are mostly full and level 2 writes longer runs)
 __host__ __device__ inline uint32_t srt_split_bits(uint32_t cnt, uint32_t hi) {
-  uint32_t D = srt_log2_ceil((cnt + SCAP / 2 - 1) / (SCAP / 2));
+  uint32_t D = srt_log2_ceil((cnt + SSPLIT - 1) / SSPLIT);
   D = D < 1 ? 1 : (D > (uint32_t)SDIG ? (uint32_t)SDIG : D);
   return D > hi ? hi : D;
 }
@@ -592,11 +595,11 @@ __device__ __forceinline__ void srt_block_scan_lds(uint32_t* v, uint32_t len, ui
   srt_lds_sync();
 }
 
-template <typename PT>
-__device__ __forceinline__ void srt_item_load(const PT* __restrict__ src, uint32_t s, uint32_t cnt, PT (&w)[SE]) {
+template <typename PT, int NSE>
+__device__ __forceinline__ void srt_item_load(const PT* __restrict__ src, uint32_t s, uint32_t cnt, PT (&w)[NSE]) {
   const uint32_t last = cnt - 1;
 #pragma unroll
-  for (int k = 0; k < SE; ++k) {
+  for (int k = 0; k < NSE; ++k) {
     const uint32_t i = (uint32_t)k * SB + threadIdx.x;
     w[k] = __builtin_nontemporal_load(src + s + (i < last ? i : last));
   }
@@ -609,12 +612,12 @@ __device__ __forceinline__ void srt_item_load(const PT* __restrict__ src, uint32
 // goes out in order.  Groups average at most one payload (D = log2(cnt)), so
 // the count is a short loop in every lane (no per-thread insertion sort, which
 // diverged).  bb, ob: SCAP payloads; c: SCAP + 1 words; all free on return.
-template <typename PT, typename KT>
-__device__ __forceinline__ void srt_item_sort(const PT (&w)[SE], uint32_t s, uint32_t cnt, uint32_t hi, KT prefix,
+template <typename PT, typename KT, int NSE>
+__device__ __forceinline__ void srt_item_sort(const PT (&w)[NSE], uint32_t s, uint32_t cnt, uint32_t hi, KT prefix,
                                               KT* __restrict__ OUT, PT* bb, PT* ob, uint32_t* c, uint32_t* wsum) {
   if (hi == 0) {  // every payload equal
 #pragma unroll
-    for (int k = 0; k < SE; ++k) {
+    for (int k = 0; k < NSE; ++k) {
       const uint32_t i = (uint32_t)k * SB + threadIdx.x;
       if (i < cnt) OUT[s + i] = prefix | (KT)w[k];
     }
@@ -626,18 +629,18 @@ __device__ __forceinline__ void srt_item_sort(const PT (&w)[SE], uint32_t s, uin
   const uint32_t nb = 1u << D, lo = hi - D, mask = nb - 1;
   for (uint32_t i = threadIdx.x; i < nb; i += SB) c[i] = 0;
   srt_lds_sync();
-  uint32_t r[SE];
+  uint32_t r[NSE];
 #pragma unroll
-  for (int k = 0; k < SE; ++k) {
+  for (int k = 0; k < NSE; ++k) {
     const uint32_t i = (uint32_t)k * SB + threadIdx.x;
     r[k] = i < cnt ? atomicAdd(&c[srt_dig(w[k], lo, mask)], 1u) : 0u;
   }
   if (threadIdx.x == 0) c[nb] = cnt;  // (the group end of the last digit; visible after the scan's barrier)
   srt_lds_sync();
   srt_block_scan_lds(c, nb, wsum);
-  uint32_t g0[SE], g1[SE];
+  uint32_t g0[NSE], g1[NSE];
 #pragma unroll
-  for (int k = 0; k < SE; ++k) {
+  for (int k = 0; k < NSE; ++k) {
     const uint32_t i = (uint32_t)k * SB + threadIdx.x;
     const uint32_t d = srt_dig(w[k], lo, mask);
     g0[k] = c[d];
@@ -651,7 +654,7 @@ __device__ __forceinline__ void srt_item_sort(const PT (&w)[SE], uint32_t s, uin
     return;
   }
 #pragma unroll
-  for (int k = 0; k < SE; ++k) {
+  for (int k = 0; k < NSE; ++k) {
     const uint32_t i = (uint32_t)k * SB + threadIdx.x;
     if (i < cnt) {
       const uint32_t p = g0[k] + r[k];
@@ -694,15 +697,30 @@ __global__ __launch_bounds__(SB) void k_srt_final(const SrtRefs a, const SrtPare
       else atomicOr(&dp.flags[0], FLAG_SORT);  // never written past the list: the pass reports it instead
     }
   };
+  // an item of cnt <= SCAP payloads in NSE registers per thread, the fewest
+  // that hold it (the slots past cnt are predicated off but still issued)
+  auto item = [&](const PT* __restrict__ src, uint32_t s, uint32_t cnt, uint32_t hi) {
+    if (cnt <= 8 * SB) {
+      PT w[8];
+      srt_item_load<PT, 8>(src, s, cnt, w);
+      srt_item_sort<PT, KT, 8>(w, s, cnt, hi, prefix, OUT, bb, ob, c, wsum);
+    } else if (cnt <= 12 * SB) {
+      PT w[12];
+      srt_item_load<PT, 12>(src, s, cnt, w);
+      srt_item_sort<PT, KT, 12>(w, s, cnt, hi, prefix, OUT, bb, ob, c, wsum);
+    } else {
+      PT w[SE];
+      srt_item_load<PT, SE>(src, s, cnt, w);
+      srt_item_sort<PT, KT, SE>(w, s, cnt, hi, prefix, OUT, bb, ob, c, wsum);
+    }
+  };
   if (P.d2 == 0) {
     if (blockIdx.x != 0 || P.count == 0) return;
     if (P.count > SCAP) {
       deep(P.start, P.count, hi1, 0);
       return;
     }
-    PT w[SE];
-    srt_item_load(X1, P.start, P.count, w);
-    srt_item_sort<PT, KT>(w, P.start, P.count, hi1, prefix, OUT, bb, ob, c, wsum);
+    item(X1, P.start, P.count, hi1);
     return;
   }
   const uint32_t nc = 1u << P.d2, hi = hi1 - P.d2;
@@ -717,9 +735,7 @@ __global__ __launch_bounds__(SB) void k_srt_final(const SrtRefs a, const SrtPare
       deep(s, cnt, hi, 1);
       continue;
     }
-    PT w[SE];
-    srt_item_load(Y, s, cnt, w);
-    srt_item_sort<PT, KT>(w, s, cnt, hi, prefix, OUT, bb, ob, c, wsum);
+    item(Y, s, cnt, hi);
   }
 }
 

@@ -31,6 +31,16 @@ static int run(int seed) {
   if (pluss_format_hist("reuse", merged.data(), nm, text.data(), text.size(), &len)) return 4;
   if (pluss_format_mrc(mrc.data(), nmrc, text.data(), text.size(), &len)) return 5;
   if (pluss_cri_v1(4, raw.data(), raw.size(), out.data(), out.size(), &n)) return 6;
+  // r10's host half in one call: six CRI threads, merge, AET, text
+  {
+    pluss_hist h = {raw.data(), raw.size(), raw.size(), {0}};
+    std::vector<pluss_kv> reuse(1 << 16), m2(400000);
+    uint64_t nr = 0, nm2 = 0, tl = 0;
+    if (pluss_r10_host_pipeline(4, &h, 6, reuse.data(), reuse.size(), &nr, m2.data(), m2.size(), &nm2, text.data(),
+                                text.size(), &tl))
+      return 8;
+    if (nm2 == 0 || tl == 0) return 9;
+  }
   // a buffer too small: an error code, nothing written past it, the needed length reported
   char small[9];
   small[8] = 'X';

@@ -15,6 +15,7 @@ SB, SE = 256, 16
 SBATCH = SB * SE
 SC = 4 * SBATCH
 SCAP = 4096
+SSPLIT = 3072
 SDIG = 8
 
 
@@ -32,7 +33,7 @@ def d1_of(n, wb):
 
 
 def split_bits(cnt, hi):
-    D = log2_ceil((cnt + SCAP // 2 - 1) // (SCAP // 2))
+    D = log2_ceil((cnt + SSPLIT - 1) // SSPLIT)
     D = max(1, min(D, SDIG))
     return min(D, hi)
 
