@@ -19,7 +19,8 @@ HOST_LIB = os.path.join(LIBDIR, "libpluss_host.so")
 HOST_SOURCES = ["host/pluss_host.cpp"]
 CLI = os.path.join(LIBDIR, "pluss_cli")
 ARCH = os.environ.get("PLUSS_OFFLOAD_ARCH", "gfx950")
-SOURCES = ["pluss_kernels.hip", "pluss_faithful.hip", "pluss_fa_w32.hip", "pluss_fa_w64.hip", "pluss_fa_smp.hip",
+SOURCES = ["pluss_kernels.hip", "pluss_faithful.hip", "pluss_fa_w32.hip", "pluss_fa_w64.hip", "pluss_fa_w32p.hip",
+           "pluss_fa_smp.hip",
            "pluss_fa_gen.hip", "pluss_fa_uni.hip", "pluss_uniform.hip", "pluss_group.hip",
            "pluss_capi.hip"]
 HEADERS = ["pluss_model.h", "pluss_internal.h", "pluss_device.h", "pluss_faithful.h", "pluss_sort.h", "pluss_uniform.h"]

@@ -195,4 +195,15 @@ __device__ __forceinline__ void bt_finish(WaveCache& w, BlockTable bt, GTable g)
   }
 }
 
+// the radix sort's top-level bucket (pluss_sort.h): range [start, start +
+// count) of the concatenated arrays; split past SCAP into 2^d2 children through
+// nc2 level-2 chunks.  (Here: the scan pipeline reads the parents' starts to put
+// 4-byte payloads' digits back, pluss_faithful.h SRC_W32P.)
+struct SrtParent {
+  uint32_t start, count, ref, b1;
+  uint32_t d2, nc2, cbase, h2off;
+  uint32_t src;         // where its payloads are in X1 (the counted path: start)
+  uint32_t ybase, cb2;  // count-free level 2: its children's region in Y, its first child's fill word
+};
+
 }  // namespace pluss

@@ -142,7 +142,10 @@ constexpr int FPW = FPART + 2;              // ... + the start count and the Q1 
 constexpr int KL = 64;                      // local starts kept per tile (one wave lane each)
 __host__ __device__ inline uint64_t fa_tiles(uint64_t n) { return (n + TILE - 1) / TILE; }
 
-enum : int { SRC_W32 = 0, SRC_W64 = 1, SRC_SAMPLES = 2, SRC_GEN = 3, SRC_UNI = 4 };
+enum : int { SRC_W32 = 0, SRC_W64 = 1, SRC_SAMPLES = 2, SRC_GEN = 3, SRC_UNI = 4, SRC_W32P = 5 };
+// SRC_W32P: the radix sort's output as 4-byte payloads (words past 32 bits
+// without their top-level digit); a payload's word is its parent bucket's
+// digit put back, looked up from the sort's parents (FaRefs::ppar, w32p_*)
 static_assert(TILE == UG_TILE, "the uniform generator stages the pipeline's tiles");
 // sources whose elements are packed samples (SRC_UNI: generated into LDS from the plan)
 template <int SRC>
@@ -185,6 +188,11 @@ struct FaRefs {
   PkView pv[6];
   KeyGen kg[6];        // SRC_GEN
   const UniSet* us;    // SRC_UNI: the plan of the uniform key-order lists (device memory)
+  // SRC_W32P: the sort's parents (device memory; reference r's are ppar[ppb[r], ppb[r] + ppn[r]), their
+  // starts in the concatenated lists, peoff[r] = reference r's first; a parent b's words are b << phi[r] | payload)
+  const SrtParent* ppar;
+  uint32_t ppb[6], ppn[6], phi[6];
+  uint64_t peoff[6];
   uint32_t fast;       // the local pass's fast path applies to the shape (fa_run)
   uint32_t unidec;     // SRC_UNI: keys below 2^61 and leaf key spans below 2^32 (uni_stage DEC)
 };
@@ -246,6 +254,9 @@ __device__ __forceinline__ Elem elem_of_word(const Model& m, const PkView& v, ui
 
 template <int SRC>
 using fa_raw_t = typename std::conditional<SRC == SRC_W32, uint32_t, unsigned long long>::type;
+// an element as it is in memory (SRC_W32P: the 4-byte payload of a 64-bit word)
+template <int SRC>
+using fa_mem_t = typename std::conditional<SRC == SRC_W32 || SRC == SRC_W32P, uint32_t, unsigned long long>::type;
 
 // the tile's reference (wave-uniform) and its place in it
 struct FaTile {
@@ -340,7 +351,42 @@ struct FaOne {
   const void* src;
   PkView pv;
   const UniSet* us;
+  const SrtParent* ppar;  // SRC_W32P: this reference's parents
+  uint32_t pn, phi;
+  uint64_t peoff;
 };
+
+// SRC_W32P: the parent holding element i of the reference (the last parent
+// whose start is at most i; empty parents share their successor's start)
+__device__ __forceinline__ uint32_t w32p_find(const FaOne& o, uint64_t i) {
+  uint32_t lo = 0, hi = o.pn;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if ((uint64_t)o.ppar[mid].start - o.peoff <= i) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+// a tile's prefixes: its elements [base, base + mt) lie in at most two parents
+// (ok; elements below B in the first), else each element looks its parent up
+struct W32P {
+  unsigned long long pa, pb;
+  uint64_t B;
+  bool ok;
+};
+__device__ __forceinline__ W32P w32p_tile(const FaOne& o, uint64_t base, uint32_t mt) {
+  W32P w;
+  const uint32_t b0 = w32p_find(o, base), b1 = w32p_find(o, base + (mt ? mt - 1 : 0));
+  w.pa = (unsigned long long)b0 << o.phi;
+  w.pb = (unsigned long long)b1 << o.phi;
+  w.B = b1 > b0 ? (uint64_t)o.ppar[b1].start - o.peoff : ~0ull;
+  w.ok = b1 <= b0 + 1;  // (an empty parent between them: each element looks up its own)
+  return w;
+}
+__device__ __forceinline__ unsigned long long w32p_word(const FaOne& o, const W32P& w, uint64_t i, uint32_t v) {
+  if (w.ok) return (i < w.B ? w.pa : w.pb) | v;
+  return ((unsigned long long)w32p_find(o, i) << o.phi) | v;
+}
 
 // This thread's run of the tile: keys (KEY_EMPTY past the end), cases (2 bits
 // at 2k) and tid == 0 flags (bit 2k).  Memory sources: coalesced loads
@@ -360,16 +406,25 @@ __device__ __forceinline__ void fa_load_run(const Model& m, const FaOne& o, cons
     if constexpr (SRC == SRC_UNI) {
       // (generated into sh.raw by fa_uni_pre, once, before the per-reference dispatch)
     } else {
-      const fa_raw_t<SRC>* src = static_cast<const fa_raw_t<SRC>*>(o.src) + T.base;
-      fa_raw_t<SRC> v[EPT];  // every load issued before the first wait (partial tiles: clamped, no branch)
+      const fa_mem_t<SRC>* src = static_cast<const fa_mem_t<SRC>*>(o.src) + T.base;
+      fa_mem_t<SRC> v[EPT];  // every load issued before the first wait (partial tiles: clamped, no branch)
       const uint32_t last = T.mt - 1;
 #pragma unroll
       for (int k = 0; k < EPT; ++k) {
         const uint32_t e = (uint32_t)k * NT + threadIdx.x;
         v[k] = src[FULLT ? e : (e < last ? e : last)];
       }
+      if constexpr (SRC == SRC_W32P) {  // the payloads' parent digits put back
+        const W32P pw = w32p_tile(o, T.base, T.mt);
 #pragma unroll
-      for (int k = 0; k < EPT; ++k) sh.raw[fa_slot_n<EPT>((uint32_t)k * NT + threadIdx.x)] = v[k];
+        for (int k = 0; k < EPT; ++k) {
+          const uint32_t e = (uint32_t)k * NT + threadIdx.x;
+          sh.raw[fa_slot_n<EPT>(e)] = w32p_word(o, pw, T.base + (e < last ? e : last), v[k]);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) sh.raw[fa_slot_n<EPT>((uint32_t)k * NT + threadIdx.x)] = v[k];
+      }
       __syncthreads();
     }
 #pragma unroll
@@ -1083,12 +1138,21 @@ __device__ __forceinline__ bool fa_lane_tile(const Model& m, const FaRefs& a, co
   const FaOne o = fa_one_ref<SRC, REF>(a, T);
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
   const fa_raw_t<SRC>* src = SRC == SRC_UNI ? tile : static_cast<const fa_raw_t<SRC>*>(o.src) + T.base;
+  const fa_mem_t<SRC>* msrc = static_cast<const fa_mem_t<SRC>*>(o.src) + T.base;  // (SRC_W32P: the payloads)
   const uint32_t last = T.mt - 1, e0 = wid * (64 * ST) + lane;
-  fa_raw_t<SRC> v[ST];
+  fa_mem_t<SRC> v[ST];  // (SRC_W32P: the payloads; each word is made where it is decoded)
+  W32P pw{};
+  uint32_t be = 0xFFFFFFFFu;  // SRC_W32P: tile elements below be are in the first parent
+  if constexpr (SRC == SRC_W32P) {
+    pw = w32p_tile(o, T.base, T.mt);
+    if (!pw.ok) return false;  // (more than two parents in the tile: the queued pass)
+    be = pw.B - T.base > (uint64_t)TILE ? 0xFFFFFFFFu : (uint32_t)(pw.B - T.base);
+  }
 #pragma unroll
   for (int k = 0; k < ST; ++k) {
     const uint32_t e = e0 + 64u * k;
     if constexpr (SRC == SRC_UNI) v[k] = src[e < last ? e : last];
+    else if constexpr (SRC == SRC_W32P) v[k] = __builtin_nontemporal_load(msrc + (e < last ? e : last));
     else v[k] = __builtin_nontemporal_load(src + (e < last ? e : last));
   }
   // ri*T per case (0xFFFFFFFF: cold) and the tile's first and last keys, in every wave
@@ -1107,8 +1171,14 @@ __device__ __forceinline__ bool fa_lane_tile(const Model& m, const FaRefs& a, co
     if constexpr (SRC == SRC_UNI) return ((unsigned long long)(w >> 35) << 32) | (uint32_t)w;
     else return fa_decode_ref<SRC, true, REF>(m, o.pv, w, b2).key;
   };
-  const unsigned long long base = key_of(src[0]);
-  const unsigned long long kl = key_of(src[last]);
+  unsigned long long base, kl;
+  if constexpr (SRC == SRC_W32P) {
+    base = key_of(pw.pa | msrc[0]);
+    kl = key_of(pw.pb | msrc[last]);
+  } else {
+    base = key_of(src[0]);
+    kl = key_of(src[last]);
+  }
   auto r32 = [](unsigned long long x) { return x == KEY_EMPTY ? 0xFFFFFFFFu : (uint32_t)x; };
   const FaRi r{r32(t0), r32(t1), r32(t2)};
   if (!(kl >= base && kl - base < 0xFFFFFFFFull - rmax && r.r0 != 0xFFFFFFFFu && r.r1 != 0xFFFFFFFFu))
@@ -1125,6 +1195,7 @@ __device__ __forceinline__ bool fa_lane_tile(const Model& m, const FaRefs& a, co
     FaDec d;
     if constexpr (SRC == SRC_UNI) d = fa_dec_staged(v[k]);
     else if constexpr (fa_smp<SRC>()) d = fa_dec_sample<REF>(m, o.pv, (uint64_t)v[k], oddk);
+    else if constexpr (SRC == SRC_W32P) d = fa_dec_word<REF>(m, o.pv, (e0 + 64u * k < be ? pw.pa : pw.pb) | v[k]);
     else d = fa_dec_word<REF>(m, o.pv, v[k]);
     odd |= val ? oddk : 0u;
     if (CHECK) {  // against the previous lane (the step before: its lane 63); integer
@@ -1323,6 +1394,10 @@ __device__ __forceinline__ FaOne fa_one_ref(const FaRefs& a, const FaTile& T) {
   o.src = a.src[R];
   o.pv = a.pv[R];
   o.us = a.us;
+  o.ppar = a.ppar ? a.ppar + a.ppb[R] : nullptr;
+  o.pn = a.ppn[R];
+  o.phi = a.phi[R];
+  o.peoff = a.peoff[R];
   return o;
 }
 
@@ -1358,7 +1433,7 @@ __global__ __launch_bounds__(TB) void k_fa_local(Model m, FaRefs a, unsigned lon
 // current one ran at 2 waves per SIMD and was 1.4x slower at config 3: the
 // scan's dependent chains need the 4 waves per SIMD of this form to issue.)
 template <int SRC>
-constexpr bool fa_mem() { return SRC == SRC_W32 || SRC == SRC_W64 || SRC == SRC_SAMPLES; }
+constexpr bool fa_mem() { return SRC == SRC_W32 || SRC == SRC_W64 || SRC == SRC_W32P || SRC == SRC_SAMPLES; }
 
 template <int SRC, bool CHECK>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4))) void k_fa_local_fast(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
@@ -1397,17 +1472,35 @@ struct FaLmLds {
 template <int SRC>
 constexpr bool fa_lm() { return fa_mem<SRC>() || SRC == SRC_UNI; }
 
-template <int SRC, bool CHECK>
-__global__ __launch_bounds__(fa_lm_nt<SRC>()) __attribute__((amdgpu_waves_per_eu(4))) void k_fa_local_lm(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
+// waves per SIMD asked of the compiler: lists in memory fit 8 (<= 64 VGPRs and
+// <= 80 SGPRs: at 83 SGPRs the SGPR file held 7); the uniform staging needs 4
+template <int SRC, bool PARTT = false>
+constexpr int fa_lm_waves() { return SRC == SRC_UNI || SRC == SRC_W32P || PARTT ? 4 : 8; }
+// the references' partial last tiles (lists in memory): their own small launch
+// of the lane-major path (k_fa_local_lm<.., true>), so the full-tile kernel
+// keeps the full tile's registers and none of them waits for the queued pass
+struct FaPartT {
+  uint32_t n;
+  uint32_t gt[6];
+};
+template <int SRC, bool CHECK, bool PARTT = false>
+__global__ __launch_bounds__(fa_lm_nt<SRC>()) __attribute__((amdgpu_waves_per_eu(fa_lm_waves<SRC, PARTT>()))) void k_fa_local_lm(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
                                                     unsigned long long* __restrict__ part,
                                                     unsigned long long* __restrict__ klist, unsigned long long* slots,
-                                                    unsigned int* slowq, GTable g) {
+                                                    unsigned int* slowq, GTable g, FaPartT pt = FaPartT{}) {
   static_assert(fa_lm<SRC>(), "the stratified generated source: k_fa_local_fast");
+  static_assert(!PARTT || fa_mem<SRC>(), "partial tiles apart: lists in memory");
   constexpr int NT = fa_lm_nt<SRC>();
   __shared__ FaLmLds<SRC> L;
   FaLm<NT>& sh = L.s;
-  const FaTile T = fa_tile(a, blockIdx.x);
-  fa_cold_slot(T, g, slots);
+  uint32_t gsel = blockIdx.x;
+  if constexpr (PARTT) {
+#pragma unroll
+    for (int x = 0; x < 6; ++x) gsel = blockIdx.x == (uint32_t)x ? pt.gt[x] : gsel;
+  }
+  const FaTile T = fa_tile(a, gsel);
+  if (!PARTT) fa_cold_slot(T, g, slots);
+  if (!PARTT && fa_mem<SRC>() && pt.n && T.mt != TILE) return;  // (the partial launch takes it)
   unsigned long long* kl_out = klist + T.gt * (uint64_t)(2 * KL);
   bool done = false;
   // lists in memory: full tiles only, the few partial ones (a reference's last
@@ -1425,16 +1518,20 @@ __global__ __launch_bounds__(fa_lm_nt<SRC>()) __attribute__((amdgpu_waves_per_eu
   else done = fa_lane_tile<SRC, CHECK, R, false, NT>(m, a, T, sh, kl_out, g, L.raw);
     PLUSS_FA_REFS(PLUSS_FA_LM)
 #undef PLUSS_FA_LM
+  } else if (PARTT) {
+#define PLUSS_FA_LM(R) done = fa_lane_tile<SRC, CHECK, R, false, NT>(m, a, T, sh, kl_out, g, L.raw);
+    PLUSS_FA_REFS(PLUSS_FA_LM)
+#undef PLUSS_FA_LM
   } else if (T.mt == TILE) {
 #define PLUSS_FA_LM(R) done = fa_lane_tile<SRC, CHECK, R, true, NT>(m, a, T, sh, kl_out, g, L.raw);
     PLUSS_FA_REFS(PLUSS_FA_LM)
 #undef PLUSS_FA_LM
   }
   if (done) {
-    if (threadIdx.x < FPW) part[blockIdx.x * (uint64_t)FPW + threadIdx.x] = sh.out[threadIdx.x];
-    if (threadIdx.x == FPW) tmax[blockIdx.x] = sh.out[FPW];
+    if (threadIdx.x < FPW) part[T.gt * (uint64_t)FPW + threadIdx.x] = sh.out[threadIdx.x];
+    if (threadIdx.x == FPW) tmax[T.gt] = sh.out[FPW];
   } else if (threadIdx.x == 0) {
-    slowq[1 + atomicAdd(&slowq[0], 1u)] = (unsigned int)blockIdx.x;
+    slowq[1 + atomicAdd(&slowq[0], 1u)] = (unsigned int)T.gt;
   }
 }
 
@@ -1959,9 +2056,19 @@ inline void fa_launch_t(const FaLaunch& L) {
         // (a pass whose chunk phase ran left it empty: no fill launch then)
         if (!b.slowq_clean) (void)hipMemsetAsync(b.slowq, 0, sizeof(unsigned int), L.s);
         b.slowq_clean = false;
-        if constexpr (fa_lm<SRC>())
+        if constexpr (fa_mem<SRC>()) {
+          // full tiles, then the references' partial last tiles in their own launch
+          FaPartT pt{};
+          for (int r = 0; r < 6; ++r)
+            if (L.a.n[r] % TILE) pt.gt[pt.n++] = (uint32_t)(L.a.toff[r] + L.a.n[r] / TILE);
+          hipLaunchKernelGGL((k_fa_local_lm<SRC, CHK>), dim3(t), dim3(fa_lm_nt<SRC>()), 0, L.s, L.m, L.a, b.tmax,
+                             b.dpart, b.klist, b.fslot, b.slowq, L.g, pt);
+          if (pt.n)
+            hipLaunchKernelGGL((k_fa_local_lm<SRC, CHK, true>), dim3(pt.n), dim3(fa_lm_nt<SRC>()), 0, L.s, L.m, L.a,
+                               b.tmax, b.dpart, b.klist, b.fslot, b.slowq, L.g, pt);
+        } else if constexpr (fa_lm<SRC>())
           hipLaunchKernelGGL((k_fa_local_lm<SRC, CHK>), dim3(t), dim3(fa_lm_nt<SRC>()), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
-                             b.fslot, b.slowq, L.g);
+                             b.fslot, b.slowq, L.g, FaPartT{});
         else
           hipLaunchKernelGGL((k_fa_local_fast<SRC, CHK>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart,
                              b.klist, b.fslot, b.slowq, L.g);
@@ -2006,6 +2113,7 @@ enum : int { SH_NONE = 0, SH_LOCAL = 1, SH_CARRY = 2, SH_CUT = 3, SH_SELECTED = 
 // the four sources (pluss_fa_w32.hip, pluss_fa_w64.hip, pluss_fa_smp.hip, pluss_fa_gen.hip)
 void fa_launch_w32(const FaLaunch& L);
 void fa_launch_w64(const FaLaunch& L);
+void fa_launch_w32p(const FaLaunch& L);
 void fa_launch_smp(const FaLaunch& L);
 void fa_launch_gen(const FaLaunch& L);
 void fa_launch_uni(const FaLaunch& L);

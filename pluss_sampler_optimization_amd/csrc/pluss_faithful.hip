@@ -537,7 +537,9 @@ struct SrtPlan {
   SrtRefs a;
   uint64_t ntot, h1, g2max, h2max, nbs;
   bool p32;  // 4-byte payloads
-  size_t o_h1, o_h2, o_bs, o_par, o_cmap, o_tot, o_deep, bytes;
+  size_t o_h1, o_h2, o_bs, o_par, o_cmap, o_tot, o_deep, o_fast, bytes;
+  bool fast1;     // level 1 without its count pass (k_srt_scatter1f; 4-byte payloads)
+  uint64_t wmax;  // the words' range [0, wmax): 4 N^3
 };
 
 static SrtPlan srt_plan(const Model& m, const void* const in[6], const uint64_t cnt[6]) {
@@ -589,7 +591,16 @@ static SrtPlan srt_plan(const Model& m, const void* const in[6], const uint64_t 
   o = al(o + 16);
   P.o_deep = o;
   o = al(o + sizeof(SrtItem) * np * SB);
+  P.o_fast = o;  // cap, off1, fill (np each), ovf, gate, glen, level 2's ovf, gate, glen, then its fills (np * 256)
+  o = al(o + 4 * (3 * (size_t)np + 8 + (size_t)np * SB));
   P.bytes = o;
+  // the count-free level 1: 4-byte payloads, and no reference whose top digit
+  // decides every bit (its whole-bucket items would be read and written at
+  // different places; such shapes are tiny)
+  P.wmax = 4ull * (uint64_t)m.N * (uint64_t)m.N * (uint64_t)m.N;
+  P.fast1 = P.p32;
+  for (int r = 0; r < 6; ++r)
+    if (cnt[r] && wb <= P.a.d1[r]) P.fast1 = false;
   return P;
 }
 
@@ -602,8 +613,11 @@ static void srt_scan(uint32_t* v, uint64_t len, const uint32_t* dlen, uint32_t* 
   hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(SB), 0, s, v, len, dlen, (const uint32_t*)bsum);
 }
 
-template <typename KT, typename PT, bool SMP>
-static int srt_launch(pluss_ctx* ctx, FaithfulBufs& b, const SrtPlan& P, PT* X1, PT* Y, KT* out, hipStream_t s) {
+// OT: the output's type -- KT (the words) or, for 4-byte payloads of longer
+// words, uint32_t (the payloads alone; SRC_W32P puts the digits back)
+template <typename KT, typename PT, bool SMP, typename OT = KT>
+static int srt_launch(pluss_ctx* ctx, FaithfulBufs& b, const SrtPlan& P, PT* X1, PT* Y, OT* out, hipStream_t s) {
+  constexpr bool PFX = std::is_same<OT, KT>::value;
   const Model& m = ctx->m;
   unsigned char* B = b.sbuf;
   uint32_t* h1 = (uint32_t*)(B + P.o_h1);
@@ -613,39 +627,92 @@ static int srt_launch(pluss_ctx* ctx, FaithfulBufs& b, const SrtPlan& P, PT* X1,
   uint32_t* cmap = (uint32_t*)(B + P.o_cmap);
   uint32_t* tot = (uint32_t*)(B + P.o_tot);
   const SrtDeep dp{(SrtItem*)(B + P.o_deep), tot + 2, P.a.np * (uint32_t)SB, ctx->g.flags};
+  uint32_t* cap = (uint32_t*)(B + P.o_fast);
+  uint32_t* off1 = cap + P.a.np;
+  uint32_t* fill = off1 + P.a.np;
+  uint32_t* ovf = fill + P.a.np;
+  uint32_t* gate = ovf + 1;
+  uint32_t* glen = ovf + 2;
+  SrtL2 l2{P.wmax, (uint32_t)std::min<uint64_t>(2 * P.ntot, 0xFFFFFFFFull), ovf + 8, ovf + 3, ovf + 4, ovf + 5};
   PLUSS_HIP_CHECK(hipMemsetAsync(tot, 0, 16, s));
   const unsigned g1 = (unsigned)P.a.coff[6];
   const bool p2 = m.p2 && (1u << P.a.tsh) == m.T;  // shift decodes of c0
+  const bool fast = P.fast1 && std::is_same<PT, uint32_t>::value;
+  if (fast) {
+    // level 1 without a count: buckets over-allocated in X1 (the whole 8 B x
+    // total scratch, 2 payloads per sample); then the counted level 1, gated
+    // on an overflow (its scan over none of hist1 when the gate is shut)
+    hipLaunchKernelGGL(k_srt_caps, dim3(1), dim3(SB), 0, s, P.a, P.wmax, (uint32_t)std::min<uint64_t>(2 * P.ntot,
+                       0xFFFFFFFFull), cap, off1, fill, ovf);
+    if (p2)
+      hipLaunchKernelGGL((k_srt_scatter1f<KT, SMP, true>), dim3(g1 * SPL), dim3(SB1), 0, s, m, P.a,
+                         (const uint32_t*)cap, (const uint32_t*)off1, fill, ovf, (uint32_t*)X1, ctx->g);
+    else
+      hipLaunchKernelGGL((k_srt_scatter1f<KT, SMP, false>), dim3(g1 * SPL), dim3(SB1), 0, s, m, P.a,
+                         (const uint32_t*)cap, (const uint32_t*)off1, fill, ovf, (uint32_t*)X1, ctx->g);
+    hipLaunchKernelGGL(k_srt_gate, dim3(1), dim3(1), 0, s, (const uint32_t*)ovf, (uint32_t)P.h1, gate, glen);
+  }
+  const uint32_t* gt = fast ? gate : nullptr;
   if (p2)
-    hipLaunchKernelGGL((k_srt_count1<KT, SMP, true>), dim3(g1), dim3(SB), 0, s, m, P.a, h1, ctx->g);
+    hipLaunchKernelGGL((k_srt_count1<KT, SMP, true>), dim3(g1), dim3(SB), 0, s, m, P.a, h1, ctx->g, gt);
   else
-    hipLaunchKernelGGL((k_srt_count1<KT, SMP, false>), dim3(g1), dim3(SB), 0, s, m, P.a, h1, ctx->g);
-  srt_scan(h1, P.h1, nullptr, bs, s);
+    hipLaunchKernelGGL((k_srt_count1<KT, SMP, false>), dim3(g1), dim3(SB), 0, s, m, P.a, h1, ctx->g, gt);
+  srt_scan(h1, P.h1, fast ? glen : nullptr, bs, s);
   if (p2)
     hipLaunchKernelGGL((k_srt_scatter1<KT, PT, SMP, true>), dim3(g1), dim3(SB), 0, s, m, P.a, (const uint32_t*)h1, X1,
-                       ctx->g);
+                       ctx->g, gt);
   else
     hipLaunchKernelGGL((k_srt_scatter1<KT, PT, SMP, false>), dim3(g1), dim3(SB), 0, s, m, P.a, (const uint32_t*)h1,
-                       X1, ctx->g);
-  hipLaunchKernelGGL(k_srt_plan, dim3(1), dim3(SB), 0, s, P.a, (const uint32_t*)h1, par, cmap, tot);
+                       X1, ctx->g, gt);
+  if (!fast) l2.fill = nullptr;  // (the counted level 2, ungated)
+  hipLaunchKernelGGL(k_srt_plan, dim3(1), dim3(SB), 0, s, P.a, (const uint32_t*)h1, par, cmap, tot,
+                     fast ? (const uint32_t*)fill : nullptr, (const uint32_t*)off1, (const uint32_t*)ovf, l2);
+  if (fast) {  // level 2 without a count (unless level 1 overflowed), then the counted one gated on an overflow
+    hipLaunchKernelGGL(k_srt_scatter2f<PT>, dim3((unsigned)P.g2max * SPL), dim3(SB1), 0, s, P.a,
+                       (const SrtParent*)par, (const uint32_t*)cmap, (const uint32_t*)tot, (const PT*)X1, Y, l2);
+    hipLaunchKernelGGL(k_srt_gate2, dim3(1), dim3(1), 0, s, (const uint32_t*)l2.ovf, (const uint32_t*)(tot + 1),
+                       l2.gate, l2.glen);
+  }
+  const uint32_t* gt2 = fast ? (const uint32_t*)l2.gate : nullptr;
   hipLaunchKernelGGL(k_srt_count2<PT>, dim3((unsigned)P.g2max), dim3(SB), 0, s, P.a, (const SrtParent*)par,
-                     (const uint32_t*)cmap, (const uint32_t*)tot, (const PT*)X1, h2);
-  srt_scan(h2, P.h2max, tot + 1, bs, s);
+                     (const uint32_t*)cmap, (const uint32_t*)tot, (const PT*)X1, h2, gt2);
+  srt_scan(h2, P.h2max, fast ? (const uint32_t*)l2.glen : tot + 1, bs, s);
   hipLaunchKernelGGL(k_srt_scatter2<PT>, dim3((unsigned)P.g2max), dim3(SB), 0, s, P.a, (const SrtParent*)par,
-                     (const uint32_t*)cmap, (const uint32_t*)tot, (const uint32_t*)h2, (const PT*)X1, Y);
-  hipLaunchKernelGGL((k_srt_final<PT, KT>), dim3(FG, P.a.np), dim3(SB), 0, s, P.a, (const SrtParent*)par,
-                     (const uint32_t*)h2, (const PT*)X1, (const PT*)Y, out, dp);
-  hipLaunchKernelGGL((k_srt_deep<PT, KT>), dim3(64), dim3(SB), 0, s, P.a, (const SrtParent*)par, X1, Y, out, dp);
+                     (const uint32_t*)cmap, (const uint32_t*)tot, (const uint32_t*)h2, (const PT*)X1, Y, gt2);
+  hipLaunchKernelGGL((k_srt_final<PT, OT, PFX>), dim3(FG, P.a.np), dim3(SB), 0, s, P.a, (const SrtParent*)par,
+                     (const uint32_t*)h2, (const PT*)X1, (const PT*)Y, out, dp, l2);
+  hipLaunchKernelGGL((k_srt_deep<PT, OT, PFX>), dim3(64), dim3(SB), 0, s, P.a, (const SrtParent*)par, X1, Y, out, dp);
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }
 
 // The sort of one or more references (cnt[r] = 0: none).  x1 (and y, for
 // 8-byte payloads) hold 8 B x total each; neither may alias in[] or out.
+// pay: when the payloads are 4 bytes and the words longer, out receives the
+// payloads alone (uint32_t) and *pay_out the parents' table for SRC_W32P
+// (false: out holds KT words).
+struct SrtPay {
+  bool on;
+  const SrtParent* par;
+  uint32_t pb[6], pn[6], hi[6];
+  uint64_t eoff[6];
+};
 template <typename KT, bool SMP>
 static int srt_sort(pluss_ctx* ctx, FaithfulBufs& b, const void* const in[6], const uint64_t cnt[6],
-                    unsigned long long* x1, unsigned long long* y, KT* out, hipStream_t s) {
+                    unsigned long long* x1, unsigned long long* y, KT* out, hipStream_t s, SrtPay* pay = nullptr) {
   const SrtPlan P = srt_plan(ctx->m, in, cnt);
+  if (pay) {
+    pay->on = P.p32 && sizeof(KT) > 4;
+    pay->par = (const SrtParent*)(b.sbuf + P.o_par);
+    uint32_t pb = 0;
+    for (int r = 0; r < 6; ++r) {
+      pay->pb[r] = pb;
+      pay->pn[r] = 1u << P.a.d1[r];
+      pay->hi[r] = P.a.wb - P.a.d1[r];
+      pay->eoff[r] = P.a.eoff[r];
+      pb += 1u << P.a.d1[r];
+    }
+  }
   if (P.ntot == 0) return PLUSS_OK;
   if (P.ntot > 0xFFFFFFFFull) {
     set_error("faithful mode: the radix source sorts at most 2^32-1 samples per call");
@@ -654,7 +721,10 @@ static int srt_sort(pluss_ctx* ctx, FaithfulBufs& b, const void* const in[6], co
   if (int rc = srt_reserve(b, P.bytes, s)) return rc;
   if (P.p32) {
     uint32_t* X1 = reinterpret_cast<uint32_t*>(x1);
-    return srt_launch<KT, uint32_t, SMP>(ctx, b, P, X1, X1 + P.ntot, out, s);
+    // (the count-free level 1 spreads X1 over all of x1: Y then lives in y)
+    uint32_t* Y = P.fast1 ? reinterpret_cast<uint32_t*>(y) : X1 + P.ntot;
+    if (pay && pay->on) return srt_launch<KT, uint32_t, SMP, uint32_t>(ctx, b, P, X1, Y, (uint32_t*)(void*)out, s);
+    return srt_launch<KT, uint32_t, SMP>(ctx, b, P, X1, Y, out, s);
   }
   return srt_launch<KT, unsigned long long, SMP>(ctx, b, P, x1, y, out, s);
 }
@@ -829,6 +899,7 @@ static int fa_launch(pluss_ctx* ctx, const FaLaunch& L, int src, int phase) {
   switch (src) {
     case SRC_W32: fa_launch_w32(l); break;
     case SRC_W64: fa_launch_w64(l); break;
+    case SRC_W32P: fa_launch_w32p(l); break;
     case SRC_SAMPLES: fa_launch_smp(l); break;
     case SRC_UNI: fa_launch_uni(l); break;
     default: fa_launch_gen(l); break;
@@ -947,7 +1018,20 @@ int launch_faithful_refs(pluss_ctx* ctx, const uint64_t* d_samples, const uint64
     if (int rc = srt_sort<uint32_t, true>(ctx, b, in, counts, b.keys, b.sinks, (uint32_t*)b.keys_s, s)) return rc;
     for (int r = 0; r < 6; ++r) a.src[r] = (const uint32_t*)b.keys_s + off[r];
   } else {
-    if (int rc = srt_sort<unsigned long long, true>(ctx, b, in, counts, b.keys, b.sinks, b.keys_s, s)) return rc;
+    SrtPay pay{};
+    if (int rc = srt_sort<unsigned long long, true>(ctx, b, in, counts, b.keys, b.sinks, b.keys_s, s, &pay)) return rc;
+    if (pay.on) {  // 4-byte payloads read back with their parents' digits (SRC_W32P)
+      for (int r = 0; r < 6; ++r) {
+        a.src[r] = (const uint32_t*)b.keys_s + off[r];
+        a.ppb[r] = pay.pb[r];
+        a.ppn[r] = pay.pn[r];
+        a.phi[r] = pay.hi[r];
+        a.peoff[r] = pay.eoff[r];
+      }
+      a.ppar = pay.par;
+      for (int r = 0; r < 6; ++r) a.n[r] = counts[r];
+      return fa_run(ctx, a, SRC_W32P, false, s);
+    }
     for (int r = 0; r < 6; ++r) a.src[r] = b.keys_s + off[r];
   }
   for (int r = 0; r < 6; ++r) a.n[r] = counts[r];
@@ -1399,13 +1483,27 @@ int faith_shards_local_words(pluss_ctx* ctx, const void* const in[6], const uint
     a.src[r] = fm == FM_PK32 ? (const void*)((const uint32_t*)b.keys_s + soff) : (const void*)(b.keys_s + soff);
     soff += cnt[r];
   }
+  SrtPay pay{};
   if (fm == FM_PK32) {
     if (int rc = srt_sort<uint32_t, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, (uint32_t*)b.keys_s, s)) return rc;
-  } else if (int rc = srt_sort<unsigned long long, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, b.keys_s, s)) {
+  } else if (int rc = srt_sort<unsigned long long, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, b.keys_s, s, &pay)) {
     return rc;
   }
   ctx->tables_dirty = true;
   f.src = fm == FM_PK32 ? SRC_W32 : SRC_W64;
+  if (pay.on) {  // 4-byte payloads read back with their parents' digits
+    f.src = SRC_W32P;
+    soff = 0;
+    for (int r = 0; r < 6; ++r) {
+      a.src[r] = (const uint32_t*)b.keys_s + soff;
+      soff += cnt[r];
+      a.ppb[r] = pay.pb[r];
+      a.ppn[r] = pay.pn[r];
+      a.phi[r] = pay.hi[r];
+      a.peoff[r] = pay.eoff[r];
+    }
+    a.ppar = pay.par;
+  }
   if (int rc = fa_prepare(ctx, a, f.src, false, true, s, &f.L)) return rc;
   return shards_phase1(ctx, f, d_row, s);
 }

@@ -63,12 +63,7 @@ struct SrtRefs {
   uint32_t tsh;       // log2(T) (P2 decodes)
 };
 
-// a top-level bucket: range [start, start + count) of the concatenated arrays;
-// split past SCAP into 2^d2 children through nc2 level-2 chunks
-struct SrtParent {
-  uint32_t start, count, ref, b1;
-  uint32_t d2, nc2, cbase, h2off;
-};
+// (SrtParent, a top-level bucket, is in pluss_device.h: the scan pipeline reads it too)
 
 // an item past SCAP for k_srt_deep: payloads [start, start + count) of X1
 // (buf 0) or Y (buf 1) of parent p, equal on every bit >= hi
@@ -312,8 +307,10 @@ __device__ __forceinline__ void srt_batch(const T (&w)[SE], uint32_t vmask, uint
 
 // ---- level 1 ---------------------------------------------------------------
 template <typename KT, bool SMP, bool P2>
-__global__ __launch_bounds__(SB) void k_srt_count1(Model m, SrtRefs a, uint32_t* __restrict__ hist, GTable g) {
+__global__ __launch_bounds__(SB) void k_srt_count1(Model m, SrtRefs a, uint32_t* __restrict__ hist, GTable g,
+                                                  const uint32_t* gate) {
   __shared__ uint32_t cnt[SB];
+  if (gate && !*gate) return;  // (the count-free level 1 placed every payload)
   cnt[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t r = srt_ref_of_chunk(a, blockIdx.x);
@@ -336,9 +333,10 @@ __global__ __launch_bounds__(SB) void k_srt_count1(Model m, SrtRefs a, uint32_t*
 
 template <typename KT, typename PT, bool SMP, bool P2>
 __global__ __launch_bounds__(SB) void k_srt_scatter1(Model m, SrtRefs a, const uint32_t* __restrict__ hist,
-                                                    PT* __restrict__ X1, GTable g) {
+                                                    PT* __restrict__ X1, GTable g, const uint32_t* gate) {
   __shared__ KT stage[SBATCH];
   __shared__ uint32_t bcnt[SB], bst[SB], cur[SB], wsum[SB / 64];
+  if (gate && !*gate) return;
   const uint32_t r = srt_ref_of_chunk(a, blockIdx.x);
   const SrtOne o = srt_one(a, r);
   const uint64_t c = blockIdx.x - o.c0;
@@ -360,13 +358,315 @@ __global__ __launch_bounds__(SB) void k_srt_scatter1(Model m, SrtRefs a, const u
 #undef PLUSS_SRT_SCATTER1
 }
 
+// ---- level 1 without a count pass (uniform-like input; 4-byte payloads):
+// each top-level bucket gets a region of X1 sized for its share of the word
+// range plus a margin (k_srt_caps), and each chunk of SC1 = 16K samples
+// reserves its runs there with one atomic per bucket (k_srt_scatter1f).  A
+// run that does not fit raises *ovf and is not written; the counted kernels
+// above then run after all (gated on *ovf) and redo level 1 exactly.
+constexpr int SB1 = 512;                       // threads of k_srt_scatter1f (41 KB of LDS: 3 per CU)
+constexpr uint32_t SC1 = SB1 * SE;             // samples per workgroup
+constexpr uint32_t SPL = SC / SC1;             // workgroups per counted chunk (chunks never span references)
+static_assert(SC % SC1 == 0, "the count-free scatter splits the counted path's chunks");
+
+// capacity of bucket b of reference r: its share of the words [0, wmax) plus margin
+__device__ __forceinline__ uint32_t srt_cap(const SrtRefs& a, uint32_t r, uint32_t b, uint64_t wmax) {
+  const uint64_t n = a.n[r];
+  if (a.d1[r] == 0) return (uint32_t)n;
+  const uint32_t lo = a.wb - a.d1[r];
+  const uint64_t b0 = (uint64_t)b << lo, b1 = (uint64_t)(b + 1) << lo;
+  const uint64_t w = b0 >= wmax ? 0 : (b1 < wmax ? b1 : wmax) - b0;
+  const double e = (double)n * ((double)w / (double)wmax);
+  const double c = e * 1.125 + 8.0 * sqrt(e) + 256.0;
+  return c >= (double)n ? (uint32_t)n : (uint32_t)c;
+}
+
+// one workgroup: every bucket's capacity and region start (off1), fills zeroed;
+// a plan larger than X1 (x1cap payloads) raises *ovf at once
+__global__ __launch_bounds__(SB) void k_srt_caps(SrtRefs a, uint64_t wmax, uint32_t x1cap, uint32_t* __restrict__ cap,
+                                                uint32_t* __restrict__ off1, uint32_t* __restrict__ fill,
+                                                uint32_t* __restrict__ ovf) {
+  __shared__ uint32_t v[SBATCH], wsum[SB / 64];
+  const uint32_t np = a.np;
+  for (uint32_t p = threadIdx.x; p < np; p += SB) {
+    uint32_t r = 0, base = 0;
+    while (r < 5 && p >= base + (1u << a.d1[r])) {
+      base += 1u << a.d1[r];
+      ++r;
+    }
+    v[p] = srt_cap(a, r, p - base, wmax);
+    cap[p] = v[p];
+    fill[p] = 0;
+  }
+  __syncthreads();
+  const uint32_t tot = srt_block_scan(v, np, wsum);
+  for (uint32_t p = threadIdx.x; p < np; p += SB) off1[p] = v[p];
+  if (threadIdx.x == 0) *ovf = tot > x1cap ? 1u : 0u;
+}
+
+// the gates of the counted level 1 (after the count-free one): gate = *ovf,
+// glen = the hist1 entries its scan covers (none when the gate is shut)
+__global__ void k_srt_gate(const uint32_t* __restrict__ ovf, uint32_t h1, uint32_t* __restrict__ gate,
+                           uint32_t* __restrict__ glen) {
+  const uint32_t o = *ovf ? 1u : 0u;
+  gate[0] = o;
+  glen[0] = o ? h1 : 0u;
+}
+
+// level 2's gates: gate = *ovf, glen = the hist2 entries in use (*h2used) or none
+__global__ void k_srt_gate2(const uint32_t* __restrict__ ovf, const uint32_t* __restrict__ h2used,
+                            uint32_t* __restrict__ gate, uint32_t* __restrict__ glen) {
+  const uint32_t o = *ovf ? 1u : 0u;
+  gate[0] = o;
+  glen[0] = o ? *h2used : 0u;
+}
+
+template <typename KT, bool SMP, bool P2>
+__global__ __launch_bounds__(SB1) void k_srt_scatter1f(Model m, SrtRefs a, const uint32_t* __restrict__ cap,
+                                                      const uint32_t* __restrict__ off1, uint32_t* __restrict__ fill,
+                                                      uint32_t* __restrict__ ovf, uint32_t* __restrict__ X1, GTable g) {
+  __shared__ uint32_t stage[SC1];
+  __shared__ uint8_t sdig[SC1];
+  __shared__ uint32_t bcnt[SB], bst[SB], bbase[SB], wsum[SB / 64];
+  if (*ovf) return;  // (the plan did not fit: the counted path runs)
+  const uint32_t r = srt_ref_of_chunk(a, blockIdx.x / SPL);
+  const SrtOne o = srt_one(a, r);
+  const uint64_t c = blockIdx.x - o.c0 * SPL;
+  const uint64_t e0 = c * SC1;
+  if (e0 >= o.n) return;  // (the last counted chunk's unused part)
+  const uint64_t e1 = o.n - e0 < SC1 ? o.n : e0 + SC1;
+  const uint32_t lo = a.wb - o.d1, mask = (1u << o.d1) - 1;
+  uint32_t pbase = 0;  // the first parent of reference r
+#pragma unroll
+  for (int x = 0; x < 5; ++x) pbase += (uint32_t)x < r ? (1u << a.d1[x]) : 0u;
+  if (threadIdx.x < SB) bcnt[threadIdx.x] = 0;
+  __syncthreads();
+  KT w[SE];
+  uint32_t rk[SE];
+#define PLUSS_SRT_LOAD1F(R)                                                                         \
+  {                                                                                                 \
+    const srt_raw_t<KT, SMP>* src = static_cast<const srt_raw_t<KT, SMP>*>(o.in);                   \
+    srt_raw_t<KT, SMP> x[SE];                                                                       \
+    _Pragma("unroll") for (int k = 0; k < SE; ++k) {                                                \
+      const uint64_t i = e0 + (uint64_t)k * SB1 + threadIdx.x;                                      \
+      x[k] = __builtin_nontemporal_load(src + (i < e1 ? i : e1 - 1));                               \
+    }                                                                                               \
+    _Pragma("unroll") for (int k = 0; k < SE; ++k) w[k] = srt_word<KT, SMP, P2, R>(m, a.tsh, x[k], g); \
+  }
+  PLUSS_SRT_REFS(PLUSS_SRT_LOAD1F)
+#undef PLUSS_SRT_LOAD1F
+#pragma unroll
+  for (int k = 0; k < SE; ++k) {
+    const uint64_t i = e0 + (uint64_t)k * SB1 + threadIdx.x;
+    rk[k] = i < e1 ? atomicAdd(&bcnt[srt_dig(w[k], lo, mask)], 1u) : 0u;
+  }
+  __syncthreads();
+  if (threadIdx.x < SB) {  // this chunk's run in each bucket's region
+    const uint32_t d = threadIdx.x, n = bcnt[d];
+    uint32_t at = 0;
+    if (d <= mask && n) {
+      const uint32_t p = pbase + d;
+      at = atomicAdd(&fill[p], n);
+      if (at + n > cap[p]) {
+        atomicOr(ovf, 1u);
+        at = 0xFFFFFFFFu;
+      } else {
+        at += off1[p];
+      }
+    }
+    bbase[d] = at;
+    bst[d] = n;
+  }
+  __syncthreads();
+  {
+    // a block scan of SB entries by the first SB threads (waves 0..3, 64 each)
+    const uint32_t t = threadIdx.x, lane = __lane_id(), wid = t >> 6;
+    uint32_t v = t < SB ? bst[t] : 0u, inc = v;
+#pragma unroll
+    for (int s2 = 1; s2 < 64; s2 <<= 1) {
+      const uint32_t y = __shfl_up(inc, s2, 64);
+      if (lane >= (uint32_t)s2) inc += y;
+    }
+    if (t < SB && lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+#pragma unroll
+    for (int x = 0; x < SB / 64; ++x) pre += x < (int)wid ? wsum[x] : 0u;
+    if (t < SB) bst[t] = pre + inc - v;
+  }
+  __syncthreads();
+  const uint32_t pmask = lo >= 32 ? 0xFFFFFFFFu : (1u << lo) - 1u;
+#pragma unroll
+  for (int k = 0; k < SE; ++k) {
+    const uint64_t i = e0 + (uint64_t)k * SB1 + threadIdx.x;
+    if (i < e1) {
+      const uint32_t d = srt_dig(w[k], lo, mask), q = bst[d] + rk[k];
+      stage[q] = (uint32_t)w[k] & pmask;
+      sdig[q] = (uint8_t)d;
+    }
+  }
+  __syncthreads();
+  const uint32_t mt = (uint32_t)(e1 - e0);
+  for (uint32_t i = threadIdx.x; i < mt; i += SB1) {
+    const uint32_t d = sdig[i], at = bbase[d];
+    if (at != 0xFFFFFFFFu) X1[at + (i - bst[d])] = stage[i];
+  }
+}
+
+// ---- level 2 without a count pass (after a count-free level 1): each split
+// parent's children get regions of Y sized like the level-1 buckets (capped
+// at SCAP, so no child goes deep), each level-2 chunk reserves its runs with
+// one atomic per child (k_srt_scatter2f), and k_srt_final takes the children
+// from their regions, their places in the output from the fills.  A run that
+// does not fit raises *ovf; the counted level 2 then runs (gated) and the
+// final pass reads its layout instead.
+struct SrtL2 {
+  uint64_t wmax;     // the words' range [0, wmax)
+  uint32_t ycap;     // Y's payloads
+  uint32_t* fill;    // per child (parent's cb2 + digit): payloads placed
+  uint32_t* ovf;     // a child's run did not fit, or the regions do not fit Y
+  uint32_t* gate;    // = *ovf, for the counted level 2 (k_srt_gate)
+  uint32_t* glen;    // the hist2 entries its scan covers (none when the gate is shut)
+};
+// a bound on the capacities of nc children sharing count payloads (whatever the
+// shares: sum sqrt(e_d) <= sqrt(nc * count)), so a parent's region is O(1) to size
+__device__ __forceinline__ uint32_t srt_cap2_sum(uint32_t count, uint32_t nc) {
+  const double b = (double)count * 1.125 + 8.0 * sqrt((double)count * (double)nc) + 65.0 * (double)nc;
+  return (uint32_t)b + 1u;
+}
+// capacity of child d of split parent P: its share of the parent's word range
+__device__ __forceinline__ uint32_t srt_cap2(const SrtRefs& a, const SrtParent& P, uint32_t d, uint64_t wmax) {
+  const uint32_t lo1 = a.wb - a.d1[P.ref], lo2 = lo1 - P.d2;
+  const uint64_t p0 = lo1 >= 64 ? 0 : (uint64_t)P.b1 << lo1;
+  const uint64_t p1 = lo1 >= 64 ? wmax : p0 + ((uint64_t)1 << lo1);
+  const uint64_t c0 = p0 + ((uint64_t)d << lo2), c1 = c0 + ((uint64_t)1 << lo2);
+  const uint64_t pw = (p1 < wmax ? p1 : wmax) - p0;
+  const uint64_t cw = c0 >= wmax ? 0 : (c1 < wmax ? c1 : wmax) - c0;
+  const double e = (double)P.count * ((double)cw / (double)pw);
+  const double c = e * 1.125 + 8.0 * sqrt(e) + 64.0;
+  return c >= (double)SCAP ? SCAP : (uint32_t)c;
+}
+
+template <typename PT>
+__global__ __launch_bounds__(SB1) void k_srt_scatter2f(const SrtRefs a, const SrtParent* __restrict__ par,
+                                                      const uint32_t* __restrict__ cmap,
+                                                      const uint32_t* __restrict__ tot, const PT* __restrict__ X1,
+                                                      PT* __restrict__ Y, const SrtL2 l2) {
+  __shared__ PT stage[SC1];
+  __shared__ uint8_t sdig[SC1];
+  __shared__ uint32_t bcnt[SB], bst[SB], bbase[SB], ccap[SB], coff[SB], wsum[SB / 64];
+  const uint32_t q2 = blockIdx.x / SPL, half = blockIdx.x - q2 * SPL;
+  if (q2 >= tot[0] || *l2.ovf) return;  // (a level 1 or region overflow: the counted level 2 runs)
+  const SrtParent P = par[cmap[q2]];
+  const uint32_t k = q2 - P.cbase;
+  const uint32_t c0 = k * SC + half * SC1;  // this workgroup's part of the parent's k-th chunk
+  if (c0 >= P.count) return;
+  const uint32_t e0 = P.src + c0, e1 = P.count - c0 < SC1 ? P.src + P.count : e0 + SC1;
+  const uint32_t lo = a.wb - a.d1[P.ref] - P.d2, mask = (1u << P.d2) - 1;
+  if (threadIdx.x < SB) bcnt[threadIdx.x] = 0;
+  if (threadIdx.x < SB) {  // the children's capacities; their region offsets below
+    ccap[threadIdx.x] = threadIdx.x <= mask ? srt_cap2(a, P, threadIdx.x, l2.wmax) : 0u;
+    coff[threadIdx.x] = ccap[threadIdx.x];
+  }
+  __syncthreads();
+  {
+    const uint32_t t = threadIdx.x, lane = __lane_id(), wid = t >> 6;
+    const uint32_t v = t < SB ? coff[t] : 0u;
+    uint32_t inc = v;
+#pragma unroll
+    for (int s2 = 1; s2 < 64; s2 <<= 1) {
+      const uint32_t y = __shfl_up(inc, s2, 64);
+      if (lane >= (uint32_t)s2) inc += y;
+    }
+    if (t < SB && lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+#pragma unroll
+    for (int x = 0; x < SB / 64; ++x) pre += x < (int)wid ? wsum[x] : 0u;
+    if (t < SB) coff[t] = pre + inc - v;
+  }
+  PT w[SE];
+  uint32_t rk[SE];
+#pragma unroll
+  for (int j = 0; j < SE; ++j) {
+    const uint32_t i = e0 + (uint32_t)j * SB1 + threadIdx.x;
+    w[j] = __builtin_nontemporal_load(X1 + (i < e1 ? i : e1 - 1));
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < SE; ++j) {
+    const uint32_t i = e0 + (uint32_t)j * SB1 + threadIdx.x;
+    rk[j] = i < e1 ? atomicAdd(&bcnt[srt_dig(w[j], lo, mask)], 1u) : 0u;
+  }
+  __syncthreads();
+  if (threadIdx.x < SB) {  // this part's run in each child's region
+    const uint32_t d = threadIdx.x, n = bcnt[d];
+    uint32_t at = 0;
+    if (d <= mask && n) {
+      at = atomicAdd(&l2.fill[P.cb2 + d], n);
+      if (at + n > ccap[d]) {
+        atomicOr(l2.ovf, 1u);
+        at = 0xFFFFFFFFu;
+      } else {
+        at += P.ybase + coff[d];
+      }
+    }
+    bbase[d] = at;
+    bst[d] = n;
+  }
+  __syncthreads();
+  {
+    const uint32_t t = threadIdx.x, lane = __lane_id(), wid = t >> 6;
+    const uint32_t v = t < SB ? bst[t] : 0u;
+    uint32_t inc = v;
+#pragma unroll
+    for (int s2 = 1; s2 < 64; s2 <<= 1) {
+      const uint32_t y = __shfl_up(inc, s2, 64);
+      if (lane >= (uint32_t)s2) inc += y;
+    }
+    if (t < SB && lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+#pragma unroll
+    for (int x = 0; x < SB / 64; ++x) pre += x < (int)wid ? wsum[x] : 0u;
+    if (t < SB) bst[t] = pre + inc - v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < SE; ++j) {
+    const uint32_t i = e0 + (uint32_t)j * SB1 + threadIdx.x;
+    if (i < e1) {
+      const uint32_t d = srt_dig(w[j], lo, mask), q = bst[d] + rk[j];
+      stage[q] = w[j];
+      sdig[q] = (uint8_t)d;
+    }
+  }
+  __syncthreads();
+  const uint32_t mt = e1 - e0;
+  for (uint32_t i = threadIdx.x; i < mt; i += SB1) {
+    const uint32_t d = sdig[i], at = bbase[d];
+    if (at != 0xFFFFFFFFu) Y[at + (i - bst[d])] = stage[i];
+  }
+}
+
 // ---- the plan: parents, their splits and level-2 chunks (one workgroup).
 // tot[0] = level-2 chunks, tot[1] = hist2 entries.
+// fill (the count-free level 1, unless *ovf): every parent's count is its
+// fill, its payloads at off1 in X1, its place in the sorted order the
+// exclusive sum of the fills before it.
 __global__ __launch_bounds__(SB) void k_srt_plan(SrtRefs a, const uint32_t* __restrict__ hist,
                                                 SrtParent* __restrict__ par, uint32_t* __restrict__ cmap,
-                                                uint32_t* __restrict__ tot) {
+                                                uint32_t* __restrict__ tot, const uint32_t* __restrict__ fill,
+                                                const uint32_t* __restrict__ off1, const uint32_t* __restrict__ ovf,
+                                                const SrtL2 l2) {
   __shared__ uint32_t v1[SBATCH], v2[SBATCH], wsum[SB / 64];
   const uint32_t np = a.np;  // <= 6 * 256
+  const bool filled = fill && !*ovf;
+  if (filled) {  // the parents' starts: the fills' exclusive sum (references in order, eoff[0] = 0)
+    for (uint32_t p = threadIdx.x; p < np; p += SB) v1[p] = fill[p];
+    __syncthreads();
+    srt_block_scan(v1, np, wsum);
+  }
   // parent p -> (reference, digit): references in order, 2^d1 parents each
   auto locate = [&](uint32_t p, uint32_t& r, uint32_t& b1) {
     r = 0;
@@ -385,14 +685,46 @@ __global__ __launch_bounds__(SB) void k_srt_plan(SrtRefs a, const uint32_t* __re
   for (uint32_t p = threadIdx.x; p < np; p += SB) {
     uint32_t r, b1;
     locate(p, r, b1);
-    const uint32_t s = bstart(r, b1);
-    const uint32_t e = b1 + 1 < (1u << a.d1[r]) ? bstart(r, b1 + 1) : (uint32_t)a.eoff[r + 1];
-    const uint32_t cnt = e - s, hi = a.wb - a.d1[r];
+    uint32_t s, cnt, src;
+    if (filled) {
+      s = v1[p];
+      cnt = fill[p];
+      src = off1[p];
+    } else {
+      s = bstart(r, b1);
+      const uint32_t e = b1 + 1 < (1u << a.d1[r]) ? bstart(r, b1 + 1) : (uint32_t)a.eoff[r + 1];
+      cnt = e - s;
+      src = s;
+    }
+    const uint32_t hi = a.wb - a.d1[r];
     const uint32_t d2 = (cnt > SCAP && hi > 0) ? srt_split_bits(cnt, hi) : 0u;
     const uint32_t nc2 = d2 ? (cnt + SC - 1) / SC : 0u;
-    par[p] = SrtParent{s, cnt, r, b1, d2, nc2, 0, 0};
+    par[p] = SrtParent{s, cnt, r, b1, d2, nc2, 0, 0, src, 0, 0};
+  }
+  __syncthreads();  // (v1 free again)
+  if (filled && l2.fill) {  // the count-free level 2's regions: per parent a bound on its children's capacities
+    for (uint32_t p = threadIdx.x; p < np; p += SB) {
+      const SrtParent P = par[p];
+      v1[p] = P.d2 ? srt_cap2_sum(P.count, 1u << P.d2) : 0u;
+      v2[p] = P.d2 ? 1u << P.d2 : 0u;
+    }
+    __syncthreads();
+    const uint32_t ysum = srt_block_scan(v1, np, wsum);
+    const uint32_t nchild = srt_block_scan(v2, np, wsum);
+    for (uint32_t p = threadIdx.x; p < np; p += SB) {
+      par[p].ybase = v1[p];
+      par[p].cb2 = v2[p];
+    }
+    for (uint32_t i = threadIdx.x; i < nchild; i += SB) l2.fill[i] = 0;
+    if (threadIdx.x == 0) *l2.ovf = ysum > l2.ycap ? 1u : 0u;
+    __syncthreads();
+  } else if (l2.fill && threadIdx.x == 0) {
+    *l2.ovf = 1u;  // (level 1 took the counted path: so does level 2)
+  }
+  for (uint32_t p = threadIdx.x; p < np; p += SB) {
+    const uint32_t nc2 = par[p].nc2;
     v1[p] = nc2;
-    v2[p] = nc2 << d2;
+    v2[p] = nc2 << par[p].d2;
   }
   __syncthreads();
   const uint32_t g2 = srt_block_scan(v1, np, wsum);
@@ -413,12 +745,13 @@ __global__ __launch_bounds__(SB) void k_srt_plan(SrtRefs a, const uint32_t* __re
 template <typename PT>
 __global__ __launch_bounds__(SB) void k_srt_count2(const SrtRefs a, const SrtParent* __restrict__ par,
                                                   const uint32_t* __restrict__ cmap, const uint32_t* __restrict__ tot,
-                                                  const PT* __restrict__ X1, uint32_t* __restrict__ hist2) {
+                                                  const PT* __restrict__ X1, uint32_t* __restrict__ hist2,
+                                                  const uint32_t* gate) {
   __shared__ uint32_t cnt[SB];
-  if (blockIdx.x >= tot[0]) return;
+  if (blockIdx.x >= tot[0] || (gate && !*gate)) return;
   const SrtParent P = par[cmap[blockIdx.x]];
   const uint32_t k = blockIdx.x - P.cbase;
-  const uint32_t e0 = P.start + k * SC, e1 = P.count - k * SC < SC ? P.start + P.count : e0 + SC;
+  const uint32_t e0 = P.src + k * SC, e1 = P.count - k * SC < SC ? P.src + P.count : e0 + SC;
   const uint32_t lo = a.wb - a.d1[P.ref] - P.d2, mask = (1u << P.d2) - 1;
   cnt[threadIdx.x] = 0;
   __syncthreads();
@@ -442,13 +775,13 @@ template <typename PT>
 __global__ __launch_bounds__(SB) void k_srt_scatter2(const SrtRefs a, const SrtParent* __restrict__ par,
                                                     const uint32_t* __restrict__ cmap,
                                                     const uint32_t* __restrict__ tot, const uint32_t* __restrict__ hist2,
-                                                    const PT* __restrict__ X1, PT* __restrict__ Y) {
+                                                    const PT* __restrict__ X1, PT* __restrict__ Y, const uint32_t* gate) {
   __shared__ PT stage[SBATCH];
   __shared__ uint32_t bcnt[SB], bst[SB], cur[SB], wsum[SB / 64];
-  if (blockIdx.x >= tot[0]) return;
+  if (blockIdx.x >= tot[0] || (gate && !*gate)) return;
   const SrtParent P = par[cmap[blockIdx.x]];
   const uint32_t k = blockIdx.x - P.cbase;
-  const uint32_t e0 = P.start + k * SC, e1 = P.count - k * SC < SC ? P.start + P.count : e0 + SC;
+  const uint32_t e0 = P.src + k * SC, e1 = P.count - k * SC < SC ? P.src + P.count : e0 + SC;
   const uint32_t lo = a.wb - a.d1[P.ref] - P.d2, mask = (1u << P.d2) - 1;
   const uint32_t base = hist2[P.h2off];
   cur[threadIdx.x] = threadIdx.x <= mask ? P.start + hist2[P.h2off + threadIdx.x * P.nc2 + k] - base : 0u;
@@ -657,12 +990,13 @@ __device__ __forceinline__ void srt_item_sort(const PT (&w)[NSE], uint32_t s, ui
   for (int k = 0; k < NSE; ++k) {
     const uint32_t i = (uint32_t)k * SB + threadIdx.x;
     if (i < cnt) {
-      const uint32_t p = g0[k] + r[k];
-      uint32_t at = g0[k];
-      for (uint32_t j = g0[k]; j < g1[k]; ++j) {
-        const PT y = bb[j];
-        at += (y < w[k] || (y == w[k] && j < p)) ? 1u : 0u;
-      }
+      const uint32_t p = g0[k] + r[k], j0 = g0[k], e = g1[k];
+      auto below = [&](PT y, uint32_t j) -> uint32_t { return (j < e && (y < w[k] || (y == w[k] && j < p))) ? 1u : 0u; };
+      // the group's first four in straight-line reads (a group averages below
+      // two payloads; bb holds SCAP + 4 so they never leave it), the rest in a loop
+      uint32_t at = j0 + below(bb[j0], j0) + below(bb[j0 + 1], j0 + 1) + below(bb[j0 + 2], j0 + 2) +
+                    below(bb[j0 + 3], j0 + 3);
+      for (uint32_t j = j0 + 4; j < e; ++j) at += below(bb[j], j);
       ob[at] = w[k];
     }
   }
@@ -676,20 +1010,21 @@ __device__ __forceinline__ void srt_item_sort(const PT (&w)[NSE], uint32_t s, ui
 // x, each child's payloads loaded while the previous one is sorted.  Items
 // past SCAP go to the deep list.
 constexpr uint32_t FG = 4;
-template <typename PT, typename KT>
+template <typename PT, typename KT, bool PFX = true>  // !PFX: the payloads alone (SRC_W32P)
 __global__ __launch_bounds__(SB) void k_srt_final(const SrtRefs a, const SrtParent* __restrict__ par,
                                                  const uint32_t* __restrict__ hist2, const PT* __restrict__ X1,
-                                                 const PT* __restrict__ Y, KT* __restrict__ OUT, SrtDeep dp) {
+                                                 const PT* __restrict__ Y, KT* __restrict__ OUT, SrtDeep dp,
+                                                 const SrtL2 l2) {
   // ob, the ranked payloads, reuses the counters once each payload holds its
   // group bounds in registers (4-byte payloads; 8-byte ones get their own)
   constexpr bool OB_IN_C = sizeof(PT) == sizeof(uint32_t);
-  __shared__ PT bb[SCAP], obx[OB_IN_C ? 1 : SCAP];
-  __shared__ uint32_t c[SCAP + 1], bnd[SB + 1], wsum[SB / 64];
+  __shared__ PT bb[SCAP + 4], obx[OB_IN_C ? 1 : SCAP];  // (bb: srt_item_sort's reads past a group's end)
+  __shared__ uint32_t c[SCAP + 1], bnd[SB + 1], ysrc[SB], wsum[SB / 64];
   PT* ob = OB_IN_C ? reinterpret_cast<PT*>(c) : obx;
   const uint32_t p = blockIdx.y;
   const SrtParent P = par[p];
   const uint32_t hi1 = a.wb - a.d1[P.ref];
-  const KT prefix = srt_prefix<KT>(a, P);
+  const KT prefix = PFX ? srt_prefix<KT>(a, P) : (KT)0;
   auto deep = [&](uint32_t s, uint32_t cnt, uint32_t hi, uint32_t buf) {
     if (threadIdx.x == 0) {
       const unsigned int q = atomicAdd(dp.head, 1u);
@@ -699,18 +1034,19 @@ __global__ __launch_bounds__(SB) void k_srt_final(const SrtRefs a, const SrtPare
   };
   // an item of cnt <= SCAP payloads in NSE registers per thread, the fewest
   // that hold it (the slots past cnt are predicated off but still issued)
-  auto item = [&](const PT* __restrict__ src, uint32_t s, uint32_t cnt, uint32_t hi) {
+  // (payloads read from src[rs, rs + cnt), written as words to OUT[s, s + cnt))
+  auto item = [&](const PT* __restrict__ src, uint32_t rs, uint32_t s, uint32_t cnt, uint32_t hi) {
     if (cnt <= 8 * SB) {
       PT w[8];
-      srt_item_load<PT, 8>(src, s, cnt, w);
+      srt_item_load<PT, 8>(src, rs, cnt, w);
       srt_item_sort<PT, KT, 8>(w, s, cnt, hi, prefix, OUT, bb, ob, c, wsum);
     } else if (cnt <= 12 * SB) {
       PT w[12];
-      srt_item_load<PT, 12>(src, s, cnt, w);
+      srt_item_load<PT, 12>(src, rs, cnt, w);
       srt_item_sort<PT, KT, 12>(w, s, cnt, hi, prefix, OUT, bb, ob, c, wsum);
     } else {
       PT w[SE];
-      srt_item_load<PT, SE>(src, s, cnt, w);
+      srt_item_load<PT, SE>(src, rs, cnt, w);
       srt_item_sort<PT, KT, SE>(w, s, cnt, hi, prefix, OUT, bb, ob, c, wsum);
     }
   };
@@ -720,29 +1056,44 @@ __global__ __launch_bounds__(SB) void k_srt_final(const SrtRefs a, const SrtPare
       deep(P.start, P.count, hi1, 0);
       return;
     }
-    item(X1, P.start, P.count, hi1);
+    item(X1, P.src, P.start, P.count, hi1);
     return;
   }
   const uint32_t nc = 1u << P.d2, hi = hi1 - P.d2;
-  const uint32_t base = hist2[P.h2off];
-  for (uint32_t i = threadIdx.x; i <= nc; i += SB)
-    bnd[i] = i < nc ? P.start + hist2[P.h2off + i * P.nc2] - base : P.start + P.count;
+  const bool f2 = l2.fill && !*l2.ovf;  // the count-free level 2's layout
+  if (f2) {  // children in their Y regions (capacities scanned), output places from the fills
+    const uint32_t d = threadIdx.x;
+    ysrc[d] = d < nc ? srt_cap2(a, P, d, l2.wmax) : 0u;
+    bnd[d] = d < nc ? l2.fill[P.cb2 + d] : 0u;
+    __syncthreads();
+    srt_block_scan(ysrc, SB, wsum);
+    srt_block_scan(bnd, SB, wsum);
+    if (d < nc) {
+      ysrc[d] += P.ybase;
+      bnd[d] += P.start;
+    }
+    if (d == 0) bnd[nc] = P.start + P.count;
+  } else {
+    const uint32_t base = hist2[P.h2off];
+    for (uint32_t i = threadIdx.x; i <= nc; i += SB)
+      bnd[i] = i < nc ? P.start + hist2[P.h2off + i * P.nc2] - base : P.start + P.count;
+  }
   __syncthreads();
   for (uint32_t d = blockIdx.x; d < nc; d += FG) {  // this workgroup's children
     const uint32_t s = bnd[d], cnt = bnd[d + 1] - s;
     if (cnt == 0) continue;
-    if (cnt > SCAP) {
+    if (cnt > SCAP) {  // (the counted layout only: a region holds at most SCAP)
       deep(s, cnt, hi, 1);
       continue;
     }
-    item(Y, s, cnt, hi);
+    item(Y, f2 ? ysrc[d] : s, s, cnt, hi);
   }
 }
 
 // ---- k_srt_deep: items past SCAP (skewed or duplicated words), split by
 // 8-bit digits depth first inside one workgroup; a level's children alternate
 // between Y and X1 at the same offsets; every item ends in OUT as words.
-template <typename PT, typename KT>
+template <typename PT, typename KT, bool PFX = true>
 __global__ __launch_bounds__(SB) void k_srt_deep(const SrtRefs a, const SrtParent* __restrict__ par,
                                                 PT* __restrict__ X1, PT* __restrict__ Y, KT* __restrict__ OUT,
                                                 SrtDeep dp) {
@@ -755,7 +1106,7 @@ __global__ __launch_bounds__(SB) void k_srt_deep(const SrtRefs a, const SrtParen
   for (uint32_t q = blockIdx.x; q < nd; q += gridDim.x) {
     int top = 0;
     const SrtItem root = dp.items[q];
-    const KT prefix = srt_prefix<KT>(a, par[root.bufp >> 1]);
+    const KT prefix = PFX ? srt_prefix<KT>(a, par[root.bufp >> 1]) : (KT)0;
     if (threadIdx.x == 0) {
       lv[0] = root;
       nxt[0] = 0xFFFFFFFFu;  // not split yet

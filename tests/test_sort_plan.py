@@ -137,6 +137,84 @@ def test_one_reference_others_empty(model_host, N, T):
         plan_and_check(N, words)
 
 
+def srt_cap(n, d1, wb, b, wmax):
+    """k_srt_caps's capacity of bucket b (pluss_sort.h srt_cap)."""
+    if d1 == 0:
+        return n
+    lo = wb - d1
+    b0, b1 = b << lo, (b + 1) << lo
+    w = 0 if b0 >= wmax else min(b1, wmax) - b0
+    e = float(n) * (float(w) / float(wmax))
+    c = e * 1.125 + 8.0 * np.sqrt(e) + 256.0
+    return n if c >= n else int(c)
+
+
+@pytest.mark.parametrize("N,T,n", [(4096, 8, 3_000_000), (1024, 8, 700_000), (1056, 8, 400_000), (2048, 64, 500_000),
+                                   (4096, 8, 2049), (4096, 8, 40_000)])
+def test_count_free_level1_capacities(model_host, N, T, n):
+    """The count-free level 1 (k_srt_scatter1f): every bucket of a uniform
+    (Feistel) list fits its capacity, so the counted fallback does not run,
+    and the regions fit X1 (2 payloads per sample)."""
+    wb = pk_bits(N)
+    wmax = 4 * N ** 3
+    for ref in ("C3", "A0", "C0"):
+        w = feistel_words(model_host, N, T, ref, n)
+        d = d1_of(n, wb)
+        if wb <= 32 + SDIG and wb > 32 and d < wb - 32:
+            d = wb - 32
+        caps = [srt_cap(n, d, wb, b, wmax) for b in range(1 << d)]
+        if sum(caps) > 2 * n:  # k_srt_caps raises the overflow at once: the counted level 1 runs
+            assert n < 40_000
+            continue
+        top = (w >> np.uint64(wb - d)).astype(np.int64) if d else np.zeros(n, np.int64)
+        counts = np.bincount(top, minlength=1 << d)
+        assert (counts <= np.array(caps)).all(), (ref, int((counts - np.array(caps)).max()))
+
+
+def srt_cap2(wb, d1, b1, d2, count, d, wmax):
+    """k_srt_scatter2f's capacity of child d of a split parent (pluss_sort.h srt_cap2)."""
+    lo1 = wb - d1
+    lo2 = lo1 - d2
+    p0 = b1 << lo1
+    p1 = p0 + (1 << lo1)
+    c0 = p0 + (d << lo2)
+    c1 = c0 + (1 << lo2)
+    pw = min(p1, wmax) - p0
+    cw = 0 if c0 >= wmax else min(c1, wmax) - c0
+    e = float(count) * (float(cw) / float(pw))
+    c = e * 1.125 + 8.0 * np.sqrt(e) + 64.0
+    return SCAP if c >= SCAP else int(c)
+
+
+@pytest.mark.parametrize("N,T,n", [(4096, 8, 3_000_000), (1024, 8, 900_000), (2048, 64, 1_500_000)])
+def test_count_free_level2_capacities(model_host, N, T, n):
+    """The count-free level 2 (k_srt_scatter2f): every child of a uniform
+    list's split parents fits its region (at most SCAP), so neither the
+    counted level 2 nor the deep pass runs."""
+    wb = pk_bits(N)
+    wmax = 4 * N ** 3
+    for ref in ("C3", "C0"):
+        w = feistel_words(model_host, N, T, ref, n)
+        d1 = d1_of(n, wb)
+        if wb <= 32 + SDIG and wb > 32 and d1 < wb - 32:
+            d1 = wb - 32
+        lo1 = wb - d1
+        top = (w >> np.uint64(lo1)).astype(np.int64)
+        nsplit = 0
+        for b1 in range(1 << d1):
+            mine = w[top == b1]
+            c = len(mine)
+            if c <= SCAP:
+                continue
+            d2 = split_bits(c, lo1)
+            nsplit += 1
+            dig = ((mine >> np.uint64(lo1 - d2)).astype(np.int64)) & ((1 << d2) - 1)
+            sizes = np.bincount(dig, minlength=1 << d2)
+            caps = np.array([srt_cap2(wb, d1, b1, d2, c, d, wmax) for d in range(1 << d2)])
+            assert (caps <= SCAP).all() and (sizes <= caps).all(), (ref, b1, int((sizes - caps).max()))
+        assert nsplit > 0 or n <= 256 * SCAP
+
+
 def test_six_references_and_skew(model_host):
     words = [feistel_words(model_host, 4096, 8, r, n) if n else np.zeros(0, np.uint64) for r, n in
              (("C0", 30_000), ("C1", 0), ("A0", 300_000), ("B0", 5), ("C2", 4096), ("C3", 70_000))]
