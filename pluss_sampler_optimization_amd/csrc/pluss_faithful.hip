@@ -701,9 +701,9 @@ template <typename KT, bool SMP>
 static int srt_sort(pluss_ctx* ctx, FaithfulBufs& b, const void* const in[6], const uint64_t cnt[6],
                     unsigned long long* x1, unsigned long long* y, KT* out, hipStream_t s, SrtPay* pay = nullptr) {
   const SrtPlan P = srt_plan(ctx->m, in, cnt);
-  if (pay) {
+  if (pay) {  // (the parents' address once srt_reserve below has grown the scratch)
     pay->on = P.p32 && sizeof(KT) > 4;
-    pay->par = (const SrtParent*)(b.sbuf + P.o_par);
+    pay->par = nullptr;
     uint32_t pb = 0;
     for (int r = 0; r < 6; ++r) {
       pay->pb[r] = pb;
@@ -719,6 +719,7 @@ static int srt_sort(pluss_ctx* ctx, FaithfulBufs& b, const void* const in[6], co
     return PLUSS_ERR_CONFIG;
   }
   if (int rc = srt_reserve(b, P.bytes, s)) return rc;
+  if (pay) pay->par = (const SrtParent*)(b.sbuf + P.o_par);
   if (P.p32) {
     uint32_t* X1 = reinterpret_cast<uint32_t*>(x1);
     // (the count-free level 1 spreads X1 over all of x1: Y then lives in y)
