@@ -374,9 +374,19 @@ struct W32P {
   uint64_t B;
   bool ok;
 };
+// (every wave by itself: its lanes read the parents' starts at once and count
+// those at or below the tile's first and last elements; starts never decrease)
 __device__ __forceinline__ W32P w32p_tile(const FaOne& o, uint64_t base, uint32_t mt) {
   W32P w;
-  const uint32_t b0 = w32p_find(o, base), b1 = w32p_find(o, base + (mt ? mt - 1 : 0));
+  const uint64_t lastx = base + (mt ? mt - 1 : 0);
+  uint32_t n0 = 0, n1 = 0;
+  for (uint32_t j0 = 0; j0 < o.pn; j0 += 64) {
+    const uint32_t j = j0 + __lane_id();
+    const uint64_t st = j < o.pn ? (uint64_t)o.ppar[j].start - o.peoff : ~0ull;
+    n0 += (uint32_t)__popcll(__ballot(st <= base));
+    n1 += (uint32_t)__popcll(__ballot(st <= lastx));
+  }
+  const uint32_t b0 = n0 ? n0 - 1 : 0, b1 = n1 ? n1 - 1 : 0;
   w.pa = (unsigned long long)b0 << o.phi;
   w.pb = (unsigned long long)b1 << o.phi;
   w.B = b1 > b0 ? (uint64_t)o.ppar[b1].start - o.peoff : ~0ull;
@@ -890,6 +900,24 @@ __device__ __forceinline__ FaDec fa_dec_word(const Model& m, const PkView& v, KT
   return d;
 }
 
+// a 4-byte payload of a longer word (SRC_W32P) whose parent's digit lies in the
+// word's q*N + c1 field: pq = the digit shifted into that field (tile-uniform,
+// one of two), so the decode stays in 32 bits like fa_dec_word's
+template <uint32_t REF>
+__device__ __forceinline__ FaDec fa_dec_w32p(const Model& m, const PkView& v, uint32_t w, uint32_t pq) {
+  const uint32_t c = w & 3u;
+  const uint32_t t = (w >> 2) & (uint32_t)(v.T - 1);
+  const uint32_t c2 = (w >> (2 + v.tsh)) & (uint32_t)(v.N - 1);
+  const uint32_t qc = pq | (w >> (2 + v.tsh + v.nsh));
+  FaDec d;
+  d.ord = 0;
+  d.lk = ((__umul24(qc, m.S) + ref_off(REF, c2)) << v.tsh) | t;
+  d.a = c == 0;
+  d.b = c == 1;
+  d.t0 = t == 0;
+  return d;
+}
+
 // inclusive 32-bit wave scan (identity 0), Hillis-Steele by DPP: row_shr
 // 1/2/4/8 inside rows of 16 lanes, then row_bcast 15 and 31 across rows
 template <bool MAX>
@@ -1143,10 +1171,14 @@ __device__ __forceinline__ bool fa_lane_tile(const Model& m, const FaRefs& a, co
   fa_mem_t<SRC> v[ST];  // (SRC_W32P: the payloads; each word is made where it is decoded)
   W32P pw{};
   uint32_t be = 0xFFFFFFFFu;  // SRC_W32P: tile elements below be are in the first parent
+  uint32_t qa = 0, qb = 0;    // ... and their parents' digits in the q*N + c1 field
   if constexpr (SRC == SRC_W32P) {
     pw = w32p_tile(o, T.base, T.mt);
     if (!pw.ok) return false;  // (more than two parents in the tile: the queued pass)
     be = pw.B - T.base > (uint64_t)TILE ? 0xFFFFFFFFu : (uint32_t)(pw.B - T.base);
+    const uint32_t qs = 2 + o.pv.tsh + o.pv.nsh;  // (the host's condition: o.phi >= qs)
+    qa = (uint32_t)(pw.pa >> qs);
+    qb = (uint32_t)(pw.pb >> qs);
   }
 #pragma unroll
   for (int k = 0; k < ST; ++k) {
@@ -1195,7 +1227,7 @@ __device__ __forceinline__ bool fa_lane_tile(const Model& m, const FaRefs& a, co
     FaDec d;
     if constexpr (SRC == SRC_UNI) d = fa_dec_staged(v[k]);
     else if constexpr (fa_smp<SRC>()) d = fa_dec_sample<REF>(m, o.pv, (uint64_t)v[k], oddk);
-    else if constexpr (SRC == SRC_W32P) d = fa_dec_word<REF>(m, o.pv, (e0 + 64u * k < be ? pw.pa : pw.pb) | v[k]);
+    else if constexpr (SRC == SRC_W32P) d = fa_dec_w32p<REF>(m, o.pv, v[k], e0 + 64u * k < be ? qa : qb);
     else d = fa_dec_word<REF>(m, o.pv, v[k]);
     odd |= val ? oddk : 0u;
     if (CHECK) {  // against the previous lane (the step before: its lane 63); integer

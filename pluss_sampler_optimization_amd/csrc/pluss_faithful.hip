@@ -705,12 +705,15 @@ static int srt_sort(pluss_ctx* ctx, FaithfulBufs& b, const void* const in[6], co
     pay->on = P.p32 && sizeof(KT) > 4;
     pay->par = nullptr;
     uint32_t pb = 0;
+    const PkView v0 = make_pkview(ctx->m, 0);
     for (int r = 0; r < 6; ++r) {
       pay->pb[r] = pb;
       pay->pn[r] = 1u << P.a.d1[r];
       pay->hi[r] = P.a.wb - P.a.d1[r];
       pay->eoff[r] = P.a.eoff[r];
       pb += 1u << P.a.d1[r];
+      // the lane-major decode puts the digit into the q*N + c1 field (fa_dec_w32p)
+      if (cnt[r] && pay->hi[r] < 2 + v0.tsh + v0.nsh) pay->on = false;
     }
   }
   if (P.ntot == 0) return PLUSS_OK;
