@@ -236,6 +236,7 @@ struct pluss_group {
   std::vector<pluss::PartBufs> part;      // per device: the any-order faithful pass
   std::map<uint32_t, hipGraphExec_t> graphs;  // dense passes captured per batch size (one local device)
   pluss::FaGraph* fg = nullptr;               // the last faithful pass, captured (pluss_group_gen_faithful)
+  bool capturing = false;                     // a pass being captured into fg (one rank: no RCCL calls in it)
 };
 
 namespace pluss {
@@ -340,6 +341,10 @@ static int fork_shards(pluss_group* G) {
 // (each device holds every shard's slot; its own shards' slots are written)
 static int gather_blocks(pluss_group* G, std::vector<unsigned long long*>& buf, size_t w) {
   if (int rc = join_shards(G)) return rc;
+  // one rank: every shard wrote its block of the one buffer, the all-gather is
+  // the identity -- left out of a captured pass (RCCL calls inside a HIP graph
+  // capture were the one place a run crashed on the host, intermittently)
+  if (G->nranks == 1 && G->capturing) return fork_shards(G);
   PLUSS_NCCL_CHECK(g_rccl.GroupStart());
   for (int d = 0; d < G->ndev; ++d) {
     unsigned long long* own = buf[d] + (size_t)(G->rank0 + d) * G->spd * w;
@@ -496,6 +501,7 @@ static int dense_merge(pluss_group* G) {
                        G->vec[d] + (size_t)G->spd * DVEC);
   }
   PLUSS_HIP_CHECK(hipGetLastError());
+  if (G->nranks == 1 && G->capturing) return fork_shards(G);  // (one rank: the all-reduce is the identity)
   PLUSS_NCCL_CHECK(g_rccl.GroupStart());
   for (int d = 0; d < G->ndev; ++d) {
     unsigned long long* v = G->vec[d] + (size_t)G->spd * DVEC;
@@ -1201,8 +1207,17 @@ int pluss_group_gen_faithful(pluss_group* G, uint64_t seed, const uint64_t total
   if (capture) {
     PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
     PLUSS_HIP_CHECK(hipStreamBeginCapture(G->xs[0], hipStreamCaptureModeThreadLocal));
+    G->capturing = true;
     for (auto* c : G->ctx) c->fb.capture = true;
-    if (int rc = fork_shards(G)) return rc;  // (the shard streams join the capture)
+    if (int rc = fork_shards(G)) {  // (the shard streams join the capture)
+      hipGraph_t gr = nullptr;
+      (void)hipStreamEndCapture(G->xs[0], &gr);
+      if (gr) (void)hipGraphDestroy(gr);
+      G->capturing = false;
+      for (auto* c : G->ctx) c->fb.capture = false;
+      F.seen = false;
+      return rc;
+    }
   }
   GErr E;
   group_reset(G, E);
@@ -1226,6 +1241,7 @@ int pluss_group_gen_faithful(pluss_group* G, uint64_t seed, const uint64_t total
   if (!rc) rc = join_shards(G);  // (every forked stream rejoins before the capture ends)
   hipGraph_t gr = nullptr;
   const hipError_t ce = hipStreamEndCapture(G->xs[0], &gr);
+  G->capturing = false;
   for (auto* c : G->ctx) c->fb.capture = false;
   if (!rc && !E.rc && ce == hipSuccess) {
     const hipError_t ie = hipGraphInstantiate(&F.ex, gr, nullptr, nullptr, 0);

@@ -1011,8 +1011,10 @@ __device__ __forceinline__ void srt_item_sort(const PT (&w)[NSE], uint32_t s, ui
 // x, each child's payloads loaded while the previous one is sorted.  Items
 // past SCAP go to the deep list.
 constexpr uint32_t FG = 4;
+// (4 waves per SIMD asked: the payload-only instantiation was otherwise given
+// 150 VGPRs and scratch, 3 waves, and ran 1.4x slower)
 template <typename PT, typename KT, bool PFX = true>  // !PFX: the payloads alone (SRC_W32P)
-__global__ __launch_bounds__(SB) void k_srt_final(const SrtRefs a, const SrtParent* __restrict__ par,
+__global__ __launch_bounds__(SB) __attribute__((amdgpu_waves_per_eu(4))) void k_srt_final(const SrtRefs a, const SrtParent* __restrict__ par,
                                                  const uint32_t* __restrict__ hist2, const PT* __restrict__ X1,
                                                  const PT* __restrict__ Y, KT* __restrict__ OUT, SrtDeep dp,
                                                  const SrtL2 l2) {
