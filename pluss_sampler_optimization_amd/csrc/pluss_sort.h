@@ -1014,7 +1014,7 @@ constexpr uint32_t FG = 4;
 // (4 waves per SIMD asked: the payload-only instantiation was otherwise given
 // 150 VGPRs and scratch, 3 waves, and ran 1.4x slower)
 template <typename PT, typename KT, bool PFX = true>  // !PFX: the payloads alone (SRC_W32P)
-__global__ __launch_bounds__(SB) __attribute__((amdgpu_waves_per_eu(4))) void k_srt_final(const SrtRefs a, const SrtParent* __restrict__ par,
+__global__ __launch_bounds__(SB) __attribute__((amdgpu_waves_per_eu(sizeof(PT) == 4 ? 4 : 1))) void k_srt_final(const SrtRefs a, const SrtParent* __restrict__ par,
                                                  const uint32_t* __restrict__ hist2, const PT* __restrict__ X1,
                                                  const PT* __restrict__ Y, KT* __restrict__ OUT, SrtDeep dp,
                                                  const SrtL2 l2) {
@@ -1038,7 +1038,9 @@ __global__ __launch_bounds__(SB) __attribute__((amdgpu_waves_per_eu(4))) void k_
   // an item of cnt <= SCAP payloads in NSE registers per thread, the fewest
   // that hold it (the slots past cnt are predicated off but still issued)
   // (payloads read from src[rs, rs + cnt), written as words to OUT[s, s + cnt))
-  auto item = [&](const PT* __restrict__ src, uint32_t rs, uint32_t s, uint32_t cnt, uint32_t hi) {
+  // (always inlined: the payload-only instantiation otherwise made it a call, with scratch)
+  auto item = [&](const PT* __restrict__ src, uint32_t rs, uint32_t s, uint32_t cnt, uint32_t hi)
+                  __attribute__((always_inline)) {
     if (cnt <= 8 * SB) {
       PT w[8];
       srt_item_load<PT, 8>(src, rs, cnt, w);
