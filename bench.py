@@ -595,12 +595,16 @@ def capi_group_bench(P, torch, dist, cfg, counts, total, world, rank, backend, s
 
 
 def capi_group_faithful(P, cfg, reps=3):
-    """Faithful mode at config 3 (2^28 samples, generated key-order lists)
-    through pluss_group_gen_faithful on one device with 1, 2 and 8 logical
-    key-range shards: the device-driven sharded pass (rows all-gathered over
-    RCCL between phases, no host round trip), the shards' tables merged on the
-    host.  Host clock around the whole call (plan, phases, gather, merge),
-    median of `reps`; every shard count's histogram equals the one-shard one."""
+    """Faithful mode at config 3 (2^28 samples) through the C-ABI group on one
+    device with 1, 2 and 8 logical key-range shards: generated key-order lists
+    (pluss_group_gen_faithful), r10's own law (pluss_group_gen_uniform_faithful)
+    and an any-order host list (pluss_group_sampled_hist, 1 and 8 shards).
+    Rows exchanged between phases on the device (RCCL over several ranks; with
+    one rank the exchanges are identities and a replayed pass leaves them
+    out), the pass ending in the dense vector.  Host clock around the whole call,
+    median of `reps` after two warm calls (the second identical gen_faithful call
+    is captured into a HIP graph and replayed after); every shard count's
+    histogram equals the one-shard one."""
     fcfg = P.SamplerConfig(n=4096, threads=cfg.threads, chunk=cfg.chunk, mode="faithful", device=cfg.device)
     totals = P.default_counts(4096, 1 << 28)
 
