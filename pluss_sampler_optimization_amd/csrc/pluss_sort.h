@@ -552,17 +552,27 @@ __global__ __launch_bounds__(SB1) void k_srt_scatter2f(const SrtRefs a, const Sr
                                                       const uint32_t* __restrict__ cmap,
                                                       const uint32_t* __restrict__ tot, const PT* __restrict__ X1,
                                                       PT* __restrict__ Y, const SrtL2 l2) {
+  // (no digit array beside the stage: a staged payload holds its own digit,
+  // so the LDS is 38 KB and four workgroups share a CU)
   __shared__ PT stage[SC1];
-  __shared__ uint8_t sdig[SC1];
   __shared__ uint32_t bcnt[SB], bst[SB], bbase[SB], ccap[SB], coff[SB], wsum[SB / 64];
   const uint32_t q2 = blockIdx.x / SPL, half = blockIdx.x - q2 * SPL;
-  if (q2 >= tot[0] || *l2.ovf) return;  // (a level 1 or region overflow: the counted level 2 runs)
-  const SrtParent P = par[cmap[q2]];
+  // (the three reads issued together; cmap has a slot for every workgroup's q2)
+  const uint32_t t0 = tot[0], of = *l2.ovf, pi = cmap[q2];
+  if (q2 >= t0 || of) return;  // (a level 1 or region overflow: the counted level 2 runs)
+  const SrtParent P = par[pi];
   const uint32_t k = q2 - P.cbase;
   const uint32_t c0 = k * SC + half * SC1;  // this workgroup's part of the parent's k-th chunk
   if (c0 >= P.count) return;
   const uint32_t e0 = P.src + c0, e1 = P.count - c0 < SC1 ? P.src + P.count : e0 + SC1;
   const uint32_t lo = a.wb - a.d1[P.ref] - P.d2, mask = (1u << P.d2) - 1;
+  PT w[SE];  // (loaded first: the capacities and their scan run while the loads are in flight)
+  uint32_t rk[SE];
+#pragma unroll
+  for (int j = 0; j < SE; ++j) {
+    const uint32_t i = e0 + (uint32_t)j * SB1 + threadIdx.x;
+    w[j] = __builtin_nontemporal_load(X1 + (i < e1 ? i : e1 - 1));
+  }
   if (threadIdx.x < SB) bcnt[threadIdx.x] = 0;
   if (threadIdx.x < SB) {  // the children's capacities; their region offsets below
     ccap[threadIdx.x] = threadIdx.x <= mask ? srt_cap2(a, P, threadIdx.x, l2.wmax) : 0u;
@@ -585,13 +595,6 @@ __global__ __launch_bounds__(SB1) void k_srt_scatter2f(const SrtRefs a, const Sr
     for (int x = 0; x < SB / 64; ++x) pre += x < (int)wid ? wsum[x] : 0u;
     if (t < SB) coff[t] = pre + inc - v;
   }
-  PT w[SE];
-  uint32_t rk[SE];
-#pragma unroll
-  for (int j = 0; j < SE; ++j) {
-    const uint32_t i = e0 + (uint32_t)j * SB1 + threadIdx.x;
-    w[j] = __builtin_nontemporal_load(X1 + (i < e1 ? i : e1 - 1));
-  }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < SE; ++j) {
@@ -599,19 +602,13 @@ __global__ __launch_bounds__(SB1) void k_srt_scatter2f(const SrtRefs a, const Sr
     rk[j] = i < e1 ? atomicAdd(&bcnt[srt_dig(w[j], lo, mask)], 1u) : 0u;
   }
   __syncthreads();
-  if (threadIdx.x < SB) {  // this part's run in each child's region
-    const uint32_t d = threadIdx.x, n = bcnt[d];
-    uint32_t at = 0;
-    if (d <= mask && n) {
-      at = atomicAdd(&l2.fill[P.cb2 + d], n);
-      if (at + n > ccap[d]) {
-        atomicOr(l2.ovf, 1u);
-        at = 0xFFFFFFFFu;
-      } else {
-        at += P.ybase + coff[d];
-      }
-    }
-    bbase[d] = at;
+  // this part's run in each child's region: reserved now, placed after the
+  // scan and the staging (the atomic's round trip overlaps them)
+  const uint32_t d = threadIdx.x;
+  uint32_t n = 0, at = 0;
+  if (d < SB) {
+    n = bcnt[d];
+    if (d <= mask && n) at = atomicAdd(&l2.fill[P.cb2 + d], n);
     bst[d] = n;
   }
   __syncthreads();
@@ -636,16 +633,27 @@ __global__ __launch_bounds__(SB1) void k_srt_scatter2f(const SrtRefs a, const Sr
   for (int j = 0; j < SE; ++j) {
     const uint32_t i = e0 + (uint32_t)j * SB1 + threadIdx.x;
     if (i < e1) {
-      const uint32_t d = srt_dig(w[j], lo, mask), q = bst[d] + rk[j];
-      stage[q] = w[j];
-      sdig[q] = (uint8_t)d;
+      const uint32_t dj = srt_dig(w[j], lo, mask);
+      stage[bst[dj] + rk[j]] = w[j];
     }
+  }
+  if (d < SB) {
+    if (d <= mask && n) {
+      if (at + n > ccap[d]) {
+        atomicOr(l2.ovf, 1u);
+        at = 0xFFFFFFFFu;
+      } else {
+        at += P.ybase + coff[d];
+      }
+    }
+    bbase[d] = at;
   }
   __syncthreads();
   const uint32_t mt = e1 - e0;
   for (uint32_t i = threadIdx.x; i < mt; i += SB1) {
-    const uint32_t d = sdig[i], at = bbase[d];
-    if (at != 0xFFFFFFFFu) Y[at + (i - bst[d])] = stage[i];
+    const PT x = stage[i];
+    const uint32_t d = srt_dig(x, lo, mask), at = bbase[d];
+    if (at != 0xFFFFFFFFu) Y[at + (i - bst[d])] = x;
   }
 }
 
@@ -682,7 +690,15 @@ __global__ __launch_bounds__(SB) void k_srt_plan(SrtRefs a, const uint32_t* __re
     const uint32_t nch = (uint32_t)(a.coff[r + 1] - a.coff[r]);
     return nch ? hist[a.hoff[r] + (uint64_t)b * nch] : (uint32_t)a.eoff[r];
   };
-  for (uint32_t p = threadIdx.x; p < np; p += SB) {
+  // (each thread's parents p = threadIdx.x + k * SB stay in registers and go
+  // out once at the end: re-reading them from memory between the scans was
+  // most of this kernel's time)
+  constexpr int PPT = (6 * 256 + SB - 1) / SB;
+  SrtParent pp[PPT];
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const uint32_t p = threadIdx.x + (uint32_t)k * SB;
+    if (p >= np) continue;
     uint32_t r, b1;
     locate(p, r, b1);
     uint32_t s, cnt, src;
@@ -699,21 +715,26 @@ __global__ __launch_bounds__(SB) void k_srt_plan(SrtRefs a, const uint32_t* __re
     const uint32_t hi = a.wb - a.d1[r];
     const uint32_t d2 = (cnt > SCAP && hi > 0) ? srt_split_bits(cnt, hi) : 0u;
     const uint32_t nc2 = d2 ? (cnt + SC - 1) / SC : 0u;
-    par[p] = SrtParent{s, cnt, r, b1, d2, nc2, 0, 0, src, 0, 0};
+    pp[k] = SrtParent{s, cnt, r, b1, d2, nc2, 0, 0, src, 0, 0};
   }
   __syncthreads();  // (v1 free again)
   if (filled && l2.fill) {  // the count-free level 2's regions: per parent a bound on its children's capacities
-    for (uint32_t p = threadIdx.x; p < np; p += SB) {
-      const SrtParent P = par[p];
-      v1[p] = P.d2 ? srt_cap2_sum(P.count, 1u << P.d2) : 0u;
-      v2[p] = P.d2 ? 1u << P.d2 : 0u;
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const uint32_t p = threadIdx.x + (uint32_t)k * SB;
+      if (p >= np) continue;
+      v1[p] = pp[k].d2 ? srt_cap2_sum(pp[k].count, 1u << pp[k].d2) : 0u;
+      v2[p] = pp[k].d2 ? 1u << pp[k].d2 : 0u;
     }
     __syncthreads();
     const uint32_t ysum = srt_block_scan(v1, np, wsum);
     const uint32_t nchild = srt_block_scan(v2, np, wsum);
-    for (uint32_t p = threadIdx.x; p < np; p += SB) {
-      par[p].ybase = v1[p];
-      par[p].cb2 = v2[p];
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const uint32_t p = threadIdx.x + (uint32_t)k * SB;
+      if (p >= np) continue;
+      pp[k].ybase = v1[p];
+      pp[k].cb2 = v2[p];
     }
     for (uint32_t i = threadIdx.x; i < nchild; i += SB) l2.fill[i] = 0;
     if (threadIdx.x == 0) *l2.ovf = ysum > l2.ycap ? 1u : 0u;
@@ -721,19 +742,24 @@ __global__ __launch_bounds__(SB) void k_srt_plan(SrtRefs a, const uint32_t* __re
   } else if (l2.fill && threadIdx.x == 0) {
     *l2.ovf = 1u;  // (level 1 took the counted path: so does level 2)
   }
-  for (uint32_t p = threadIdx.x; p < np; p += SB) {
-    const uint32_t nc2 = par[p].nc2;
-    v1[p] = nc2;
-    v2[p] = nc2 << par[p].d2;
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const uint32_t p = threadIdx.x + (uint32_t)k * SB;
+    if (p >= np) continue;
+    v1[p] = pp[k].nc2;
+    v2[p] = pp[k].nc2 << pp[k].d2;
   }
   __syncthreads();
   const uint32_t g2 = srt_block_scan(v1, np, wsum);
   const uint32_t h2 = srt_block_scan(v2, np, wsum);
-  for (uint32_t p = threadIdx.x; p < np; p += SB) {
-    par[p].cbase = v1[p];
-    par[p].h2off = v2[p];
-    const uint32_t nc2 = par[p].nc2;
-    for (uint32_t k = 0; k < nc2; ++k) cmap[v1[p] + k] = p;
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const uint32_t p = threadIdx.x + (uint32_t)k * SB;
+    if (p >= np) continue;
+    pp[k].cbase = v1[p];
+    pp[k].h2off = v2[p];
+    par[p] = pp[k];
+    for (uint32_t j = 0; j < pp[k].nc2; ++j) cmap[v1[p] + j] = p;
   }
   if (threadIdx.x == 0) {
     tot[0] = g2;
