@@ -1506,33 +1506,23 @@ constexpr bool fa_lm() { return fa_mem<SRC>() || SRC == SRC_UNI; }
 
 // waves per SIMD asked of the compiler: lists in memory fit 8 (<= 64 VGPRs and
 // <= 80 SGPRs: at 83 SGPRs the SGPR file held 7); the uniform staging needs 4
-template <int SRC, bool PARTT = false>
-constexpr int fa_lm_waves() { return SRC == SRC_UNI || SRC == SRC_W32P || PARTT ? 4 : 8; }
-// the references' partial last tiles (lists in memory): their own small launch
-// of the lane-major path (k_fa_local_lm<.., true>), so the full-tile kernel
-// keeps the full tile's registers and none of them waits for the queued pass
-struct FaPartT {
-  uint32_t n;
-  uint32_t gt[6];
-};
-template <int SRC, bool CHECK, bool PARTT = false>
-__global__ __launch_bounds__(fa_lm_nt<SRC>()) __attribute__((amdgpu_waves_per_eu(fa_lm_waves<SRC, PARTT>()))) void k_fa_local_lm(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
+template <int SRC>
+constexpr int fa_lm_waves() { return SRC == SRC_UNI || SRC == SRC_W32P ? 4 : 8; }
+// (the references' partial last tiles of lists in memory go to the queued
+// pass: every list at the BASELINE shapes already queues C0's and C1's tiles,
+// whose keys span more than 32 bits, so a launch of their own for the partial
+// tiles only added a kernel to the pass, r5 ab1)
+template <int SRC, bool CHECK>
+__global__ __launch_bounds__(fa_lm_nt<SRC>()) __attribute__((amdgpu_waves_per_eu(fa_lm_waves<SRC>()))) void k_fa_local_lm(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
                                                     unsigned long long* __restrict__ part,
                                                     unsigned long long* __restrict__ klist, unsigned long long* slots,
-                                                    unsigned int* slowq, GTable g, FaPartT pt = FaPartT{}) {
+                                                    unsigned int* slowq, GTable g) {
   static_assert(fa_lm<SRC>(), "the stratified generated source: k_fa_local_fast");
-  static_assert(!PARTT || fa_mem<SRC>(), "partial tiles apart: lists in memory");
   constexpr int NT = fa_lm_nt<SRC>();
   __shared__ FaLmLds<SRC> L;
   FaLm<NT>& sh = L.s;
-  uint32_t gsel = blockIdx.x;
-  if constexpr (PARTT) {
-#pragma unroll
-    for (int x = 0; x < 6; ++x) gsel = blockIdx.x == (uint32_t)x ? pt.gt[x] : gsel;
-  }
-  const FaTile T = fa_tile(a, gsel);
-  if (!PARTT) fa_cold_slot(T, g, slots);
-  if (!PARTT && fa_mem<SRC>() && pt.n && T.mt != TILE) return;  // (the partial launch takes it)
+  const FaTile T = fa_tile(a, blockIdx.x);
+  fa_cold_slot(T, g, slots);
   unsigned long long* kl_out = klist + T.gt * (uint64_t)(2 * KL);
   bool done = false;
   // lists in memory: full tiles only, the few partial ones (a reference's last
@@ -1548,10 +1538,6 @@ __global__ __launch_bounds__(fa_lm_nt<SRC>()) __attribute__((amdgpu_waves_per_eu
 #define PLUSS_FA_LM(R)                                                                              \
   if (T.mt == TILE) done = fa_lane_tile<SRC, CHECK, R, true, NT>(m, a, T, sh, kl_out, g, L.raw);   \
   else done = fa_lane_tile<SRC, CHECK, R, false, NT>(m, a, T, sh, kl_out, g, L.raw);
-    PLUSS_FA_REFS(PLUSS_FA_LM)
-#undef PLUSS_FA_LM
-  } else if (PARTT) {
-#define PLUSS_FA_LM(R) done = fa_lane_tile<SRC, CHECK, R, false, NT>(m, a, T, sh, kl_out, g, L.raw);
     PLUSS_FA_REFS(PLUSS_FA_LM)
 #undef PLUSS_FA_LM
   } else if (T.mt == TILE) {
@@ -2088,19 +2074,9 @@ inline void fa_launch_t(const FaLaunch& L) {
         // (a pass whose chunk phase ran left it empty: no fill launch then)
         if (!b.slowq_clean) (void)hipMemsetAsync(b.slowq, 0, sizeof(unsigned int), L.s);
         b.slowq_clean = false;
-        if constexpr (fa_mem<SRC>()) {
-          // full tiles, then the references' partial last tiles in their own launch
-          FaPartT pt{};
-          for (int r = 0; r < 6; ++r)
-            if (L.a.n[r] % TILE) pt.gt[pt.n++] = (uint32_t)(L.a.toff[r] + L.a.n[r] / TILE);
-          hipLaunchKernelGGL((k_fa_local_lm<SRC, CHK>), dim3(t), dim3(fa_lm_nt<SRC>()), 0, L.s, L.m, L.a, b.tmax,
-                             b.dpart, b.klist, b.fslot, b.slowq, L.g, pt);
-          if (pt.n)
-            hipLaunchKernelGGL((k_fa_local_lm<SRC, CHK, true>), dim3(pt.n), dim3(fa_lm_nt<SRC>()), 0, L.s, L.m, L.a,
-                               b.tmax, b.dpart, b.klist, b.fslot, b.slowq, L.g, pt);
-        } else if constexpr (fa_lm<SRC>())
+        if constexpr (fa_lm<SRC>())
           hipLaunchKernelGGL((k_fa_local_lm<SRC, CHK>), dim3(t), dim3(fa_lm_nt<SRC>()), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
-                             b.fslot, b.slowq, L.g, FaPartT{});
+                             b.fslot, b.slowq, L.g);
         else
           hipLaunchKernelGGL((k_fa_local_fast<SRC, CHK>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart,
                              b.klist, b.fslot, b.slowq, L.g);
