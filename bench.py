@@ -313,7 +313,7 @@ def faithful_bench(P, torch, device, stream):
     return out
 
 
-def faithful_config3_bench(P, torch, device, stream, reps=5):
+def faithful_config3_bench(P, torch, device, stream, reps=20):
     """FAITHFUL mode (r10's queue semantics, bit-exact with the reference's
     sampler_<REF> on the same sample list) at the headline shape: N=4096,
     T=8, 2^28 samples on one GPU, six references concurrently.  sorted = the
