@@ -426,10 +426,29 @@ __device__ __forceinline__ void fa_load_run(const Model& m, const FaOne& o, cons
       }
       if constexpr (SRC == SRC_W32P) {  // the payloads' parent digits put back
         const W32P pw = w32p_tile(o, T.base, T.mt);
+        const uint32_t b0 = (uint32_t)(pw.pa >> o.phi), b1 = (uint32_t)(pw.pb >> o.phi);
+        if (pw.ok || b1 - b0 > 8u) {
 #pragma unroll
-        for (int k = 0; k < EPT; ++k) {
-          const uint32_t e = (uint32_t)k * NT + threadIdx.x;
-          sh.raw[fa_slot_n<EPT>(e)] = w32p_word(o, pw, T.base + (e < last ? e : last), v[k]);
+          for (int k = 0; k < EPT; ++k) {
+            const uint32_t e = (uint32_t)k * NT + threadIdx.x;
+            sh.raw[fa_slot_n<EPT>(e)] = w32p_word(o, pw, T.base + (e < last ? e : last), v[k]);
+          }
+        } else {
+          // a tile over three to nine parents (a sparse reference's, like C0's):
+          // the starts of parents b0+1..b1 read once, each element's parent is b0
+          // plus the starts at or below it (no search through memory per element)
+          uint64_t st[8];
+#pragma unroll
+          for (uint32_t x = 0; x < 8; ++x) st[x] = b0 + 1 + x <= b1 ? (uint64_t)o.ppar[b0 + 1 + x].start - o.peoff : ~0ull;
+#pragma unroll
+          for (int k = 0; k < EPT; ++k) {
+            const uint32_t e = (uint32_t)k * NT + threadIdx.x;
+            const uint64_t i = T.base + (e < last ? e : last);
+            uint32_t q = b0;
+#pragma unroll
+            for (uint32_t x = 0; x < 8; ++x) q += st[x] <= i ? 1u : 0u;
+            sh.raw[fa_slot_n<EPT>(e)] = ((unsigned long long)q << o.phi) | v[k];
+          }
         }
       } else {
 #pragma unroll
