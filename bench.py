@@ -518,7 +518,8 @@ def collective_costs(args, torch, dist, ctx, samples, n_local, dense, stream, re
             "allreduce_words": int(t.numel()), "backend": args.backend,
             "note": "kernel_only_ms: the K timed launches without their all-reduces (HIP events); "
                     "allreduce_eager_us: one eager all-reduce of the dense vector and its wait, median; in the timed "
-                    "steps the all-reduces run asynchronously from HIP graphs, overlapped with the next launch"}
+                    "steps each step's all-reduce is issued eagerly and asynchronously (no collective inside a HIP "
+                    "graph), overlapped with the next launch"}
 
 
 def faithful_sharded_bench(P, torch, dist, device, stream, world, reps=3):
@@ -555,8 +556,9 @@ def faithful_sharded_bench(P, torch, dist, device, stream, world, reps=3):
 def capi_group_bench(P, torch, dist, cfg, counts, total, world, rank, backend, steps, warmup):
     """The same dense step through the C ABI's multi-GPU group (pluss_group_*,
     csrc/pluss_group.hip): the library holds the shards' resident lists, runs
-    the count and the RCCL all-reduce of the 19-word vector itself (one local
-    device: replayed from HIP graphs of 16 steps) -- what a C++ or Rust caller
+    the count and the RCCL all-reduce of the 19-word vector itself (one rank
+    on one device: replayed from HIP graphs of 16 steps without the identity
+    all-reduce; several ranks: eager) -- what a C++ or Rust caller
     of the reference gets without torch.  N>1: one rank per process, the RCCL
     id made by rank 0 and handed over by torch.distributed.  N=1 also runs 8
     logical shards on the one GPU (SURVEY §4.4's exchange rehearsal: not a
@@ -767,12 +769,14 @@ def main():
 
     ctx.reset(sp)
     enqueue(args.warmup)
-    # The timed steps are replayed from HIP graphs of G steps (kernel launches
-    # and, N>1, the all-reduces with their double-buffer dependencies): one
-    # graph launch per G steps instead of a Python launch + a c10d call per step.
+    # The timed steps are replayed from HIP graphs of G steps (one graph launch
+    # per G steps instead of a Python launch per step) when a step holds no
+    # collective.  With N>1 every step's all-reduce is issued eagerly: no RCCL
+    # call is ever captured into a graph (the library's capture rule, DESIGN.md
+    # section 8: a replayed capture holding RCCL calls crashed on the host, r5m).
     graphs = []  # (graph, steps, vector of its last step)
-    launch_mode = "eager"
-    if args.graph and args.backend == "nccl":
+    launch_mode = "eager (one c10d all_reduce per step, asynchronous)" if collective else "eager"
+    if args.graph and not collective:
         G = min(args.steps, args.graph)
         try:
             for size in ([G] if args.steps % G == 0 else [G, args.steps % G]):

@@ -323,9 +323,11 @@ int pluss_keyorder_index_range(const pluss_cfg *cfg, uint64_t seed, int32_t ref,
      pluss_group_expand       resident Feistel lists, each shard its slices of
                               counts[r] samples per reference (pluss_expand_samples)
      pluss_group_dense        `passes` dense passes over them (the bench step;
-                              one local device: replayed from HIP graphs); out:
-                              the last pass's merged dense vector (as
-                              pluss_dev_sampled_hist_dense)
+                              one rank on one device: replayed from HIP graphs
+                              without collectives, which are identities there;
+                              several ranks: eager); out: the last pass's
+                              merged dense vector (as pluss_dev_sampled_hist_dense;
+                              passes == 0: runs nothing, out all zero)
      pluss_group_gen_count_dense  generated key-order slices counted and merged */
 typedef struct pluss_group pluss_group;
 #define PLUSS_GROUP_ID_BYTES 128

@@ -601,6 +601,9 @@ static SrtPlan srt_plan(const Model& m, const void* const in[6], const uint64_t 
   P.fast1 = P.p32;
   for (int r = 0; r < 6; ++r)
     if (cnt[r] && wb <= P.a.d1[r]) P.fast1 = false;
+  // the count-free levels size X1 and Y as 2 payloads per sample and sum their
+  // regions' capacities in 32 bits: past 2^31 samples the counted levels
+  if (e > ((uint64_t)1 << 31)) P.fast1 = false;
   return P;
 }
 
@@ -701,10 +704,6 @@ template <typename KT, bool SMP>
 static int srt_sort(pluss_ctx* ctx, FaithfulBufs& b, const void* const in[6], const uint64_t cnt[6],
                     unsigned long long* x1, unsigned long long* y, KT* out, hipStream_t s, SrtPay* pay = nullptr) {
   SrtPlan P = srt_plan(ctx->m, in, cnt);
-  // words already made (the group's partitioned lists): the counted levels
-  // (a group pass over config 3 faulted with the count-free ones on this input,
-  // cause not yet found; the caller's samples keep them)
-  if (!SMP) P.fast1 = false;
   if (pay) {  // (the parents' address once srt_reserve below has grown the scratch)
     pay->on = P.p32 && sizeof(KT) > 4;
     pay->par = nullptr;
@@ -1491,14 +1490,29 @@ int faith_shards_local_words(pluss_ctx* ctx, const void* const in[6], const uint
     a.src[r] = fm == FM_PK32 ? (const void*)((const uint32_t*)b.keys_s + soff) : (const void*)(b.keys_s + soff);
     soff += cnt[r];
   }
+  // the same sort as one GPU's radix pass (count-free levels, 4-byte payloads
+  // read back with their parents' digits past N = 1024)
+  SrtPay pay{};
   if (fm == FM_PK32) {
     if (int rc = srt_sort<uint32_t, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, (uint32_t*)b.keys_s, s)) return rc;
-  } else if (int rc = srt_sort<unsigned long long, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, b.keys_s, s)) {
+  } else if (int rc = srt_sort<unsigned long long, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, b.keys_s, s, &pay)) {
     return rc;
   }
   ctx->tables_dirty = true;
   f.src = fm == FM_PK32 ? SRC_W32 : SRC_W64;
-
+  if (pay.on) {
+    f.src = SRC_W32P;
+    soff = 0;
+    for (int r = 0; r < 6; ++r) {
+      a.src[r] = (const uint32_t*)b.keys_s + soff;
+      soff += cnt[r];
+      a.ppb[r] = pay.pb[r];
+      a.ppn[r] = pay.pn[r];
+      a.phi[r] = pay.hi[r];
+      a.peoff[r] = pay.eoff[r];
+    }
+    a.ppar = pay.par;
+  }
   if (int rc = fa_prepare(ctx, a, f.src, false, true, s, &f.L)) return rc;
   return shards_phase1(ctx, f, d_row, s);
 }

@@ -236,7 +236,14 @@ struct pluss_group {
   std::vector<pluss::PartBufs> part;      // per device: the any-order faithful pass
   std::map<uint32_t, hipGraphExec_t> graphs;  // dense passes captured per batch size (one local device)
   pluss::FaGraph* fg = nullptr;               // the last faithful pass, captured (pluss_group_gen_faithful)
-  bool capturing = false;                     // a pass being captured into fg (one rank: no RCCL calls in it)
+  // A pass being captured into a HIP graph.  The capture rule (one for every
+  // rank count): a captured graph never holds an RCCL call.  Only one-rank
+  // groups capture, and there every collective is the identity (each shard
+  // writes its block of the one buffer), so it is left out; groups of several
+  // ranks run every pass eagerly.  (r5m: a host segfault while replaying a
+  // pass whose capture held RCCL calls)
+  bool capturing = false;
+  std::vector<unsigned long long*> agr;       // per device: a failure word summed over the ranks (agree_failed)
 };
 
 namespace pluss {
@@ -261,7 +268,7 @@ static void group_free(pluss_group* G) {
   }
   for (int d = 0; d < G->ndev; ++d) {
     (void)hipSetDevice(G->dev[d]);
-    for (auto* v : {&G->rows, &G->vec, &G->blk})
+    for (auto* v : {&G->rows, &G->vec, &G->blk, &G->agr})
       if (d < (int)v->size() && (*v)[d]) (void)hipFree((*v)[d]);
     if (d < (int)G->part.size()) {
       PartBufs& P = G->part[d];
@@ -289,6 +296,7 @@ static int group_setup(pluss_group* G) {
   G->rows.assign(G->ndev, nullptr);
   G->vec.assign(G->ndev, nullptr);
   G->blk.assign(G->ndev, nullptr);
+  G->agr.assign(G->ndev, nullptr);
   G->part.assign(G->ndev, PartBufs{});
   for (int d = 0; d < G->ndev; ++d) {
     PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
@@ -303,6 +311,12 @@ static int group_setup(pluss_group* G) {
     PLUSS_HIP_CHECK(hipMalloc((void**)&G->vec[d], (size_t)(S + 1) * DVEC * 8));
     PLUSS_HIP_CHECK(hipMemset(G->vec[d], 0, (size_t)(S + 1) * DVEC * 8));
     PLUSS_HIP_CHECK(hipMalloc((void**)&G->blk[d], (size_t)G->nshards * GBLOCK * 8));
+    PLUSS_HIP_CHECK(hipMalloc((void**)&G->agr[d], 64));
+    // the any-order pass's gathered bin totals (R x 6S words): allocated here,
+    // so no rank can miss that all-gather for want of its buffer
+    PartBufs::Buf& tb = G->part[d].tot;
+    tb.cap = (size_t)G->nranks * 6 * G->nshards * 8;
+    PLUSS_HIP_CHECK(hipMalloc(&tb.p, tb.cap));
   }
   for (auto& e : G->ev) PLUSS_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   return PLUSS_OK;
@@ -341,10 +355,9 @@ static int fork_shards(pluss_group* G) {
 // (each device holds every shard's slot; its own shards' slots are written)
 static int gather_blocks(pluss_group* G, std::vector<unsigned long long*>& buf, size_t w) {
   if (int rc = join_shards(G)) return rc;
-  // one rank: every shard wrote its block of the one buffer, the all-gather is
-  // the identity -- left out of a captured pass (RCCL calls inside a HIP graph
-  // capture were the one place a run crashed on the host, intermittently)
-  if (G->nranks == 1 && G->capturing) return fork_shards(G);
+  // (a captured pass is a one-rank pass: the all-gather is the identity, left
+  // out -- the capture rule at pluss_group::capturing)
+  if (G->capturing) return fork_shards(G);
   PLUSS_NCCL_CHECK(g_rccl.GroupStart());
   for (int d = 0; d < G->ndev; ++d) {
     unsigned long long* own = buf[d] + (size_t)(G->rank0 + d) * G->spd * w;
@@ -501,7 +514,7 @@ static int dense_merge(pluss_group* G) {
                        G->vec[d] + (size_t)G->spd * DVEC);
   }
   PLUSS_HIP_CHECK(hipGetLastError());
-  if (G->nranks == 1 && G->capturing) return fork_shards(G);  // (one rank: the all-reduce is the identity)
+  if (G->capturing) return fork_shards(G);  // (one rank: the all-reduce is the identity)
   PLUSS_NCCL_CHECK(g_rccl.GroupStart());
   for (int d = 0; d < G->ndev; ++d) {
     unsigned long long* v = G->vec[d] + (size_t)G->spd * DVEC;
@@ -536,12 +549,42 @@ static int dense_pass_on_xs(pluss_group* G, GErr& E) {
                        G->vec[d] + (size_t)G->spd * DVEC);
   }
   PLUSS_HIP_CHECK(hipGetLastError());
+  if (G->capturing) return PLUSS_OK;  // (one rank, one device: the all-reduce is the identity)
   PLUSS_NCCL_CHECK(g_rccl.GroupStart());
   for (int d = 0; d < G->ndev; ++d) {
     unsigned long long* v = G->vec[d] + (size_t)G->spd * DVEC;
     PLUSS_NCCL_CHECK(g_rccl.AllReduce(v, v, GV_W, ncclUint64, ncclSum, G->comm[d], G->xs[d]));
   }
   PLUSS_NCCL_CHECK(g_rccl.GroupEnd());
+  return PLUSS_OK;
+}
+
+// Whether any rank of the job failed, the same answer on every rank: each
+// device's failure word summed over the ranks (one 1-word all-reduce and a
+// read-back).  A process that drives every rank itself (pluss_group_create)
+// already knows: its GErr holds every device's error.  Used before a
+// point-to-point exchange, where a rank that returned early would leave its
+// peers waiting in ncclSend / ncclRecv.
+static int agree_failed(pluss_group* G, bool mine, bool* any) {
+  *any = mine;
+  if (G->nranks == G->ndev) return PLUSS_OK;
+  for (int d = 0; d < G->ndev; ++d) {
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    hipLaunchKernelGGL(k_group_word, dim3(1), dim3(1), 0, G->xs[d], G->agr[d], mine ? 1ull : 0ull);
+  }
+  PLUSS_HIP_CHECK(hipGetLastError());
+  PLUSS_NCCL_CHECK(g_rccl.GroupStart());
+  for (int d = 0; d < G->ndev; ++d)
+    PLUSS_NCCL_CHECK(g_rccl.AllReduce(G->agr[d], G->agr[d], 1, ncclUint64, ncclSum, G->comm[d], G->xs[d]));
+  PLUSS_NCCL_CHECK(g_rccl.GroupEnd());
+  unsigned long long v = 0;
+  PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
+  PLUSS_HIP_CHECK(hipMemcpyAsync(&v, G->agr[0], 8, hipMemcpyDeviceToHost, G->xs[0]));
+  for (int d = 0; d < G->ndev; ++d) {
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+    PLUSS_HIP_CHECK(hipStreamSynchronize(G->xs[d]));
+  }
+  *any = v != 0;
   return PLUSS_OK;
 }
 
@@ -676,7 +719,6 @@ static int group_any_order(pluss_group* G, const uint64_t* samples, uint64_t n, 
     sln[d] = (uint64_t)((unsigned __int128)n * (gd + 1) / R) - sl0[d];
     nblk[d] = faith_part_blocks(sln[d], (uint32_t)S);
     int rc = E.rc;
-    if (!rc) rc = part_buf(G, d, P.tot, (size_t)R * nb * 8);
     if (!rc) rc = part_buf(G, d, P.smp, sln[d] * 8);
     if (!rc) rc = part_buf(G, d, P.bounds, ((size_t)S + 1) * 8);
     if (!rc) rc = part_buf(G, d, P.hist, (size_t)nb * nblk[d] * 4);
@@ -689,13 +731,13 @@ static int group_any_order(pluss_group* G, const uint64_t* samples, uint64_t n, 
     if (!rc && sln[d])
       rc = hip_rc(hipMemcpyAsync(P.smp.p, samples + sl0[d], sln[d] * 8, hipMemcpyHostToDevice, G->xs[d]),
                   "hipMemcpyAsync (list slice)");
-    unsigned long long* own = P.tot.p ? (unsigned long long*)P.tot.p + (size_t)gd * nb : nullptr;
+    // (P.tot is allocated with the group: every rank takes part in the gather below)
+    unsigned long long* own = (unsigned long long*)P.tot.p + (size_t)gd * nb;
     if (!rc)
       rc = faith_part_count(shard(G, d, 0), (const uint64_t*)P.smp.p, sln[d], (const unsigned long long*)P.bounds.p,
                             (uint32_t)S, (uint32_t*)P.hist.p, nblk[d], own, G->xs[d]);
     if (rc) {
       E.note(rc);
-      if (!own) return rc;  // (no buffer to take part in the gather with: nothing else to do)
       E.note(hip_rc(hipMemsetAsync(own, 0xFF, (size_t)nb * 8, G->xs[d]), "hipMemsetAsync"));
     }
   }
@@ -762,7 +804,17 @@ static int group_any_order(pluss_group* G, const uint64_t* samples, uint64_t n, 
       E.note(part_buf(G, d, P.fin, rtot[d] * wb));
       E.note(part_buf(G, d, P.seg, (size_t)R * spd * 6 * 3 * 8));
     }
-    if (E.rc) return E.rc;  // (allocation failures here are on every rank alike only by chance: reported, not hung)
+    // a failure since the totals' gather (a buffer, the placement) may be this
+    // rank's alone: every rank learns of it before the send / receive, and all
+    // of them skip the exchange together (the shards then fail their rows)
+    bool any = false;
+    if (int rc = agree_failed(G, E.rc != 0, &any)) return rc;
+    if (any) {
+      E.note(PLUSS_ERR_PEER, "a rank failed before the any-order exchange");
+      failed = true;
+    }
+  }
+  if (R > 1 && !failed) {
     PLUSS_NCCL_CHECK(g_rccl.GroupStart());
     for (int d = 0; d < G->ndev; ++d) {
       PartBufs& P = G->part[d];
@@ -789,7 +841,7 @@ static int group_any_order(pluss_group* G, const uint64_t* samples, uint64_t n, 
     for (int d = 0; d < G->ndev; ++d) {
       PartBufs& P = G->part[d];
       const int gd = G->rank0 + d;
-      PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
+      E.note(hip_rc(hipSetDevice(G->dev[d]), "hipSetDevice"));
       uint64_t o = 0;
       for (int x = 0; x < spd * 6; ++x) {
         foff[d][x] = o;
@@ -814,11 +866,15 @@ static int group_any_order(pluss_group* G, const uint64_t* samples, uint64_t n, 
         roff += before_e;
       }
       const uint32_t nseg = (uint32_t)(P.h_seg.size() / 3);
+      // (a failure here stays local: fin[d] is left null, this device's shards
+      // fail their rows and every rank still takes part in the phases' gathers)
+      int rc = PLUSS_OK;
       if (nseg)
-        PLUSS_HIP_CHECK(hipMemcpyAsync(P.seg.p, P.h_seg.data(), P.h_seg.size() * 8, hipMemcpyHostToDevice, G->xs[d]));
-      if (int rc = faith_seg_copy((const unsigned long long*)P.seg.p, nseg, maxn, P.recv.p, P.fin.p, wb, G->xs[d]))
-        return rc;
-      fin[d] = (const unsigned char*)P.fin.p;
+        rc = hip_rc(hipMemcpyAsync(P.seg.p, P.h_seg.data(), P.h_seg.size() * 8, hipMemcpyHostToDevice, G->xs[d]),
+                    "hipMemcpyAsync (segments)");
+      if (!rc) rc = faith_seg_copy((const unsigned long long*)P.seg.p, nseg, maxn, P.recv.p, P.fin.p, wb, G->xs[d]);
+      E.note(rc);
+      if (!rc) fin[d] = (const unsigned char*)P.fin.p;
     }
   }
   if (int rc = fork_shards(G)) return rc;  // (every shard's sort after its device's words)
@@ -1040,10 +1096,16 @@ int pluss_group_dense(pluss_group* G, uint32_t passes, uint64_t counts[PLUSS_DEN
     PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
     PLUSS_HIP_CHECK(hipMemsetAsync(G->vec[d], 0, (size_t)(G->spd + 1) * DVEC * 8, G->xs[d]));
   }
+  if (passes == 0) {  // nothing to run: the zero vector
+    if (counts)
+      for (int b = 0; b <= PLUSS_DENSE_BINS; ++b) counts[b] = 0;
+    return PLUSS_OK;
+  }
   constexpr uint32_t BATCH = 16;  // passes per captured graph
-  uint32_t left = passes ? passes : 1;
-  if (G->ndev == 1 && lists && left >= BATCH) {
-    // one local device: BATCH passes (kernels and RCCL all-reduces) replayed from one HIP graph
+  uint32_t left = passes;
+  if (G->ndev == 1 && G->nranks == 1 && lists && left >= BATCH) {
+    // one rank, one local device: BATCH passes replayed from one HIP graph
+    // (kernels and the shard sums; the all-reduce, the identity, left out)
     PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
     hipGraphExec_t ex = nullptr;
     auto it = G->graphs.find(BATCH);
@@ -1051,10 +1113,12 @@ int pluss_group_dense(pluss_group* G, uint32_t passes, uint64_t counts[PLUSS_DEN
       ex = it->second;
     } else {
       PLUSS_HIP_CHECK(hipStreamBeginCapture(G->xs[0], hipStreamCaptureModeThreadLocal));
+      G->capturing = true;
       int rc = PLUSS_OK;
       for (uint32_t k = 0; k < BATCH && !rc; ++k) rc = dense_pass_on_xs(G, E);
       hipGraph_t gr = nullptr;
       const hipError_t e = hipStreamEndCapture(G->xs[0], &gr);
+      G->capturing = false;
       if (rc || E.rc) {
         if (gr) (void)hipGraphDestroy(gr);
         return rc ? rc : E.rc;  // (host-side failures while capturing: nothing was launched)
@@ -1189,7 +1253,7 @@ int pluss_group_gen_faithful(pluss_group* G, uint64_t seed, const uint64_t total
   if (!G->fg) G->fg = new FaGraph();
   FaGraph& F = *G->fg;
   const bool same = F.seen && F.src == 0 && F.seed == seed && std::memcmp(F.totals, totals, sizeof F.totals) == 0;
-  if (G->ndev == 1 && same && F.have) {  // the captured pass, replayed
+  if (G->ndev == 1 && G->nranks == 1 && same && F.have) {  // the captured pass, replayed
     PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
     PLUSS_HIP_CHECK(hipGraphLaunch(F.ex, G->xs[0]));
     GErr E;
@@ -1202,8 +1266,10 @@ int pluss_group_gen_faithful(pluss_group* G, uint64_t seed, const uint64_t total
   F.src = 0;
   F.seed = seed;
   std::memcpy(F.totals, totals, sizeof F.totals);
-  // a second identical call is captured (the first ran eagerly and grew every buffer)
-  const bool capture = G->ndev == 1 && same && G->m.fast;
+  // a second identical call is captured (the first ran eagerly and grew every
+  // buffer); one-rank groups only, without their identity collectives (the
+  // capture rule at pluss_group::capturing)
+  const bool capture = G->ndev == 1 && G->nranks == 1 && same && G->m.fast;
   if (capture) {
     PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
     PLUSS_HIP_CHECK(hipStreamBeginCapture(G->xs[0], hipStreamCaptureModeThreadLocal));

@@ -214,6 +214,43 @@ def test_group_any_order_equals_one_device(N, total, spd):
 
 
 @pytest.mark.gpu
+def test_group_any_order_config3_equals_one_device():
+    """BASELINE config 3's any-order list (N=4096, T=8, 2^28 Feistel samples)
+    through the group at 1, 2 and 8 logical shards, two calls each on one
+    group (the second on grown buffers: the sequence that faulted in r5p):
+    every call equals the one-device radix pass.  The group's word sorts take
+    the same count-free levels and 4-byte payloads as that pass (at one shard
+    their level-1 buckets fit; at 2 and 8 a shard's words fill a fraction of
+    the word range and the counted level-1 fallback runs)."""
+    P = _P()
+    import torch
+    N, T = 4096, 8
+    c = P.SamplerConfig(n=N, threads=T, mode="faithful")
+    totals = P.default_counts(N, 1 << 28)
+    st = torch.cuda.Stream()
+    host = torch.empty(sum(totals), dtype=torch.int64, pin_memory=True)
+    d = torch.empty(sum(totals), dtype=torch.int64, device="cuda")
+    with P.Context(c) as ctx:
+        off = 0
+        for r, n in enumerate(totals):
+            ctx.expand(0x5EED0001, r, 0, n, d.data_ptr() + 8 * off, st.cuda_stream)
+            off += n
+        ctx.reset(st.cuda_stream)
+        ctx.faithful_hist_refs(d.data_ptr(), totals, st.cuda_stream)
+        st.synchronize()
+        one = ctx.fetch()
+    host.copy_(d)
+    del d
+    lst = host.numpy().view(np.uint64)
+    assert sum(one.bins.values()) > 0.5 * sum(totals)
+    for spd in (1, 2, 8):
+        with P.Group(c, [0], spd) as g:
+            for call in range(2):
+                h = g.sampled_hist(lst)
+                assert h.bins == one.bins and list(h.traversed) == list(one.traversed), (spd, call)
+
+
+@pytest.mark.gpu
 def test_group_pairs_shape_and_errors(orc):
     """A shape with N % (cls/ds) != 0 ((key, sink) pairs, not key-range
     sharded: the job's first shard runs the samplers) equals one device; a
