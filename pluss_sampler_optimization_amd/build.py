@@ -40,35 +40,54 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose=False, force=False):
-    os.makedirs(OBJDIR, exist_ok=True)
+def build(verbose=False, force=False, variant=None):
+    """variant "stages": the diagnostic build (-DPLUSS_DEBUG_STAGES: each named
+    stage drains its stream and prints its outcome) into lib/stages/, for
+    tools that load it explicitly; never the product library."""
+    if variant == "stages":
+        return _build_gpu(os.path.join(LIBDIR, "stages", "obj"), os.path.join(LIBDIR, "stages", "libpluss_gpu.so"),
+                          ["-DPLUSS_DEBUG_STAGES"], verbose, force)
+    lib = _build_gpu(OBJDIR, LIB, [], verbose, force)
+    _build_host(verbose, force)
+    return lib
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def _build_gpu(objdir, libpath, extra, verbose, force):
+    os.makedirs(objdir, exist_ok=True)
     hipcc = _hipcc()
     inc = os.path.join(HERE, "..", "include")
     common_deps = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(inc, "pluss_gpu.h"),
                                                               os.path.join(inc, "pluss_diag.h"), __file__]
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", inc, "-I", CSRC,
-             "-Wall", "-Wno-unused-result"]
+             "-Wall", "-Wno-unused-result", *extra]
     jobs = []
     objs = []
     for src in SOURCES:
         s = os.path.join(CSRC, src)
-        o = os.path.join(OBJDIR, src.replace(".hip", ".o"))
+        o = os.path.join(objdir, src.replace(".hip", ".o"))
         objs.append(o)
         if force or _stale(o, [s] + common_deps):
             jobs.append([hipcc, *flags, "-c", s, "-o", o])
 
-    def run(cmd):
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-        return r
-
     with ThreadPoolExecutor(max_workers=len(jobs) or 1) as ex:
-        list(ex.map(run, jobs))
-    if force or jobs or _stale(LIB, objs):
-        run([hipcc, "-shared", f"--offload-arch={ARCH}", "-o", LIB, *objs])
+        list(ex.map(lambda c: _run(c, verbose), jobs))
+    if force or jobs or _stale(libpath, objs):
+        _run([hipcc, "-shared", f"--offload-arch={ARCH}", "-o", libpath, *objs], verbose)
+    return libpath
+
+
+def _build_host(verbose, force):
+    inc = os.path.join(HERE, "..", "include")
+    run = lambda c: _run(c, verbose)  # noqa: E731
     # host half of the pipeline (CRI / AET / formats): plain C++, no HIP
     hsrc = [os.path.join(CSRC, h) for h in HOST_SOURCES]
     if force or _stale(HOST_LIB, hsrc + [os.path.join(inc, "pluss_host.h"), os.path.join(inc, "pluss_gpu.h")]):
@@ -79,8 +98,7 @@ def build(verbose=False, force=False):
     if force or _stale(CLI, [csrc_cli, LIB, HOST_LIB]):
         run([os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", "-I", inc, "-o", CLI, csrc_cli,
              "-L", LIBDIR, "-lpluss_gpu", "-lpluss_host", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath,/opt/rocm/lib"])
-    return LIB
 
 
 if __name__ == "__main__":
-    print(build(verbose=True, force="--force" in sys.argv))
+    print(build(verbose=True, force="--force" in sys.argv, variant="stages" if "--stages" in sys.argv else None))

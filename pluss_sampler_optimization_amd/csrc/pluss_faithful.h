@@ -2099,8 +2099,10 @@ inline void fa_launch_t(const FaLaunch& L) {
         else
           hipLaunchKernelGGL((k_fa_local_fast<SRC, CHK>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart,
                              b.klist, b.fslot, b.slowq, L.g);
+        PLUSS_STAGE(L.s, "pipeline: local fast pass");
         hipLaunchKernelGGL((k_fa_local<SRC, P2, CHK, true>), dim3(nres), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart,
                            b.klist, b.fslot, b.slowq, L.g);
+        PLUSS_STAGE(L.s, "pipeline: queued pass");
         fast = true;
       }
     }
@@ -2118,6 +2120,7 @@ inline void fa_launch_t(const FaLaunch& L) {
   if (ph == FA_PH_ALL || ph == FA_PH_CHUNK)
     hipLaunchKernelGGL((k_fa_chunk<SRC, P2>), dim3((unsigned)L.a.coff[6]), dim3(CH), 0, L.s, L.m, L.a, b.tmax,
                        b.pmin, b.dpart, b.klist, b.cval, b.cflag, b.crec, L.epoch, b.slowq, L.g);
+  if (ph == FA_PH_ALL || ph == FA_PH_CHUNK) PLUSS_STAGE(L.s, "pipeline: chunks");
   if (ph == FA_PH_ALL)
     hipLaunchKernelGGL((k_fa_finish<SRC, P2, false>), dim3(6), dim3(CH), 0, L.s, L.m, L.a, b.tmax, b.pmin, b.dpart,
                        b.crec, b.fslot, b.shrec, (unsigned long long*)nullptr, L.g);

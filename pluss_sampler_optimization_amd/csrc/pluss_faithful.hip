@@ -654,6 +654,7 @@ static int srt_launch(pluss_ctx* ctx, FaithfulBufs& b, const SrtPlan& P, PT* X1,
       hipLaunchKernelGGL((k_srt_scatter1f<KT, SMP, false>), dim3(g1 * SPL), dim3(SB1), 0, s, m, P.a,
                          (const uint32_t*)cap, (const uint32_t*)off1, fill, ovf, (uint32_t*)X1, ctx->g);
     hipLaunchKernelGGL(k_srt_gate, dim3(1), dim3(1), 0, s, (const uint32_t*)ovf, (uint32_t)P.h1, gate, glen);
+    PLUSS_STAGE(s, "sort: level 1, count-free");
   }
   const uint32_t* gt = fast ? gate : nullptr;
   if (p2)
@@ -667,24 +668,30 @@ static int srt_launch(pluss_ctx* ctx, FaithfulBufs& b, const SrtPlan& P, PT* X1,
   else
     hipLaunchKernelGGL((k_srt_scatter1<KT, PT, SMP, false>), dim3(g1), dim3(SB), 0, s, m, P.a, (const uint32_t*)h1,
                        X1, ctx->g, gt);
+  PLUSS_STAGE(s, "sort: level 1, counted");
   if (!fast) l2.fill = nullptr;  // (the counted level 2, ungated)
   hipLaunchKernelGGL(k_srt_plan, dim3(1), dim3(SB), 0, s, P.a, (const uint32_t*)h1, par, cmap, tot,
                      fast ? (const uint32_t*)fill : nullptr, (const uint32_t*)off1, (const uint32_t*)ovf, l2);
+  PLUSS_STAGE(s, "sort: plan");
   if (fast) {  // level 2 without a count (unless level 1 overflowed), then the counted one gated on an overflow
     hipLaunchKernelGGL(k_srt_scatter2f<PT>, dim3((unsigned)P.g2max * SPL), dim3(SB1), 0, s, P.a,
                        (const SrtParent*)par, (const uint32_t*)cmap, (const uint32_t*)tot, (const PT*)X1, Y, l2);
     hipLaunchKernelGGL(k_srt_gate2, dim3(1), dim3(1), 0, s, (const uint32_t*)l2.ovf, (const uint32_t*)(tot + 1),
                        l2.gate, l2.glen);
   }
+  PLUSS_STAGE(s, "sort: level 2, count-free");
   const uint32_t* gt2 = fast ? (const uint32_t*)l2.gate : nullptr;
   hipLaunchKernelGGL(k_srt_count2<PT>, dim3((unsigned)P.g2max), dim3(SB), 0, s, P.a, (const SrtParent*)par,
                      (const uint32_t*)cmap, (const uint32_t*)tot, (const PT*)X1, h2, gt2);
   srt_scan(h2, P.h2max, fast ? (const uint32_t*)l2.glen : tot + 1, bs, s);
   hipLaunchKernelGGL(k_srt_scatter2<PT>, dim3((unsigned)P.g2max), dim3(SB), 0, s, P.a, (const SrtParent*)par,
                      (const uint32_t*)cmap, (const uint32_t*)tot, (const uint32_t*)h2, (const PT*)X1, Y, gt2);
+  PLUSS_STAGE(s, "sort: level 2, counted");
   hipLaunchKernelGGL((k_srt_final<PT, OT, PFX>), dim3(FG, P.a.np), dim3(SB), 0, s, P.a, (const SrtParent*)par,
                      (const uint32_t*)h2, (const PT*)X1, (const PT*)Y, out, dp, l2);
+  PLUSS_STAGE(s, "sort: final");
   hipLaunchKernelGGL((k_srt_deep<PT, OT, PFX>), dim3(64), dim3(SB), 0, s, P.a, (const SrtParent*)par, X1, Y, out, dp);
+  PLUSS_STAGE(s, "sort: deep");
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }
@@ -1157,6 +1164,7 @@ static int shards_phase1(pluss_ctx* ctx, FaShards& f, uint64_t* d_row, hipStream
   hipLaunchKernelGGL(k_fa_shard_sums<0>, dim3(6), dim3(SS_NT), 0, s, f.L.a, b.tmax, b.crec, (unsigned long long*)d_row,
                      0);
   PLUSS_HIP_CHECK(hipGetLastError());
+  PLUSS_STAGE(s, "shard phase 1 (local)");
   f.phase = SH_LOCAL;
   f.has_slice = true;
   return PLUSS_OK;
@@ -1625,6 +1633,7 @@ int faith_shards_carry(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, in
   hipLaunchKernelGGL(k_fa_shard_sums<0>, dim3(6), dim3(SS_NT), 0, s, f.L.a, b.tmax, b.crec, (unsigned long long*)d_row,
                      1);
   PLUSS_HIP_CHECK(hipGetLastError());
+  PLUSS_STAGE(s, "shard phase 2 (carry)");
   f.phase = SH_CARRY;
   return PLUSS_OK;
 }
@@ -1644,6 +1653,7 @@ int faith_shards_cut(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int3
     if (int rc = fa_launch(ctx, f.L, f.src, FA_PH_CUT)) return rc;
   }
   PLUSS_HIP_CHECK(hipGetLastError());
+  PLUSS_STAGE(s, "shard phase 3 (cut)");
   f.phase = SH_CUT;
   return PLUSS_OK;
 }
@@ -1659,6 +1669,7 @@ int faith_shards_hist(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int
     hipLaunchKernelGGL(k_fa_shard_apply<0>, dim3(1), dim3(64), 0, s, f.L.m, f.L.a, b.shrec,
                        (const unsigned long long*)b.xin, b.fslot, f.L.g);
   PLUSS_HIP_CHECK(hipGetLastError());
+  PLUSS_STAGE(s, "shard phase 4 (hist)");
   ctx->tables_dirty = true;
   return PLUSS_OK;
 }

@@ -627,6 +627,7 @@ static int collect_enqueue(pluss_group* G, GErr& E) {
     }
     E.note(hip_rc(hipGetLastError(), "k_group_vec"));
   }
+  PLUSS_STAGE(G->ctx[0]->stream, "collect: shard slots");
   return dense_merge(G);
 }
 
@@ -741,6 +742,7 @@ static int group_any_order(pluss_group* G, const uint64_t* samples, uint64_t n, 
       E.note(hip_rc(hipMemsetAsync(own, 0xFF, (size_t)nb * 8, G->xs[d]), "hipMemsetAsync"));
     }
   }
+  PLUSS_STAGE(G->xs[0], "any-order: slice upload and partition count");
   std::vector<unsigned long long*> tots(G->ndev);
   for (int d = 0; d < G->ndev; ++d) tots[d] = (unsigned long long*)G->part[d].tot.p;
   if (int rc = gather_blocks(G, tots, (size_t)6 * R)) return rc;
@@ -877,6 +879,7 @@ static int group_any_order(pluss_group* G, const uint64_t* samples, uint64_t n, 
       if (!rc) fin[d] = (const unsigned char*)P.fin.p;
     }
   }
+  PLUSS_STAGE(G->xs[0], "any-order: placement and exchange");
   if (int rc = fork_shards(G)) return rc;  // (every shard's sort after its device's words)
   ShardFn loc = [&](pluss_ctx* c, int d, int j, int g, uint64_t* row) -> int {
     if (failed || !fin[d]) {

@@ -140,6 +140,17 @@ void set_error(const std::string& msg);
     }                                                                                                    \
   } while (0)
 
+// Diagnostic builds only (-DPLUSS_DEBUG_STAGES, build.py variant "stages", never
+// the product library): after each named stage the stream is drained and the
+// stage's outcome printed to stderr, so a device fault is pinned to the first
+// stage that reports it.  Compiles to nothing in the product build.
+#ifdef PLUSS_DEBUG_STAGES
+void debug_stage(hipStream_t s, const char* what);
+#define PLUSS_STAGE(s, what) ::pluss::debug_stage((s), (what))
+#else
+#define PLUSS_STAGE(s, what) ((void)0)
+#endif
+
 int validate_cfg(const pluss_cfg* cfg, Model* m);
 // the error reported by a pass's flags (flags[0] bits, flags[1] malformed input), or PLUSS_OK
 int flags_error(unsigned int f0, unsigned int bad, const std::string& who);

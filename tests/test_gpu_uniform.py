@@ -147,6 +147,74 @@ def test_uniform_source_vs_oracle_at_baseline_n(orc, N):
         assert 0.3 * totals[P.REF_ID[ref]] < rec < 0.8 * totals[P.REF_ID[ref]]
 
 
+def _oracle_all(orc, oc, seed, totals):
+    """orc_faithful over the oracle's own uniform lists of every reference,
+    the six replays on host threads at once (ctypes drops the GIL): {ref:
+    (histogram, traversed)}."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def one(ref, n):
+        return ref, orc.faithful(oc, ref, orc.expand_uniform(oc, seed, ref, n, 0, n))
+    with ThreadPoolExecutor(6) as ex:
+        futs = [ex.submit(one, ref, totals[r]) for r, ref in enumerate(P.REFS) if totals[r]]
+        return dict(f.result() for f in futs)
+
+
+def _b0_edges(N, T, s):
+    """(cross-row reuses c1 % 8 == 7, cold: those in a thread's last row,
+    first-row samples, last-row samples) of packed B0 samples."""
+    m = np.uint64(0xFFFFF)
+    c0 = ((s >> np.uint64(40)) & m).astype(np.int64)
+    c1 = ((s >> np.uint64(20)) & m).astype(np.int64)
+    q = (c0 // (4 * T)) * 4 + c0 % 4
+    cross = c1 % 8 == 7
+    last = q == N // T - 1
+    return int(cross.sum()), int((cross & last).sum()), int((q == 0).sum()), int(last.sum())
+
+
+# r10's law with B0 in the pass at the BASELINE shapes' N: seeds picked (on the
+# CPU, over the oracle's own lists) so B0's few samples hold cross-row share
+# reuses (c1 % 8 == 7, RI R - 7S), one cold sample in a thread's last row, and
+# samples of the first and last thread-local rows; each cross-row or cold B0
+# sample is one replay of (N - 7)(4N + 2) lockstep steps per thread in the
+# oracle, so B0 stays small while C0 / C1 are dense enough for Q1 to cut them
+# inside the list.  (N, T, seed, totals, B0 edges expected)
+B0_LAW = [(4096, 8, 2066, [8_000_000, 8_000_000, 3_000, 48, 1_000_000, 1_000_000], (5, 1, 1, 1)),
+          (2048, 64, 10, [2_000_000, 2_000_000, 5_000, 24, 1_000_000, 1_000_000], (2, 1, 2, 2))]
+
+
+@pytest.mark.parametrize("N,T,seed,totals,edges", B0_LAW)
+def test_uniform_b0_share_and_cold_at_baseline_n(orc, N, T, seed, totals, edges):
+    """Config 3's N (4096, T=8) and config 4's shape (2048, T=64): the faithful
+    pass over r10's law generated inside the pipeline, B0 included (the share
+    split r10:2482-2486, cross-row reuses, cold samples of a thread's last
+    row: r10:2221-2636), through one GPU and through a group of 5 logical
+    key-range shards: equal to the stepping r10 oracle replaying the oracle's
+    own lists; Q1 cuts C0 / C1 inside the list."""
+    c = P.SamplerConfig(n=N, threads=T, mode="faithful")
+    oc = orc.cfg(N, T)
+    assert _b0_edges(N, T, orc.expand_uniform(oc, seed, "B0", totals[3], 0, totals[3])) == edges
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(1) as ex:
+        fut = ex.submit(_oracle_all, orc, oc, seed, totals)  # (the replays run while the GPU works)
+        with P.Context(c) as ctx:
+            ctx.reset(stream())
+            ctx.gen_uniform_faithful_refs(seed, totals, stream())
+            one = ctx.fetch()
+        with P.Group(c, [0], 5) as g:
+            grp = g.gen_uniform_faithful(seed, totals)
+        want = fut.result()
+    assert grp.bins == one.bins and grp.traversed == one.traversed
+    for r, ref in enumerate(P.REFS):
+        wbins, wtrav = want[ref]
+        assert {k: v for k, v in one.bins.items() if k[0] == ref} == wbins, (N, ref)
+        assert one.traversed[r] == wtrav, (N, ref)
+    assert any(k[0] == "B0" and k[1] == 1 for k in one.bins)  # the share split (cross-row reuses)
+    for ref in ("C0", "C1"):  # Q1 cut inside the list
+        rec = sum(v for k, v in one.bins.items() if k[0] == ref and k[2] != -1)
+        assert 0.3 * totals[P.REF_ID[ref]] < rec < 0.8 * totals[P.REF_ID[ref]]
+
+
 def test_uniform_key_range_shards_by_hand(orc):
     """The uniform source's shard phases (uniform_count, gather,
     uniform_local, carry, cut, hist) run by hand over 6 handles on one GPU at
