@@ -46,8 +46,8 @@ def build(verbose=False, force=False, variant=None):
     tools that load it explicitly; never the product library."""
     if variant == "stages":
         return _build_gpu(os.path.join(LIBDIR, "stages", "obj"), os.path.join(LIBDIR, "stages", "libpluss_gpu.so"),
-                          ["-DPLUSS_DEBUG_STAGES"], verbose, force)
-    lib = _build_gpu(OBJDIR, LIB, [], verbose, force)
+                          ["-DPLUSS_DEBUG_STAGES"], verbose, force, SOURCES + ["diag/pluss_stages.hip"])
+    lib = _build_gpu(OBJDIR, LIB, [], verbose, force, SOURCES)
     _build_host(verbose, force)
     return lib
 
@@ -61,7 +61,7 @@ def _run(cmd, verbose):
     return r
 
 
-def _build_gpu(objdir, libpath, extra, verbose, force):
+def _build_gpu(objdir, libpath, extra, verbose, force, sources):
     os.makedirs(objdir, exist_ok=True)
     hipcc = _hipcc()
     inc = os.path.join(HERE, "..", "include")
@@ -71,9 +71,9 @@ def _build_gpu(objdir, libpath, extra, verbose, force):
              "-Wall", "-Wno-unused-result", *extra]
     jobs = []
     objs = []
-    for src in SOURCES:
+    for src in sources:
         s = os.path.join(CSRC, src)
-        o = os.path.join(objdir, src.replace(".hip", ".o"))
+        o = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
         objs.append(o)
         if force or _stale(o, [s] + common_deps):
             jobs.append([hipcc, *flags, "-c", s, "-o", o])

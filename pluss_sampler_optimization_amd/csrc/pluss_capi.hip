@@ -7,7 +7,6 @@
 // every entry point returns PLUSS_ERR_HIP.
 #include <hip/hip_runtime.h>
 
-#include <cstdio>
 
 #include <algorithm>
 #include <cstring>
@@ -22,15 +21,6 @@ namespace pluss {
 
 static thread_local std::string g_err;
 
-#ifdef PLUSS_DEBUG_STAGES
-void debug_stage(hipStream_t s, const char* what) {
-  static unsigned long long seq = 0;
-  hipError_t e = hipStreamSynchronize(s);
-  if (e == hipSuccess) e = hipPeekAtLastError();
-  std::fprintf(stderr, "[stage %llu] %s: %s\n", ++seq, what, e == hipSuccess ? "ok" : hipGetErrorString(e));
-  std::fflush(stderr);
-}
-#endif
 void set_error(const std::string& msg) { g_err = msg; }
 
 int validate_cfg(const pluss_cfg* c, Model* m) {

@@ -404,7 +404,11 @@ __device__ __forceinline__ unsigned long long w32p_word(const FaOne& o, const W3
 // generated lists: each thread generates its run (keyrunf_* when the whole
 // tile lies in block A with small strata -- tile-uniform -- else one direct
 // decode per sample).
-template <int SRC, bool P2, uint32_t REF, int NT, int EPT, bool FULLT>
+// (RANGE8: SRC_W32P tiles over three to nine parents take the parents' starts
+// in registers -- the queued pass; the chunk and finish passes' rare rescans
+// look each element's parent up, which keeps their registers below the
+// point where the compiler reserved a scratch slot in them)
+template <int SRC, bool P2, uint32_t REF, int NT, int EPT, bool FULLT, bool RANGE8 = true>
 __device__ __forceinline__ void fa_load_run(const Model& m, const FaOne& o, const KeyGen& kg, FaLds<SRC, NT, EPT>& sh,
                                             unsigned long long (&key)[EPT], uint32_t& cases, uint32_t& t0s,
                                             bool& bad) {
@@ -427,7 +431,7 @@ __device__ __forceinline__ void fa_load_run(const Model& m, const FaOne& o, cons
       if constexpr (SRC == SRC_W32P) {  // the payloads' parent digits put back
         const W32P pw = w32p_tile(o, T.base, T.mt);
         const uint32_t b0 = (uint32_t)(pw.pa >> o.phi), b1 = (uint32_t)(pw.pb >> o.phi);
-        if (pw.ok || b1 - b0 > 8u) {
+        if (!RANGE8 || pw.ok || b1 - b0 > 8u) {
 #pragma unroll
           for (int k = 0; k < EPT; ++k) {
             const uint32_t e = (uint32_t)k * NT + threadIdx.x;
@@ -1724,10 +1728,10 @@ __global__ __launch_bounds__(CH) void k_fa_chunk(Model m, FaRefs a, const unsign
   const unsigned long long cin = pmin[T.gt];                                                                \
   fa_rt(m, o.pv, sh);                                                                                       \
   if (T.mt == TILE) {                                                                                       \
-    fa_load_run<SRC, P2, R, TB, TI, true>(m, o, kg, sh, key, cases, t0s, bad);                              \
+    fa_load_run<SRC, P2, R, TB, TI, true, false>(m, o, kg, sh, key, cases, t0s, bad);                              \
     fa_scan<FA_FULL, SRC, TB, TI, true>(m, o, key, cases, t0s, cin, 0, sh, nullptr);                        \
   } else {                                                                                                  \
-    fa_load_run<SRC, P2, R, TB, TI, false>(m, o, kg, sh, key, cases, t0s, bad);                             \
+    fa_load_run<SRC, P2, R, TB, TI, false, false>(m, o, kg, sh, key, cases, t0s, bad);                             \
     fa_scan<FA_FULL, SRC, TB, TI, false>(m, o, key, cases, t0s, cin, 0, sh, nullptr);                       \
   }
     __threadfence_block();  // pmin of the tile (written above) is read by every thread
@@ -1888,10 +1892,10 @@ __global__ __launch_bounds__(CH) void k_fa_finish(Model m, FaRefs a, const unsig
   bool bad = false;                                                                                         \
   fa_rt(m, o.pv, sh);                                                                                       \
   if (T.mt == TILE) {                                                                                       \
-    fa_load_run<SRC, P2, R, TB, TI, true>(m, o, kg, sh, key, cases, t0s, bad);                              \
+    fa_load_run<SRC, P2, R, TB, TI, true, false>(m, o, kg, sh, key, cases, t0s, bad);                              \
     fa_scan<FA_CUT, SRC, TB, TI, true>(m, o, key, cases, t0s, carry, cin, sh, nullptr);                     \
   } else {                                                                                                  \
-    fa_load_run<SRC, P2, R, TB, TI, false>(m, o, kg, sh, key, cases, t0s, bad);                             \
+    fa_load_run<SRC, P2, R, TB, TI, false, false>(m, o, kg, sh, key, cases, t0s, bad);                             \
     fa_scan<FA_CUT, SRC, TB, TI, false>(m, o, key, cases, t0s, carry, cin, sh, nullptr);                    \
   }
     fa_uni_pre<SRC>(a, T, sh);

@@ -236,12 +236,13 @@ struct pluss_group {
   std::vector<pluss::PartBufs> part;      // per device: the any-order faithful pass
   std::map<uint32_t, hipGraphExec_t> graphs;  // dense passes captured per batch size (one local device)
   pluss::FaGraph* fg = nullptr;               // the last faithful pass, captured (pluss_group_gen_faithful)
-  // A pass being captured into a HIP graph.  The capture rule (one for every
-  // rank count): a captured graph never holds an RCCL call.  Only one-rank
-  // groups capture, and there every collective is the identity (each shard
-  // writes its block of the one buffer), so it is left out; groups of several
-  // ranks run every pass eagerly.  (r5m: a host segfault while replaying a
-  // pass whose capture held RCCL calls)
+  // A pass being captured into a HIP graph.  The rule, one for every rank
+  // count: a one-rank group makes no RCCL call at all (every collective is
+  // the identity there: each shard writes its block of the one buffer), so
+  // its captured passes hold none; groups of several ranks never capture and
+  // run every pass eagerly.  (r5m: a host segfault while replaying a pass
+  // whose capture held RCCL calls; r5p: a device fault in back-to-back
+  // one-rank passes)
   bool capturing = false;
   std::vector<unsigned long long*> agr;       // per device: a failure word summed over the ranks (agree_failed)
 };
@@ -355,15 +356,16 @@ static int fork_shards(pluss_group* G) {
 // (each device holds every shard's slot; its own shards' slots are written)
 static int gather_blocks(pluss_group* G, std::vector<unsigned long long*>& buf, size_t w) {
   if (int rc = join_shards(G)) return rc;
-  // (a captured pass is a one-rank pass: the all-gather is the identity, left
-  // out -- the capture rule at pluss_group::capturing)
-  if (G->capturing) return fork_shards(G);
+  // (one rank: every shard wrote its block of the one buffer, the all-gather
+  // is the identity and is left out -- the rule at pluss_group::capturing)
+  if (G->nranks == 1) return fork_shards(G);
   PLUSS_NCCL_CHECK(g_rccl.GroupStart());
   for (int d = 0; d < G->ndev; ++d) {
     unsigned long long* own = buf[d] + (size_t)(G->rank0 + d) * G->spd * w;
     PLUSS_NCCL_CHECK(g_rccl.AllGather(own, buf[d], (size_t)G->spd * w, ncclUint64, G->comm[d], G->xs[d]));
   }
   PLUSS_NCCL_CHECK(g_rccl.GroupEnd());
+  PLUSS_STAGE(G->xs[0], "group: all-gather");
   return fork_shards(G);
 }
 
@@ -514,13 +516,14 @@ static int dense_merge(pluss_group* G) {
                        G->vec[d] + (size_t)G->spd * DVEC);
   }
   PLUSS_HIP_CHECK(hipGetLastError());
-  if (G->capturing) return fork_shards(G);  // (one rank: the all-reduce is the identity)
+  if (G->nranks == 1) return fork_shards(G);  // (one rank: the all-reduce is the identity)
   PLUSS_NCCL_CHECK(g_rccl.GroupStart());
   for (int d = 0; d < G->ndev; ++d) {
     unsigned long long* v = G->vec[d] + (size_t)G->spd * DVEC;
     PLUSS_NCCL_CHECK(g_rccl.AllReduce(v, v, GV_W, ncclUint64, ncclSum, G->comm[d], G->xs[d]));
   }
   PLUSS_NCCL_CHECK(g_rccl.GroupEnd());
+  PLUSS_STAGE(G->xs[0], "group: dense all-reduce");
   return fork_shards(G);
 }
 
@@ -549,7 +552,7 @@ static int dense_pass_on_xs(pluss_group* G, GErr& E) {
                        G->vec[d] + (size_t)G->spd * DVEC);
   }
   PLUSS_HIP_CHECK(hipGetLastError());
-  if (G->capturing) return PLUSS_OK;  // (one rank, one device: the all-reduce is the identity)
+  if (G->nranks == 1) return PLUSS_OK;  // (one rank, one device: the all-reduce is the identity)
   PLUSS_NCCL_CHECK(g_rccl.GroupStart());
   for (int d = 0; d < G->ndev; ++d) {
     unsigned long long* v = G->vec[d] + (size_t)G->spd * DVEC;
@@ -712,6 +715,7 @@ static int group_any_order(pluss_group* G, const uint64_t* samples, uint64_t n, 
   std::vector<uint64_t> sl0(G->ndev), sln(G->ndev);
   std::vector<uint32_t> nblk(G->ndev);
   if (int rc = join_shards(G)) return rc;  // (the shards' table resets come first)
+  PLUSS_STAGE(G->xs[0], "any-order: start (after the table resets)");
   for (int d = 0; d < G->ndev; ++d) {
     E.note(hip_rc(hipSetDevice(G->dev[d]), "hipSetDevice"));
     PartBufs& P = G->part[d];

@@ -109,27 +109,28 @@ __device__ __forceinline__ uint32_t srt_ref_of_chunk(const SrtRefs& a, uint64_t 
   for (int x = 1; x < 6; ++x) r += c >= a.coff[x] ? 1u : 0u;
   return __builtin_amdgcn_readfirstlane(r);
 }
-// per-reference fields copied out by a switch (the kernel argument is never indexed dynamically)
+// per-reference fields copied out by selects on the (wave-uniform) reference:
+// the kernel argument is never indexed dynamically -- a switch here was
+// lowered to a private-memory copy of d1[] indexed by r, and no product
+// kernel may request scratch
 struct SrtOne {
   uint64_t n, eoff, c0, h0;
   uint32_t d1, nch;
   const void* in;
 };
 __device__ __forceinline__ SrtOne srt_one(const SrtRefs& a, uint32_t r) {
-  SrtOne o;
-#define PLUSS_SRT_ONE(R)                                                                           \
-  case R:                                                                                          \
-    o = SrtOne{a.n[R], a.eoff[R], a.coff[R], a.hoff[R], a.d1[R], (uint32_t)(a.coff[R + 1] - a.coff[R]), a.in[R]}; \
-    break;
-  switch (r) {
-    PLUSS_SRT_ONE(0)
-    PLUSS_SRT_ONE(1)
-    PLUSS_SRT_ONE(2)
-    PLUSS_SRT_ONE(3)
-    PLUSS_SRT_ONE(4)
-    default: o = SrtOne{a.n[5], a.eoff[5], a.coff[5], a.hoff[5], a.d1[5], (uint32_t)(a.coff[6] - a.coff[5]), a.in[5]};
+  SrtOne o{a.n[0], a.eoff[0], a.coff[0], a.hoff[0], a.d1[0], (uint32_t)(a.coff[1] - a.coff[0]), a.in[0]};
+#pragma unroll
+  for (uint32_t x = 1; x < 6; ++x) {
+    const bool h = r == x;
+    o.n = h ? a.n[x] : o.n;
+    o.eoff = h ? a.eoff[x] : o.eoff;
+    o.c0 = h ? a.coff[x] : o.c0;
+    o.h0 = h ? a.hoff[x] : o.h0;
+    o.d1 = h ? a.d1[x] : o.d1;
+    o.nch = h ? (uint32_t)(a.coff[x + 1] - a.coff[x]) : o.nch;
+    o.in = h ? a.in[x] : o.in;
   }
-#undef PLUSS_SRT_ONE
   return o;
 }
 

@@ -9,6 +9,9 @@ import sys
 import time
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+if os.environ.get("PLUSS_PROBE_LIB") == "stages":  # the stage-checked diagnostic build (tools/r5p_probe.py)
+    import pluss_sampler_optimization_amd._lib as L  # noqa: E402
+    L.LIB_PATH = os.path.join(os.path.dirname(L.LIB_PATH), "stages", "libpluss_gpu.so")
 import pluss_sampler_optimization_amd as P  # noqa: E402
 
 src = sys.argv[1] if len(sys.argv) > 1 else "generated"
