@@ -37,7 +37,6 @@
 #include <string>
 #include <type_traits>
 #include <vector>
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include "pluss_faithful.h"
 #include "pluss_sort.h"
@@ -501,23 +500,16 @@ static int faith_reserve(pluss_ctx* ctx, FaithfulBufs& b, uint64_t n, hipStream_
   return PLUSS_OK;
 }
 
+// scratch of the (key, sink) pair sort (shapes with N % (cls/ds) != 0; packed
+// words are sorted by the bucket sort below): the (digit, block) histogram and
+// its scan's block sums, in the sort scratch b.sbuf
+static uint64_t pair_blocks(uint64_t n) { return (n + PTILE - 1) / PTILE; }
+static size_t pair_hist_bytes(uint64_t n) { return ((size_t)256 * pair_blocks(n) * 4 + 255) & ~(size_t)255; }
+static int srt_reserve(FaithfulBufs& b, uint64_t bytes, hipStream_t s);
 static int faith_tmp(pluss_ctx* ctx, FaithfulBufs& b, uint64_t n, hipStream_t s) {
-  // rocPRIM temporary storage of the (key, sink) pair sort (shapes with
-  // N % (cls/ds) != 0); packed words are sorted by pluss_sort.h (none needed)
-  size_t need = 0;
-  PLUSS_HIP_CHECK(
-      rocprim::radix_sort_pairs(nullptr, need, b.keys, b.keys_s, b.sinks, b.sinks_s, n, 0, key_bits(ctx->m), s));
-  if (need > b.tmp_bytes) {
-    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
-    if (b.tmp) (void)hipFree(b.tmp);
-    b.tmp = nullptr;
-    if (hipMalloc(&b.tmp, need) != hipSuccess) {
-      set_error("hipMalloc failed for rocprim temporary storage");
-      return PLUSS_ERR_ALLOC;
-    }
-    b.tmp_bytes = need;
-  }
-  return PLUSS_OK;
+  (void)ctx;
+  const uint64_t h = 256 * pair_blocks(n), nbs = (h + SBATCH - 1) / SBATCH;
+  return srt_reserve(b, pair_hist_bytes(n) + 4 * nbs + 256, s);
 }
 
 // ---- the bucket sort of packed words (pluss_sort.h): the references' words,
@@ -772,12 +764,32 @@ static int faith_keys(pluss_ctx* ctx, FaithfulBufs& b, int32_t ref, const uint64
   return PLUSS_OK;
 }
 
-// sort n (key, sink) pairs by key (k_faith_scan takes the prefix max of sinks)
+// sort n (key, sink) pairs by key: b.keys / b.sinks -> b.keys_s / b.sinks_s
+// (k_faith_scan takes the prefix max of sinks); the LSD pair sort of
+// pluss_sort.h over the keys' significant bits, ping-ponging between the two
+// buffer pairs
 static int faith_sort(pluss_ctx* ctx, FaithfulBufs& b, uint64_t n, hipStream_t s) {
+  if (n == 0) return PLUSS_OK;
   if (int rc = faith_tmp(ctx, b, n, s)) return rc;
-  size_t sz = b.tmp_bytes;
-  PLUSS_HIP_CHECK(
-      rocprim::radix_sort_pairs(b.tmp, sz, b.keys, b.keys_s, b.sinks, b.sinks_s, n, 0, key_bits(ctx->m), s));
+  const uint32_t nblk = (uint32_t)pair_blocks(n), passes = (key_bits(ctx->m) + 7) / 8;
+  uint32_t* hist = (uint32_t*)b.sbuf;
+  uint32_t* bsum = (uint32_t*)(b.sbuf + pair_hist_bytes(n));
+  unsigned long long *ki = b.keys, *vi = b.sinks, *ko = b.keys_s, *vo = b.sinks_s;
+  if (passes % 2 == 0) {  // (an even number of passes ends where it began: start from the other pair)
+    PLUSS_HIP_CHECK(hipMemcpyAsync(b.keys_s, b.keys, n * 8, hipMemcpyDeviceToDevice, s));
+    PLUSS_HIP_CHECK(hipMemcpyAsync(b.sinks_s, b.sinks, n * 8, hipMemcpyDeviceToDevice, s));
+    std::swap(ki, ko);
+    std::swap(vi, vo);
+  }
+  for (uint32_t p = 0; p < passes; ++p) {
+    hipLaunchKernelGGL(k_pair_count, dim3(nblk), dim3(PB), 0, s, (const unsigned long long*)ki, n, 8 * p, hist, nblk);
+    srt_scan(hist, (uint64_t)256 * nblk, nullptr, bsum, s);
+    hipLaunchKernelGGL(k_pair_scatter, dim3(nblk), dim3(PB), 0, s, (const unsigned long long*)ki,
+                       (const unsigned long long*)vi, n, 8 * p, (const uint32_t*)hist, nblk, ko, vo);
+    std::swap(ki, ko);
+    std::swap(vi, vo);
+  }
+  PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }
 

@@ -1215,4 +1215,126 @@ __global__ __launch_bounds__(SB) void k_srt_deep(const SrtRefs a, const SrtParen
   }
 }
 
+// ---- (key, value) pairs by key: shapes with N % (CLS/DS) != 0, whose sink is
+// not a function of a 2-bit case (pluss_faithful.hip faith_sort).  An LSD
+// radix sort by 8-bit digits, stable: per pass a per-block digit histogram
+// (k_pair_count), its exclusive scan over (digit, block) -- the scan kernels
+// above -- and k_pair_scatter: each block of PT pairs sorted by the digit in
+// LDS by eight stable one-bit splits (a block scan each), then written at its
+// digit's place.  The pairs ping-pong between two buffer pairs.  Only the
+// generic shapes take it (tests, small lists): simple, stable, no scratch.
+constexpr int PB = 256;                  // threads of the pair kernels
+constexpr int PE = 8;                    // pairs per thread (32 KB of LDS per block)
+constexpr uint32_t PTILE = PB * PE;      // pairs per block
+
+__global__ __launch_bounds__(PB) void k_pair_count(const unsigned long long* __restrict__ keys, uint64_t n,
+                                                   uint32_t sh, uint32_t* __restrict__ hist, uint32_t nblk) {
+  __shared__ uint32_t c[256];
+  c[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * PTILE;
+#pragma unroll
+  for (int k = 0; k < PE; ++k) {
+    const uint64_t i = base + (uint64_t)k * PB + threadIdx.x;
+    if (i < n) atomicAdd(&c[(uint32_t)(keys[i] >> sh) & 255u], 1u);
+  }
+  __syncthreads();
+  hist[(uint64_t)threadIdx.x * nblk + blockIdx.x] = c[threadIdx.x];
+}
+
+// exclusive scan of one value per thread over the block (PB threads)
+__device__ __forceinline__ uint32_t pair_block_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += y;
+  }
+  __syncthreads();  // (wsum reused)
+  if (lane == 63) wsum[wid] = inc;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int x = 0; x < PB / 64; ++x) {
+    pre += x < (int)wid ? wsum[x] : 0u;
+    tot += wsum[x];
+  }
+  total = tot;
+  return pre + inc - v;
+}
+
+__global__ __launch_bounds__(PB) void k_pair_scatter(const unsigned long long* __restrict__ kin,
+                                                     const unsigned long long* __restrict__ vin, uint64_t n,
+                                                     uint32_t sh, const uint32_t* __restrict__ hist, uint32_t nblk,
+                                                     unsigned long long* __restrict__ kout,
+                                                     unsigned long long* __restrict__ vout) {
+  __shared__ unsigned long long kk[PTILE], vv[PTILE];
+  __shared__ uint32_t c[256], gb[256], wsum[PB / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * PTILE;
+  const uint32_t m = n - base < PTILE ? (uint32_t)(n - base) : PTILE;  // pairs in this block
+  c[threadIdx.x] = 0;
+  gb[threadIdx.x] = hist[(uint64_t)threadIdx.x * nblk + blockIdx.x];
+  // coalesced loads; the pad past m sorts last (digit 255, after every real pair)
+#pragma unroll
+  for (int k = 0; k < PE; ++k) {
+    const uint32_t e = (uint32_t)k * PB + threadIdx.x;
+    kk[e] = e < m ? kin[base + e] : ~0ull;
+    vv[e] = e < m ? vin[base + e] : 0ull;
+  }
+  __syncthreads();
+  // thread t holds pairs [PE*t, PE*t + PE) in order; eight stable splits by the digit's bits
+  unsigned long long k[PE], v[PE];
+#pragma unroll
+  for (int j = 0; j < PE; ++j) {
+    k[j] = kk[PE * threadIdx.x + j];
+    v[j] = vv[PE * threadIdx.x + j];
+  }
+  for (uint32_t b = 0; b < 8; ++b) {
+    uint32_t ones = 0;
+#pragma unroll
+    for (int j = 0; j < PE; ++j) ones += (uint32_t)(k[j] >> (sh + b)) & 1u;
+    uint32_t tot0;
+    const uint32_t z0 = pair_block_scan((uint32_t)PE - ones, wsum, tot0);  // zeros before this thread's run
+    uint32_t o0 = PE * threadIdx.x - z0;                                    // ones before it
+    uint32_t z = z0;
+    __syncthreads();  // (every thread's run read before any is overwritten)
+#pragma unroll
+    for (int j = 0; j < PE; ++j) {
+      const bool one = (k[j] >> (sh + b)) & 1u;
+      const uint32_t at = one ? tot0 + o0 : z;
+      o0 += one ? 1u : 0u;
+      z += one ? 0u : 1u;
+      kk[at] = k[j];
+      vv[at] = v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PE; ++j) {
+      k[j] = kk[PE * threadIdx.x + j];
+      v[j] = vv[PE * threadIdx.x + j];
+    }
+  }
+  // the block's digit histogram and each digit's first place in the sorted block
+#pragma unroll
+  for (int j = 0; j < PE; ++j)
+    if (PE * threadIdx.x + j < m) atomicAdd(&c[(uint32_t)(k[j] >> sh) & 255u], 1u);
+  __syncthreads();
+  uint32_t all;
+  const uint32_t first = pair_block_scan(c[threadIdx.x], wsum, all);
+  __syncthreads();
+  c[threadIdx.x] = first;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PE; ++j) {
+    const uint32_t e = PE * threadIdx.x + j;
+    if (e < m) {
+      const uint32_t d = (uint32_t)(k[j] >> sh) & 255u;
+      const uint64_t at = (uint64_t)gb[d] + (e - c[d]);
+      kout[at] = k[j];
+      vout[at] = v[j];
+    }
+  }
+}
+
 }  // namespace pluss

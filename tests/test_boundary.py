@@ -58,7 +58,6 @@ def test_product_reads_no_environment():
 # section 8).
 SCRATCH_ALLOWED = {
     "k_fa_local_lmILi4E": "the uniform source's local pass: register spills of the tile staging",
-    "rocprim": "rocPRIM's pair sort, shapes with N % (cls/ds) != 0 only",
 }
 
 

@@ -987,3 +987,26 @@ def test_random_shapes_clean_and_faithful_equal_oracle(orc, shape):
             want, trav = orc.faithful(oc, ref, part)
             assert {k: v for k, v in h.bins.items() if k[0] == ref} == want, (shape, ref)
             assert h.traversed[P.REF_ID[ref]] == trav, (shape, ref)
+
+
+@pytest.mark.parametrize("N,T", [(104, 2), (264, 2)])
+def test_pair_sort_shapes_vs_oracle(orc, N, T):
+    """Shapes with N % (CLS/DS) != 0 (DS=4: lines of 16 elements) take the
+    (key, sink) pair path, sorted by the hand-written LSD pair sort (no
+    library sort left): tens of thousands of samples per reference in any
+    order (several blocks per pass; 3 passes at N=104, 4 at N=264, so both
+    buffer parities end in place), through the six-reference and the
+    one-reference entry points == the stepping r10 oracle."""
+    c = cfg(N, T, 4, 4, 64, mode="faithful")
+    span = N - 1
+    per = [min(6000, span * span), min(6000, span * span), 40000, 3000, 40000, 40000]
+    lists = [P.expand_samples(c, 0x5EED0200 + N, r, 0, n) for r, n in enumerate(per)]
+    s = np.concatenate(lists)
+    h = P.sampled_hist(c, s)
+    oc = orc.cfg(N, T, 4, 4, 64)
+    for r, ref in enumerate(P.REFS):
+        want, trav = orc.faithful(oc, ref, lists[r])
+        assert {k: v for k, v in h.bins.items() if k[0] == ref} == want, (N, ref)
+        assert h.traversed[r] == trav, (N, ref)
+    one = P.sampled_hist(c, lists[4])  # (one reference)
+    assert {k: v for k, v in one.bins.items() if k[0] == "C2"} == {k: v for k, v in h.bins.items() if k[0] == "C2"}
