@@ -1206,7 +1206,7 @@ __device__ __forceinline__ bool fa_lane_tile(const Model& m, const FaRefs& a, co
 #pragma unroll
   for (int k = 0; k < ST; ++k) {
     const uint32_t e = e0 + 64u * k;
-    if constexpr (SRC == SRC_UNI) v[k] = src[e < last ? e : last];
+    if constexpr (SRC == SRC_UNI) (void)e;  // (staged in LDS: each step reads its element where it decodes it)
     else if constexpr (SRC == SRC_W32P) v[k] = __builtin_nontemporal_load(msrc + (e < last ? e : last));
     else v[k] = __builtin_nontemporal_load(src + (e < last ? e : last));
   }
@@ -1248,7 +1248,10 @@ __device__ __forceinline__ bool fa_lane_tile(const Model& m, const FaRefs& a, co
     const bool val = FULLT || e0 + 64u * k <= last;
     uint32_t oddk = 0;
     FaDec d;
-    if constexpr (SRC == SRC_UNI) d = fa_dec_staged(v[k]);
+    if constexpr (SRC == SRC_UNI) {
+      const uint32_t e = e0 + 64u * k;
+      d = fa_dec_staged(src[e < last ? e : last]);
+    }
     else if constexpr (fa_smp<SRC>()) d = fa_dec_sample<REF>(m, o.pv, (uint64_t)v[k], oddk);
     else if constexpr (SRC == SRC_W32P) d = fa_dec_w32p<REF>(m, o.pv, v[k], e0 + 64u * k < be ? qa : qb);
     else d = fa_dec_word<REF>(m, o.pv, v[k]);
@@ -1528,9 +1531,11 @@ template <int SRC>
 constexpr bool fa_lm() { return fa_mem<SRC>() || SRC == SRC_UNI; }
 
 // waves per SIMD asked of the compiler: lists in memory fit 8 (<= 64 VGPRs and
-// <= 80 SGPRs: at 83 SGPRs the SGPR file held 7); the uniform staging needs 4
+// <= 80 SGPRs: at 83 SGPRs the SGPR file held 7); the uniform staging takes 3
+// (145 VGPRs; at 4, 128 VGPRs, it spilled to scratch, and no product kernel
+// may request scratch -- DESIGN.md section 8, r5p)
 template <int SRC>
-constexpr int fa_lm_waves() { return SRC == SRC_UNI || SRC == SRC_W32P ? 4 : 8; }
+constexpr int fa_lm_waves() { return SRC == SRC_UNI ? 3 : SRC == SRC_W32P ? 4 : 8; }
 // (the references' partial last tiles of lists in memory go to the queued
 // pass: every list at the BASELINE shapes already queues C0's and C1's tiles,
 // whose keys span more than 32 bits, so a launch of their own for the partial
@@ -1557,7 +1562,10 @@ __global__ __launch_bounds__(fa_lm_nt<SRC>()) __attribute__((amdgpu_waves_per_eu
   if constexpr (SRC == SRC_UNI) {
     // (T, N and their shifts are the same in every reference's view)
     const UniDec dz{(uint32_t)m.N, (uint32_t)m.W - 1u, a.pv[0].Q, (uint32_t)m.S, a.pv[0].nsh, a.pv[0].tsh};
-    uni_stage<NT, true>(a.us, T.r, T.lt, T.mt, L.raw, L.cand, a.us->flags, [](uint32_t e) { return e; }, dz);
+    // (the leaf table of the two-phase emission lives in the scan's own LDS,
+    // unused until the staging is done)
+    uni_stage<NT, true>(a.us, T.r, T.lt, T.mt, L.raw, L.cand, a.us->flags, [](uint32_t e) { return e; }, dz,
+                        reinterpret_cast<unsigned long long*>(&L.s), (uint32_t)(sizeof(L.s) / 8));
 #define PLUSS_FA_LM(R)                                                                              \
   if (T.mt == TILE) done = fa_lane_tile<SRC, CHECK, R, true, NT>(m, a, T, sh, kl_out, g, L.raw);   \
   else done = fa_lane_tile<SRC, CHECK, R, false, NT>(m, a, T, sh, kl_out, g, L.raw);

@@ -434,10 +434,20 @@ struct UniDec {
 // case 1 flag << 33 | tid == 0 << 34 | the key's high bits << 35
 // (fa_lane_tile's element, nothing left to decode; shapes whose keys stay
 // below 2^61 and whose leaves span less than 2^32 keys, FaRefs::unidec).
+// DEC emits in two phases (round 6): each leaf's thread writes, per kept
+// candidate, only (its leaf's slot in `tab`, its offset) -- a few
+// instructions per slot of the 32-slot emission -- and the leaf's fixed
+// decode bits once into tab; then every thread decodes its share of the
+// tile's elements from the table.  (Decoding inside each of a leaf's 32
+// predicated slots held the row's constants live through the sorting
+// network: 128 VGPRs and 80 B of register spills per lane.)  `tab`: tcap
+// LDS words of 8 bytes; the leaves go in rounds of at most tcap leaves whose
+// key bases lie within 2^32 of the round's first (one round for a dense tile).
 template <int NT, bool DEC, class SLOT>
 __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_t r, uint64_t lt, uint32_t mt,
                                           unsigned long long* raw, uint32_t* cand, unsigned int* flags,
-                                          SLOT&& slot, const UniDec dz = UniDec{}) {
+                                          SLOT&& slot, const UniDec dz = UniDec{}, unsigned long long* tab = nullptr,
+                                          uint32_t tcap = 0) {
   // the generator and the plan's arrays copied out once: read through the
   // plan pointer after every LDS store (generic stores may alias it), they
   // were reloaded from memory per candidate
@@ -448,7 +458,7 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
   const uint64_t nl = us->loff[r + 1] - lg0, lbase = us->lbase[r];  // (leaves held; their first's number)
   const uint64_t la = us->tmap[tm0 + lt], lb = lt + 1 < nt ? us->tmap[tm0 + lt + 1] : nl - 1;
   const uint64_t pbase = pre[lg0];
-  const bool leaves_ok = nl > 0 && la <= lb && lb < nl;
+  const bool leaves_ok = nl > 0 && la <= lb && lb < nl && (!DEC || tcap > 0);
   const uint64_t r0 = leaves_ok ? pre[lg0 + la] - pbase : 0, rend = leaves_ok ? pre[lg0 + lb + 1] - pbase : 0;
   if (!leaves_ok || rend - r0 > UG_CAP) {
     if (threadIdx.x == 0) atomicOr(flags, FLAG_UNI);
@@ -474,12 +484,18 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
   if (threadIdx.x == 0) *alloc = 0;
   __syncthreads();
   const uint64_t f0 = lt * UG_TILE;
-  for (uint64_t l = la + threadIdx.x; l <= lb; l += NT) {
+  // (DEC) a leaf's key base: ((q << nsh) + (3-D ? c1 : w0)) * S + (C0, C1: ref; else ref + 4 w0), times T
+  auto leaf_key = [&](const UniRowD& rd) -> uint64_t {
+    const uint32_t qc0 = (rd.q << dz.nsh) + (u.dim3 ? rd.c1 : rd.w0);
+    return ((uint64_t)qc0 * dz.S + (u.ref < 2 ? u.ref : u.ref + 4u * rd.w0)) << dz.tsh;
+  };
+  // leaf l's candidates (DEC: its table slot ts, the round's key base K0)
+  auto leaf = [&](uint64_t l, uint32_t ts, uint64_t K0) {
     const uint32_t c = cnt[lg0 + l];
-    if (!c) continue;
+    if (!c) return;
     if (c > UG_LEAFMAX) {
       atomicOr(flags, FLAG_UNI);
-      continue;
+      return;
     }
     const uint64_t x0 = pre[lg0 + l] - pbase;
     const UniLeaf f = uni_leaf(u, lbase + l);
@@ -493,37 +509,30 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
     // two: every BASELINE shape): offset o adds t = o % T to c0 and w = o / T
     // to c2 (3-D) or c1 (2-D); other leaves divide
     const bool fastp = !f.blk && u.tp2 && u.csp2;
+    if constexpr (DEC) {
+      // the leaf's entry: its key base relative to the round's, and its row's
+      // decode bits (pluss_faithful.h fa_dec_digits: for 3-D references only
+      // c2 = w moves, so case 0 is ((w & am) != av) && w < alim and case 1 a
+      // leaf constant): w0 | case-1 flag << 20 | av << 21 | block B << 22
+      uint32_t av = 1u, b1 = 1u;
+      if (u.ref == C3) b1 = (rd.c1 & dz.Wm1) != dz.Wm1 ? 1u : 0u;
+      else if (u.ref == A0) b1 = rd.c1 + 1 < dz.N ? 1u : 0u;
+      else if (u.ref == B0) {
+        av = (rd.c1 & dz.Wm1) != dz.Wm1 ? 1u : 0u;
+        b1 = rd.q + 1 < dz.Q ? 1u : 0u;
+      }
+      const uint32_t meta = rd.w0 | (b1 << 20) | ((av & 1u) << 21) | (f.blk << 22);
+      tab[ts] = (unsigned long long)(uint32_t)(leaf_key(rd) - K0) | ((unsigned long long)meta << 32);
+    }
     const uint32_t c0b = ((rd.q >> u.cssh) << (u.tsh + u.cssh)) | (rd.q & (u.CS - 1));
     const uint64_t pkb = pack(u.ref, c0b, u.dim3 ? rd.c1 : 0u, u.dim3 ? rd.w0 : 0u);
-    // DEC: the key lkb64 + (wq * dk + t) (the increment below 2^32, the
-    // shape's condition for this mode) and the case flags of the leaf's row
-    // (pluss_faithful.h fa_dec_digits): for 3-D references only c2 = w moves,
-    // so case 0 is ((w & am) != av) && w < alim and case 1 a leaf constant
-    uint32_t lkb = 0, khi = 0, dk = 0, am = 0, av = 1, alim = 0xFFFFFFFFu, bfl = 2u;
-    if constexpr (DEC) {
-      const uint32_t qc0 = (rd.q << dz.nsh) + (u.dim3 ? rd.c1 : rd.w0);
-      const uint64_t lk64 = ((uint64_t)qc0 * dz.S + (u.ref < 2 ? u.ref : u.ref + 4u * rd.w0)) << dz.tsh;
-      lkb = (uint32_t)lk64;
-      khi = (uint32_t)(lk64 >> 32);
-      dk = (u.dim3 ? 4u : dz.S) << dz.tsh;
-      if (u.ref == C3) {
-        alim = dz.N - 1;                          // c2 + 1 < N
-        bfl = (rd.c1 & dz.Wm1) != dz.Wm1 ? 2u : 0u;
-      } else if (u.ref == A0) {
-        am = av = dz.Wm1;                         // (c2 & Wm1) != Wm1
-        bfl = rd.c1 + 1 < dz.N ? 2u : 0u;
-      } else if (u.ref == B0) {
-        av = (rd.c1 & dz.Wm1) != dz.Wm1 ? 1u : 0u;  // a leaf constant
-        bfl = rd.q + 1 < dz.Q ? 2u : 0u;
-      }
-    }
     const FastDiv fd = f.blk ? u.fB : u.fA;
     const uint32_t tb = (uint32_t)f.tb;
     auto put = [&](uint32_t e, uint32_t o, auto fastc) {  // candidate at offset o, kept as tile element e < mt
-      constexpr bool FP = decltype(fastc)::value;       // (block A, T and CS powers of two: shifts)
-      const uint32_t wq = FP ? o >> u.tsh : (uint32_t)(((uint64_t)umulhi32(o, fd.m) + o) >> fd.s);
-      const uint32_t t = FP ? o & (u.T - 1) : o - wq * tb;
       if constexpr (!DEC) {
+        constexpr bool FP = decltype(fastc)::value;       // (block A, T and CS powers of two: shifts)
+        const uint32_t wq = FP ? o >> u.tsh : (uint32_t)(((uint64_t)umulhi32(o, fd.m) + o) >> fd.s);
+        const uint32_t t = FP ? o & (u.T - 1) : o - wq * tb;
         uint64_t pk;
         if (FP) {
           pk = pkb | ((uint64_t)t << (40 + u.cssh));
@@ -533,12 +542,7 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
         }
         raw[slot(e)] = pk;
       } else {
-        const uint32_t w = rd.w0 + wq;
-        const uint32_t ca = ((w & am) != av && w < alim) ? 1u : 0u;
-        const uint32_t lk = lkb + (wq * dk + t);
-        const uint32_t hi = khi + (lk < lkb ? 1u : 0u);
-        raw[e] = (unsigned long long)lk |
-                 ((unsigned long long)(ca | bfl | (t == 0 ? 4u : 0u) | (hi << 3)) << 32);
+        raw[e] = ((unsigned long long)ts << 32) | o;  // (decoded from the table after the round)
       }
     };
     // one candidate at a time, the removed ones counted as they come (the rare paths)
@@ -601,8 +605,8 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
           if (q < c && !((rm >> q) & 1u) && (uint32_t)e < mt) put((uint32_t)e, v[q], fastc);
         }
       };
-      if (fastp) slots(std::true_type{});
-      else slots(std::false_type{});
+      if (DEC || !fastp) slots(std::false_type{});
+      else slots(std::true_type{});
     } else {  // a large leaf (rare)
       const uint32_t G = (uint32_t)f.G;
       const uint32_t off = atomicAdd(alloc, c);
@@ -649,8 +653,67 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
         }
       }
     }
+  };
+  if constexpr (!DEC) {
+    for (uint64_t l = la + threadIdx.x; l <= lb; l += NT) leaf(l, 0u, 0ull);
+    __syncthreads();
+    return;
+  } else {
+    // the tile element of leaf l's first kept candidate (l in [la, lb + 1])
+    auto first_elem = [&](uint64_t l) -> int64_t {
+      const uint64_t x0 = pre[lg0 + l] - pbase;
+      const uint32_t w0i = (uint32_t)((x0 >> 5) - wlo), sh = (uint32_t)x0 & 31u;
+      const uint64_t remb = rem0 + rbw[w0i] + (uint64_t)__popc(bw[w0i] & ((1u << sh) - 1u));
+      return (int64_t)(x0 - remb) - (int64_t)f0;
+    };
+    auto key_of_leaf = [&](uint64_t l) { return leaf_key(uni_row(u, uni_leaf(u, lbase + l))); };
+    // the reference's decode constants (fa_dec_digits): case 0 = ((w & am) != av) && w < alim
+    const uint32_t am = u.ref == A0 ? dz.Wm1 : 0u, alim = u.ref == C3 ? dz.N - 1 : 0xFFFFFFFFu;
+    const uint32_t dk = (u.dim3 ? 4u : dz.S) << dz.tsh;
+    const bool tp2 = u.tp2 != 0;
+    for (uint64_t l0 = la; l0 <= lb;) {
+      const uint64_t K0 = key_of_leaf(l0);
+      uint64_t l1 = lb - l0 >= tcap ? l0 + tcap - 1 : lb;
+      if (key_of_leaf(l1) - K0 > 0xFFFFFFFFull) {  // (keys grow with the leaf: the last within 2^32 of K0)
+        uint64_t lo = l0, hi = l1;
+        while (lo < hi) {
+          const uint64_t mid = lo + (hi - lo + 1) / 2;
+          if (key_of_leaf(mid) - K0 <= 0xFFFFFFFFull) lo = mid;
+          else hi = mid - 1;
+        }
+        l1 = lo;
+      }
+      for (uint64_t l = l0 + threadIdx.x; l <= l1; l += NT) leaf(l, (uint32_t)(l - l0), K0);
+      __syncthreads();
+      // this round's elements: (slot, offset) -> the decoded word
+      const int64_t ea = first_elem(l0), eb = first_elem(l1 + 1);
+      const uint32_t e0 = ea < 0 ? 0u : (ea > (int64_t)mt ? mt : (uint32_t)ea);
+      const uint32_t e1 = eb < 0 ? 0u : (eb > (int64_t)mt ? mt : (uint32_t)eb);
+      for (uint32_t e = e0 + threadIdx.x; e < e1; e += NT) {
+        const unsigned long long pw = raw[e];
+        const uint32_t o = (uint32_t)pw;
+        const unsigned long long en = tab[(uint32_t)(pw >> 32)];
+        const uint32_t meta = (uint32_t)(en >> 32), blk = (meta >> 22) & 1u;
+        uint32_t wq, t;
+        if (!blk && tp2) {
+          wq = o >> u.tsh;
+          t = o & (u.T - 1);
+        } else {
+          const FastDiv fd = blk ? u.fB : u.fA;
+          wq = (uint32_t)(((uint64_t)umulhi32(o, fd.m) + o) >> fd.s);
+          t = o - wq * (blk ? u.T - 1 : u.T);
+        }
+        const uint32_t w = (meta & 0xFFFFFu) + wq, av = (meta >> 21) & 1u;
+        const uint32_t ca = ((w & am) != (u.ref == A0 ? dz.Wm1 : av) && w < alim) ? 1u : 0u;
+        const unsigned long long key = K0 + (uint32_t)en + (uint32_t)(wq * dk + t);
+        raw[e] = (unsigned long long)(uint32_t)key |
+                 ((unsigned long long)(ca | (((meta >> 20) & 1u) << 1) | (t == 0 ? 4u : 0u) |
+                                       ((uint32_t)(key >> 32) << 3)) << 32);
+      }
+      __syncthreads();
+      l0 = l1 + 1;
+    }
   }
-  __syncthreads();
 }
 #endif
 

@@ -314,7 +314,7 @@ __global__ void k_ug_setup(const UniSet h, UniSet* d) { *d = h; }
 template <bool DEC>
 __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(4))) void k_ug_stage_only(
     const UniSet* __restrict__ us, UniDec dz, uint64_t* __restrict__ out) {
-  __shared__ unsigned long long raw[UG_TILE];
+  __shared__ unsigned long long raw[UG_TILE], tab[DEC ? 294 : 1];  // (tab: the faithful scan's 2352 B)
   __shared__ uint32_t cand[UG_CAND];
   const uint64_t gt = blockIdx.x;
   uint32_t r = 0;
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(4))) void k_
   r = __builtin_amdgcn_readfirstlane(r);
   const uint64_t lt = gt - us->tmoff[r], S = us->u[r].S;
   if ((lt + 1) * UG_TILE > S) return;  // (full tiles only)
-  uni_stage<UB, DEC>(us, r, lt, UG_TILE, raw, cand, us->flags, [](uint32_t e) { return e; }, dz);
+  uni_stage<UB, DEC>(us, r, lt, UG_TILE, raw, cand, us->flags, [](uint32_t e) { return e; }, dz, tab, DEC ? 294u : 0u);
   if (threadIdx.x == 0) out[gt] = raw[0] ^ raw[UG_TILE - 1];
 }
 

@@ -56,9 +56,7 @@ def test_product_reads_no_environment():
 # gfx950 under ROCm 7's scratch reclaim, a kernel that does, running while the
 # process's other HSA queues hold work, faulted the device (r5p, DESIGN.md
 # section 8).
-SCRATCH_ALLOWED = {
-    "k_fa_local_lmILi4E": "the uniform source's local pass: register spills of the tile staging",
-}
+SCRATCH_ALLOWED = {}
 
 
 def kernel_resources(lib):
