@@ -51,6 +51,11 @@ void debug_stage(hipStream_t s, const char* what) {
   g_stage_names.emplace_back(what, (const void*)s);
   hipLaunchKernelGGL(k_stage_mark, dim3(1), dim3(1), 0, s, g_stage_marks + i, (unsigned long long)(i + 1));
 }
+int debug_knob(const char* name) {
+  const std::string k = std::string("PLUSS_KNOB_") + name;
+  const char* e = std::getenv(k.c_str());
+  return e ? std::atoi(e) : 0;
+}
 }  // namespace pluss
 
 extern "C" void pluss_debug_stage_dump(int last) {

@@ -32,6 +32,8 @@
 // Validated against the reference's own dumps (tests/golden/r10_*, 42/42).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -703,6 +705,7 @@ template <typename KT, bool SMP>
 static int srt_sort(pluss_ctx* ctx, FaithfulBufs& b, const void* const in[6], const uint64_t cnt[6],
                     unsigned long long* x1, unsigned long long* y, KT* out, hipStream_t s, SrtPay* pay = nullptr) {
   SrtPlan P = srt_plan(ctx->m, in, cnt);
+  if (!SMP && PLUSS_KNOB("WORDS_COUNTED")) P.fast1 = false;  // (diagnostic build only)
   if (pay) {  // (the parents' address once srt_reserve below has grown the scratch)
     pay->on = P.p32 && sizeof(KT) > 4;
     pay->par = nullptr;
@@ -1369,7 +1372,10 @@ __global__ __launch_bounds__(PT_NT) void k_fa_part(Model m, const uint64_t* __re
       if ((int)lane == lead) at = atomicAdd(&lc[bb], (uint32_t)__popcll(mk));
       if (!COUNT) {
         at = __shfl(at, lead, 64);
-        if (bin == bb) out[lbase[bb] + at + __popcll(mk & ((1ull << lane) - 1))] = word;
+        if (bin == bb) {
+          const uint64_t o = lbase[bb] + at + __popcll(mk & ((1ull << lane) - 1));
+          if (SRT_OK(o < n, 8, o, n)) out[o] = word;
+        }
       }
       pend &= ~mk;
     }
@@ -1429,6 +1435,17 @@ uint32_t faith_part_blocks(uint64_t n, uint32_t S) {
   B = std::min<uint64_t>(std::min<uint64_t>(B, 4096), cap);
   return (uint32_t)std::max<uint64_t>(B, 1);
 }
+
+#ifdef PLUSS_DEBUG_STAGES
+}  // namespace pluss
+extern "C" void pluss_debug_sort_dump(void) {
+  unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(pluss::g_srt_dbg), sizeof h);
+  std::fprintf(stderr, "[sort checks] first failure code %llu index %llu bound %llu block %llx thread %llu; failures %llu\n",
+               h[0], h[1], h[2], h[3], h[4], h[5]);
+}
+namespace pluss {
+#endif
 
 int faith_word_bytes(const pluss_ctx* ctx) {
   const int fm = faith_fm(ctx->m);
@@ -1515,7 +1532,8 @@ int faith_shards_local_words(pluss_ctx* ctx, const void* const in[6], const uint
   SrtPay pay{};
   if (fm == FM_PK32) {
     if (int rc = srt_sort<uint32_t, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, (uint32_t*)b.keys_s, s)) return rc;
-  } else if (int rc = srt_sort<unsigned long long, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, b.keys_s, s, &pay)) {
+  } else if (int rc = srt_sort<unsigned long long, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, b.keys_s, s,
+                                                          PLUSS_KNOB("WORDS_W64") ? nullptr : &pay)) {
     return rc;
   }
   ctx->tables_dirty = true;

@@ -146,9 +146,12 @@ void set_error(const std::string& msg);
 // stage that reports it.  Compiles to nothing in the product build.
 #ifdef PLUSS_DEBUG_STAGES
 void debug_stage(hipStream_t s, const char* what);
+int debug_knob(const char* name);  // a diagnostic switch (environment PLUSS_KNOB_<name>; 0 when unset)
 #define PLUSS_STAGE(s, what) ::pluss::debug_stage((s), (what))
+#define PLUSS_KNOB(name) ::pluss::debug_knob(name)
 #else
 #define PLUSS_STAGE(s, what) ((void)0)
+#define PLUSS_KNOB(name) 0
 #endif
 
 int validate_cfg(const pluss_cfg* cfg, Model* m);

@@ -40,6 +40,29 @@
 
 namespace pluss {
 
+// Diagnostic builds only (-DPLUSS_DEBUG_STAGES): bounds checks on the sort's
+// global accesses; a failing one is recorded (code, index, bound, block) in
+// g_srt_dbg -- the first one, plus a count -- and its access skipped.  In the
+// product build SRT_OK(...) is `true` and compiles away.
+#ifdef PLUSS_DEBUG_STAGES
+__device__ unsigned long long g_srt_dbg[8];
+__device__ __forceinline__ bool srt_ok(bool ok, uint32_t code, uint64_t idx, uint64_t bound) {
+  if (!ok) {
+    atomicAdd(&g_srt_dbg[5], 1ull);
+    if (atomicCAS(&g_srt_dbg[0], 0ull, (unsigned long long)code) == 0ull) {
+      g_srt_dbg[1] = idx;
+      g_srt_dbg[2] = bound;
+      g_srt_dbg[3] = blockIdx.x | ((unsigned long long)blockIdx.y << 32);
+      g_srt_dbg[4] = threadIdx.x;
+    }
+  }
+  return ok;
+}
+#define SRT_OK(cond, code, idx, bound) ::pluss::srt_ok((cond), (code), (uint64_t)(idx), (uint64_t)(bound))
+#else
+#define SRT_OK(cond, code, idx, bound) true
+#endif
+
 constexpr int SB = 256;                   // threads per sort workgroup
 constexpr int SE = 16;                    // words per thread per batch
 constexpr uint32_t SBATCH = SB * SE;      // words per LDS batch
@@ -428,8 +451,15 @@ __global__ __launch_bounds__(SB1) void k_srt_scatter1f(Model m, SrtRefs a, const
                                                       uint32_t* __restrict__ ovf, uint32_t* __restrict__ X1, GTable g) {
   __shared__ uint32_t stage[SC1];
   __shared__ uint8_t sdig[SC1];
-  __shared__ uint32_t bcnt[SB], bst[SB], bbase[SB], wsum[SB / 64];
-  if (*ovf) return;  // (the plan did not fit: the counted path runs)
+  __shared__ uint32_t bcnt[SB], bst[SB], bbase[SB], wsum[SB / 64], s_of;
+  // (the plan did not fit, or another workgroup's run did not: the counted
+  // path runs.  Read once for the workgroup: *ovf may be raised while this
+  // workgroup starts, and waves that saw different values -- some returning,
+  // some going on without their bucket counters zeroed -- wrote runs at
+  // garbage offsets)
+  if (threadIdx.x == 0) s_of = *ovf;
+  __syncthreads();
+  if (s_of) return;
   const uint32_t r = srt_ref_of_chunk(a, blockIdx.x / SPL);
   const SrtOne o = srt_one(a, r);
   const uint64_t c = blockIdx.x - o.c0 * SPL;
@@ -510,7 +540,8 @@ __global__ __launch_bounds__(SB1) void k_srt_scatter1f(Model m, SrtRefs a, const
   const uint32_t mt = (uint32_t)(e1 - e0);
   for (uint32_t i = threadIdx.x; i < mt; i += SB1) {
     const uint32_t d = sdig[i], at = bbase[d];
-    if (at != 0xFFFFFFFFu) X1[at + (i - bst[d])] = stage[i];
+    if (at != 0xFFFFFFFFu && SRT_OK(at + (i - bst[d]) < 2 * a.eoff[6], 1, at + (i - bst[d]), 2 * a.eoff[6]))
+      X1[at + (i - bst[d])] = stage[i];
   }
 }
 
@@ -556,11 +587,17 @@ __global__ __launch_bounds__(SB1) void k_srt_scatter2f(const SrtRefs a, const Sr
   // (no digit array beside the stage: a staged payload holds its own digit,
   // so the LDS is 38 KB and four workgroups share a CU)
   __shared__ PT stage[SC1];
-  __shared__ uint32_t bcnt[SB], bst[SB], bbase[SB], ccap[SB], coff[SB], wsum[SB / 64];
+  __shared__ uint32_t bcnt[SB], bst[SB], bbase[SB], ccap[SB], coff[SB], wsum[SB / 64], s_of;
   const uint32_t q2 = blockIdx.x / SPL, half = blockIdx.x - q2 * SPL;
   // (the three reads issued together; cmap has a slot for every workgroup's q2)
-  const uint32_t t0 = tot[0], of = *l2.ovf, pi = cmap[q2];
-  if (q2 >= t0 || of) return;  // (a level 1 or region overflow: the counted level 2 runs)
+  const uint32_t t0 = tot[0], pi = cmap[q2];
+  if (q2 >= t0) return;
+  // a level 1 or region overflow: the counted level 2 runs (*l2.ovf read once
+  // for the workgroup: it may be raised by another workgroup meanwhile, see
+  // k_srt_scatter1f)
+  if (threadIdx.x == 0) s_of = *l2.ovf;
+  __syncthreads();
+  if (s_of) return;
   const SrtParent P = par[pi];
   const uint32_t k = q2 - P.cbase;
   const uint32_t c0 = k * SC + half * SC1;  // this workgroup's part of the parent's k-th chunk
@@ -572,7 +609,8 @@ __global__ __launch_bounds__(SB1) void k_srt_scatter2f(const SrtRefs a, const Sr
 #pragma unroll
   for (int j = 0; j < SE; ++j) {
     const uint32_t i = e0 + (uint32_t)j * SB1 + threadIdx.x;
-    w[j] = __builtin_nontemporal_load(X1 + (i < e1 ? i : e1 - 1));
+    const uint32_t ii = i < e1 ? i : e1 - 1;
+    w[j] = SRT_OK(ii < 2 * a.eoff[6], 3, ii, 2 * a.eoff[6]) ? __builtin_nontemporal_load(X1 + ii) : (PT)0;
   }
   if (threadIdx.x < SB) bcnt[threadIdx.x] = 0;
   if (threadIdx.x < SB) {  // the children's capacities; their region offsets below
@@ -654,7 +692,8 @@ __global__ __launch_bounds__(SB1) void k_srt_scatter2f(const SrtRefs a, const Sr
   for (uint32_t i = threadIdx.x; i < mt; i += SB1) {
     const PT x = stage[i];
     const uint32_t d = srt_dig(x, lo, mask), at = bbase[d];
-    if (at != 0xFFFFFFFFu) Y[at + (i - bst[d])] = x;
+    if (at != 0xFFFFFFFFu && SRT_OK(at + (i - bst[d]) < l2.ycap, 2, at + (i - bst[d]), l2.ycap))
+      Y[at + (i - bst[d])] = x;
   }
 }
 
@@ -1088,6 +1127,9 @@ __global__ __launch_bounds__(SB) __attribute__((amdgpu_waves_per_eu(sizeof(PT) =
       deep(P.start, P.count, hi1, 0);
       return;
     }
+    if (!SRT_OK((uint64_t)P.src + P.count <= 2 * a.eoff[6], 4, (uint64_t)P.src + P.count, 2 * a.eoff[6]) ||
+        !SRT_OK((uint64_t)P.start + P.count <= a.eoff[6], 5, (uint64_t)P.start + P.count, a.eoff[6]))
+      return;
     item(X1, P.src, P.start, P.count, hi1);
     return;
   }
@@ -1118,6 +1160,9 @@ __global__ __launch_bounds__(SB) __attribute__((amdgpu_waves_per_eu(sizeof(PT) =
       deep(s, cnt, hi, 1);
       continue;
     }
+    if (!SRT_OK((uint64_t)(f2 ? ysrc[d] : s) + cnt <= l2.ycap, 6, (uint64_t)(f2 ? ysrc[d] : s) + cnt, l2.ycap) ||
+        !SRT_OK((uint64_t)s + cnt <= a.eoff[6] && bnd[d + 1] >= s, 7, (uint64_t)s + cnt, a.eoff[6]))
+      continue;
     item(Y, f2 ? ysrc[d] : s, s, cnt, hi);
   }
 }

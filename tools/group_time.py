@@ -48,6 +48,9 @@ for spd in (1, 2, 8):
             call = lambda: g.gen_uniform_faithful(SEED, totals)  # noqa: E731
         else:
             call = lambda: g.sampled_hist(lst)  # noqa: E731
+        if os.environ.get("PLUSS_PROBE_LIB") == "stages" and src == "any_order":
+            import atexit  # (the stage build's sort checks: printed at exit, after a fault too)
+            atexit.register(lambda: L.lib().pluss_debug_sort_dump())
         h = call()
         call()  # (the second identical call is captured into a graph)
         ts = []
