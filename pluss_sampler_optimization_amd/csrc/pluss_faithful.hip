@@ -702,9 +702,14 @@ struct SrtPay {
   uint64_t eoff[6];
 };
 template <typename KT, bool SMP>
+// narrow: the words are one key range's of the lists (a key-range shard's),
+// so they fill a fraction of the word range: the count-free level 1 sizes its
+// buckets for the whole range and would overflow, so the counted levels run
 static int srt_sort(pluss_ctx* ctx, FaithfulBufs& b, const void* const in[6], const uint64_t cnt[6],
-                    unsigned long long* x1, unsigned long long* y, KT* out, hipStream_t s, SrtPay* pay = nullptr) {
+                    unsigned long long* x1, unsigned long long* y, KT* out, hipStream_t s, SrtPay* pay = nullptr,
+                    bool narrow = false) {
   SrtPlan P = srt_plan(ctx->m, in, cnt);
+  if (narrow) P.fast1 = false;
   if (!SMP && PLUSS_KNOB("WORDS_COUNTED")) P.fast1 = false;  // (diagnostic build only)
   if (pay) {  // (the parents' address once srt_reserve below has grown the scratch)
     pay->on = P.p32 && sizeof(KT) > 4;
@@ -1293,9 +1298,14 @@ int faith_shards_local_selected(pluss_ctx* ctx, const uint64_t* d_rows, int32_t 
     woff += f.tot[r];
     soff += cnt[r];
   }
+  bool narrow = false;  // (a key range of the lists: the counted sort levels, srt_sort)
+  for (int r = 0; r < 6; ++r) narrow |= cnt[r] != f.tot[r];
   if (fm == FM_PK32) {
-    if (int rc = srt_sort<uint32_t, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, (uint32_t*)b.keys_s, s)) return rc;
-  } else if (int rc = srt_sort<unsigned long long, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, b.keys_s, s)) {
+    if (int rc = srt_sort<uint32_t, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, (uint32_t*)b.keys_s, s, nullptr,
+                                           narrow))
+      return rc;
+  } else if (int rc = srt_sort<unsigned long long, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, b.keys_s, s, nullptr,
+                                                          narrow)) {
     return rc;
   }
   f.src = fm == FM_PK32 ? SRC_W32 : SRC_W64;
@@ -1439,10 +1449,11 @@ uint32_t faith_part_blocks(uint64_t n, uint32_t S) {
 #ifdef PLUSS_DEBUG_STAGES
 }  // namespace pluss
 extern "C" void pluss_debug_sort_dump(void) {
-  unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long h[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(pluss::g_srt_dbg), sizeof h);
-  std::fprintf(stderr, "[sort checks] first failure code %llu index %llu bound %llu block %llx thread %llu; failures %llu\n",
-               h[0], h[1], h[2], h[3], h[4], h[5]);
+  std::fprintf(stderr, "[sort checks] first failure code %llu index %llu bound %llu block %llx thread %llu; failures %llu;"
+               " level-1 overflowing runs %llu, level-2 %llu; level-1 workgroups whose waves read different"
+               " overflow flags %llu\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]);
 }
 namespace pluss {
 #endif
@@ -1527,13 +1538,18 @@ int faith_shards_local_words(pluss_ctx* ctx, const void* const in[6], const uint
     a.src[r] = fm == FM_PK32 ? (const void*)((const uint32_t*)b.keys_s + soff) : (const void*)(b.keys_s + soff);
     soff += cnt[r];
   }
-  // the same sort as one GPU's radix pass (count-free levels, 4-byte payloads
-  // read back with their parents' digits past N = 1024)
+  // the same sort as one GPU's radix pass (4-byte payloads read back with
+  // their parents' digits past N = 1024); the count-free levels only when the
+  // shard holds whole lists (one shard), else the counted ones
   SrtPay pay{};
+  bool narrow = false;
+  for (int r = 0; r < 6; ++r) narrow |= cnt[r] != all[r];
   if (fm == FM_PK32) {
-    if (int rc = srt_sort<uint32_t, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, (uint32_t*)b.keys_s, s)) return rc;
+    if (int rc = srt_sort<uint32_t, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, (uint32_t*)b.keys_s, s, nullptr,
+                                           narrow))
+      return rc;
   } else if (int rc = srt_sort<unsigned long long, false>(ctx, b, in, cnt, b.sinks_s, b.pmax, b.keys_s, s,
-                                                          PLUSS_KNOB("WORDS_W64") ? nullptr : &pay)) {
+                                                          PLUSS_KNOB("WORDS_W64") ? nullptr : &pay, narrow)) {
     return rc;
   }
   ctx->tables_dirty = true;

@@ -45,7 +45,7 @@ namespace pluss {
 // g_srt_dbg -- the first one, plus a count -- and its access skipped.  In the
 // product build SRT_OK(...) is `true` and compiles away.
 #ifdef PLUSS_DEBUG_STAGES
-__device__ unsigned long long g_srt_dbg[8];
+__device__ unsigned long long g_srt_dbg[12];
 __device__ __forceinline__ bool srt_ok(bool ok, uint32_t code, uint64_t idx, uint64_t bound) {
   if (!ok) {
     atomicAdd(&g_srt_dbg[5], 1ull);
@@ -458,6 +458,22 @@ __global__ __launch_bounds__(SB1) void k_srt_scatter1f(Model m, SrtRefs a, const
   // some going on without their bucket counters zeroed -- wrote runs at
   // garbage offsets)
   if (threadIdx.x == 0) s_of = *ovf;
+#ifdef PLUSS_DEBUG_STAGES
+  {  // (diagnostic: would the waves, each reading *ovf itself as before, have disagreed?)
+    __shared__ uint32_t s_wv[SB1 / 64];
+    const uint32_t v = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)ovf);
+    if (__lane_id() == 0) s_wv[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t any = 0, all = 1;
+      for (int x = 0; x < SB1 / 64; ++x) {
+        any |= s_wv[x];
+        all &= s_wv[x] ? 1u : 0u;
+      }
+      if (any && !all) atomicAdd(&g_srt_dbg[8], 1ull);  // waves of one workgroup saw different flags
+    }
+  }
+#endif
   __syncthreads();
   if (s_of) return;
   const uint32_t r = srt_ref_of_chunk(a, blockIdx.x / SPL);
@@ -499,6 +515,9 @@ __global__ __launch_bounds__(SB1) void k_srt_scatter1f(Model m, SrtRefs a, const
       const uint32_t p = pbase + d;
       at = atomicAdd(&fill[p], n);
       if (at + n > cap[p]) {
+#ifdef PLUSS_DEBUG_STAGES
+        atomicAdd(&g_srt_dbg[6], 1ull);  // (level-1 overflows, counted)
+#endif
         atomicOr(ovf, 1u);
         at = 0xFFFFFFFFu;
       } else {
@@ -679,6 +698,9 @@ __global__ __launch_bounds__(SB1) void k_srt_scatter2f(const SrtRefs a, const Sr
   if (d < SB) {
     if (d <= mask && n) {
       if (at + n > ccap[d]) {
+#ifdef PLUSS_DEBUG_STAGES
+        atomicAdd(&g_srt_dbg[7], 1ull);  // (level-2 overflows, counted)
+#endif
         atomicOr(l2.ovf, 1u);
         at = 0xFFFFFFFFu;
       } else {

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r6l}
 mkdir -p "$OUT"
-for k in 1 2 3; do
+for k in 1 2 3 4; do
   timeout -k 10 300 python tools/group_time.py any_order 5 > "$OUT/any_order_$k.json" 2>&1 || { tail -2 "$OUT/any_order_$k.json"; exit 1; }
   tail -1 "$OUT/any_order_$k.json"
 done

@@ -49,12 +49,14 @@ for spd in (1, 2, 8):
         else:
             call = lambda: g.sampled_hist(lst)  # noqa: E731
         if os.environ.get("PLUSS_PROBE_LIB") == "stages" and src == "any_order":
-            import atexit  # (the stage build's sort checks: printed at exit, after a fault too)
-            atexit.register(lambda: L.lib().pluss_debug_sort_dump())
+            L.lib().pluss_debug_sort_dump()  # (the stage build's sort checks so far: after the last group)
+        print(f"shards {spd}: call 0", file=sys.stderr, flush=True)  # (progress: which call a failure hit)
         h = call()
+        print(f"shards {spd}: call 1", file=sys.stderr, flush=True)
         call()  # (the second identical call is captured into a graph)
         ts = []
-        for _ in range(reps):
+        for k in range(reps):
+            print(f"shards {spd}: call {2 + k}", file=sys.stderr, flush=True)
             t0 = time.perf_counter()
             call()
             ts.append((time.perf_counter() - t0) * 1e3)
