@@ -1531,11 +1531,14 @@ template <int SRC>
 constexpr bool fa_lm() { return fa_mem<SRC>() || SRC == SRC_UNI; }
 
 // waves per SIMD asked of the compiler: lists in memory fit 8 (<= 64 VGPRs and
-// <= 80 SGPRs: at 83 SGPRs the SGPR file held 7); the uniform staging takes 3
-// (145 VGPRs; at 4, 128 VGPRs, it spilled to scratch, and no product kernel
-// may request scratch -- DESIGN.md section 8, r5p)
+// <= 80 SGPRs: at 83 SGPRs the SGPR file held 7); the uniform staging fits 4
+// (127 VGPRs, no scratch: no product kernel may request scratch, DESIGN.md
+// section 8, r5p) with its register network at 30 candidates (UG_NET), its
+// per-leaf values computed where they are used and the tile's constants read
+// again after it; at 3 waves (145 VGPRs) the config-3 pass took 2.58 ms, at 4
+// 2.42 ms (r6r)
 template <int SRC>
-constexpr int fa_lm_waves() { return SRC == SRC_UNI ? 3 : SRC == SRC_W32P ? 4 : 8; }
+constexpr int fa_lm_waves() { return SRC == SRC_UNI || SRC == SRC_W32P ? 4 : 8; }
 // (the references' partial last tiles of lists in memory go to the queued
 // pass: every list at the BASELINE shapes already queues C0's and C1's tiles,
 // whose keys span more than 32 bits, so a launch of their own for the partial
@@ -1560,15 +1563,23 @@ __global__ __launch_bounds__(fa_lm_nt<SRC>()) __attribute__((amdgpu_waves_per_eu
   // occupancy is set by the staging's registers and LDS either way; in the
   // slow pass they cost ~60 us per pass)
   if constexpr (SRC == SRC_UNI) {
-    // (T, N and their shifts are the same in every reference's view)
-    const UniDec dz{(uint32_t)m.N, (uint32_t)m.W - 1u, a.pv[0].Q, (uint32_t)m.S, a.pv[0].nsh, a.pv[0].tsh};
-    // (the leaf table of the two-phase emission lives in the scan's own LDS,
-    // unused until the staging is done)
-    uni_stage<NT, true>(a.us, T.r, T.lt, T.mt, L.raw, L.cand, a.us->flags, [](uint32_t e) { return e; }, dz,
-                        reinterpret_cast<unsigned long long*>(&L.s), (uint32_t)(sizeof(L.s) / 8));
-#define PLUSS_FA_LM(R)                                                                              \
-  if (T.mt == TILE) done = fa_lane_tile<SRC, CHECK, R, true, NT>(m, a, T, sh, kl_out, g, L.raw);   \
-  else done = fa_lane_tile<SRC, CHECK, R, false, NT>(m, a, T, sh, kl_out, g, L.raw);
+    {
+      // (T, N and their shifts are the same in every reference's view)
+      const UniDec dz{(uint32_t)m.N, (uint32_t)m.W - 1u, a.pv[0].Q, (uint32_t)m.S, a.pv[0].nsh, a.pv[0].tsh};
+      // (the leaf table of the two-phase emission lives in the scan's own LDS,
+      // unused until the staging is done)
+      uni_stage<NT, true>(a.us, T.r, T.lt, T.mt, L.raw, L.cand, a.us->flags, [](uint32_t e) { return e; }, dz,
+                          reinterpret_cast<unsigned long long*>(&L.s), (uint32_t)(sizeof(L.s) / 8));
+    }
+    // the tile's constants read again for the scan (an opaque tile number: held
+    // through the staging, they pushed it past 128 VGPRs into scratch)
+    uint32_t bid = blockIdx.x;
+    asm volatile("" : "+s"(bid));
+    const FaTile T2 = fa_tile(a, bid);
+    unsigned long long* kl2 = klist + T2.gt * (uint64_t)(2 * KL);
+#define PLUSS_FA_LM(R)                                                                               \
+  if (T2.mt == TILE) done = fa_lane_tile<SRC, CHECK, R, true, NT>(m, a, T2, sh, kl2, g, L.raw);     \
+  else done = fa_lane_tile<SRC, CHECK, R, false, NT>(m, a, T2, sh, kl2, g, L.raw);
     PLUSS_FA_REFS(PLUSS_FA_LM)
 #undef PLUSS_FA_LM
   } else if (T.mt == TILE) {
@@ -1576,11 +1587,12 @@ __global__ __launch_bounds__(fa_lm_nt<SRC>()) __attribute__((amdgpu_waves_per_eu
     PLUSS_FA_REFS(PLUSS_FA_LM)
 #undef PLUSS_FA_LM
   }
+  const uint64_t gt = blockIdx.x;  // (== T.gt)
   if (done) {
-    if (threadIdx.x < FPW) part[T.gt * (uint64_t)FPW + threadIdx.x] = sh.out[threadIdx.x];
-    if (threadIdx.x == FPW) tmax[T.gt] = sh.out[FPW];
+    if (threadIdx.x < FPW) part[gt * FPW + threadIdx.x] = sh.out[threadIdx.x];
+    if (threadIdx.x == FPW) tmax[gt] = sh.out[FPW];
   } else if (threadIdx.x == 0) {
-    slowq[1 + atomicAdd(&slowq[0], 1u)] = (unsigned int)T.gt;
+    slowq[1 + atomicAdd(&slowq[0], 1u)] = (unsigned int)gt;
   }
 }
 

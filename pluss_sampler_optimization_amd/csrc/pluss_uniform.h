@@ -418,7 +418,11 @@ __device__ __forceinline__ void uni_sort_net(uint32_t (&v)[NC]) {
             v[i + j + k] = a < b ? b : a;
           }
 }
-constexpr uint32_t UG_NET = 32;  // leaves of at most this many candidates: sorted in registers
+// leaves of at most this many candidates: sorted in registers (30, not 32:
+// the 32-wide network held the uniform scan at 128 VGPRs with 16 B of spills;
+// P(c > 30) = 5e-4 at UG_MEAN 16, those leaves take the large-leaf path and
+// draw the same offsets)
+constexpr uint32_t UG_NET = 30;
 
 // What the faithful scan needs of a shape to take staged elements decoded
 // (uni_stage DEC): the key's low 32 bits and the case flags, per candidate,
@@ -484,6 +488,10 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
   if (threadIdx.x == 0) *alloc = 0;
   __syncthreads();
   const uint64_t f0 = lt * UG_TILE;
+  // tile element of window rank (wlo << 5) if nothing before it were removed: a
+  // window rank xr (kept, with remr removed below it in the window) lands at
+  // ebase + xr - remr
+  const int32_t ebase = (int32_t)((int64_t)(wlo << 5) - (int64_t)rem0 - (int64_t)f0);
   // (DEC) a leaf's key base: ((q << nsh) + (3-D ? c1 : w0)) * S + (C0, C1: ref; else ref + 4 w0), times T
   auto leaf_key = [&](const UniRowD& rd) -> uint64_t {
     const uint32_t qc0 = (rd.q << dz.nsh) + (u.dim3 ? rd.c1 : rd.w0);
@@ -497,14 +505,18 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
       atomicOr(flags, FLAG_UNI);
       return;
     }
-    const uint64_t x0 = pre[lg0 + l] - pbase;
+    // (32-bit, relative to the window: a window holds at most UG_CAP candidates)
+    const uint32_t xr = (uint32_t)(pre[lg0 + l] - pbase - (wlo << 5));  // rank of the leaf's first, from bit 0 of bw[0]
     const UniLeaf f = uni_leaf(u, lbase + l);
     const UniRowD rd = uni_row(u, f);
     // candidate i of the leaf (in key order) has rank x0 + i; the removed ones are skipped
-    const uint32_t w0i = (uint32_t)((x0 >> 5) - wlo), sh = (uint32_t)x0 & 31u;
-    const uint64_t remb = rem0 + rbw[w0i] + (uint64_t)__popc(bw[w0i] & ((1u << sh) - 1u));  // removed before x0
-    // tile-relative index of the leaf's first candidate if nothing of it were removed
-    const int32_t be = (int32_t)((int64_t)(x0 - remb) - (int64_t)f0);
+    // tile-relative index of the leaf's first candidate if nothing of it were
+    // removed (computed where it is used: held through the sorting network it
+    // pushed the uniform scan past 128 VGPRs)
+    auto first_e = [&]() -> int32_t {
+      const uint32_t remr = rbw[xr >> 5] + (uint32_t)__popc(bw[xr >> 5] & ((1u << (xr & 31u)) - 1u));
+      return ebase + (int32_t)xr - (int32_t)remr;  // (remr: removed in the window before it)
+    };
     // the packed sample's fixed bits for this leaf (block A, T and CS powers of
     // two: every BASELINE shape): offset o adds t = o % T to c0 and w = o / T
     // to c2 (3-D) or c1 (2-D); other leaves divide
@@ -542,38 +554,40 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
         }
         raw[slot(e)] = pk;
       } else {
-        raw[e] = ((unsigned long long)ts << 32) | o;  // (decoded from the table after the round)
+        reinterpret_cast<uint2*>(raw)[e] = make_uint2(o, ts);  // (slot << 32 | offset, decoded after the round)
       }
     };
     // one candidate at a time, the removed ones counted as they come (the rare paths)
-    uint64_t rem = remb;
+    int32_t e = 0;
     auto emit = [&](uint32_t i, uint32_t o) {
-      const uint64_t x = x0 + i;
-      if ((bw[(uint32_t)((x >> 5) - wlo)] >> (x & 31)) & 1u) {
-        ++rem;
-        return;
-      }
-      const uint64_t e = x - rem - f0;
-      if (e < mt) put((uint32_t)e, o, std::false_type{});
+      const uint32_t x = xr + i;
+      if ((bw[x >> 5] >> (x & 31)) & 1u) return;
+      if ((uint32_t)e < mt) put((uint32_t)e, o, std::false_type{});
+      ++e;
     };
+    const uint64_t gl = lbase + l;      // the leaf's number (its hash key's)
+    const uint32_t G = (uint32_t)f.G;  // (K*T < 2^32)
+    const bool direct = uni_direct(u, f);
     if (u.p >= 1.0) {
+      e = first_e();
       for (uint32_t j = 0; j < c; ++j) emit(j, j);
-    } else if (uni_direct(u, f)) {  // per-point draws: already in order
-      const uint64_t lk = uni_leafkey(u, lbase + l, 0xFFFFFFFFu);
+    } else if (direct) {  // per-point draws: already in order
+      const uint64_t lk = uni_leafkey(u, gl, 0xFFFFFFFFu);
+      e = first_e();
       uint32_t k = 0;
-      for (uint32_t j = 0; j < (uint32_t)f.G && k < c; ++j)
+      for (uint32_t j = 0; j < G && k < c; ++j)
         if (uni_u01(uni_hash(lk, j)) < u.p) emit(k++, j);
     } else if (c <= UG_NET) {
       // the common leaf: its offsets drawn and sorted in registers (an insertion
       // sort through LDS was a chain of dependent LDS round trips, divergent per lane)
-      const uint32_t G = (uint32_t)f.G;  // (K*T < 2^32)
       uint32_t v[UG_NET];
+      const uint64_t lm = uni_leafkey(u, gl, 0);  // (draw a's key: lm ^ a * the draw constant, uni_leafkey)
       for (uint32_t a = 0;; ++a) {
         if (a == UG_TRIES) {
           atomicOr(flags, FLAG_UNI);
           break;
         }
-        const uint64_t lk = uni_leafkey(u, lbase + l, a);
+        const uint64_t lk = lm ^ ((uint64_t)a * 0xD1B54A32D192ED03ull);
         if (G <= UG_PAIRG) {  // two offsets per hash; slots past every lane's count skipped
 #pragma unroll
           for (uint32_t q = 0; q < UG_NET; q += 2) {
@@ -596,8 +610,10 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
       }
       // the leaf's removed candidates from its two bitmap words at once (c <= 32
       // ranks from x0); candidate q is tile element be + q - (removed below q)
+      const int32_t be = first_e();
+      const uint32_t w0i = xr >> 5;
       const uint64_t W = (uint64_t)bw[w0i] | ((uint64_t)bw[w0i + 1] << 32);
-      const uint32_t rm = (uint32_t)(W >> sh) & (c >= 32 ? 0xFFFFFFFFu : (1u << c) - 1u);
+      const uint32_t rm = (uint32_t)(W >> (xr & 31u)) & (c >= 32 ? 0xFFFFFFFFu : (1u << c) - 1u);
       auto slots = [&](auto fastc) {
 #pragma unroll
         for (uint32_t q = 0; q < UG_NET; ++q) {
@@ -608,7 +624,6 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
       if (DEC || !fastp) slots(std::false_type{});
       else slots(std::true_type{});
     } else {  // a large leaf (rare)
-      const uint32_t G = (uint32_t)f.G;
       const uint32_t off = atomicAdd(alloc, c);
       uint64_t lk = 0;
       for (uint32_t a = 0;; ++a) {  // independent uniform offsets, sorted; redrawn on a duplicate
@@ -616,7 +631,7 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
           atomicOr(flags, FLAG_UNI);
           break;
         }
-        lk = uni_leafkey(u, lbase + l, a);
+        lk = uni_leafkey(u, gl, a);
         bool dup = false;
         if (off + c <= UG_SCR) {
           uint32_t* seg = scr + off;
@@ -638,6 +653,7 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
         }
         if (!dup) break;
       }
+      e = first_e();
       if (off + c <= UG_SCR) {
         for (uint32_t i = 0; i < c; ++i) emit(i, scr[off + i]);
       } else {  // no scratch left: the offsets in order by repeated minimum search
@@ -661,10 +677,9 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
   } else {
     // the tile element of leaf l's first kept candidate (l in [la, lb + 1])
     auto first_elem = [&](uint64_t l) -> int64_t {
-      const uint64_t x0 = pre[lg0 + l] - pbase;
-      const uint32_t w0i = (uint32_t)((x0 >> 5) - wlo), sh = (uint32_t)x0 & 31u;
-      const uint64_t remb = rem0 + rbw[w0i] + (uint64_t)__popc(bw[w0i] & ((1u << sh) - 1u));
-      return (int64_t)(x0 - remb) - (int64_t)f0;
+      const uint32_t xr = (uint32_t)(pre[lg0 + l] - pbase - (wlo << 5));
+      const uint32_t remr = rbw[xr >> 5] + (uint32_t)__popc(bw[xr >> 5] & ((1u << (xr & 31u)) - 1u));
+      return (int64_t)ebase + (int64_t)xr - (int64_t)remr;
     };
     auto key_of_leaf = [&](uint64_t l) { return leaf_key(uni_row(u, uni_leaf(u, lbase + l))); };
     // the reference's decode constants (fa_dec_digits): case 0 = ((w & am) != av) && w < alim
@@ -683,7 +698,9 @@ __device__ __forceinline__ void uni_stage(const UniSet* __restrict__ us, uint32_
         }
         l1 = lo;
       }
-      for (uint64_t l = l0 + threadIdx.x; l <= l1; l += NT) leaf(l, (uint32_t)(l - l0), K0);
+      // (a 32-bit loop over the round's slots: the leaf is l0 + its slot)
+      const uint32_t nr = (uint32_t)(l1 - l0);
+      for (uint32_t i = threadIdx.x; i <= nr; i += NT) leaf(l0 + i, i, K0);
       __syncthreads();
       // this round's elements: (slot, offset) -> the decoded word
       const int64_t ea = first_elem(l0), eb = first_elem(l1 + 1);
