@@ -320,6 +320,11 @@ int pluss_keyorder_index_range(const pluss_cfg *cfg, uint64_t seed, int32_t ref,
      pluss_group_gen_uniform_faithful  the same over r10's own law
                               (pluss_expand_uniform_sorted's lists; equal to
                               pluss_dev_gen_uniform_faithful_refs on one device)
+                              (both: one rank on one device captures a second
+                              identical call -- same seed and totals, no other
+                              group call between -- into a HIP graph without
+                              collectives and replays it for later ones;
+                              several ranks or devices: eager)
      pluss_group_expand       resident Feistel lists, each shard its slices of
                               counts[r] samples per reference (pluss_expand_samples)
      pluss_group_dense        `passes` dense passes over them (the bench step;

@@ -1614,7 +1614,7 @@ int faith_shards_uniform_count(pluss_ctx* ctx, uint64_t seed, const uint64_t* to
 // to the host (asynchronously: a caller driving several shards issues every
 // shard's window before waiting on any)
 int faith_shards_uniform_window(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards,
-                                hipStream_t s) {
+                                hipStream_t s, bool to_host) {
   if (int rc = shards_expect(ctx, SH_UCOUNT, "pluss_dev_faithful_shards_uniform_local", d_rows, shard, nshards))
     return rc;
   FaShards& f = *ctx->fsh2;
@@ -1624,23 +1624,29 @@ int faith_shards_uniform_window(pluss_ctx* ctx, const uint64_t* d_rows, int32_t 
   }
   if (int rc = uni_plan_remove(ctx, (const unsigned long long*)d_rows, (uint32_t)shard, (uint32_t)nshards, s))
     return rc;
-  PLUSS_HIP_CHECK(hipMemcpyAsync(ctx->ub.hinfo, ctx->ub.info, UI_W * 8, hipMemcpyDeviceToHost, s));
+  if (to_host) PLUSS_HIP_CHECK(hipMemcpyAsync(ctx->ub.hinfo, ctx->ub.info, UI_W * 8, hipMemcpyDeviceToHost, s));
   f.phase = SH_UWINDOW;
   return PLUSS_OK;
 }
 
 // ... then the shard's slice, its tile map and the local pass (phase 1)
-int faith_shards_uniform_finish(pluss_ctx* ctx, uint64_t* d_row, hipStream_t s) {
+int faith_shards_uniform_finish(pluss_ctx* ctx, uint64_t* d_row, hipStream_t s, const uint64_t* known) {
   if (!ctx->fsh2 || ctx->fsh2->phase != SH_UWINDOW) {
     set_error("pluss_dev_faithful_shards_uniform_local: out of order");
     return PLUSS_ERR_CONFIG;
   }
   FaShards& f = *ctx->fsh2;
-  PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+  const uint64_t* info = (const uint64_t*)ctx->ub.hinfo + 6;  // (first[6], n[6])
+  if (known) {
+    if (int rc = uni_slice_check(ctx, known, s)) return rc;
+    info = known;
+  } else {
+    PLUSS_HIP_CHECK(hipStreamSynchronize(s));
+  }
   FaRefs a = fa_none();
   uint64_t n[6];
   for (int r = 0; r < 6; ++r) {
-    const uint64_t first = ctx->ub.hinfo[6 + r], m = ctx->ub.hinfo[12 + r];
+    const uint64_t first = info[r], m = info[6 + r];
     n[r] = f.tot[r] && first <= f.tot[r] && m <= f.tot[r] - first ? m : 0;  // (a flagged plan: reported at the fetch)
     a.n[r] = n[r];
     a.ntot[r] = f.tot[r];

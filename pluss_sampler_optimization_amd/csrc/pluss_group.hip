@@ -115,6 +115,7 @@ constexpr int GB_FAIL = 15;  // (tail word: nonzero when the shard failed on the
 // met it).  A shard that fails on the host still sends its slot, with the
 // local-failure word set, so no rank waits in the all-reduce.
 constexpr int DVEC = 48;
+constexpr size_t MAX_RETIRED = 64;  // replaced graphs kept by a group (pluss_group::retired)
 enum : int { GV_BAD = 18, GV_COLD = 19, GV_PRES = 25, GV_TRAV = 31, GV_COND = 37, GV_W = 45 };
 enum : int { GC_LOCAL = 0, GC_BAD = 1, GC_OVERFLOW = 2, GC_LOOKBACK = 3, GC_SHARD = 4, GC_SORT = 5, GC_UNI = 6,
              GC_NONDENSE = 7 };
@@ -191,8 +192,9 @@ __global__ void k_group_block_tail(GTable g, unsigned long long* __restrict__ bl
 // host's launch rate, not the device, set the call's time.)
 struct FaGraph {
   bool have = false, seen = false;
-  int src = 0;
+  int src = 0;  // 0 generated (gen_faithful), 1 uniform (gen_uniform_faithful)
   uint64_t seed = 0, totals[6] = {0, 0, 0, 0, 0, 0};
+  std::vector<uint64_t> slice;  // (uniform) each local shard's slice from the last eager pass: first[6], n[6]
   hipGraphExec_t ex = nullptr;
 };
 
@@ -236,6 +238,14 @@ struct pluss_group {
   std::vector<pluss::PartBufs> part;      // per device: the any-order faithful pass
   std::map<uint32_t, hipGraphExec_t> graphs;  // dense passes captured per batch size (one local device)
   pluss::FaGraph* fg = nullptr;               // the last faithful pass, captured (pluss_group_gen_faithful)
+  // Replaced graphs, kept until the group is destroyed, never destroyed
+  // before: on this ROCm (7.2), the first hipGraphLaunch of a graph
+  // instantiated after another graph of the process was destroyed crashed
+  // inside the HIP runtime on the host, intermittently (r5m; r6x: a
+  // segmentation fault in hipGraphLaunch in round 1 of the replay probe;
+  // with replaced graphs kept, 20 of 20 rounds clean, r6y).  At most
+  // MAX_RETIRED: past that the group stops capturing and runs eagerly.
+  std::vector<hipGraphExec_t> retired;
   // A pass being captured into a HIP graph.  The rule, one for every rank
   // count: a one-rank group makes no RCCL call at all (every collective is
   // the identity there: each shard writes its block of the one buffer), so
@@ -262,6 +272,7 @@ static void group_free(pluss_group* G) {
     if (G->fg->ex) (void)hipGraphExecDestroy(G->fg->ex);
     delete G->fg;
   }
+  for (hipGraphExec_t e : G->retired) (void)hipGraphExecDestroy(e);
   for (size_t i = 0; i < G->ctx.size(); ++i) {
     if (i < G->list.size() && G->list[i]) (void)hipFree(G->list[i]);
     if (i < G->hl.size() && G->hl[i]) (void)hipFree(G->hl[i]);
@@ -490,7 +501,16 @@ static int group_faithful(pluss_group* G, const ShardFn& phase1, const ShardFn& 
   if (int rc = gather_blocks(G, G->rows, ROW_W)) return rc;
   if (mid1) {
     each(mid1);
-    if (mid2) each(mid2);
+    if (mid2) {
+      // mid1 reads every shard's gathered row, and mid2's local phase writes
+      // its own row into the same buffer: every local shard's mid1 first (the
+      // uniform window reads the candidate counts that a local phase's sample
+      // counts overwrite; without this join a captured 8-shard pass read them
+      // half overwritten, r6v)
+      if (int rc = join_shards(G)) return rc;
+      if (int rc = fork_shards(G)) return rc;
+      each(mid2);
+    }
     if (int rc = gather_blocks(G, G->rows, ROW_W)) return rc;
   }
   each([&](pluss_ctx* c, int d, int, int g, uint64_t* row) {
@@ -669,6 +689,86 @@ static int collect(pluss_group* G, GErr& E, pluss_hist* out) {
 // any other pass on the shards' handles: the next gen_faithful starts eagerly
 static void forget_faithful_graph(pluss_group* G) {
   if (G->fg) G->fg->seen = false;
+}
+
+// A faithful pass (source src: 0 generated, 1 uniform) run eagerly, captured
+// or replayed (FaGraph).  body(E, captured) enqueues the pass from the table
+// resets to its last phase; `extra`: whatever else a capture of this source
+// needs from the eager pass before it is present.  The capture rule of
+// pluss_group::capturing: one rank on one device only.
+static int graph_pass(pluss_group* G, int src, uint64_t seed, const uint64_t totals[6], bool extra, pluss_hist* out,
+                      const std::function<int(GErr&, bool)>& body) {
+  if (!G->fg) G->fg = new FaGraph();
+  FaGraph& F = *G->fg;
+  const bool one = G->ndev == 1 && G->nranks == 1;
+  const bool same =
+      F.seen && F.src == src && F.seed == seed && std::memcmp(F.totals, totals, sizeof F.totals) == 0 && extra;
+  if (one && same && F.have) {  // the captured pass, replayed
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
+    PLUSS_HIP_CHECK(hipGraphLaunch(F.ex, G->xs[0]));
+    GErr E;
+    return collect_finish(G, E, out);
+  }
+  if (F.ex) G->retired.push_back(F.ex);  // (kept, not destroyed: pluss_group::retired)
+  F.ex = nullptr;
+  F.have = false;
+  F.seen = true;
+  F.src = src;
+  F.seed = seed;
+  std::memcpy(F.totals, totals, sizeof F.totals);
+  // a second identical call is captured (the first ran eagerly and grew every
+  // buffer); one-rank groups only, without their identity collectives
+  const bool capture = one && same && G->m.fast && G->retired.size() < MAX_RETIRED;
+  if (capture) {
+    PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
+    PLUSS_HIP_CHECK(hipStreamBeginCapture(G->xs[0], hipStreamCaptureModeThreadLocal));
+    G->capturing = true;
+    for (auto* c : G->ctx) c->fb.capture = true;
+    if (int rc = fork_shards(G)) {  // (the shard streams join the capture)
+      hipGraph_t gr = nullptr;
+      (void)hipStreamEndCapture(G->xs[0], &gr);
+      if (gr) (void)hipGraphDestroy(gr);
+      G->capturing = false;
+      for (auto* c : G->ctx) c->fb.capture = false;
+      F.seen = false;
+      return rc;
+    }
+  }
+  GErr E;
+  group_reset(G, E);
+  int rc = body(E, capture);
+  if (!capture) {
+    if (rc || E.rc) F.seen = false;  // (a failed pass is not captured next)
+    return rc ? rc : collect(G, E, out);
+  }
+  if (!rc) rc = collect_enqueue(G, E);
+  if (!rc) rc = join_shards(G);  // (every forked stream rejoins before the capture ends)
+  hipGraph_t gr = nullptr;
+  const hipError_t ce = hipStreamEndCapture(G->xs[0], &gr);
+  G->capturing = false;
+  for (auto* c : G->ctx) c->fb.capture = false;
+  if (!rc && !E.rc && ce == hipSuccess) {
+    const hipError_t ie = hipGraphInstantiate(&F.ex, gr, nullptr, nullptr, 0);
+    if (ie != hipSuccess) {
+      F.ex = nullptr;
+      set_error(std::string("faithful group pass: graph instantiate: ") + hipGetErrorString(ie));
+      rc = PLUSS_ERR_HIP;
+    }
+  } else if (!rc && !E.rc) {
+    set_error(std::string("faithful group pass: graph capture: ") + hipGetErrorString(ce));
+    rc = PLUSS_ERR_HIP;
+  }
+  if (gr) (void)hipGraphDestroy(gr);
+  F.seen = false;  // (a failed capture starts over; nothing of it ran)
+  if (rc) return rc;
+  if (E.rc) {
+    set_error(E.msg);
+    return E.rc;
+  }
+  F.seen = true;
+  F.have = true;
+  PLUSS_HIP_CHECK(hipGraphLaunch(F.ex, G->xs[0]));
+  return collect_finish(G, E, out);
 }
 
 // a device buffer of at least `bytes` (the device's streams drained before it is replaced)
@@ -1051,7 +1151,7 @@ static int drop_graphs(pluss_group* G) {
     PLUSS_HIP_CHECK(hipSetDevice(G->dev[d]));
     PLUSS_HIP_CHECK(hipStreamSynchronize(G->xs[d]));
   }
-  for (auto& kv : G->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : G->graphs) G->retired.push_back(kv.second);  // (kept: pluss_group::retired)
   G->graphs.clear();
   return PLUSS_OK;
 }
@@ -1110,7 +1210,8 @@ int pluss_group_dense(pluss_group* G, uint32_t passes, uint64_t counts[PLUSS_DEN
   }
   constexpr uint32_t BATCH = 16;  // passes per captured graph
   uint32_t left = passes;
-  if (G->ndev == 1 && G->nranks == 1 && lists && left >= BATCH) {
+  if (G->ndev == 1 && G->nranks == 1 && lists && left >= BATCH &&
+      (G->graphs.count(BATCH) || G->retired.size() < MAX_RETIRED)) {
     // one rank, one local device: BATCH passes replayed from one HIP graph
     // (kernels and the shard sums; the all-reduce, the identity, left out)
     PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
@@ -1257,110 +1358,60 @@ int pluss_group_gen_faithful(pluss_group* G, uint64_t seed, const uint64_t total
   if (!G || !totals || !out) return PLUSS_ERR_CONFIG;
   uint64_t key_end = 0;
   if (int rc = pluss_faithful_key_space(&G->cfg, &key_end)) return rc;  // (the same on every rank)
-  if (!G->fg) G->fg = new FaGraph();
-  FaGraph& F = *G->fg;
-  const bool same = F.seen && F.src == 0 && F.seed == seed && std::memcmp(F.totals, totals, sizeof F.totals) == 0;
-  if (G->ndev == 1 && G->nranks == 1 && same && F.have) {  // the captured pass, replayed
-    PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
-    PLUSS_HIP_CHECK(hipGraphLaunch(F.ex, G->xs[0]));
-    GErr E;
-    return collect_finish(G, E, out);
-  }
-  if (F.ex) (void)hipGraphExecDestroy(F.ex);
-  F.ex = nullptr;
-  F.have = false;
-  F.seen = true;
-  F.src = 0;
-  F.seed = seed;
-  std::memcpy(F.totals, totals, sizeof F.totals);
-  // a second identical call is captured (the first ran eagerly and grew every
-  // buffer); one-rank groups only, without their identity collectives (the
-  // capture rule at pluss_group::capturing)
-  const bool capture = G->ndev == 1 && G->nranks == 1 && same && G->m.fast;
-  if (capture) {
-    PLUSS_HIP_CHECK(hipSetDevice(G->dev[0]));
-    PLUSS_HIP_CHECK(hipStreamBeginCapture(G->xs[0], hipStreamCaptureModeThreadLocal));
-    G->capturing = true;
-    for (auto* c : G->ctx) c->fb.capture = true;
-    if (int rc = fork_shards(G)) {  // (the shard streams join the capture)
-      hipGraph_t gr = nullptr;
-      (void)hipStreamEndCapture(G->xs[0], &gr);
-      if (gr) (void)hipGraphDestroy(gr);
-      G->capturing = false;
-      for (auto* c : G->ctx) c->fb.capture = false;
-      F.seen = false;
-      return rc;
-    }
-  }
-  GErr E;
-  group_reset(G, E);
   const int S = G->nshards;
-  ShardFn gen = [&](pluss_ctx* c, int, int, int g, uint64_t* row) -> int {
-    const uint64_t lo = (uint64_t)((unsigned __int128)key_end * g / S);
-    const uint64_t hi = (uint64_t)((unsigned __int128)key_end * (g + 1) / S);
-    uint64_t f[6] = {0, 0, 0, 0, 0, 0}, m[6] = {0, 0, 0, 0, 0, 0};
-    for (int r = 0; r < 6; ++r) {
-      if (!totals[r]) continue;
-      uint64_t a = 0, b = 0;
-      if (int rc = pluss_keyorder_index_range(&G->cfg, seed, r, totals[r], lo, hi, &a, &b)) return rc;
-      f[r] = a;
-      m[r] = b - a;
-    }
-    return pluss_dev_faithful_shards_local(c, nullptr, seed, totals, f, m, row, c->stream);
-  };
-  int rc = group_faithful(G, gen, nullptr, nullptr, E);
-  if (!capture) return rc ? rc : collect(G, E, out);
-  if (!rc) rc = collect_enqueue(G, E);
-  if (!rc) rc = join_shards(G);  // (every forked stream rejoins before the capture ends)
-  hipGraph_t gr = nullptr;
-  const hipError_t ce = hipStreamEndCapture(G->xs[0], &gr);
-  G->capturing = false;
-  for (auto* c : G->ctx) c->fb.capture = false;
-  if (!rc && !E.rc && ce == hipSuccess) {
-    const hipError_t ie = hipGraphInstantiate(&F.ex, gr, nullptr, nullptr, 0);
-    if (ie != hipSuccess) {
-      F.ex = nullptr;
-      set_error(std::string("pluss_group_gen_faithful: graph instantiate: ") + hipGetErrorString(ie));
-      rc = PLUSS_ERR_HIP;
-    }
-  } else if (!rc && !E.rc) {
-    set_error(std::string("pluss_group_gen_faithful: graph capture: ") + hipGetErrorString(ce));
-    rc = PLUSS_ERR_HIP;
-  }
-  if (gr) (void)hipGraphDestroy(gr);
-  F.seen = false;  // (a failed capture starts over; nothing of it ran)
-  if (rc) return rc;
-  if (E.rc) {
-    set_error(E.msg);
-    return E.rc;
-  }
-  F.seen = true;
-  F.have = true;
-  PLUSS_HIP_CHECK(hipGraphLaunch(F.ex, G->xs[0]));
-  return collect_finish(G, E, out);
+  return graph_pass(G, 0, seed, totals, true, out, [&](GErr& E, bool) {
+    ShardFn gen = [&](pluss_ctx* c, int, int, int g, uint64_t* row) -> int {
+      const uint64_t lo = (uint64_t)((unsigned __int128)key_end * g / S);
+      const uint64_t hi = (uint64_t)((unsigned __int128)key_end * (g + 1) / S);
+      uint64_t f[6] = {0, 0, 0, 0, 0, 0}, m[6] = {0, 0, 0, 0, 0, 0};
+      for (int r = 0; r < 6; ++r) {
+        if (!totals[r]) continue;
+        uint64_t a = 0, b = 0;
+        if (int rc = pluss_keyorder_index_range(&G->cfg, seed, r, totals[r], lo, hi, &a, &b)) return rc;
+        f[r] = a;
+        m[r] = b - a;
+      }
+      return pluss_dev_faithful_shards_local(c, nullptr, seed, totals, f, m, row, c->stream);
+    };
+    return group_faithful(G, gen, nullptr, nullptr, E);
+  });
 }
 
 int pluss_group_gen_uniform_faithful(pluss_group* G, uint64_t seed, const uint64_t totals[6], pluss_hist* out) {
   if (!G || !totals || !out) return PLUSS_ERR_CONFIG;
-  forget_faithful_graph(G);
   uint64_t key_end = 0;
   if (int rc = pluss_faithful_key_space(&G->cfg, &key_end)) return rc;  // (the same on every rank)
-  GErr E;
-  group_reset(G, E);
-  const int S = G->nshards;
-  // phase 0: each shard's candidates; then every shard's window (enqueued on
-  // all shards before any waits for its slice), then each local pass
-  ShardFn count = [&](pluss_ctx* c, int, int, int g, uint64_t* row) {
-    return faith_shards_uniform_count(c, seed, totals, g, S, row, c->stream);
-  };
-  ShardFn window = [&](pluss_ctx* c, int d, int, int g, uint64_t*) {
-    return faith_shards_uniform_window(c, (const uint64_t*)G->rows[d], g, S, c->stream);
-  };
-  ShardFn finish = [&](pluss_ctx* c, int, int, int, uint64_t* row) {
-    return faith_shards_uniform_finish(c, row, c->stream);
-  };
-  if (int rc = group_faithful(G, count, window, finish, E)) return rc;
-  return collect(G, E, out);
+  const int S = G->nshards, local = G->ndev * G->spd;
+  if (!G->fg) G->fg = new FaGraph();
+  FaGraph& F = *G->fg;
+  // a captured pass takes each shard's slice from the eager pass before it:
+  // the one mid-pass read-back (the slice sizes the local pass's grids) is
+  // what kept this pass from being captured
+  const bool slices = F.slice.size() == (size_t)local * 12;
+  return graph_pass(G, 1, seed, totals, slices, out, [&](GErr& E, bool captured) {
+    // phase 0: each shard's candidates; then every shard's window (enqueued on
+    // all shards before any waits for its slice), then each local pass
+    ShardFn count = [&](pluss_ctx* c, int, int, int g, uint64_t* row) {
+      return faith_shards_uniform_count(c, seed, totals, g, S, row, c->stream);
+    };
+    ShardFn window = [&](pluss_ctx* c, int d, int, int g, uint64_t*) {
+      return faith_shards_uniform_window(c, (const uint64_t*)G->rows[d], g, S, c->stream, !captured);
+    };
+    ShardFn finish = [&](pluss_ctx* c, int d, int j, int, uint64_t* row) {
+      return faith_shards_uniform_finish(c, row, c->stream,
+                                         captured ? F.slice.data() + ((size_t)d * G->spd + j) * 12 : nullptr);
+    };
+    const int rc = group_faithful(G, count, window, finish, E);
+    if (!captured && !rc) {  // (the eager pass waited for every slice: kept for the capture)
+      F.slice.assign((size_t)local * 12, 0);
+      for (int d = 0; d < G->ndev; ++d)
+        for (int j = 0; j < G->spd; ++j) {
+          const uint64_t* h = (const uint64_t*)shard(G, d, j)->ub.hinfo;
+          if (h) std::memcpy(F.slice.data() + ((size_t)d * G->spd + j) * 12, h + 6, 12 * 8);
+        }
+    }
+    return rc;
+  });
 }
 
 }  // extern "C"

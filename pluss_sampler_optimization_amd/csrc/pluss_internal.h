@@ -224,9 +224,13 @@ int faith_shards_hist(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int
 // the window (enqueued, slice read back asynchronously) and the local pass
 int faith_shards_uniform_count(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, int32_t shard, int32_t nshards,
                                uint64_t* d_row, hipStream_t s);
+// (known: the slice's 12 raw info words -- first[6], n[6] -- from an earlier
+// identical pass: no read-back, nothing waits on the host, and the device's
+// own values are checked against them (FLAG_UNI on a difference); the window
+// then skips its copy to the host (to_host false).  A group's captured pass.)
 int faith_shards_uniform_window(pluss_ctx* ctx, const uint64_t* d_rows, int32_t shard, int32_t nshards,
-                                hipStream_t s);
-int faith_shards_uniform_finish(pluss_ctx* ctx, uint64_t* d_row, hipStream_t s);
+                                hipStream_t s, bool to_host = true);
+int faith_shards_uniform_finish(pluss_ctx* ctx, uint64_t* d_row, hipStream_t s, const uint64_t* known = nullptr);
 int faith_shards_slice(pluss_ctx* ctx, uint64_t* first, uint64_t* n);
 void faith_shards_abandon(pluss_ctx* ctx);
 // r10's uniform draw in key order (pluss_uniform.h / .hip)
@@ -235,6 +239,8 @@ int uni_plan(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, hipStream_t 
 int uni_plan_count(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, uint32_t shard, uint32_t ns, hipStream_t s);
 int uni_plan_remove(pluss_ctx* ctx, const unsigned long long* rows, uint32_t shard, uint32_t ns, hipStream_t s);
 int uni_plan_tiles(pluss_ctx* ctx, const uint64_t* n, hipStream_t s, const UniSet** out);
+// the plan's slice words (info[6, 18)) checked against known values (FLAG_UNI on a difference)
+int uni_slice_check(pluss_ctx* ctx, const uint64_t* known, hipStream_t s);
 void uni_free(pluss_ctx* ctx);
 int diag_uniform_parts(pluss_ctx* ctx, uint64_t seed, const uint64_t* totals, int32_t what, uint64_t* d_out,
                        hipStream_t s);

@@ -274,6 +274,22 @@ __global__ void k_ug_info(const UniSet* __restrict__ us, const unsigned long lon
   info[12 + r] = n;
 }
 
+// a replayed shard pass took its slice from an earlier identical pass: the
+// device's own values must be the same (they are a function of the seed, the
+// budget and the shard), else the pass reports a uniform-plan failure
+struct UniSlice {
+  unsigned long long w[12];  // first[6], n[6]
+};
+__global__ void k_ug_slice_check(const unsigned long long* __restrict__ info, UniSlice e, unsigned int* flags) {
+  const uint32_t k = threadIdx.x;
+  if (k < 12 && info[6 + k] != e.w[k]) {
+    atomicOr(flags, FLAG_UNI);
+#ifdef PLUSS_DEBUG_STAGES
+    printf("uniform slice check: word %u device %llu known %llu\n", k, info[6 + k], e.w[k]);
+#endif
+  }
+}
+
 // per leaf: the sample index of its first surviving candidate and their
 // number; the leaf holding each tile's first sample
 __global__ __launch_bounds__(UB) void k_ug_tiles(const UniSet* __restrict__ us, uint32_t* __restrict__ tmap) {
@@ -481,6 +497,15 @@ int uni_plan_tiles(pluss_ctx* ctx, const uint64_t* n, hipStream_t s, const UniSe
   hipLaunchKernelGGL(k_ug_tiles, dim3(grid), dim3(UB), 0, s, (const UniSet*)b.set, b.tmap);
   PLUSS_HIP_CHECK(hipGetLastError());
   *out = b.set;
+  return PLUSS_OK;
+}
+
+int uni_slice_check(pluss_ctx* ctx, const uint64_t* known, hipStream_t s) {
+  UniSlice e;
+  for (int k = 0; k < 12; ++k) e.w[k] = known[k];
+  hipLaunchKernelGGL(k_ug_slice_check, dim3(1), dim3(64), 0, s, (const unsigned long long*)ctx->ub.info, e,
+                     ctx->g.flags);
+  PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }
 

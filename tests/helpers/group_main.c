@@ -178,7 +178,15 @@ int main(int argc, char** argv) {
     CHECK(pluss_dev_hist_reset(c, NULL));
     CHECK(pluss_dev_gen_uniform_faithful_refs(c, seed, counts, NULL));
     CHECK(pluss_hist_fetch(c, &u2));
-    report("faithful gen_uniform_faithful (r10's law)", same_hist(&u1, &u2));
+    /* the same call again: captured, then replayed (one device), each equal */
+    int same_u = same_hist(&u1, &u2);
+    for (int k = 0; k < 3; ++k) {
+      free(u1.entries);
+      u1 = new_hist();
+      CHECK(pluss_group_gen_uniform_faithful(g, seed, counts, &u1));
+      same_u = same_u && same_hist(&u1, &u2);
+    }
+    report("faithful gen_uniform_faithful (r10's law)", same_u);
     free(u1.entries);
     free(u2.entries);
     pluss_ctx_destroy(c);

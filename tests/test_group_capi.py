@@ -171,6 +171,39 @@ def test_group_faithful_replays_equal_one_device(spd):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("spd", [1, 3, 8])
+def test_group_uniform_replays_equal_one_device(spd):
+    """Repeated identical pluss_group_gen_uniform_faithful calls: the first
+    eager (it reads every shard's slice back), the second captured with those
+    slices (no read-back, the device's own slice checked against them), later
+    ones replayed; each equals the one-device uniform pass.  A different seed
+    in between runs eagerly; a generated pass in between drops the graph."""
+    P = _P()
+    import torch
+    N, T = 1024, 8
+    c = P.SamplerConfig(n=N, threads=T, mode="faithful")
+    totals = P.default_counts(N, 1 << 22)
+    st = torch.cuda.Stream()
+
+    def one(seed):
+        with P.Context(c) as ctx:
+            ctx.reset(st.cuda_stream)
+            ctx.gen_uniform_faithful_refs(seed, totals, st.cuda_stream)
+            st.synchronize()
+            return ctx.fetch()
+    a, b = one(21), one(22)
+    with P.Group(c, [0], spd) as g:
+        for seed in (21, 21, 21, 21, 22, 21, 21, 21):
+            h = g.gen_uniform_faithful(seed, totals)
+            w = a if seed == 21 else b
+            assert h.bins == w.bins and h.traversed == w.traversed, seed
+        g.gen_faithful(21, totals)  # another pass on the same handles
+        for _ in range(3):
+            h = g.gen_uniform_faithful(21, totals)
+            assert h.bins == a.bins and h.traversed == a.traversed
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spd", [1, 3, 8])
 @pytest.mark.parametrize("N,total", [(1024, 1 << 20), (2048, 1 << 20)])
 def test_group_any_order_equals_one_device(N, total, spd):
     """r10's any-order input through the group, partitioned on the device by
