@@ -43,6 +43,8 @@ CONFIGS = {
 }
 
 
+_KEPT_GRAPHS = []  # HIP graphs kept alive until the process exits (r5m)
+
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -773,7 +775,9 @@ def main():
     # per G steps instead of a Python launch per step) when a step holds no
     # collective.  With N>1 every step's all-reduce is issued eagerly: no RCCL
     # call is ever captured into a graph (the library's capture rule, DESIGN.md
-    # section 8: a replayed capture holding RCCL calls crashed on the host, r5m).
+    # section 8).  The graphs are kept alive to the end of the run: on this
+    # ROCm a graph launched after another graph was destroyed crashed inside
+    # the HIP runtime (r5m).
     graphs = []  # (graph, steps, vector of its last step)
     launch_mode = "eager (one c10d all_reduce per step, asynchronous)" if collective else "eager"
     if args.graph and not collective:
@@ -818,6 +822,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    _KEPT_GRAPHS.extend(graphs)  # (never destroyed before exit: see above)
     kern_ms = e0.elapsed_time(e1) / args.steps
     # correctness of the (merged) histogram: every sample of every rank is counted once
     dv = dense[last].cpu().numpy()  # the last step's (merged) histogram
