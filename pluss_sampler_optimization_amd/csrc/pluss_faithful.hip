@@ -1333,19 +1333,19 @@ __global__ __launch_bounds__(PT_NT) void k_fa_part(Model m, const uint64_t* __re
                                                    const unsigned long long* __restrict__ bounds, uint32_t S,
                                                    uint32_t* __restrict__ hist, uint32_t B,
                                                    const unsigned long long* __restrict__ rstart, KT* __restrict__ out,
-                                                   GTable g) {
+                                                   GTable g, uint32_t boff) {
   extern __shared__ unsigned long long pt_lds[];
   unsigned long long* lb = pt_lds;                       // S + 1 bounds
   uint32_t* lc = (uint32_t*)(pt_lds + S + 1);            // per bin: the block's count so far
   unsigned long long* lbase = pt_lds + S + 1 + (part_bins(S) + 1) / 2;  // scatter: per bin its base
-  const uint32_t nb = part_bins(S), b = blockIdx.x;
+  const uint32_t nb = part_bins(S), b = boff + blockIdx.x;
   for (uint32_t i = threadIdx.x; i <= S; i += PT_NT) lb[i] = bounds[i];
   for (uint32_t i = threadIdx.x; i < nb; i += PT_NT) {
     lc[i] = 0;
     if (!COUNT) lbase[i] = rstart[i] + hist[(size_t)i * B + b];
   }
   __syncthreads();
-  const uint64_t lo = n * b / B, hi = n * (b + 1) / B;  // (n < 2^40, B <= 4096)
+  const uint64_t lo = n * b / B, hi = n * (b + 1) / B;  // (n < 2^40, B <= 16384: no overflow)
   const uint32_t lane = __lane_id();
   for (uint64_t base = lo; base < hi; base += PT_NT) {
     const uint64_t i = base + threadIdx.x;
@@ -1442,7 +1442,9 @@ __global__ __launch_bounds__(PT_NT) void k_fa_seg_copy(const unsigned long long*
 uint32_t faith_part_blocks(uint64_t n, uint32_t S) {
   uint64_t B = n / 16384;  // >= 16K samples per workgroup
   const uint64_t cap = std::max<uint64_t>(1, ((uint64_t)1 << 22) / part_bins(S));  // hist <= 16 MB
-  B = std::min<uint64_t>(std::min<uint64_t>(B, 4096), cap);
+  // (up to 16K workgroups: the group counts its slice in 8 upload pieces, and
+  // a piece of 2^25 samples over 512 workgroups of 64K ran at 0.8 TB/s, r6ab)
+  B = std::min<uint64_t>(std::min<uint64_t>(B, 16384), cap);
   return (uint32_t)std::max<uint64_t>(B, 1);
 }
 
@@ -1466,19 +1468,23 @@ int faith_word_bytes(const pluss_ctx* ctx) {
 static size_t part_lds(uint32_t S) { return 8 * ((size_t)S + 1 + (part_bins(S) + 1) / 2 + part_bins(S)); }
 
 int faith_part_count(pluss_ctx* ctx, const uint64_t* d_smp, uint64_t n, const unsigned long long* d_bounds,
-                     uint32_t S, uint32_t* d_hist, uint32_t B, unsigned long long* d_tot, hipStream_t s) {
+                     uint32_t S, uint32_t* d_hist, uint32_t B, unsigned long long* d_tot, hipStream_t s, uint32_t b0,
+                     uint32_t b1, bool scan) {
   if (S < 1 || S > 1024 || part_lds(S) > 64 * 1024) {
     set_error("faithful partition: at most 1024 shards");
     return PLUSS_ERR_CONFIG;
   }
-  if (faith_word_bytes(ctx) == 4)
-    hipLaunchKernelGGL((k_fa_part<true, uint32_t>), dim3(B), dim3(PT_NT), part_lds(S), s, ctx->m, d_smp, n, d_bounds, S,
-                       d_hist, B, (const unsigned long long*)nullptr, (uint32_t*)nullptr, ctx->g);
-  else
-    hipLaunchKernelGGL((k_fa_part<true, unsigned long long>), dim3(B), dim3(PT_NT), part_lds(S), s, ctx->m, d_smp, n,
-                       d_bounds, S, d_hist, B, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                       ctx->g);
-  hipLaunchKernelGGL(k_fa_part_scan, dim3(part_bins(S)), dim3(PT_NT), 0, s, d_hist, B, d_tot);
+  if (b1 > B) b1 = B;
+  if (b0 < b1) {
+    if (faith_word_bytes(ctx) == 4)
+      hipLaunchKernelGGL((k_fa_part<true, uint32_t>), dim3(b1 - b0), dim3(PT_NT), part_lds(S), s, ctx->m, d_smp, n,
+                         d_bounds, S, d_hist, B, (const unsigned long long*)nullptr, (uint32_t*)nullptr, ctx->g, b0);
+    else
+      hipLaunchKernelGGL((k_fa_part<true, unsigned long long>), dim3(b1 - b0), dim3(PT_NT), part_lds(S), s, ctx->m,
+                         d_smp, n, d_bounds, S, d_hist, B, (const unsigned long long*)nullptr,
+                         (unsigned long long*)nullptr, ctx->g, b0);
+  }
+  if (scan) hipLaunchKernelGGL(k_fa_part_scan, dim3(part_bins(S)), dim3(PT_NT), 0, s, d_hist, B, d_tot);
   PLUSS_HIP_CHECK(hipGetLastError());
   ctx->tables_dirty = true;
   return PLUSS_OK;
@@ -1489,10 +1495,10 @@ int faith_part_scatter(pluss_ctx* ctx, const uint64_t* d_smp, uint64_t n, const 
                        hipStream_t s) {
   if (faith_word_bytes(ctx) == 4)
     hipLaunchKernelGGL((k_fa_part<false, uint32_t>), dim3(B), dim3(PT_NT), part_lds(S), s, ctx->m, d_smp, n, d_bounds,
-                       S, d_hist, B, d_rstart, (uint32_t*)d_out, ctx->g);
+                       S, d_hist, B, d_rstart, (uint32_t*)d_out, ctx->g, 0u);
   else
     hipLaunchKernelGGL((k_fa_part<false, unsigned long long>), dim3(B), dim3(PT_NT), part_lds(S), s, ctx->m, d_smp, n,
-                       d_bounds, S, d_hist, B, d_rstart, (unsigned long long*)d_out, ctx->g);
+                       d_bounds, S, d_hist, B, d_rstart, (unsigned long long*)d_out, ctx->g, 0u);
   PLUSS_HIP_CHECK(hipGetLastError());
   return PLUSS_OK;
 }

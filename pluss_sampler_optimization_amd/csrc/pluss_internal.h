@@ -206,8 +206,12 @@ int faith_shards_local_selected(pluss_ctx* ctx, const uint64_t* d_rows, int32_t 
 // device (the group's any-order faithful pass), and phase 1 over the words
 uint32_t faith_part_blocks(uint64_t n, uint32_t S);
 int faith_word_bytes(const pluss_ctx* ctx);
+// (the count over workgroup blocks [b0, b1) of the B, and the bins' scan and
+// totals when `scan`: the whole count is [0, B) with the scan; a caller that
+// uploads the list in pieces counts each piece's blocks as it lands)
 int faith_part_count(pluss_ctx* ctx, const uint64_t* d_smp, uint64_t n, const unsigned long long* d_bounds,
-                     uint32_t S, uint32_t* d_hist, uint32_t B, unsigned long long* d_tot, hipStream_t s);
+                     uint32_t S, uint32_t* d_hist, uint32_t B, unsigned long long* d_tot, hipStream_t s,
+                     uint32_t b0 = 0, uint32_t b1 = ~0u, bool scan = true);
 int faith_part_scatter(pluss_ctx* ctx, const uint64_t* d_smp, uint64_t n, const unsigned long long* d_bounds,
                        uint32_t S, uint32_t* d_hist, uint32_t B, const unsigned long long* d_rstart, void* d_out,
                        hipStream_t s);
