@@ -216,6 +216,9 @@ int pluss_ctx_destroy(pluss_ctx* c) {
       if (p) (void)hipFree(p);
   }
   uni_free(c);
+  if (c->fb.side) (void)hipStreamDestroy(c->fb.side);
+  for (hipEvent_t e : c->fb.sev)
+    if (e) (void)hipEventDestroy(e);
   for (int r = 0; r < 6; ++r)
     if (c->fst[r]) (void)hipStreamDestroy(c->fst[r]);
   for (int e = 0; e < 7; ++e)

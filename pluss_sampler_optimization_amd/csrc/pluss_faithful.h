@@ -1547,12 +1547,12 @@ template <int SRC, bool CHECK>
 __global__ __launch_bounds__(fa_lm_nt<SRC>()) __attribute__((amdgpu_waves_per_eu(fa_lm_waves<SRC>()))) void k_fa_local_lm(Model m, FaRefs a, unsigned long long* __restrict__ tmax,
                                                     unsigned long long* __restrict__ part,
                                                     unsigned long long* __restrict__ klist, unsigned long long* slots,
-                                                    unsigned int* slowq, GTable g) {
+                                                    unsigned int* slowq, GTable g, uint32_t g0) {
   static_assert(fa_lm<SRC>(), "the stratified generated source: k_fa_local_fast");
   constexpr int NT = fa_lm_nt<SRC>();
   __shared__ FaLmLds<SRC> L;
   FaLm<NT>& sh = L.s;
-  const FaTile T = fa_tile(a, blockIdx.x);
+  const FaTile T = fa_tile(a, g0 + blockIdx.x);  // (g0: tiles before it run elsewhere, FaLaunch::side)
   fa_cold_slot(T, g, slots);
   unsigned long long* kl_out = klist + T.gt * (uint64_t)(2 * KL);
   bool done = false;
@@ -1573,7 +1573,7 @@ __global__ __launch_bounds__(fa_lm_nt<SRC>()) __attribute__((amdgpu_waves_per_eu
     }
     // the tile's constants read again for the scan (an opaque tile number: held
     // through the staging, they pushed it past 128 VGPRs into scratch)
-    uint32_t bid = blockIdx.x;
+    uint32_t bid = g0 + blockIdx.x;
     asm volatile("" : "+s"(bid));
     const FaTile T2 = fa_tile(a, bid);
     unsigned long long* kl2 = klist + T2.gt * (uint64_t)(2 * KL);
@@ -1587,7 +1587,7 @@ __global__ __launch_bounds__(fa_lm_nt<SRC>()) __attribute__((amdgpu_waves_per_eu
     PLUSS_FA_REFS(PLUSS_FA_LM)
 #undef PLUSS_FA_LM
   }
-  const uint64_t gt = blockIdx.x;  // (== T.gt)
+  const uint64_t gt = g0 + blockIdx.x;  // (== T.gt)
   if (done) {
     if (threadIdx.x < FPW) part[gt * FPW + threadIdx.x] = sh.out[threadIdx.x];
     if (threadIdx.x == FPW) tmax[gt] = sh.out[FPW];
@@ -2097,6 +2097,7 @@ struct FaLaunch {
   int phase;      // FA_PH_*
   hipStream_t s;
   unsigned long long* row;  // a key-range shard's summary row (FA_PH_CUT writes its cut candidates)
+  uint32_t side = 0;        // (SRC_UNI) tiles [0, side) -- the sparse 2-D references' -- on b->side
 };
 
 // phases of the pipeline: 1 local pass, 2 chunks (carry, fix-up), 3 finish
@@ -2117,15 +2118,26 @@ inline void fa_launch_t(const FaLaunch& L) {
         // (a pass whose chunk phase ran left it empty: no fill launch then)
         if (!b.slowq_clean) (void)hipMemsetAsync(b.slowq, 0, sizeof(unsigned int), L.s);
         b.slowq_clean = false;
+        const uint32_t t0 = SRC == SRC_UNI && L.side < t ? L.side : 0u;
+        if (t0) {  // the sparse references' tiles: the generic pass on the side stream, beside the lane-major one
+          (void)hipEventRecord(b.sev[0], L.s);
+          (void)hipStreamWaitEvent(b.side, b.sev[0], 0);
+          hipLaunchKernelGGL((k_fa_local<SRC, P2, CHK, false>), dim3(t0), dim3(TB), 0, b.side, L.m, L.a, b.tmax,
+                             b.dpart, b.klist, b.fslot, (unsigned int*)nullptr, L.g);
+        }
         if constexpr (fa_lm<SRC>())
-          hipLaunchKernelGGL((k_fa_local_lm<SRC, CHK>), dim3(t), dim3(fa_lm_nt<SRC>()), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
-                             b.fslot, b.slowq, L.g);
+          hipLaunchKernelGGL((k_fa_local_lm<SRC, CHK>), dim3(t - t0), dim3(fa_lm_nt<SRC>()), 0, L.s, L.m, L.a, b.tmax, b.dpart, b.klist,
+                             b.fslot, b.slowq, L.g, t0);
         else
           hipLaunchKernelGGL((k_fa_local_fast<SRC, CHK>), dim3(t), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart,
                              b.klist, b.fslot, b.slowq, L.g);
         PLUSS_STAGE(L.s, "pipeline: local fast pass");
         hipLaunchKernelGGL((k_fa_local<SRC, P2, CHK, true>), dim3(nres), dim3(TB), 0, L.s, L.m, L.a, b.tmax, b.dpart,
                            b.klist, b.fslot, b.slowq, L.g);
+        if (t0) {  // (joined before the chunk pass reads every tile's record)
+          (void)hipEventRecord(b.sev[1], b.side);
+          (void)hipStreamWaitEvent(L.s, b.sev[1], 0);
+        }
         PLUSS_STAGE(L.s, "pipeline: queued pass");
         fast = true;
       }

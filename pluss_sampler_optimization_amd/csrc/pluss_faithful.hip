@@ -918,6 +918,22 @@ static int fa_prepare(pluss_ctx* ctx, FaRefs& a, int src, bool check, bool shard
               (uint64_t)m.N * m.S * m.T < (1ull << 32)) ? 1u : 0u;
   *out = FaLaunch{m, a, ctx->g, &b, p2, t, 0, FA_PH_ALL, s, nullptr};
   if (t == 0) return PLUSS_OK;
+  // the uniform source's 2-D references, whose tiles span more than 2^32 keys
+  // when the lists are sparse in them (C0 / C1 at every BASELINE shape): every
+  // such tile left the lane-major pass for the queued one, which regenerated
+  // it after the lane-major pass, ~0.1 ms at config 3 (r6r).  They run on a
+  // second stream beside it instead (FaLaunch::side).
+  if (src == SRC_UNI && a.fast && a.unidec && a.toff[2] > 0 && a.toff[2] < t) {
+    bool sparse = false;
+    for (int r = 0; r < 2; ++r)
+      sparse |= a.n[r] > 0 && (unsigned __int128)m.A * m.T * TILE > ((unsigned __int128)a.ntot[r] << 32);
+    if (sparse && !b.side && !b.capture) {  // (made on an eager pass: a capture only reuses them)
+      if (hipStreamCreateWithFlags(&b.side, hipStreamNonBlocking) != hipSuccess) b.side = nullptr;
+      for (hipEvent_t& e : b.sev)
+        if (b.side && !e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    }
+    if (sparse && b.side && b.sev[0] && b.sev[1]) out->side = (uint32_t)a.toff[2];
+  }
   if (int rc = fa_reserve(b, t, c, s)) return rc;
   if (!b.shrec) {
     if (int rc = grow(&b.shrec, 6 * SRW + 16)) return rc;

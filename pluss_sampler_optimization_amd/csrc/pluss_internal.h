@@ -86,6 +86,10 @@ struct FaithfulBufs {
   // the radix source's bucket sort (pluss_sort.h): its histograms, parents, chunk map, deep items
   uint64_t sbcap = 0;
   unsigned char* sbuf = nullptr;
+  // the uniform source's sparse-reference tiles, run beside the lane-major pass
+  // (fa_launch_t): a second stream and its fork / join events, made on first use
+  hipStream_t side = nullptr;
+  hipEvent_t sev[2] = {nullptr, nullptr};
 };
 
 struct UniSet;  // the uniform key-order generator's plan (pluss_uniform.h)
