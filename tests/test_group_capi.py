@@ -203,6 +203,32 @@ def test_group_uniform_replays_equal_one_device(spd):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("spd", [1, 8])
+def test_group_uniform_replays_sparse_2d_references(spd):
+    """N=4096 with the BASELINE budget of the 2-D references (1% of (N-1)^2):
+    their tiles span more than 2^32 keys, so eager passes run them on the
+    handle's side stream and captured passes queue them (the side stream
+    inside a captured pass crashed the bench on the host, r6ah); repeated
+    group calls -- eager, captured, replayed -- equal the one-device pass."""
+    P = _P()
+    import torch
+    N, T = 4096, 8
+    c = P.SamplerConfig(n=N, threads=T, mode="faithful")
+    c2 = P.default_counts(N, 1 << 28)[0]
+    totals = [c2, c2, 200_000, 200_000, 200_000, 200_000]
+    st = torch.cuda.Stream()
+    with P.Context(c) as ctx:
+        ctx.reset(st.cuda_stream)
+        ctx.gen_uniform_faithful_refs(31, totals, st.cuda_stream)
+        st.synchronize()
+        one = ctx.fetch()
+    with P.Group(c, [0], spd) as g:
+        for _ in range(4):
+            h = g.gen_uniform_faithful(31, totals)
+            assert h.bins == one.bins and h.traversed == one.traversed
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("spd", [1, 3, 8])
 @pytest.mark.parametrize("N,total", [(1024, 1 << 20), (2048, 1 << 20)])
 def test_group_any_order_equals_one_device(N, total, spd):
