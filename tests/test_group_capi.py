@@ -203,6 +203,39 @@ def test_group_uniform_replays_equal_one_device(spd):
 
 
 @pytest.mark.gpu
+def test_group_graph_replacement_rounds():
+    """r5m's sequence: groups created and destroyed in
+    turn, each replacing its captured graph twice (a new seed, then a new
+    uniform pass) and capturing again.  A group that destroyed a replaced
+    graph crashed the host in hipGraphLaunch within two rounds (r6x); kept
+    graphs ran 20 rounds clean (r6y, r6z).  Here 4 rounds, every result
+    equal to one device."""
+    P = _P()
+    import torch
+    N, T = 1024, 8
+    c = P.SamplerConfig(n=N, threads=T, mode="faithful")
+    totals = P.default_counts(N, 1 << 21)
+    st = torch.cuda.Stream()
+    want = {}
+    for seed in (41, 42):
+        with P.Context(c) as ctx:
+            ctx.reset(st.cuda_stream)
+            ctx.gen_faithful_refs(seed, totals, st.cuda_stream)
+            st.synchronize()
+            want[seed] = ctx.fetch()
+    for _ in range(4):
+        for spd in (8, 1):
+            with P.Group(c, [0], spd) as g:
+                for seed in (41, 41, 41, 42, 42, 41, 41, 41):
+                    h = g.gen_faithful(seed, totals)
+                    assert h.bins == want[seed].bins and h.traversed == want[seed].traversed
+                g.gen_uniform_faithful(41, totals)
+                for _ in range(3):
+                    h = g.gen_faithful(41, totals)
+                    assert h.bins == want[41].bins
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("spd", [1, 8])
 def test_group_uniform_replays_sparse_2d_references(spd):
     """N=4096 with the BASELINE budget of the 2-D references (1% of (N-1)^2):
