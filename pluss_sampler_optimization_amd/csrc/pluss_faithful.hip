@@ -934,7 +934,8 @@ static int fa_prepare(pluss_ctx* ctx, FaRefs& a, int src, bool check, bool shard
     }
     // (eager passes only: with the side stream inside a group's captured
     // pass, the bench's config-3 group legs crashed on the host, r6ah-r6ak)
-    if (sparse && b.side && b.sev[0] && b.sev[1] && !b.capture) out->side = (uint32_t)a.toff[2];
+    if (sparse && b.side && b.sev[0] && b.sev[1] && (!b.capture || PLUSS_KNOB("SIDE_CAPTURE")))
+      out->side = (uint32_t)a.toff[2];  // (the knob: diagnostic build only, the crash's reproduction)
   }
   if (int rc = fa_reserve(b, t, c, s)) return rc;
   if (!b.shrec) {
